@@ -1,0 +1,270 @@
+/*
+ * kmer_oracle.c — CPU restatement of the kmerjs FASTQ k-mer hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity checker for the HIP
+ * product path (kmerjs_amd/csrc).  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it; the product never links, calls or
+ * falls back to it.
+ *
+ * Parity pinned: the outputs of this restatement are compared bit-for-bit
+ * (ordered key/count lists) against golden vectors produced by running the
+ * UNMODIFIED reference lib/kmers.js under node in the build container
+ * (tools/ref_loader.js, tests/golden/gen_golden.py), and against the
+ * reference's own known-answer tests (test/kmers.js:12-52) — see
+ * tests/test_oracle.py.
+ *
+ * Semantics followed, byte for byte (reference = /root/reference):
+ *   lines    lib/kmers.js:114-136  split on '\n' only; carry partial lines;
+ *                                  trailing segment emitted only if non-empty;
+ *                                  empty lines ARE lines; '\r' stays in a line.
+ *   records  lib/kmers.js:143-171  line counter i cycles 0..3; a line is a
+ *                                  sequence line iff i==1 && line.length>1.
+ *   strands  lib/kmers.js:152-155  kmersInLine(line) then
+ *                                  kmersInLine(complement(line)).
+ *   revcomp  lib/kmers.js:12-17,31-38  map A<->T, G<->C only (other bytes,
+ *                                  including N, X, lowercase and '\r', kept),
+ *                                  then reverse.
+ *   windows  lib/kmers.js:88-100   for index=0..L-k: key = substring(ini,
+ *                                  ini+k) (clamped to L), kept iff
+ *                                  key.startsWith(preffix); ini += step.
+ *   order    lib/kmers.js:76,95    Map insertion order = first occurrence.
+ * Input bytes >= 0x80 are rejected (ORACLE_E_NONASCII): the reference decodes
+ * chunks as UTF-8 (lib/kmers.js:116) and non-ASCII data would change lengths.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORACLE_OK 0
+#define ORACLE_E_NONASCII 1
+#define ORACLE_E_OOM 2
+
+typedef struct {
+    uint8_t *keys;      /* packed key bytes, entry i at keys[key_off[i]] */
+    uint64_t *key_off;
+    uint32_t *key_len;
+    uint64_t *counts;
+    uint64_t *first;    /* ordinal of the first occurrence (monotone) */
+    uint64_t n;         /* distinct keys */
+    uint64_t lines;     /* lines seen (kmerObj.lines, lib/kmers.js:165) */
+    uint64_t windows;   /* windows examined on both strands */
+    uint64_t seq_lines; /* sequence lines processed */
+    /* private */
+    uint64_t cap, keys_cap, keys_used;
+    uint64_t *slots;    /* hash slots: entry index + 1, 0 = empty */
+    uint64_t slot_mask;
+    uint64_t *hashes;
+    uint64_t ordinal;
+} oracle_result;
+
+static uint64_t hash_bytes(const uint8_t *p, size_t n) {
+    uint64_t h = 0xcbf29ce484222325ull ^ (n * 0x9E3779B97F4A7C15ull);
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        memcpy(&w, p + i, 8);
+        h = (h ^ w) * 0x100000001b3ull;
+        h ^= h >> 29;
+    }
+    for (; i < n; ++i) h = (h ^ p[i]) * 0x100000001b3ull;
+    h ^= h >> 31;
+    h *= 0xbf58476d1ce4e5b9ull;
+    h ^= h >> 27;
+    return h;
+}
+
+static int res_init(oracle_result *r) {
+    memset(r, 0, sizeof(*r));
+    r->cap = 1024;
+    r->keys_cap = 1 << 16;
+    r->key_off = malloc(r->cap * sizeof(uint64_t));
+    r->key_len = malloc(r->cap * sizeof(uint32_t));
+    r->counts = malloc(r->cap * sizeof(uint64_t));
+    r->first = malloc(r->cap * sizeof(uint64_t));
+    r->hashes = malloc(r->cap * sizeof(uint64_t));
+    r->keys = malloc(r->keys_cap);
+    r->slot_mask = 2048 - 1;
+    r->slots = calloc(r->slot_mask + 1, sizeof(uint64_t));
+    if (!r->key_off || !r->key_len || !r->counts || !r->first || !r->hashes || !r->keys || !r->slots)
+        return ORACLE_E_OOM;
+    return ORACLE_OK;
+}
+
+void oracle_free(oracle_result *r) {
+    free(r->keys); free(r->key_off); free(r->key_len); free(r->counts);
+    free(r->first); free(r->slots); free(r->hashes);
+    memset(r, 0, sizeof(*r));
+}
+
+static int rehash(oracle_result *r) {
+    uint64_t nslots = (r->slot_mask + 1) * 2;
+    uint64_t *s = calloc(nslots, sizeof(uint64_t));
+    if (!s) return ORACLE_E_OOM;
+    for (uint64_t e = 0; e < r->n; ++e) {
+        uint64_t j = r->hashes[e] & (nslots - 1);
+        while (s[j]) j = (j + 1) & (nslots - 1);
+        s[j] = e + 1;
+    }
+    free(r->slots);
+    r->slots = s;
+    r->slot_mask = nslots - 1;
+    return ORACLE_OK;
+}
+
+/* Map.set(kmer, (Map.get(kmer) || 0) + 1)  — lib/kmers.js:95 */
+static int map_incr(oracle_result *r, const uint8_t *key, size_t n) {
+    uint64_t h = hash_bytes(key, n);
+    uint64_t j = h & r->slot_mask;
+    for (;;) {
+        uint64_t e = r->slots[j];
+        if (!e) break;
+        e -= 1;
+        if (r->hashes[e] == h && r->key_len[e] == n && memcmp(r->keys + r->key_off[e], key, n) == 0) {
+            r->counts[e] += 1;
+            r->ordinal++;
+            return ORACLE_OK;
+        }
+        j = (j + 1) & r->slot_mask;
+    }
+    if (r->n == r->cap) {
+        uint64_t c = r->cap * 2;
+        void *a = realloc(r->key_off, c * sizeof(uint64_t)); if (!a) return ORACLE_E_OOM; r->key_off = a;
+        a = realloc(r->key_len, c * sizeof(uint32_t)); if (!a) return ORACLE_E_OOM; r->key_len = a;
+        a = realloc(r->counts, c * sizeof(uint64_t)); if (!a) return ORACLE_E_OOM; r->counts = a;
+        a = realloc(r->first, c * sizeof(uint64_t)); if (!a) return ORACLE_E_OOM; r->first = a;
+        a = realloc(r->hashes, c * sizeof(uint64_t)); if (!a) return ORACLE_E_OOM; r->hashes = a;
+        r->cap = c;
+    }
+    if (r->keys_used + n > r->keys_cap) {
+        uint64_t c = r->keys_cap * 2;
+        while (c < r->keys_used + n) c *= 2;
+        void *a = realloc(r->keys, c); if (!a) return ORACLE_E_OOM;
+        r->keys = a; r->keys_cap = c;
+    }
+    uint64_t e = r->n++;
+    memcpy(r->keys + r->keys_used, key, n);
+    r->key_off[e] = r->keys_used;
+    r->key_len[e] = (uint32_t)n;
+    r->keys_used += n;
+    r->counts[e] = 1;
+    r->first[e] = r->ordinal++;
+    r->hashes[e] = h;
+    r->slots[j] = e + 1;
+    if (r->n * 2 > r->slot_mask + 1) return rehash(r);
+    return ORACLE_OK;
+}
+
+/* complementMap (lib/kmers.js:12-17): only A,T,G,C are mapped. */
+static inline uint8_t comp_byte(uint8_t c) {
+    switch (c) {
+    case 'A': return 'T';
+    case 'T': return 'A';
+    case 'G': return 'C';
+    case 'C': return 'G';
+    default: return c;
+    }
+}
+
+/* complement(string) — lib/kmers.js:31-38: replace then reverse. */
+void oracle_complement(const uint8_t *in, size_t n, uint8_t *out) {
+    for (size_t i = 0; i < n; ++i) out[n - 1 - i] = comp_byte(in[i]);
+}
+
+/* KmerJS.kmersInLine(line) — lib/kmers.js:88-100. */
+static int kmers_in_line(oracle_result *r, const uint8_t *t, size_t L,
+                         const uint8_t *prefix, size_t plen, uint64_t k, uint64_t step) {
+    if (L < k) return ORACLE_OK;              /* stop = L - k < 0: no iteration */
+    uint64_t stop = L - k;
+    uint64_t ini = 0;
+    for (uint64_t index = 0; index <= stop; ++index) {
+        /* substring(ini, ini + k) clamps both ends to L (ES2015 21.1.3.19) */
+        uint64_t a = ini < L ? ini : L;
+        uint64_t b = ini + k < L ? ini + k : L;
+        size_t klen = (size_t)(b - a);
+        r->windows++;
+        if (klen >= plen && memcmp(t + a, prefix, plen) == 0) {
+            int st = map_incr(r, t + a, klen);
+            if (st) return st;
+        }
+        ini += step;
+    }
+    return ORACLE_OK;
+}
+
+int oracle_kmers_in_line(const uint8_t *line, size_t n, const uint8_t *prefix, size_t plen,
+                         uint32_t k, uint32_t step, oracle_result *out) {
+    int st = res_init(out);
+    if (st) return st;
+    return kmers_in_line(out, line, n, prefix, plen, k, step);
+}
+
+/* readFile() — lib/kmers.js:106-185, over an in-memory byte buffer. */
+int oracle_count_buffer(const uint8_t *buf, size_t len, const uint8_t *prefix, size_t plen,
+                        uint32_t k, uint32_t step, oracle_result *out) {
+    int st = res_init(out);
+    if (st) return st;
+    for (size_t i = 0; i < len; ++i)
+        if (buf[i] >= 0x80) return ORACLE_E_NONASCII;
+    uint8_t *rc = NULL;
+    size_t rc_cap = 0;
+    int li = 0;                 /* `i` of lib/kmers.js:143 */
+    size_t pos = 0;
+    while (pos < len) {
+        const uint8_t *nl = memchr(buf + pos, '\n', len - pos);
+        size_t end = nl ? (size_t)(nl - buf) : len;
+        size_t L = end - pos;
+        if (!nl && L == 0) break;   /* _flush: empty trailing segment dropped (:131) */
+        const uint8_t *line = buf + pos;
+        if (li == 1 && L > 1) {     /* :151 */
+            out->seq_lines++;
+            st = kmers_in_line(out, line, L, prefix, plen, k, step);
+            if (st) break;
+            if (L > rc_cap) {
+                free(rc);
+                rc_cap = L * 2;
+                rc = malloc(rc_cap);
+                if (!rc) { st = ORACLE_E_OOM; break; }
+            }
+            oracle_complement(line, L, rc);
+            st = kmers_in_line(out, rc, L, prefix, plen, k, step);
+            if (st) break;
+        } else if (li == 3) {
+            li = -1;                /* :160-161 */
+        }
+        li += 1;
+        out->lines++;
+        pos = nl ? end + 1 : len;
+    }
+    free(rc);
+    return st;
+}
+
+/* ---- synthetic FASTQ, identical to the device generator ----
+ * Record i: "@r%010llu\n" + 150 bases + "\n+\n" + 150 x 'I' + "\n" = 317 B.
+ * Base b of read i = "ACGT"[(mix(seed*G + i*8 + b/32) >> 2*(b%32)) & 3]. */
+static inline uint64_t splitmix_mix(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+void oracle_synth_fastq(uint64_t seed, uint64_t first_read, uint64_t n_reads, uint8_t *out) {
+    static const char B[4] = {'A', 'C', 'G', 'T'};
+    for (uint64_t r = 0; r < n_reads; ++r) {
+        uint64_t i = first_read + r;
+        uint8_t *p = out + r * 317;
+        p[0] = '@'; p[1] = 'r';
+        uint64_t v = i;
+        for (int d = 9; d >= 0; --d) { p[2 + d] = (uint8_t)('0' + v % 10); v /= 10; }
+        p[12] = '\n';
+        uint8_t *s = p + 13;
+        for (int m = 0; m < 5; ++m) {
+            uint64_t w = splitmix_mix(seed * 0x9E3779B97F4A7C15ull + i * 8 + (uint64_t)m);
+            for (int b = 0; b < 32 && m * 32 + b < 150; ++b) s[m * 32 + b] = (uint8_t)B[(w >> (2 * b)) & 3];
+        }
+        s[150] = '\n'; s[151] = '+'; s[152] = '\n';
+        memset(s + 153, 'I', 150);
+        s[303] = '\n';
+    }
+}
