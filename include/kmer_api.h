@@ -1,0 +1,125 @@
+/*
+ * kmer_api.h — C-ABI of libkmerhip, the MI355X (gfx950) k-mer counter that
+ * replaces the FASTQ sliding-window loop of kmerjs (lib/kmers.js).
+ *
+ * The reference has no native interface; these entry points are what a
+ * kmerjs binding (the N-API addon in kmerjs_amd/node/, or ctypes) needs to
+ * implement the reference's KmerJS surface unchanged:
+ *
+ *   reference                                    replaced by
+ *   -------------------------------------------  ------------------------------------
+ *   new KmerJS(fastq, preffix, length, step, ..) kmer_open(params)        lib/kmers.js:67-82
+ *   KmerJS.readFile() -> {promise: Map, event}   kmer_count_file()        lib/kmers.js:106-185
+ *     (stream -> liner -> mod-4 -> kmersInLine)  kmer_count_buffer()      lib/kmers.js:114-171
+ *   kmersInLine(line), complement(line)          (inside the kernels)     lib/kmers.js:88-100,31-38
+ *   Map insertion order / size / entries         kmer_result_*            lib/kmers.js:76,95,177
+ *   kmerObj.lines                                kmer_result_lines()      lib/kmers.js:145,165
+ *
+ * Results are bit-exact with the reference: identical keys (byte strings,
+ * including non-ACGT bytes such as N, X, lowercase or '\r'), identical counts,
+ * and entries in the reference Map's insertion (first-occurrence) order.
+ *
+ * Device-resident entry points (kmer_reset / kmer_feed_device /
+ * kmer_finish_device) let a caller that already holds the FASTQ bytes in HBM
+ * count them without any host copy; kmer_table_* expose the dense count
+ * tables so that per-GPU tables can be merged with an RCCL reduce.
+ *
+ * Threading: a kmer_ctx is used by one thread at a time (one in-flight call
+ * per context); distinct contexts are independent.  All calls return a
+ * kmer_status; kmer_last_error() gives a message for the last failure.
+ */
+#ifndef KMER_API_H
+#define KMER_API_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    KMER_OK = 0,
+    KMER_E_IO = 1,            /* file missing/unreadable (reference: uncaught stream error) */
+    KMER_E_BAD_PARAM = 2,     /* k == 0, step == 0, NULL pointers, ... */
+    KMER_E_OOM = 3,           /* host or device allocation failed */
+    KMER_E_DEVICE = 4,        /* HIP runtime error */
+    KMER_E_TOO_MANY_KEYS = 5, /* more than max_keys distinct keys (reference: RangeError at 2^24, lib/kmers.js:95) */
+    KMER_E_NONASCII = 6,      /* input byte >= 0x80 (reference decodes UTF-8, lib/kmers.js:116) */
+    KMER_E_LINE_TOO_LONG = 7, /* a sequence line longer than 2^23 bytes */
+    KMER_E_STATE = 8          /* call out of sequence (e.g. finish without reset) */
+} kmer_status;
+
+enum {
+    KMER_FLAG_TWO_PASS = 1u << 0,  /* debug: exact two-pass line scan instead of single-pass look-back */
+    KMER_FLAG_NO_DENSE = 1u << 1   /* debug: force the general (record) path */
+};
+
+typedef struct {
+    uint32_t k;               /* kmerLength (reference default 16) */
+    uint32_t step;            /* step (reference default 1) */
+    const uint8_t *prefix;    /* preffix bytes (reference default "ATGAC"); may be NULL if prefix_len == 0 */
+    uint32_t prefix_len;
+    int32_t device;           /* HIP device ordinal */
+    uint32_t flags;           /* KMER_FLAG_* */
+    uint64_t max_keys;        /* 0 = unlimited; 16777216 reproduces the reference Map cap */
+    uint64_t batch_bytes;     /* host->device batch size for file/buffer input; 0 = default (1 GiB) */
+} kmer_params;
+
+typedef struct kmer_ctx kmer_ctx;
+typedef struct kmer_result kmer_result;
+
+/* Context lifecycle (replaces `new KmerJS(...)`, lib/kmers.js:67-82). */
+kmer_status kmer_open(const kmer_params *params, kmer_ctx **out);
+kmer_status kmer_close(kmer_ctx *ctx);
+
+/* Whole-input calls (replace readFile(), lib/kmers.js:106-185). */
+kmer_status kmer_count_file(kmer_ctx *ctx, const char *path, kmer_result **out);
+kmer_status kmer_count_buffer(kmer_ctx *ctx, const uint8_t *bytes, size_t len, kmer_result **out);
+
+/* Device-resident streaming: bytes already in HBM.  Each fed chunk must start
+ * at a line start (offset 0 of the input, or just after a '\n'); all chunks
+ * but the last must end with '\n'.  `stream` is a hipStream_t (NULL = the
+ * context's own stream).  kmer_finish_device leaves the ordered result in
+ * device memory (see kmer_result_device_*) and also returns it as a host
+ * result when `out` is non-NULL. */
+kmer_status kmer_reset(kmer_ctx *ctx);
+kmer_status kmer_feed_device(kmer_ctx *ctx, const void *d_bytes, size_t len, void *stream);
+kmer_status kmer_finish_device(kmer_ctx *ctx, kmer_result **out);
+
+/* Dense-table view for multi-GPU merges (valid between reset and finish).
+ * counts: uint64[n], first: uint64[n] (first-occurrence order, UINT64_MAX = none).
+ * Returns KMER_E_STATE when the configuration does not use the dense table. */
+kmer_status kmer_table_view(kmer_ctx *ctx, void **d_counts, void **d_first, uint64_t *n);
+/* Set the running line/byte position (lines already consumed, absolute byte
+ * offset of the next fed chunk) — used when one input is sharded over ranks. */
+kmer_status kmer_set_position(kmer_ctx *ctx, uint64_t lines_before, uint64_t byte_offset);
+/* Lines consumed so far (reference kmerObj.lines). */
+kmer_status kmer_lines(kmer_ctx *ctx, uint64_t *lines);
+
+/* Ordered result (Map insertion order). */
+uint64_t kmer_result_size(const kmer_result *r);
+uint64_t kmer_result_lines(const kmer_result *r);
+kmer_status kmer_result_get(const kmer_result *r, uint64_t i, const char **key, uint32_t *klen,
+                            uint64_t *count);
+/* Bulk view: keys packed back to back; key i = keys[offsets[i] .. offsets[i+1]). */
+kmer_status kmer_result_arrays(const kmer_result *r, const char **keys, const uint64_t **offsets,
+                               const uint64_t **counts);
+void kmer_result_free(kmer_result *r);
+
+/* Benchmark utility: write n_reads synthetic 317-byte FASTQ records (SURVEY.md
+ * §8d generator, splitmix64 of (seed, read index)) to device memory. */
+kmer_status kmer_synth_fastq_device(void *d_out, uint64_t seed, uint64_t first_read, uint64_t n_reads,
+                                    void *stream);
+
+/* Timing of the last finish (device time of the counting kernels, ms). */
+kmer_status kmer_last_timing(kmer_ctx *ctx, double *count_ms, double *finish_ms);
+
+const char *kmer_status_string(kmer_status s);
+const char *kmer_last_error(const kmer_ctx *ctx);
+const char *kmer_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KMER_API_H */

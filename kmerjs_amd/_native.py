@@ -1,0 +1,194 @@
+"""ctypes binding of libkmerhip.so (include/kmer_api.h).
+
+The product path.  There is no CPU fallback: if the HIP library is missing
+this module raises at import time, and every compute call goes to the GPU.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libkmerhip.so")
+
+KMER_OK = 0
+STATUS = {0: "ok", 1: "i/o error", 2: "bad parameter", 3: "out of memory", 4: "device error",
+          5: "too many keys", 6: "non-ASCII input", 7: "line too long", 8: "bad call sequence"}
+FLAG_TWO_PASS = 1
+FLAG_NO_DENSE = 2
+
+# every symbol the header declares (tests/test_abi.py checks header <-> library)
+EXPORTS = ["kmer_open", "kmer_close", "kmer_count_file", "kmer_count_buffer", "kmer_reset",
+           "kmer_feed_device", "kmer_finish_device", "kmer_table_view", "kmer_set_position",
+           "kmer_lines", "kmer_result_size", "kmer_result_lines", "kmer_result_get",
+           "kmer_result_arrays", "kmer_result_free", "kmer_synth_fastq_device", "kmer_last_timing",
+           "kmer_status_string", "kmer_last_error", "kmer_version"]
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("k", ctypes.c_uint32), ("step", ctypes.c_uint32),
+                ("prefix", ctypes.c_char_p), ("prefix_len", ctypes.c_uint32),
+                ("device", ctypes.c_int32), ("flags", ctypes.c_uint32),
+                ("max_keys", ctypes.c_uint64), ("batch_bytes", ctypes.c_uint64)]
+
+
+class KmerError(RuntimeError):
+    def __init__(self, status, msg=""):
+        super().__init__("%s: %s" % (STATUS.get(status, status), msg))
+        self.status = status
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libkmerhip.so not built (run `python -c 'import __graft_entry__ as g; g.build()'` "
+                          "or `make -C kmerjs_amd/csrc`)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u64, pu64 = ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)
+    sig = {
+        "kmer_open": (ctypes.c_int, [ctypes.POINTER(Params), ctypes.POINTER(vp)]),
+        "kmer_close": (ctypes.c_int, [vp]),
+        "kmer_count_file": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.POINTER(vp)]),
+        "kmer_count_buffer": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp)]),
+        "kmer_reset": (ctypes.c_int, [vp]),
+        "kmer_feed_device": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp]),
+        "kmer_finish_device": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
+        "kmer_table_view": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), pu64]),
+        "kmer_set_position": (ctypes.c_int, [vp, u64, u64]),
+        "kmer_lines": (ctypes.c_int, [vp, pu64]),
+        "kmer_result_size": (u64, [vp]),
+        "kmer_result_lines": (u64, [vp]),
+        "kmer_result_get": (ctypes.c_int, [vp, u64, ctypes.POINTER(ctypes.c_char_p),
+                                           ctypes.POINTER(ctypes.c_uint32), pu64]),
+        "kmer_result_arrays": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(pu64),
+                                              ctypes.POINTER(pu64)]),
+        "kmer_result_free": (None, [vp]),
+        "kmer_synth_fastq_device": (ctypes.c_int, [vp, u64, u64, u64, vp]),
+        "kmer_last_timing": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double),
+                                            ctypes.POINTER(ctypes.c_double)]),
+        "kmer_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+        "kmer_last_error": (ctypes.c_char_p, [vp]),
+        "kmer_version": (ctypes.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    return L
+
+
+LIB = _load()
+
+
+def version():
+    return LIB.kmer_version().decode()
+
+
+class Result:
+    """Ordered (Map insertion order) result copied out of a kmer_result."""
+
+    def __init__(self, handle):
+        keys = ctypes.c_void_p()
+        offs = ctypes.POINTER(ctypes.c_uint64)()
+        cnts = ctypes.POINTER(ctypes.c_uint64)()
+        n = LIB.kmer_result_size(handle)
+        self.lines = LIB.kmer_result_lines(handle)
+        LIB.kmer_result_arrays(handle, ctypes.byref(keys), ctypes.byref(offs), ctypes.byref(cnts))
+        if n:
+            import numpy as np
+            off = np.ctypeslib.as_array(offs, shape=(n + 1,)).copy()
+            self.counts = np.ctypeslib.as_array(cnts, shape=(n,)).copy()
+            self.keybuf = ctypes.string_at(keys, int(off[-1]))
+            self.offsets = off
+        else:
+            import numpy as np
+            self.counts = np.zeros(0, dtype=np.uint64)
+            self.keybuf = b""
+            self.offsets = np.zeros(1, dtype=np.uint64)
+        LIB.kmer_result_free(handle)
+
+    def __len__(self):
+        return len(self.counts)
+
+    def entries(self):
+        """[(key_bytes, count)] in first-occurrence order."""
+        o = self.offsets.tolist()
+        c = self.counts.tolist()
+        b = self.keybuf
+        return [(b[o[i]:o[i + 1]], c[i]) for i in range(len(c))]
+
+
+class Counter:
+    """One kmer_ctx (device, configuration)."""
+
+    def __init__(self, k=16, prefix=b"ATGAC", step=1, device=0, flags=0, max_keys=0, batch_bytes=0):
+        if isinstance(prefix, str):
+            prefix = prefix.encode("latin-1")
+        self._prefix = prefix
+        p = Params(k=k, step=step, prefix=prefix, prefix_len=len(prefix), device=device, flags=flags,
+                   max_keys=max_keys, batch_bytes=batch_bytes)
+        h = ctypes.c_void_p()
+        st = LIB.kmer_open(ctypes.byref(p), ctypes.byref(h))
+        if st != KMER_OK:
+            raise KmerError(st, "kmer_open(k=%d, step=%d, prefix=%r)" % (k, step, prefix))
+        self.h = h
+        self.k, self.step = k, step
+
+    def _check(self, st, what):
+        if st != KMER_OK:
+            raise KmerError(st, "%s: %s" % (what, LIB.kmer_last_error(self.h).decode()))
+
+    def close(self):
+        if self.h:
+            LIB.kmer_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def count_buffer(self, data: bytes) -> Result:
+        r = ctypes.c_void_p()
+        self._check(LIB.kmer_count_buffer(self.h, data, len(data), ctypes.byref(r)), "count_buffer")
+        return Result(r)
+
+    def count_file(self, path) -> Result:
+        r = ctypes.c_void_p()
+        self._check(LIB.kmer_count_file(self.h, os.fsencode(path), ctypes.byref(r)), "count_file")
+        return Result(r)
+
+    # ---- device-resident streaming ----
+    def reset(self):
+        self._check(LIB.kmer_reset(self.h), "reset")
+
+    def set_position(self, lines_before, byte_offset):
+        self._check(LIB.kmer_set_position(self.h, lines_before, byte_offset), "set_position")
+
+    def feed_device(self, ptr: int, nbytes: int, stream: int = 0):
+        self._check(LIB.kmer_feed_device(self.h, ctypes.c_void_p(ptr), nbytes, ctypes.c_void_p(stream)),
+                    "feed_device")
+
+    def finish(self, want_result=True):
+        r = ctypes.c_void_p()
+        self._check(LIB.kmer_finish_device(self.h, ctypes.byref(r) if want_result else None), "finish")
+        return Result(r) if want_result else None
+
+    def table_view(self):
+        c, f, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+        self._check(LIB.kmer_table_view(self.h, ctypes.byref(c), ctypes.byref(f), ctypes.byref(n)), "table_view")
+        return c.value, f.value, n.value
+
+    def lines(self):
+        n = ctypes.c_uint64()
+        self._check(LIB.kmer_lines(self.h, ctypes.byref(n)), "lines")
+        return n.value
+
+    def last_timing(self):
+        a, b = ctypes.c_double(), ctypes.c_double()
+        self._check(LIB.kmer_last_timing(self.h, ctypes.byref(a), ctypes.byref(b)), "last_timing")
+        return a.value, b.value
+
+
+def synth_fastq_device(ptr: int, seed: int, first_read: int, n_reads: int, stream: int = 0):
+    st = LIB.kmer_synth_fastq_device(ctypes.c_void_p(ptr), seed, first_read, n_reads, ctypes.c_void_p(stream))
+    if st != KMER_OK:
+        raise KmerError(st, "synth_fastq_device")

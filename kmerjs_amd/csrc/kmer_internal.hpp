@@ -1,0 +1,124 @@
+// kmer_internal.hpp — shared definitions between the gfx950 kernels
+// (kmer_kernels.hip) and the host orchestration (kmer_api.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace kmerhip {
+
+// ---- tile geometry (tile kernel) -------------------------------------------
+// One workgroup owns one 16 KiB tile of the input.  The tile plus a front halo
+// (rc windows whose start lies in the previous tile) and a back halo (forward
+// windows that run into the next tile) is staged in LDS.
+constexpr int TPB = 256;                 // threads per workgroup (4 waves)
+constexpr int BPT = 64;                  // bytes scanned per thread
+constexpr int TILE = TPB * BPT;          // 16384
+constexpr int FH = 64;                   // front halo bytes
+constexpr int BH = 80;                   // back halo bytes (>= KMAX_TILE - 1 + 3, x16)
+constexpr int KMAX_TILE = 64;            // longest k handled by the tile kernel
+constexpr int KMAX_DENSE = 32;           // longest k packed into 2-bit codes
+constexpr int DENSE_MAX_SUFFIX = 13;     // dense table = 4^(k-|P|) entries, |suffix| <= 13
+constexpr uint32_t MAXREL = (1u << 23) - 1;  // longest sequence line (bytes - 1)
+
+// error bits (device-side, OR-ed into ctx->d_err)
+enum : uint32_t {
+    ERR_NONASCII = 1u << 0,
+    ERR_LINE_TOO_LONG = 1u << 1,
+    ERR_LOOKBACK_TIMEOUT = 1u << 2,
+    ERR_REC_OVERFLOW = 1u << 3,
+    ERR_LINE_OVERFLOW = 1u << 4,
+};
+
+// look-back word: [63:62] status, [61:0] value
+constexpr uint64_t LB_AGG = 1ull << 62;
+constexpr uint64_t LB_INC = 2ull << 62;
+constexpr uint64_t LB_VAL = (1ull << 62) - 1;
+
+// Running position of the stream, kept in device memory so consecutive
+// launches chain without host round trips.
+struct StreamPos {
+    uint64_t lines;        // newlines consumed before the next chunk (= its first line index)
+    uint64_t unused;
+    uint64_t ends_open;    // 1 if the last chunk did not end with '\n'
+    uint64_t pad;
+};
+
+// A window that cannot take the dense path (non-ACGT byte, long key, or a
+// non-dense configuration).  Its key bytes are gathered later:
+// key = strand ? rc(data[pos, pos+len)) : data[pos, pos+len)   (pos is chunk-relative)
+struct Record {
+    uint64_t order;
+    uint64_t pos;
+    uint32_t len;
+    uint32_t strand;
+};
+
+// A sequence line for the general (any k / any step) kernel.
+struct SeqLine {
+    uint64_t start;        // chunk-relative byte offset
+    uint64_t len;
+    uint64_t line_index;   // global line index
+};
+
+struct TileArgs {
+    const uint8_t *data;
+    uint64_t len;
+    uint32_t n_tiles;
+    uint32_t k;
+    uint32_t plen;
+    uint32_t p4, r4, pmask;        // first min(4,|P|) bytes of P and rc(P) (little-endian), byte mask
+    uint32_t dense;                // 1: ACGT windows go to the dense table
+    uint32_t dense_update;         // 0: skip dense atomics (record-overflow redo of a chunk)
+    uint64_t abs_offset;           // absolute byte offset of data[0] in the whole input
+    uint32_t emit_lines;           // 1: emit sequence-line descriptors instead of windows
+    const uint8_t *PR;             // device: P[0..KMAX_TILE) then rc(P)[0..KMAX_TILE)
+    // dense table
+    unsigned long long *counts;
+    unsigned long long *first;
+    // records
+    Record *recs;
+    unsigned long long *rec_count;
+    uint64_t rec_cap;
+    // line list
+    SeqLine *lines_out;
+    unsigned long long *line_count;
+    uint64_t line_cap;
+    // look-back / positions
+    unsigned long long *lb_cnt;
+    unsigned long long *lb_lnl;
+    unsigned int *ticket;
+    StreamPos *pos;
+    const uint64_t *tp_cnt;        // two-pass mode: exclusive newline count per tile (absolute line index)
+    const uint64_t *tp_lnl;        // two-pass mode: line start before tile (absolute)
+    unsigned int *err;
+};
+
+struct WindowArgs {
+    const uint8_t *data;
+    const SeqLine *lines;
+    const unsigned long long *n_lines;
+    uint32_t k, step, plen;
+    const uint8_t *P;              // device copy of the prefix
+    Record *recs;
+    unsigned long long *rec_count;
+    uint64_t rec_cap;
+    unsigned int *err;
+};
+
+// ---- launchers (kmer_kernels.hip) ------------------------------------------
+hipError_t launch_tile(const TileArgs &a, bool lookback, hipStream_t s);
+hipError_t launch_tile_aggregate(const uint8_t *data, uint64_t len, uint32_t n_tiles, uint64_t *agg_cnt,
+                                 uint64_t *agg_lnl, unsigned int *err, hipStream_t s);
+hipError_t launch_windows(const WindowArgs &a, uint32_t grid, hipStream_t s);
+hipError_t launch_dense_compact(const unsigned long long *counts, const unsigned long long *first,
+                                uint64_t n, uint64_t *out_order, uint64_t *out_idx,
+                                unsigned long long *out_n, hipStream_t s);
+hipError_t launch_dense_decode(const uint64_t *idx_sorted, const unsigned long long *n, uint64_t cap,
+                               uint32_t k, uint32_t plen, const uint8_t *P, const unsigned long long *counts,
+                               uint8_t *keys_out, uint64_t *counts_out, hipStream_t s);
+hipError_t launch_gather_records(const Record *recs, const uint64_t *key_off, uint64_t n,
+                                 const uint8_t *data, uint8_t *out, hipStream_t s);
+hipError_t launch_synth_fastq(uint8_t *out, uint64_t seed, uint64_t first_read, uint64_t n_reads,
+                              hipStream_t s);
+
+}  // namespace kmerhip

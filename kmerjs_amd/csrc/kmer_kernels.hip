@@ -1,0 +1,703 @@
+// kmer_kernels.hip — gfx950 (CDNA4) kernels for the kmerjs FASTQ k-mer loop.
+//
+// Reference semantics (lib/kmers.js, see oracle/kmer_oracle.c for the exact
+// restatement): lines split on '\n' (:114-136); a line is a sequence line iff
+// its 0-based index n has n % 4 == 1 and length > 1 (:151,:160); each sequence
+// line s is scanned, then complement(s) (:152-155, :31-38); every k-window
+// key = substring(ini, ini+k) that startsWith(preffix) is counted (:88-100);
+// Map order = first occurrence (:95).
+//
+// Device pipeline:
+//   tile_kernel   one 16 KiB tile per workgroup, single pass over HBM:
+//                 stage tile + halos in LDS, count '\n' per thread, block
+//                 scan, decoupled look-back across tiles (line index and line
+//                 start of the tile), SWAR 4-byte scan for P and rc(P) at
+//                 every byte, exact verification of the rare candidates,
+//                 dense-table atomics (count + first-occurrence atomicMin)
+//                 for ACGT windows, records for everything else.
+//   windows_kernel general path (any k, any step, empty prefix): one
+//                 workgroup per sequence line, every window enumerated.
+//   dense_compact / dense_decode / gather_records: result materialisation.
+//
+// Canonical identity used by the tile kernel: the
+// reverse-complement strand's window at j is rc of the forward window at
+// p = L-k-j, so both strands are served by ONE forward scan: a forward window
+// w at p yields key w if w starts with P, and key rc(w) if w ends with rc(P).
+#include "kmer_internal.hpp"
+
+namespace kmerhip {
+
+// ---------------------------------------------------------------------------
+// small helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t align4(uint32_t hi, uint32_t lo, uint32_t sel) {
+    return __builtin_amdgcn_alignbyte(hi, lo, sel);
+}
+
+// per-byte 0x80 flag for bytes equal to '\n'; exact for ASCII bytes (< 0x80)
+__device__ __forceinline__ uint32_t nl_flags(uint32_t x) {
+    uint32_t t = x ^ 0x0A0A0A0Au;
+    return ~(t + 0x7F7F7F7Fu) & 0x80808080u;
+}
+
+// 2-bit code, A=0 C=1 G=2 T=3; returns 4 for any other byte
+__device__ __forceinline__ uint32_t base_code(uint32_t b) {
+    uint32_t c = ((b >> 1) ^ (b >> 2)) & 3u;
+    uint32_t expect = (0x54474341u >> (8u * c)) & 0xFFu;  // "ACGT"[c]
+    return b == expect ? c : 4u;
+}
+
+__device__ __forceinline__ uint8_t comp_byte(uint8_t c) {
+    return c == 'A' ? 'T' : c == 'T' ? 'A' : c == 'G' ? 'C' : c == 'C' ? 'G' : c;
+}
+
+__device__ __forceinline__ uint64_t lb_load(unsigned long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(unsigned long long *p, uint64_t v) {
+    __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr uint32_t SPIN_LIMIT = 1u << 22;
+
+// Decoupled look-back over one of the two per-tile words (wave 0 only).
+// SUM: exclusive prefix sum of aggregates (line index of the tile start).
+// !SUM: nearest non-zero value (line start before the tile: positions grow
+// with the tile index, so the nearest predecessor that saw a '\n' holds the max).
+template <bool SUM>
+__device__ uint64_t look_back(unsigned long long *words, uint32_t tile, unsigned int *err) {
+    const int lane = threadIdx.x & 63;
+    uint64_t acc = 0;
+    int64_t top = (int64_t)tile - 1;
+    uint32_t spins = 0;
+    while (true) {
+        int64_t idx = top - lane;
+        uint64_t v = 0;
+        bool valid = idx >= 0;
+        // spin until every predecessor in the window has published something
+        while (true) {
+            v = valid ? lb_load(words + idx) : LB_INC;
+            bool ready = (v >> 62) != 0;
+            if (__all(ready)) break;
+            if (++spins > SPIN_LIMIT) {
+                if (lane == 0) atomicOr(err, ERR_LOOKBACK_TIMEOUT);
+                return acc;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const uint64_t val = valid ? (v & LB_VAL) : 0;
+        const bool inc = (v >> 62) == 2;
+        if (SUM) {
+            unsigned long long incmask = __ballot(inc);
+            int stop = incmask ? __ffsll((long long)incmask) - 1 : 64;
+            uint64_t contrib = lane <= stop ? val : 0;
+            // wave reduce
+            for (int d = 32; d >= 1; d >>= 1) contrib += __shfl_xor(contrib, d);
+            acc += contrib;
+            if (incmask) return acc;
+        } else {
+            unsigned long long hit = __ballot(inc || val != 0);
+            if (hit) {
+                int stop = __ffsll((long long)hit) - 1;
+                return __shfl(val, stop);
+            }
+        }
+        top -= 64;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// tile kernel
+// ---------------------------------------------------------------------------
+constexpr int NCH_MAIN = TILE / 16;          // 1024 16-byte chunks
+constexpr int NCH_FRONT = FH / 16;           // 4
+constexpr int NCH_BACK = BH / 16;            // 5
+constexpr int BUFSZ = FH + TILE + BH;
+
+__device__ __forceinline__ uint4 load_chunk(const uint8_t *data, int64_t g, uint64_t len) {
+    if (g >= 0 && (uint64_t)g + 16 <= len) return *(const uint4 *)(data + g);
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            int64_t p = g + i * 4 + b;
+            uint32_t c = (p >= 0 && (uint64_t)p < len) ? data[p] : (uint32_t)'\n';
+            x |= c << (8 * b);
+        }
+        w[i] = x;
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+struct TileShared {
+    uint32_t tpre[TPB + 1];      // exclusive '\n' count per thread inside the tile; [TPB] = total
+    uint32_t wsum[TPB / 64];
+    int32_t last_thr;            // highest thread owning a '\n'
+    uint32_t tile;
+    uint64_t line_base;          // global line index of the tile's first byte
+    uint64_t lnl_before;         // absolute start of the line containing the tile's first byte
+    uint64_t lnl_tile;           // absolute line start after the tile's last '\n' (0 = none)
+};
+
+// newline count in [64*thr, q) for tile-relative q within thread thr's range
+__device__ __forceinline__ uint32_t nl_before_in_thread(const uint8_t *buf, int thr, int q) {
+    const uint32_t *lw = (const uint32_t *)(buf + FH + 64 * thr);
+    int n = q - 64 * thr;        // bytes to count, 0..64
+    uint32_t c = 0;
+#pragma unroll 1
+    for (int i = 0; i < 16 && n > 0; ++i, n -= 4) {
+        uint32_t z = nl_flags(lw[i]);
+        if (n < 4) z &= (1u << (8 * n)) - 1u;
+        c += __popc(z);
+    }
+    return c;
+}
+
+// tile-relative position of the c-th (1-based) '\n' of the tile
+__device__ int nth_newline(const uint8_t *buf, const uint32_t *tpre, uint32_t c) {
+    int lo = 0, hi = TPB - 1;     // largest thr with tpre[thr] < c
+    while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (tpre[mid] < c) lo = mid; else hi = mid - 1;
+    }
+    uint32_t need = c - tpre[lo];
+    const uint8_t *p = buf + FH + 64 * lo;
+#pragma unroll 1
+    for (int i = 0; i < 64; ++i) {
+        if (p[i] == '\n' && --need == 0) return 64 * lo + i;
+    }
+    return -1;  // unreachable for consistent inputs
+}
+
+template <bool LOOKBACK, bool FULL4>
+__global__ __launch_bounds__(TPB) void tile_kernel(TileArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t buf[BUFSZ];
+    __shared__ TileShared sh;
+    __shared__ uint8_t s_pr[2 * KMAX_TILE];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+
+    if (tid == 0) {
+        sh.tile = LOOKBACK ? atomicAdd(a.ticket, 1u) : blockIdx.x;
+        sh.last_thr = -1;
+    }
+    if (tid < 2 * KMAX_TILE) s_pr[tid] = a.PR[tid];
+    __syncthreads();
+    const uint32_t tile = sh.tile;
+    const int64_t g0 = (int64_t)tile * TILE;
+    const uint64_t len = a.len;
+
+    // ---- stage tile + halos into LDS (16 B per lane, coalesced) ----
+    uint4 v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = load_chunk(a.data, g0 + (int64_t)(tid + TPB * i) * 16, len);
+    uint4 vh = make_uint4(0, 0, 0, 0);
+    const bool halo = tid < NCH_FRONT + NCH_BACK;
+    int hc = tid < NCH_FRONT ? tid : NCH_FRONT + NCH_MAIN + (tid - NCH_FRONT);
+    if (halo) vh = load_chunk(a.data, g0 - FH + (int64_t)hc * 16, len);
+    uint32_t orall = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        orall |= v[i].x | v[i].y | v[i].z | v[i].w;
+        *(uint4 *)(buf + FH + (tid + TPB * i) * 16) = v[i];
+    }
+    if (halo) *(uint4 *)(buf + hc * 16) = vh;
+    if (orall & 0x80808080u) atomicOr(a.err, ERR_NONASCII);
+    __syncthreads();
+
+    // ---- per-thread view: bytes [64*tid, 64*tid + 68) ----
+    uint32_t w[17];
+    {
+        const uint4 *lp = (const uint4 *)(buf + FH + 64 * tid);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint4 x = lp[i];
+            w[4 * i] = x.x; w[4 * i + 1] = x.y; w[4 * i + 2] = x.z; w[4 * i + 3] = x.w;
+        }
+        w[16] = *(const uint32_t *)(buf + FH + 64 * tid + 64);
+    }
+
+    // ---- '\n' count of the bytes this thread owns (only real bytes < len) ----
+    uint32_t cnt = 0;
+    {
+        const int64_t gt = g0 + 64 * tid;
+        if (gt + 64 <= (int64_t)len) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) cnt += __popc(nl_flags(w[i]));
+        } else {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                int64_t n = (int64_t)len - (gt + 4 * i);
+                uint32_t z = nl_flags(w[i]);
+                if (n <= 0) z = 0; else if (n < 4) z &= (1u << (8 * n)) - 1u;
+                cnt += __popc(z);
+            }
+        }
+    }
+    // block exclusive scan of cnt
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t y = __shfl_up(incl, d);
+        if (lane >= d) incl += y;
+    }
+    if (lane == 63) sh.wsum[wid] = incl;
+    if (cnt) atomicMax(&sh.last_thr, tid);
+    __syncthreads();
+    uint32_t woff = 0, total = 0;
+#pragma unroll
+    for (int i = 0; i < TPB / 64; ++i) {
+        woff += i < wid ? sh.wsum[i] : 0;
+        total += sh.wsum[i];
+    }
+    sh.tpre[tid] = woff + incl - cnt;
+    if (tid == 0) sh.tpre[TPB] = total;
+    if (tid == sh.last_thr) {
+        int lastpos = -1;
+        const int64_t gt = g0 + 64 * tid;
+#pragma unroll 1
+        for (int i = 0; i < 64; ++i)
+            if (gt + i < (int64_t)len && buf[FH + 64 * tid + i] == '\n') lastpos = i;
+        sh.lnl_tile = a.abs_offset + (uint64_t)(gt + lastpos + 1);
+    }
+    if (sh.last_thr < 0 && tid == 0) sh.lnl_tile = 0;
+    __syncthreads();
+
+    // ---- tile prefix: decoupled look-back (wave 0) or two-pass arrays ----
+    if (wid == 0) {
+        uint64_t lbase, lnlb;
+        const uint64_t lnl_tile = sh.lnl_tile;
+        if (LOOKBACK) {
+            if (tile == 0) {
+                lbase = a.pos->lines;
+                lnlb = a.abs_offset;
+                if (lane == 0) {
+                    lb_store(a.lb_cnt, LB_INC | (lbase + total));
+                    lb_store(a.lb_lnl, LB_INC | (lnl_tile > lnlb ? lnl_tile : lnlb));
+                }
+            } else {
+                if (lane == 0) {
+                    lb_store(a.lb_cnt + tile, LB_AGG | total);
+                    lb_store(a.lb_lnl + tile, LB_AGG | lnl_tile);
+                }
+                lbase = look_back<true>(a.lb_cnt, tile, a.err);
+                lnlb = look_back<false>(a.lb_lnl, tile, a.err);
+                if (lane == 0) {
+                    lb_store(a.lb_cnt + tile, LB_INC | (lbase + total));
+                    lb_store(a.lb_lnl + tile, LB_INC | (lnl_tile > lnlb ? lnl_tile : lnlb));
+                }
+            }
+            if (tile == a.n_tiles - 1 && lane == 0) {
+                // advance the running stream position for the next chunk
+                a.pos->lines = lbase + total;
+                a.pos->ends_open = (len > 0 && a.data[len - 1] != '\n') ? 1 : 0;
+            }
+        } else {
+            lbase = a.tp_cnt[tile];
+            lnlb = a.tp_lnl[tile];
+        }
+        if (lane == 0) {
+            sh.line_base = lbase;
+            sh.lnl_before = lnlb;
+        }
+    }
+
+    const uint64_t abs0 = a.abs_offset + (uint64_t)g0;   // absolute offset of tile byte 0
+
+    if (a.emit_lines) {
+        // ---- general path: emit sequence-line descriptors for lines starting here ----
+        __syncthreads();
+        const uint64_t lbase = sh.line_base;
+#pragma unroll 1
+        for (int i = 0; i < 64; ++i) {
+            const int q = 64 * tid + i;
+            if ((uint64_t)(g0 + q) >= len) break;
+            if (buf[FH + q - 1] != '\n') continue;
+            const uint32_t c = sh.tpre[tid] + nl_before_in_thread(buf, tid, q);
+            const uint64_t li = lbase + c;
+            if ((li & 3) != 1) continue;
+            // find the end of the line
+            int64_t e = g0 + q;
+            while ((uint64_t)e < len && (e - g0 < TILE + BH ? buf[FH + (e - g0)] : a.data[e]) != '\n') ++e;
+            const uint64_t L = (uint64_t)e - (uint64_t)(g0 + q);
+            if (L > 1 && L >= a.k) {
+                unsigned long long n = atomicAdd(a.line_count, 1ull);
+                if (n < a.line_cap) {
+                    a.lines_out[n].start = (uint64_t)(g0 + q);
+                    a.lines_out[n].len = L;
+                    a.lines_out[n].line_index = li;
+                } else {
+                    atomicOr(a.err, ERR_LINE_OVERFLOW);
+                }
+            }
+        }
+        return;
+    }
+
+    // ---- SWAR scan: 4-byte windows at every byte vs P[0:4] and rc(P)[0:4] ----
+    const uint32_t P4 = a.p4, R4 = a.r4, PM = a.pmask;
+    uint32_t cand = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t x0 = w[i];
+        const uint32_t x1 = align4(w[i + 1], w[i], 1);
+        const uint32_t x2 = align4(w[i + 1], w[i], 2);
+        const uint32_t x3 = align4(w[i + 1], w[i], 3);
+        uint32_t m;
+        if (FULL4) {
+            m = min(min(min(x0 ^ P4, x1 ^ P4), min(x2 ^ P4, x3 ^ P4)),
+                    min(min(x0 ^ R4, x1 ^ R4), min(x2 ^ R4, x3 ^ R4)));
+        } else {
+            m = min(min(min((x0 ^ P4) & PM, (x1 ^ P4) & PM), min((x2 ^ P4) & PM, (x3 ^ P4) & PM)),
+                    min(min((x0 ^ R4) & PM, (x1 ^ R4) & PM), min((x2 ^ R4) & PM, (x3 ^ R4) & PM)));
+        }
+        cand |= (m == 0 ? 1u : 0u) << i;
+    }
+    __syncthreads();   // line_base / lnl_before visible
+
+    if (cand == 0 || a.plen > a.k) return;
+    const uint64_t lbase = sh.line_base;
+    const uint64_t lnlb = sh.lnl_before;
+    const uint32_t k = a.k, plen = a.plen;
+    const uint64_t smask = (2 * (k - plen) >= 64) ? ~0ull : ((1ull << (2 * (k - plen))) - 1ull);
+
+    while (cand) {
+        const int i = __ffs(cand) - 1;
+        cand &= cand - 1;
+        const uint32_t *lw = (const uint32_t *)(buf + FH + 64 * tid + 4 * i);
+        const uint32_t lo = lw[0], hi = lw[1];
+#pragma unroll 1
+        for (int jj = 0; jj < 4; ++jj) {
+            const int q = 64 * tid + 4 * i + jj;
+            const uint32_t win = align4(hi, lo, jj);
+#pragma unroll 1
+            for (int strand = 0; strand < 2; ++strand) {
+                const uint32_t pat = strand ? R4 : P4;
+                if (((win ^ pat) & PM) != 0) continue;
+                const uint8_t *pp = strand ? s_pr + KMAX_TILE : s_pr;
+                bool ok = true;
+#pragma unroll 1
+                for (uint32_t b = 4; b < plen; ++b) ok &= buf[FH + q + b] == pp[b];
+                if (!ok) continue;
+                const int s = strand ? q + (int)plen - (int)k : q;   // window start, tile-relative
+                // window bytes: '\n' (or past-EOF sentinel) => not a window
+                bool exotic = false, bad = false;
+                uint64_t code = 0, rcode = 0;
+#pragma unroll 1
+                for (uint32_t b = 0; b < k; ++b) {
+                    const uint32_t ch = buf[FH + s + b];
+                    bad |= ch == '\n';
+                    const uint32_t c = base_code(ch);
+                    exotic |= c > 3;
+                    code = (code << 2) | (c & 3u);
+                    rcode = (rcode >> 2) | ((uint64_t)(3u - (c & 3u)) << (2 * (k - 1)));
+                }
+                if (bad) continue;
+                // line context of the window start
+                uint64_t li, lstart;
+                if (s <= 0) {
+                    li = lbase;
+                    lstart = lnlb;
+                } else {
+                    const int thr = (s - 1) >> 6;   // byte s-1 decides; count '\n' in [0, s)
+                    const uint32_t c = sh.tpre[thr] + nl_before_in_thread(buf, thr, s);
+                    li = lbase + c;
+                    lstart = c == 0 ? lnlb : abs0 + (uint64_t)nth_newline(buf, sh.tpre, c) + 1;
+                }
+                if ((li & 3) != 1) continue;
+                const uint64_t sabs = abs0 + (uint64_t)(int64_t)s;
+                const uint64_t rel = sabs - lstart;
+                if (k == 1 && rel == 0 && buf[FH + s + 1] == '\n') continue;   // line.length > 1
+                if (rel > MAXREL) {
+                    atomicOr(a.err, ERR_LINE_TOO_LONG);
+                    continue;
+                }
+                const uint64_t order = (li << 24) | ((uint64_t)strand << 23) |
+                                       (strand ? (uint64_t)(MAXREL - rel) : rel);
+                if (a.dense && !exotic) {
+                    if (a.dense_update) {
+                        const uint64_t idx = (strand ? rcode : code) & smask;
+                        atomicAdd(a.counts + idx, 1ull);
+                        atomicMin(a.first + idx, (unsigned long long)order);
+                    }
+                } else {
+                    unsigned long long n = atomicAdd(a.rec_count, 1ull);
+                    if (n < a.rec_cap) {
+                        Record r;
+                        r.order = order;
+                        r.pos = (uint64_t)(g0 + s);
+                        r.len = k;
+                        r.strand = strand;
+                        a.recs[n] = r;
+                    } else {
+                        atomicOr(a.err, ERR_REC_OVERFLOW);
+                    }
+                }
+            }
+        }
+    }
+}
+
+// Two-pass mode, pass 1: per-tile '\n' count and last '\n' position.
+__global__ __launch_bounds__(TPB) void tile_aggregate_kernel(const uint8_t *data, uint64_t len,
+                                                             uint64_t *agg_cnt, uint64_t *agg_last,
+                                                             unsigned int *err) {
+    __shared__ uint32_t s_cnt[TPB / 64];
+    __shared__ int32_t s_last;
+    const int tid = threadIdx.x;
+    const int64_t g0 = (int64_t)blockIdx.x * TILE;
+    if (tid == 0) s_last = -1;
+    __syncthreads();
+    uint32_t cnt = 0, orall = 0;
+    int last = -1;
+    for (int i = 0; i < 4; ++i) {
+        const int off = (tid + TPB * i) * 16;
+        uint4 v = load_chunk(data, g0 + off, len);
+        orall |= v.x | v.y | v.z | v.w;
+        uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+        for (int j = 0; j < 4; ++j) {
+            uint32_t z = nl_flags(ws[j]);
+            for (int b = 0; b < 4; ++b) {
+                int64_t p = g0 + off + 4 * j + b;
+                if (((z >> (8 * b + 7)) & 1u) && p < (int64_t)len) {
+                    ++cnt;
+                    last = max(last, off + 4 * j + b);
+                }
+            }
+        }
+    }
+    if (orall & 0x80808080u) atomicOr(err, ERR_NONASCII);
+    for (int d = 32; d >= 1; d >>= 1) cnt += __shfl_xor(cnt, d);
+    if ((tid & 63) == 0) s_cnt[tid >> 6] = cnt;
+    if (last >= 0) atomicMax(&s_last, last);
+    __syncthreads();
+    if (tid == 0) {
+        agg_cnt[blockIdx.x] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+        agg_last[blockIdx.x] = s_last < 0 ? 0 : (uint64_t)(g0 + s_last + 1);   // chunk-relative line start + 0 = none
+    }
+}
+
+// ---------------------------------------------------------------------------
+// general windows kernel (any k, any step, any prefix incl. empty)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void windows_kernel(WindowArgs a) {
+    const uint64_t nl = *a.n_lines;
+    const uint32_t k = a.k, step = a.step, plen = a.plen;
+    for (uint64_t li = blockIdx.x; li < nl; li += gridDim.x) {
+        const SeqLine sl = a.lines[li];
+        const uint8_t *line = a.data + sl.start;
+        const uint64_t L = sl.len;
+        const uint64_t nwin = L - k + 1;       // sl.len >= k guaranteed
+        if (nwin - 1 > MAXREL) {
+            if (threadIdx.x == 0) atomicOr(a.err, ERR_LINE_TOO_LONG);
+            continue;
+        }
+        for (int strand = 0; strand < 2; ++strand) {
+            for (uint64_t j = threadIdx.x; j < nwin; j += blockDim.x) {
+                const uint64_t ini = j * step;
+                const uint64_t lo = ini < L ? ini : L;
+                const uint64_t hi = ini + k < L ? ini + k : L;
+                const uint64_t klen = hi - lo;
+                if (klen < plen) continue;
+                bool ok = true;
+                for (uint32_t b = 0; b < plen && ok; ++b) {
+                    const uint8_t c = strand ? comp_byte(line[L - 1 - lo - b]) : line[lo + b];
+                    ok = c == a.P[b];
+                }
+                if (!ok) continue;
+                unsigned long long n = atomicAdd(a.rec_count, 1ull);
+                if (n < a.rec_cap) {
+                    Record r;
+                    r.order = (sl.line_index << 24) | ((uint64_t)strand << 23) | j;
+                    r.pos = strand ? sl.start + (L - hi) : sl.start + lo;
+                    r.len = (uint32_t)klen;
+                    r.strand = strand;
+                    a.recs[n] = r;
+                } else {
+                    atomicOr(a.err, ERR_REC_OVERFLOW);
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// result materialisation
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void dense_compact_kernel(const unsigned long long *counts,
+                                                            const unsigned long long *first, uint64_t n,
+                                                            uint64_t *out_order, uint64_t *out_idx,
+                                                            unsigned long long *out_n) {
+    const int lane = threadIdx.x & 63;
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n; base += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = base + threadIdx.x;
+        const bool pred = i < n && counts[i] != 0;
+        const unsigned long long m = __ballot(pred);
+        if (!m) continue;
+        unsigned long long wbase = 0;
+        if (lane == 0) wbase = atomicAdd(out_n, (unsigned long long)__popcll(m));
+        wbase = __shfl(wbase, 0);
+        if (pred) {
+            const unsigned long long below = m & ((1ull << lane) - 1ull);
+            const uint64_t o = wbase + __popcll(below);
+            out_order[o] = first[i];
+            out_idx[o] = i;
+        }
+    }
+}
+
+// key = P + decode(idx) (k bytes), count gathered from the table
+__global__ __launch_bounds__(256) void dense_decode_kernel(const uint64_t *idx_sorted,
+                                                           const unsigned long long *n_ptr, uint32_t k,
+                                                           uint32_t plen, const uint8_t *P,
+                                                           const unsigned long long *counts,
+                                                           uint8_t *keys_out, uint64_t *counts_out) {
+    const uint64_t n = *n_ptr;
+    const uint32_t sl = k - plen;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t idx = idx_sorted[i];
+        uint8_t *o = keys_out + i * k;
+        for (uint32_t b = 0; b < plen; ++b) o[b] = P[b];
+        for (uint32_t b = 0; b < sl; ++b) o[plen + b] = "ACGT"[(idx >> (2 * (sl - 1 - b))) & 3u];
+        counts_out[i] = counts[idx];
+    }
+}
+
+__global__ __launch_bounds__(256) void gather_records_kernel(const Record *recs, const uint64_t *key_off,
+                                                             uint64_t n, const uint8_t *data, uint8_t *out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const Record r = recs[i];
+        uint8_t *o = out + key_off[i];
+        const uint8_t *src = data + r.pos;
+        if (r.strand) {
+            for (uint32_t b = 0; b < r.len; ++b) o[b] = comp_byte(src[r.len - 1 - b]);
+        } else {
+            for (uint32_t b = 0; b < r.len; ++b) o[b] = src[b];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// synthetic FASTQ: record i = "@r%010d\n" + 150 bases + "\n+\n"
+// + 150 x 'I' + "\n" (317 B), base b = "ACGT"[(mix(seed*G + i*8 + b/32) >> 2(b%32)) & 3]
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix_mix(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void synth_kernel(uint8_t *out, uint64_t seed, uint64_t first_read,
+                                                    uint64_t n_reads) {
+    const uint64_t total = n_reads * 317;
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c * 16 < total;
+         c += (uint64_t)gridDim.x * blockDim.x) {
+        uint8_t bytes[16];
+        for (int b = 0; b < 16; ++b) {
+            const uint64_t o = c * 16 + b;
+            uint8_t ch = 0;
+            if (o < total) {
+                const uint64_t r = o / 317, p = o % 317, i = first_read + r;
+                if (p == 0) ch = '@';
+                else if (p == 1) ch = 'r';
+                else if (p < 12) {
+                    uint64_t v = i;
+                    for (int d = 11 - (int)p; d > 0; --d) v /= 10;
+                    ch = (uint8_t)('0' + v % 10);
+                } else if (p == 12 || p == 163 || p == 165 || p == 316) ch = '\n';
+                else if (p < 163) {
+                    const uint64_t bidx = p - 13;
+                    const uint64_t wv = splitmix_mix(seed * 0x9E3779B97F4A7C15ull + i * 8 + bidx / 32);
+                    ch = (uint8_t)"ACGT"[(wv >> (2 * (bidx % 32))) & 3];
+                } else if (p == 164) ch = '+';
+                else ch = 'I';
+            }
+            bytes[b] = ch;
+        }
+        const uint64_t o = c * 16;
+        if (o + 16 <= total) {
+            uint4 v;
+            uint32_t *vw = (uint32_t *)&v;
+            for (int j = 0; j < 4; ++j)
+                vw[j] = bytes[4 * j] | (bytes[4 * j + 1] << 8) | (bytes[4 * j + 2] << 16) |
+                        ((uint32_t)bytes[4 * j + 3] << 24);
+            *(uint4 *)(out + o) = v;
+        } else {
+            for (int b = 0; o + b < total; ++b) out[o + b] = bytes[b];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+hipError_t launch_tile(const TileArgs &a, bool lookback, hipStream_t s) {
+    const bool full4 = a.plen >= 4;
+    if (lookback) {
+        if (full4) hipLaunchKernelGGL((tile_kernel<true, true>), dim3(a.n_tiles), dim3(TPB), 0, s, a);
+        else hipLaunchKernelGGL((tile_kernel<true, false>), dim3(a.n_tiles), dim3(TPB), 0, s, a);
+    } else {
+        if (full4) hipLaunchKernelGGL((tile_kernel<false, true>), dim3(a.n_tiles), dim3(TPB), 0, s, a);
+        else hipLaunchKernelGGL((tile_kernel<false, false>), dim3(a.n_tiles), dim3(TPB), 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_aggregate(const uint8_t *data, uint64_t len, uint32_t n_tiles, uint64_t *agg_cnt,
+                                 uint64_t *agg_lnl, unsigned int *err, hipStream_t s) {
+    hipLaunchKernelGGL(tile_aggregate_kernel, dim3(n_tiles), dim3(TPB), 0, s, data, len, agg_cnt, agg_lnl, err);
+    return hipGetLastError();
+}
+
+hipError_t launch_windows(const WindowArgs &a, uint32_t grid, hipStream_t s) {
+    hipLaunchKernelGGL(windows_kernel, dim3(grid), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_dense_compact(const unsigned long long *counts, const unsigned long long *first, uint64_t n,
+                                uint64_t *out_order, uint64_t *out_idx, unsigned long long *out_n,
+                                hipStream_t s) {
+    uint64_t blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(dense_compact_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, counts, first, n, out_order,
+                       out_idx, out_n);
+    return hipGetLastError();
+}
+
+hipError_t launch_dense_decode(const uint64_t *idx_sorted, const unsigned long long *n, uint64_t cap, uint32_t k,
+                               uint32_t plen, const uint8_t *P, const unsigned long long *counts,
+                               uint8_t *keys_out, uint64_t *counts_out, hipStream_t s) {
+    uint64_t blocks = (cap + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(dense_decode_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, idx_sorted, n, k, plen, P,
+                       counts, keys_out, counts_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_records(const Record *recs, const uint64_t *key_off, uint64_t n, const uint8_t *data,
+                                 uint8_t *out, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    uint64_t blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(gather_records_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, recs, key_off, n, data, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_synth_fastq(uint8_t *out, uint64_t seed, uint64_t first_read, uint64_t n_reads, hipStream_t s) {
+    const uint64_t chunks = (n_reads * 317 + 15) / 16;
+    uint64_t blocks = (chunks + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(synth_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, out, seed, first_read, n_reads);
+    return hipGetLastError();
+}
+
+}  // namespace kmerhip

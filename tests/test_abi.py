@@ -1,0 +1,54 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library loads and
+exports every symbol include/kmer_api.h declares (no compute without a GPU)."""
+import ctypes
+import os
+import re
+
+from tests.conftest import REPO
+
+
+def header_symbols():
+    with open(os.path.join(REPO, "include", "kmer_api.h")) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"\b(kmer_[a-z_]+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = ctypes.CDLL(os.path.join(REPO, "kmerjs_amd", "libkmerhip.so"))
+    syms = header_symbols()
+    assert len(syms) >= 18
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_python_binding_lists_header_symbols():
+    from kmerjs_amd import _native
+    assert sorted(_native.EXPORTS) == header_symbols()
+
+
+def test_version_and_status_strings():
+    from kmerjs_amd import _native
+    assert "gfx950" in _native.version()
+    assert _native.LIB.kmer_status_string(5) == b"too many keys"
+
+
+def test_open_rejects_bad_params_without_gpu():
+    from kmerjs_amd import _native
+    for kw in ({"k": 0}, {"step": 0}):
+        try:
+            _native.Counter(**kw)
+        except _native.KmerError as e:
+            assert e.status == 2
+        else:
+            raise AssertionError("accepted %r" % kw)
+
+
+def test_product_does_not_reference_oracle():
+    # the product package must never route through the CPU restatement
+    pkg = os.path.join(REPO, "kmerjs_amd")
+    for root, _, files in os.walk(pkg):
+        for fn in files:
+            if fn.endswith((".py", ".js", ".cc", ".hip", ".hpp")):
+                with open(os.path.join(root, fn), encoding="utf-8") as f:
+                    src = f.read()
+                assert "oracle" not in src.replace("oracle/kmer_oracle.c", ""), fn

@@ -1,0 +1,83 @@
+"""The CPU restatement (oracle/) against the reference's golden vectors.
+
+Goldens come from running the unmodified reference lib/kmers.js
+(tests/golden/gen_golden.py); the KATs are the reference's own tests
+(test/kmers.js:12-52).
+"""
+import hashlib
+
+from oracle import oracle
+from tests.util import digest, js_stringify
+
+
+def test_oracle_matches_every_golden(golden, inputs):
+    bad = []
+    for c in golden["cases"]:
+        e, st = oracle.count_buffer(inputs[c["input"]], c["prefix"].encode(), c["k"], c["step"], stats=True)
+        if digest(e) != c["digest"] or st["lines"] != c["lines"]:
+            bad.append((c["input"], c["prefix"], c["k"], c["step"]))
+    assert not bad, bad[:10]
+
+
+def test_inputs_match_golden_sha(golden, inputs):
+    for name, sha in golden["inputs"].items():
+        assert hashlib.sha256(inputs[name]).hexdigest() == sha, name
+
+
+def test_kat_first_key_kmersInLine():
+    # test/kmers.js:12-19 — the template literal keeps its newline + indentation
+    seq = ("NTTTATGACGCAATACTCCTCTCTCCTTCGTGGTCTTGCAGCGGGTTCTGC\n"
+           "                   ATTTTTATTCCTTTTTGCCCCAACGGCATTCGCGGCGGAACAAACCGTTG")
+    e = oracle.kmers_in_line(seq.encode())
+    assert e[0][0] == b"ATGACGCAATACTCCT"
+    assert e == [(b"ATGACGCAATACTCCT", 1)]
+
+
+def test_kat_complement():
+    # test/kmers.js:21-26
+    assert oracle.complement(b"ATGACCTGAGAGCCTT") == b"AAGGCTCTCAGGTCAT"
+    assert oracle.complement(b"acgtNX\r") == b"\rXNtgca"
+
+
+def test_kat_read_file_sizes(inputs):
+    # test/kmers.js:28-35 and :45-52
+    short = oracle.count_buffer(inputs["test_short.fastq"])
+    assert short == [(b"ATGACGCAATACTCCT", 1), (b"ATGACCTGAGAGCCTT", 1)]
+    assert len(oracle.count_buffer(inputs["test_long.kmer.fastq"])) == 401
+
+
+def test_appendix_c_digests(golden):
+    # SURVEY.md Appendix C (first 16 hex of the ordered digest)
+    want = {("test_short.fastq", "ATGAC", 16): "14056308710d569d",
+            ("test_short.fastq", "", 31): "6c9b4d7ab7bda846",
+            ("test_long.kmer.fastq", "ATGAC", 16): "05444cfc9ac76c53",
+            ("test_long.kmer.fastq", "", 16): "f2884dd21ecdceaa",
+            ("test_kmers.fastq", "ATGAC", 16): "060076d7e1acea40",
+            ("test_kmers.fastq", "", 31): "f5b2531dc2f77941"}
+    got = {(c["input"], c["prefix"], c["k"]): c["digest"][:16] for c in golden["cases"] if c["step"] == 1}
+    for key, d in want.items():
+        assert got[key] == d, key
+
+
+def test_synth_generator_twins():
+    from tests.golden.make_inputs import synth_fastq
+    assert oracle.synth_fastq(7, 123, 50) == synth_fastq(7, 123, 50)
+    b = oracle.synth_fastq(1, 0, 3)
+    assert len(b) == 3 * 317 and b.startswith(b"@r0000000000\n")
+
+
+def test_kmers_long_json_subset(inputs):
+    # test_data/kmers_long.json is the golden Map of the missing test_long.fastq;
+    # test_long.kmer.fastq's 401 keys are a subset with counts <=
+    import json
+    import os
+    here = os.path.dirname(os.path.abspath(__file__))
+    with open(os.path.join(here, "golden", "kmers_long.json")) as f:
+        big = json.load(f)
+    assert len(big) == 6191 and sum(big.values()) == 9301
+    for k, v in oracle.count_buffer(inputs["test_long.kmer.fastq"]):
+        assert k.decode() in big and v <= big[k.decode()]
+
+
+def test_js_stringify_format():
+    assert js_stringify([(b"A\rC", 2)]) == '[["A\\rC",2]]'
