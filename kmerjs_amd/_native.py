@@ -37,6 +37,14 @@ class KmerError(RuntimeError):
 
 
 def _load():
+    # PyTorch-ROCm wheels bundle their own HIP runtime (libamdhip64.so, SONAME
+    # libamdhip64.so.7).  Importing torch first makes the dynamic linker bind
+    # libkmerhip.so to that same runtime, so one process never holds two HIP
+    # runtimes (and device pointers from torch tensors are valid here).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError("libkmerhip.so not built (run `python -c 'import __graft_entry__ as g; g.build()'` "
                           "or `make -C kmerjs_amd/csrc`)")

@@ -527,29 +527,50 @@ __global__ __launch_bounds__(256) void windows_kernel(WindowArgs a) {
 // ---------------------------------------------------------------------------
 // result materialisation
 // ---------------------------------------------------------------------------
+// Nonzero entries of the dense table -> (first-occurrence order, index) pairs.
+// Each block owns one contiguous span: count, ONE global atomic per block,
+// then write (the output order is irrelevant: it is radix-sorted next).
+constexpr int COMPACT_SPAN = 16384;
 __global__ __launch_bounds__(256) void dense_compact_kernel(const unsigned long long *counts,
                                                             const unsigned long long *first, uint64_t n,
                                                             uint64_t *out_order, uint64_t *out_idx,
                                                             unsigned long long *out_n) {
-    const int lane = threadIdx.x & 63;
-    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n; base += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t i = base + threadIdx.x;
-        const bool pred = i < n && counts[i] != 0;
+    __shared__ uint32_t s_wcnt[4];
+    __shared__ unsigned long long s_base;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t lo = (uint64_t)blockIdx.x * COMPACT_SPAN;
+    const uint64_t hi = lo + COMPACT_SPAN < n ? lo + COMPACT_SPAN : n;
+    // pass 1: count (each wave owns a quarter of the span)
+    const uint64_t wlo = lo + (uint64_t)wid * (COMPACT_SPAN / 4);
+    const uint64_t whi = wlo + COMPACT_SPAN / 4 < hi ? wlo + COMPACT_SPAN / 4 : hi;
+    uint32_t c = 0;
+    for (uint64_t b = wlo; b < whi; b += 64) {
+        const uint64_t i = b + lane;
+        const bool pred = i < whi && counts[i] != 0;
+        c += __popcll(__ballot(pred));
+    }
+    if (lane == 0) s_wcnt[wid] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) s_base = atomicAdd(out_n, (unsigned long long)(s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3]));
+    __syncthreads();
+    uint64_t base = s_base;
+    for (int w = 0; w < wid; ++w) base += s_wcnt[w];
+    // pass 2: write
+    for (uint64_t b = wlo; b < whi; b += 64) {
+        const uint64_t i = b + lane;
+        const bool pred = i < whi && counts[i] != 0;
         const unsigned long long m = __ballot(pred);
-        if (!m) continue;
-        unsigned long long wbase = 0;
-        if (lane == 0) wbase = atomicAdd(out_n, (unsigned long long)__popcll(m));
-        wbase = __shfl(wbase, 0);
         if (pred) {
-            const unsigned long long below = m & ((1ull << lane) - 1ull);
-            const uint64_t o = wbase + __popcll(below);
+            const uint64_t o = base + __popcll(m & ((1ull << lane) - 1ull));
             out_order[o] = first[i];
             out_idx[o] = i;
         }
+        base += __popcll(m);
     }
 }
 
-// key = P + decode(idx) (k bytes), count gathered from the table
+// key = P + decode(idx) (k bytes), count gathered from the table.  One lane
+// per 4 output bytes so consecutive lanes write consecutive words.
 __global__ __launch_bounds__(256) void dense_decode_kernel(const uint64_t *idx_sorted,
                                                            const unsigned long long *n_ptr, uint32_t k,
                                                            uint32_t plen, const uint8_t *P,
@@ -557,14 +578,25 @@ __global__ __launch_bounds__(256) void dense_decode_kernel(const uint64_t *idx_s
                                                            uint8_t *keys_out, uint64_t *counts_out) {
     const uint64_t n = *n_ptr;
     const uint32_t sl = k - plen;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t idx = idx_sorted[i];
-        uint8_t *o = keys_out + i * k;
-        for (uint32_t b = 0; b < plen; ++b) o[b] = P[b];
-        for (uint32_t b = 0; b < sl; ++b) o[plen + b] = "ACGT"[(idx >> (2 * (sl - 1 - b))) & 3u];
-        counts_out[i] = counts[idx];
+    const uint64_t words = (n * k + 3) / 4;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t wi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; wi < words; wi += stride) {
+        uint32_t v = 0;
+        for (int b = 0; b < 4; ++b) {
+            const uint64_t o = wi * 4 + b;
+            if (o >= n * k) break;
+            const uint64_t e = o / k;
+            const uint32_t j = (uint32_t)(o - e * k);
+            uint32_t ch;
+            if (j < plen) ch = P[j];
+            else ch = (uint8_t)"ACGT"[(idx_sorted[e] >> (2 * (sl - 1 - (j - plen)))) & 3u];
+            v |= ch << (8 * b);
+        }
+        if (wi * 4 + 4 <= n * k) *(uint32_t *)(keys_out + wi * 4) = v;
+        else for (int b = 0; wi * 4 + b < n * k; ++b) keys_out[wi * 4 + b] = (uint8_t)(v >> (8 * b));
     }
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        counts_out[i] = counts[idx_sorted[i]];
 }
 
 __global__ __launch_bounds__(256) void gather_records_kernel(const Record *recs, const uint64_t *key_off,
@@ -663,8 +695,7 @@ hipError_t launch_windows(const WindowArgs &a, uint32_t grid, hipStream_t s) {
 hipError_t launch_dense_compact(const unsigned long long *counts, const unsigned long long *first, uint64_t n,
                                 uint64_t *out_order, uint64_t *out_idx, unsigned long long *out_n,
                                 hipStream_t s) {
-    uint64_t blocks = (n + 255) / 256;
-    if (blocks > 8192) blocks = 8192;
+    uint64_t blocks = (n + COMPACT_SPAN - 1) / COMPACT_SPAN;
     if (blocks == 0) blocks = 1;
     hipLaunchKernelGGL(dense_compact_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, counts, first, n, out_order,
                        out_idx, out_n);

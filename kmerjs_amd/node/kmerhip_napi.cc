@@ -1,0 +1,271 @@
+// kmerhip_napi.cc — thin N-API addon over the libkmerhip C-ABI
+// (include/kmer_api.h).  All counting runs on the GPU inside napi_async_work
+// (libuv pool); the completion callback hands packed results back to JS,
+// where kmers.js builds the Map in the reference's insertion order.
+//
+// JS surface (used by kmers.js only):
+//   open(k, prefixBuffer, step, device, flags, maxKeys, batchBytes) -> handle
+//   countFile(handle, path, cb(err, {keys, offsets, counts, lines}))
+//   countBuffer(handle, buffer, cb(err, {...}))
+//   close(handle)
+//   version() -> string
+#include <node_api.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/kmer_api.h"
+
+namespace {
+
+#define NAPI_CALL(env, call)                                                    \
+    do {                                                                        \
+        if ((call) != napi_ok) {                                                \
+            napi_throw_error((env), nullptr, "N-API call failed: " #call);     \
+            return nullptr;                                                     \
+        }                                                                       \
+    } while (0)
+
+struct Handle {
+    kmer_ctx *ctx = nullptr;
+    bool busy = false;
+};
+
+struct Work {
+    napi_async_work work = nullptr;
+    napi_ref cb = nullptr;
+    napi_ref keep = nullptr;   // keeps the input Buffer alive
+    Handle *h = nullptr;
+    std::string path;
+    const uint8_t *bytes = nullptr;
+    size_t len = 0;
+    bool is_file = false;
+    kmer_status st = KMER_OK;
+    std::string err;
+    kmer_result *res = nullptr;
+};
+
+void finalize_handle(napi_env, void *data, void *) {
+    Handle *h = static_cast<Handle *>(data);
+    if (h->ctx) kmer_close(h->ctx);
+    delete h;
+}
+
+Handle *get_handle(napi_env env, napi_value v) {
+    void *p = nullptr;
+    if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
+        napi_throw_type_error(env, nullptr, "invalid kmerhip handle");
+        return nullptr;
+    }
+    return static_cast<Handle *>(p);
+}
+
+uint32_t get_u32(napi_env env, napi_value v, uint32_t dflt) {
+    napi_valuetype t;
+    napi_typeof(env, v, &t);
+    if (t != napi_number) return dflt;
+    double d = 0;
+    napi_get_value_double(env, v, &d);
+    return d < 0 ? 0u : (uint32_t)d;
+}
+
+napi_value Open(napi_env env, napi_callback_info info) {
+    size_t argc = 7;
+    napi_value argv[7];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    if (argc < 3) {
+        napi_throw_type_error(env, nullptr, "open(k, prefix, step, ...)");
+        return nullptr;
+    }
+    void *pdata = nullptr;
+    size_t plen = 0;
+    bool isbuf = false;
+    napi_is_buffer(env, argv[1], &isbuf);
+    if (!isbuf) {
+        napi_throw_type_error(env, nullptr, "prefix must be a Buffer (latin1)");
+        return nullptr;
+    }
+    NAPI_CALL(env, napi_get_buffer_info(env, argv[1], &pdata, &plen));
+    kmer_params p;
+    memset(&p, 0, sizeof(p));
+    p.k = get_u32(env, argv[0], 16);
+    p.prefix = (const uint8_t *)pdata;
+    p.prefix_len = (uint32_t)plen;
+    p.step = get_u32(env, argv[2], 1);
+    p.device = argc > 3 ? (int32_t)get_u32(env, argv[3], 0) : 0;
+    p.flags = argc > 4 ? get_u32(env, argv[4], 0) : 0;
+    if (argc > 5) {
+        double d = 0;
+        if (napi_get_value_double(env, argv[5], &d) == napi_ok && d > 0) p.max_keys = (uint64_t)d;
+    }
+    if (argc > 6) {
+        double d = 0;
+        if (napi_get_value_double(env, argv[6], &d) == napi_ok && d > 0) p.batch_bytes = (uint64_t)d;
+    }
+    Handle *h = new Handle();
+    kmer_status st = kmer_open(&p, &h->ctx);
+    if (st != KMER_OK) {
+        delete h;
+        std::string msg = std::string("kmer_open: ") + kmer_status_string(st);
+        napi_value err, code, m;
+        napi_create_string_utf8(env, msg.c_str(), NAPI_AUTO_LENGTH, &m);
+        napi_create_error(env, nullptr, m, &err);
+        napi_create_int32(env, (int)st, &code);
+        napi_set_named_property(env, err, "status", code);
+        napi_throw(env, err);
+        return nullptr;
+    }
+    napi_value ext;
+    NAPI_CALL(env, napi_create_external(env, h, finalize_handle, nullptr, &ext));
+    return ext;
+}
+
+void Execute(napi_env, void *data) {
+    Work *w = static_cast<Work *>(data);
+    if (w->is_file)
+        w->st = kmer_count_file(w->h->ctx, w->path.c_str(), &w->res);
+    else
+        w->st = kmer_count_buffer(w->h->ctx, w->bytes, w->len, &w->res);
+    if (w->st != KMER_OK) w->err = std::string(kmer_status_string(w->st)) + ": " + kmer_last_error(w->h->ctx);
+}
+
+napi_value make_f64_array(napi_env env, const uint64_t *src, size_t n) {
+    napi_value ab, ta;
+    void *data = nullptr;
+    napi_create_arraybuffer(env, n * sizeof(double), &data, &ab);
+    double *d = static_cast<double *>(data);
+    for (size_t i = 0; i < n; ++i) d[i] = (double)src[i];
+    napi_create_typedarray(env, napi_float64_array, n, ab, 0, &ta);
+    return ta;
+}
+
+void Complete(napi_env env, napi_status, void *data) {
+    Work *w = static_cast<Work *>(data);
+    w->h->busy = false;
+    napi_value cb, undef, args[2];
+    napi_get_reference_value(env, w->cb, &cb);
+    napi_get_undefined(env, &undef);
+    if (w->st != KMER_OK) {
+        napi_value m, code;
+        napi_create_string_utf8(env, w->err.c_str(), NAPI_AUTO_LENGTH, &m);
+        napi_create_error(env, nullptr, m, &args[0]);
+        napi_create_int32(env, (int)w->st, &code);
+        napi_set_named_property(env, args[0], "status", code);
+        args[1] = undef;
+    } else {
+        const char *keys = nullptr;
+        const uint64_t *offs = nullptr, *cnts = nullptr;
+        kmer_result_arrays(w->res, &keys, &offs, &cnts);
+        const uint64_t n = kmer_result_size(w->res);
+        napi_value obj, kb, lines;
+        napi_create_object(env, &obj);
+        void *copy = nullptr;
+        napi_create_buffer_copy(env, (size_t)offs[n], n ? keys : "", &copy, &kb);
+        napi_set_named_property(env, obj, "keys", kb);
+        napi_set_named_property(env, obj, "offsets", make_f64_array(env, offs, n + 1));
+        napi_set_named_property(env, obj, "counts", make_f64_array(env, cnts, n));
+        napi_create_double(env, (double)kmer_result_lines(w->res), &lines);
+        napi_set_named_property(env, obj, "lines", lines);
+        args[0] = undef;
+        args[1] = obj;
+        kmer_result_free(w->res);
+    }
+    napi_call_function(env, undef, cb, 2, args, nullptr);
+    napi_delete_reference(env, w->cb);
+    if (w->keep) napi_delete_reference(env, w->keep);
+    napi_delete_async_work(env, w->work);
+    delete w;
+}
+
+napi_value queue(napi_env env, Work *w, napi_value cb) {
+    napi_value name;
+    napi_create_string_utf8(env, "kmerhip.count", NAPI_AUTO_LENGTH, &name);
+    NAPI_CALL(env, napi_create_reference(env, cb, 1, &w->cb));
+    NAPI_CALL(env, napi_create_async_work(env, nullptr, name, Execute, Complete, w, &w->work));
+    w->h->busy = true;
+    NAPI_CALL(env, napi_queue_async_work(env, w->work));
+    napi_value undef;
+    napi_get_undefined(env, &undef);
+    return undef;
+}
+
+napi_value CountFile(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    Handle *h = get_handle(env, argv[0]);
+    if (!h) return nullptr;
+    if (h->busy) {
+        napi_throw_error(env, nullptr, "kmerhip handle busy (one in-flight call per context)");
+        return nullptr;
+    }
+    size_t n = 0;
+    NAPI_CALL(env, napi_get_value_string_utf8(env, argv[1], nullptr, 0, &n));
+    Work *w = new Work();
+    w->path.resize(n + 1);
+    NAPI_CALL(env, napi_get_value_string_utf8(env, argv[1], &w->path[0], n + 1, &n));
+    w->path.resize(n);
+    w->h = h;
+    w->is_file = true;
+    return queue(env, w, argv[2]);
+}
+
+napi_value CountBuffer(napi_env env, napi_callback_info info) {
+    size_t argc = 3;
+    napi_value argv[3];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    Handle *h = get_handle(env, argv[0]);
+    if (!h) return nullptr;
+    if (h->busy) {
+        napi_throw_error(env, nullptr, "kmerhip handle busy (one in-flight call per context)");
+        return nullptr;
+    }
+    void *data = nullptr;
+    size_t len = 0;
+    NAPI_CALL(env, napi_get_buffer_info(env, argv[1], &data, &len));
+    Work *w = new Work();
+    w->h = h;
+    w->bytes = (const uint8_t *)data;
+    w->len = len;
+    NAPI_CALL(env, napi_create_reference(env, argv[1], 1, &w->keep));
+    return queue(env, w, argv[2]);
+}
+
+napi_value Close(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    Handle *h = get_handle(env, argv[0]);
+    if (!h) return nullptr;
+    if (h->ctx && !h->busy) {
+        kmer_close(h->ctx);
+        h->ctx = nullptr;
+    }
+    napi_value undef;
+    napi_get_undefined(env, &undef);
+    return undef;
+}
+
+napi_value Version(napi_env env, napi_callback_info) {
+    napi_value v;
+    napi_create_string_utf8(env, kmer_version(), NAPI_AUTO_LENGTH, &v);
+    return v;
+}
+
+napi_value Init(napi_env env, napi_value exports) {
+    napi_property_descriptor props[] = {
+        {"open", nullptr, Open, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"countFile", nullptr, CountFile, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"countBuffer", nullptr, CountBuffer, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"close", nullptr, Close, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"version", nullptr, Version, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+    };
+    napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
+    return exports;
+}
+
+}  // namespace
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, Init)

@@ -1,0 +1,179 @@
+/* kmers.js — drop-in replacement for kmerjs's lib/kmers.js, backed by the
+ * MI355X HIP counter (libkmerhip via the kmerhip.node N-API addon).
+ *
+ * Same exports, constructor, fields and readFile() contract as the reference,
+ * so KmerFinderClient / KmerFinderServer (which `extends KmerJS`) work
+ * unchanged:
+ *   complementMap, jsonToStrMap, complement, stringToMap, objectToMap,
+ *   mapToJSON, KmerJS                                   lib/kmers.js:12-186
+ * plus the legacy npm-main loop `kmers(line, kmerMap, length, preffix, step)`
+ * (lib/index.js:60-73).
+ *
+ * readFile() resolves to this.kmerMap: a real, mutable JS Map whose
+ * iteration order is the reference's first-occurrence order (consumers rely on
+ * it: lib/kmerFinderServer.js:175,742).  kmersInLine() stays a synchronous CPU
+ * loop over one line, as in the reference (lib/kmers.js:88-100).
+ *
+ * Documented divergences (error/diagnostic paths only): a missing file
+ * rejects the promise (the reference throws from an unhandled stream error,
+ * lib/kmers.js:139); progress is printed once per file instead of once per
+ * line (lib/kmers.js:166-169); env 'browser' is not served by the GPU addon.
+ */
+'use strict';
+const EventEmitter = require('events');
+const path = require('path');
+
+let addon = null;
+function native() {
+    if (!addon) {
+        // fails loudly if the HIP library / addon is not built: no CPU fallback
+        addon = require(path.join(__dirname, 'kmerhip.node'));
+    }
+    return addon;
+}
+
+let BN;
+try {
+    BN = require('bignumber.js');   // the reference's evalue type (lib/kmers.js:75)
+} catch (e) {
+    BN = class SmallBN {            // minimal stand-in with the comparison API consumers use
+        constructor(v) { this.v = Number(v); }
+        cmp(o) { const x = o instanceof SmallBN ? o.v : Number(o); return this.v < x ? -1 : this.v > x ? 1 : 0; }
+        lt(o) { return this.cmp(o) < 0; }
+        gt(o) { return this.cmp(o) > 0; }
+        toNumber() { return this.v; }
+        valueOf() { return this.v; }
+        toString() { return String(this.v); }
+    };
+}
+
+const complementMap = new Map([['A', 'T'], ['T', 'A'], ['G', 'C'], ['C', 'G']]);
+
+function objToStrMap(obj) {
+    const m = new Map();
+    for (const k of Object.keys(obj)) m.set(k, obj[k]);
+    return m;
+}
+function jsonToStrMap(jsonStr) { return objToStrMap(jsonStr); }
+function stringToMap(string) { return objToStrMap(JSON.parse(string)); }
+function objectToMap(object) { return objToStrMap(object); }
+function mapToJSON(strMap) {
+    const obj = Object.create(null);
+    for (const [k, v] of strMap) obj[k] = v;
+    return obj;
+}
+
+// reverse complement; only A/T/G/C are mapped, every other char is kept (lib/kmers.js:31-38)
+function complement(string) {
+    let out = '';
+    for (let i = string.length - 1; i >= 0; i -= 1) {
+        const c = string[i];
+        const m = complementMap.get(c);
+        out += m === undefined ? c : m;
+    }
+    return out;
+}
+
+// legacy loop of the npm main (lib/index.js:60-73)
+function kmers(line, kmerMap, length, preffix, step) {
+    const stop = line.length - length + 1;
+    let ini = 0;
+    for (let index = 0; index < stop; index += 1) {
+        const key = line.substring(ini, ini + length);
+        if (key.startsWith(preffix)) kmerMap.set(key, (kmerMap.get(key) || 0) + 1);
+        ini += step;
+    }
+    return true;
+}
+
+// Fold a packed native result into an existing Map, preserving Map semantics:
+// existing keys keep their position, new keys append in first-occurrence order.
+function foldResult(map, res) {
+    const keys = res.keys;
+    const off = res.offsets;
+    const cnt = res.counts;
+    const n = cnt.length;
+    for (let i = 0; i < n; i += 1) {
+        const key = keys.latin1Slice(off[i], off[i + 1]);
+        const prev = map.get(key);
+        map.set(key, prev === undefined ? cnt[i] : prev + cnt[i]);
+    }
+}
+
+class KmerJS {
+    constructor(fastq = '', preffix = 'ATGAC', length = 16, step = 1,
+        coverage = 1, progress = true, env = 'node') {
+        this.fastq = fastq;
+        this.preffix = preffix;
+        this.kmerLength = length;
+        this.step = step;
+        this.progress = progress;
+        this.coverage = coverage;
+        this.evalue = new BN(0.05);
+        this.kmerMap = new Map();
+        this.kmerMapSize = 0;
+        this.env = env;
+        if (env === 'browser') this.fileDataRead = 0;
+    }
+
+    kmersInLine(line) {
+        const k = this.kmerLength;
+        const p = this.preffix;
+        const stop = line.length - k;
+        let ini = 0;
+        for (let index = 0; index <= stop; index += 1) {
+            const kmer = line.substring(ini, ini + k);
+            if (kmer.startsWith(p)) this.kmerMap.set(kmer, (this.kmerMap.get(kmer) || 0) + 1);
+            ini += this.step;
+        }
+    }
+
+    readFile() {
+        const kmerObj = this;
+        const event = new EventEmitter();
+        kmerObj.lines = 0;
+        kmerObj.bytesRead = 0;
+        kmerObj.linesPerChunk = 0;
+        const promise = new Promise((resolve, reject) => {
+            if (kmerObj.env !== 'node') {
+                reject(new Error("kmerjs_amd: env '" + kmerObj.env + "' is not served by the GPU addon"));
+                return;
+            }
+            let handle;
+            try {
+                handle = native().open(kmerObj.kmerLength, Buffer.from(String(kmerObj.preffix), 'latin1'),
+                    kmerObj.step, Number(process.env.KMERHIP_DEVICE || 0));
+            } catch (e) {
+                reject(e);
+                return;
+            }
+            native().countFile(handle, String(kmerObj.fastq), (err, res) => {
+                native().close(handle);
+                if (err) {
+                    reject(err);
+                    return;
+                }
+                foldResult(kmerObj.kmerMap, res);
+                kmerObj.lines = res.lines;
+                event.emit('progress', { percentage: 100, transferred: 0, length: 0 });
+                if (kmerObj.progress) {
+                    process.stdout.write(`Lines: ${res.lines} / Kmers: ${kmerObj.kmerMap.size}\r`);
+                    process.stdout.write('\n                               \n');
+                }
+                kmerObj.kmerMapSize = kmerObj.kmerMap.size;
+                resolve(kmerObj.kmerMap);
+            });
+        });
+        return { promise, event };
+    }
+}
+
+// README-style convenience (README.md:15): kmerjs(fastq, preffix, length, step) -> Promise<Map>
+function kmerjs(fastq, preffix = 'ATGAC', length = 16, step = 1) {
+    return new KmerJS(fastq, preffix, length, step, 1, false, 'node').readFile().promise;
+}
+
+module.exports = {
+    complementMap, jsonToStrMap, complement, stringToMap, objectToMap, mapToJSON, KmerJS,
+    kmers, kmerjs, version: () => native().version(),
+};
