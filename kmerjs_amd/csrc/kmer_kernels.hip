@@ -131,6 +131,8 @@ __device__ __forceinline__ uint4 load_chunk(const uint8_t *data, int64_t g, uint
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+constexpr int QCAP = 1024;
+
 struct TileShared {
     uint32_t tpre[TPB + 1];      // exclusive '\n' count per thread inside the tile; [TPB] = total
     uint32_t wsum[TPB / 64];
@@ -139,6 +141,9 @@ struct TileShared {
     uint64_t line_base;          // global line index of the tile's first byte
     uint64_t lnl_before;         // absolute start of the line containing the tile's first byte
     uint64_t lnl_tile;           // absolute line start after the tile's last '\n' (0 = none)
+    uint32_t qn;                 // hit queue fill
+    uint32_t more;               // a lane could not queue all its hits this round
+    uint32_t q[1024];            // verified hits: (tile position << 1) | strand
 };
 
 // newline count in [64*thr, q) for tile-relative q within thread thr's range
@@ -155,27 +160,38 @@ __device__ __forceinline__ uint32_t nl_before_in_thread(const uint8_t *buf, int 
     return c;
 }
 
-// tile-relative position of the c-th (1-based) '\n' of the tile
-__device__ int nth_newline(const uint8_t *buf, const uint32_t *tpre, uint32_t c) {
-    int lo = 0, hi = TPB - 1;     // largest thr with tpre[thr] < c
-    while (lo < hi) {
-        int mid = (lo + hi + 1) >> 1;
-        if (tpre[mid] < c) lo = mid; else hi = mid - 1;
-    }
-    uint32_t need = c - tpre[lo];
-    const uint8_t *p = buf + FH + 64 * lo;
+// unaligned 32-bit read of tile bytes at tile-relative position p (p >= -FH)
+__device__ __forceinline__ uint32_t lds_word(const uint8_t *buf, int p) {
+    const int a = FH + p;
+    const uint32_t *w = (const uint32_t *)(buf + (a & ~3));
+    return align4(w[1], w[0], (uint32_t)(a & 3));
+}
+
+// position of the last '\n' inside thread thr's 64 bytes (-1 if none)
+__device__ __forceinline__ int last_newline_in_thread(const uint8_t *buf, int thr) {
+    const uint32_t *lw = (const uint32_t *)(buf + FH + 64 * thr);
 #pragma unroll 1
-    for (int i = 0; i < 64; ++i) {
-        if (p[i] == '\n' && --need == 0) return 64 * lo + i;
+    for (int i = 15; i >= 0; --i) {
+        const uint32_t z = nl_flags(lw[i]);
+        if (z) return 64 * thr + 4 * i + ((31 - __clz(z)) >> 3);
     }
-    return -1;  // unreachable for consistent inputs
+    return -1;
+}
+
+// reverse complement of a 2-bit code of k bases (A=0 C=1 G=2 T=3)
+__device__ __forceinline__ uint64_t revcomp_code(uint64_t x, uint32_t k) {
+    x = ~x;
+    x = ((x >> 2) & 0x3333333333333333ull) | ((x & 0x3333333333333333ull) << 2);
+    x = ((x >> 4) & 0x0F0F0F0F0F0F0F0Full) | ((x & 0x0F0F0F0F0F0F0F0Full) << 4);
+    x = __builtin_bswap64(x);
+    return k >= 32 ? x : (x >> (64 - 2 * k));
 }
 
 template <bool LOOKBACK, bool FULL4>
 __global__ __launch_bounds__(TPB) void tile_kernel(TileArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t buf[BUFSZ];
     __shared__ TileShared sh;
-    __shared__ uint8_t s_pr[2 * KMAX_TILE];
+    __shared__ __attribute__((aligned(16))) uint8_t s_pr[2 * KMAX_TILE];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wid = tid >> 6;
@@ -357,87 +373,137 @@ __global__ __launch_bounds__(TPB) void tile_kernel(TileArgs a) {
         cand |= (m == 0 ? 1u : 0u) << i;
     }
     __syncthreads();   // line_base / lnl_before visible
-
-    if (cand == 0 || a.plen > a.k) return;
+    if (a.plen > a.k) return;
     const uint64_t lbase = sh.line_base;
     const uint64_t lnlb = sh.lnl_before;
     const uint32_t k = a.k, plen = a.plen;
     const uint64_t smask = (2 * (k - plen) >= 64) ? ~0ull : ((1ull << (2 * (k - plen))) - 1ull);
+    const uint32_t *pw = (const uint32_t *)s_pr;             // P words, then rc(P) words
 
-    while (cand) {
-        const int i = __ffs(cand) - 1;
-        cand &= cand - 1;
-        const uint32_t *lw = (const uint32_t *)(buf + FH + 64 * tid + 4 * i);
-        const uint32_t lo = lw[0], hi = lw[1];
+    // ---- hits: verify candidates into an LDS queue, then one hit per lane ----
+    // Rounds bound the queue; a lane resumes at its cursor (word bit, sub-position).
+    uint32_t sub = 0;                                        // next (jj*2 + strand) in the current word
+    while (true) {
+        __syncthreads();                                     // previous round done (queue + `more` read)
+        if (tid == 0) { sh.qn = 0; sh.more = 0; }
+        __syncthreads();
+        while (cand) {
+            const int i = __ffs(cand) - 1;
+            const int q0 = 64 * tid + 4 * i;
+            const uint32_t lo = *(const uint32_t *)(buf + FH + q0);
+            const uint32_t hi = *(const uint32_t *)(buf + FH + q0 + 4);
+            bool full = false;
 #pragma unroll 1
-        for (int jj = 0; jj < 4; ++jj) {
-            const int q = 64 * tid + 4 * i + jj;
-            const uint32_t win = align4(hi, lo, jj);
-#pragma unroll 1
-            for (int strand = 0; strand < 2; ++strand) {
-                const uint32_t pat = strand ? R4 : P4;
-                if (((win ^ pat) & PM) != 0) continue;
-                const uint8_t *pp = strand ? s_pr + KMAX_TILE : s_pr;
+            for (; sub < 8; ++sub) {
+                const uint32_t jj = sub >> 1, strand = sub & 1;
+                const uint32_t win = align4(hi, lo, jj);
+                if (((win ^ (strand ? R4 : P4)) & PM) != 0) continue;
                 bool ok = true;
+                const int q = q0 + (int)jj;
 #pragma unroll 1
-                for (uint32_t b = 4; b < plen; ++b) ok &= buf[FH + q + b] == pp[b];
-                if (!ok) continue;
-                const int s = strand ? q + (int)plen - (int)k : q;   // window start, tile-relative
-                // window bytes: '\n' (or past-EOF sentinel) => not a window
-                bool exotic = false, bad = false;
-                uint64_t code = 0, rcode = 0;
-#pragma unroll 1
-                for (uint32_t b = 0; b < k; ++b) {
-                    const uint32_t ch = buf[FH + s + b];
-                    bad |= ch == '\n';
-                    const uint32_t c = base_code(ch);
-                    exotic |= c > 3;
-                    code = (code << 2) | (c & 3u);
-                    rcode = (rcode >> 2) | ((uint64_t)(3u - (c & 3u)) << (2 * (k - 1)));
+                for (uint32_t b = 4; b < plen && ok; b += 4) {
+                    const uint32_t n = plen - b;
+                    const uint32_t mk = n >= 4 ? 0xFFFFFFFFu : ((1u << (8 * n)) - 1u);
+                    ok = ((lds_word(buf, q + (int)b) ^ pw[(strand ? KMAX_TILE / 4 : 0) + b / 4]) & mk) == 0;
                 }
-                if (bad) continue;
-                // line context of the window start
-                uint64_t li, lstart;
-                if (s <= 0) {
-                    li = lbase;
+                if (!ok) continue;
+                const uint32_t slot = atomicAdd(&sh.qn, 1u);
+                if (slot >= QCAP) { full = true; break; }
+                sh.q[slot] = ((uint32_t)q << 1) | strand;
+            }
+            if (full) { sh.more = 1; break; }
+            sub = 0;
+            cand &= cand - 1;
+        }
+        __syncthreads();
+        const bool again = sh.more != 0;
+        const uint32_t nq = min(sh.qn, (uint32_t)QCAP);
+        for (uint32_t h = tid; h < nq; h += TPB) {
+            const uint32_t e = sh.q[h];
+            const int strand = (int)(e & 1u);
+            const int q = (int)(e >> 1);
+            const int s0 = strand ? q + (int)plen - (int)k : q;   // window start, tile-relative
+            // window bytes: ACGT check (v_perm against "ACGT"), '\n' check, 2-bit codes
+            bool exotic = false, hasnl = false;
+            uint64_t code = 0;
+#pragma unroll 1
+            for (uint32_t b = 0; b < k; b += 4) {
+                const uint32_t x = lds_word(buf, s0 + (int)b);
+                const uint32_t nb = k - b >= 4 ? 4u : k - b;
+                const uint32_t mk = nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
+                const uint32_t c = ((x >> 1) ^ (x >> 2)) & 0x03030303u;
+                const uint32_t expect = __builtin_amdgcn_perm(0u, 0x54474341u, c);   // "ACGT"[c] per byte
+                exotic |= ((expect ^ x) & mk) != 0;
+                hasnl |= (nl_flags(x) & mk) != 0;
+                const uint32_t packed = ((c & 3u) << 6) | (((c >> 8) & 3u) << 4) | (((c >> 16) & 3u) << 2) |
+                                        ((c >> 24) & 3u);            // first byte most significant
+                code = (code << (2 * nb)) | (packed >> (2 * (4 - nb)));
+            }
+            if (hasnl) continue;          // crosses a line end (or the end of input)
+            // line context of the window start
+            uint64_t li, lstart;
+            if (s0 <= 0) {
+                li = lbase;
+                lstart = lnlb;
+            } else {
+                const int ts = (s0 - 1) >> 6;
+                uint32_t cnt = 0;
+                int last = -1;
+                const uint32_t *lw = (const uint32_t *)(buf + FH + 64 * ts);
+#pragma unroll 1
+                for (int i = 0; 64 * ts + 4 * i < s0; ++i) {
+                    uint32_t z = nl_flags(lw[i]);
+                    const int rem = s0 - (64 * ts + 4 * i);
+                    if (rem < 4) z &= (1u << (8 * rem)) - 1u;
+                    cnt += __popc(z);
+                    if (z) last = 64 * ts + 4 * i + ((31 - __clz(z)) >> 3);
+                }
+                const uint32_t c = sh.tpre[ts] + cnt;
+                li = lbase + c;
+                if (last >= 0) {
+                    lstart = abs0 + (uint64_t)(last + 1);
+                } else if (c == 0) {
                     lstart = lnlb;
                 } else {
-                    const int thr = (s - 1) >> 6;   // byte s-1 decides; count '\n' in [0, s)
-                    const uint32_t c = sh.tpre[thr] + nl_before_in_thread(buf, thr, s);
-                    li = lbase + c;
-                    lstart = c == 0 ? lnlb : abs0 + (uint64_t)nth_newline(buf, sh.tpre, c) + 1;
-                }
-                if ((li & 3) != 1) continue;
-                const uint64_t sabs = abs0 + (uint64_t)(int64_t)s;
-                const uint64_t rel = sabs - lstart;
-                if (k == 1 && rel == 0 && buf[FH + s + 1] == '\n') continue;   // line.length > 1
-                if (rel > MAXREL) {
-                    atomicOr(a.err, ERR_LINE_TOO_LONG);
-                    continue;
-                }
-                const uint64_t order = (li << 24) | ((uint64_t)strand << 23) |
-                                       (strand ? (uint64_t)(MAXREL - rel) : rel);
-                if (a.dense && !exotic) {
-                    if (a.dense_update) {
-                        const uint64_t idx = (strand ? rcode : code) & smask;
-                        atomicAdd(a.counts + idx, 1ull);
-                        atomicMin(a.first + idx, (unsigned long long)order);
+                    // the c-th '\n' is the last one of the last earlier thread that has any
+                    int lo2 = 0, hi2 = ts - 1;                  // largest t with tpre[t] < c
+                    while (lo2 < hi2) {
+                        const int mid = (lo2 + hi2 + 1) >> 1;
+                        if (sh.tpre[mid] < c) lo2 = mid; else hi2 = mid - 1;
                     }
+                    lstart = abs0 + (uint64_t)(last_newline_in_thread(buf, lo2) + 1);
+                }
+            }
+            if ((li & 3) != 1) continue;
+            const uint64_t sabs = abs0 + (uint64_t)(int64_t)s0;
+            const uint64_t rel = sabs - lstart;
+            if (k == 1 && rel == 0 && buf[FH + s0 + 1] == '\n') continue;   // line.length > 1
+            if (rel > MAXREL) {
+                atomicOr(a.err, ERR_LINE_TOO_LONG);
+                continue;
+            }
+            const uint64_t order = (li << 24) | ((uint64_t)strand << 23) | (strand ? (uint64_t)(MAXREL - rel) : rel);
+            if (a.dense && !exotic) {
+                if (a.dense_update) {
+                    const uint64_t idx = (strand ? revcomp_code(code, k) : code) & smask;
+                    atomicAdd(a.counts + idx, 1ull);
+                    atomicMin(a.first + idx, (unsigned long long)order);
+                }
+            } else {
+                const unsigned long long n = atomicAdd(a.rec_count, 1ull);
+                if (n < a.rec_cap) {
+                    Record r;
+                    r.order = order;
+                    r.pos = (uint64_t)(g0 + s0);
+                    r.len = k;
+                    r.strand = (uint32_t)strand;
+                    a.recs[n] = r;
                 } else {
-                    unsigned long long n = atomicAdd(a.rec_count, 1ull);
-                    if (n < a.rec_cap) {
-                        Record r;
-                        r.order = order;
-                        r.pos = (uint64_t)(g0 + s);
-                        r.len = k;
-                        r.strand = strand;
-                        a.recs[n] = r;
-                    } else {
-                        atomicOr(a.err, ERR_REC_OVERFLOW);
-                    }
+                    atomicOr(a.err, ERR_REC_OVERFLOW);
                 }
             }
         }
+        if (!again) break;
     }
 }
 
