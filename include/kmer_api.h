@@ -112,8 +112,11 @@ void kmer_result_free(kmer_result *r);
 kmer_status kmer_synth_fastq_device(void *d_out, uint64_t seed, uint64_t first_read, uint64_t n_reads,
                                     void *stream);
 
-/* Timing of the last finish (device time of the counting kernels, ms). */
-kmer_status kmer_last_timing(kmer_ctx *ctx, double *count_ms, double *finish_ms);
+/* Device time (HIP events on the context's stream, ms) since the last reset:
+ * scan_ms = the streaming tile-scan kernel(s) alone, feed_ms = every kernel of
+ * the feeds (scan + line scans + hit resolution), finish_ms = the last finish
+ * (compaction + sort + decode). */
+kmer_status kmer_last_timing(kmer_ctx *ctx, double *scan_ms, double *feed_ms, double *finish_ms);
 
 const char *kmer_status_string(kmer_status s);
 const char *kmer_last_error(const kmer_ctx *ctx);

@@ -69,7 +69,7 @@ def _load():
                                               ctypes.POINTER(pu64)]),
         "kmer_result_free": (None, [vp]),
         "kmer_synth_fastq_device": (ctypes.c_int, [vp, u64, u64, u64, vp]),
-        "kmer_last_timing": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double),
+        "kmer_last_timing": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                             ctypes.POINTER(ctypes.c_double)]),
         "kmer_status_string": (ctypes.c_char_p, [ctypes.c_int]),
         "kmer_last_error": (ctypes.c_char_p, [vp]),
@@ -191,9 +191,10 @@ class Counter:
         return n.value
 
     def last_timing(self):
-        a, b = ctypes.c_double(), ctypes.c_double()
-        self._check(LIB.kmer_last_timing(self.h, ctypes.byref(a), ctypes.byref(b)), "last_timing")
-        return a.value, b.value
+        """(scan_kernel_ms, feed_ms, finish_ms) device times since the last reset."""
+        a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        self._check(LIB.kmer_last_timing(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "last_timing")
+        return a.value, b.value, c.value
 
 
 def synth_fastq_device(ptr: int, seed: int, first_read: int, n_reads: int, stream: int = 0):

@@ -9,6 +9,7 @@
 // the reference Map's exact iteration order (lib/kmers.js:76,95).
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -55,6 +56,15 @@ struct kmer_ctx {
     uint64_t tile_cap = 0;
     unsigned long long *d_lb_cnt = nullptr, *d_lb_lnl = nullptr;
     uint64_t *d_tp_cnt = nullptr, *d_tp_lnl = nullptr;
+    // streaming scan path: per-tile aggregates, their scans, hit slots
+    uint64_t *d_agg_cnt = nullptr, *d_agg_lnl = nullptr, *d_cscan = nullptr, *d_lnl_before = nullptr;
+    uint32_t *d_tile_nhits = nullptr;
+    HitRec *d_hits = nullptr;
+    HitRec *d_ovf = nullptr;
+    uint64_t ovf_cap = 0;
+    unsigned long long *d_ovf_count = nullptr;
+    void *d_scan_tmp = nullptr;
+    size_t scan_tmp_bytes = 0;
     // small device words
     unsigned int *d_ticket = nullptr, *d_err = nullptr;
     unsigned long long *d_rec_count = nullptr, *d_line_count = nullptr, *d_nout = nullptr;
@@ -86,8 +96,8 @@ struct kmer_ctx {
     uint8_t *h_stage = nullptr;
     uint64_t stage_cap = 0;
     // timing
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr;
-    double count_ms = 0.0, finish_ms = 0.0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr;
+    double count_ms = 0.0, finish_ms = 0.0, feed_ms = 0.0;
 };
 
 namespace {
@@ -142,11 +152,30 @@ kmer_status ensure_tiles(kmer_ctx *c, uint64_t n_tiles) {
     dfree(c->d_lb_lnl);
     dfree(c->d_tp_cnt);
     dfree(c->d_tp_lnl);
+    dfree(c->d_agg_cnt); dfree(c->d_agg_lnl); dfree(c->d_cscan); dfree(c->d_lnl_before);
+    dfree(c->d_tile_nhits); dfree(c->d_hits);
+    if (c->d_scan_tmp) (void)hipFree(c->d_scan_tmp);
+    c->d_scan_tmp = nullptr;
     uint64_t cap = std::max<uint64_t>(n_tiles, 1024);
     HIPCHK(c, dalloc(&c->d_lb_cnt, cap));
     HIPCHK(c, dalloc(&c->d_lb_lnl, cap));
     HIPCHK(c, dalloc(&c->d_tp_cnt, cap));
     HIPCHK(c, dalloc(&c->d_tp_lnl, cap));
+    if (c->mode != MODE_GENERAL) {
+        HIPCHK(c, dalloc(&c->d_agg_cnt, cap));
+        HIPCHK(c, dalloc(&c->d_agg_lnl, cap));
+        HIPCHK(c, dalloc(&c->d_cscan, cap));
+        HIPCHK(c, dalloc(&c->d_lnl_before, cap));
+        HIPCHK(c, dalloc(&c->d_tile_nhits, cap));
+        HIPCHK(c, dalloc(&c->d_hits, cap * HMAX));
+        size_t a = 0, b = 0;
+        HIPCHK(c, rocprim::exclusive_scan(nullptr, a, c->d_agg_cnt, c->d_cscan, (uint64_t)0, (size_t)cap,
+                                          rocprim::plus<uint64_t>(), c->stream));
+        HIPCHK(c, rocprim::exclusive_scan(nullptr, b, c->d_agg_lnl, c->d_lnl_before, (uint64_t)0, (size_t)cap,
+                                          rocprim::maximum<uint64_t>(), c->stream));
+        c->scan_tmp_bytes = std::max(a, b);
+        HIPCHK(c, hipMalloc(&c->d_scan_tmp, std::max<size_t>(c->scan_tmp_bytes, 16)));
+    }
     c->tile_cap = cap;
     return KMER_OK;
 }
@@ -172,6 +201,16 @@ kmer_status ensure_lines(kmer_ctx *c, uint64_t n) {
     uint64_t cap = std::max<uint64_t>(n, 1 << 16);
     HIPCHK(c, dalloc(&c->d_lines, cap));
     c->line_cap = cap;
+    return KMER_OK;
+}
+
+kmer_status ensure_ovf(kmer_ctx *c, uint64_t n) {
+    if (n <= c->ovf_cap) return KMER_OK;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    dfree(c->d_ovf);
+    uint64_t cap = std::max<uint64_t>(n, 1 << 16);
+    HIPCHK(c, dalloc(&c->d_ovf, cap));
+    c->ovf_cap = cap;
     return KMER_OK;
 }
 
@@ -240,6 +279,115 @@ kmer_status two_pass_prefix(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_
     return KMER_OK;
 }
 
+// Fast path (dense / tile-record modes): streaming tile scan -> scans of the
+// per-tile aggregates -> hit resolution -> stream position update.
+kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s) {
+    ScanArgs a;
+    memset(&a, 0, sizeof(a));
+    a.data = d;
+    a.len = len;
+    a.abs_offset = c->abs_offset;
+    a.n_tiles = n_tiles;
+    a.k = c->p.k;
+    a.plen = (uint32_t)c->prefix.size();
+    a.p4 = pack4(c->prefix);
+    a.r4 = pack4(c->rprefix);
+    a.pmask = a.plen >= 4 ? 0xFFFFFFFFu : ((1u << (8 * a.plen)) - 1u);
+    a.PR = c->d_PR;
+    a.agg_cnt = c->d_agg_cnt;
+    a.agg_lnl = c->d_agg_lnl;
+    a.hits = c->d_hits;
+    a.tile_nhits = c->d_tile_nhits;
+    a.ovf = c->d_ovf;
+    a.ovf_count = c->d_ovf_count;
+    a.ovf_cap = c->ovf_cap;
+    a.err = c->d_err;
+
+    HitArgs h;
+    memset(&h, 0, sizeof(h));
+    h.hits = c->d_hits;
+    h.tile_nhits = c->d_tile_nhits;
+    h.ovf = c->d_ovf;
+    h.ovf_count = c->d_ovf_count;
+    h.ovf_cap = c->ovf_cap;
+    h.n_tiles = n_tiles;
+    h.k = a.k;
+    h.plen = a.plen;
+    h.abs_offset = c->abs_offset;
+    h.pos = c->d_pos;
+    h.cscan = c->d_cscan;
+    h.lnl_before = c->d_lnl_before;
+    h.dense = c->mode == MODE_DENSE;
+    h.dense_update = 1;
+    h.smask = (2 * (a.k - std::min(a.plen, a.k)) >= 64) ? ~0ull : ((1ull << (2 * (a.k - std::min(a.plen, a.k)))) - 1ull);
+    h.counts = c->d_counts;
+    h.first = c->d_first;
+    h.recs = c->d_recs;
+    h.rec_count = c->d_rec_count;
+    h.rec_cap = c->rec_cap;
+    h.err = c->d_err;
+
+    HIPCHK(c, hipMemcpyAsync(c->d_pos_saved, c->d_pos, sizeof(StreamPos), hipMemcpyDeviceToDevice, s));
+    kmer_status st;
+    for (int attempt = 0; attempt < 8; ++attempt) {
+        HIPCHK(c, hipMemsetAsync(c->d_ovf_count, 0, 8, s));
+        HIPCHK(c, hipMemsetAsync(c->d_rec_count, 0, 8, s));
+        HIPCHK(c, hipEventRecord(c->ev0, s));
+        HIPCHK(c, launch_scan_tiles(a, s));
+        HIPCHK(c, hipEventRecord(c->ev1, s));
+        size_t tmp = c->scan_tmp_bytes;
+        HIPCHK(c, rocprim::exclusive_scan(c->d_scan_tmp, tmp, c->d_agg_cnt, c->d_cscan, (uint64_t)0, (size_t)n_tiles,
+                                          rocprim::plus<uint64_t>(), s));
+        tmp = c->scan_tmp_bytes;
+        HIPCHK(c, rocprim::exclusive_scan(c->d_scan_tmp, tmp, c->d_agg_lnl, c->d_lnl_before, (uint64_t)c->abs_offset,
+                                          (size_t)n_tiles, rocprim::maximum<uint64_t>(), s));
+        HIPCHK(c, launch_hits(h, s));
+        HIPCHK(c, launch_pos_update(c->d_pos, c->d_cscan, c->d_agg_cnt, n_tiles, d, len, s));
+        HIPCHK(c, hipEventRecord(c->ev4, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 0, c->d_rec_count, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 1, c->d_ovf_count, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 2, c->d_err, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        const uint32_t e = (uint32_t)c->h_small[2];
+        st = check_err(c, e);
+        if (st) return st;
+        float ms = 0.f, ms_all = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        HIPCHK(c, hipEventElapsedTime(&ms_all, c->ev0, c->ev4));
+        c->count_ms += ms;
+        c->feed_ms += ms_all;
+        if (e & (ERR_OVF_OVERFLOW | ERR_REC_OVERFLOW)) {
+            HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
+            HIPCHK(c, hipMemcpyAsync(c->d_pos, c->d_pos_saved, sizeof(StreamPos), hipMemcpyDeviceToDevice, s));
+            if (e & ERR_OVF_OVERFLOW) {
+                // nothing was resolved: plain redo with a larger overflow list
+                st = ensure_ovf(c, c->h_small[1] + 1024);
+                if (st) return st;
+                a.ovf = c->d_ovf;
+                h.ovf = c->d_ovf;
+                a.ovf_cap = c->ovf_cap;
+                h.ovf_cap = c->ovf_cap;
+            } else {
+                // dense table already holds this chunk: redo for the records only
+                st = ensure_records(c, c->h_small[0] + 1024);
+                if (st) return st;
+                h.recs = c->d_recs;
+                h.rec_cap = c->rec_cap;
+                h.dense_update = 0;
+            }
+            continue;
+        }
+        break;
+    }
+    const uint64_t nrec = c->h_small[0];
+    if (nrec) {
+        st = drain_records(c, d, nrec, s);
+        if (st) return st;
+    }
+    c->abs_offset += len;
+    return KMER_OK;
+}
+
 kmer_status feed(kmer_ctx *c, const uint8_t *d, uint64_t len, hipStream_t s) {
     if (len == 0) return KMER_OK;
     const uint64_t n_tiles64 = (len + TILE - 1) / TILE;
@@ -247,6 +395,7 @@ kmer_status feed(kmer_ctx *c, const uint8_t *d, uint64_t len, hipStream_t s) {
     const uint32_t n_tiles = (uint32_t)n_tiles64;
     kmer_status st = ensure_tiles(c, n_tiles);
     if (st) return st;
+    if (c->mode != MODE_GENERAL) return scan_feed(c, d, len, n_tiles, s);
     const bool lookback = !(c->p.flags & KMER_FLAG_TWO_PASS);
 
     TileArgs a;
@@ -292,7 +441,7 @@ kmer_status feed(kmer_ctx *c, const uint8_t *d, uint64_t len, hipStream_t s) {
             if (st) return st;
         }
         HIPCHK(c, hipEventRecord(c->ev0, s));
-        HIPCHK(c, launch_tile(a, lookback, s));
+        HIPCHK(c, launch_lines(a, lookback, s));
         HIPCHK(c, hipEventRecord(c->ev1, s));
         HIPCHK(c, hipMemcpyAsync(c->h_small + 0, c->d_rec_count, 8, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipMemcpyAsync(c->h_small + 1, c->d_line_count, 8, hipMemcpyDeviceToHost, s));
@@ -391,6 +540,7 @@ kmer_status reset(kmer_ctx *c) {
     c->abs_offset = 0;
     c->count_ms = 0.0;
     c->finish_ms = 0.0;
+    c->feed_ms = 0.0;
     c->open_stream = true;
     return KMER_OK;
 }
@@ -610,9 +760,12 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
     ok &= dalloc(&c->d_pos_saved, 1) == hipSuccess;
     ok &= hipHostMalloc((void **)&c->h_small, 16 * sizeof(uint64_t), hipHostMallocDefault) == hipSuccess;
     ok &= hipEventCreate(&c->ev0) == hipSuccess && hipEventCreate(&c->ev1) == hipSuccess &&
-          hipEventCreate(&c->ev2) == hipSuccess && hipEventCreate(&c->ev3) == hipSuccess;
+          hipEventCreate(&c->ev2) == hipSuccess && hipEventCreate(&c->ev3) == hipSuccess &&
+          hipEventCreate(&c->ev4) == hipSuccess;
+    ok &= dalloc(&c->d_ovf_count, 1) == hipSuccess;
     if (!ok) return cleanup(KMER_E_OOM);
-    if (ensure_records(c, 1 << 16) || ensure_lines(c, 1 << 16) || ensure_tiles(c, 1 << 12))
+    if (ensure_records(c, 1 << 16) || ensure_lines(c, 1 << 16) || ensure_tiles(c, 1 << 12) ||
+        ensure_ovf(c, 1 << 16))
         return cleanup(KMER_E_OOM);
     if (hipMemset(c->d_err, 0, 4) != hipSuccess) return cleanup(KMER_E_DEVICE);
     if (reset(c) != KMER_OK) return cleanup(KMER_E_DEVICE);
@@ -634,9 +787,12 @@ kmer_status kmer_close(kmer_ctx *c) {
     dfree(c->d_keys_out); dfree(c->d_cnt_out); dfree(c->d_P); dfree(c->d_PR);
     if (c->d_sort_tmp) (void)hipFree(c->d_sort_tmp);
     dfree(c->d_batch);
+    dfree(c->d_agg_cnt); dfree(c->d_agg_lnl); dfree(c->d_cscan); dfree(c->d_lnl_before);
+    dfree(c->d_tile_nhits); dfree(c->d_hits); dfree(c->d_ovf); dfree(c->d_ovf_count);
+    if (c->d_scan_tmp) (void)hipFree(c->d_scan_tmp);
     if (c->h_small) (void)hipHostFree(c->h_small);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
-    for (hipEvent_t e : {c->ev0, c->ev1, c->ev2, c->ev3})
+    for (hipEvent_t e : {c->ev0, c->ev1, c->ev2, c->ev3, c->ev4})
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -759,9 +915,10 @@ kmer_status kmer_lines(kmer_ctx *c, uint64_t *lines) {
     return KMER_OK;
 }
 
-kmer_status kmer_last_timing(kmer_ctx *c, double *count_ms, double *finish_ms) {
+kmer_status kmer_last_timing(kmer_ctx *c, double *count_ms, double *feed_ms, double *finish_ms) {
     if (!c) return KMER_E_BAD_PARAM;
     if (count_ms) *count_ms = c->count_ms;
+    if (feed_ms) *feed_ms = c->feed_ms > 0 ? c->feed_ms : c->count_ms;
     if (finish_ms) *finish_ms = c->finish_ms;
     return KMER_OK;
 }

@@ -27,6 +27,7 @@ enum : uint32_t {
     ERR_LOOKBACK_TIMEOUT = 1u << 2,
     ERR_REC_OVERFLOW = 1u << 3,
     ERR_LINE_OVERFLOW = 1u << 4,
+    ERR_OVF_OVERFLOW = 1u << 5,
 };
 
 // look-back word: [63:62] status, [61:0] value
@@ -58,6 +59,55 @@ struct SeqLine {
     uint64_t start;        // chunk-relative byte offset
     uint64_t len;
     uint64_t line_index;   // global line index
+};
+
+// A verified prefix hit from the tile scan with its tile-local line context.
+struct HitRec {
+    uint64_t code;         // 2-bit codes of the k-byte forward window (k <= 32)
+    uint32_t tile;
+    uint32_t qm;           // [13:0] pattern position q, [14] strand, [15] exotic, [16] line start in tile
+    uint32_t c_local;      // '\n' count in the tile before the window start
+    uint32_t lstart;       // tile-relative line start (when [16] is set)
+};
+constexpr int HMAX = 64;   // hit slots per tile (more go to the overflow list)
+
+struct ScanArgs {
+    const uint8_t *data;
+    uint64_t len;
+    uint64_t abs_offset;
+    uint32_t n_tiles, k, plen;
+    uint32_t p4, r4, pmask;
+    const uint8_t *PR;
+    uint64_t *agg_cnt;             // per tile: real '\n' count
+    uint64_t *agg_lnl;             // per tile: absolute line start after its last '\n' (0 = none)
+    HitRec *hits;                  // n_tiles * HMAX slots
+    uint32_t *tile_nhits;
+    HitRec *ovf;
+    unsigned long long *ovf_count;
+    uint64_t ovf_cap;
+    unsigned int *err;
+};
+
+struct HitArgs {
+    const HitRec *hits;
+    const uint32_t *tile_nhits;
+    const HitRec *ovf;
+    const unsigned long long *ovf_count;
+    uint64_t ovf_cap;
+    uint32_t n_tiles, k, plen;
+    uint64_t abs_offset;
+    const StreamPos *pos;
+    const uint64_t *cscan;         // exclusive sum of agg_cnt
+    const uint64_t *lnl_before;    // exclusive max of agg_lnl (init abs_offset)
+    uint32_t dense;
+    uint32_t dense_update;         // 0: records only (redo after a record overflow)
+    uint64_t smask;
+    unsigned long long *counts;
+    unsigned long long *first;
+    Record *recs;
+    unsigned long long *rec_count;
+    uint64_t rec_cap;
+    unsigned int *err;
 };
 
 struct TileArgs {
@@ -106,7 +156,11 @@ struct WindowArgs {
 };
 
 // ---- launchers (kmer_kernels.hip) ------------------------------------------
-hipError_t launch_tile(const TileArgs &a, bool lookback, hipStream_t s);
+hipError_t launch_lines(const TileArgs &a, bool lookback, hipStream_t s);
+hipError_t launch_scan_tiles(const ScanArgs &a, hipStream_t s);
+hipError_t launch_hits(const HitArgs &a, hipStream_t s);
+hipError_t launch_pos_update(StreamPos *pos, const uint64_t *cscan, const uint64_t *agg_cnt, uint32_t n_tiles,
+                             const uint8_t *data, uint64_t len, hipStream_t s);
 hipError_t launch_tile_aggregate(const uint8_t *data, uint64_t len, uint32_t n_tiles, uint64_t *agg_cnt,
                                  uint64_t *agg_lnl, unsigned int *err, hipStream_t s);
 hipError_t launch_windows(const WindowArgs &a, uint32_t grid, hipStream_t s);

@@ -141,6 +141,8 @@ struct TileShared {
     uint64_t line_base;          // global line index of the tile's first byte
     uint64_t lnl_before;         // absolute start of the line containing the tile's first byte
     uint64_t lnl_tile;           // absolute line start after the tile's last '\n' (0 = none)
+    int32_t lastpos;             // tile-relative position of the tile's last real '\n' (-1 = none)
+    uint32_t nh;                 // hit records written by this tile
     uint32_t qn;                 // hit queue fill
     uint32_t more;               // a lane could not queue all its hits this round
     uint32_t q[1024];            // verified hits: (tile position << 1) | strand
@@ -187,33 +189,20 @@ __device__ __forceinline__ uint64_t revcomp_code(uint64_t x, uint32_t k) {
     return k >= 32 ? x : (x >> (64 - 2 * k));
 }
 
-template <bool LOOKBACK, bool FULL4>
-__global__ __launch_bounds__(TPB) void tile_kernel(TileArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t buf[BUFSZ];
-    __shared__ TileShared sh;
-    __shared__ __attribute__((aligned(16))) uint8_t s_pr[2 * KMAX_TILE];
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wid = tid >> 6;
-
-    if (tid == 0) {
-        sh.tile = LOOKBACK ? atomicAdd(a.ticket, 1u) : blockIdx.x;
-        sh.last_thr = -1;
-    }
-    if (tid < 2 * KMAX_TILE) s_pr[tid] = a.PR[tid];
-    __syncthreads();
-    const uint32_t tile = sh.tile;
-    const int64_t g0 = (int64_t)tile * TILE;
-    const uint64_t len = a.len;
-
+// Shared tile prologue: stage tile + halos in LDS, per-thread words, '\n'
+// count, block exclusive scan (sh.tpre), tile's last '\n' (sh.lastpos).
+// Returns the tile's '\n' count (bytes < len only).
+__device__ __forceinline__ uint32_t tile_prologue(const uint8_t *data, uint64_t len, int64_t g0, uint8_t *buf,
+                                                  TileShared &sh, uint32_t (&w)[17], unsigned int *err) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     // ---- stage tile + halos into LDS (16 B per lane, coalesced) ----
     uint4 v[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = load_chunk(a.data, g0 + (int64_t)(tid + TPB * i) * 16, len);
+    for (int i = 0; i < 4; ++i) v[i] = load_chunk(data, g0 + (int64_t)(tid + TPB * i) * 16, len);
     uint4 vh = make_uint4(0, 0, 0, 0);
     const bool halo = tid < NCH_FRONT + NCH_BACK;
-    int hc = tid < NCH_FRONT ? tid : NCH_FRONT + NCH_MAIN + (tid - NCH_FRONT);
-    if (halo) vh = load_chunk(a.data, g0 - FH + (int64_t)hc * 16, len);
+    const int hc = tid < NCH_FRONT ? tid : NCH_FRONT + NCH_MAIN + (tid - NCH_FRONT);
+    if (halo) vh = load_chunk(data, g0 - FH + (int64_t)hc * 16, len);
     uint32_t orall = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -221,43 +210,39 @@ __global__ __launch_bounds__(TPB) void tile_kernel(TileArgs a) {
         *(uint4 *)(buf + FH + (tid + TPB * i) * 16) = v[i];
     }
     if (halo) *(uint4 *)(buf + hc * 16) = vh;
-    if (orall & 0x80808080u) atomicOr(a.err, ERR_NONASCII);
+    if (orall & 0x80808080u) atomicOr(err, ERR_NONASCII);
     __syncthreads();
 
     // ---- per-thread view: bytes [64*tid, 64*tid + 68) ----
-    uint32_t w[17];
     {
         const uint4 *lp = (const uint4 *)(buf + FH + 64 * tid);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            uint4 x = lp[i];
+            const uint4 x = lp[i];
             w[4 * i] = x.x; w[4 * i + 1] = x.y; w[4 * i + 2] = x.z; w[4 * i + 3] = x.w;
         }
         w[16] = *(const uint32_t *)(buf + FH + 64 * tid + 64);
     }
-
     // ---- '\n' count of the bytes this thread owns (only real bytes < len) ----
     uint32_t cnt = 0;
-    {
-        const int64_t gt = g0 + 64 * tid;
-        if (gt + 64 <= (int64_t)len) {
+    const int64_t gt = g0 + 64 * tid;
+    if (gt + 64 <= (int64_t)len) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) cnt += __popc(nl_flags(w[i]));
-        } else {
+        for (int i = 0; i < 16; ++i) cnt += __popc(nl_flags(w[i]));
+    } else {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                int64_t n = (int64_t)len - (gt + 4 * i);
-                uint32_t z = nl_flags(w[i]);
-                if (n <= 0) z = 0; else if (n < 4) z &= (1u << (8 * n)) - 1u;
-                cnt += __popc(z);
-            }
+        for (int i = 0; i < 16; ++i) {
+            const int64_t n = (int64_t)len - (gt + 4 * i);
+            uint32_t z = nl_flags(w[i]);
+            if (n <= 0) z = 0; else if (n < 4) z &= (1u << (8 * n)) - 1u;
+            cnt += __popc(z);
         }
     }
-    // block exclusive scan of cnt
+    // ---- block exclusive scan of cnt ----
     uint32_t incl = cnt;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        uint32_t y = __shfl_up(incl, d);
+        const uint32_t y = __shfl_up(incl, d);
         if (lane >= d) incl += y;
     }
     if (lane == 63) sh.wsum[wid] = incl;
@@ -272,20 +257,47 @@ __global__ __launch_bounds__(TPB) void tile_kernel(TileArgs a) {
     sh.tpre[tid] = woff + incl - cnt;
     if (tid == 0) sh.tpre[TPB] = total;
     if (tid == sh.last_thr) {
+        // last real '\n' of this thread's bytes (word-wise, from the end)
         int lastpos = -1;
-        const int64_t gt = g0 + 64 * tid;
 #pragma unroll 1
-        for (int i = 0; i < 64; ++i)
-            if (gt + i < (int64_t)len && buf[FH + 64 * tid + i] == '\n') lastpos = i;
-        sh.lnl_tile = a.abs_offset + (uint64_t)(gt + lastpos + 1);
+        for (int i = 15; i >= 0 && lastpos < 0; --i) {
+            const int64_t n = (int64_t)len - (gt + 4 * i);
+            uint32_t z = nl_flags(*(const uint32_t *)(buf + FH + 64 * tid + 4 * i));
+            if (n <= 0) z = 0; else if (n < 4) z &= (1u << (8 * n)) - 1u;
+            if (z) lastpos = 64 * tid + 4 * i + ((31 - __clz(z)) >> 3);
+        }
+        sh.lastpos = lastpos;
     }
-    if (sh.last_thr < 0 && tid == 0) sh.lnl_tile = 0;
+    if (sh.last_thr < 0 && tid == 0) sh.lastpos = -1;
     __syncthreads();
+    return total;
+}
 
-    // ---- tile prefix: decoupled look-back (wave 0) or two-pass arrays ----
+// ---------------------------------------------------------------------------
+// General path, step 1: sequence-line descriptors (decoupled look-back over
+// tiles for the line index / line start of each tile).
+// ---------------------------------------------------------------------------
+template <bool LOOKBACK>
+__global__ __launch_bounds__(TPB) void lines_kernel(TileArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t buf[BUFSZ];
+    __shared__ TileShared sh;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    if (tid == 0) {
+        sh.tile = LOOKBACK ? atomicAdd(a.ticket, 1u) : blockIdx.x;
+        sh.last_thr = -1;
+    }
+    __syncthreads();
+    const uint32_t tile = sh.tile;
+    const int64_t g0 = (int64_t)tile * TILE;
+    const uint64_t len = a.len;
+    uint32_t w[17];
+    const uint32_t total = tile_prologue(a.data, len, g0, buf, sh, w, a.err);
+    const uint64_t lnl_tile = sh.lastpos >= 0 ? a.abs_offset + (uint64_t)(g0 + sh.lastpos + 1) : 0;
+
     if (wid == 0) {
         uint64_t lbase, lnlb;
-        const uint64_t lnl_tile = sh.lnl_tile;
         if (LOOKBACK) {
             if (tile == 0) {
                 lbase = a.pos->lines;
@@ -320,37 +332,60 @@ __global__ __launch_bounds__(TPB) void tile_kernel(TileArgs a) {
             sh.lnl_before = lnlb;
         }
     }
-
-    const uint64_t abs0 = a.abs_offset + (uint64_t)g0;   // absolute offset of tile byte 0
-
-    if (a.emit_lines) {
-        // ---- general path: emit sequence-line descriptors for lines starting here ----
-        __syncthreads();
-        const uint64_t lbase = sh.line_base;
+    __syncthreads();
+    const uint64_t lbase = sh.line_base;
 #pragma unroll 1
-        for (int i = 0; i < 64; ++i) {
-            const int q = 64 * tid + i;
-            if ((uint64_t)(g0 + q) >= len) break;
-            if (buf[FH + q - 1] != '\n') continue;
-            const uint32_t c = sh.tpre[tid] + nl_before_in_thread(buf, tid, q);
-            const uint64_t li = lbase + c;
-            if ((li & 3) != 1) continue;
-            // find the end of the line
-            int64_t e = g0 + q;
-            while ((uint64_t)e < len && (e - g0 < TILE + BH ? buf[FH + (e - g0)] : a.data[e]) != '\n') ++e;
-            const uint64_t L = (uint64_t)e - (uint64_t)(g0 + q);
-            if (L > 1 && L >= a.k) {
-                unsigned long long n = atomicAdd(a.line_count, 1ull);
-                if (n < a.line_cap) {
-                    a.lines_out[n].start = (uint64_t)(g0 + q);
-                    a.lines_out[n].len = L;
-                    a.lines_out[n].line_index = li;
-                } else {
-                    atomicOr(a.err, ERR_LINE_OVERFLOW);
-                }
+    for (int i = 0; i < 64; ++i) {
+        const int q = 64 * tid + i;
+        if ((uint64_t)(g0 + q) >= len) break;
+        if (buf[FH + q - 1] != '\n') continue;
+        const uint32_t c = sh.tpre[tid] + nl_before_in_thread(buf, tid, q);
+        const uint64_t li = lbase + c;
+        if ((li & 3) != 1) continue;
+        // find the end of the line
+        int64_t e = g0 + q;
+        while ((uint64_t)e < len && (e - g0 < TILE + BH ? buf[FH + (e - g0)] : a.data[e]) != '\n') ++e;
+        const uint64_t L = (uint64_t)e - (uint64_t)(g0 + q);
+        if (L > 1 && L >= a.k) {
+            const unsigned long long n = atomicAdd(a.line_count, 1ull);
+            if (n < a.line_cap) {
+                a.lines_out[n].start = (uint64_t)(g0 + q);
+                a.lines_out[n].len = L;
+                a.lines_out[n].line_index = li;
+            } else {
+                atomicOr(a.err, ERR_LINE_OVERFLOW);
             }
         }
-        return;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Fast path, step 1: streaming tile scan (no inter-tile dependency).
+// Per tile: '\n' aggregate for the line scan, SWAR prefix scan at every byte
+// on both strands, exact verification, and one 24-byte hit record per
+// verified window with its tile-local line context.  Line index / order are
+// resolved by hit_kernel after a scan over the per-tile aggregates.
+// ---------------------------------------------------------------------------
+template <bool FULL4>
+__global__ __launch_bounds__(TPB) void scan_tile_kernel(ScanArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t buf[BUFSZ];
+    __shared__ TileShared sh;
+    __shared__ __attribute__((aligned(16))) uint8_t s_pr[2 * KMAX_TILE];
+    const int tid = threadIdx.x;
+    const uint32_t tile = blockIdx.x;
+    const int64_t g0 = (int64_t)tile * TILE;
+    const uint64_t len = a.len;
+    if (tid == 0) {
+        sh.last_thr = -1;
+        sh.nh = 0;
+    }
+    if (tid < 2 * KMAX_TILE) s_pr[tid] = a.PR[tid];
+    __syncthreads();
+    uint32_t w[17];
+    const uint32_t total = tile_prologue(a.data, len, g0, buf, sh, w, a.err);
+    if (tid == 0) {
+        a.agg_cnt[tile] = total;
+        a.agg_lnl[tile] = sh.lastpos >= 0 ? a.abs_offset + (uint64_t)(g0 + sh.lastpos + 1) : 0;
     }
 
     // ---- SWAR scan: 4-byte windows at every byte vs P[0:4] and rc(P)[0:4] ----
@@ -372,19 +407,19 @@ __global__ __launch_bounds__(TPB) void tile_kernel(TileArgs a) {
         }
         cand |= (m == 0 ? 1u : 0u) << i;
     }
-    __syncthreads();   // line_base / lnl_before visible
-    if (a.plen > a.k) return;
-    const uint64_t lbase = sh.line_base;
-    const uint64_t lnlb = sh.lnl_before;
     const uint32_t k = a.k, plen = a.plen;
-    const uint64_t smask = (2 * (k - plen) >= 64) ? ~0ull : ((1ull << (2 * (k - plen))) - 1ull);
+    if (plen > k) cand = 0;
     const uint32_t *pw = (const uint32_t *)s_pr;             // P words, then rc(P) words
+    HitRec *tile_hits = a.hits + (uint64_t)tile * HMAX;
 
-    // ---- hits: verify candidates into an LDS queue, then one hit per lane ----
-    // Rounds bound the queue; a lane resumes at its cursor (word bit, sub-position).
-    uint32_t sub = 0;                                        // next (jj*2 + strand) in the current word
+    // ---- verified hits -> LDS queue (bounded rounds) -> hit records ----
+    // Per candidate word: the 8 (position, strand) matches in straight-line
+    // code, the rest of the prefix checked only for set bits, then ONE LDS
+    // atomic reserves queue slots for all of the word's hits.  A word whose
+    // hits do not fit is retried whole in the next round (its reserved slots
+    // are filled with a sentinel so nothing is processed twice).
     while (true) {
-        __syncthreads();                                     // previous round done (queue + `more` read)
+        __syncthreads();                                     // previous round done
         if (tid == 0) { sh.qn = 0; sh.more = 0; }
         __syncthreads();
         while (cand) {
@@ -392,27 +427,45 @@ __global__ __launch_bounds__(TPB) void tile_kernel(TileArgs a) {
             const int q0 = 64 * tid + 4 * i;
             const uint32_t lo = *(const uint32_t *)(buf + FH + q0);
             const uint32_t hi = *(const uint32_t *)(buf + FH + q0 + 4);
-            bool full = false;
-#pragma unroll 1
-            for (; sub < 8; ++sub) {
-                const uint32_t jj = sub >> 1, strand = sub & 1;
+            uint32_t bits = 0;
+#pragma unroll
+            for (uint32_t jj = 0; jj < 4; ++jj) {
                 const uint32_t win = align4(hi, lo, jj);
-                if (((win ^ (strand ? R4 : P4)) & PM) != 0) continue;
-                bool ok = true;
-                const int q = q0 + (int)jj;
-#pragma unroll 1
-                for (uint32_t b = 4; b < plen && ok; b += 4) {
-                    const uint32_t n = plen - b;
-                    const uint32_t mk = n >= 4 ? 0xFFFFFFFFu : ((1u << (8 * n)) - 1u);
-                    ok = ((lds_word(buf, q + (int)b) ^ pw[(strand ? KMAX_TILE / 4 : 0) + b / 4]) & mk) == 0;
-                }
-                if (!ok) continue;
-                const uint32_t slot = atomicAdd(&sh.qn, 1u);
-                if (slot >= QCAP) { full = true; break; }
-                sh.q[slot] = ((uint32_t)q << 1) | strand;
+                bits |= (((win ^ P4) & PM) == 0 ? 1u : 0u) << (2 * jj);
+                bits |= (((win ^ R4) & PM) == 0 ? 1u : 0u) << (2 * jj + 1);
             }
-            if (full) { sh.more = 1; break; }
-            sub = 0;
+            if (plen > 4) {
+                uint32_t check = bits;
+                while (check) {
+                    const uint32_t bit = __ffs(check) - 1;
+                    check &= check - 1;
+                    const uint32_t strand = bit & 1u;
+                    const int q = q0 + (int)(bit >> 1);
+                    bool ok = true;
+#pragma unroll 1
+                    for (uint32_t b = 4; b < plen && ok; b += 4) {
+                        const uint32_t n = plen - b;
+                        const uint32_t mk = n >= 4 ? 0xFFFFFFFFu : ((1u << (8 * n)) - 1u);
+                        ok = ((lds_word(buf, q + (int)b) ^ pw[(strand ? KMAX_TILE / 4 : 0) + b / 4]) & mk) == 0;
+                    }
+                    if (!ok) bits &= ~(1u << bit);
+                }
+            }
+            const uint32_t n = __popc(bits);
+            if (n) {
+                const uint32_t slot = atomicAdd(&sh.qn, n);
+                if (slot + n > QCAP) {
+                    for (uint32_t j = slot; j < QCAP; ++j) sh.q[j] = 0xFFFFFFFFu;
+                    sh.more = 1;
+                    break;                                   // keep this word for the next round
+                }
+                uint32_t o = slot;
+                while (bits) {
+                    const uint32_t bit = __ffs(bits) - 1;
+                    bits &= bits - 1;
+                    sh.q[o++] = ((uint32_t)(q0 + (int)(bit >> 1)) << 1) | (bit & 1u);
+                }
+            }
             cand &= cand - 1;
         }
         __syncthreads();
@@ -420,13 +473,14 @@ __global__ __launch_bounds__(TPB) void tile_kernel(TileArgs a) {
         const uint32_t nq = min(sh.qn, (uint32_t)QCAP);
         for (uint32_t h = tid; h < nq; h += TPB) {
             const uint32_t e = sh.q[h];
-            const int strand = (int)(e & 1u);
+            if (e == 0xFFFFFFFFu) continue;
+            const uint32_t strand = e & 1u;
             const int q = (int)(e >> 1);
             const int s0 = strand ? q + (int)plen - (int)k : q;   // window start, tile-relative
             // window bytes: ACGT check (v_perm against "ACGT"), '\n' check, 2-bit codes
             bool exotic = false, hasnl = false;
             uint64_t code = 0;
-#pragma unroll 1
+#pragma unroll 4
             for (uint32_t b = 0; b < k; b += 4) {
                 const uint32_t x = lds_word(buf, s0 + (int)b);
                 const uint32_t nb = k - b >= 4 ? 4u : k - b;
@@ -440,70 +494,128 @@ __global__ __launch_bounds__(TPB) void tile_kernel(TileArgs a) {
                 code = (code << (2 * nb)) | (packed >> (2 * (4 - nb)));
             }
             if (hasnl) continue;          // crosses a line end (or the end of input)
-            // line context of the window start
-            uint64_t li, lstart;
-            if (s0 <= 0) {
-                li = lbase;
-                lstart = lnlb;
-            } else {
+            // tile-local line context of the window start: '\n' count before s0
+            // and the start of its line if that lies inside this tile
+            uint32_t c_local = 0;
+            int lstart = -1;
+            if (s0 > 0) {
                 const int ts = (s0 - 1) >> 6;
+                const uint4 *lp = (const uint4 *)(buf + FH + 64 * ts);
                 uint32_t cnt = 0;
                 int last = -1;
-                const uint32_t *lw = (const uint32_t *)(buf + FH + 64 * ts);
-#pragma unroll 1
-                for (int i = 0; 64 * ts + 4 * i < s0; ++i) {
-                    uint32_t z = nl_flags(lw[i]);
-                    const int rem = s0 - (64 * ts + 4 * i);
-                    if (rem < 4) z &= (1u << (8 * rem)) - 1u;
-                    cnt += __popc(z);
-                    if (z) last = 64 * ts + 4 * i + ((31 - __clz(z)) >> 3);
+#pragma unroll
+                for (int i4 = 0; i4 < 4; ++i4) {
+                    const uint4 x4 = lp[i4];
+                    const uint32_t xs[4] = {x4.x, x4.y, x4.z, x4.w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int pos = 64 * ts + 16 * i4 + 4 * j;
+                        const int rem = s0 - pos;
+                        uint32_t z = nl_flags(xs[j]);
+                        z = rem <= 0 ? 0u : rem < 4 ? (z & ((1u << (8 * rem)) - 1u)) : z;
+                        cnt += __popc(z);
+                        last = z ? pos + ((31 - __clz(z)) >> 3) : last;
+                    }
                 }
-                const uint32_t c = sh.tpre[ts] + cnt;
-                li = lbase + c;
+                c_local = sh.tpre[ts] + cnt;
                 if (last >= 0) {
-                    lstart = abs0 + (uint64_t)(last + 1);
-                } else if (c == 0) {
-                    lstart = lnlb;
-                } else {
-                    // the c-th '\n' is the last one of the last earlier thread that has any
-                    int lo2 = 0, hi2 = ts - 1;                  // largest t with tpre[t] < c
+                    lstart = last + 1;
+                } else if (c_local > 0) {
+                    // the c_local-th '\n' is the last one of the last earlier thread that has any
+                    int lo2 = 0, hi2 = ts - 1;                  // largest t with tpre[t] < c_local
                     while (lo2 < hi2) {
                         const int mid = (lo2 + hi2 + 1) >> 1;
-                        if (sh.tpre[mid] < c) lo2 = mid; else hi2 = mid - 1;
+                        if (sh.tpre[mid] < c_local) lo2 = mid; else hi2 = mid - 1;
                     }
-                    lstart = abs0 + (uint64_t)(last_newline_in_thread(buf, lo2) + 1);
+                    lstart = last_newline_in_thread(buf, lo2) + 1;
                 }
             }
-            if ((li & 3) != 1) continue;
-            const uint64_t sabs = abs0 + (uint64_t)(int64_t)s0;
-            const uint64_t rel = sabs - lstart;
-            if (k == 1 && rel == 0 && buf[FH + s0 + 1] == '\n') continue;   // line.length > 1
-            if (rel > MAXREL) {
-                atomicOr(a.err, ERR_LINE_TOO_LONG);
-                continue;
-            }
-            const uint64_t order = (li << 24) | ((uint64_t)strand << 23) | (strand ? (uint64_t)(MAXREL - rel) : rel);
-            if (a.dense && !exotic) {
-                if (a.dense_update) {
-                    const uint64_t idx = (strand ? revcomp_code(code, k) : code) & smask;
-                    atomicAdd(a.counts + idx, 1ull);
-                    atomicMin(a.first + idx, (unsigned long long)order);
-                }
+            if (k == 1 && buf[FH + s0 - 1] == '\n' && buf[FH + s0 + 1] == '\n') continue;   // line.length > 1
+            HitRec r;
+            r.code = code;
+            r.tile = tile;
+            r.qm = (uint32_t)q | (strand << 14) | ((exotic ? 1u : 0u) << 15) | ((lstart >= 0 ? 1u : 0u) << 16);
+            r.c_local = c_local;
+            r.lstart = lstart >= 0 ? (uint32_t)lstart : 0u;
+            const uint32_t slot = atomicAdd(&sh.nh, 1u);
+            if (slot < HMAX) {
+                tile_hits[slot] = r;
             } else {
-                const unsigned long long n = atomicAdd(a.rec_count, 1ull);
-                if (n < a.rec_cap) {
-                    Record r;
-                    r.order = order;
-                    r.pos = (uint64_t)(g0 + s0);
-                    r.len = k;
-                    r.strand = (uint32_t)strand;
-                    a.recs[n] = r;
-                } else {
-                    atomicOr(a.err, ERR_REC_OVERFLOW);
-                }
+                const unsigned long long o = atomicAdd(a.ovf_count, 1ull);
+                if (o < a.ovf_cap) a.ovf[o] = r;
+                else atomicOr(a.err, ERR_OVF_OVERFLOW);
             }
         }
         if (!again) break;
+    }
+    __syncthreads();
+    if (tid == 0) a.tile_nhits[tile] = min(sh.nh, (uint32_t)HMAX);
+}
+
+// Resolve one hit: global line index / line start from the per-tile scans,
+// the reference's sequence-line rule, first-occurrence order, then the dense
+// table (count + atomicMin order) or a record for the host merge.
+__device__ __forceinline__ void resolve_hit(const HitArgs &a, const HitRec &r) {
+    const uint32_t t = r.tile;
+    const uint32_t strand = (r.qm >> 14) & 1u;
+    const bool exotic = (r.qm >> 15) & 1u;
+    const bool lvalid = (r.qm >> 16) & 1u;
+    const int q = (int)(r.qm & 0x3FFFu);
+    const int s0 = strand ? q + (int)a.plen - (int)a.k : q;
+    const uint64_t tile_abs = a.abs_offset + (uint64_t)t * TILE;
+    const uint64_t li = a.pos->lines + a.cscan[t] + r.c_local;
+    if ((li & 3) != 1) return;
+    const uint64_t lstart = lvalid ? tile_abs + r.lstart : a.lnl_before[t];
+    const uint64_t sabs = tile_abs + (uint64_t)(int64_t)s0;
+    const uint64_t rel = sabs - lstart;
+    if (rel > MAXREL) {
+        atomicOr(a.err, ERR_LINE_TOO_LONG);
+        return;
+    }
+    const uint64_t order = (li << 24) | ((uint64_t)strand << 23) | (strand ? (uint64_t)(MAXREL - rel) : rel);
+    if (a.dense && !exotic) {
+        if (a.dense_update) {
+            const uint64_t idx = (strand ? revcomp_code(r.code, a.k) : r.code) & a.smask;
+            atomicAdd(a.counts + idx, 1ull);
+            atomicMin(a.first + idx, (unsigned long long)order);
+        }
+    } else {
+        const unsigned long long n = atomicAdd(a.rec_count, 1ull);
+        if (n < a.rec_cap) {
+            Record rec;
+            rec.order = order;
+            rec.pos = (uint64_t)t * TILE + (uint64_t)(int64_t)s0;
+            rec.len = a.k;
+            rec.strand = strand;
+            a.recs[n] = rec;
+        } else {
+            atomicOr(a.err, ERR_REC_OVERFLOW);
+        }
+    }
+}
+
+// one wave per tile: lane i resolves the tile's i-th hit
+__global__ __launch_bounds__(256) void hit_kernel(HitArgs a) {
+    const uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (t >= a.n_tiles || *a.ovf_count > a.ovf_cap) return;   // overflowed scan: the host redoes the chunk
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t n = a.tile_nhits[t];
+    for (uint32_t h = lane; h < n; h += 64) resolve_hit(a, a.hits[(uint64_t)t * HMAX + h]);
+}
+
+__global__ __launch_bounds__(256) void hit_overflow_kernel(HitArgs a) {
+    if (*a.ovf_count > a.ovf_cap) return;
+    const uint64_t n = *a.ovf_count;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        resolve_hit(a, a.ovf[i]);
+}
+
+// advance the running stream position past this chunk
+__global__ void pos_update_kernel(StreamPos *pos, const uint64_t *cscan, const uint64_t *agg_cnt, uint32_t n_tiles,
+                                  const uint8_t *data, uint64_t len) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {   // (a redo after an overflow restores pos first)
+        pos->lines += cscan[n_tiles - 1] + agg_cnt[n_tiles - 1];
+        pos->ends_open = (len > 0 && data[len - 1] != '\n') ? 1 : 0;
     }
 }
 
@@ -735,15 +847,27 @@ __global__ __launch_bounds__(256) void synth_kernel(uint8_t *out, uint64_t seed,
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-hipError_t launch_tile(const TileArgs &a, bool lookback, hipStream_t s) {
-    const bool full4 = a.plen >= 4;
-    if (lookback) {
-        if (full4) hipLaunchKernelGGL((tile_kernel<true, true>), dim3(a.n_tiles), dim3(TPB), 0, s, a);
-        else hipLaunchKernelGGL((tile_kernel<true, false>), dim3(a.n_tiles), dim3(TPB), 0, s, a);
-    } else {
-        if (full4) hipLaunchKernelGGL((tile_kernel<false, true>), dim3(a.n_tiles), dim3(TPB), 0, s, a);
-        else hipLaunchKernelGGL((tile_kernel<false, false>), dim3(a.n_tiles), dim3(TPB), 0, s, a);
-    }
+hipError_t launch_lines(const TileArgs &a, bool lookback, hipStream_t s) {
+    if (lookback) hipLaunchKernelGGL((lines_kernel<true>), dim3(a.n_tiles), dim3(TPB), 0, s, a);
+    else hipLaunchKernelGGL((lines_kernel<false>), dim3(a.n_tiles), dim3(TPB), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_tiles(const ScanArgs &a, hipStream_t s) {
+    if (a.plen >= 4) hipLaunchKernelGGL((scan_tile_kernel<true>), dim3(a.n_tiles), dim3(TPB), 0, s, a);
+    else hipLaunchKernelGGL((scan_tile_kernel<false>), dim3(a.n_tiles), dim3(TPB), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_hits(const HitArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(hit_kernel, dim3((a.n_tiles + 3) / 4), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(hit_overflow_kernel, dim3(64), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_pos_update(StreamPos *pos, const uint64_t *cscan, const uint64_t *agg_cnt, uint32_t n_tiles,
+                             const uint8_t *data, uint64_t len, hipStream_t s) {
+    hipLaunchKernelGGL(pos_update_kernel, dim3(1), dim3(64), 0, s, pos, cscan, agg_cnt, n_tiles, data, len);
     return hipGetLastError();
 }
 

@@ -25,12 +25,16 @@ torch.cuda.synchronize()
 out["torch_sum_GBs"] = n * 317 * 10 / (time.perf_counter() - t0) / 1e9
 for name, flags in (("lookback", 0), ("two_pass", _native.FLAG_TWO_PASS)):
     ctr = Counter(k=16, prefix=b"ATGAC", flags=flags)
-    ts = []
+    ts, fs, fin = [], [], []
     for i in range(6):
         ctr.reset()
         ctr.feed_device(buf.data_ptr(), n * 317)
-        ts.append(ctr.last_timing()[0])
+        t = ctr.last_timing()
         r = ctr.finish(want_result=(i == 5))
-    out[name] = {"tile_ms": ts[1:], "distinct": len(r), "GBs": n * 317 / (min(ts[1:]) * 1e-3) / 1e9}
+        ts.append(t[0])
+        fs.append(t[1])
+        fin.append(ctr.last_timing()[2])
+    out[name] = {"scan_ms": ts[1:], "feed_ms": fs[1:], "finish_ms": fin[1:], "distinct": len(r),
+                 "scan_GBs": n * 317 / (min(ts[1:]) * 1e-3) / 1e9}
     ctr.close()
 print(json.dumps(out))
