@@ -302,6 +302,7 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
     a.ovf_count = c->d_ovf_count;
     a.ovf_cap = c->ovf_cap;
     a.err = c->d_err;
+    a.ablate = (c->p.flags >> 8) & 0xFFu;   // KMER_FLAG_ABLATE_* (experiments only)
 
     HitArgs h;
     memset(&h, 0, sizeof(h));

@@ -86,6 +86,7 @@ struct ScanArgs {
     unsigned long long *ovf_count;
     uint64_t ovf_cap;
     unsigned int *err;
+    uint32_t ablate;               // experiments only: bit0 = drop all candidates
 };
 
 struct HitArgs {

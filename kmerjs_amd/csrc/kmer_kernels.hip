@@ -114,16 +114,15 @@ constexpr int NCH_FRONT = FH / 16;           // 4
 constexpr int NCH_BACK = BH / 16;            // 5
 constexpr int BUFSZ = FH + TILE + BH;
 
-__device__ __forceinline__ uint4 load_chunk(const uint8_t *data, int64_t g, uint64_t len) {
-    if (g >= 0 && (uint64_t)g + 16 <= len) return *(const uint4 *)(data + g);
+// bytes outside [0, len) read as '\n' (a line boundary that is never a window byte)
+__device__ __noinline__ uint4 load_chunk_edge(const uint8_t *data, int64_t g, uint64_t len) {
     uint32_t w[4];
-#pragma unroll
+#pragma unroll 1
     for (int i = 0; i < 4; ++i) {
         uint32_t x = 0;
-#pragma unroll
         for (int b = 0; b < 4; ++b) {
-            int64_t p = g + i * 4 + b;
-            uint32_t c = (p >= 0 && (uint64_t)p < len) ? data[p] : (uint32_t)'\n';
+            const int64_t p = g + i * 4 + b;
+            const uint32_t c = (p >= 0 && (uint64_t)p < len) ? data[p] : (uint32_t)'\n';
             x |= c << (8 * b);
         }
         w[i] = x;
@@ -131,7 +130,11 @@ __device__ __forceinline__ uint4 load_chunk(const uint8_t *data, int64_t g, uint
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-constexpr int QCAP = 1024;
+__device__ __forceinline__ uint4 load_chunk(const uint8_t *data, int64_t g, uint64_t len) {
+    if (g >= 0 && (uint64_t)g + 16 <= len) return *(const uint4 *)(data + g);
+    return load_chunk_edge(data, g, len);
+}
+
 
 struct TileShared {
     uint32_t tpre[TPB + 1];      // exclusive '\n' count per thread inside the tile; [TPB] = total
@@ -366,191 +369,288 @@ __global__ __launch_bounds__(TPB) void lines_kernel(TileArgs a) {
 // verified window with its tile-local line context.  Line index / order are
 // resolved by hit_kernel after a scan over the per-tile aggregates.
 // ---------------------------------------------------------------------------
+constexpr int QCAP = 256;
+
+struct ScanShared {
+    uint16_t cpre[NCH_MAIN];     // exclusive '\n' count per 16-byte chunk inside the tile
+    uint32_t wsum[TPB / 64][4];  // per-wave totals of the four packed chunk columns
+    int32_t last_chunk;          // highest chunk holding a real '\n' (-1 = none)
+    int32_t lastpos;             // tile-relative position of the tile's last real '\n'
+    uint32_t nh;                 // hit records written by this tile
+    uint32_t qn;                 // verified-hit queue fill
+    uint32_t q[QCAP];            // verified hits: (tile position << 1) | strand
+};
+
+// last '\n' (tile-relative) inside 16-byte chunk c at a position < limit, -1 if none
+__device__ __forceinline__ int last_newline_in_chunk(const uint8_t *buf, int c, int limit = 1 << 30) {
+    const uint4 x = *(const uint4 *)(buf + FH + 16 * c);
+    const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
+    int last = -1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int pos = 16 * c + 4 * j;
+        const int rem = limit - pos;
+        uint32_t z = nl_flags(xs[j]);
+        z = rem <= 0 ? 0u : rem < 4 ? (z & ((1u << (8 * rem)) - 1u)) : z;
+        last = z ? pos + ((31 - __clz(z)) >> 3) : last;
+    }
+    return last;
+}
+
+// One verified prefix hit (queue entry (q << 1) | strand): window analysis,
+// tile-local line context, hit record.
+__device__ __forceinline__ void emit_hit(const ScanArgs &a, const uint8_t *buf, ScanShared &sh, uint32_t tile,
+                                      uint32_t e) {
+    const uint32_t k = a.k, plen = a.plen;
+    const uint32_t strand = e & 1u;
+    const int q = (int)(e >> 1);
+    const int s0 = strand ? q + (int)plen - (int)k : q;   // window start, tile-relative
+    // window bytes: ACGT check (v_perm against "ACGT"), '\n' check, 2-bit codes
+    bool exotic = false, hasnl = false;
+    uint64_t code = 0;
+#pragma unroll 4
+    for (uint32_t b = 0; b < k; b += 4) {
+        const uint32_t x = lds_word(buf, s0 + (int)b);
+        const uint32_t nb = k - b >= 4 ? 4u : k - b;
+        const uint32_t mk = nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
+        const uint32_t c = ((x >> 1) ^ (x >> 2)) & 0x03030303u;
+        const uint32_t expect = __builtin_amdgcn_perm(0u, 0x54474341u, c);   // "ACGT"[c] per byte
+        exotic |= ((expect ^ x) & mk) != 0;
+        hasnl |= (nl_flags(x) & mk) != 0;
+        const uint32_t pk = ((c & 3u) << 6) | (((c >> 8) & 3u) << 4) | (((c >> 16) & 3u) << 2) |
+                            ((c >> 24) & 3u);                // first byte most significant
+        code = (code << (2 * nb)) | (pk >> (2 * (4 - nb)));
+    }
+    if (hasnl) return;            // crosses a line end (or the end of input)
+    if (k == 1 && buf[FH + s0 - 1] == '\n' && buf[FH + s0 + 1] == '\n') return;   // line.length > 1
+    // tile-local line context of the window start: '\n' count before s0 and
+    // the start of its line if that lies inside this tile
+    uint32_t c_local = 0;
+    int lstart = -1;
+    if (s0 > 0) {
+        const int cs = (s0 - 1) >> 4;               // chunk holding byte s0-1
+        const uint4 x4 = *(const uint4 *)(buf + FH + 16 * cs);
+        const uint32_t xs[4] = {x4.x, x4.y, x4.z, x4.w};
+        uint32_t cnt = 0;
+        int last = -1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int pos = 16 * cs + 4 * j;
+            const int rem = s0 - pos;
+            uint32_t z = nl_flags(xs[j]);
+            z = rem <= 0 ? 0u : rem < 4 ? (z & ((1u << (8 * rem)) - 1u)) : z;
+            cnt += __popc(z);
+            last = z ? pos + ((31 - __clz(z)) >> 3) : last;
+        }
+        c_local = sh.cpre[cs] + cnt;
+        if (last >= 0) {
+            lstart = last + 1;
+        } else if (c_local > 0) {
+            // the c_local-th '\n' is the last one of the last earlier chunk that has any
+            int lo2 = 0, hi2 = cs - 1;                  // largest chunk with cpre < c_local
+            while (lo2 < hi2) {
+                const int mid = (lo2 + hi2 + 1) >> 1;
+                if (sh.cpre[mid] < c_local) lo2 = mid; else hi2 = mid - 1;
+            }
+            lstart = last_newline_in_chunk(buf, lo2) + 1;
+        }
+    }
+    HitRec r;
+    r.code = code;
+    r.tile = tile;
+    r.qm = (uint32_t)q | (strand << 14) | ((exotic ? 1u : 0u) << 15) | ((lstart >= 0 ? 1u : 0u) << 16);
+    r.c_local = c_local;
+    r.lstart = lstart >= 0 ? (uint32_t)lstart : 0u;
+    const uint32_t slot = atomicAdd(&sh.nh, 1u);
+    if (slot < HMAX) {
+        a.hits[(uint64_t)tile * HMAX + slot] = r;
+    } else {
+        const unsigned long long o = atomicAdd(a.ovf_count, 1ull);
+        if (o < a.ovf_cap) a.ovf[o] = r;
+        else atomicOr(a.err, ERR_OVF_OVERFLOW);
+    }
+}
+
+// Fast path, step 1 — streaming tile scan, coalesced layout.  Lane t of the
+// workgroup owns the 16-byte chunks c = t + 256*i (i < 4) of the tile, exactly
+// as it loaded them (one 1 KiB coalesced load per wave-instruction); the three
+// look-ahead bytes of a chunk come from the next lane (shfl) or, at wave
+// edges, from the LDS copy.  Per chunk: '\n' count (SWAR), and the 4-byte
+// window at each of its 16 positions compared to P[0:4] and rc(P)[0:4] with
+// v_cmp (the compiler ORs the lane masks on the scalar unit).  A packed
+// 4 x 16-bit block scan gives the exclusive '\n' count of every chunk.
 template <bool FULL4>
 __global__ __launch_bounds__(TPB) void scan_tile_kernel(ScanArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t buf[BUFSZ];
-    __shared__ TileShared sh;
+    __shared__ ScanShared sh;
     __shared__ __attribute__((aligned(16))) uint8_t s_pr[2 * KMAX_TILE];
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint64_t len = a.len;
+    const bool halo = tid < NCH_FRONT + NCH_BACK;
+    const int hc = tid < NCH_FRONT ? tid : NCH_FRONT + NCH_MAIN + (tid - NCH_FRONT);
+    if (tid < 2 * KMAX_TILE) s_pr[tid] = a.PR[tid];
     const uint32_t tile = blockIdx.x;
     const int64_t g0 = (int64_t)tile * TILE;
-    const uint64_t len = a.len;
     if (tid == 0) {
-        sh.last_thr = -1;
+        sh.last_chunk = -1;
         sh.nh = 0;
     }
-    if (tid < 2 * KMAX_TILE) s_pr[tid] = a.PR[tid];
+    {
+        uint4 v[4];
+        uint4 vh = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = load_chunk(a.data, g0 + (int64_t)(tid + TPB * i) * 16, len);
+        if (halo) vh = load_chunk(a.data, g0 - FH + (int64_t)hc * 16, len);
+        uint32_t orall = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            orall |= v[i].x | v[i].y | v[i].z | v[i].w;
+            *(uint4 *)(buf + FH + (tid + TPB * i) * 16) = v[i];
+        }
+        if (halo) *(uint4 *)(buf + hc * 16) = vh;
+        if (orall & 0x80808080u) atomicOr(a.err, ERR_NONASCII);
+    }
     __syncthreads();
-    uint32_t w[17];
-    const uint32_t total = tile_prologue(a.data, len, g0, buf, sh, w, a.err);
-    if (tid == 0) {
-        a.agg_cnt[tile] = total;
-        a.agg_lnl[tile] = sh.lastpos >= 0 ? a.abs_offset + (uint64_t)(g0 + sh.lastpos + 1) : 0;
+
+    // ---- per chunk (from LDS, conflict-free 16-B rows): '\n' count and SWAR candidates ----
+    const uint32_t P4 = a.p4, R4 = a.r4, PM = a.pmask;
+    uint32_t cand = 0;           // bit 4*i + j: word j of chunk i has a 4-byte match
+    uint64_t packed = 0;         // 16-bit '\n' count of chunk i in bits [16i, 16i+16)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int c = tid + TPB * i;
+        const uint4 xv = *(const uint4 *)(buf + FH + 16 * c);
+        const uint32_t x[5] = {xv.x, xv.y, xv.z, xv.w, *(const uint32_t *)(buf + FH + 16 * c + 16)};
+        const int64_t gc = g0 + (int64_t)c * 16;
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint32_t z = nl_flags(x[j]);
+            if (gc + 16 > (int64_t)len) {   // last tile: only bytes < len are lines
+                const int64_t n = (int64_t)len - (gc + 4 * j);
+                z = n <= 0 ? 0u : n < 4 ? (z & ((1u << (8 * n)) - 1u)) : z;
+            }
+            cnt += __popc(z);
+            if (a.ablate & 2u) continue;
+            const uint32_t x0 = x[j];
+            const uint32_t x1 = align4(x[j + 1], x[j], 1);
+            const uint32_t x2 = align4(x[j + 1], x[j], 2);
+            const uint32_t x3 = align4(x[j + 1], x[j], 3);
+            bool hit;
+            if (FULL4) {
+                hit = (x0 == P4) | (x1 == P4) | (x2 == P4) | (x3 == P4) |
+                      (x0 == R4) | (x1 == R4) | (x2 == R4) | (x3 == R4);
+            } else {
+                hit = (((x0 ^ P4) & PM) == 0) | (((x1 ^ P4) & PM) == 0) | (((x2 ^ P4) & PM) == 0) |
+                      (((x3 ^ P4) & PM) == 0) | (((x0 ^ R4) & PM) == 0) | (((x1 ^ R4) & PM) == 0) |
+                      (((x2 ^ R4) & PM) == 0) | (((x3 ^ R4) & PM) == 0);
+            }
+            cand |= hit ? (1u << (4 * i + j)) : 0u;
+        }
+        packed |= (uint64_t)cnt << (16 * i);
+        if (cnt) atomicMax(&sh.last_chunk, c);
     }
 
-    // ---- SWAR scan: 4-byte windows at every byte vs P[0:4] and rc(P)[0:4] ----
-    const uint32_t P4 = a.p4, R4 = a.r4, PM = a.pmask;
-    uint32_t cand = 0;
+    // ---- block scan of the 4 packed chunk columns ----
+    uint64_t incl = packed;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const uint32_t x0 = w[i];
-        const uint32_t x1 = align4(w[i + 1], w[i], 1);
-        const uint32_t x2 = align4(w[i + 1], w[i], 2);
-        const uint32_t x3 = align4(w[i + 1], w[i], 3);
-        uint32_t m;
-        if (FULL4) {
-            m = min(min(min(x0 ^ P4, x1 ^ P4), min(x2 ^ P4, x3 ^ P4)),
-                    min(min(x0 ^ R4, x1 ^ R4), min(x2 ^ R4, x3 ^ R4)));
-        } else {
-            m = min(min(min((x0 ^ P4) & PM, (x1 ^ P4) & PM), min((x2 ^ P4) & PM, (x3 ^ P4) & PM)),
-                    min(min((x0 ^ R4) & PM, (x1 ^ R4) & PM), min((x2 ^ R4) & PM, (x3 ^ R4) & PM)));
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(incl, d);
+        if (lane >= d) incl += y;
+    }
+    if (lane == 63) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sh.wsum[wid][i] = (uint32_t)(incl >> (16 * i)) & 0xFFFFu;
+    }
+    __syncthreads();
+    {
+        uint32_t col_total[4], col_off[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            col_total[i] = 0;
+            col_off[i] = 0;
+#pragma unroll
+            for (int ww = 0; ww < TPB / 64; ++ww) {
+                col_total[i] += sh.wsum[ww][i];
+                col_off[i] += ww < wid ? sh.wsum[ww][i] : 0;
+            }
         }
-        cand |= (m == 0 ? 1u : 0u) << i;
+        const uint64_t excl = incl - packed;
+        uint32_t base = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            sh.cpre[tid + TPB * i] = (uint16_t)(base + col_off[i] + ((excl >> (16 * i)) & 0xFFFFu));
+            base += col_total[i];
+        }
+        if (tid == 0) a.agg_cnt[tile] = base;
+    }
+    if (tid == 0) {
+        const int lc = sh.last_chunk;
+        // (the last tile's sentinel bytes past len are not lines)
+        const int64_t lim = (int64_t)len - g0;
+        const int lp = lc >= 0 ? last_newline_in_chunk(buf, lc, lim < TILE ? (int)lim : TILE) : -1;
+        sh.lastpos = lp;
+        a.agg_lnl[tile] = lp >= 0 ? a.abs_offset + (uint64_t)(g0 + lp + 1) : 0;
     }
     const uint32_t k = a.k, plen = a.plen;
-    if (plen > k) cand = 0;
+    if (plen > k || (a.ablate & 1u)) cand = 0;
     const uint32_t *pw = (const uint32_t *)s_pr;             // P words, then rc(P) words
-    HitRec *tile_hits = a.hits + (uint64_t)tile * HMAX;
 
-    // ---- verified hits -> LDS queue (bounded rounds) -> hit records ----
-    // Per candidate word: the 8 (position, strand) matches in straight-line
-    // code, the rest of the prefix checked only for set bits, then ONE LDS
-    // atomic reserves queue slots for all of the word's hits.  A word whose
-    // hits do not fit is retried whole in the next round (its reserved slots
-    // are filled with a sentinel so nothing is processed twice).
-    while (true) {
-        __syncthreads();                                     // previous round done
-        if (tid == 0) { sh.qn = 0; sh.more = 0; }
-        __syncthreads();
-        while (cand) {
-            const int i = __ffs(cand) - 1;
-            const int q0 = 64 * tid + 4 * i;
-            const uint32_t lo = *(const uint32_t *)(buf + FH + q0);
-            const uint32_t hi = *(const uint32_t *)(buf + FH + q0 + 4);
-            uint32_t bits = 0;
+    // ---- candidates -> verified hits (each lane its own words, straight-line)
+    //      -> LDS queue -> hit records (one hit per lane: the rare, branchy work
+    //      runs once per tile in as few waves as possible) ----
+    if (tid == 0) sh.qn = 0;
+    __syncthreads();             // cpre / qn visible
+    while (cand) {
+        const int bitc = __ffs(cand) - 1;
+        cand &= cand - 1;
+        const int q0 = 16 * (tid + TPB * (bitc >> 2)) + 4 * (bitc & 3);
+        const uint32_t lo = *(const uint32_t *)(buf + FH + q0);
+        const uint32_t hi = *(const uint32_t *)(buf + FH + q0 + 4);
+        uint32_t bits = 0;
 #pragma unroll
-            for (uint32_t jj = 0; jj < 4; ++jj) {
-                const uint32_t win = align4(hi, lo, jj);
-                bits |= (((win ^ P4) & PM) == 0 ? 1u : 0u) << (2 * jj);
-                bits |= (((win ^ R4) & PM) == 0 ? 1u : 0u) << (2 * jj + 1);
-            }
-            if (plen > 4) {
-                uint32_t check = bits;
-                while (check) {
-                    const uint32_t bit = __ffs(check) - 1;
-                    check &= check - 1;
-                    const uint32_t strand = bit & 1u;
-                    const int q = q0 + (int)(bit >> 1);
-                    bool ok = true;
+        for (uint32_t jj = 0; jj < 4; ++jj) {
+            const uint32_t win = align4(hi, lo, jj);
+            bits |= (((win ^ P4) & PM) == 0 ? 1u : 0u) << (2 * jj);
+            bits |= (((win ^ R4) & PM) == 0 ? 1u : 0u) << (2 * jj + 1);
+        }
+        if (plen > 4) {
+            uint32_t check = bits;
+            while (check) {
+                const uint32_t bit = __ffs(check) - 1;
+                check &= check - 1;
+                const uint32_t strand = bit & 1u;
+                const int q = q0 + (int)(bit >> 1);
+                bool ok = true;
 #pragma unroll 1
-                    for (uint32_t b = 4; b < plen && ok; b += 4) {
-                        const uint32_t n = plen - b;
-                        const uint32_t mk = n >= 4 ? 0xFFFFFFFFu : ((1u << (8 * n)) - 1u);
-                        ok = ((lds_word(buf, q + (int)b) ^ pw[(strand ? KMAX_TILE / 4 : 0) + b / 4]) & mk) == 0;
-                    }
-                    if (!ok) bits &= ~(1u << bit);
+                for (uint32_t b = 4; b < plen && ok; b += 4) {
+                    const uint32_t n = plen - b;
+                    const uint32_t mk = n >= 4 ? 0xFFFFFFFFu : ((1u << (8 * n)) - 1u);
+                    ok = ((lds_word(buf, q + (int)b) ^ pw[(strand ? KMAX_TILE / 4 : 0) + b / 4]) & mk) == 0;
                 }
-            }
-            const uint32_t n = __popc(bits);
-            if (n) {
-                const uint32_t slot = atomicAdd(&sh.qn, n);
-                if (slot + n > QCAP) {
-                    for (uint32_t j = slot; j < QCAP; ++j) sh.q[j] = 0xFFFFFFFFu;
-                    sh.more = 1;
-                    break;                                   // keep this word for the next round
-                }
-                uint32_t o = slot;
-                while (bits) {
-                    const uint32_t bit = __ffs(bits) - 1;
-                    bits &= bits - 1;
-                    sh.q[o++] = ((uint32_t)(q0 + (int)(bit >> 1)) << 1) | (bit & 1u);
-                }
-            }
-            cand &= cand - 1;
-        }
-        __syncthreads();
-        const bool again = sh.more != 0;
-        const uint32_t nq = min(sh.qn, (uint32_t)QCAP);
-        for (uint32_t h = tid; h < nq; h += TPB) {
-            const uint32_t e = sh.q[h];
-            if (e == 0xFFFFFFFFu) continue;
-            const uint32_t strand = e & 1u;
-            const int q = (int)(e >> 1);
-            const int s0 = strand ? q + (int)plen - (int)k : q;   // window start, tile-relative
-            // window bytes: ACGT check (v_perm against "ACGT"), '\n' check, 2-bit codes
-            bool exotic = false, hasnl = false;
-            uint64_t code = 0;
-#pragma unroll 4
-            for (uint32_t b = 0; b < k; b += 4) {
-                const uint32_t x = lds_word(buf, s0 + (int)b);
-                const uint32_t nb = k - b >= 4 ? 4u : k - b;
-                const uint32_t mk = nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
-                const uint32_t c = ((x >> 1) ^ (x >> 2)) & 0x03030303u;
-                const uint32_t expect = __builtin_amdgcn_perm(0u, 0x54474341u, c);   // "ACGT"[c] per byte
-                exotic |= ((expect ^ x) & mk) != 0;
-                hasnl |= (nl_flags(x) & mk) != 0;
-                const uint32_t packed = ((c & 3u) << 6) | (((c >> 8) & 3u) << 4) | (((c >> 16) & 3u) << 2) |
-                                        ((c >> 24) & 3u);            // first byte most significant
-                code = (code << (2 * nb)) | (packed >> (2 * (4 - nb)));
-            }
-            if (hasnl) continue;          // crosses a line end (or the end of input)
-            // tile-local line context of the window start: '\n' count before s0
-            // and the start of its line if that lies inside this tile
-            uint32_t c_local = 0;
-            int lstart = -1;
-            if (s0 > 0) {
-                const int ts = (s0 - 1) >> 6;
-                const uint4 *lp = (const uint4 *)(buf + FH + 64 * ts);
-                uint32_t cnt = 0;
-                int last = -1;
-#pragma unroll
-                for (int i4 = 0; i4 < 4; ++i4) {
-                    const uint4 x4 = lp[i4];
-                    const uint32_t xs[4] = {x4.x, x4.y, x4.z, x4.w};
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int pos = 64 * ts + 16 * i4 + 4 * j;
-                        const int rem = s0 - pos;
-                        uint32_t z = nl_flags(xs[j]);
-                        z = rem <= 0 ? 0u : rem < 4 ? (z & ((1u << (8 * rem)) - 1u)) : z;
-                        cnt += __popc(z);
-                        last = z ? pos + ((31 - __clz(z)) >> 3) : last;
-                    }
-                }
-                c_local = sh.tpre[ts] + cnt;
-                if (last >= 0) {
-                    lstart = last + 1;
-                } else if (c_local > 0) {
-                    // the c_local-th '\n' is the last one of the last earlier thread that has any
-                    int lo2 = 0, hi2 = ts - 1;                  // largest t with tpre[t] < c_local
-                    while (lo2 < hi2) {
-                        const int mid = (lo2 + hi2 + 1) >> 1;
-                        if (sh.tpre[mid] < c_local) lo2 = mid; else hi2 = mid - 1;
-                    }
-                    lstart = last_newline_in_thread(buf, lo2) + 1;
-                }
-            }
-            if (k == 1 && buf[FH + s0 - 1] == '\n' && buf[FH + s0 + 1] == '\n') continue;   // line.length > 1
-            HitRec r;
-            r.code = code;
-            r.tile = tile;
-            r.qm = (uint32_t)q | (strand << 14) | ((exotic ? 1u : 0u) << 15) | ((lstart >= 0 ? 1u : 0u) << 16);
-            r.c_local = c_local;
-            r.lstart = lstart >= 0 ? (uint32_t)lstart : 0u;
-            const uint32_t slot = atomicAdd(&sh.nh, 1u);
-            if (slot < HMAX) {
-                tile_hits[slot] = r;
-            } else {
-                const unsigned long long o = atomicAdd(a.ovf_count, 1ull);
-                if (o < a.ovf_cap) a.ovf[o] = r;
-                else atomicOr(a.err, ERR_OVF_OVERFLOW);
+                if (!ok) bits &= ~(1u << bit);
             }
         }
-        if (!again) break;
+        while (bits) {
+            const uint32_t bit = __ffs(bits) - 1;
+            bits &= bits - 1;
+            const uint32_t e = ((uint32_t)(q0 + (int)(bit >> 1)) << 1) | (bit & 1u);
+            const uint32_t slot = atomicAdd(&sh.qn, 1u);
+            if (slot < QCAP) sh.q[slot] = e;
+            else emit_hit(a, buf, sh, tile, e);      // queue full (short prefixes): process in place
+        }
     }
     __syncthreads();
-    if (tid == 0) a.tile_nhits[tile] = min(sh.nh, (uint32_t)HMAX);
+    const uint32_t nq = min(sh.qn, (uint32_t)QCAP);
+    for (uint32_t h = tid; h < nq; h += TPB) emit_hit(a, buf, sh, tile, sh.q[h]);
+    if (nq > 64 || sh.qn > QCAP) {
+        __syncthreads();         // uniform: every wave may have written records
+        if (tid == 0) a.tile_nhits[tile] = min(sh.nh, (uint32_t)HMAX);
+    } else if (tid == 0) {
+        a.tile_nhits[tile] = min(sh.nh, (uint32_t)HMAX);   // wave 0 wrote them all
+    }
 }
+
 
 // Resolve one hit: global line index / line start from the per-tile scans,
 // the reference's sequence-line rule, first-occurrence order, then the dense

@@ -23,7 +23,8 @@ for _ in range(10):
     v.sum()
 torch.cuda.synchronize()
 out["torch_sum_GBs"] = n * 317 * 10 / (time.perf_counter() - t0) / 1e9
-for name, flags in (("lookback", 0), ("two_pass", _native.FLAG_TWO_PASS)):
+modes = (("full", 0), ("no_hits", 1 << 8), ("no_swar", (1 << 8) | (1 << 9)))
+for name, flags in modes:
     ctr = Counter(k=16, prefix=b"ATGAC", flags=flags)
     ts, fs, fin = [], [], []
     for i in range(6):
