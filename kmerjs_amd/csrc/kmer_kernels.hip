@@ -34,6 +34,18 @@ __device__ __forceinline__ uint32_t align4(uint32_t hi, uint32_t lo, uint32_t se
     return __builtin_amdgcn_alignbyte(hi, lo, sel);
 }
 
+// Inclusive wave64 prefix sum with DPP (row_shr 1/2/4/8 inside rows of 16,
+// then row_bcast 15 / 31 across rows): no LDS round trips on the critical path.
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
+}
+
 // per-byte 0x80 flag for bytes equal to '\n'; exact for ASCII bytes (< 0x80)
 __device__ __forceinline__ uint32_t nl_flags(uint32_t x) {
     uint32_t t = x ^ 0x0A0A0A0Au;
@@ -373,6 +385,7 @@ constexpr int QCAP = 256;
 
 struct ScanShared {
     uint16_t cpre[NCH_MAIN];     // exclusive '\n' count per 16-byte chunk inside the tile
+    uint32_t nlmap[NCH_MAIN / 32];   // bit c: chunk c holds a real '\n' 
     uint32_t wsum[TPB / 64][4];  // per-wave totals of the four packed chunk columns
     int32_t last_chunk;          // highest chunk holding a real '\n' (-1 = none)
     int32_t lastpos;             // tile-relative position of the tile's last real '\n'
@@ -446,13 +459,12 @@ __device__ __forceinline__ void emit_hit(const ScanArgs &a, const uint8_t *buf, 
         if (last >= 0) {
             lstart = last + 1;
         } else if (c_local > 0) {
-            // the c_local-th '\n' is the last one of the last earlier chunk that has any
-            int lo2 = 0, hi2 = cs - 1;                  // largest chunk with cpre < c_local
-            while (lo2 < hi2) {
-                const int mid = (lo2 + hi2 + 1) >> 1;
-                if (sh.cpre[mid] < c_local) lo2 = mid; else hi2 = mid - 1;
-            }
-            lstart = last_newline_in_chunk(buf, lo2) + 1;
+            // the line started in the last earlier chunk that holds a '\n' (chunk bitmap)
+            const int cc = cs - 1;
+            int wi = cc >> 5;
+            uint32_t m = sh.nlmap[wi] & (0xFFFFFFFFu >> (31 - (cc & 31)));
+            while (m == 0) m = sh.nlmap[--wi];
+            lstart = last_newline_in_chunk(buf, 32 * wi + 31 - __clz(m)) + 1;
         }
     }
     HitRec r;
@@ -549,15 +561,16 @@ __global__ __launch_bounds__(TPB) void scan_tile_kernel(ScanArgs a) {
         }
         packed |= (uint64_t)cnt << (16 * i);
         if (cnt) atomicMax(&sh.last_chunk, c);
+        const unsigned long long m = __ballot(cnt != 0);
+        if (lane == 0) {
+            sh.nlmap[(c - lane) >> 5] = (uint32_t)m;
+            sh.nlmap[((c - lane) >> 5) + 1] = (uint32_t)(m >> 32);
+        }
     }
 
-    // ---- block scan of the 4 packed chunk columns ----
-    uint64_t incl = packed;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t y = __shfl_up(incl, d);
-        if (lane >= d) incl += y;
-    }
+    // ---- block scan of the 4 packed chunk columns (16-bit fields never carry) ----
+    const uint64_t incl = (uint64_t)wave_incl_sum((uint32_t)packed) |
+                          ((uint64_t)wave_incl_sum((uint32_t)(packed >> 32)) << 32);
     if (lane == 63) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) sh.wsum[wid][i] = (uint32_t)(incl >> (16 * i)) & 0xFFFFu;
