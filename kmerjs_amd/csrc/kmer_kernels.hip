@@ -500,19 +500,29 @@ __global__ __launch_bounds__(TPB) void scan_tile_kernel(ScanArgs a) {
     const uint64_t len = a.len;
     const bool halo = tid < NCH_FRONT + NCH_BACK;
     const int hc = tid < NCH_FRONT ? tid : NCH_FRONT + NCH_MAIN + (tid - NCH_FRONT);
-    if (tid < 2 * KMAX_TILE) s_pr[tid] = a.PR[tid];
     const uint32_t tile = blockIdx.x;
     const int64_t g0 = (int64_t)tile * TILE;
-    if (tid == 0) {
-        sh.last_chunk = -1;
-        sh.nh = 0;
-    }
     {
+        // every tile but the first / last has its halos inside [0, len): plain
+        // 16-B loads with no per-chunk bounds logic, all issued back to back
         uint4 v[4];
         uint4 vh = make_uint4(0, 0, 0, 0);
+        if (g0 - FH >= 0 && (uint64_t)(g0 + TILE + BH) <= len) {
+            const uint8_t *src = a.data + g0 + 16 * tid;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = load_chunk(a.data, g0 + (int64_t)(tid + TPB * i) * 16, len);
-        if (halo) vh = load_chunk(a.data, g0 - FH + (int64_t)hc * 16, len);
+            for (int i = 0; i < 4; ++i) v[i] = *(const uint4 *)(src + 16 * TPB * i);
+            // every lane loads (lanes >= 9 repeat chunk 0): no divergent load, so no early wait
+            vh = *(const uint4 *)(a.data + g0 - FH + 16 * (halo ? hc : 0));
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = load_chunk(a.data, g0 + (int64_t)(tid + TPB * i) * 16, len);
+            if (halo) vh = load_chunk(a.data, g0 - FH + (int64_t)hc * 16, len);
+        }
+        if (tid == 0) {
+            sh.last_chunk = -1;
+            sh.nh = 0;
+            sh.qn = 0;
+        }
         uint32_t orall = 0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -520,6 +530,7 @@ __global__ __launch_bounds__(TPB) void scan_tile_kernel(ScanArgs a) {
             *(uint4 *)(buf + FH + (tid + TPB * i) * 16) = v[i];
         }
         if (halo) *(uint4 *)(buf + hc * 16) = vh;
+        if (tid < 2 * KMAX_TILE) s_pr[tid] = a.PR[tid];     // (behind the tile loads)
         if (orall & 0x80808080u) atomicOr(a.err, ERR_NONASCII);
     }
     __syncthreads();
@@ -528,43 +539,57 @@ __global__ __launch_bounds__(TPB) void scan_tile_kernel(ScanArgs a) {
     const uint32_t P4 = a.p4, R4 = a.r4, PM = a.pmask;
     uint32_t cand = 0;           // bit 4*i + j: word j of chunk i has a 4-byte match
     uint64_t packed = 0;         // 16-bit '\n' count of chunk i in bits [16i, 16i+16)
+    // only the last tile has bytes past len (sentinels): keep the masking out of the hot loop
+    const bool tail_tile = (uint64_t)(g0 + TILE) > len;
+    const bool do_swar = !(a.ablate & 2u);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int c = tid + TPB * i;
         const uint4 xv = *(const uint4 *)(buf + FH + 16 * c);
         const uint32_t x[5] = {xv.x, xv.y, xv.z, xv.w, *(const uint32_t *)(buf + FH + 16 * c + 16)};
-        const int64_t gc = g0 + (int64_t)c * 16;
         uint32_t cnt = 0;
+        if (!tail_tile) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            uint32_t z = nl_flags(x[j]);
-            if (gc + 16 > (int64_t)len) {   // last tile: only bytes < len are lines
+            for (int j = 0; j < 4; ++j) cnt += __popc(nl_flags(x[j]));
+        } else {
+            const int64_t gc = g0 + (int64_t)c * 16;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
                 const int64_t n = (int64_t)len - (gc + 4 * j);
+                uint32_t z = nl_flags(x[j]);
                 z = n <= 0 ? 0u : n < 4 ? (z & ((1u << (8 * n)) - 1u)) : z;
+                cnt += __popc(z);
             }
-            cnt += __popc(z);
-            if (a.ablate & 2u) continue;
-            const uint32_t x0 = x[j];
-            const uint32_t x1 = align4(x[j + 1], x[j], 1);
-            const uint32_t x2 = align4(x[j + 1], x[j], 2);
-            const uint32_t x3 = align4(x[j + 1], x[j], 3);
-            bool hit;
-            if (FULL4) {
-                hit = (x0 == P4) | (x1 == P4) | (x2 == P4) | (x3 == P4) |
-                      (x0 == R4) | (x1 == R4) | (x2 == R4) | (x3 == R4);
-            } else {
-                hit = (((x0 ^ P4) & PM) == 0) | (((x1 ^ P4) & PM) == 0) | (((x2 ^ P4) & PM) == 0) |
-                      (((x3 ^ P4) & PM) == 0) | (((x0 ^ R4) & PM) == 0) | (((x1 ^ R4) & PM) == 0) |
-                      (((x2 ^ R4) & PM) == 0) | (((x3 ^ R4) & PM) == 0);
+        }
+        if (do_swar) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                // 4-byte windows at the word's 4 positions vs P[0:4] / rc(P)[0:4]:
+                // xor + min on the vector unit (the compare-and-OR form would
+                // load the scalar unit, which this kernel is short of)
+                const uint32_t x0 = x[j];
+                const uint32_t x1 = align4(x[j + 1], x[j], 1);
+                const uint32_t x2 = align4(x[j + 1], x[j], 2);
+                const uint32_t x3 = align4(x[j + 1], x[j], 3);
+                uint32_t m;
+                if (FULL4) {
+                    m = min(min(min(x0 ^ P4, x1 ^ P4), min(x2 ^ P4, x3 ^ P4)),
+                            min(min(x0 ^ R4, x1 ^ R4), min(x2 ^ R4, x3 ^ R4)));
+                } else {
+                    m = min(min(min((x0 ^ P4) & PM, (x1 ^ P4) & PM), min((x2 ^ P4) & PM, (x3 ^ P4) & PM)),
+                            min(min((x0 ^ R4) & PM, (x1 ^ R4) & PM), min((x2 ^ R4) & PM, (x3 ^ R4) & PM)));
+                }
+                cand |= m == 0 ? (1u << (4 * i + j)) : 0u;
             }
-            cand |= hit ? (1u << (4 * i + j)) : 0u;
         }
         packed |= (uint64_t)cnt << (16 * i);
-        if (cnt) atomicMax(&sh.last_chunk, c);
+        // chunk bitmap + highest chunk with a '\n', from one ballot (no per-lane atomics)
         const unsigned long long m = __ballot(cnt != 0);
         if (lane == 0) {
-            sh.nlmap[(c - lane) >> 5] = (uint32_t)m;
-            sh.nlmap[((c - lane) >> 5) + 1] = (uint32_t)(m >> 32);
+            const int c0 = c;                               // wave's first chunk of this column
+            sh.nlmap[c0 >> 5] = (uint32_t)m;
+            sh.nlmap[(c0 >> 5) + 1] = (uint32_t)(m >> 32);
+            if (m) atomicMax(&sh.last_chunk, c0 + 63 - (int)__clzll((long long)m));
         }
     }
 
@@ -612,8 +637,7 @@ __global__ __launch_bounds__(TPB) void scan_tile_kernel(ScanArgs a) {
     // ---- candidates -> verified hits (each lane its own words, straight-line)
     //      -> LDS queue -> hit records (one hit per lane: the rare, branchy work
     //      runs once per tile in as few waves as possible) ----
-    if (tid == 0) sh.qn = 0;
-    __syncthreads();             // cpre / qn visible
+    __syncthreads();             // cpre / nlmap visible
     while (cand) {
         const int bitc = __ffs(cand) - 1;
         cand &= cand - 1;
