@@ -3,10 +3,11 @@
 Workload (BASELINE.json configs[1]): per GPU, 10 M synthetic
 150 bp reads (317 B FASTQ records, 3.17 GB, generated on the device), k=16,
 prefix 'ATGAC'.  A step = one pass of the hot path over the resident batch:
-the single-pass tile kernel (line framing + both strands + prefix filter +
-dense count/first-occurrence table), the RCCL table merge when N > 1, and the
-finish on rank 0 (compaction, radix sort by first occurrence, key decode):
-the ordered Map-equivalent result, in HBM.
+the single-pass scan kernel (line framing + both strands + prefix filter ->
+packed hit per accepted window), hit resolution, the per-rank reduce of
+packed keys (radix sort + reduce-by-key), the RCCL gather of the partials to
+rank 0 when N > 1, and the finish on rank 0 (merged reduce, radix sort by
+first occurrence, key decode): the ordered Map-equivalent result, in HBM.
 
 value = windows examined on both strands (k-mers) per second,
 whole job.  Also reported: distinct k-mers/s, the tile kernel's roofline
@@ -79,7 +80,7 @@ def main():
     import torch
     import torch.distributed as dist
     from kmerjs_amd import Counter, synth_fastq_device
-    from kmerjs_amd.multi import device_u64, merge_dense_tables, shard_plan
+    from kmerjs_amd.multi import merge_to, shard_plan
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -99,16 +100,7 @@ def main():
     torch.cuda.synchronize()
 
     ctr = Counter(k=args.k, prefix=prefix, device=local, flags=args.flags)
-    dense = True
-    try:
-        c_ptr, f_ptr, n_tab = ctr.table_view()
-        counts_t = device_u64(c_ptr, n_tab, dev)
-        first_t = device_u64(f_ptr, n_tab, dev)
-    except Exception:
-        dense = False
-        if world > 1:
-            raise
-
+    total_lines = world * args.reads * 4
     tile_ms, feed_ms_l = [], []
 
     def step(record):
@@ -120,11 +112,8 @@ def main():
             tile_ms.append(scan_ms)
             feed_ms_l.append(feed_ms)
         if world > 1:
-            torch.cuda.synchronize()
-            merge_dense_tables(counts_t, first_t, dst=0)
-            if rank == 0:   # the merged table spans every shard's lines
-                ctr.set_position(world * args.reads * 4, world * nbytes)
-        if rank == 0:
+            merge_to(ctr, args.k, len(prefix), total_lines, dst=0, want_result=False)
+        else:
             ctr.finish(want_result=False)
 
     for _ in range(args.warmup):
@@ -148,28 +137,21 @@ def main():
     ctr.reset()
     ctr.set_position(plan["lines_before"], plan["byte_offset"])
     ctr.feed_device(buf.data_ptr(), nbytes)
-    if world > 1:
-        torch.cuda.synchronize()
-        merge_dense_tables(counts_t, first_t, dst=0)
-        if rank == 0:
-            ctr.set_position(world * args.reads * 4, world * nbytes)
     distinct, accepted = 0, 0
+    res = merge_to(ctr, args.k, len(prefix), total_lines, dst=0) if world > 1 else ctr.finish(want_result=True)
     if rank == 0:
-        res = ctr.finish(want_result=True)
         distinct = len(res)
         accepted = int(res.counts.sum())
-        local_accepted = int(counts_t.sum().item()) if (dense and world == 1) else None
-        if local_accepted is not None:
-            assert local_accepted == accepted
+        assert res.lines == total_lines, (res.lines, total_lines)
 
     if rank == 0:
         windows_step = world * args.reads * windows_per_read(args.k)
         ms_per_step = elapsed / args.steps * 1e3
         value = windows_step * args.steps / elapsed
         kern_ms = sum(tile_ms) / len(tile_ms)
-        # algorithmic bytes per launch: the whole FASTQ batch is read once
-        # (B_in) + one 8-B count RMW and one 8-B first-occurrence RMW per accepted window
-        algo_bytes = nbytes + 32 * (accepted / world)
+        # algorithmic bytes per scan launch: the whole FASTQ batch is read
+        # once (B_in) + one 24-B hit record written per accepted window
+        algo_bytes = nbytes + 24 * (accepted / world)
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
         traffic = load_traffic(args)
         out = {
@@ -188,7 +170,7 @@ def main():
             "config": {"workload": "C2: %d synthetic 150bp reads per GPU, k=%d, prefix '%s'"
                                    % (args.reads, args.k, args.prefix),
                        "reads_per_gpu": args.reads, "k": args.k, "prefix": args.prefix,
-                       "bytes_per_gpu": nbytes, "parallelism": "dp%d (reads sharded, RCCL table reduce)" % world},
+                       "bytes_per_gpu": nbytes, "parallelism": "dp%d (reads sharded, RCCL gather of partials)" % world},
             "distinct_kmers_per_s": distinct * args.steps / elapsed,
             "distinct_kmers": distinct,
             "accepted_windows": accepted,

@@ -21,8 +21,8 @@
  *
  * Device-resident entry points (kmer_reset / kmer_feed_device /
  * kmer_finish_device) let a caller that already holds the FASTQ bytes in HBM
- * count them without any host copy; kmer_table_* expose the dense count
- * tables so that per-GPU tables can be merged with an RCCL reduce.
+ * count them without any host copy; kmer_partial_device / kmer_finish_merged
+ * merge per-GPU partial results (shards of one input, RCCL over xGMI).
  *
  * Threading: a kmer_ctx is used by one thread at a time (one in-flight call
  * per context); distinct contexts are independent.  All calls return a
@@ -52,7 +52,7 @@ typedef enum {
 
 enum {
     KMER_FLAG_TWO_PASS = 1u << 0,  /* debug: exact two-pass line scan instead of single-pass look-back */
-    KMER_FLAG_NO_DENSE = 1u << 1,  /* debug: force the general (record) path */
+    KMER_FLAG_NO_DENSE = 1u << 1,  /* debug: records instead of packed keys (host merge) */
     /* experiments only (results are WRONG with these set): ablate parts of the tile scan */
     KMER_FLAG_ABLATE_HITS = 1u << 8,   /* drop every prefix candidate */
     KMER_FLAG_ABLATE_SWAR = 1u << 9    /* skip the SWAR prefix scan entirely */
@@ -84,16 +84,32 @@ kmer_status kmer_count_buffer(kmer_ctx *ctx, const uint8_t *bytes, size_t len, k
  * at a line start (offset 0 of the input, or just after a '\n'); all chunks
  * but the last must end with '\n'.  `stream` is a hipStream_t (NULL = the
  * context's own stream).  kmer_finish_device leaves the ordered result in
- * device memory (see kmer_result_device_*) and also returns it as a host
- * result when `out` is non-NULL. */
+ * device memory (kmer_result_device) and also returns it as a host result
+ * when `out` is non-NULL. */
 kmer_status kmer_reset(kmer_ctx *ctx);
 kmer_status kmer_feed_device(kmer_ctx *ctx, const void *d_bytes, size_t len, void *stream);
 kmer_status kmer_finish_device(kmer_ctx *ctx, kmer_result **out);
 
-/* Dense-table view for multi-GPU merges (valid between reset and finish).
- * counts: uint64[n], first: uint64[n] (first-occurrence order, UINT64_MAX = none).
- * Returns KMER_E_STATE when the configuration does not use the dense table. */
-kmer_status kmer_table_view(kmer_ctx *ctx, void **d_counts, void **d_first, uint64_t *n);
+/* Multi-GPU merge.  kmer_partial_device reduces this context's session to its
+ * unique packed keys: keys = uint64[n] 2-bit suffix codes (the k-|P| bases
+ * after the prefix, first base most significant), vals = n x {uint64 first,
+ * uint64 count} (first-occurrence order, count).  Device pointers, valid until
+ * the next call on the context.  Concatenate the partials of every rank on one
+ * device (e.g. RCCL gather over xGMI) and hand them to kmer_finish_merged,
+ * which reduces again (min first, sum count), orders by first occurrence and
+ * decodes.  Record keys (non-ACGT windows) stay on the host: move them with
+ * kmer_records_export / kmer_records_import.  KMER_E_STATE when the
+ * configuration has no packed keys. */
+kmer_status kmer_partial_device(kmer_ctx *ctx, const void **d_keys, const void **d_vals, uint64_t *n);
+kmer_status kmer_finish_merged(kmer_ctx *ctx, const void *d_keys, const void *d_vals, uint64_t n,
+                               uint64_t total_lines, kmer_result **out);
+kmer_status kmer_records_export(kmer_ctx *ctx, kmer_result **out);
+kmer_status kmer_records_import(kmer_ctx *ctx, const char *keys, const uint64_t *offsets,
+                                const uint64_t *counts, const uint64_t *firsts, uint64_t n);
+/* Ordered result of the last finish, still in device memory (packed path):
+ * keys = n * k bytes, counts = uint64[n], firsts = uint64[n]. */
+kmer_status kmer_result_device(kmer_ctx *ctx, const void **d_keys, const void **d_counts,
+                               const void **d_firsts, uint64_t *n);
 /* Set the running line/byte position (lines already consumed, absolute byte
  * offset of the next fed chunk) — used when one input is sharded over ranks. */
 kmer_status kmer_set_position(kmer_ctx *ctx, uint64_t lines_before, uint64_t byte_offset);
@@ -108,6 +124,8 @@ kmer_status kmer_result_get(const kmer_result *r, uint64_t i, const char **key, 
 /* Bulk view: keys packed back to back; key i = keys[offsets[i] .. offsets[i+1]). */
 kmer_status kmer_result_arrays(const kmer_result *r, const char **keys, const uint64_t **offsets,
                                const uint64_t **counts);
+/* First-occurrence order key of every entry (monotone in Map order). */
+kmer_status kmer_result_firsts(const kmer_result *r, const uint64_t **firsts);
 void kmer_result_free(kmer_result *r);
 
 /* Benchmark utility: write n_reads synthetic 317-byte FASTQ records (SURVEY.md

@@ -17,10 +17,11 @@ FLAG_NO_DENSE = 2
 
 # every symbol the header declares (tests/test_abi.py checks header <-> library)
 EXPORTS = ["kmer_open", "kmer_close", "kmer_count_file", "kmer_count_buffer", "kmer_reset",
-           "kmer_feed_device", "kmer_finish_device", "kmer_table_view", "kmer_set_position",
+           "kmer_feed_device", "kmer_finish_device", "kmer_partial_device", "kmer_finish_merged",
+           "kmer_records_export", "kmer_records_import", "kmer_result_device", "kmer_set_position",
            "kmer_lines", "kmer_result_size", "kmer_result_lines", "kmer_result_get",
-           "kmer_result_arrays", "kmer_result_free", "kmer_synth_fastq_device", "kmer_last_timing",
-           "kmer_status_string", "kmer_last_error", "kmer_version"]
+           "kmer_result_arrays", "kmer_result_firsts", "kmer_result_free", "kmer_synth_fastq_device",
+           "kmer_last_timing", "kmer_status_string", "kmer_last_error", "kmer_version"]
 
 
 class Params(ctypes.Structure):
@@ -58,7 +59,12 @@ def _load():
         "kmer_reset": (ctypes.c_int, [vp]),
         "kmer_feed_device": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp]),
         "kmer_finish_device": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
-        "kmer_table_view": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), pu64]),
+        "kmer_partial_device": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), pu64]),
+        "kmer_finish_merged": (ctypes.c_int, [vp, vp, vp, u64, u64, ctypes.POINTER(vp)]),
+        "kmer_records_export": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
+        "kmer_records_import": (ctypes.c_int, [vp, ctypes.c_char_p, pu64, pu64, pu64, u64]),
+        "kmer_result_device": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), pu64]),
+        "kmer_result_firsts": (ctypes.c_int, [vp, ctypes.POINTER(pu64)]),
         "kmer_set_position": (ctypes.c_int, [vp, u64, u64]),
         "kmer_lines": (ctypes.c_int, [vp, pu64]),
         "kmer_result_size": (u64, [vp]),
@@ -99,21 +105,30 @@ class Result:
         n = LIB.kmer_result_size(handle)
         self.lines = LIB.kmer_result_lines(handle)
         LIB.kmer_result_arrays(handle, ctypes.byref(keys), ctypes.byref(offs), ctypes.byref(cnts))
+        import numpy as np
         if n:
-            import numpy as np
+            firsts = ctypes.POINTER(ctypes.c_uint64)()
+            LIB.kmer_result_firsts(handle, ctypes.byref(firsts))
             off = np.ctypeslib.as_array(offs, shape=(n + 1,)).copy()
             self.counts = np.ctypeslib.as_array(cnts, shape=(n,)).copy()
+            self.firsts = np.ctypeslib.as_array(firsts, shape=(n,)).copy()
             self.keybuf = ctypes.string_at(keys, int(off[-1]))
             self.offsets = off
         else:
-            import numpy as np
             self.counts = np.zeros(0, dtype=np.uint64)
+            self.firsts = np.zeros(0, dtype=np.uint64)
             self.keybuf = b""
             self.offsets = np.zeros(1, dtype=np.uint64)
         LIB.kmer_result_free(handle)
 
     def __len__(self):
         return len(self.counts)
+
+    def keys(self):
+        """[key_bytes] in first-occurrence order."""
+        o = self.offsets.tolist()
+        b = self.keybuf
+        return [b[o[i]:o[i + 1]] for i in range(len(o) - 1)]
 
     def entries(self):
         """[(key_bytes, count)] in first-occurrence order."""
@@ -180,10 +195,46 @@ class Counter:
         self._check(LIB.kmer_finish_device(self.h, ctypes.byref(r) if want_result else None), "finish")
         return Result(r) if want_result else None
 
-    def table_view(self):
-        c, f, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
-        self._check(LIB.kmer_table_view(self.h, ctypes.byref(c), ctypes.byref(f), ctypes.byref(n)), "table_view")
-        return c.value, f.value, n.value
+    # ---- multi-GPU merge ----
+    def partial_device(self):
+        """(d_keys, d_vals, n): this session's unique packed keys (uint64[n]) and
+        {first, count} pairs (uint64[n, 2]) in device memory."""
+        k, v, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+        self._check(LIB.kmer_partial_device(self.h, ctypes.byref(k), ctypes.byref(v), ctypes.byref(n)),
+                    "partial_device")
+        return k.value or 0, v.value or 0, n.value
+
+    def finish_merged(self, d_keys, d_vals, n, total_lines, want_result=True):
+        r = ctypes.c_void_p()
+        self._check(LIB.kmer_finish_merged(self.h, ctypes.c_void_p(d_keys), ctypes.c_void_p(d_vals), n, total_lines,
+                                           ctypes.byref(r) if want_result else None), "finish_merged")
+        return Result(r) if want_result else None
+
+    def records_export(self):
+        """Host-side record keys (non-ACGT windows) as (keys, offsets, counts, firsts)."""
+        r = ctypes.c_void_p()
+        self._check(LIB.kmer_records_export(self.h, ctypes.byref(r)), "records_export")
+        res = Result(r)
+        return res.keybuf, res.offsets, res.counts, res.firsts
+
+    def records_import(self, keybuf, offsets, counts, firsts):
+        import numpy as np
+        n = len(counts)
+        if n == 0:
+            return
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        cnt = np.ascontiguousarray(counts, dtype=np.uint64)
+        fst = np.ascontiguousarray(firsts, dtype=np.uint64)
+        P = ctypes.POINTER(ctypes.c_uint64)
+        self._check(LIB.kmer_records_import(self.h, keybuf, off.ctypes.data_as(P), cnt.ctypes.data_as(P),
+                                            fst.ctypes.data_as(P), n), "records_import")
+
+    def result_device(self):
+        """(d_keys, d_counts, d_firsts, n) of the last finish, in device memory."""
+        k, c, f, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+        self._check(LIB.kmer_result_device(self.h, ctypes.byref(k), ctypes.byref(c), ctypes.byref(f),
+                                           ctypes.byref(n)), "result_device")
+        return k.value or 0, c.value or 0, f.value or 0, n.value
 
     def lines(self):
         n = ctypes.c_uint64()

@@ -1,14 +1,23 @@
 // kmer_api.hip — host orchestration behind the C-ABI (include/kmer_api.h).
 //
-// One kmer_ctx = one device, one HIP stream, the device tables for one
-// (k, preffix, step) configuration.  Input flows in chunks that start at a
-// line start; every chunk is one launch of the single-pass tile kernel (or,
-// for configurations the tile kernel does not cover, the line-list + window
-// kernels).  finish() compacts the dense table, radix-sorts it by first
-// occurrence (rocPRIM), decodes keys and merges the rare record keys, giving
-// the reference Map's exact iteration order (lib/kmers.js:76,95).
+// One kmer_ctx = one device, one HIP stream, one (k, preffix, step)
+// configuration.  Input flows in chunks that start at a line start.
+//
+// Packed path (step 1, ACGT prefix, |P| <= k <= 32) and tile-record path
+// (step 1, any prefix, k <= 64), per chunk:
+//   scan_tile_kernel   one HBM pass: '\n' aggregates + verified prefix hits
+//   3 x rocPRIM scan   per-tile line index / line start / hit-slot offsets
+//   hit_kernel         line rule + first-occurrence order; packed hits go to
+//                      the session's (suffix code, {order, 1}) array, the
+//                      rest become records merged on the host
+// finish: radix-sort the packed hits by code, reduce_by_key (min order, sum
+// count), radix-sort the unique keys by first occurrence, decode -> the
+// reference Map's exact iteration order (lib/kmers.js:76,95).
+// General path (step > 1, empty prefix, k > 64): line list (decoupled
+// look-back over tiles) + one-workgroup-per-line window kernel -> records.
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_reduce_by_key.hpp>
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
@@ -25,11 +34,52 @@ using namespace kmerhip;
 
 namespace {
 
-enum Mode { MODE_DENSE, MODE_TILE_REC, MODE_GENERAL };
+enum Mode { MODE_PACKED, MODE_TILE_REC, MODE_GENERAL };
 
 struct Ent {
     uint64_t count;
     uint64_t first;
+};
+
+struct AggMinSum {
+    __host__ __device__ Agg operator()(const Agg &x, const Agg &y) const {
+        Agg r;
+        r.first = x.first < y.first ? x.first : y.first;
+        r.count = x.count + y.count;
+        return r;
+    }
+};
+
+// growable device array; `keep` preserves the first `used` elements on growth
+template <typename T>
+struct DBuf {
+    T *p = nullptr;
+    uint64_t cap = 0;
+    hipError_t ensure(uint64_t n, hipStream_t s, bool keep = false, uint64_t used = 0) {
+        if (n <= cap) return hipSuccess;
+        uint64_t nc = std::max<uint64_t>(n, cap + cap / 2);
+        nc = std::max<uint64_t>(nc, 1024);
+        T *q = nullptr;
+        hipError_t e = hipMalloc((void **)&q, nc * sizeof(T));
+        if (e != hipSuccess) return e;
+        if (p) {
+            if (keep && used) {
+                e = hipMemcpyAsync(q, p, used * sizeof(T), hipMemcpyDeviceToDevice, s);
+                if (e != hipSuccess) return e;
+            }
+            e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return e;
+            (void)hipFree(p);
+        }
+        p = q;
+        cap = nc;
+        return hipSuccess;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
 };
 
 }  // namespace
@@ -39,6 +89,7 @@ struct kmer_result {
     std::vector<char> keys;
     std::vector<uint64_t> offsets{0};
     std::vector<uint64_t> counts;
+    std::vector<uint64_t> firsts;
 };
 
 struct kmer_ctx {
@@ -48,56 +99,43 @@ struct kmer_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
+    uint32_t kbits = 0;            // packed key bits = 2*(k - |P|)
 
-    // dense table
-    uint64_t n_dense = 0;
-    unsigned long long *d_counts = nullptr, *d_first = nullptr;
-    // look-back state
+    // per tile
     uint64_t tile_cap = 0;
-    unsigned long long *d_lb_cnt = nullptr, *d_lb_lnl = nullptr;
-    uint64_t *d_tp_cnt = nullptr, *d_tp_lnl = nullptr;
-    // streaming scan path: per-tile aggregates, their scans, hit slots
-    uint64_t *d_agg_cnt = nullptr, *d_agg_lnl = nullptr, *d_cscan = nullptr, *d_lnl_before = nullptr;
-    uint32_t *d_tile_nhits = nullptr;
-    HitRec *d_hits = nullptr;
-    HitRec *d_ovf = nullptr;
-    uint64_t ovf_cap = 0;
-    unsigned long long *d_ovf_count = nullptr;
-    void *d_scan_tmp = nullptr;
-    size_t scan_tmp_bytes = 0;
-    // small device words
-    unsigned int *d_ticket = nullptr, *d_err = nullptr;
-    unsigned long long *d_rec_count = nullptr, *d_line_count = nullptr, *d_nout = nullptr;
-    StreamPos *d_pos = nullptr, *d_pos_saved = nullptr;
+    DBuf<uint64_t> agg_cnt, agg_lnl, cscan, lnl_before, hscan;
+    DBuf<uint32_t> tile_nhits;
+    DBuf<HitRec> hits, ovf;
+    DBuf<unsigned long long> lb_cnt, lb_lnl;   // general path look-back
+    DBuf<uint64_t> tp_cnt, tp_lnl;             // general path, two-pass debug mode
+    // session packed hits and finish buffers
+    uint64_t n_hits = 0;
+    DBuf<uint64_t> hkey, hkey2, ukey, first, first2, idx, idx2, cnt_out;
+    DBuf<Agg> hval, hval2, uval;
+    DBuf<uint8_t> keys_out;
+    uint64_t n_out = 0;            // ordered entries of the last finish (device)
     // records & lines
-    uint64_t rec_cap = 0, line_cap = 0;
-    Record *d_recs = nullptr;
-    SeqLine *d_lines = nullptr;
-    uint8_t *d_rec_keys = nullptr;
-    uint64_t *d_rec_off = nullptr;
-    // finish buffers (dense)
-    uint64_t *d_order = nullptr, *d_order2 = nullptr, *d_idx = nullptr, *d_idx2 = nullptr;
-    uint8_t *d_keys_out = nullptr;
-    uint64_t *d_cnt_out = nullptr;
-    uint8_t *d_P = nullptr;
-    uint8_t *d_PR = nullptr;       // P[0..64) then rc(P)[0..64) (tile layout); long P copied after
-    void *d_sort_tmp = nullptr;
-    size_t sort_tmp_bytes = 0;
-    uint64_t last_n = 0;
+    DBuf<Record> recs;
+    DBuf<SeqLine> lines;
+    DBuf<uint8_t> rec_keys;
+    // scratch
+    DBuf<uint8_t> tmp;
+    unsigned int *d_ticket = nullptr, *d_err = nullptr;
+    unsigned long long *d_rec_count = nullptr, *d_line_count = nullptr, *d_ovf_count = nullptr;
+    uint64_t *d_nuniq = nullptr;
+    StreamPos *d_pos = nullptr, *d_pos_saved = nullptr;
+    uint8_t *d_P = nullptr;        // prefix bytes (decode)
+    uint8_t *d_PR = nullptr;       // [0,64) P, [64,128) rc(P) (tile kernel), [128,..) full P (general kernel)
     // host side
     uint64_t abs_offset = 0;
     bool open_stream = false;      // reset called, not finished
     std::unordered_map<std::string, Ent> exotic;
-    // pinned scratch
-    uint64_t *h_small = nullptr;   // [0]=rec_count [1]=line_count [2]=err [3]=nout [4..7]=pos
-    // batch staging for host input
-    uint8_t *d_batch = nullptr;
-    uint64_t batch_cap = 0;
-    uint8_t *h_stage = nullptr;
-    uint64_t stage_cap = 0;
-    // timing
+    uint64_t *h_small = nullptr;   // pinned: [0] rec_count [1] ovf/line count [2] err [3] hscan last
+                                   //         [4] nhits last [5] nuniq [6] last key [8..11] pos
+    DBuf<uint8_t> batch;
+    // timing (HIP events on the context stream)
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr;
-    double count_ms = 0.0, finish_ms = 0.0, feed_ms = 0.0;
+    double scan_ms = 0.0, feed_ms = 0.0, finish_ms = 0.0;
 };
 
 namespace {
@@ -111,6 +149,18 @@ const uint64_t DEFAULT_BATCH = 1ull << 30;
             (ctx)->err = std::string("HIP error: ") + hipGetErrorString(e_) + " at " #x;    \
             return KMER_E_DEVICE;                                                           \
         }                                                                                   \
+    } while (0)
+
+// rocPRIM call with context-owned temporary storage: size query, grow, run.
+// `CALL` is an expression in the names t (storage) and b (its size).
+#define ROCPRIM_RUN(ctx, CALL)                                                          \
+    do {                                                                                \
+        size_t b = 0;                                                                   \
+        void *t = nullptr;                                                              \
+        HIPCHK(ctx, CALL);                                                              \
+        HIPCHK(ctx, (ctx)->tmp.ensure(b + 16, (ctx)->stream));                          \
+        t = (ctx)->tmp.p;                                                               \
+        HIPCHK(ctx, CALL);                                                              \
     } while (0)
 
 kmer_status fail(kmer_ctx *c, kmer_status s, const std::string &msg) {
@@ -145,72 +195,33 @@ void dfree(T *&p) {
     p = nullptr;
 }
 
+int bit_width(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 0; }
+
 kmer_status ensure_tiles(kmer_ctx *c, uint64_t n_tiles) {
     if (n_tiles <= c->tile_cap) return KMER_OK;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    dfree(c->d_lb_cnt);
-    dfree(c->d_lb_lnl);
-    dfree(c->d_tp_cnt);
-    dfree(c->d_tp_lnl);
-    dfree(c->d_agg_cnt); dfree(c->d_agg_lnl); dfree(c->d_cscan); dfree(c->d_lnl_before);
-    dfree(c->d_tile_nhits); dfree(c->d_hits);
-    if (c->d_scan_tmp) (void)hipFree(c->d_scan_tmp);
-    c->d_scan_tmp = nullptr;
-    uint64_t cap = std::max<uint64_t>(n_tiles, 1024);
-    HIPCHK(c, dalloc(&c->d_lb_cnt, cap));
-    HIPCHK(c, dalloc(&c->d_lb_lnl, cap));
-    HIPCHK(c, dalloc(&c->d_tp_cnt, cap));
-    HIPCHK(c, dalloc(&c->d_tp_lnl, cap));
-    if (c->mode != MODE_GENERAL) {
-        HIPCHK(c, dalloc(&c->d_agg_cnt, cap));
-        HIPCHK(c, dalloc(&c->d_agg_lnl, cap));
-        HIPCHK(c, dalloc(&c->d_cscan, cap));
-        HIPCHK(c, dalloc(&c->d_lnl_before, cap));
-        HIPCHK(c, dalloc(&c->d_tile_nhits, cap));
-        HIPCHK(c, dalloc(&c->d_hits, cap * HMAX));
-        size_t a = 0, b = 0;
-        HIPCHK(c, rocprim::exclusive_scan(nullptr, a, c->d_agg_cnt, c->d_cscan, (uint64_t)0, (size_t)cap,
-                                          rocprim::plus<uint64_t>(), c->stream));
-        HIPCHK(c, rocprim::exclusive_scan(nullptr, b, c->d_agg_lnl, c->d_lnl_before, (uint64_t)0, (size_t)cap,
-                                          rocprim::maximum<uint64_t>(), c->stream));
-        c->scan_tmp_bytes = std::max(a, b);
-        HIPCHK(c, hipMalloc(&c->d_scan_tmp, std::max<size_t>(c->scan_tmp_bytes, 16)));
+    const uint64_t cap = std::max<uint64_t>(n_tiles, 1024);
+    hipStream_t s = c->stream;
+    if (c->mode == MODE_GENERAL) {
+        HIPCHK(c, c->lb_cnt.ensure(cap, s));
+        HIPCHK(c, c->lb_lnl.ensure(cap, s));
+        HIPCHK(c, c->tp_cnt.ensure(cap, s));
+        HIPCHK(c, c->tp_lnl.ensure(cap, s));
+    } else {
+        HIPCHK(c, c->agg_cnt.ensure(cap, s));
+        HIPCHK(c, c->agg_lnl.ensure(cap, s));
+        HIPCHK(c, c->cscan.ensure(cap, s));
+        HIPCHK(c, c->lnl_before.ensure(cap, s));
+        HIPCHK(c, c->hscan.ensure(cap, s));
+        HIPCHK(c, c->tile_nhits.ensure(cap, s));
+        HIPCHK(c, c->hits.ensure(cap * HMAX, s));
     }
     c->tile_cap = cap;
     return KMER_OK;
 }
 
 kmer_status ensure_records(kmer_ctx *c, uint64_t n) {
-    if (n <= c->rec_cap) return KMER_OK;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    dfree(c->d_recs);
-    dfree(c->d_rec_keys);
-    dfree(c->d_rec_off);
-    uint64_t cap = std::max<uint64_t>(n, 1 << 16);
-    HIPCHK(c, dalloc(&c->d_recs, cap));
-    HIPCHK(c, dalloc(&c->d_rec_off, cap));
-    HIPCHK(c, dalloc(&c->d_rec_keys, cap * (uint64_t)c->p.k));
-    c->rec_cap = cap;
-    return KMER_OK;
-}
-
-kmer_status ensure_lines(kmer_ctx *c, uint64_t n) {
-    if (n <= c->line_cap) return KMER_OK;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    dfree(c->d_lines);
-    uint64_t cap = std::max<uint64_t>(n, 1 << 16);
-    HIPCHK(c, dalloc(&c->d_lines, cap));
-    c->line_cap = cap;
-    return KMER_OK;
-}
-
-kmer_status ensure_ovf(kmer_ctx *c, uint64_t n) {
-    if (n <= c->ovf_cap) return KMER_OK;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    dfree(c->d_ovf);
-    uint64_t cap = std::max<uint64_t>(n, 1 << 16);
-    HIPCHK(c, dalloc(&c->d_ovf, cap));
-    c->ovf_cap = cap;
+    HIPCHK(c, c->recs.ensure(n, c->stream));
+    HIPCHK(c, c->rec_keys.ensure(c->recs.cap * (uint64_t)c->p.k, c->stream));
     return KMER_OK;
 }
 
@@ -220,14 +231,17 @@ kmer_status ensure_ovf(kmer_ctx *c, uint64_t n) {
 kmer_status drain_records(kmer_ctx *c, const uint8_t *d_data, uint64_t n, hipStream_t s) {
     if (n == 0) return KMER_OK;
     const uint64_t k = c->p.k;
+    kmer_status st = ensure_records(c, n);
+    if (st) return st;
+    HIPCHK(c, c->idx.ensure(n, s));
     std::vector<uint64_t> off(n);
     for (uint64_t i = 0; i < n; ++i) off[i] = i * k;
-    HIPCHK(c, hipMemcpyAsync(c->d_rec_off, off.data(), n * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(c, launch_gather_records(c->d_recs, c->d_rec_off, n, d_data, c->d_rec_keys, s));
+    HIPCHK(c, hipMemcpyAsync(c->idx.p, off.data(), n * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(c, launch_gather_records(c->recs.p, c->idx.p, n, d_data, c->rec_keys.p, s));
     std::vector<Record> recs(n);
     std::vector<char> keys(n * k);
-    HIPCHK(c, hipMemcpyAsync(recs.data(), c->d_recs, n * sizeof(Record), hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipMemcpyAsync(keys.data(), c->d_rec_keys, n * k, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(recs.data(), c->recs.p, n * sizeof(Record), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(keys.data(), c->rec_keys.p, n * k, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     std::string key;
     for (uint64_t i = 0; i < n; ++i) {
@@ -250,13 +264,144 @@ kmer_status check_err(kmer_ctx *c, uint32_t e) {
     return KMER_OK;
 }
 
+// ---------------------------------------------------------------------------
+// fast path feed
+// ---------------------------------------------------------------------------
+kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s) {
+    const bool packed = c->mode == MODE_PACKED;
+    // capacity for every hit this chunk can produce: its tile slots + the overflow list
+    if (packed) {
+        const uint64_t need = c->n_hits + (uint64_t)n_tiles * HMAX + c->ovf.cap;
+        HIPCHK(c, c->hkey.ensure(need, s, true, c->n_hits));
+        HIPCHK(c, c->hval.ensure(need, s, true, c->n_hits));
+    }
+    ScanArgs a;
+    memset(&a, 0, sizeof(a));
+    a.data = d;
+    a.len = len;
+    a.abs_offset = c->abs_offset;
+    a.n_tiles = n_tiles;
+    a.k = c->p.k;
+    a.plen = (uint32_t)c->prefix.size();
+    a.p4 = pack4(c->prefix);
+    a.r4 = pack4(c->rprefix);
+    a.pmask = a.plen >= 4 ? 0xFFFFFFFFu : ((1u << (8 * a.plen)) - 1u);
+    a.PR = c->d_PR;
+    a.agg_cnt = c->agg_cnt.p;
+    a.agg_lnl = c->agg_lnl.p;
+    a.hits = c->hits.p;
+    a.tile_nhits = c->tile_nhits.p;
+    a.ovf = c->ovf.p;
+    a.ovf_count = c->d_ovf_count;
+    a.ovf_cap = c->ovf.cap;
+    a.err = c->d_err;
+    a.ablate = (c->p.flags >> 8) & 0xFFu;   // KMER_FLAG_ABLATE_* (experiments only)
+
+    HitArgs h;
+    memset(&h, 0, sizeof(h));
+    h.hits = c->hits.p;
+    h.tile_nhits = c->tile_nhits.p;
+    h.hscan = c->hscan.p;
+    h.ovf = c->ovf.p;
+    h.ovf_count = c->d_ovf_count;
+    h.ovf_cap = c->ovf.cap;
+    h.n_tiles = n_tiles;
+    h.k = a.k;
+    h.plen = a.plen;
+    h.abs_offset = c->abs_offset;
+    h.pos = c->d_pos;
+    h.cscan = c->cscan.p;
+    h.lnl_before = c->lnl_before.p;
+    h.packed = packed;
+    h.smask = (c->kbits >= 64) ? ~0ull : ((1ull << c->kbits) - 1ull);
+    h.invalid_key = c->kbits >= 63 ? ~0ull : (1ull << c->kbits);
+    h.out_key = packed ? c->hkey.p : nullptr;
+    h.out_val = packed ? c->hval.p : nullptr;
+    h.out_base = c->n_hits;
+    h.recs = c->recs.p;
+    h.rec_count = c->d_rec_count;
+    h.rec_cap = c->recs.cap;
+    h.err = c->d_err;
+
+    HIPCHK(c, hipMemcpyAsync(c->d_pos_saved, c->d_pos, sizeof(StreamPos), hipMemcpyDeviceToDevice, s));
+    kmer_status st;
+    for (int attempt = 0; attempt < 8; ++attempt) {
+        HIPCHK(c, hipMemsetAsync(c->d_ovf_count, 0, 8, s));
+        HIPCHK(c, hipMemsetAsync(c->d_rec_count, 0, 8, s));
+        HIPCHK(c, hipEventRecord(c->ev0, s));
+        HIPCHK(c, launch_scan_tiles(a, s));
+        HIPCHK(c, hipEventRecord(c->ev1, s));
+        ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->agg_cnt.p, c->cscan.p, (uint64_t)0, (size_t)n_tiles,
+                                               rocprim::plus<uint64_t>(), s));
+        ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->agg_lnl.p, c->lnl_before.p, (uint64_t)c->abs_offset,
+                                               (size_t)n_tiles, rocprim::maximum<uint64_t>(), s));
+        ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tile_nhits.p, c->hscan.p, (uint64_t)0, (size_t)n_tiles,
+                                               rocprim::plus<uint64_t>(), s));
+        HIPCHK(c, launch_hits(h, s));
+        HIPCHK(c, launch_pos_update(c->d_pos, c->cscan.p, c->agg_cnt.p, n_tiles, d, len, s));
+        HIPCHK(c, hipEventRecord(c->ev4, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 0, c->d_rec_count, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 1, c->d_ovf_count, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 2, c->d_err, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 3, c->hscan.p + (n_tiles - 1), 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 4, c->tile_nhits.p + (n_tiles - 1), 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        const uint32_t e = (uint32_t)c->h_small[2];
+        st = check_err(c, e);
+        if (st) return st;
+        float ms = 0.f, ms_all = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        HIPCHK(c, hipEventElapsedTime(&ms_all, c->ev0, c->ev4));
+        c->scan_ms += ms;
+        c->feed_ms += ms_all;
+        if (e & (ERR_OVF_OVERFLOW | ERR_REC_OVERFLOW)) {
+            // grow and redo the chunk from the saved position; hit resolution is
+            // idempotent (fixed slots), so a redo rewrites, never double counts
+            HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
+            HIPCHK(c, hipMemcpyAsync(c->d_pos, c->d_pos_saved, sizeof(StreamPos), hipMemcpyDeviceToDevice, s));
+            if (e & ERR_OVF_OVERFLOW) {
+                HIPCHK(c, c->ovf.ensure(c->h_small[1] + 1024, s));
+                a.ovf = c->ovf.p;
+                h.ovf = c->ovf.p;
+                a.ovf_cap = h.ovf_cap = c->ovf.cap;
+                if (packed) {
+                    const uint64_t need = c->n_hits + (uint64_t)n_tiles * HMAX + c->ovf.cap;
+                    HIPCHK(c, c->hkey.ensure(need, s, true, c->n_hits));
+                    HIPCHK(c, c->hval.ensure(need, s, true, c->n_hits));
+                    h.out_key = c->hkey.p;
+                    h.out_val = c->hval.p;
+                }
+            }
+            if (e & ERR_REC_OVERFLOW) {
+                st = ensure_records(c, c->h_small[0] + 1024);
+                if (st) return st;
+                h.recs = c->recs.p;
+                h.rec_cap = c->recs.cap;
+            }
+            continue;
+        }
+        break;
+    }
+    if (packed) c->n_hits += c->h_small[3] + (uint32_t)c->h_small[4] + c->h_small[1];
+    const uint64_t nrec = c->h_small[0];
+    if (nrec) {
+        st = drain_records(c, d, nrec, s);
+        if (st) return st;
+    }
+    c->abs_offset += len;
+    return KMER_OK;
+}
+
+// ---------------------------------------------------------------------------
+// general path feed
+// ---------------------------------------------------------------------------
 // Two-pass prefixes (debug mode): per-tile aggregates -> host scan -> arrays.
 kmer_status two_pass_prefix(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s) {
-    HIPCHK(c, launch_tile_aggregate(d, len, n_tiles, c->d_tp_cnt, c->d_tp_lnl, c->d_err, s));
+    HIPCHK(c, launch_tile_aggregate(d, len, n_tiles, c->tp_cnt.p, c->tp_lnl.p, c->d_err, s));
     std::vector<uint64_t> cnt(n_tiles), last(n_tiles);
     StreamPos pos;
-    HIPCHK(c, hipMemcpyAsync(cnt.data(), c->d_tp_cnt, n_tiles * 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipMemcpyAsync(last.data(), c->d_tp_lnl, n_tiles * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(cnt.data(), c->tp_cnt.p, n_tiles * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(last.data(), c->tp_lnl.p, n_tiles * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipMemcpyAsync(&pos, c->d_pos, sizeof(pos), hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     uint64_t lines = pos.lines, lnl = c->abs_offset;
@@ -272,115 +417,109 @@ kmer_status two_pass_prefix(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_
     HIPCHK(c, hipMemcpyAsync(&lastb, d + len - 1, 1, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     pos.ends_open = lastb != '\n';
-    HIPCHK(c, hipMemcpyAsync(c->d_tp_cnt, cnt.data(), n_tiles * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(c, hipMemcpyAsync(c->d_tp_lnl, last.data(), n_tiles * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->tp_cnt.p, cnt.data(), n_tiles * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->tp_lnl.p, last.data(), n_tiles * 8, hipMemcpyHostToDevice, s));
     HIPCHK(c, hipMemcpyAsync(c->d_pos, &pos, sizeof(pos), hipMemcpyHostToDevice, s));
     HIPCHK(c, hipStreamSynchronize(s));
     return KMER_OK;
 }
 
-// Fast path (dense / tile-record modes): streaming tile scan -> scans of the
-// per-tile aggregates -> hit resolution -> stream position update.
-kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s) {
-    ScanArgs a;
+kmer_status general_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s) {
+    const bool lookback = !(c->p.flags & KMER_FLAG_TWO_PASS);
+    HIPCHK(c, c->lines.ensure(1 << 16, s));
+    TileArgs a;
     memset(&a, 0, sizeof(a));
     a.data = d;
     a.len = len;
-    a.abs_offset = c->abs_offset;
     a.n_tiles = n_tiles;
     a.k = c->p.k;
     a.plen = (uint32_t)c->prefix.size();
-    a.p4 = pack4(c->prefix);
-    a.r4 = pack4(c->rprefix);
-    a.pmask = a.plen >= 4 ? 0xFFFFFFFFu : ((1u << (8 * a.plen)) - 1u);
-    a.PR = c->d_PR;
-    a.agg_cnt = c->d_agg_cnt;
-    a.agg_lnl = c->d_agg_lnl;
-    a.hits = c->d_hits;
-    a.tile_nhits = c->d_tile_nhits;
-    a.ovf = c->d_ovf;
-    a.ovf_count = c->d_ovf_count;
-    a.ovf_cap = c->ovf_cap;
+    a.abs_offset = c->abs_offset;
+    a.emit_lines = 1;
+    a.lines_out = c->lines.p;
+    a.line_count = c->d_line_count;
+    a.line_cap = c->lines.cap;
+    a.lb_cnt = c->lb_cnt.p;
+    a.lb_lnl = c->lb_lnl.p;
+    a.ticket = c->d_ticket;
+    a.pos = c->d_pos;
+    a.tp_cnt = c->tp_cnt.p;
+    a.tp_lnl = c->tp_lnl.p;
     a.err = c->d_err;
-    a.ablate = (c->p.flags >> 8) & 0xFFu;   // KMER_FLAG_ABLATE_* (experiments only)
-
-    HitArgs h;
-    memset(&h, 0, sizeof(h));
-    h.hits = c->d_hits;
-    h.tile_nhits = c->d_tile_nhits;
-    h.ovf = c->d_ovf;
-    h.ovf_count = c->d_ovf_count;
-    h.ovf_cap = c->ovf_cap;
-    h.n_tiles = n_tiles;
-    h.k = a.k;
-    h.plen = a.plen;
-    h.abs_offset = c->abs_offset;
-    h.pos = c->d_pos;
-    h.cscan = c->d_cscan;
-    h.lnl_before = c->d_lnl_before;
-    h.dense = c->mode == MODE_DENSE;
-    h.dense_update = 1;
-    h.smask = (2 * (a.k - std::min(a.plen, a.k)) >= 64) ? ~0ull : ((1ull << (2 * (a.k - std::min(a.plen, a.k)))) - 1ull);
-    h.counts = c->d_counts;
-    h.first = c->d_first;
-    h.recs = c->d_recs;
-    h.rec_count = c->d_rec_count;
-    h.rec_cap = c->rec_cap;
-    h.err = c->d_err;
-
-    HIPCHK(c, hipMemcpyAsync(c->d_pos_saved, c->d_pos, sizeof(StreamPos), hipMemcpyDeviceToDevice, s));
     kmer_status st;
+    HIPCHK(c, hipMemcpyAsync(c->d_pos_saved, c->d_pos, sizeof(StreamPos), hipMemcpyDeviceToDevice, s));
     for (int attempt = 0; attempt < 8; ++attempt) {
-        HIPCHK(c, hipMemsetAsync(c->d_ovf_count, 0, 8, s));
-        HIPCHK(c, hipMemsetAsync(c->d_rec_count, 0, 8, s));
+        HIPCHK(c, hipMemsetAsync(c->lb_cnt.p, 0, n_tiles * 8ull, s));
+        HIPCHK(c, hipMemsetAsync(c->lb_lnl.p, 0, n_tiles * 8ull, s));
+        HIPCHK(c, hipMemsetAsync(c->d_ticket, 0, 16, s));
+        HIPCHK(c, hipMemsetAsync(c->d_line_count, 0, 8, s));
+        if (!lookback) {
+            st = two_pass_prefix(c, d, len, n_tiles, s);
+            if (st) return st;
+        }
         HIPCHK(c, hipEventRecord(c->ev0, s));
-        HIPCHK(c, launch_scan_tiles(a, s));
+        HIPCHK(c, launch_lines(a, lookback, s));
         HIPCHK(c, hipEventRecord(c->ev1, s));
-        size_t tmp = c->scan_tmp_bytes;
-        HIPCHK(c, rocprim::exclusive_scan(c->d_scan_tmp, tmp, c->d_agg_cnt, c->d_cscan, (uint64_t)0, (size_t)n_tiles,
-                                          rocprim::plus<uint64_t>(), s));
-        tmp = c->scan_tmp_bytes;
-        HIPCHK(c, rocprim::exclusive_scan(c->d_scan_tmp, tmp, c->d_agg_lnl, c->d_lnl_before, (uint64_t)c->abs_offset,
-                                          (size_t)n_tiles, rocprim::maximum<uint64_t>(), s));
-        HIPCHK(c, launch_hits(h, s));
-        HIPCHK(c, launch_pos_update(c->d_pos, c->d_cscan, c->d_agg_cnt, n_tiles, d, len, s));
-        HIPCHK(c, hipEventRecord(c->ev4, s));
-        HIPCHK(c, hipMemcpyAsync(c->h_small + 0, c->d_rec_count, 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipMemcpyAsync(c->h_small + 1, c->d_ovf_count, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 1, c->d_line_count, 8, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipMemcpyAsync(c->h_small + 2, c->d_err, 4, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
         const uint32_t e = (uint32_t)c->h_small[2];
         st = check_err(c, e);
         if (st) return st;
-        float ms = 0.f, ms_all = 0.f;
+        float ms = 0.f;
         HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
-        HIPCHK(c, hipEventElapsedTime(&ms_all, c->ev0, c->ev4));
-        c->count_ms += ms;
-        c->feed_ms += ms_all;
-        if (e & (ERR_OVF_OVERFLOW | ERR_REC_OVERFLOW)) {
+        c->scan_ms += ms;
+        c->feed_ms += ms;
+        if (e & ERR_LINE_OVERFLOW) {
             HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
             HIPCHK(c, hipMemcpyAsync(c->d_pos, c->d_pos_saved, sizeof(StreamPos), hipMemcpyDeviceToDevice, s));
-            if (e & ERR_OVF_OVERFLOW) {
-                // nothing was resolved: plain redo with a larger overflow list
-                st = ensure_ovf(c, c->h_small[1] + 1024);
-                if (st) return st;
-                a.ovf = c->d_ovf;
-                h.ovf = c->d_ovf;
-                a.ovf_cap = c->ovf_cap;
-                h.ovf_cap = c->ovf_cap;
-            } else {
-                // dense table already holds this chunk: redo for the records only
-                st = ensure_records(c, c->h_small[0] + 1024);
-                if (st) return st;
-                h.recs = c->d_recs;
-                h.rec_cap = c->rec_cap;
-                h.dense_update = 0;
-            }
+            HIPCHK(c, c->lines.ensure(c->h_small[1] + 1024, s));
+            a.lines_out = c->lines.p;
+            a.line_cap = c->lines.cap;
             continue;
         }
         break;
     }
-    const uint64_t nrec = c->h_small[0];
+    const uint64_t nlines = c->h_small[1];
+    uint64_t nrec = 0;
+    if (nlines) {
+        WindowArgs w;
+        memset(&w, 0, sizeof(w));
+        w.data = d;
+        w.lines = c->lines.p;
+        w.n_lines = c->d_line_count;
+        w.k = c->p.k;
+        w.step = c->p.step;
+        w.plen = (uint32_t)c->prefix.size();
+        w.P = c->d_PR + 2 * KMAX_TILE;
+        w.err = c->d_err;
+        for (int attempt = 0; attempt < 8; ++attempt) {
+            w.recs = c->recs.p;
+            w.rec_count = c->d_rec_count;
+            w.rec_cap = c->recs.cap;
+            HIPCHK(c, hipMemsetAsync(c->d_rec_count, 0, 8, s));
+            HIPCHK(c, hipEventRecord(c->ev0, s));
+            HIPCHK(c, launch_windows(w, (uint32_t)std::min<uint64_t>(nlines, 65536), s));
+            HIPCHK(c, hipEventRecord(c->ev1, s));
+            HIPCHK(c, hipMemcpyAsync(c->h_small + 0, c->d_rec_count, 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipMemcpyAsync(c->h_small + 2, c->d_err, 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            const uint32_t e = (uint32_t)c->h_small[2];
+            st = check_err(c, e);
+            if (st) return st;
+            float ms = 0.f;
+            HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+            c->feed_ms += ms;
+            if (e & ERR_REC_OVERFLOW) {
+                HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
+                st = ensure_records(c, c->h_small[0] + 1024);
+                if (st) return st;
+                continue;
+            }
+            break;
+        }
+        nrec = c->h_small[0];
+    }
     if (nrec) {
         st = drain_records(c, d, nrec, s);
         if (st) return st;
@@ -396,230 +535,116 @@ kmer_status feed(kmer_ctx *c, const uint8_t *d, uint64_t len, hipStream_t s) {
     const uint32_t n_tiles = (uint32_t)n_tiles64;
     kmer_status st = ensure_tiles(c, n_tiles);
     if (st) return st;
-    if (c->mode != MODE_GENERAL) return scan_feed(c, d, len, n_tiles, s);
-    const bool lookback = !(c->p.flags & KMER_FLAG_TWO_PASS);
-
-    TileArgs a;
-    memset(&a, 0, sizeof(a));
-    a.data = d;
-    a.len = len;
-    a.n_tiles = n_tiles;
-    a.k = c->p.k;
-    a.plen = (uint32_t)c->prefix.size();
-    a.p4 = pack4(c->prefix);
-    a.r4 = pack4(c->rprefix);
-    a.pmask = a.plen >= 4 ? 0xFFFFFFFFu : ((1u << (8 * a.plen)) - 1u);
-    a.dense = c->mode == MODE_DENSE;
-    a.dense_update = 1;
-    a.abs_offset = c->abs_offset;
-    a.emit_lines = c->mode == MODE_GENERAL;
-    a.PR = c->d_PR;
-    a.counts = c->d_counts;
-    a.first = c->d_first;
-    a.recs = c->d_recs;
-    a.rec_count = c->d_rec_count;
-    a.rec_cap = c->rec_cap;
-    a.lines_out = c->d_lines;
-    a.line_count = c->d_line_count;
-    a.line_cap = c->line_cap;
-    a.lb_cnt = c->d_lb_cnt;
-    a.lb_lnl = c->d_lb_lnl;
-    a.ticket = c->d_ticket;
-    a.pos = c->d_pos;
-    a.tp_cnt = c->d_tp_cnt;
-    a.tp_lnl = c->d_tp_lnl;
-    a.err = c->d_err;
-
-    HIPCHK(c, hipMemcpyAsync(c->d_pos_saved, c->d_pos, sizeof(StreamPos), hipMemcpyDeviceToDevice, s));
-    for (int attempt = 0; attempt < 8; ++attempt) {
-        HIPCHK(c, hipMemsetAsync(c->d_lb_cnt, 0, n_tiles * 8ull, s));
-        HIPCHK(c, hipMemsetAsync(c->d_lb_lnl, 0, n_tiles * 8ull, s));
-        HIPCHK(c, hipMemsetAsync(c->d_ticket, 0, 16, s));
-        HIPCHK(c, hipMemsetAsync(c->d_rec_count, 0, 8, s));
-        HIPCHK(c, hipMemsetAsync(c->d_line_count, 0, 8, s));
-        if (!lookback) {
-            st = two_pass_prefix(c, d, len, n_tiles, s);
-            if (st) return st;
-        }
-        HIPCHK(c, hipEventRecord(c->ev0, s));
-        HIPCHK(c, launch_lines(a, lookback, s));
-        HIPCHK(c, hipEventRecord(c->ev1, s));
-        HIPCHK(c, hipMemcpyAsync(c->h_small + 0, c->d_rec_count, 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipMemcpyAsync(c->h_small + 1, c->d_line_count, 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipMemcpyAsync(c->h_small + 2, c->d_err, 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipStreamSynchronize(s));
-        const uint32_t e = (uint32_t)c->h_small[2];
-        st = check_err(c, e);
-        if (st) return st;
-        float ms = 0.f;
-        HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
-        c->count_ms += ms;
-        if (e & (ERR_REC_OVERFLOW | ERR_LINE_OVERFLOW)) {
-            // capacity exceeded: grow and redo the chunk from the saved position;
-            // the dense table already holds this chunk, so the redo skips it
-            HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
-            HIPCHK(c, hipMemcpyAsync(c->d_pos, c->d_pos_saved, sizeof(StreamPos), hipMemcpyDeviceToDevice, s));
-            if (e & ERR_REC_OVERFLOW) {
-                st = ensure_records(c, c->h_small[0] + 1024);
-                if (st) return st;
-                a.recs = c->d_recs;
-                a.rec_cap = c->rec_cap;
-                if (c->mode == MODE_DENSE) a.dense_update = 0;
-            }
-            if (e & ERR_LINE_OVERFLOW) {
-                st = ensure_lines(c, c->h_small[1] + 1024);
-                if (st) return st;
-                a.lines_out = c->d_lines;
-                a.line_cap = c->line_cap;
-            }
-            continue;
-        }
-        break;
-    }
-    uint64_t nrec = c->h_small[0];
-    if (c->mode == MODE_GENERAL) {
-        const uint64_t nlines = c->h_small[1];
-        if (nlines) {
-            WindowArgs w;
-            memset(&w, 0, sizeof(w));
-            w.data = d;
-            w.lines = c->d_lines;
-            w.n_lines = c->d_line_count;
-            w.k = c->p.k;
-            w.step = c->p.step;
-            w.plen = (uint32_t)c->prefix.size();
-            w.P = c->d_PR + 2 * KMAX_TILE;
-            w.err = c->d_err;
-            // upper bound on records: every window of every line on both strands
-            // is not known cheaply; start from the capacity and grow on overflow
-            for (int attempt = 0; attempt < 8; ++attempt) {
-                w.recs = c->d_recs;
-                w.rec_count = c->d_rec_count;
-                w.rec_cap = c->rec_cap;
-                HIPCHK(c, hipMemsetAsync(c->d_rec_count, 0, 8, s));
-                HIPCHK(c, hipEventRecord(c->ev0, s));
-                const uint32_t grid = (uint32_t)std::min<uint64_t>(nlines, 65536);
-                HIPCHK(c, launch_windows(w, grid, s));
-                HIPCHK(c, hipEventRecord(c->ev1, s));
-                HIPCHK(c, hipMemcpyAsync(c->h_small + 0, c->d_rec_count, 8, hipMemcpyDeviceToHost, s));
-                HIPCHK(c, hipMemcpyAsync(c->h_small + 2, c->d_err, 4, hipMemcpyDeviceToHost, s));
-                HIPCHK(c, hipStreamSynchronize(s));
-                const uint32_t e = (uint32_t)c->h_small[2];
-                st = check_err(c, e);
-                if (st) return st;
-                float ms = 0.f;
-                HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
-                c->count_ms += ms;
-                if (e & ERR_REC_OVERFLOW) {
-                    HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
-                    st = ensure_records(c, c->h_small[0] + 1024);
-                    if (st) return st;
-                    continue;
-                }
-                break;
-            }
-            nrec = c->h_small[0];
-        }
-    }
-    if (nrec) {
-        st = drain_records(c, d, nrec, s);
-        if (st) return st;
-    }
-    c->abs_offset += len;
-    return KMER_OK;
+    return c->mode == MODE_GENERAL ? general_feed(c, d, len, n_tiles, s) : scan_feed(c, d, len, n_tiles, s);
 }
 
 kmer_status reset(kmer_ctx *c) {
     hipStream_t s = c->stream;
-    if (c->mode == MODE_DENSE) {
-        HIPCHK(c, hipMemsetAsync(c->d_counts, 0, c->n_dense * 8, s));
-        HIPCHK(c, hipMemsetAsync(c->d_first, 0xFF, c->n_dense * 8, s));
-    }
     HIPCHK(c, hipMemsetAsync(c->d_pos, 0, sizeof(StreamPos), s));
     HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
     c->exotic.clear();
     c->abs_offset = 0;
-    c->count_ms = 0.0;
-    c->finish_ms = 0.0;
-    c->feed_ms = 0.0;
+    c->n_hits = 0;
+    c->n_out = 0;
+    c->scan_ms = c->feed_ms = c->finish_ms = 0.0;
     c->open_stream = true;
     return KMER_OK;
 }
 
-kmer_status finish(kmer_ctx *c, kmer_result **out) {
-    if (!c->open_stream) return fail(c, KMER_E_STATE, "finish without reset/feed");
+// ---------------------------------------------------------------------------
+// finish
+// ---------------------------------------------------------------------------
+// Sort (key, value) pairs by key and reduce equal keys (min first, sum count)
+// into c->ukey / c->uval; returns the unique count (sentinel group dropped).
+kmer_status reduce_pairs(kmer_ctx *c, uint64_t *keys, Agg *vals, uint64_t n, uint64_t *nu_out) {
     hipStream_t s = c->stream;
-    StreamPos pos;
-    HIPCHK(c, hipEventRecord(c->ev2, s));
-    uint64_t n = 0;
-    if (c->mode == MODE_DENSE) {
-        HIPCHK(c, hipMemsetAsync(c->d_nout, 0, 8, s));
-        HIPCHK(c, launch_dense_compact(c->d_counts, c->d_first, c->n_dense, c->d_order, c->d_idx, c->d_nout, s));
-        HIPCHK(c, hipMemcpyAsync(c->h_small + 3, c->d_nout, 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipMemcpyAsync(c->h_small + 4, c->d_pos, sizeof(StreamPos), hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipStreamSynchronize(s));
-        n = c->h_small[3];
-        memcpy(&pos, c->h_small + 4, sizeof(pos));
-        // sort by first-occurrence order; only the bits the orders can use
-        const uint64_t max_order = ((pos.lines + 1) << 24) | 0xFFFFFFull;
-        int end_bit = 64 - __builtin_clzll(max_order);
-        if (n) {
-            rocprim::double_buffer<uint64_t> keys(c->d_order, c->d_order2);
-            rocprim::double_buffer<uint64_t> vals(c->d_idx, c->d_idx2);
-            size_t tmp = c->sort_tmp_bytes;
-            HIPCHK(c, rocprim::radix_sort_pairs(c->d_sort_tmp, tmp, keys, vals, (size_t)n, 0, end_bit, s));
-            HIPCHK(c, launch_dense_decode(vals.current(), c->d_nout, n, c->p.k, (uint32_t)c->prefix.size(), c->d_P,
-                                          c->d_counts, c->d_keys_out, c->d_cnt_out, s));
-            if (keys.current() != c->d_order) {
-                HIPCHK(c, hipMemcpyAsync(c->d_order, keys.current(), n * 8, hipMemcpyDeviceToDevice, s));
-            }
-        }
-    } else {
-        HIPCHK(c, hipMemcpyAsync(c->h_small + 4, c->d_pos, sizeof(StreamPos), hipMemcpyDeviceToHost, s));
-    }
-    HIPCHK(c, hipEventRecord(c->ev3, s));
+    *nu_out = 0;
+    if (n == 0) return KMER_OK;
+    HIPCHK(c, c->hkey2.ensure(n, s));
+    HIPCHK(c, c->hval2.ensure(n, s));
+    HIPCHK(c, c->ukey.ensure(n, s));
+    HIPCHK(c, c->uval.ensure(n, s));
+    rocprim::double_buffer<uint64_t> kb(keys, c->hkey2.p);
+    rocprim::double_buffer<Agg> vb(vals, c->hval2.p);
+    const int end_bit = std::min<int>(64, (int)c->kbits + 1);   // + the invalid-key bit
+    ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, kb, vb, (size_t)n, 0, end_bit, s));
+    ROCPRIM_RUN(c, rocprim::reduce_by_key(t, b, kb.current(), vb.current(), (size_t)n, c->ukey.p, c->uval.p,
+                                          c->d_nuniq, AggMinSum(), rocprim::equal_to<uint64_t>(), s));
+    HIPCHK(c, hipMemcpyAsync(c->h_small + 5, c->d_nuniq, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
-    memcpy(&pos, c->h_small + 4, sizeof(pos));
-    float ms = 0.f;
-    HIPCHK(c, hipEventElapsedTime(&ms, c->ev2, c->ev3));
-    c->finish_ms = ms;
-    c->last_n = n;
-    c->open_stream = false;
+    uint64_t nu = c->h_small[5];
+    if (nu) {
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 6, c->ukey.p + nu - 1, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        const uint64_t invalid = c->kbits >= 63 ? ~0ull : (1ull << c->kbits);
+        if (c->h_small[6] == invalid) --nu;   // filtered-out / record hits
+    }
+    *nu_out = nu;
+    return KMER_OK;
+}
 
-    const uint64_t total = n + c->exotic.size();
-    if (c->p.max_keys && total > c->p.max_keys)
-        return fail(c, KMER_E_TOO_MANY_KEYS, "more distinct keys than max_keys (reference Map limit)");
-    if (!out) return KMER_OK;
+// unique entries -> first-occurrence order -> decoded keys (device)
+kmer_status order_and_decode(kmer_ctx *c, uint64_t nu, uint64_t max_line) {
+    hipStream_t s = c->stream;
+    c->n_out = nu;
+    if (nu == 0) return KMER_OK;
+    HIPCHK(c, c->first.ensure(nu, s));
+    HIPCHK(c, c->first2.ensure(nu, s));
+    HIPCHK(c, c->idx.ensure(nu, s));
+    HIPCHK(c, c->idx2.ensure(nu, s));
+    HIPCHK(c, c->keys_out.ensure(nu * c->p.k, s));
+    HIPCHK(c, c->cnt_out.ensure(nu, s));
+    HIPCHK(c, launch_split_first(c->uval.p, nu, c->first.p, c->idx.p, s));
+    const int end_bit = std::min(64, bit_width(((max_line + 1) << 24) | 0xFFFFFFull));
+    rocprim::double_buffer<uint64_t> kb(c->first.p, c->first2.p);
+    rocprim::double_buffer<uint64_t> vb(c->idx.p, c->idx2.p);
+    ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, kb, vb, (size_t)nu, 0, end_bit, s));
+    HIPCHK(c, launch_packed_decode(vb.current(), nu, c->ukey.p, c->uval.p, c->p.k, (uint32_t)c->prefix.size(),
+                                   c->d_P, c->keys_out.p, c->cnt_out.p, s));
+    if (kb.current() != c->first.p)
+        HIPCHK(c, hipMemcpyAsync(c->first.p, kb.current(), nu * 8, hipMemcpyDeviceToDevice, s));
+    return KMER_OK;
+}
 
+// ordered device entries + host records -> host result
+kmer_status build_result(kmer_ctx *c, uint64_t lines, kmer_result **out) {
     kmer_result *r = new (std::nothrow) kmer_result();
     if (!r) return fail(c, KMER_E_OOM, "host allocation failed");
-    r->lines = pos.lines + pos.ends_open;
-    const uint64_t k = c->p.k;
+    r->lines = lines;
+    const uint64_t n = c->n_out, k = c->p.k;
     std::vector<uint64_t> order(n), cnt(n);
     std::vector<char> dkeys(n * k);
     if (n) {
-        HIPCHK(c, hipMemcpy(order.data(), c->d_order, n * 8, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(cnt.data(), c->d_cnt_out, n * 8, hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(dkeys.data(), c->d_keys_out, n * k, hipMemcpyDeviceToHost));
+        hipStream_t s = c->stream;
+        if (hipMemcpyAsync(order.data(), c->first.p, n * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(cnt.data(), c->cnt_out.p, n * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(dkeys.data(), c->keys_out.p, n * k, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+            delete r;
+            return fail(c, KMER_E_DEVICE, "result copy failed");
+        }
     }
-    // records (exotic / general) sorted by first occurrence
     std::vector<std::pair<uint64_t, const std::pair<const std::string, Ent> *>> ex;
     ex.reserve(c->exotic.size());
     for (auto &kv : c->exotic) ex.emplace_back(kv.second.first, &kv);
     std::sort(ex.begin(), ex.end(), [](const auto &x, const auto &y) { return x.first < y.first; });
+    const uint64_t total = n + ex.size();
     r->keys.reserve(n * k + ex.size() * k);
     r->offsets.reserve(total + 1);
     r->counts.reserve(total);
+    r->firsts.reserve(total);
     uint64_t i = 0, j = 0;
     while (i < n || j < ex.size()) {
         if (j >= ex.size() || (i < n && order[i] < ex[j].first)) {
             r->keys.insert(r->keys.end(), dkeys.begin() + i * k, dkeys.begin() + (i + 1) * k);
             r->counts.push_back(cnt[i]);
+            r->firsts.push_back(order[i]);
             ++i;
         } else {
             const std::string &key = ex[j].second->first;
             r->keys.insert(r->keys.end(), key.begin(), key.end());
             r->counts.push_back(ex[j].second->second.count);
+            r->firsts.push_back(ex[j].first);
             ++j;
         }
         r->offsets.push_back(r->keys.size());
@@ -628,9 +653,44 @@ kmer_status finish(kmer_ctx *c, kmer_result **out) {
     return KMER_OK;
 }
 
+kmer_status read_pos(kmer_ctx *c, StreamPos *pos) {
+    HIPCHK(c, hipMemcpyAsync(c->h_small + 8, c->d_pos, sizeof(StreamPos), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    memcpy(pos, c->h_small + 8, sizeof(StreamPos));
+    return KMER_OK;
+}
+
+kmer_status finish(kmer_ctx *c, kmer_result **out) {
+    if (!c->open_stream) return fail(c, KMER_E_STATE, "finish without reset/feed");
+    StreamPos pos;
+    kmer_status st = read_pos(c, &pos);
+    if (st) return st;
+    HIPCHK(c, hipEventRecord(c->ev2, c->stream));
+    uint64_t nu = 0;
+    if (c->mode == MODE_PACKED) {
+        st = reduce_pairs(c, c->hkey.p, c->hval.p, c->n_hits, &nu);
+        if (st) return st;
+        st = order_and_decode(c, nu, pos.lines);
+        if (st) return st;
+    } else {
+        c->n_out = 0;
+    }
+    HIPCHK(c, hipEventRecord(c->ev3, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev2, c->ev3));
+    c->finish_ms = ms;
+    c->open_stream = false;
+    const uint64_t total = c->n_out + c->exotic.size();
+    if (c->p.max_keys && total > c->p.max_keys)
+        return fail(c, KMER_E_TOO_MANY_KEYS, "more distinct keys than max_keys (reference Map limit)");
+    if (!out) return KMER_OK;
+    return build_result(c, pos.lines + pos.ends_open, out);
+}
+
 // Feed host bytes through the device in batches cut at '\n' boundaries.
 kmer_status feed_host(kmer_ctx *c, const uint8_t *bytes, uint64_t len) {
-    uint64_t batch = c->p.batch_bytes ? c->p.batch_bytes : DEFAULT_BATCH;
+    const uint64_t batch = c->p.batch_bytes ? c->p.batch_bytes : DEFAULT_BATCH;
     uint64_t pos = 0;
     while (pos < len) {
         uint64_t end = std::min(len, pos + batch);
@@ -647,14 +707,9 @@ kmer_status feed_host(kmer_ctx *c, const uint8_t *bytes, uint64_t len) {
             }
         }
         const uint64_t n = end - pos;
-        if (n > c->batch_cap) {
-            HIPCHK(c, hipStreamSynchronize(c->stream));
-            dfree(c->d_batch);
-            HIPCHK(c, dalloc(&c->d_batch, n));
-            c->batch_cap = n;
-        }
-        HIPCHK(c, hipMemcpyAsync(c->d_batch, bytes + pos, n, hipMemcpyHostToDevice, c->stream));
-        kmer_status st = feed(c, c->d_batch, n, c->stream);
+        HIPCHK(c, c->batch.ensure(n, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->batch.p, bytes + pos, n, hipMemcpyHostToDevice, c->stream));
+        kmer_status st = feed(c, c->batch.p, n, c->stream);
         if (st) return st;
         pos = end;
     }
@@ -665,7 +720,7 @@ kmer_status feed_host(kmer_ctx *c, const uint8_t *bytes, uint64_t len) {
 
 extern "C" {
 
-const char *kmer_version(void) { return "kmerhip 0.1 (gfx950)"; }
+const char *kmer_version(void) { return "kmerhip 0.2 (gfx950)"; }
 
 const char *kmer_status_string(kmer_status s) {
     switch (s) {
@@ -687,9 +742,9 @@ const char *kmer_last_error(const kmer_ctx *ctx) { return ctx ? ctx->err.c_str()
 kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
     if (!pp || !out) return KMER_E_BAD_PARAM;
     if (pp->k == 0 || pp->step == 0 || (pp->prefix_len && !pp->prefix)) return KMER_E_BAD_PARAM;
+    *out = nullptr;
     kmer_ctx *c = new (std::nothrow) kmer_ctx();
     if (!c) return KMER_E_OOM;
-    *out = nullptr;
     c->p = *pp;
     c->prefix.assign((const char *)pp->prefix, pp->prefix_len);
     c->rprefix.resize(c->prefix.size());
@@ -712,37 +767,17 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
     const uint32_t k = pp->k, plen = (uint32_t)c->prefix.size();
     bool acgt = plen > 0;
     for (char ch : c->prefix) acgt &= ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T';
-    if (pp->step == 1 && acgt && plen <= k && k <= (uint32_t)KMAX_DENSE && k - plen <= (uint32_t)DENSE_MAX_SUFFIX &&
-        !(pp->flags & KMER_FLAG_NO_DENSE))
-        c->mode = MODE_DENSE;
+    if (pp->step == 1 && acgt && plen <= k && k <= (uint32_t)KMAX_DENSE && !(pp->flags & KMER_FLAG_NO_DENSE))
+        c->mode = MODE_PACKED;
     else if (pp->step == 1 && plen > 0 && k <= (uint32_t)KMAX_TILE)
         c->mode = MODE_TILE_REC;
     else
         c->mode = MODE_GENERAL;
+    c->kbits = c->mode == MODE_PACKED ? 2 * (k - plen) : 0;
 
     bool ok = true;
-    if (c->mode == MODE_DENSE) {
-        c->n_dense = 1ull << (2 * (k - plen));
-        ok &= dalloc(&c->d_counts, c->n_dense) == hipSuccess;
-        ok &= dalloc(&c->d_first, c->n_dense) == hipSuccess;
-        ok &= dalloc(&c->d_order, c->n_dense) == hipSuccess;
-        ok &= dalloc(&c->d_order2, c->n_dense) == hipSuccess;
-        ok &= dalloc(&c->d_idx, c->n_dense) == hipSuccess;
-        ok &= dalloc(&c->d_idx2, c->n_dense) == hipSuccess;
-        ok &= dalloc(&c->d_keys_out, c->n_dense * k) == hipSuccess;
-        ok &= dalloc(&c->d_cnt_out, c->n_dense) == hipSuccess;
-        ok &= dalloc(&c->d_P, std::max<uint32_t>(plen, 1)) == hipSuccess;
-        if (ok && plen) ok &= hipMemcpy(c->d_P, c->prefix.data(), plen, hipMemcpyHostToDevice) == hipSuccess;
-        if (ok) {
-            rocprim::double_buffer<uint64_t> keys(c->d_order, c->d_order2);
-            rocprim::double_buffer<uint64_t> vals(c->d_idx, c->d_idx2);
-            size_t tmp = 0;
-            ok &= rocprim::radix_sort_pairs(nullptr, tmp, keys, vals, (size_t)c->n_dense, 0, 64, c->stream) ==
-                  hipSuccess;
-            c->sort_tmp_bytes = tmp;
-            ok &= dalloc((uint8_t **)&c->d_sort_tmp, tmp) == hipSuccess;
-        }
-    }
+    ok &= dalloc(&c->d_P, std::max<uint32_t>(plen, 1)) == hipSuccess;
+    if (ok && plen) ok &= hipMemcpy(c->d_P, c->prefix.data(), plen, hipMemcpyHostToDevice) == hipSuccess;
     {
         // [0,64) P and [64,128) rc(P) (tile kernel, truncated), [128, 128+|P|) full P (general kernel)
         std::vector<uint8_t> pr(2 * KMAX_TILE + c->prefix.size(), 0);
@@ -756,18 +791,17 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
     ok &= dalloc(&c->d_err, 1) == hipSuccess;
     ok &= dalloc(&c->d_rec_count, 1) == hipSuccess;
     ok &= dalloc(&c->d_line_count, 1) == hipSuccess;
-    ok &= dalloc(&c->d_nout, 1) == hipSuccess;
+    ok &= dalloc(&c->d_ovf_count, 1) == hipSuccess;
+    ok &= dalloc(&c->d_nuniq, 1) == hipSuccess;
     ok &= dalloc(&c->d_pos, 1) == hipSuccess;
     ok &= dalloc(&c->d_pos_saved, 1) == hipSuccess;
     ok &= hipHostMalloc((void **)&c->h_small, 16 * sizeof(uint64_t), hipHostMallocDefault) == hipSuccess;
     ok &= hipEventCreate(&c->ev0) == hipSuccess && hipEventCreate(&c->ev1) == hipSuccess &&
           hipEventCreate(&c->ev2) == hipSuccess && hipEventCreate(&c->ev3) == hipSuccess &&
           hipEventCreate(&c->ev4) == hipSuccess;
-    ok &= dalloc(&c->d_ovf_count, 1) == hipSuccess;
     if (!ok) return cleanup(KMER_E_OOM);
-    if (ensure_records(c, 1 << 16) || ensure_lines(c, 1 << 16) || ensure_tiles(c, 1 << 12) ||
-        ensure_ovf(c, 1 << 16))
-        return cleanup(KMER_E_OOM);
+    if (ensure_records(c, 1 << 16) || ensure_tiles(c, 1 << 12)) return cleanup(KMER_E_OOM);
+    if (c->ovf.ensure(1 << 16, c->stream) != hipSuccess) return cleanup(KMER_E_OOM);
     if (hipMemset(c->d_err, 0, 4) != hipSuccess) return cleanup(KMER_E_DEVICE);
     if (reset(c) != KMER_OK) return cleanup(KMER_E_DEVICE);
     c->open_stream = false;
@@ -779,20 +813,27 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
 kmer_status kmer_close(kmer_ctx *c) {
     if (!c) return KMER_E_BAD_PARAM;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    dfree(c->d_counts); dfree(c->d_first);
-    dfree(c->d_lb_cnt); dfree(c->d_lb_lnl); dfree(c->d_tp_cnt); dfree(c->d_tp_lnl);
-    dfree(c->d_ticket); dfree(c->d_err); dfree(c->d_rec_count); dfree(c->d_line_count); dfree(c->d_nout);
-    dfree(c->d_pos); dfree(c->d_pos_saved);
-    dfree(c->d_recs); dfree(c->d_lines); dfree(c->d_rec_keys); dfree(c->d_rec_off);
-    dfree(c->d_order); dfree(c->d_order2); dfree(c->d_idx); dfree(c->d_idx2);
-    dfree(c->d_keys_out); dfree(c->d_cnt_out); dfree(c->d_P); dfree(c->d_PR);
-    if (c->d_sort_tmp) (void)hipFree(c->d_sort_tmp);
-    dfree(c->d_batch);
-    dfree(c->d_agg_cnt); dfree(c->d_agg_lnl); dfree(c->d_cscan); dfree(c->d_lnl_before);
-    dfree(c->d_tile_nhits); dfree(c->d_hits); dfree(c->d_ovf); dfree(c->d_ovf_count);
-    if (c->d_scan_tmp) (void)hipFree(c->d_scan_tmp);
+    for (auto *b : {&c->agg_cnt, &c->agg_lnl, &c->cscan, &c->lnl_before, &c->hscan, &c->tp_cnt, &c->tp_lnl,
+                    &c->hkey, &c->hkey2, &c->ukey, &c->first, &c->first2, &c->idx, &c->idx2, &c->cnt_out})
+        b->release();
+    c->tile_nhits.release();
+    c->hits.release();
+    c->ovf.release();
+    c->lb_cnt.release();
+    c->lb_lnl.release();
+    c->hval.release();
+    c->hval2.release();
+    c->uval.release();
+    c->keys_out.release();
+    c->recs.release();
+    c->lines.release();
+    c->rec_keys.release();
+    c->tmp.release();
+    c->batch.release();
+    dfree(c->d_ticket); dfree(c->d_err); dfree(c->d_rec_count); dfree(c->d_line_count);
+    dfree(c->d_ovf_count); dfree(c->d_nuniq); dfree(c->d_pos); dfree(c->d_pos_saved);
+    dfree(c->d_P); dfree(c->d_PR);
     if (c->h_small) (void)hipHostFree(c->h_small);
-    if (c->h_stage) (void)hipHostFree(c->h_stage);
     for (hipEvent_t e : {c->ev0, c->ev1, c->ev2, c->ev3, c->ev4})
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -810,8 +851,8 @@ kmer_status kmer_feed_device(kmer_ctx *c, const void *d_bytes, size_t len, void 
     if (!c || (!d_bytes && len)) return KMER_E_BAD_PARAM;
     if (!c->open_stream) return fail(c, KMER_E_STATE, "feed without reset");
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    if (s != c->stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (s && s != c->stream) {
         // order the context's own stream after the caller's work
         hipEvent_t ev;
         HIPCHK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -859,7 +900,7 @@ kmer_status kmer_count_file(kmer_ctx *c, const char *path, kmer_result **out) {
     bool eof = false;
     while (!st && !eof) {
         buf.resize(carry + batch);
-        size_t got = fread(buf.data() + carry, 1, batch, f);
+        const size_t got = fread(buf.data() + carry, 1, batch, f);
         if (got < batch) {
             if (ferror(f)) {
                 st = fail(c, KMER_E_IO, std::string("read error on ") + path);
@@ -867,7 +908,7 @@ kmer_status kmer_count_file(kmer_ctx *c, const char *path, kmer_result **out) {
             }
             eof = true;
         }
-        uint64_t have = carry + got;
+        const uint64_t have = carry + got;
         uint64_t cut = have;
         if (!eof) {
             while (cut > 0 && buf[cut - 1] != '\n') --cut;
@@ -888,12 +929,83 @@ kmer_status kmer_count_file(kmer_ctx *c, const char *path, kmer_result **out) {
     return finish(c, out);
 }
 
-kmer_status kmer_table_view(kmer_ctx *c, void **d_counts, void **d_first, uint64_t *n) {
-    if (!c || !d_counts || !d_first || !n) return KMER_E_BAD_PARAM;
-    if (c->mode != MODE_DENSE) return fail(c, KMER_E_STATE, "configuration does not use the dense table");
-    *d_counts = c->d_counts;
-    *d_first = c->d_first;
-    *n = c->n_dense;
+kmer_status kmer_partial_device(kmer_ctx *c, const void **d_keys, const void **d_vals, uint64_t *n) {
+    if (!c || !d_keys || !d_vals || !n) return KMER_E_BAD_PARAM;
+    if (c->mode != MODE_PACKED) return fail(c, KMER_E_STATE, "configuration has no packed keys");
+    if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
+    uint64_t nu = 0;
+    kmer_status st = reduce_pairs(c, c->hkey.p, c->hval.p, c->n_hits, &nu);
+    if (st) return st;
+    *d_keys = c->ukey.p;
+    *d_vals = c->uval.p;
+    *n = nu;
+    return KMER_OK;
+}
+
+kmer_status kmer_finish_merged(kmer_ctx *c, const void *d_keys, const void *d_vals, uint64_t n,
+                               uint64_t total_lines, kmer_result **out) {
+    if (!c || (n && (!d_keys || !d_vals))) return KMER_E_BAD_PARAM;
+    if (c->mode != MODE_PACKED) return fail(c, KMER_E_STATE, "configuration has no packed keys");
+    if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
+    if (out) *out = nullptr;
+    hipStream_t s = c->stream;
+    HIPCHK(c, hipEventRecord(c->ev2, s));
+    // private copies: the reduce sorts in place
+    HIPCHK(c, c->hkey.ensure(n, s));
+    HIPCHK(c, c->hval.ensure(n, s));
+    if (n) {
+        HIPCHK(c, hipMemcpyAsync(c->hkey.p, d_keys, n * 8, hipMemcpyDeviceToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->hval.p, d_vals, n * sizeof(Agg), hipMemcpyDeviceToDevice, s));
+    }
+    uint64_t nu = 0;
+    kmer_status st = reduce_pairs(c, c->hkey.p, c->hval.p, n, &nu);
+    if (st) return st;
+    st = order_and_decode(c, nu, total_lines);
+    if (st) return st;
+    HIPCHK(c, hipEventRecord(c->ev3, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev2, c->ev3));
+    c->finish_ms = ms;
+    c->n_hits = 0;
+    c->open_stream = false;
+    const uint64_t total = c->n_out + c->exotic.size();
+    if (c->p.max_keys && total > c->p.max_keys)
+        return fail(c, KMER_E_TOO_MANY_KEYS, "more distinct keys than max_keys (reference Map limit)");
+    if (!out) return KMER_OK;
+    return build_result(c, total_lines, out);
+}
+
+kmer_status kmer_records_export(kmer_ctx *c, kmer_result **out) {
+    if (!c || !out) return KMER_E_BAD_PARAM;
+    kmer_result *r = new (std::nothrow) kmer_result();
+    if (!r) return KMER_E_OOM;
+    std::vector<std::pair<uint64_t, const std::pair<const std::string, Ent> *>> ex;
+    for (auto &kv : c->exotic) ex.emplace_back(kv.second.first, &kv);
+    std::sort(ex.begin(), ex.end(), [](const auto &x, const auto &y) { return x.first < y.first; });
+    for (auto &e : ex) {
+        r->keys.insert(r->keys.end(), e.second->first.begin(), e.second->first.end());
+        r->offsets.push_back(r->keys.size());
+        r->counts.push_back(e.second->second.count);
+        r->firsts.push_back(e.first);
+    }
+    *out = r;
+    return KMER_OK;
+}
+
+kmer_status kmer_records_import(kmer_ctx *c, const char *keys, const uint64_t *offsets, const uint64_t *counts,
+                                const uint64_t *firsts, uint64_t n) {
+    if (!c || (n && (!keys || !offsets || !counts || !firsts))) return KMER_E_BAD_PARAM;
+    for (uint64_t i = 0; i < n; ++i) {
+        std::string key(keys + offsets[i], offsets[i + 1] - offsets[i]);
+        auto it = c->exotic.find(key);
+        if (it == c->exotic.end()) {
+            c->exotic.emplace(key, Ent{counts[i], firsts[i]});
+        } else {
+            it->second.count += counts[i];
+            it->second.first = std::min(it->second.first, firsts[i]);
+        }
+    }
     return KMER_OK;
 }
 
@@ -910,16 +1022,26 @@ kmer_status kmer_set_position(kmer_ctx *c, uint64_t lines_before, uint64_t byte_
 kmer_status kmer_lines(kmer_ctx *c, uint64_t *lines) {
     if (!c || !lines) return KMER_E_BAD_PARAM;
     StreamPos pos;
-    HIPCHK(c, hipMemcpyAsync(&pos, c->d_pos, sizeof(pos), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    kmer_status st = read_pos(c, &pos);
+    if (st) return st;
     *lines = pos.lines + pos.ends_open;
     return KMER_OK;
 }
 
-kmer_status kmer_last_timing(kmer_ctx *c, double *count_ms, double *feed_ms, double *finish_ms) {
+kmer_status kmer_result_device(kmer_ctx *c, const void **d_keys, const void **d_counts, const void **d_firsts,
+                               uint64_t *n) {
+    if (!c || !n) return KMER_E_BAD_PARAM;
+    if (d_keys) *d_keys = c->keys_out.p;
+    if (d_counts) *d_counts = c->cnt_out.p;
+    if (d_firsts) *d_firsts = c->first.p;
+    *n = c->n_out;
+    return KMER_OK;
+}
+
+kmer_status kmer_last_timing(kmer_ctx *c, double *scan_ms, double *feed_ms, double *finish_ms) {
     if (!c) return KMER_E_BAD_PARAM;
-    if (count_ms) *count_ms = c->count_ms;
-    if (feed_ms) *feed_ms = c->feed_ms > 0 ? c->feed_ms : c->count_ms;
+    if (scan_ms) *scan_ms = c->scan_ms;
+    if (feed_ms) *feed_ms = c->feed_ms;
     if (finish_ms) *finish_ms = c->finish_ms;
     return KMER_OK;
 }
@@ -949,6 +1071,12 @@ kmer_status kmer_result_arrays(const kmer_result *r, const char **keys, const ui
     if (keys) *keys = r->keys.data();
     if (offsets) *offsets = r->offsets.data();
     if (counts) *counts = r->counts.data();
+    return KMER_OK;
+}
+
+kmer_status kmer_result_firsts(const kmer_result *r, const uint64_t **firsts) {
+    if (!r || !firsts) return KMER_E_BAD_PARAM;
+    *firsts = r->firsts.data();
     return KMER_OK;
 }
 

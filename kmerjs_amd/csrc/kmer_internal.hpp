@@ -17,7 +17,6 @@ constexpr int FH = 64;                   // front halo bytes
 constexpr int BH = 80;                   // back halo bytes (>= KMAX_TILE - 1 + 3, x16)
 constexpr int KMAX_TILE = 64;            // longest k handled by the tile kernel
 constexpr int KMAX_DENSE = 32;           // longest k packed into 2-bit codes
-constexpr int DENSE_MAX_SUFFIX = 13;     // dense table = 4^(k-|P|) entries, |suffix| <= 13
 constexpr uint32_t MAXREL = (1u << 23) - 1;  // longest sequence line (bytes - 1)
 
 // error bits (device-side, OR-ed into ctx->d_err)
@@ -89,9 +88,16 @@ struct ScanArgs {
     uint32_t ablate;               // experiments only: bit0 = drop all candidates
 };
 
+// value of a packed hit / unique key: first-occurrence order and count
+struct Agg {
+    uint64_t first;
+    uint64_t count;
+};
+
 struct HitArgs {
     const HitRec *hits;
     const uint32_t *tile_nhits;
+    const uint64_t *hscan;         // exclusive scan of tile_nhits
     const HitRec *ovf;
     const unsigned long long *ovf_count;
     uint64_t ovf_cap;
@@ -100,11 +106,12 @@ struct HitArgs {
     const StreamPos *pos;
     const uint64_t *cscan;         // exclusive sum of agg_cnt
     const uint64_t *lnl_before;    // exclusive max of agg_lnl (init abs_offset)
-    uint32_t dense;
-    uint32_t dense_update;         // 0: records only (redo after a record overflow)
-    uint64_t smask;
-    unsigned long long *counts;
-    unsigned long long *first;
+    uint32_t packed;               // ACGT windows (k <= 32) go to the packed hit array
+    uint64_t smask;                // suffix mask: 2*(k - |P|) bits
+    uint64_t invalid_key;          // 2^(2*(k-|P|)): sorts after every real key
+    uint64_t *out_key;             // session hit array (NULL: records only)
+    Agg *out_val;
+    uint64_t out_base;             // session hits before this chunk
     Record *recs;
     unsigned long long *rec_count;
     uint64_t rec_cap;
@@ -165,12 +172,10 @@ hipError_t launch_pos_update(StreamPos *pos, const uint64_t *cscan, const uint64
 hipError_t launch_tile_aggregate(const uint8_t *data, uint64_t len, uint32_t n_tiles, uint64_t *agg_cnt,
                                  uint64_t *agg_lnl, unsigned int *err, hipStream_t s);
 hipError_t launch_windows(const WindowArgs &a, uint32_t grid, hipStream_t s);
-hipError_t launch_dense_compact(const unsigned long long *counts, const unsigned long long *first,
-                                uint64_t n, uint64_t *out_order, uint64_t *out_idx,
-                                unsigned long long *out_n, hipStream_t s);
-hipError_t launch_dense_decode(const uint64_t *idx_sorted, const unsigned long long *n, uint64_t cap,
-                               uint32_t k, uint32_t plen, const uint8_t *P, const unsigned long long *counts,
-                               uint8_t *keys_out, uint64_t *counts_out, hipStream_t s);
+hipError_t launch_split_first(const Agg *uval, uint64_t n, uint64_t *first, uint64_t *idx, hipStream_t s);
+hipError_t launch_packed_decode(const uint64_t *idx, uint64_t n, const uint64_t *ukey, const Agg *uval, uint32_t k,
+                                uint32_t plen, const uint8_t *P, uint8_t *keys_out, uint64_t *counts_out,
+                                hipStream_t s);
 hipError_t launch_gather_records(const Record *recs, const uint64_t *key_off, uint64_t n,
                                  const uint8_t *data, uint8_t *out, hipStream_t s);
 hipError_t launch_synth_fastq(uint8_t *out, uint64_t seed, uint64_t first_read, uint64_t n_reads,

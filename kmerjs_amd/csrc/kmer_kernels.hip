@@ -690,9 +690,11 @@ __global__ __launch_bounds__(TPB) void scan_tile_kernel(ScanArgs a) {
 
 
 // Resolve one hit: global line index / line start from the per-tile scans,
-// the reference's sequence-line rule, first-occurrence order, then the dense
-// table (count + atomicMin order) or a record for the host merge.
-__device__ __forceinline__ void resolve_hit(const HitArgs &a, const HitRec &r) {
+// the reference's sequence-line rule, first-occurrence order.  Packed (ACGT,
+// k <= 32) hits become one (suffix code, {order, 1}) pair at a fixed slot of
+// the session's hit array (idempotent: a re-run rewrites the same slot);
+// everything else becomes a record for the host merge.
+__device__ __forceinline__ void resolve_hit(const HitArgs &a, const HitRec &r, uint64_t slot) {
     const uint32_t t = r.tile;
     const uint32_t strand = (r.qm >> 14) & 1u;
     const bool exotic = (r.qm >> 15) & 1u;
@@ -701,50 +703,62 @@ __device__ __forceinline__ void resolve_hit(const HitArgs &a, const HitRec &r) {
     const int s0 = strand ? q + (int)a.plen - (int)a.k : q;
     const uint64_t tile_abs = a.abs_offset + (uint64_t)t * TILE;
     const uint64_t li = a.pos->lines + a.cscan[t] + r.c_local;
-    if ((li & 3) != 1) return;
-    const uint64_t lstart = lvalid ? tile_abs + r.lstart : a.lnl_before[t];
-    const uint64_t sabs = tile_abs + (uint64_t)(int64_t)s0;
-    const uint64_t rel = sabs - lstart;
-    if (rel > MAXREL) {
-        atomicOr(a.err, ERR_LINE_TOO_LONG);
-        return;
-    }
-    const uint64_t order = (li << 24) | ((uint64_t)strand << 23) | (strand ? (uint64_t)(MAXREL - rel) : rel);
-    if (a.dense && !exotic) {
-        if (a.dense_update) {
-            const uint64_t idx = (strand ? revcomp_code(r.code, a.k) : r.code) & a.smask;
-            atomicAdd(a.counts + idx, 1ull);
-            atomicMin(a.first + idx, (unsigned long long)order);
-        }
-    } else {
-        const unsigned long long n = atomicAdd(a.rec_count, 1ull);
-        if (n < a.rec_cap) {
-            Record rec;
-            rec.order = order;
-            rec.pos = (uint64_t)t * TILE + (uint64_t)(int64_t)s0;
-            rec.len = a.k;
-            rec.strand = strand;
-            a.recs[n] = rec;
+    uint64_t key = a.invalid_key;
+    Agg val;
+    val.first = ~0ull;
+    val.count = 0;
+    if ((li & 3) == 1) {
+        const uint64_t lstart = lvalid ? tile_abs + r.lstart : a.lnl_before[t];
+        const uint64_t sabs = tile_abs + (uint64_t)(int64_t)s0;
+        const uint64_t rel = sabs - lstart;
+        if (rel > MAXREL) {
+            atomicOr(a.err, ERR_LINE_TOO_LONG);
         } else {
-            atomicOr(a.err, ERR_REC_OVERFLOW);
+            const uint64_t order = (li << 24) | ((uint64_t)strand << 23) |
+                                   (strand ? (uint64_t)(MAXREL - rel) : rel);
+            if (a.packed && !exotic) {
+                key = (strand ? revcomp_code(r.code, a.k) : r.code) & a.smask;
+                val.first = order;
+                val.count = 1;
+            } else {
+                const unsigned long long n = atomicAdd(a.rec_count, 1ull);
+                if (n < a.rec_cap) {
+                    Record rec;
+                    rec.order = order;
+                    rec.pos = (uint64_t)t * TILE + (uint64_t)(int64_t)s0;
+                    rec.len = a.k;
+                    rec.strand = strand;
+                    a.recs[n] = rec;
+                } else {
+                    atomicOr(a.err, ERR_REC_OVERFLOW);
+                }
+            }
         }
+    }
+    if (a.out_key) {
+        a.out_key[slot] = key;
+        a.out_val[slot] = val;
     }
 }
 
-// one wave per tile: lane i resolves the tile's i-th hit
+// one wave per tile: lane i resolves the tile's i-th hit into slot
+// out_base + hscan[tile] + i (hscan = exclusive scan of the per-tile counts)
 __global__ __launch_bounds__(256) void hit_kernel(HitArgs a) {
     const uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (t >= a.n_tiles || *a.ovf_count > a.ovf_cap) return;   // overflowed scan: the host redoes the chunk
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t n = a.tile_nhits[t];
-    for (uint32_t h = lane; h < n; h += 64) resolve_hit(a, a.hits[(uint64_t)t * HMAX + h]);
+    const uint64_t base = a.out_base + a.hscan[t];
+    for (uint32_t h = lane; h < n; h += 64) resolve_hit(a, a.hits[(uint64_t)t * HMAX + h], base + h);
 }
 
+// hits that did not fit their tile's slots; they follow all tile hits
 __global__ __launch_bounds__(256) void hit_overflow_kernel(HitArgs a) {
     if (*a.ovf_count > a.ovf_cap) return;
     const uint64_t n = *a.ovf_count;
+    const uint64_t base = a.out_base + a.hscan[a.n_tiles - 1] + a.tile_nhits[a.n_tiles - 1];
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-        resolve_hit(a, a.ovf[i]);
+        resolve_hit(a, a.ovf[i], base + i);
 }
 
 // advance the running stream position past this chunk
@@ -842,76 +856,44 @@ __global__ __launch_bounds__(256) void windows_kernel(WindowArgs a) {
 // ---------------------------------------------------------------------------
 // result materialisation
 // ---------------------------------------------------------------------------
-// Nonzero entries of the dense table -> (first-occurrence order, index) pairs.
-// Each block owns one contiguous span: count, ONE global atomic per block,
-// then write (the output order is irrelevant: it is radix-sorted next).
-constexpr int COMPACT_SPAN = 16384;
-__global__ __launch_bounds__(256) void dense_compact_kernel(const unsigned long long *counts,
-                                                            const unsigned long long *first, uint64_t n,
-                                                            uint64_t *out_order, uint64_t *out_idx,
-                                                            unsigned long long *out_n) {
-    __shared__ uint32_t s_wcnt[4];
-    __shared__ unsigned long long s_base;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint64_t lo = (uint64_t)blockIdx.x * COMPACT_SPAN;
-    const uint64_t hi = lo + COMPACT_SPAN < n ? lo + COMPACT_SPAN : n;
-    // pass 1: count (each wave owns a quarter of the span)
-    const uint64_t wlo = lo + (uint64_t)wid * (COMPACT_SPAN / 4);
-    const uint64_t whi = wlo + COMPACT_SPAN / 4 < hi ? wlo + COMPACT_SPAN / 4 : hi;
-    uint32_t c = 0;
-    for (uint64_t b = wlo; b < whi; b += 64) {
-        const uint64_t i = b + lane;
-        const bool pred = i < whi && counts[i] != 0;
-        c += __popcll(__ballot(pred));
-    }
-    if (lane == 0) s_wcnt[wid] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) s_base = atomicAdd(out_n, (unsigned long long)(s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3]));
-    __syncthreads();
-    uint64_t base = s_base;
-    for (int w = 0; w < wid; ++w) base += s_wcnt[w];
-    // pass 2: write
-    for (uint64_t b = wlo; b < whi; b += 64) {
-        const uint64_t i = b + lane;
-        const bool pred = i < whi && counts[i] != 0;
-        const unsigned long long m = __ballot(pred);
-        if (pred) {
-            const uint64_t o = base + __popcll(m & ((1ull << lane) - 1ull));
-            out_order[o] = first[i];
-            out_idx[o] = i;
-        }
-        base += __popcll(m);
+// unique (key, {first, count}) -> (first, index) for the order sort
+__global__ __launch_bounds__(256) void split_first_kernel(const Agg *uval, uint64_t n, uint64_t *first,
+                                                          uint64_t *idx) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        first[i] = uval[i].first;
+        idx[i] = i;
     }
 }
 
-// key = P + decode(idx) (k bytes), count gathered from the table.  One lane
-// per 4 output bytes so consecutive lanes write consecutive words.
-__global__ __launch_bounds__(256) void dense_decode_kernel(const uint64_t *idx_sorted,
-                                                           const unsigned long long *n_ptr, uint32_t k,
-                                                           uint32_t plen, const uint8_t *P,
-                                                           const unsigned long long *counts,
-                                                           uint8_t *keys_out, uint64_t *counts_out) {
-    const uint64_t n = *n_ptr;
+// Ordered output: entry i = unique entry idx[i]; key bytes = P + decode(code)
+// (k bytes, first base most significant), count.  One thread per entry; the
+// key is built in registers and written with dword stores when k % 4 == 0.
+__global__ __launch_bounds__(256) void packed_decode_kernel(const uint64_t *idx, uint64_t n, const uint64_t *ukey,
+                                                            const Agg *uval, uint32_t k, uint32_t plen,
+                                                            const uint8_t *P, uint8_t *keys_out,
+                                                            uint64_t *counts_out) {
     const uint32_t sl = k - plen;
-    const uint64_t words = (n * k + 3) / 4;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t wi = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; wi < words; wi += stride) {
-        uint32_t v = 0;
-        for (int b = 0; b < 4; ++b) {
-            const uint64_t o = wi * 4 + b;
-            if (o >= n * k) break;
-            const uint64_t e = o / k;
-            const uint32_t j = (uint32_t)(o - e * k);
-            uint32_t ch;
-            if (j < plen) ch = P[j];
-            else ch = (uint8_t)"ACGT"[(idx_sorted[e] >> (2 * (sl - 1 - (j - plen)))) & 3u];
-            v |= ch << (8 * b);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t e = idx[i];
+        const uint64_t code = ukey[e];
+        counts_out[i] = uval[e].count;
+        uint8_t *o = keys_out + i * k;
+        if ((k & 3) == 0) {
+            for (uint32_t b = 0; b < k; b += 4) {
+                uint32_t wv = 0;
+                for (uint32_t j = 0; j < 4; ++j) {
+                    const uint32_t pos = b + j;
+                    const uint32_t ch = pos < plen ? P[pos]
+                                                   : (uint32_t)(uint8_t)"ACGT"[(code >> (2 * (sl - 1 - (pos - plen)))) & 3u];
+                    wv |= ch << (8 * j);
+                }
+                *(uint32_t *)(o + b) = wv;
+            }
+        } else {
+            for (uint32_t pos = 0; pos < k; ++pos)
+                o[pos] = pos < plen ? P[pos] : (uint8_t)"ACGT"[(code >> (2 * (sl - 1 - (pos - plen)))) & 3u];
         }
-        if (wi * 4 + 4 <= n * k) *(uint32_t *)(keys_out + wi * 4) = v;
-        else for (int b = 0; wi * 4 + b < n * k; ++b) keys_out[wi * 4 + b] = (uint8_t)(v >> (8 * b));
     }
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-        counts_out[i] = counts[idx_sorted[i]];
 }
 
 __global__ __launch_bounds__(256) void gather_records_kernel(const Record *recs, const uint64_t *key_off,
@@ -1019,24 +1001,22 @@ hipError_t launch_windows(const WindowArgs &a, uint32_t grid, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_dense_compact(const unsigned long long *counts, const unsigned long long *first, uint64_t n,
-                                uint64_t *out_order, uint64_t *out_idx, unsigned long long *out_n,
-                                hipStream_t s) {
-    uint64_t blocks = (n + COMPACT_SPAN - 1) / COMPACT_SPAN;
-    if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL(dense_compact_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, counts, first, n, out_order,
-                       out_idx, out_n);
+static uint32_t grid_for(uint64_t n) {
+    uint64_t blocks = (n + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    return (uint32_t)(blocks ? blocks : 1);
+}
+
+hipError_t launch_split_first(const Agg *uval, uint64_t n, uint64_t *first, uint64_t *idx, hipStream_t s) {
+    hipLaunchKernelGGL(split_first_kernel, dim3(grid_for(n)), dim3(256), 0, s, uval, n, first, idx);
     return hipGetLastError();
 }
 
-hipError_t launch_dense_decode(const uint64_t *idx_sorted, const unsigned long long *n, uint64_t cap, uint32_t k,
-                               uint32_t plen, const uint8_t *P, const unsigned long long *counts,
-                               uint8_t *keys_out, uint64_t *counts_out, hipStream_t s) {
-    uint64_t blocks = (cap + 255) / 256;
-    if (blocks > 8192) blocks = 8192;
-    if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL(dense_decode_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, idx_sorted, n, k, plen, P,
-                       counts, keys_out, counts_out);
+hipError_t launch_packed_decode(const uint64_t *idx, uint64_t n, const uint64_t *ukey, const Agg *uval, uint32_t k,
+                                uint32_t plen, const uint8_t *P, uint8_t *keys_out, uint64_t *counts_out,
+                                hipStream_t s) {
+    hipLaunchKernelGGL(packed_decode_kernel, dim3(grid_for(n)), dim3(256), 0, s, idx, n, ukey, uval, k, plen, P,
+                       keys_out, counts_out);
     return hipGetLastError();
 }
 

@@ -1,12 +1,14 @@
 """Multi-GPU sharding of the k-mer count (one process per GPU).
 
 Reads are independent units (lib/kmers.js:151-155), so an input is split into
-per-rank shards at record boundaries; each rank counts its shard into its own
-dense table with the global line index / byte offset of its first line
-(kmer_set_position), and the only exchange is one merge of the tables: an
-RCCL reduce over xGMI, SUM for counts and MIN for first-occurrence orders
-(SURVEY.md §8e).  Record (non-ACGT) keys are merged on the host with a small
-object gather.
+per-rank shards at record boundaries; each rank counts its shard with the
+global line index / byte offset of its first line (kmer_set_position), which
+makes first-occurrence order keys comparable across ranks.  The only exchange
+is one gather of the per-rank partial results to rank 0 (RCCL over xGMI):
+unique packed keys + {first, count} pairs, padded to the largest rank with the
+invalid key (which the merged reduce drops), followed by one reduce/order/
+decode on rank 0 (kmer_finish_merged).  Record (non-ACGT) keys
+are merged on the host with a small object gather.
 """
 import torch
 import torch.distributed as dist
@@ -21,6 +23,7 @@ class _CudaArray:
 
 
 def device_u64(ptr, n, device):
+    """int64 view (uint64 bits) of n words of device memory owned by the library."""
     t = torch.as_tensor(_CudaArray(ptr, n), device=device)
     assert t.data_ptr() == ptr
     return t.view(torch.int64)
@@ -56,16 +59,74 @@ def split_at_records(buf: bytes, world):
     return out
 
 
-def merge_dense_tables(counts: torch.Tensor, first: torch.Tensor, dst=0, group=None):
-    """In-place reduce of per-rank dense tables to rank `dst`.
+def invalid_key(k, plen):
+    """Packed-key sentinel of the device reduce: 1 << 2(k-|P|) (kmer_api.hip)."""
+    return 1 << (2 * (k - plen))
 
-    counts: int64 (uint64 bits) counts, SUM.  first: first-occurrence orders
-    as uint64 bits, MIN.  Orders are < 2^63 and the empty value is
-    0xFFFF_FFFF_FFFF_FFFF (-1 as int64), so MIN on int64 would pick the empty
-    marker; flip to order-preserving signed form (x ^ 2^63) around the reduce.
+
+def gather_partials(keys, vals, pad_key, dst=0, group=None):
+    """Gather variable-length partials (keys int64[n], vals int64[n, 2]) to `dst`.
+
+    Every rank pads to the largest n with (pad_key, {first=-1, count=0}); the
+    padding sorts into the sentinel group that the merged reduce drops.
+    Returns the concatenated (keys, vals) on dst, (None, None) elsewhere.
     """
-    sign = torch.tensor(-(1 << 63), dtype=torch.int64, device=first.device)
-    first.bitwise_xor_(sign)
-    dist.reduce(counts, dst, op=dist.ReduceOp.SUM, group=group)
-    dist.reduce(first, dst, op=dist.ReduceOp.MIN, group=group)
-    first.bitwise_xor_(sign)
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = keys.device
+    n = torch.tensor([keys.numel()], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    maxn = max(int(x.item()) for x in sizes)
+    if maxn == 0:
+        return (keys[:0], vals[:0]) if rank == dst else (None, None)
+    kp = torch.full((maxn,), pad_key, dtype=torch.int64, device=dev)
+    vp = torch.empty((maxn, 2), dtype=torch.int64, device=dev)
+    vp[:, 0] = -1
+    vp[:, 1] = 0
+    kp[:keys.numel()] = keys
+    vp[:keys.numel()] = vals
+    if rank == dst:
+        kl = [torch.empty_like(kp) for _ in range(world)]
+        vl = [torch.empty_like(vp) for _ in range(world)]
+        dist.gather(kp, kl, dst=dst, group=group)
+        dist.gather(vp, vl, dst=dst, group=group)
+        return torch.cat(kl), torch.cat(vl)
+    dist.gather(kp, None, dst=dst, group=group)
+    dist.gather(vp, None, dst=dst, group=group)
+    return None, None
+
+
+def gather_records(ctr, dst=0, group=None):
+    """Move every rank's host record keys (non-ACGT windows) into rank dst's context."""
+    rank = dist.get_rank(group)
+    mine = ctr.records_export()
+    payload = (mine[0], mine[1].tolist(), mine[2].tolist(), mine[3].tolist())
+    got = [None] * dist.get_world_size(group) if rank == dst else None
+    dist.gather_object(payload, got, dst=dst, group=group)
+    if rank == dst:
+        import numpy as np
+        for r, (kb, off, cnt, fst) in enumerate(got):
+            if r != dst and cnt:
+                ctr.records_import(kb, np.array(off, dtype=np.uint64), np.array(cnt, dtype=np.uint64),
+                                   np.array(fst, dtype=np.uint64))
+
+
+def merge_to(ctr, k, plen, total_lines, dst=0, group=None, want_result=True, records=True):
+    """Finish a sharded count: gather every rank's partial to `dst` and finish there.
+
+    ctr: kmerjs_amd.Counter that has fed this rank's shard.  Returns the merged
+    ordered Result on dst (None elsewhere or when want_result is False).
+    """
+    d_k, d_v, n = ctr.partial_device()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    keys = device_u64(d_k, n, dev) if n else torch.empty(0, dtype=torch.int64, device=dev)
+    vals = device_u64(d_v, 2 * n, dev).view(n, 2) if n else torch.empty((0, 2), dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    gk, gv = gather_partials(keys, vals, invalid_key(k, plen), dst=dst, group=group)
+    if records:
+        gather_records(ctr, dst=dst, group=group)
+    if dist.get_rank(group) != dst:
+        return None
+    torch.cuda.synchronize()
+    return ctr.finish_merged(gk.data_ptr(), gv.data_ptr(), gk.numel(), total_lines, want_result=want_result)

@@ -1,0 +1,111 @@
+"""Multi-rank exchange on CPU (gloo, world_size 2): the collective layer of the
+multi-GPU path (kmerjs_amd/multi.py) without a GPU.  The device reduce that
+consumes the gathered partials is covered by the GPU sharded-merge tests."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from kmerjs_amd import multi
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class _FakeCounter:
+    """Stands in for Counter's record export/import (host-side record keys)."""
+
+    def __init__(self, recs):
+        self.recs = dict(recs)
+
+    def records_export(self):
+        items = sorted(self.recs.items(), key=lambda kv: kv[1][1])
+        kb = b"".join(k for k, _ in items)
+        off = np.cumsum([0] + [len(k) for k, _ in items]).astype(np.uint64)
+        return kb, off, np.array([v[0] for _, v in items], dtype=np.uint64), \
+            np.array([v[1] for _, v in items], dtype=np.uint64)
+
+    def records_import(self, kb, off, cnt, fst):
+        for i in range(len(cnt)):
+            key = kb[int(off[i]):int(off[i + 1])]
+            c, f = self.recs.get(key, (0, 1 << 63))
+            self.recs[key] = (c + int(cnt[i]), min(f, int(fst[i])))
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = [5, 0, 3][rank]
+        keys = torch.arange(n, dtype=torch.int64) + 100 * rank
+        vals = torch.stack([keys * 10, torch.ones(n, dtype=torch.int64)], dim=1) if n else \
+            torch.empty((0, 2), dtype=torch.int64)
+        gk, gv = multi.gather_partials(keys, vals, pad_key=1 << 22, dst=0)
+        ctr = _FakeCounter({b"NNA": (rank + 1, 7 + rank), (b"X%d" % rank): (1, rank)})
+        multi.gather_records(ctr, dst=0)
+        if rank == 0:
+            q.put(("ok", gk.tolist(), gv.tolist(), sorted(ctr.recs.items())))
+    except Exception as e:  # pragma: no cover - surfaced through the queue
+        q.put(("err", repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_partials_and_records_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    status, *payload = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+    assert status == "ok", payload
+    gk, gv, recs = payload
+    sizes = [5, 0, 3][:world]
+    maxn = max(sizes)
+    assert len(gk) == world * maxn and len(gv) == world * maxn
+    for r, n in enumerate(sizes):
+        blk = gk[r * maxn:(r + 1) * maxn]
+        assert blk[:n] == [100 * r + i for i in range(n)]
+        assert all(x == 1 << 22 for x in blk[n:])          # pad key -> dropped by the device reduce
+        vb = gv[r * maxn:(r + 1) * maxn]
+        assert all(v == [-1, 0] for v in vb[n:])           # pad value: count 0
+        assert vb[:n] == [[(100 * r + i) * 10, 1] for i in range(n)]
+    recs = dict(recs)
+    assert recs[b"NNA"] == (sum(range(1, world + 1)), 7)  # counts add, first = min
+    for r in range(world):
+        assert recs[b"X%d" % r] == (1, r)
+
+
+def test_split_at_records_covers_input():
+    from oracle import oracle
+    data = oracle.synth_fastq(3, 0, 101)
+    for world in (1, 2, 3, 8):
+        shards = multi.split_at_records(data, world)
+        assert b"".join(data[lo:hi] for lo, hi, _ in shards) == data
+        for lo, hi, lines_before in shards:
+            assert data[:lo].count(b"\n") == lines_before
+            assert lines_before % 4 == 0
+            assert lo == 0 or data[lo - 1:lo] == b"\n"
+
+
+def test_shard_plan_positions():
+    p = multi.shard_plan(1000, 3)
+    assert p == {"first_read": 3000, "lines_before": 12000, "byte_offset": 3000 * 317, "n_reads": 1000}
+
+
+def test_invalid_key_is_past_every_suffix():
+    assert multi.invalid_key(16, 5) == 1 << 22
+    assert multi.invalid_key(5, 5) == 1

@@ -147,3 +147,109 @@ def test_determinism_and_repeat(native, inputs):
     b = ctr.count_buffer(inputs["test_long.kmer.fastq"]).entries()
     ctr.close()
     assert a == b and len(a) == 401
+
+
+def _shard_and_merge(native, data, k, prefix, world, batch_bytes=0):
+    """Count `data` as `world` record-aligned shards (one context each, as one
+    rank each would) and merge the partials in context 0 (multi.merge_to's
+    exchange, done in-process)."""
+    import torch
+    from kmerjs_amd.multi import device_u64, invalid_key, split_at_records
+    shards = split_at_records(data, world)
+    ctrs = [native.Counter(k=k, prefix=prefix, batch_bytes=batch_bytes) for _ in range(world)]
+    try:
+        keys, vals, recs = [], [], []
+        total_lines = 0
+        for ctr, (lo, hi, lines_before) in zip(ctrs, shards):
+            ctr.reset()
+            ctr.set_position(lines_before, lo)
+            part = data[lo:hi]
+            if part:
+                t = torch.frombuffer(bytearray(part), dtype=torch.uint8).cuda()
+                ctr.feed_device(t.data_ptr(), len(part))
+                torch.cuda.synchronize()
+            total_lines = max(total_lines, ctr.lines())
+            d_k, d_v, n = ctr.partial_device()
+            if n:
+                keys.append(device_u64(d_k, n, torch.device("cuda")).clone())
+                vals.append(device_u64(d_v, 2 * n, torch.device("cuda")).view(n, 2).clone())
+            recs.append(ctr.records_export())
+        # pad like gather_partials does
+        pad = torch.full((7,), invalid_key(k, len(prefix)), dtype=torch.int64, device="cuda")
+        padv = torch.tensor([[-1, 0]] * 7, dtype=torch.int64, device="cuda")
+        gk = torch.cat(keys + [pad])
+        gv = torch.cat(vals + [padv])
+        for r in recs[1:]:
+            ctrs[0].records_import(*r)
+        torch.cuda.synchronize()
+        return ctrs[0].finish_merged(gk.data_ptr(), gv.data_ptr(), gk.numel(), total_lines)
+    finally:
+        for c in ctrs:
+            c.close()
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_sharded_merge_matches_oracle(native, world):
+    # multi-GPU exchange (SURVEY.md §8e): per-shard partials + merged finish == whole count
+    from oracle import oracle
+    rng = np.random.default_rng(world)
+    arr = np.frombuffer(bytearray(oracle.synth_fastq(7, 0, 30000)), dtype=np.uint8).reshape(-1, 317).copy()
+    seq = arr[:, 13:163]
+    seq[rng.random(seq.shape) < 0.002] = ord("N")
+    arr[:, 13:163] = seq
+    data = arr.tobytes()
+    for k, p in ((16, b"ATGAC"), (13, b"AC"), (32, b"ATGAC")):
+        want = oracle.count_buffer(data, p, k, 1)
+        r = _shard_and_merge(native, data, k, p, world)
+        assert r.lines == 4 * 30000
+        assert first_diff(r.entries(), want) is None, (world, k, p)
+
+
+def test_full_size_properties(native):
+    # BASELINE configs[1] size (10 M reads, 3.17 GB): properties that need no oracle
+    import torch
+    from kmerjs_amd import synth_fastq_device
+    n = 10_000_000
+    k, prefix = 16, b"ATGAC"
+    buf = torch.empty(n * 317, dtype=torch.uint8, device="cuda")
+    synth_fastq_device(buf.data_ptr(), 1, 0, n)
+    torch.cuda.synchronize()
+    ctr = native.Counter(k=k, prefix=prefix)
+    ctr.reset()
+    ctr.feed_device(buf.data_ptr(), buf.numel())
+    res = ctr.finish()
+    assert res.lines == 4 * n
+    # accepted windows counted independently: forward windows start with P, reverse-strand
+    # windows end (in forward coordinates) with rc(P) at q >= k - |P|
+    seq = buf.view(n, 317)[:, 13:163]
+    fwd = torch.ones((n, 150 - 5 + 1), dtype=torch.bool, device="cuda")
+    rev = torch.ones_like(fwd)
+    for i in range(5):
+        fwd &= seq[:, i:146 + i] == prefix[i]
+        rev &= seq[:, i:146 + i] == b"GTCAT"[i]
+    accepted = int(fwd[:, :150 - k + 1].sum()) + int(rev[:, k - 5:].sum())
+    del fwd, rev
+    assert int(res.counts.sum()) == accepted
+    assert len(set(res.keys())) == len(res)
+    assert all(key.startswith(prefix) for key in res.keys()[:100000])
+    f = res.firsts.astype(np.uint64)
+    assert bool(np.all(f[1:] > f[:-1]))
+    # sharded (4 ranks' worth) + merged finish reproduces the whole result
+    from kmerjs_amd.multi import device_u64, invalid_key
+    per = n // 4
+    keys, vals = [], []
+    for r in range(4):
+        ctr.reset()
+        ctr.set_position(4 * per * r, 317 * per * r)
+        ctr.feed_device(buf.data_ptr() + 317 * per * r, 317 * per)
+        d_k, d_v, m = ctr.partial_device()
+        keys.append(device_u64(d_k, m, torch.device("cuda")).clone())
+        vals.append(device_u64(d_v, 2 * m, torch.device("cuda")).view(m, 2).clone())
+    del buf
+    gk, gv = torch.cat(keys), torch.cat(vals)
+    merged = ctr.finish_merged(gk.data_ptr(), gv.data_ptr(), gk.numel(), 4 * n)
+    ctr.close()
+    assert merged.lines == res.lines
+    assert np.array_equal(merged.counts, res.counts)
+    assert np.array_equal(merged.firsts, res.firsts)
+    assert merged.keybuf == res.keybuf
