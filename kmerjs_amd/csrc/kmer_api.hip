@@ -17,8 +17,8 @@
 // look-back over tiles) + one-workgroup-per-line window kernel -> records.
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_reduce_by_key.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -39,15 +39,6 @@ enum Mode { MODE_PACKED, MODE_TILE_REC, MODE_GENERAL };
 struct Ent {
     uint64_t count;
     uint64_t first;
-};
-
-struct AggMinSum {
-    __host__ __device__ Agg operator()(const Agg &x, const Agg &y) const {
-        Agg r;
-        r.first = x.first < y.first ? x.first : y.first;
-        r.count = x.count + y.count;
-        return r;
-    }
 };
 
 // growable device array; `keep` preserves the first `used` elements on growth
@@ -103,15 +94,21 @@ struct kmer_ctx {
 
     // per tile
     uint64_t tile_cap = 0;
-    DBuf<uint64_t> agg_cnt, agg_lnl, cscan, lnl_before, hscan;
-    DBuf<uint32_t> tile_nhits;
+    DBuf<TileSum> tsum, tscan;
     DBuf<HitRec> hits, ovf;
     DBuf<unsigned long long> lb_cnt, lb_lnl;   // general path look-back
     DBuf<uint64_t> tp_cnt, tp_lnl;             // general path, two-pass debug mode
-    // session packed hits and finish buffers
-    uint64_t n_hits = 0;
-    DBuf<uint64_t> hkey, hkey2, ukey, first, first2, idx, idx2, cnt_out;
-    DBuf<Agg> hval, hval2, uval;
+    // session packed hits, by rank (first-occurrence order of all hits)
+    uint64_t n_hits = 0, n_cross = 0;
+    DBuf<uint64_t> rkey, rkey2, rord, rcnt;
+    DBuf<uint32_t> ridx, ridx2, opos;
+    DBuf<HeadRec> hrec;
+    bool long_seg = false;         // INFO_LONGSEG seen this session
+    DBuf<uint64_t> xord, xord2, xkey, xkey2;   // cross list
+    DBuf<uint32_t> xslot;
+    // finish outputs
+    DBuf<uint64_t> ukey, first, cnt_out, roff;
+    DBuf<Agg> uval;
     DBuf<uint8_t> keys_out;
     uint64_t n_out = 0;            // ordered entries of the last finish (device)
     // records & lines
@@ -120,8 +117,13 @@ struct kmer_ctx {
     DBuf<uint8_t> rec_keys;
     // scratch
     DBuf<uint8_t> tmp;
+    // device scalars, one block so that a feed reads them back with one copy:
+    // [0] rec_count [1] ovf_count [2] cross count [3] chunk hits [4] unique keys
+    // [5] err (u32) [6] line count
+    uint64_t *d_scal = nullptr;
     unsigned int *d_ticket = nullptr, *d_err = nullptr;
     unsigned long long *d_rec_count = nullptr, *d_line_count = nullptr, *d_ovf_count = nullptr;
+    unsigned long long *d_xcount = nullptr, *d_chunk_hits = nullptr;
     uint64_t *d_nuniq = nullptr;
     StreamPos *d_pos = nullptr, *d_pos_saved = nullptr;
     uint8_t *d_P = nullptr;        // prefix bytes (decode)
@@ -130,8 +132,7 @@ struct kmer_ctx {
     uint64_t abs_offset = 0;
     bool open_stream = false;      // reset called, not finished
     std::unordered_map<std::string, Ent> exotic;
-    uint64_t *h_small = nullptr;   // pinned: [0] rec_count [1] ovf/line count [2] err [3] hscan last
-                                   //         [4] nhits last [5] nuniq [6] last key [8..11] pos
+    uint64_t *h_small = nullptr;   // pinned: [0..7] copy of d_scal, [8..11] pos
     DBuf<uint8_t> batch;
     // timing (HIP events on the context stream)
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr;
@@ -207,12 +208,8 @@ kmer_status ensure_tiles(kmer_ctx *c, uint64_t n_tiles) {
         HIPCHK(c, c->tp_cnt.ensure(cap, s));
         HIPCHK(c, c->tp_lnl.ensure(cap, s));
     } else {
-        HIPCHK(c, c->agg_cnt.ensure(cap, s));
-        HIPCHK(c, c->agg_lnl.ensure(cap, s));
-        HIPCHK(c, c->cscan.ensure(cap, s));
-        HIPCHK(c, c->lnl_before.ensure(cap, s));
-        HIPCHK(c, c->hscan.ensure(cap, s));
-        HIPCHK(c, c->tile_nhits.ensure(cap, s));
+        HIPCHK(c, c->tsum.ensure(cap, s));
+        HIPCHK(c, c->tscan.ensure(cap, s));
         HIPCHK(c, c->hits.ensure(cap * HMAX, s));
     }
     c->tile_cap = cap;
@@ -233,11 +230,11 @@ kmer_status drain_records(kmer_ctx *c, const uint8_t *d_data, uint64_t n, hipStr
     const uint64_t k = c->p.k;
     kmer_status st = ensure_records(c, n);
     if (st) return st;
-    HIPCHK(c, c->idx.ensure(n, s));
+    HIPCHK(c, c->roff.ensure(n, s));
     std::vector<uint64_t> off(n);
     for (uint64_t i = 0; i < n; ++i) off[i] = i * k;
-    HIPCHK(c, hipMemcpyAsync(c->idx.p, off.data(), n * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(c, launch_gather_records(c->recs.p, c->idx.p, n, d_data, c->rec_keys.p, s));
+    HIPCHK(c, hipMemcpyAsync(c->roff.p, off.data(), n * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(c, launch_gather_records(c->recs.p, c->roff.p, n, d_data, c->rec_keys.p, s));
     std::vector<Record> recs(n);
     std::vector<char> keys(n * k);
     HIPCHK(c, hipMemcpyAsync(recs.data(), c->recs.p, n * sizeof(Record), hipMemcpyDeviceToHost, s));
@@ -267,13 +264,46 @@ kmer_status check_err(kmer_ctx *c, uint32_t e) {
 // ---------------------------------------------------------------------------
 // fast path feed
 // ---------------------------------------------------------------------------
+struct IsHead {
+    __host__ __device__ uint32_t operator()(const HeadRec &h) const { return h.count ? 1u : 0u; }
+};
+
+struct TileSumOp {
+    __host__ __device__ TileSum operator()(const TileSum &x, const TileSum &y) const {
+        TileSum r;
+        r.cnt = x.cnt + y.cnt;
+        r.lnl = x.lnl > y.lnl ? x.lnl : y.lnl;
+        r.nh = x.nh + y.nh;
+        r.nx = x.nx + y.nx;
+        return r;
+    }
+};
+
+// Grow the session rank arrays (preserving the first `keep` entries).
+kmer_status ensure_rank_arrays(kmer_ctx *c, uint64_t need, uint64_t keep, hipStream_t s) {
+    if (need >= (1ull << 32)) return fail(c, KMER_E_TOO_MANY_KEYS, "more than 2^32 prefix hits in one session");
+    HIPCHK(c, c->rkey.ensure(need, s, true, keep));
+    HIPCHK(c, c->rord.ensure(need, s, true, keep));
+    HIPCHK(c, c->ridx.ensure(need, s, true, keep));
+    return KMER_OK;
+}
+
+kmer_status ensure_cross(kmer_ctx *c, uint64_t need, hipStream_t s) {
+    HIPCHK(c, c->xord.ensure(need, s, true, c->n_cross));
+    HIPCHK(c, c->xkey.ensure(need, s, true, c->n_cross));
+    HIPCHK(c, c->xslot.ensure(need, s, true, c->n_cross));
+    return KMER_OK;
+}
+
 kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s) {
     const bool packed = c->mode == MODE_PACKED;
-    // capacity for every hit this chunk can produce: its tile slots + the overflow list
+    kmer_status st;
+    // rank capacity for every hit this chunk can produce: its tile slots + the overflow list
     if (packed) {
-        const uint64_t need = c->n_hits + (uint64_t)n_tiles * HMAX + c->ovf.cap;
-        HIPCHK(c, c->hkey.ensure(need, s, true, c->n_hits));
-        HIPCHK(c, c->hval.ensure(need, s, true, c->n_hits));
+        st = ensure_rank_arrays(c, c->n_hits + (uint64_t)n_tiles * HMAX + c->ovf.cap, c->n_hits, s);
+        if (st) return st;
+        st = ensure_cross(c, c->n_cross + std::max<uint64_t>(n_tiles / 4, 4096), s);
+        if (st) return st;
     }
     ScanArgs a;
     memset(&a, 0, sizeof(a));
@@ -287,10 +317,8 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
     a.r4 = pack4(c->rprefix);
     a.pmask = a.plen >= 4 ? 0xFFFFFFFFu : ((1u << (8 * a.plen)) - 1u);
     a.PR = c->d_PR;
-    a.agg_cnt = c->agg_cnt.p;
-    a.agg_lnl = c->agg_lnl.p;
+    a.tsum = c->tsum.p;
     a.hits = c->hits.p;
-    a.tile_nhits = c->tile_nhits.p;
     a.ovf = c->ovf.p;
     a.ovf_count = c->d_ovf_count;
     a.ovf_cap = c->ovf.cap;
@@ -300,8 +328,8 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
     HitArgs h;
     memset(&h, 0, sizeof(h));
     h.hits = c->hits.p;
-    h.tile_nhits = c->tile_nhits.p;
-    h.hscan = c->hscan.p;
+    h.tsum = c->tsum.p;
+    h.tscan = c->tscan.p;
     h.ovf = c->ovf.p;
     h.ovf_count = c->d_ovf_count;
     h.ovf_cap = c->ovf.cap;
@@ -310,43 +338,41 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
     h.plen = a.plen;
     h.abs_offset = c->abs_offset;
     h.pos = c->d_pos;
-    h.cscan = c->cscan.p;
-    h.lnl_before = c->lnl_before.p;
     h.packed = packed;
     h.smask = (c->kbits >= 64) ? ~0ull : ((1ull << c->kbits) - 1ull);
     h.invalid_key = c->kbits >= 63 ? ~0ull : (1ull << c->kbits);
-    h.out_key = packed ? c->hkey.p : nullptr;
-    h.out_val = packed ? c->hval.p : nullptr;
     h.out_base = c->n_hits;
     h.recs = c->recs.p;
     h.rec_count = c->d_rec_count;
     h.rec_cap = c->recs.cap;
     h.err = c->d_err;
+    auto bind_session = [&]() {
+        h.rkey = c->rkey.p;
+        h.rord = c->rord.p;
+        h.ridx = c->ridx.p;
+        h.xord = c->xord.p;
+        h.xkey = c->xkey.p;
+        h.xslot = c->xslot.p;
+        h.xbase = c->n_cross;
+        h.xcap = c->xord.cap;
+    };
+    bind_session();
+    const TileSum init{0, c->abs_offset, 0, 0};
 
     HIPCHK(c, hipMemcpyAsync(c->d_pos_saved, c->d_pos, sizeof(StreamPos), hipMemcpyDeviceToDevice, s));
-    kmer_status st;
     for (int attempt = 0; attempt < 8; ++attempt) {
-        HIPCHK(c, hipMemsetAsync(c->d_ovf_count, 0, 8, s));
-        HIPCHK(c, hipMemsetAsync(c->d_rec_count, 0, 8, s));
+        HIPCHK(c, hipMemsetAsync(c->d_scal, 0, 3 * 8, s));   // rec, ovf, cross counts of this chunk
         HIPCHK(c, hipEventRecord(c->ev0, s));
         HIPCHK(c, launch_scan_tiles(a, s));
         HIPCHK(c, hipEventRecord(c->ev1, s));
-        ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->agg_cnt.p, c->cscan.p, (uint64_t)0, (size_t)n_tiles,
-                                               rocprim::plus<uint64_t>(), s));
-        ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->agg_lnl.p, c->lnl_before.p, (uint64_t)c->abs_offset,
-                                               (size_t)n_tiles, rocprim::maximum<uint64_t>(), s));
-        ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tile_nhits.p, c->hscan.p, (uint64_t)0, (size_t)n_tiles,
-                                               rocprim::plus<uint64_t>(), s));
+        ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tsum.p, c->tscan.p, init, (size_t)n_tiles, TileSumOp(), s));
         HIPCHK(c, launch_hits(h, s));
-        HIPCHK(c, launch_pos_update(c->d_pos, c->cscan.p, c->agg_cnt.p, n_tiles, d, len, s));
+        HIPCHK(c, launch_pos_update(c->d_pos, c->tsum.p, c->tscan.p, n_tiles, d, len, c->d_chunk_hits, c->d_xcount,
+                                    s));
         HIPCHK(c, hipEventRecord(c->ev4, s));
-        HIPCHK(c, hipMemcpyAsync(c->h_small + 0, c->d_rec_count, 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipMemcpyAsync(c->h_small + 1, c->d_ovf_count, 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipMemcpyAsync(c->h_small + 2, c->d_err, 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipMemcpyAsync(c->h_small + 3, c->hscan.p + (n_tiles - 1), 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipMemcpyAsync(c->h_small + 4, c->tile_nhits.p + (n_tiles - 1), 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
-        const uint32_t e = (uint32_t)c->h_small[2];
+        const uint32_t e = (uint32_t)c->h_small[5];
         st = check_err(c, e);
         if (st) return st;
         float ms = 0.f, ms_all = 0.f;
@@ -354,9 +380,9 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
         HIPCHK(c, hipEventElapsedTime(&ms_all, c->ev0, c->ev4));
         c->scan_ms += ms;
         c->feed_ms += ms_all;
-        if (e & (ERR_OVF_OVERFLOW | ERR_REC_OVERFLOW)) {
-            // grow and redo the chunk from the saved position; hit resolution is
-            // idempotent (fixed slots), so a redo rewrites, never double counts
+        if (e & (ERR_OVF_OVERFLOW | ERR_REC_OVERFLOW | ERR_CROSS_OVERFLOW)) {
+            // grow and redo the chunk from the saved position; hit placement is
+            // idempotent (rank slots are rewritten, lists restart at this chunk's base)
             HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
             HIPCHK(c, hipMemcpyAsync(c->d_pos, c->d_pos_saved, sizeof(StreamPos), hipMemcpyDeviceToDevice, s));
             if (e & ERR_OVF_OVERFLOW) {
@@ -365,12 +391,13 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
                 h.ovf = c->ovf.p;
                 a.ovf_cap = h.ovf_cap = c->ovf.cap;
                 if (packed) {
-                    const uint64_t need = c->n_hits + (uint64_t)n_tiles * HMAX + c->ovf.cap;
-                    HIPCHK(c, c->hkey.ensure(need, s, true, c->n_hits));
-                    HIPCHK(c, c->hval.ensure(need, s, true, c->n_hits));
-                    h.out_key = c->hkey.p;
-                    h.out_val = c->hval.p;
+                    st = ensure_rank_arrays(c, c->n_hits + (uint64_t)n_tiles * HMAX + c->ovf.cap, c->n_hits, s);
+                    if (st) return st;
                 }
+            }
+            if (e & ERR_CROSS_OVERFLOW) {
+                st = ensure_cross(c, c->n_cross + c->h_small[2] + 1024, s);
+                if (st) return st;
             }
             if (e & ERR_REC_OVERFLOW) {
                 st = ensure_records(c, c->h_small[0] + 1024);
@@ -378,11 +405,16 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
                 h.recs = c->recs.p;
                 h.rec_cap = c->recs.cap;
             }
+            bind_session();
             continue;
         }
         break;
     }
-    if (packed) c->n_hits += c->h_small[3] + (uint32_t)c->h_small[4] + c->h_small[1];
+    if (packed) {
+        c->n_hits += c->h_small[3];
+        c->n_cross += c->h_small[2];
+        c->long_seg |= (c->h_small[5] & INFO_LONGSEG) != 0;
+    }
     const uint64_t nrec = c->h_small[0];
     if (nrec) {
         st = drain_records(c, d, nrec, s);
@@ -460,10 +492,9 @@ kmer_status general_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n
         HIPCHK(c, hipEventRecord(c->ev0, s));
         HIPCHK(c, launch_lines(a, lookback, s));
         HIPCHK(c, hipEventRecord(c->ev1, s));
-        HIPCHK(c, hipMemcpyAsync(c->h_small + 1, c->d_line_count, 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipMemcpyAsync(c->h_small + 2, c->d_err, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
-        const uint32_t e = (uint32_t)c->h_small[2];
+        const uint32_t e = (uint32_t)c->h_small[5];
         st = check_err(c, e);
         if (st) return st;
         float ms = 0.f;
@@ -473,14 +504,14 @@ kmer_status general_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n
         if (e & ERR_LINE_OVERFLOW) {
             HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
             HIPCHK(c, hipMemcpyAsync(c->d_pos, c->d_pos_saved, sizeof(StreamPos), hipMemcpyDeviceToDevice, s));
-            HIPCHK(c, c->lines.ensure(c->h_small[1] + 1024, s));
+            HIPCHK(c, c->lines.ensure(c->h_small[6] + 1024, s));
             a.lines_out = c->lines.p;
             a.line_cap = c->lines.cap;
             continue;
         }
         break;
     }
-    const uint64_t nlines = c->h_small[1];
+    const uint64_t nlines = c->h_small[6];
     uint64_t nrec = 0;
     if (nlines) {
         WindowArgs w;
@@ -501,10 +532,9 @@ kmer_status general_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n
             HIPCHK(c, hipEventRecord(c->ev0, s));
             HIPCHK(c, launch_windows(w, (uint32_t)std::min<uint64_t>(nlines, 65536), s));
             HIPCHK(c, hipEventRecord(c->ev1, s));
-            HIPCHK(c, hipMemcpyAsync(c->h_small + 0, c->d_rec_count, 8, hipMemcpyDeviceToHost, s));
-            HIPCHK(c, hipMemcpyAsync(c->h_small + 2, c->d_err, 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
             HIPCHK(c, hipStreamSynchronize(s));
-            const uint32_t e = (uint32_t)c->h_small[2];
+            const uint32_t e = (uint32_t)c->h_small[5];
             st = check_err(c, e);
             if (st) return st;
             float ms = 0.f;
@@ -545,6 +575,8 @@ kmer_status reset(kmer_ctx *c) {
     c->exotic.clear();
     c->abs_offset = 0;
     c->n_hits = 0;
+    c->n_cross = 0;
+    c->long_seg = false;
     c->n_out = 0;
     c->scan_ms = c->feed_ms = c->finish_ms = 0.0;
     c->open_stream = true;
@@ -554,55 +586,79 @@ kmer_status reset(kmer_ctx *c) {
 // ---------------------------------------------------------------------------
 // finish
 // ---------------------------------------------------------------------------
-// Sort (key, value) pairs by key and reduce equal keys (min first, sum count)
-// into c->ukey / c->uval; returns the unique count (sentinel group dropped).
-kmer_status reduce_pairs(kmer_ctx *c, uint64_t *keys, Agg *vals, uint64_t n, uint64_t *nu_out) {
+// Place the cross entries: sorted by order key they take the natural slots
+// sorted ascending (the slots that tile-local ranking left to them).
+kmer_status apply_cross(kmer_ctx *c, uint64_t max_line) {
     hipStream_t s = c->stream;
-    *nu_out = 0;
+    const uint64_t n = c->n_cross;
     if (n == 0) return KMER_OK;
-    HIPCHK(c, c->hkey2.ensure(n, s));
-    HIPCHK(c, c->hval2.ensure(n, s));
-    HIPCHK(c, c->ukey.ensure(n, s));
-    HIPCHK(c, c->uval.ensure(n, s));
-    rocprim::double_buffer<uint64_t> kb(keys, c->hkey2.p);
-    rocprim::double_buffer<Agg> vb(vals, c->hval2.p);
-    const int end_bit = std::min<int>(64, (int)c->kbits + 1);   // + the invalid-key bit
-    ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, kb, vb, (size_t)n, 0, end_bit, s));
-    ROCPRIM_RUN(c, rocprim::reduce_by_key(t, b, kb.current(), vb.current(), (size_t)n, c->ukey.p, c->uval.p,
-                                          c->d_nuniq, AggMinSum(), rocprim::equal_to<uint64_t>(), s));
-    HIPCHK(c, hipMemcpyAsync(c->h_small + 5, c->d_nuniq, 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipStreamSynchronize(s));
-    uint64_t nu = c->h_small[5];
-    if (nu) {
-        HIPCHK(c, hipMemcpyAsync(c->h_small + 6, c->ukey.p + nu - 1, 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipStreamSynchronize(s));
-        const uint64_t invalid = c->kbits >= 63 ? ~0ull : (1ull << c->kbits);
-        if (c->h_small[6] == invalid) --nu;   // filtered-out / record hits
+    if (!c->long_seg) {
+        HIPCHK(c, launch_cross_segsort(c->xord.p, c->xkey.p, c->xslot.p, n, c->rkey.p, c->rord.p, s));
+    } else if (n <= XSMALL_MAX) {
+        HIPCHK(c, launch_cross_sort_small(c->xslot.p, c->xord.p, c->xkey.p, n, c->rkey.p, c->rord.p, s));
+    } else {
+        HIPCHK(c, c->xord2.ensure(n, s));
+        HIPCHK(c, c->xkey2.ensure(n, s));
+        rocprim::double_buffer<uint64_t> ob(c->xord.p, c->xord2.p);
+        rocprim::double_buffer<uint64_t> kb(c->xkey.p, c->xkey2.p);
+        const int obits = std::min(64, bit_width(((max_line + 1) << 24) | 0xFFFFFFull));
+        ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, ob, kb, (size_t)n, 0, obits, s));
+        HIPCHK(c, launch_cross_scatter(c->xslot.p, ob.current(), kb.current(), n, c->rkey.p, c->rord.p, s));
     }
-    *nu_out = nu;
+    c->n_cross = 0;
     return KMER_OK;
 }
 
-// unique entries -> first-occurrence order -> decoded keys (device)
-kmer_status order_and_decode(kmer_ctx *c, uint64_t nu, uint64_t max_line) {
+// Rank arrays (rkey / rord / ridx [/ rcnt]) of n hits -> unique keys in
+// first-occurrence order: stable radix sort of (key, rank); group heads flag
+// their rank; a scan of the flags gives each unique key its output position.
+// partial: (code, {first, count}) into ukey/uval; else decoded keys, counts
+// and firsts into keys_out / cnt_out / first.  Returns the unique count.
+kmer_status rank_finish(kmer_ctx *c, uint64_t n, bool partial, bool with_counts, uint64_t *nu_out) {
     hipStream_t s = c->stream;
-    c->n_out = nu;
-    if (nu == 0) return KMER_OK;
-    HIPCHK(c, c->first.ensure(nu, s));
-    HIPCHK(c, c->first2.ensure(nu, s));
-    HIPCHK(c, c->idx.ensure(nu, s));
-    HIPCHK(c, c->idx2.ensure(nu, s));
-    HIPCHK(c, c->keys_out.ensure(nu * c->p.k, s));
-    HIPCHK(c, c->cnt_out.ensure(nu, s));
-    HIPCHK(c, launch_split_first(c->uval.p, nu, c->first.p, c->idx.p, s));
-    const int end_bit = std::min(64, bit_width(((max_line + 1) << 24) | 0xFFFFFFull));
-    rocprim::double_buffer<uint64_t> kb(c->first.p, c->first2.p);
-    rocprim::double_buffer<uint64_t> vb(c->idx.p, c->idx2.p);
-    ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, kb, vb, (size_t)nu, 0, end_bit, s));
-    HIPCHK(c, launch_packed_decode(vb.current(), nu, c->ukey.p, c->uval.p, c->p.k, (uint32_t)c->prefix.size(),
-                                   c->d_P, c->keys_out.p, c->cnt_out.p, s));
-    if (kb.current() != c->first.p)
-        HIPCHK(c, hipMemcpyAsync(c->first.p, kb.current(), nu * 8, hipMemcpyDeviceToDevice, s));
+    *nu_out = 0;
+    if (n == 0) return KMER_OK;
+    HIPCHK(c, c->rkey2.ensure(n, s));
+    HIPCHK(c, c->ridx2.ensure(n, s));
+    HIPCHK(c, c->hrec.ensure(n, s));
+    HIPCHK(c, c->opos.ensure(n, s));
+    if (partial) {
+        HIPCHK(c, c->ukey.ensure(n, s));
+        HIPCHK(c, c->uval.ensure(n, s));
+    } else {
+        HIPCHK(c, c->keys_out.ensure(n * c->p.k, s));
+        HIPCHK(c, c->cnt_out.ensure(n, s));
+        HIPCHK(c, c->first.ensure(n, s));
+    }
+    const uint64_t invalid = c->kbits >= 63 ? ~0ull : (1ull << c->kbits);
+    rocprim::double_buffer<uint64_t> kb(c->rkey.p, c->rkey2.p);
+    rocprim::double_buffer<uint32_t> vb(c->ridx.p, c->ridx2.p);
+    const int end_bit = std::min<int>(64, (int)c->kbits + 1);   // + the invalid-key bit
+    ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, kb, vb, (size_t)n, 0, end_bit, s));
+    HIPCHK(c, launch_heads(kb.current(), vb.current(), n, invalid, with_counts ? c->rcnt.p : nullptr, c->hrec.p, s));
+    auto is_head = rocprim::make_transform_iterator(c->hrec.p, IsHead());
+    ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, is_head, c->opos.p, 0u, (size_t)n, rocprim::plus<uint32_t>(), s));
+    EmitArgs e;
+    memset(&e, 0, sizeof(e));
+    e.hrec = c->hrec.p;
+    e.opos = c->opos.p;
+    e.rord = c->rord.p;
+    e.n = n;
+    e.invalid_key = invalid;
+    e.nuniq = c->d_nuniq;
+    e.k = c->p.k;
+    e.plen = (uint32_t)c->prefix.size();
+    e.partial = partial ? 1u : 0u;
+    memcpy(e.P, c->prefix.data(), std::min<size_t>(c->prefix.size(), sizeof(e.P)));
+    e.keys_out = c->keys_out.p;
+    e.cnt_out = c->cnt_out.p;
+    e.first_out = c->first.p;
+    e.ukey = c->ukey.p;
+    e.uval = c->uval.p;
+    HIPCHK(c, launch_emit(e, s));
+    HIPCHK(c, hipMemcpyAsync(c->h_small + 4, c->d_nuniq, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    *nu_out = c->h_small[4];
     return KMER_OK;
 }
 
@@ -667,13 +723,13 @@ kmer_status finish(kmer_ctx *c, kmer_result **out) {
     if (st) return st;
     HIPCHK(c, hipEventRecord(c->ev2, c->stream));
     uint64_t nu = 0;
+    c->n_out = 0;
     if (c->mode == MODE_PACKED) {
-        st = reduce_pairs(c, c->hkey.p, c->hval.p, c->n_hits, &nu);
+        st = apply_cross(c, pos.lines);
         if (st) return st;
-        st = order_and_decode(c, nu, pos.lines);
+        st = rank_finish(c, c->n_hits, false, false, &nu);
         if (st) return st;
-    } else {
-        c->n_out = 0;
+        c->n_out = nu;
     }
     HIPCHK(c, hipEventRecord(c->ev3, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -788,11 +844,17 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
         if (ok) ok &= hipMemcpy(c->d_PR, pr.data(), pr.size(), hipMemcpyHostToDevice) == hipSuccess;
     }
     ok &= dalloc(&c->d_ticket, 4) == hipSuccess;
-    ok &= dalloc(&c->d_err, 1) == hipSuccess;
-    ok &= dalloc(&c->d_rec_count, 1) == hipSuccess;
-    ok &= dalloc(&c->d_line_count, 1) == hipSuccess;
-    ok &= dalloc(&c->d_ovf_count, 1) == hipSuccess;
-    ok &= dalloc(&c->d_nuniq, 1) == hipSuccess;
+    ok &= dalloc(&c->d_scal, 8) == hipSuccess;
+    if (ok) {
+        ok &= hipMemset(c->d_scal, 0, 64) == hipSuccess;
+        c->d_rec_count = (unsigned long long *)(c->d_scal + 0);
+        c->d_ovf_count = (unsigned long long *)(c->d_scal + 1);
+        c->d_xcount = (unsigned long long *)(c->d_scal + 2);
+        c->d_chunk_hits = (unsigned long long *)(c->d_scal + 3);
+        c->d_nuniq = c->d_scal + 4;
+        c->d_err = (unsigned int *)(c->d_scal + 5);
+        c->d_line_count = (unsigned long long *)(c->d_scal + 6);
+    }
     ok &= dalloc(&c->d_pos, 1) == hipSuccess;
     ok &= dalloc(&c->d_pos_saved, 1) == hipSuccess;
     ok &= hipHostMalloc((void **)&c->h_small, 16 * sizeof(uint64_t), hipHostMallocDefault) == hipSuccess;
@@ -813,16 +875,17 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
 kmer_status kmer_close(kmer_ctx *c) {
     if (!c) return KMER_E_BAD_PARAM;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (auto *b : {&c->agg_cnt, &c->agg_lnl, &c->cscan, &c->lnl_before, &c->hscan, &c->tp_cnt, &c->tp_lnl,
-                    &c->hkey, &c->hkey2, &c->ukey, &c->first, &c->first2, &c->idx, &c->idx2, &c->cnt_out})
+    for (auto *b : {&c->tp_cnt, &c->tp_lnl, &c->rkey, &c->rkey2, &c->rord, &c->rcnt, &c->xord, &c->xord2,
+                    &c->xkey, &c->xkey2, &c->ukey, &c->first, &c->cnt_out, &c->roff})
         b->release();
-    c->tile_nhits.release();
+    for (auto *b : {&c->ridx, &c->ridx2, &c->opos, &c->xslot}) b->release();
+    c->hrec.release();
+    c->tsum.release();
+    c->tscan.release();
     c->hits.release();
     c->ovf.release();
     c->lb_cnt.release();
     c->lb_lnl.release();
-    c->hval.release();
-    c->hval2.release();
     c->uval.release();
     c->keys_out.release();
     c->recs.release();
@@ -830,8 +893,7 @@ kmer_status kmer_close(kmer_ctx *c) {
     c->rec_keys.release();
     c->tmp.release();
     c->batch.release();
-    dfree(c->d_ticket); dfree(c->d_err); dfree(c->d_rec_count); dfree(c->d_line_count);
-    dfree(c->d_ovf_count); dfree(c->d_nuniq); dfree(c->d_pos); dfree(c->d_pos_saved);
+    dfree(c->d_ticket); dfree(c->d_scal); dfree(c->d_pos); dfree(c->d_pos_saved);
     dfree(c->d_P); dfree(c->d_PR);
     if (c->h_small) (void)hipHostFree(c->h_small);
     for (hipEvent_t e : {c->ev0, c->ev1, c->ev2, c->ev3, c->ev4})
@@ -933,9 +995,15 @@ kmer_status kmer_partial_device(kmer_ctx *c, const void **d_keys, const void **d
     if (!c || !d_keys || !d_vals || !n) return KMER_E_BAD_PARAM;
     if (c->mode != MODE_PACKED) return fail(c, KMER_E_STATE, "configuration has no packed keys");
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
-    uint64_t nu = 0;
-    kmer_status st = reduce_pairs(c, c->hkey.p, c->hval.p, c->n_hits, &nu);
+    StreamPos pos;
+    kmer_status st = read_pos(c, &pos);
     if (st) return st;
+    st = apply_cross(c, pos.lines);
+    if (st) return st;
+    uint64_t nu = 0;
+    st = rank_finish(c, c->n_hits, true, false, &nu);
+    if (st) return st;
+    c->n_hits = 0;           // the rank arrays were consumed by the sort
     *d_keys = c->ukey.p;
     *d_vals = c->uval.p;
     *n = nu;
@@ -950,24 +1018,24 @@ kmer_status kmer_finish_merged(kmer_ctx *c, const void *d_keys, const void *d_va
     if (out) *out = nullptr;
     hipStream_t s = c->stream;
     HIPCHK(c, hipEventRecord(c->ev2, s));
-    // private copies: the reduce sorts in place
-    HIPCHK(c, c->hkey.ensure(n, s));
-    HIPCHK(c, c->hval.ensure(n, s));
-    if (n) {
-        HIPCHK(c, hipMemcpyAsync(c->hkey.p, d_keys, n * 8, hipMemcpyDeviceToDevice, s));
-        HIPCHK(c, hipMemcpyAsync(c->hval.p, d_vals, n * sizeof(Agg), hipMemcpyDeviceToDevice, s));
-    }
+    // the partials, concatenated in shard order, are already in first-occurrence
+    // order: their index is their rank
+    kmer_status st = ensure_rank_arrays(c, n, 0, s);
+    if (st) return st;
+    HIPCHK(c, c->rcnt.ensure(n, s));
+    HIPCHK(c, launch_merge_prep((const uint64_t *)d_keys, (const Agg *)d_vals, n, c->rkey.p, c->rord.p, c->rcnt.p,
+                                c->ridx.p, s));
     uint64_t nu = 0;
-    kmer_status st = reduce_pairs(c, c->hkey.p, c->hval.p, n, &nu);
+    st = rank_finish(c, n, false, true, &nu);
     if (st) return st;
-    st = order_and_decode(c, nu, total_lines);
-    if (st) return st;
+    c->n_out = nu;
     HIPCHK(c, hipEventRecord(c->ev3, s));
     HIPCHK(c, hipStreamSynchronize(s));
     float ms = 0.f;
     HIPCHK(c, hipEventElapsedTime(&ms, c->ev2, c->ev3));
     c->finish_ms = ms;
     c->n_hits = 0;
+    c->n_cross = 0;
     c->open_stream = false;
     const uint64_t total = c->n_out + c->exotic.size();
     if (c->p.max_keys && total > c->p.max_keys)

@@ -27,6 +27,10 @@ enum : uint32_t {
     ERR_REC_OVERFLOW = 1u << 3,
     ERR_LINE_OVERFLOW = 1u << 4,
     ERR_OVF_OVERFLOW = 1u << 5,
+    ERR_CROSS_OVERFLOW = 1u << 6,
+    // not an error: a tile without '\n' had hits, or a tile overflowed its hit
+    // slots -- cross segments may be long (finish sorts the whole cross list)
+    INFO_LONGSEG = 1u << 16,
 };
 
 // look-back word: [63:62] status, [61:0] value
@@ -64,11 +68,22 @@ struct SeqLine {
 struct HitRec {
     uint64_t code;         // 2-bit codes of the k-byte forward window (k <= 32)
     uint32_t tile;
-    uint32_t qm;           // [13:0] pattern position q, [14] strand, [15] exotic, [16] line start in tile
+    uint32_t qm;           // [13:0] pattern position q, [14] strand, [15] exotic, [16] line start in tile,
+                           // [31:17] ordinal of the hit in its tile
     uint32_t c_local;      // '\n' count in the tile before the window start
     uint32_t lstart;       // tile-relative line start (when [16] is set)
 };
 constexpr int HMAX = 64;   // hit slots per tile (more go to the overflow list)
+
+// Per-tile aggregates of the scan kernel, scanned (exclusive) across tiles
+// with TileSumOp: lines before the tile, start of the line open at the tile
+// start, hits before the tile.
+struct TileSum {
+    uint64_t cnt;                  // real '\n' count
+    uint64_t lnl;                  // absolute start of the line after its last '\n' (0 = none; scan: max)
+    uint64_t nh;                   // prefix hits (stored + overflow)
+    uint64_t nx;                   // ... of which cross hits (line crosses a tile edge; all if overflowed)
+};
 
 struct ScanArgs {
     const uint8_t *data;
@@ -77,10 +92,8 @@ struct ScanArgs {
     uint32_t n_tiles, k, plen;
     uint32_t p4, r4, pmask;
     const uint8_t *PR;
-    uint64_t *agg_cnt;             // per tile: real '\n' count
-    uint64_t *agg_lnl;             // per tile: absolute line start after its last '\n' (0 = none)
+    TileSum *tsum;                 // per tile
     HitRec *hits;                  // n_tiles * HMAX slots
-    uint32_t *tile_nhits;
     HitRec *ovf;
     unsigned long long *ovf_count;
     uint64_t ovf_cap;
@@ -88,34 +101,64 @@ struct ScanArgs {
     uint32_t ablate;               // experiments only: bit0 = drop all candidates
 };
 
-// value of a packed hit / unique key: first-occurrence order and count
+// value of a unique packed key: first-occurrence order and count
 struct Agg {
     uint64_t first;
     uint64_t count;
 };
 
+// Hit resolution.  Packed mode places every hit of the session at its RANK
+// (position in first-occurrence order of all hits): a hit whose line lies
+// inside one tile gets hits-before-tile + its rank among the tile's hits;
+// hits of lines that cross a tile edge (or of overflowed tiles) go to the
+// cross list with their natural slot and are placed by a sort at finish.
 struct HitArgs {
     const HitRec *hits;
-    const uint32_t *tile_nhits;
-    const uint64_t *hscan;         // exclusive scan of tile_nhits
+    const TileSum *tsum;
+    const TileSum *tscan;          // exclusive scan of tsum (cnt: sum, lnl: max from abs_offset, nh: sum)
     const HitRec *ovf;
     const unsigned long long *ovf_count;
     uint64_t ovf_cap;
     uint32_t n_tiles, k, plen;
     uint64_t abs_offset;
     const StreamPos *pos;
-    const uint64_t *cscan;         // exclusive sum of agg_cnt
-    const uint64_t *lnl_before;    // exclusive max of agg_lnl (init abs_offset)
-    uint32_t packed;               // ACGT windows (k <= 32) go to the packed hit array
+    uint32_t packed;               // ACGT windows (k <= 32) are ranked packed keys
     uint64_t smask;                // suffix mask: 2*(k - |P|) bits
     uint64_t invalid_key;          // 2^(2*(k-|P|)): sorts after every real key
-    uint64_t *out_key;             // session hit array (NULL: records only)
-    Agg *out_val;
     uint64_t out_base;             // session hits before this chunk
+    uint64_t *rkey;                // by rank: suffix code (invalid_key: filtered / record)
+    uint64_t *rord;                // by rank: first-occurrence order key
+    uint32_t *ridx;                // by rank: the rank itself (sort payload)
+    uint64_t *xord, *xkey;         // cross list in natural-slot order (order, key, natural slot)
+    uint32_t *xslot;
+    uint64_t xbase, xcap;          // session cross entries before this chunk, capacity
     Record *recs;
     unsigned long long *rec_count;
     uint64_t rec_cap;
     unsigned int *err;
+};
+
+// By rank, after the key sort: the key and its total count if this rank is
+// the key's first occurrence, count 0 otherwise.
+struct HeadRec {
+    uint64_t key;
+    uint64_t count;
+};
+
+// Ordered output from the rank arrays after the key sort.
+struct EmitArgs {
+    const HeadRec *hrec;           // by rank
+    const uint32_t *opos;          // exclusive scan of (count != 0): output position
+    const uint64_t *rord;          // by rank: order key
+    uint64_t n;
+    uint64_t invalid_key;
+    uint64_t *nuniq;
+    uint32_t k, plen, partial;
+    uint8_t P[32];
+    uint8_t *keys_out;             // decode: n * k bytes
+    uint64_t *cnt_out, *first_out;
+    uint64_t *ukey;                // partial: suffix codes
+    Agg *uval;                     // partial: {first, count}
 };
 
 struct TileArgs {
@@ -167,15 +210,24 @@ struct WindowArgs {
 hipError_t launch_lines(const TileArgs &a, bool lookback, hipStream_t s);
 hipError_t launch_scan_tiles(const ScanArgs &a, hipStream_t s);
 hipError_t launch_hits(const HitArgs &a, hipStream_t s);
-hipError_t launch_pos_update(StreamPos *pos, const uint64_t *cscan, const uint64_t *agg_cnt, uint32_t n_tiles,
-                             const uint8_t *data, uint64_t len, hipStream_t s);
+hipError_t launch_pos_update(StreamPos *pos, const TileSum *tsum, const TileSum *tscan, uint32_t n_tiles,
+                             const uint8_t *data, uint64_t len, unsigned long long *chunk_hits,
+                             unsigned long long *chunk_cross, hipStream_t s);
 hipError_t launch_tile_aggregate(const uint8_t *data, uint64_t len, uint32_t n_tiles, uint64_t *agg_cnt,
                                  uint64_t *agg_lnl, unsigned int *err, hipStream_t s);
 hipError_t launch_windows(const WindowArgs &a, uint32_t grid, hipStream_t s);
-hipError_t launch_split_first(const Agg *uval, uint64_t n, uint64_t *first, uint64_t *idx, hipStream_t s);
-hipError_t launch_packed_decode(const uint64_t *idx, uint64_t n, const uint64_t *ukey, const Agg *uval, uint32_t k,
-                                uint32_t plen, const uint8_t *P, uint8_t *keys_out, uint64_t *counts_out,
-                                hipStream_t s);
+hipError_t launch_cross_scatter(const uint32_t *slot, const uint64_t *ord, const uint64_t *key, uint64_t n,
+                                uint64_t *rkey, uint64_t *rord, hipStream_t s);
+hipError_t launch_cross_sort_small(const uint32_t *slot, const uint64_t *ord, const uint64_t *key, uint64_t n,
+                                   uint64_t *rkey, uint64_t *rord, hipStream_t s);
+constexpr uint64_t XSMALL_MAX = 16384;   // cross lists up to this size: one-workgroup sort
+hipError_t launch_cross_segsort(uint64_t *ord, uint64_t *key, const uint32_t *slot, uint64_t n, uint64_t *rkey,
+                                uint64_t *rord, hipStream_t s);
+hipError_t launch_heads(const uint64_t *skey, const uint32_t *srank, uint64_t n, uint64_t invalid_key,
+                        const uint64_t *rcnt, HeadRec *hrec, hipStream_t s);
+hipError_t launch_emit(const EmitArgs &a, hipStream_t s);
+hipError_t launch_merge_prep(const uint64_t *keys, const Agg *vals, uint64_t n, uint64_t *rkey, uint64_t *rord,
+                             uint64_t *rcnt, uint32_t *ridx, hipStream_t s);
 hipError_t launch_gather_records(const Record *recs, const uint64_t *key_off, uint64_t n,
                                  const uint8_t *data, uint8_t *out, hipStream_t s);
 hipError_t launch_synth_fastq(uint8_t *out, uint64_t seed, uint64_t first_read, uint64_t n_reads,

@@ -390,6 +390,8 @@ struct ScanShared {
     int32_t last_chunk;          // highest chunk holding a real '\n' (-1 = none)
     int32_t lastpos;             // tile-relative position of the tile's last real '\n'
     uint32_t nh;                 // hit records written by this tile
+    uint32_t nx;                 // ... of which on lines that cross a tile edge
+    uint32_t tcnt;               // real '\n' count of the tile
     uint32_t qn;                 // verified-hit queue fill
     uint32_t q[QCAP];            // verified hits: (tile position << 1) | strand
 };
@@ -473,7 +475,11 @@ __device__ __forceinline__ void emit_hit(const ScanArgs &a, const uint8_t *buf, 
     r.qm = (uint32_t)q | (strand << 14) | ((exotic ? 1u : 0u) << 15) | ((lstart >= 0 ? 1u : 0u) << 16);
     r.c_local = c_local;
     r.lstart = lstart >= 0 ? (uint32_t)lstart : 0u;
-    const uint32_t slot = atomicAdd(&sh.nh, 1u);
+    const uint32_t slot = atomicAdd(&sh.nh, 1u);     // < 2 * TILE: fits qm[31:17]
+    r.qm |= slot << 17;
+    // the hit kernel ranks hits of lines inside the tile; lines that cross a
+    // tile edge are placed at finish (same predicate there)
+    if (lstart < 0 || c_local == sh.tcnt) atomicAdd(&sh.nx, 1u);
     if (slot < HMAX) {
         a.hits[(uint64_t)tile * HMAX + slot] = r;
     } else {
@@ -521,6 +527,7 @@ __global__ __launch_bounds__(TPB) void scan_tile_kernel(ScanArgs a) {
         if (tid == 0) {
             sh.last_chunk = -1;
             sh.nh = 0;
+            sh.nx = 0;
             sh.qn = 0;
         }
         uint32_t orall = 0;
@@ -620,7 +627,10 @@ __global__ __launch_bounds__(TPB) void scan_tile_kernel(ScanArgs a) {
             sh.cpre[tid + TPB * i] = (uint16_t)(base + col_off[i] + ((excl >> (16 * i)) & 0xFFFFu));
             base += col_total[i];
         }
-        if (tid == 0) a.agg_cnt[tile] = base;
+        if (tid == 0) {
+            a.tsum[tile].cnt = base;
+            sh.tcnt = base;
+        }
     }
     if (tid == 0) {
         const int lc = sh.last_chunk;
@@ -628,7 +638,7 @@ __global__ __launch_bounds__(TPB) void scan_tile_kernel(ScanArgs a) {
         const int64_t lim = (int64_t)len - g0;
         const int lp = lc >= 0 ? last_newline_in_chunk(buf, lc, lim < TILE ? (int)lim : TILE) : -1;
         sh.lastpos = lp;
-        a.agg_lnl[tile] = lp >= 0 ? a.abs_offset + (uint64_t)(g0 + lp + 1) : 0;
+        a.tsum[tile].lnl = lp >= 0 ? a.abs_offset + (uint64_t)(g0 + lp + 1) : 0;
     }
     const uint32_t k = a.k, plen = a.plen;
     if (plen > k || (a.ablate & 1u)) cand = 0;
@@ -682,91 +692,160 @@ __global__ __launch_bounds__(TPB) void scan_tile_kernel(ScanArgs a) {
     for (uint32_t h = tid; h < nq; h += TPB) emit_hit(a, buf, sh, tile, sh.q[h]);
     if (nq > 64 || sh.qn > QCAP) {
         __syncthreads();         // uniform: every wave may have written records
-        if (tid == 0) a.tile_nhits[tile] = min(sh.nh, (uint32_t)HMAX);
-    } else if (tid == 0) {
-        a.tile_nhits[tile] = min(sh.nh, (uint32_t)HMAX);   // wave 0 wrote them all
+        if (tid == 0) {
+            a.tsum[tile].nh = sh.nh;
+            a.tsum[tile].nx = sh.nh > (uint32_t)HMAX ? sh.nh : sh.nx;   // overflowed: all hits cross
+            if (sh.nh > (uint32_t)HMAX || sh.tcnt == 0) atomicOr(a.err, INFO_LONGSEG);
+        }
+    } else if (tid == 0) {                       // wave 0 wrote them all
+        a.tsum[tile].nh = sh.nh;
+        a.tsum[tile].nx = sh.nx;
+        if (sh.nh && sh.tcnt == 0) atomicOr(a.err, INFO_LONGSEG);
     }
 }
 
 
-// Resolve one hit: global line index / line start from the per-tile scans,
-// the reference's sequence-line rule, first-occurrence order.  Packed (ACGT,
-// k <= 32) hits become one (suffix code, {order, 1}) pair at a fixed slot of
-// the session's hit array (idempotent: a re-run rewrites the same slot);
-// everything else becomes a record for the host merge.
-__device__ __forceinline__ void resolve_hit(const HitArgs &a, const HitRec &r, uint64_t slot) {
+// Resolve one hit: global line index / line start from the tile scans, the
+// reference's sequence-line rule (lib/kmers.js:151-155), first-occurrence
+// order key (line << 24 | strand << 23 | strand ? MAXREL - rel : rel).
+// Returns the packed key (invalid_key when the hit does not count as a packed
+// key: non-sequence line, or a record) and writes records for exotic windows
+// / record mode.  *lk = order of the hit among its tile's hits (local).
+__device__ __forceinline__ uint64_t resolve_hit(const HitArgs &a, const HitRec &r, const TileSum &tb,
+                                                uint64_t *order_out, uint32_t *lk, bool *lvalid_out) {
     const uint32_t t = r.tile;
     const uint32_t strand = (r.qm >> 14) & 1u;
     const bool exotic = (r.qm >> 15) & 1u;
     const bool lvalid = (r.qm >> 16) & 1u;
     const int q = (int)(r.qm & 0x3FFFu);
-    const int s0 = strand ? q + (int)a.plen - (int)a.k : q;
+    const int s0 = strand ? q + (int)a.plen - (int)a.k : q;     // >= -63
     const uint64_t tile_abs = a.abs_offset + (uint64_t)t * TILE;
-    const uint64_t li = a.pos->lines + a.cscan[t] + r.c_local;
+    const uint64_t li = a.pos->lines + tb.cnt + r.c_local;
+    const uint64_t lstart = lvalid ? tile_abs + r.lstart : tb.lnl;
+    const uint64_t sabs = tile_abs + (uint64_t)(int64_t)s0;
+    uint64_t rel = sabs - lstart;
+    const bool seq = (li & 3) == 1;
+    if (rel > MAXREL) {
+        if (seq) atomicOr(a.err, ERR_LINE_TOO_LONG);
+        rel = MAXREL;                            // (non-sequence lines only need a consistent order)
+    }
+    const uint64_t order = (li << 24) | ((uint64_t)strand << 23) | (strand ? (uint64_t)(MAXREL - rel) : rel);
+    *order_out = order;
+    const uint32_t sp = (uint32_t)(s0 + 64);     // < 2^15
+    *lk = (r.c_local << 17) | (strand << 16) | (strand ? 0xFFFFu - sp : sp);
+    *lvalid_out = lvalid;
     uint64_t key = a.invalid_key;
-    Agg val;
-    val.first = ~0ull;
-    val.count = 0;
-    if ((li & 3) == 1) {
-        const uint64_t lstart = lvalid ? tile_abs + r.lstart : a.lnl_before[t];
-        const uint64_t sabs = tile_abs + (uint64_t)(int64_t)s0;
-        const uint64_t rel = sabs - lstart;
-        if (rel > MAXREL) {
-            atomicOr(a.err, ERR_LINE_TOO_LONG);
+    if (seq) {
+        if (a.packed && !exotic) {
+            key = (strand ? revcomp_code(r.code, a.k) : r.code) & a.smask;
         } else {
-            const uint64_t order = (li << 24) | ((uint64_t)strand << 23) |
-                                   (strand ? (uint64_t)(MAXREL - rel) : rel);
-            if (a.packed && !exotic) {
-                key = (strand ? revcomp_code(r.code, a.k) : r.code) & a.smask;
-                val.first = order;
-                val.count = 1;
+            const unsigned long long n = atomicAdd(a.rec_count, 1ull);
+            if (n < a.rec_cap) {
+                Record rec;
+                rec.order = order;
+                rec.pos = (uint64_t)t * TILE + (uint64_t)(int64_t)s0;
+                rec.len = a.k;
+                rec.strand = strand;
+                a.recs[n] = rec;
             } else {
-                const unsigned long long n = atomicAdd(a.rec_count, 1ull);
-                if (n < a.rec_cap) {
-                    Record rec;
-                    rec.order = order;
-                    rec.pos = (uint64_t)t * TILE + (uint64_t)(int64_t)s0;
-                    rec.len = a.k;
-                    rec.strand = strand;
-                    a.recs[n] = rec;
-                } else {
-                    atomicOr(a.err, ERR_REC_OVERFLOW);
-                }
+                atomicOr(a.err, ERR_REC_OVERFLOW);
             }
         }
     }
-    if (a.out_key) {
-        a.out_key[slot] = key;
-        a.out_val[slot] = val;
+    return key;
+}
+
+// One wave per tile.  Packed mode: lane i takes the tile's i-th stored hit,
+// ranks it among the tile's hits by (line, strand, +-offset) with a 64-lane
+// compare, and writes it at rank out_base + hits-before-tile + local rank --
+// unless its line crosses a tile edge (or the tile overflowed), in which case
+// it goes to the cross list with that natural slot.
+__global__ __launch_bounds__(256) void hit_kernel(HitArgs a) {
+    const uint32_t t = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (t >= a.n_tiles || *a.ovf_count > a.ovf_cap) return;   // overflowed scan: the host redoes the chunk
+    const uint32_t lane = threadIdx.x & 63;
+    const TileSum ts = a.tsum[t];
+    const TileSum tb = a.tscan[t];
+    const uint32_t n = (uint32_t)ts.nh;
+    const uint32_t m = min(n, (uint32_t)HMAX);
+    const bool have = lane < m;
+    const bool over = n > (uint32_t)HMAX;
+    uint64_t order = 0, key = a.invalid_key;
+    uint32_t lk = 0xFFFFFFFFu, c_local = 0;
+    bool lvalid = false;
+    if (have) {
+        const HitRec r = a.hits[(uint64_t)t * HMAX + lane];
+        key = resolve_hit(a, r, tb, &order, &lk, &lvalid);
+        c_local = r.c_local;
+    }
+    if (!a.packed) return;
+    const bool cross = have && (over || !lvalid || c_local == (uint32_t)ts.cnt);
+    // rank among the tile's hits, and among its cross hits (so that the cross
+    // list is in slot order); an overflowed tile uses the in-tile ordinal
+    uint32_t rank = lane, xr = lane;
+    if (!over) {
+        const uint64_t cm = __ballot(cross);
+        rank = 0;
+        xr = 0;
+        for (uint32_t j = 0; j < m; ++j) {
+            const uint32_t less = __shfl(lk, (int)j) < lk ? 1u : 0u;
+            rank += less;
+            xr += less & (uint32_t)(cm >> j);
+        }
+    }
+    if (!have) return;
+    const uint64_t slot = a.out_base + tb.nh + rank;
+    a.ridx[slot] = (uint32_t)slot;
+    if (!cross) {
+        a.rkey[slot] = key;
+        a.rord[slot] = order;
+    } else {
+        const uint64_t xi = a.xbase + tb.nx + xr;
+        if (xi < a.xcap) {
+            a.xord[xi] = order;
+            a.xkey[xi] = key;
+            a.xslot[xi] = (uint32_t)slot;
+        } else {
+            atomicOr(a.err, ERR_CROSS_OVERFLOW);
+        }
     }
 }
 
-// one wave per tile: lane i resolves the tile's i-th hit into slot
-// out_base + hscan[tile] + i (hscan = exclusive scan of the per-tile counts)
-__global__ __launch_bounds__(256) void hit_kernel(HitArgs a) {
-    const uint32_t t = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (t >= a.n_tiles || *a.ovf_count > a.ovf_cap) return;   // overflowed scan: the host redoes the chunk
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t n = a.tile_nhits[t];
-    const uint64_t base = a.out_base + a.hscan[t];
-    for (uint32_t h = lane; h < n; h += 64) resolve_hit(a, a.hits[(uint64_t)t * HMAX + h], base + h);
-}
-
-// hits that did not fit their tile's slots; they follow all tile hits
+// hits that did not fit their tile's slots (their tile is all cross)
 __global__ __launch_bounds__(256) void hit_overflow_kernel(HitArgs a) {
     if (*a.ovf_count > a.ovf_cap) return;
     const uint64_t n = *a.ovf_count;
-    const uint64_t base = a.out_base + a.hscan[a.n_tiles - 1] + a.tile_nhits[a.n_tiles - 1];
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-        resolve_hit(a, a.ovf[i], base + i);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const HitRec r = a.ovf[i];
+        const TileSum tb = a.tscan[r.tile];
+        uint64_t order;
+        uint32_t lk;
+        bool lvalid;
+        const uint64_t key = resolve_hit(a, r, tb, &order, &lk, &lvalid);
+        if (!a.packed) continue;
+        const uint32_t ord = r.qm >> 17;
+        const uint64_t slot = a.out_base + tb.nh + ord;
+        a.ridx[slot] = (uint32_t)slot;
+        const uint64_t xi = a.xbase + tb.nx + ord;
+        if (xi < a.xcap) {
+            a.xord[xi] = order;
+            a.xkey[xi] = key;
+            a.xslot[xi] = (uint32_t)slot;
+        } else {
+            atomicOr(a.err, ERR_CROSS_OVERFLOW);
+        }
+    }
 }
 
-// advance the running stream position past this chunk
-__global__ void pos_update_kernel(StreamPos *pos, const uint64_t *cscan, const uint64_t *agg_cnt, uint32_t n_tiles,
-                                  const uint8_t *data, uint64_t len) {
+// advance the running stream position past this chunk; hits of the chunk
+__global__ void pos_update_kernel(StreamPos *pos, const TileSum *tsum, const TileSum *tscan, uint32_t n_tiles,
+                                  const uint8_t *data, uint64_t len, unsigned long long *chunk_hits,
+                                  unsigned long long *chunk_cross) {
     if (threadIdx.x == 0 && blockIdx.x == 0) {   // (a redo after an overflow restores pos first)
-        pos->lines += cscan[n_tiles - 1] + agg_cnt[n_tiles - 1];
+        pos->lines += tscan[n_tiles - 1].cnt + tsum[n_tiles - 1].cnt;
         pos->ends_open = (len > 0 && data[len - 1] != '\n') ? 1 : 0;
+        *chunk_hits = tscan[n_tiles - 1].nh + tsum[n_tiles - 1].nh;
+        *chunk_cross = tscan[n_tiles - 1].nx + tsum[n_tiles - 1].nx;
     }
 }
 
@@ -856,43 +935,193 @@ __global__ __launch_bounds__(256) void windows_kernel(WindowArgs a) {
 // ---------------------------------------------------------------------------
 // result materialisation
 // ---------------------------------------------------------------------------
-// unique (key, {first, count}) -> (first, index) for the order sort
-__global__ __launch_bounds__(256) void split_first_kernel(const Agg *uval, uint64_t n, uint64_t *first,
-                                                          uint64_t *idx) {
+// Cross entries (in natural-slot order) sorted by order key: the i-th
+// smallest order takes the i-th natural slot.  Large lists: radix-sorted on
+// the host side of the pipeline, then cross_scatter_kernel.
+__global__ __launch_bounds__(256) void cross_scatter_kernel(const uint32_t *slot, const uint64_t *ord,
+                                                            const uint64_t *key, uint64_t n, uint64_t *rkey,
+                                                            uint64_t *rord) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        first[i] = uval[i].first;
-        idx[i] = i;
+        const uint32_t sl = slot[i];
+        rkey[sl] = key[i];
+        rord[sl] = ord[i];
     }
 }
 
-// Ordered output: entry i = unique entry idx[i]; key bytes = P + decode(code)
-// (k bytes, first base most significant), count.  One thread per entry; the
-// key is built in registers and written with dword stores when k % 4 == 0.
-__global__ __launch_bounds__(256) void packed_decode_kernel(const uint64_t *idx, uint64_t n, const uint64_t *ukey,
-                                                            const Agg *uval, uint32_t k, uint32_t plen,
-                                                            const uint8_t *P, uint8_t *keys_out,
-                                                            uint64_t *counts_out) {
-    const uint32_t sl = k - plen;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t e = idx[i];
-        const uint64_t code = ukey[e];
-        counts_out[i] = uval[e].count;
-        uint8_t *o = keys_out + i * k;
-        if ((k & 3) == 0) {
-            for (uint32_t b = 0; b < k; b += 4) {
-                uint32_t wv = 0;
-                for (uint32_t j = 0; j < 4; ++j) {
-                    const uint32_t pos = b + j;
-                    const uint32_t ch = pos < plen ? P[pos]
-                                                   : (uint32_t)(uint8_t)"ACGT"[(code >> (2 * (sl - 1 - (pos - plen)))) & 3u];
-                    wv |= ch << (8 * j);
+// Small lists (n <= XSMALL): one workgroup, bitonic sort of (order, index) in
+// LDS, then the scatter.
+constexpr uint32_t XSMALL = 16384;
+__global__ __launch_bounds__(1024) void cross_sort_small_kernel(const uint32_t *slot, const uint64_t *ord,
+                                                                const uint64_t *key, uint32_t n, uint64_t *rkey,
+                                                                uint64_t *rord) {
+    __shared__ uint64_t so[XSMALL];
+    __shared__ uint16_t si[XSMALL];
+    uint32_t N = 2;
+    while (N < n) N <<= 1;
+    for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
+        so[i] = i < n ? ord[i] : ~0ull;
+        si[i] = (uint16_t)i;
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= N; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < N; i += blockDim.x) {
+                const uint32_t p = i ^ j;
+                if (p > i) {
+                    const uint64_t x = so[i], y = so[p];
+                    const bool asc = (i & k) == 0;
+                    if ((x > y) == asc) {
+                        so[i] = y;
+                        so[p] = x;
+                        const uint16_t t = si[i];
+                        si[i] = si[p];
+                        si[p] = t;
+                    }
                 }
-                *(uint32_t *)(o + b) = wv;
             }
-        } else {
-            for (uint32_t pos = 0; pos < k; ++pos)
-                o[pos] = pos < plen ? P[pos] : (uint8_t)"ACGT"[(code >> (2 * (sl - 1 - (pos - plen)))) & 3u];
+            __syncthreads();
         }
+    }
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t sl = slot[i];
+        rkey[sl] = key[si[i]];
+        rord[sl] = so[i];
+    }
+}
+
+// Common case (no long lines, no overflowed tile): the cross list is already
+// ordered by line, and one line's entries come from at most two tiles
+// (<= 2 * HMAX).  One thread per line segment: insertion sort by order key,
+// then the scatter to the natural slots.
+__global__ __launch_bounds__(256) void cross_segsort_kernel(uint64_t *ord, uint64_t *key, const uint32_t *slot,
+                                                            uint64_t n, uint64_t *rkey, uint64_t *rord) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t line = ord[i] >> 24;      // (the line bits of a segment never change while it is sorted)
+        if (i > 0 && (ord[i - 1] >> 24) == line) continue;
+        uint64_t e = i + 1;
+        while (e < n && (ord[e] >> 24) == line) ++e;
+        for (uint64_t j = i + 1; j < e; ++j) {
+            const uint64_t v = ord[j], kv = key[j];
+            uint64_t p = j;
+            while (p > i && ord[p - 1] > v) {
+                ord[p] = ord[p - 1];
+                key[p] = key[p - 1];
+                --p;
+            }
+            ord[p] = v;
+            key[p] = kv;
+        }
+        for (uint64_t j = i; j < e; ++j) {
+            const uint32_t sl = slot[j];
+            rkey[sl] = key[j];
+            rord[sl] = ord[j];
+        }
+    }
+}
+
+// End of the key group starting at sorted index i: galloping then binary search.
+__device__ __forceinline__ uint64_t group_end(const uint64_t *skey, uint64_t i, uint64_t n, uint64_t key) {
+    uint64_t lo = i, step = 1, hi = n;
+    for (;;) {
+        const uint64_t p = lo + step;
+        if (p >= n || skey[p] != key) {
+            hi = p < n ? p : n;
+            break;
+        }
+        lo = p;
+        step <<= 1;
+    }
+    while (hi - lo > 1) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (skey[mid] == key) lo = mid;
+        else hi = mid;
+    }
+    return hi;
+}
+
+// After the stable key sort (payload = rank): the first element of each key
+// group has the smallest rank = the key's first occurrence.  Every rank gets
+// its record written (srank is a permutation), so no clearing pass is needed.
+__global__ __launch_bounds__(256) void heads_kernel(const uint64_t *skey, const uint32_t *srank, uint64_t n,
+                                                    uint64_t invalid_key, const uint64_t *rcnt, HeadRec *hrec) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = skey[i];
+        HeadRec v;
+        v.key = 0;
+        v.count = 0;
+        if (k != invalid_key && (i == 0 || skey[i - 1] != k)) {
+            const uint64_t e = group_end(skey, i, n, k);
+            uint64_t cnt = e - i;
+            if (rcnt) {
+                cnt = 0;
+                for (uint64_t j = i; j < e; ++j) cnt += rcnt[srank[j]];
+            }
+            v.key = k;
+            v.count = cnt;
+        }
+        hrec[srank[i]] = v;
+    }
+}
+
+// One thread per rank; flagged ranks emit output entry opos[rank]: decoded key
+// (P + suffix, 'ACGT' from the 2-bit code, first base most significant),
+// count, first-occurrence order -- or the packed (code, {first, count}) pair
+// for a partial result.
+__global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
+    const uint64_t n = a.n;
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
+        const HeadRec v = a.hrec[r];
+        const uint32_t o = a.opos[r];
+        if (r == n - 1) *a.nuniq = (uint64_t)o + (v.count ? 1u : 0u);
+        if (!v.count) continue;
+        const uint64_t key = v.key, cnt = v.count;
+        const uint64_t first = a.rord[r];
+        if (a.partial) {
+            a.ukey[o] = key;
+            Agg v;
+            v.first = first;
+            v.count = cnt;
+            a.uval[o] = v;
+            continue;
+        }
+        a.cnt_out[o] = cnt;
+        a.first_out[o] = first;
+        const uint32_t k = a.k, plen = a.plen;
+        uint8_t *out = a.keys_out + (uint64_t)o * k;
+        uint32_t words[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t pos = 4 * w + j;
+                uint32_t ch = 0;
+                if (pos < plen) ch = a.P[pos];
+                else if (pos < k) ch = (0x54474341u >> (8 * ((uint32_t)(key >> (2 * (k - 1 - pos))) & 3u))) & 0xFFu;
+                v |= ch << (8 * j);
+            }
+            words[w] = v;
+        }
+        if (k == 16) {
+            *(uint4 *)out = make_uint4(words[0], words[1], words[2], words[3]);
+        } else if ((k & 3) == 0) {
+            for (uint32_t w = 0; w < k / 4; ++w) *(uint32_t *)(out + 4 * w) = words[w];
+        } else {
+            for (uint32_t b = 0; b < k; ++b) out[b] = (uint8_t)(words[b >> 2] >> (8 * (b & 3)));
+        }
+    }
+}
+
+// merged partials (in shard order = first-occurrence order) -> rank arrays
+__global__ __launch_bounds__(256) void merge_prep_kernel(const uint64_t *keys, const Agg *vals, uint64_t n,
+                                                         uint64_t *rkey, uint64_t *rord, uint64_t *rcnt,
+                                                         uint32_t *ridx) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const Agg v = vals[i];
+        rkey[i] = keys[i];
+        rord[i] = v.first;
+        rcnt[i] = v.count;
+        ridx[i] = (uint32_t)i;
     }
 }
 
@@ -984,12 +1213,13 @@ hipError_t launch_hits(const HitArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_pos_update(StreamPos *pos, const uint64_t *cscan, const uint64_t *agg_cnt, uint32_t n_tiles,
-                             const uint8_t *data, uint64_t len, hipStream_t s) {
-    hipLaunchKernelGGL(pos_update_kernel, dim3(1), dim3(64), 0, s, pos, cscan, agg_cnt, n_tiles, data, len);
+hipError_t launch_pos_update(StreamPos *pos, const TileSum *tsum, const TileSum *tscan, uint32_t n_tiles,
+                             const uint8_t *data, uint64_t len, unsigned long long *chunk_hits,
+                             unsigned long long *chunk_cross, hipStream_t s) {
+    hipLaunchKernelGGL(pos_update_kernel, dim3(1), dim3(64), 0, s, pos, tsum, tscan, n_tiles, data, len, chunk_hits,
+                       chunk_cross);
     return hipGetLastError();
 }
-
 hipError_t launch_tile_aggregate(const uint8_t *data, uint64_t len, uint32_t n_tiles, uint64_t *agg_cnt,
                                  uint64_t *agg_lnl, unsigned int *err, hipStream_t s) {
     hipLaunchKernelGGL(tile_aggregate_kernel, dim3(n_tiles), dim3(TPB), 0, s, data, len, agg_cnt, agg_lnl, err);
@@ -1007,19 +1237,36 @@ static uint32_t grid_for(uint64_t n) {
     return (uint32_t)(blocks ? blocks : 1);
 }
 
-hipError_t launch_split_first(const Agg *uval, uint64_t n, uint64_t *first, uint64_t *idx, hipStream_t s) {
-    hipLaunchKernelGGL(split_first_kernel, dim3(grid_for(n)), dim3(256), 0, s, uval, n, first, idx);
+hipError_t launch_cross_scatter(const uint32_t *slot, const uint64_t *ord, const uint64_t *key, uint64_t n,
+                                uint64_t *rkey, uint64_t *rord, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(cross_scatter_kernel, dim3(grid_for(n)), dim3(256), 0, s, slot, ord, key, n, rkey, rord);
     return hipGetLastError();
 }
-
-hipError_t launch_packed_decode(const uint64_t *idx, uint64_t n, const uint64_t *ukey, const Agg *uval, uint32_t k,
-                                uint32_t plen, const uint8_t *P, uint8_t *keys_out, uint64_t *counts_out,
-                                hipStream_t s) {
-    hipLaunchKernelGGL(packed_decode_kernel, dim3(grid_for(n)), dim3(256), 0, s, idx, n, ukey, uval, k, plen, P,
-                       keys_out, counts_out);
+hipError_t launch_cross_sort_small(const uint32_t *slot, const uint64_t *ord, const uint64_t *key, uint64_t n,
+                                   uint64_t *rkey, uint64_t *rord, hipStream_t s) {
+    if (n > XSMALL) return hipErrorInvalidValue;
+    if (n) hipLaunchKernelGGL(cross_sort_small_kernel, dim3(1), dim3(1024), 0, s, slot, ord, key, (uint32_t)n, rkey, rord);
     return hipGetLastError();
 }
-
+hipError_t launch_cross_segsort(uint64_t *ord, uint64_t *key, const uint32_t *slot, uint64_t n, uint64_t *rkey,
+                                uint64_t *rord, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(cross_segsort_kernel, dim3(grid_for(n)), dim3(256), 0, s, ord, key, slot, n, rkey, rord);
+    return hipGetLastError();
+}
+hipError_t launch_heads(const uint64_t *skey, const uint32_t *srank, uint64_t n, uint64_t invalid_key,
+                        const uint64_t *rcnt, HeadRec *hrec, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(heads_kernel, dim3(grid_for(n)), dim3(256), 0, s, skey, srank, n, invalid_key, rcnt, hrec);
+    return hipGetLastError();
+}
+hipError_t launch_emit(const EmitArgs &a, hipStream_t s) {
+    if (a.n) hipLaunchKernelGGL(emit_kernel, dim3(grid_for(a.n)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+hipError_t launch_merge_prep(const uint64_t *keys, const Agg *vals, uint64_t n, uint64_t *rkey, uint64_t *rord,
+                             uint64_t *rcnt, uint32_t *ridx, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(merge_prep_kernel, dim3(grid_for(n)), dim3(256), 0, s, keys, vals, n, rkey, rord, rcnt, ridx);
+    return hipGetLastError();
+}
 hipError_t launch_gather_records(const Record *recs, const uint64_t *key_off, uint64_t n, const uint8_t *data,
                                  uint8_t *out, hipStream_t s) {
     if (n == 0) return hipSuccess;

@@ -253,3 +253,24 @@ def test_full_size_properties(native):
     assert np.array_equal(merged.counts, res.counts)
     assert np.array_equal(merged.firsts, res.firsts)
     assert merged.keybuf == res.keybuf
+
+
+def test_long_lines_and_dense_hits(native):
+    # lines spanning many tiles (every hit on the cross path, > one-workgroup sort)
+    # and hit-dense prefixes (tiles overflowing their hit slots)
+    from oracle import oracle
+    rng = np.random.default_rng(5)
+    recs = []
+    for i, L in enumerate((300_000, 70_000, 151, 250_000)):
+        seq = bytes(rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), L))
+        recs.append(b"@c%d\n" % i + seq + b"\n+\n" + b"I" * L + b"\n")
+    data = b"".join(recs)
+    short = oracle.synth_fastq(9, 0, 3000)
+    for buf, k, p in ((data, 16, b"AC"), (data, 21, b"ATGAC"), (short, 8, b"A"), (short, 12, b"AC"),
+                      (data, 32, b"G")):
+        want = oracle.count_buffer(buf, p, k, 1)
+        ctr = native.Counter(k=k, prefix=p)
+        got = ctr.count_buffer(buf).entries()
+        ctr.close()
+        assert len(got) == len(want), (k, p)
+        assert first_diff(got, want) is None, (k, p)
