@@ -1079,10 +1079,8 @@ kmer_status kmer_records_import(kmer_ctx *c, const char *keys, const uint64_t *o
 
 kmer_status kmer_set_position(kmer_ctx *c, uint64_t lines_before, uint64_t byte_offset) {
     if (!c) return KMER_E_BAD_PARAM;
-    StreamPos pos{};
-    pos.lines = lines_before;
-    HIPCHK(c, hipMemcpyAsync(c->d_pos, &pos, sizeof(pos), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
+    HIPCHK(c, launch_set_pos(c->d_pos, lines_before, c->stream));
     c->abs_offset = byte_offset;
     return KMER_OK;
 }

@@ -213,6 +213,7 @@ hipError_t launch_hits(const HitArgs &a, hipStream_t s);
 hipError_t launch_pos_update(StreamPos *pos, const TileSum *tsum, const TileSum *tscan, uint32_t n_tiles,
                              const uint8_t *data, uint64_t len, unsigned long long *chunk_hits,
                              unsigned long long *chunk_cross, hipStream_t s);
+hipError_t launch_set_pos(StreamPos *pos, uint64_t lines, hipStream_t s);
 hipError_t launch_tile_aggregate(const uint8_t *data, uint64_t len, uint32_t n_tiles, uint64_t *agg_cnt,
                                  uint64_t *agg_lnl, unsigned int *err, hipStream_t s);
 hipError_t launch_windows(const WindowArgs &a, uint32_t grid, hipStream_t s);

@@ -393,7 +393,7 @@ struct ScanShared {
     uint32_t nx;                 // ... of which on lines that cross a tile edge
     uint32_t tcnt;               // real '\n' count of the tile
     uint32_t qn;                 // verified-hit queue fill
-    uint32_t q[QCAP];            // verified hits: (tile position << 1) | strand
+    uint32_t q[QCAP];            // candidate words: tile position of the word's first window
 };
 
 // last '\n' (tile-relative) inside 16-byte chunk c at a position < limit, -1 if none
@@ -486,6 +486,37 @@ __device__ __forceinline__ void emit_hit(const ScanArgs &a, const uint8_t *buf, 
         const unsigned long long o = atomicAdd(a.ovf_count, 1ull);
         if (o < a.ovf_cap) a.ovf[o] = r;
         else atomicOr(a.err, ERR_OVF_OVERFLOW);
+    }
+}
+
+// One candidate word (4 window starts at tile position q0 with a 4-byte
+// match on some strand): exact prefix test of its 8 (position, strand)
+// windows, then one hit record per verified window.
+__device__ __forceinline__ void scan_word(const ScanArgs &a, const uint8_t *buf, ScanShared &sh, uint32_t tile,
+                                          const uint32_t *pw, uint32_t q0) {
+    const uint32_t plen = a.plen, P4 = a.p4, R4 = a.r4, PM = a.pmask;
+    const uint32_t lo = *(const uint32_t *)(buf + FH + q0);
+    const uint32_t hi = *(const uint32_t *)(buf + FH + q0 + 4);
+    uint32_t bits = 0;
+#pragma unroll
+    for (uint32_t jj = 0; jj < 4; ++jj) {
+        const uint32_t win = align4(hi, lo, jj);
+        bits |= (((win ^ P4) & PM) == 0 ? 1u : 0u) << (2 * jj);
+        bits |= (((win ^ R4) & PM) == 0 ? 1u : 0u) << (2 * jj + 1);
+    }
+    while (bits) {
+        const uint32_t bit = __ffs(bits) - 1;
+        bits &= bits - 1;
+        const uint32_t strand = bit & 1u;
+        const int q = (int)q0 + (int)(bit >> 1);
+        bool ok = true;
+#pragma unroll 1
+        for (uint32_t b = 4; b < plen && ok; b += 4) {
+            const uint32_t n = plen - b;
+            const uint32_t mk = n >= 4 ? 0xFFFFFFFFu : ((1u << (8 * n)) - 1u);
+            ok = ((lds_word(buf, q + (int)b) ^ pw[(strand ? KMAX_TILE / 4 : 0) + b / 4]) & mk) == 0;
+        }
+        if (ok) emit_hit(a, buf, sh, tile, ((uint32_t)q << 1) | strand);
     }
 }
 
@@ -644,63 +675,43 @@ __global__ __launch_bounds__(TPB) void scan_tile_kernel(ScanArgs a) {
     if (plen > k || (a.ablate & 1u)) cand = 0;
     const uint32_t *pw = (const uint32_t *)s_pr;             // P words, then rc(P) words
 
-    // ---- candidates -> verified hits (each lane its own words, straight-line)
-    //      -> LDS queue -> hit records (one hit per lane: the rare, branchy work
-    //      runs once per tile in as few waves as possible) ----
+    // ---- candidate words -> LDS queue (one LDS atomic per wave) -> verified
+    //      hits -> hit records, one queued word per lane: the rare, branchy
+    //      work runs once per tile in as few waves as possible ----
     __syncthreads();             // cpre / nlmap visible
-    while (cand) {
-        const int bitc = __ffs(cand) - 1;
-        cand &= cand - 1;
-        const int q0 = 16 * (tid + TPB * (bitc >> 2)) + 4 * (bitc & 3);
-        const uint32_t lo = *(const uint32_t *)(buf + FH + q0);
-        const uint32_t hi = *(const uint32_t *)(buf + FH + q0 + 4);
-        uint32_t bits = 0;
-#pragma unroll
-        for (uint32_t jj = 0; jj < 4; ++jj) {
-            const uint32_t win = align4(hi, lo, jj);
-            bits |= (((win ^ P4) & PM) == 0 ? 1u : 0u) << (2 * jj);
-            bits |= (((win ^ R4) & PM) == 0 ? 1u : 0u) << (2 * jj + 1);
+    {
+        const uint32_t nc = __popc(cand);
+        const uint32_t incl_c = wave_incl_sum(nc);
+        const uint32_t wtotal = (uint32_t)__builtin_amdgcn_readlane((int)incl_c, 63);
+        uint32_t pos = 0;
+        if (wtotal) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&sh.qn, wtotal);
+            pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)base, 0)) + incl_c - nc;
         }
-        if (plen > 4) {
-            uint32_t check = bits;
-            while (check) {
-                const uint32_t bit = __ffs(check) - 1;
-                check &= check - 1;
-                const uint32_t strand = bit & 1u;
-                const int q = q0 + (int)(bit >> 1);
-                bool ok = true;
-#pragma unroll 1
-                for (uint32_t b = 4; b < plen && ok; b += 4) {
-                    const uint32_t n = plen - b;
-                    const uint32_t mk = n >= 4 ? 0xFFFFFFFFu : ((1u << (8 * n)) - 1u);
-                    ok = ((lds_word(buf, q + (int)b) ^ pw[(strand ? KMAX_TILE / 4 : 0) + b / 4]) & mk) == 0;
-                }
-                if (!ok) bits &= ~(1u << bit);
-            }
-        }
-        while (bits) {
-            const uint32_t bit = __ffs(bits) - 1;
-            bits &= bits - 1;
-            const uint32_t e = ((uint32_t)(q0 + (int)(bit >> 1)) << 1) | (bit & 1u);
-            const uint32_t slot = atomicAdd(&sh.qn, 1u);
-            if (slot < QCAP) sh.q[slot] = e;
-            else emit_hit(a, buf, sh, tile, e);      // queue full (short prefixes): process in place
+        while (cand) {
+            const int bitc = __ffs(cand) - 1;
+            cand &= cand - 1;
+            const uint32_t q0 = 16u * (uint32_t)(tid + TPB * (bitc >> 2)) + 4u * (uint32_t)(bitc & 3);
+            if (pos < QCAP) sh.q[pos] = q0;
+            else scan_word(a, buf, sh, tile, pw, q0);   // queue full (short prefixes): process in place
+            ++pos;
         }
     }
     __syncthreads();
     const uint32_t nq = min(sh.qn, (uint32_t)QCAP);
-    for (uint32_t h = tid; h < nq; h += TPB) emit_hit(a, buf, sh, tile, sh.q[h]);
+    for (uint32_t h = tid; h < nq; h += TPB) scan_word(a, buf, sh, tile, pw, sh.q[h]);
     if (nq > 64 || sh.qn > QCAP) {
         __syncthreads();         // uniform: every wave may have written records
         if (tid == 0) {
             a.tsum[tile].nh = sh.nh;
             a.tsum[tile].nx = sh.nh > (uint32_t)HMAX ? sh.nh : sh.nx;   // overflowed: all hits cross
-            if (sh.nh > (uint32_t)HMAX || sh.tcnt == 0) atomicOr(a.err, INFO_LONGSEG);
+            if (sh.nh > (uint32_t)HMAX || (sh.nh && sh.tcnt == 0)) atomicOr(a.err, INFO_LONGSEG);
         }
-    } else if (tid == 0) {                       // wave 0 wrote them all
+    } else if (tid == 0) {                       // wave 0 wrote them all (a word can hold 8 hits)
         a.tsum[tile].nh = sh.nh;
-        a.tsum[tile].nx = sh.nx;
-        if (sh.nh && sh.tcnt == 0) atomicOr(a.err, INFO_LONGSEG);
+        a.tsum[tile].nx = sh.nh > (uint32_t)HMAX ? sh.nh : sh.nx;
+        if (sh.nh > (uint32_t)HMAX || (sh.nh && sh.tcnt == 0)) atomicOr(a.err, INFO_LONGSEG);
     }
 }
 
@@ -834,6 +845,16 @@ __global__ __launch_bounds__(256) void hit_overflow_kernel(HitArgs a) {
         } else {
             atomicOr(a.err, ERR_CROSS_OVERFLOW);
         }
+    }
+}
+
+// set the running stream position (kernel argument: no host staging, no sync)
+__global__ void set_pos_kernel(StreamPos *pos, uint64_t lines) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        pos->lines = lines;
+        pos->unused = 0;
+        pos->ends_open = 0;
+        pos->pad = 0;
     }
 }
 
@@ -1218,6 +1239,10 @@ hipError_t launch_pos_update(StreamPos *pos, const TileSum *tsum, const TileSum 
                              unsigned long long *chunk_cross, hipStream_t s) {
     hipLaunchKernelGGL(pos_update_kernel, dim3(1), dim3(64), 0, s, pos, tsum, tscan, n_tiles, data, len, chunk_hits,
                        chunk_cross);
+    return hipGetLastError();
+}
+hipError_t launch_set_pos(StreamPos *pos, uint64_t lines, hipStream_t s) {
+    hipLaunchKernelGGL(set_pos_kernel, dim3(1), dim3(64), 0, s, pos, lines);
     return hipGetLastError();
 }
 hipError_t launch_tile_aggregate(const uint8_t *data, uint64_t len, uint32_t n_tiles, uint64_t *agg_cnt,
