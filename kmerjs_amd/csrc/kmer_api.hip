@@ -94,16 +94,21 @@ struct kmer_ctx {
 
     // per tile
     uint64_t tile_cap = 0;
-    DBuf<TileSum> tsum, tscan;
+    DBuf<TileSum> tsum, tscan, bsum, bscan;
     DBuf<HitRec> hits, ovf;
     DBuf<unsigned long long> lb_cnt, lb_lnl;   // general path look-back
     DBuf<uint64_t> tp_cnt, tp_lnl;             // general path, two-pass debug mode
     // session packed hits, by rank (first-occurrence order of all hits)
     uint64_t n_hits = 0, n_cross = 0;
     DBuf<uint64_t> rkey, rkey2, rord, rcnt;
+    DBuf<uint32_t> rkey32, rkey32b;   // narrow keys: 2(k-|P|) + 1 <= 32 bits
+    bool narrow = false;
     DBuf<uint32_t> ridx, ridx2, opos;
     DBuf<HeadRec> hrec;
     bool long_seg = false;         // INFO_LONGSEG seen this session
+    bool chunk_open = false;       // the last chunk did not end with '\n'
+    bool out_pending = false;      // unique count of the last finish not yet read back (h_small[13])
+    bool timing_pending = false;   // finish events not yet read
     DBuf<uint64_t> xord, xord2, xkey, xkey2;   // cross list
     DBuf<uint32_t> xslot;
     // finish outputs
@@ -119,11 +124,11 @@ struct kmer_ctx {
     DBuf<uint8_t> tmp;
     // device scalars, one block so that a feed reads them back with one copy:
     // [0] rec_count [1] ovf_count [2] cross count [3] chunk hits [4] unique keys
-    // [5] err (u32) [6] line count
+    // [5] err (u32) [6] line count [7] chunk ends open
     uint64_t *d_scal = nullptr;
     unsigned int *d_ticket = nullptr, *d_err = nullptr;
     unsigned long long *d_rec_count = nullptr, *d_line_count = nullptr, *d_ovf_count = nullptr;
-    unsigned long long *d_xcount = nullptr, *d_chunk_hits = nullptr;
+    unsigned long long *d_xcount = nullptr, *d_chunk_hits = nullptr, *d_ends_open = nullptr;
     uint64_t *d_nuniq = nullptr;
     StreamPos *d_pos = nullptr, *d_pos_saved = nullptr;
     uint8_t *d_P = nullptr;        // prefix bytes (decode)
@@ -210,6 +215,8 @@ kmer_status ensure_tiles(kmer_ctx *c, uint64_t n_tiles) {
     } else {
         HIPCHK(c, c->tsum.ensure(cap, s));
         HIPCHK(c, c->tscan.ensure(cap, s));
+        HIPCHK(c, c->bsum.ensure(cap / TSCAN_BLOCK + 2, s));
+        HIPCHK(c, c->bscan.ensure(cap / TSCAN_BLOCK + 2, s));
         HIPCHK(c, c->hits.ensure(cap * HMAX, s));
     }
     c->tile_cap = cap;
@@ -269,20 +276,14 @@ struct IsHead {
 };
 
 struct TileSumOp {
-    __host__ __device__ TileSum operator()(const TileSum &x, const TileSum &y) const {
-        TileSum r;
-        r.cnt = x.cnt + y.cnt;
-        r.lnl = x.lnl > y.lnl ? x.lnl : y.lnl;
-        r.nh = x.nh + y.nh;
-        r.nx = x.nx + y.nx;
-        return r;
-    }
+    __host__ __device__ TileSum operator()(const TileSum &x, const TileSum &y) const { return tile_sum_op(x, y); }
 };
 
 // Grow the session rank arrays (preserving the first `keep` entries).
 kmer_status ensure_rank_arrays(kmer_ctx *c, uint64_t need, uint64_t keep, hipStream_t s) {
     if (need >= (1ull << 32)) return fail(c, KMER_E_TOO_MANY_KEYS, "more than 2^32 prefix hits in one session");
-    HIPCHK(c, c->rkey.ensure(need, s, true, keep));
+    if (c->narrow) HIPCHK(c, c->rkey32.ensure(need, s, true, keep));
+    else HIPCHK(c, c->rkey.ensure(need, s, true, keep));
     HIPCHK(c, c->rord.ensure(need, s, true, keep));
     HIPCHK(c, c->ridx.ensure(need, s, true, keep));
     return KMER_OK;
@@ -348,6 +349,7 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
     h.err = c->d_err;
     auto bind_session = [&]() {
         h.rkey = c->rkey.p;
+        h.rkey32 = c->narrow ? c->rkey32.p : nullptr;
         h.rord = c->rord.p;
         h.ridx = c->ridx.p;
         h.xord = c->xord.p;
@@ -357,7 +359,12 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
         h.xcap = c->xord.cap;
     };
     bind_session();
-    const TileSum init{0, c->abs_offset, 0, 0};
+    TileSum init;
+    init.cnt = 0;
+    init.nh = 0;
+    init.nx = 0;
+    init.lnl = c->abs_offset;
+    const uint32_t n_blocks = (n_tiles + TSCAN_BLOCK - 1) / TSCAN_BLOCK;
 
     HIPCHK(c, hipMemcpyAsync(c->d_pos_saved, c->d_pos, sizeof(StreamPos), hipMemcpyDeviceToDevice, s));
     for (int attempt = 0; attempt < 8; ++attempt) {
@@ -365,10 +372,18 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
         HIPCHK(c, hipEventRecord(c->ev0, s));
         HIPCHK(c, launch_scan_tiles(a, s));
         HIPCHK(c, hipEventRecord(c->ev1, s));
-        ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tsum.p, c->tscan.p, init, (size_t)n_tiles, TileSumOp(), s));
+        HIPCHK(c, launch_tile_reduce(c->tsum.p, n_tiles, c->bsum.p, s));
+        if (n_blocks > TSCAN_INLINE_MAX) {
+            TileSum zero;
+            memset(&zero, 0, sizeof(zero));
+            ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->bsum.p, c->bscan.p, zero, (size_t)n_blocks, TileSumOp(), s));
+            HIPCHK(c, launch_tile_scan(c->tsum.p, n_tiles, c->bscan.p, true, init, c->tscan.p, s));
+        } else {
+            HIPCHK(c, launch_tile_scan(c->tsum.p, n_tiles, c->bsum.p, false, init, c->tscan.p, s));
+        }
         HIPCHK(c, launch_hits(h, s));
         HIPCHK(c, launch_pos_update(c->d_pos, c->tsum.p, c->tscan.p, n_tiles, d, len, c->d_chunk_hits, c->d_xcount,
-                                    s));
+                                    c->d_ends_open, s));
         HIPCHK(c, hipEventRecord(c->ev4, s));
         HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
@@ -415,6 +430,7 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
         c->n_cross += c->h_small[2];
         c->long_seg |= (c->h_small[5] & INFO_LONGSEG) != 0;
     }
+    c->chunk_open = c->h_small[7] != 0;
     const uint64_t nrec = c->h_small[0];
     if (nrec) {
         st = drain_records(c, d, nrec, s);
@@ -563,6 +579,8 @@ kmer_status feed(kmer_ctx *c, const uint8_t *d, uint64_t len, hipStream_t s) {
     const uint64_t n_tiles64 = (len + TILE - 1) / TILE;
     if (n_tiles64 > 0x7FFFFFFFull) return fail(c, KMER_E_BAD_PARAM, "chunk too large");
     const uint32_t n_tiles = (uint32_t)n_tiles64;
+    if (c->chunk_open)
+        return fail(c, KMER_E_BAD_PARAM, "the previous chunk did not end with '\\n' (chunks must be cut at line ends)");
     kmer_status st = ensure_tiles(c, n_tiles);
     if (st) return st;
     return c->mode == MODE_GENERAL ? general_feed(c, d, len, n_tiles, s) : scan_feed(c, d, len, n_tiles, s);
@@ -577,6 +595,9 @@ kmer_status reset(kmer_ctx *c) {
     c->n_hits = 0;
     c->n_cross = 0;
     c->long_seg = false;
+    c->chunk_open = false;
+    c->out_pending = false;
+    c->timing_pending = false;
     c->n_out = 0;
     c->scan_ms = c->feed_ms = c->finish_ms = 0.0;
     c->open_stream = true;
@@ -588,24 +609,64 @@ kmer_status reset(kmer_ctx *c) {
 // ---------------------------------------------------------------------------
 // Place the cross entries: sorted by order key they take the natural slots
 // sorted ascending (the slots that tile-local ranking left to them).
-kmer_status apply_cross(kmer_ctx *c, uint64_t max_line) {
+kmer_status read_pos(kmer_ctx *c, StreamPos *pos);
+
+kmer_status apply_cross(kmer_ctx *c) {
     hipStream_t s = c->stream;
     const uint64_t n = c->n_cross;
     if (n == 0) return KMER_OK;
+    uint32_t *k32 = c->narrow ? c->rkey32.p : nullptr;
     if (!c->long_seg) {
-        HIPCHK(c, launch_cross_segsort(c->xord.p, c->xkey.p, c->xslot.p, n, c->rkey.p, c->rord.p, s));
+        HIPCHK(c, launch_cross_segsort(c->xord.p, c->xkey.p, c->xslot.p, n, c->rkey.p, k32, c->rord.p, s));
     } else if (n <= XSMALL_MAX) {
-        HIPCHK(c, launch_cross_sort_small(c->xslot.p, c->xord.p, c->xkey.p, n, c->rkey.p, c->rord.p, s));
+        HIPCHK(c, launch_cross_sort_small(c->xslot.p, c->xord.p, c->xkey.p, n, c->rkey.p, k32, c->rord.p, s));
     } else {
+        StreamPos pos;
+        kmer_status st = read_pos(c, &pos);
+        if (st) return st;
         HIPCHK(c, c->xord2.ensure(n, s));
         HIPCHK(c, c->xkey2.ensure(n, s));
         rocprim::double_buffer<uint64_t> ob(c->xord.p, c->xord2.p);
         rocprim::double_buffer<uint64_t> kb(c->xkey.p, c->xkey2.p);
-        const int obits = std::min(64, bit_width(((max_line + 1) << 24) | 0xFFFFFFull));
+        const int obits = std::min(64, bit_width(((pos.lines + 1) << 24) | 0xFFFFFFull));
         ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, ob, kb, (size_t)n, 0, obits, s));
-        HIPCHK(c, launch_cross_scatter(c->xslot.p, ob.current(), kb.current(), n, c->rkey.p, c->rord.p, s));
+        HIPCHK(c, launch_cross_scatter(c->xslot.p, ob.current(), kb.current(), n, c->rkey.p, k32, c->rord.p, s));
     }
     c->n_cross = 0;
+    return KMER_OK;
+}
+
+// stable radix sort of (key, rank), then one head record per rank
+template <typename K>
+kmer_status sort_and_heads(kmer_ctx *c, K *keys, K *keys2, uint64_t n, bool with_counts) {
+    hipStream_t s = c->stream;
+    const uint64_t invalid = c->kbits >= 63 ? ~0ull : (1ull << c->kbits);
+    rocprim::double_buffer<K> kb(keys, keys2);
+    rocprim::double_buffer<uint32_t> vb(c->ridx.p, c->ridx2.p);
+    const int end_bit = std::min<int>(8 * (int)sizeof(K), (int)c->kbits + 1);   // + the invalid-key bit
+    ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, kb, vb, (size_t)n, 0, end_bit, s));
+    const uint64_t *rcnt = with_counts ? c->rcnt.p : nullptr;
+    if (sizeof(K) == 4)
+        HIPCHK(c, launch_heads32((const uint32_t *)kb.current(), vb.current(), n, (uint32_t)invalid, rcnt, c->hrec.p, s));
+    else
+        HIPCHK(c, launch_heads((const uint64_t *)kb.current(), vb.current(), n, invalid, rcnt, c->hrec.p, s));
+    return KMER_OK;
+}
+
+// resolve a deferred unique count (finish without a host result)
+kmer_status resolve_out(kmer_ctx *c) {
+    if (c->out_pending) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        c->n_out = c->h_small[13];
+        c->out_pending = false;
+    }
+    if (c->timing_pending) {
+        float ms = 0.f;
+        HIPCHK(c, hipEventSynchronize(c->ev3));
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev2, c->ev3));
+        c->finish_ms = ms;
+        c->timing_pending = false;
+    }
     return KMER_OK;
 }
 
@@ -614,11 +675,13 @@ kmer_status apply_cross(kmer_ctx *c, uint64_t max_line) {
 // their rank; a scan of the flags gives each unique key its output position.
 // partial: (code, {first, count}) into ukey/uval; else decoded keys, counts
 // and firsts into keys_out / cnt_out / first.  Returns the unique count.
-kmer_status rank_finish(kmer_ctx *c, uint64_t n, bool partial, bool with_counts, uint64_t *nu_out) {
+// sync = false: the unique count is copied back asynchronously (resolve_out).
+kmer_status rank_finish(kmer_ctx *c, uint64_t n, bool partial, bool with_counts, uint64_t *nu_out, bool sync = true) {
     hipStream_t s = c->stream;
     *nu_out = 0;
     if (n == 0) return KMER_OK;
-    HIPCHK(c, c->rkey2.ensure(n, s));
+    if (c->narrow) HIPCHK(c, c->rkey32b.ensure(n, s));
+    else HIPCHK(c, c->rkey2.ensure(n, s));
     HIPCHK(c, c->ridx2.ensure(n, s));
     HIPCHK(c, c->hrec.ensure(n, s));
     HIPCHK(c, c->opos.ensure(n, s));
@@ -631,11 +694,9 @@ kmer_status rank_finish(kmer_ctx *c, uint64_t n, bool partial, bool with_counts,
         HIPCHK(c, c->first.ensure(n, s));
     }
     const uint64_t invalid = c->kbits >= 63 ? ~0ull : (1ull << c->kbits);
-    rocprim::double_buffer<uint64_t> kb(c->rkey.p, c->rkey2.p);
-    rocprim::double_buffer<uint32_t> vb(c->ridx.p, c->ridx2.p);
-    const int end_bit = std::min<int>(64, (int)c->kbits + 1);   // + the invalid-key bit
-    ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, kb, vb, (size_t)n, 0, end_bit, s));
-    HIPCHK(c, launch_heads(kb.current(), vb.current(), n, invalid, with_counts ? c->rcnt.p : nullptr, c->hrec.p, s));
+    kmer_status st = c->narrow ? sort_and_heads<uint32_t>(c, c->rkey32.p, c->rkey32b.p, n, with_counts)
+                               : sort_and_heads<uint64_t>(c, c->rkey.p, c->rkey2.p, n, with_counts);
+    if (st) return st;
     auto is_head = rocprim::make_transform_iterator(c->hrec.p, IsHead());
     ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, is_head, c->opos.p, 0u, (size_t)n, rocprim::plus<uint32_t>(), s));
     EmitArgs e;
@@ -656,9 +717,13 @@ kmer_status rank_finish(kmer_ctx *c, uint64_t n, bool partial, bool with_counts,
     e.ukey = c->ukey.p;
     e.uval = c->uval.p;
     HIPCHK(c, launch_emit(e, s));
-    HIPCHK(c, hipMemcpyAsync(c->h_small + 4, c->d_nuniq, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(c->h_small + 13, c->d_nuniq, 8, hipMemcpyDeviceToHost, s));
+    if (!sync) {
+        c->out_pending = true;
+        return KMER_OK;
+    }
     HIPCHK(c, hipStreamSynchronize(s));
-    *nu_out = c->h_small[4];
+    *nu_out = c->h_small[13];
     return KMER_OK;
 }
 
@@ -716,31 +781,35 @@ kmer_status read_pos(kmer_ctx *c, StreamPos *pos) {
     return KMER_OK;
 }
 
+// Without a host result (`out` NULL) and without max_keys, nothing here waits
+// for the device: the unique count and the timing are read back lazily.
 kmer_status finish(kmer_ctx *c, kmer_result **out) {
     if (!c->open_stream) return fail(c, KMER_E_STATE, "finish without reset/feed");
-    StreamPos pos;
-    kmer_status st = read_pos(c, &pos);
-    if (st) return st;
+    kmer_status st;
     HIPCHK(c, hipEventRecord(c->ev2, c->stream));
     uint64_t nu = 0;
     c->n_out = 0;
+    const bool sync = out || c->p.max_keys;
     if (c->mode == MODE_PACKED) {
-        st = apply_cross(c, pos.lines);
+        st = apply_cross(c);
         if (st) return st;
-        st = rank_finish(c, c->n_hits, false, false, &nu);
+        st = rank_finish(c, c->n_hits, false, false, &nu, sync);
         if (st) return st;
         c->n_out = nu;
     }
     HIPCHK(c, hipEventRecord(c->ev3, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    float ms = 0.f;
-    HIPCHK(c, hipEventElapsedTime(&ms, c->ev2, c->ev3));
-    c->finish_ms = ms;
+    c->timing_pending = true;
     c->open_stream = false;
+    if (!sync) return KMER_OK;
+    st = resolve_out(c);
+    if (st) return st;
     const uint64_t total = c->n_out + c->exotic.size();
     if (c->p.max_keys && total > c->p.max_keys)
         return fail(c, KMER_E_TOO_MANY_KEYS, "more distinct keys than max_keys (reference Map limit)");
     if (!out) return KMER_OK;
+    StreamPos pos;
+    st = read_pos(c, &pos);
+    if (st) return st;
     return build_result(c, pos.lines + pos.ends_open, out);
 }
 
@@ -830,6 +899,7 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
     else
         c->mode = MODE_GENERAL;
     c->kbits = c->mode == MODE_PACKED ? 2 * (k - plen) : 0;
+    c->narrow = c->mode == MODE_PACKED && c->kbits <= 31;
 
     bool ok = true;
     ok &= dalloc(&c->d_P, std::max<uint32_t>(plen, 1)) == hipSuccess;
@@ -854,6 +924,7 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
         c->d_nuniq = c->d_scal + 4;
         c->d_err = (unsigned int *)(c->d_scal + 5);
         c->d_line_count = (unsigned long long *)(c->d_scal + 6);
+        c->d_ends_open = (unsigned long long *)(c->d_scal + 7);
     }
     ok &= dalloc(&c->d_pos, 1) == hipSuccess;
     ok &= dalloc(&c->d_pos_saved, 1) == hipSuccess;
@@ -878,7 +949,9 @@ kmer_status kmer_close(kmer_ctx *c) {
     for (auto *b : {&c->tp_cnt, &c->tp_lnl, &c->rkey, &c->rkey2, &c->rord, &c->rcnt, &c->xord, &c->xord2,
                     &c->xkey, &c->xkey2, &c->ukey, &c->first, &c->cnt_out, &c->roff})
         b->release();
-    for (auto *b : {&c->ridx, &c->ridx2, &c->opos, &c->xslot}) b->release();
+    for (auto *b : {&c->ridx, &c->ridx2, &c->opos, &c->xslot, &c->rkey32, &c->rkey32b}) b->release();
+    c->bsum.release();
+    c->bscan.release();
     c->hrec.release();
     c->tsum.release();
     c->tscan.release();
@@ -995,10 +1068,7 @@ kmer_status kmer_partial_device(kmer_ctx *c, const void **d_keys, const void **d
     if (!c || !d_keys || !d_vals || !n) return KMER_E_BAD_PARAM;
     if (c->mode != MODE_PACKED) return fail(c, KMER_E_STATE, "configuration has no packed keys");
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
-    StreamPos pos;
-    kmer_status st = read_pos(c, &pos);
-    if (st) return st;
-    st = apply_cross(c, pos.lines);
+    kmer_status st = apply_cross(c);
     if (st) return st;
     uint64_t nu = 0;
     st = rank_finish(c, c->n_hits, true, false, &nu);
@@ -1023,20 +1093,21 @@ kmer_status kmer_finish_merged(kmer_ctx *c, const void *d_keys, const void *d_va
     kmer_status st = ensure_rank_arrays(c, n, 0, s);
     if (st) return st;
     HIPCHK(c, c->rcnt.ensure(n, s));
-    HIPCHK(c, launch_merge_prep((const uint64_t *)d_keys, (const Agg *)d_vals, n, c->rkey.p, c->rord.p, c->rcnt.p,
-                                c->ridx.p, s));
+    HIPCHK(c, launch_merge_prep((const uint64_t *)d_keys, (const Agg *)d_vals, n, c->rkey.p,
+                                c->narrow ? c->rkey32.p : nullptr, c->rord.p, c->rcnt.p, c->ridx.p, s));
     uint64_t nu = 0;
-    st = rank_finish(c, n, false, true, &nu);
+    const bool sync = out || c->p.max_keys;
+    st = rank_finish(c, n, false, true, &nu, sync);
     if (st) return st;
     c->n_out = nu;
     HIPCHK(c, hipEventRecord(c->ev3, s));
-    HIPCHK(c, hipStreamSynchronize(s));
-    float ms = 0.f;
-    HIPCHK(c, hipEventElapsedTime(&ms, c->ev2, c->ev3));
-    c->finish_ms = ms;
+    c->timing_pending = true;
     c->n_hits = 0;
     c->n_cross = 0;
     c->open_stream = false;
+    if (!sync) return KMER_OK;
+    st = resolve_out(c);
+    if (st) return st;
     const uint64_t total = c->n_out + c->exotic.size();
     if (c->p.max_keys && total > c->p.max_keys)
         return fail(c, KMER_E_TOO_MANY_KEYS, "more distinct keys than max_keys (reference Map limit)");
@@ -1097,6 +1168,8 @@ kmer_status kmer_lines(kmer_ctx *c, uint64_t *lines) {
 kmer_status kmer_result_device(kmer_ctx *c, const void **d_keys, const void **d_counts, const void **d_firsts,
                                uint64_t *n) {
     if (!c || !n) return KMER_E_BAD_PARAM;
+    kmer_status st = resolve_out(c);
+    if (st) return st;
     if (d_keys) *d_keys = c->keys_out.p;
     if (d_counts) *d_counts = c->cnt_out.p;
     if (d_firsts) *d_firsts = c->first.p;
@@ -1106,6 +1179,8 @@ kmer_status kmer_result_device(kmer_ctx *c, const void **d_keys, const void **d_
 
 kmer_status kmer_last_timing(kmer_ctx *c, double *scan_ms, double *feed_ms, double *finish_ms) {
     if (!c) return KMER_E_BAD_PARAM;
+    kmer_status st = resolve_out(c);
+    if (st) return st;
     if (scan_ms) *scan_ms = c->scan_ms;
     if (feed_ms) *feed_ms = c->feed_ms;
     if (finish_ms) *finish_ms = c->finish_ms;

@@ -80,10 +80,21 @@ constexpr int HMAX = 64;   // hit slots per tile (more go to the overflow list)
 // start, hits before the tile.
 struct TileSum {
     uint64_t cnt;                  // real '\n' count
+    uint32_t nh;                   // prefix hits (stored + overflow)
+    uint32_t nx;                   // ... of which cross hits (line crosses a tile edge; all if overflowed)
     uint64_t lnl;                  // absolute start of the line after its last '\n' (0 = none; scan: max)
-    uint64_t nh;                   // prefix hits (stored + overflow)
-    uint64_t nx;                   // ... of which cross hits (line crosses a tile edge; all if overflowed)
 };
+
+__host__ __device__ inline TileSum tile_sum_op(const TileSum &x, const TileSum &y) {
+    TileSum r;
+    r.cnt = x.cnt + y.cnt;
+    r.nh = x.nh + y.nh;
+    r.nx = x.nx + y.nx;
+    r.lnl = x.lnl > y.lnl ? x.lnl : y.lnl;
+    return r;
+}
+constexpr uint32_t TSCAN_BLOCK = 1024;     // tiles per block of the tile scan
+constexpr uint32_t TSCAN_INLINE_MAX = 2048; // block-sum prefixes computed in-kernel up to this many blocks
 
 struct ScanArgs {
     const uint8_t *data;
@@ -127,6 +138,7 @@ struct HitArgs {
     uint64_t invalid_key;          // 2^(2*(k-|P|)): sorts after every real key
     uint64_t out_base;             // session hits before this chunk
     uint64_t *rkey;                // by rank: suffix code (invalid_key: filtered / record)
+    uint32_t *rkey32;              // ... as u32 when 2(k-|P|) + 1 <= 32 (then rkey is unused)
     uint64_t *rord;                // by rank: first-occurrence order key
     uint32_t *ridx;                // by rank: the rank itself (sort payload)
     uint64_t *xord, *xkey;         // cross list in natural-slot order (order, key, natural slot)
@@ -210,25 +222,32 @@ struct WindowArgs {
 hipError_t launch_lines(const TileArgs &a, bool lookback, hipStream_t s);
 hipError_t launch_scan_tiles(const ScanArgs &a, hipStream_t s);
 hipError_t launch_hits(const HitArgs &a, hipStream_t s);
+// exclusive scan of the per-tile sums (init folded in); bsum / bscan: n_blocks scratch
+hipError_t launch_tile_reduce(const TileSum *in, uint32_t n, TileSum *bsum, hipStream_t s);
+hipError_t launch_tile_scan(const TileSum *in, uint32_t n, const TileSum *bsum, bool bsum_scanned, TileSum init,
+                            TileSum *out, hipStream_t s);
 hipError_t launch_pos_update(StreamPos *pos, const TileSum *tsum, const TileSum *tscan, uint32_t n_tiles,
                              const uint8_t *data, uint64_t len, unsigned long long *chunk_hits,
-                             unsigned long long *chunk_cross, hipStream_t s);
+                             unsigned long long *chunk_cross, unsigned long long *ends_open, hipStream_t s);
 hipError_t launch_set_pos(StreamPos *pos, uint64_t lines, hipStream_t s);
 hipError_t launch_tile_aggregate(const uint8_t *data, uint64_t len, uint32_t n_tiles, uint64_t *agg_cnt,
                                  uint64_t *agg_lnl, unsigned int *err, hipStream_t s);
 hipError_t launch_windows(const WindowArgs &a, uint32_t grid, hipStream_t s);
+// rkey32 != NULL: keys are written as u32 (narrow mode), else to rkey
 hipError_t launch_cross_scatter(const uint32_t *slot, const uint64_t *ord, const uint64_t *key, uint64_t n,
-                                uint64_t *rkey, uint64_t *rord, hipStream_t s);
+                                uint64_t *rkey, uint32_t *rkey32, uint64_t *rord, hipStream_t s);
 hipError_t launch_cross_sort_small(const uint32_t *slot, const uint64_t *ord, const uint64_t *key, uint64_t n,
-                                   uint64_t *rkey, uint64_t *rord, hipStream_t s);
+                                   uint64_t *rkey, uint32_t *rkey32, uint64_t *rord, hipStream_t s);
 constexpr uint64_t XSMALL_MAX = 16384;   // cross lists up to this size: one-workgroup sort
 hipError_t launch_cross_segsort(uint64_t *ord, uint64_t *key, const uint32_t *slot, uint64_t n, uint64_t *rkey,
-                                uint64_t *rord, hipStream_t s);
+                                uint32_t *rkey32, uint64_t *rord, hipStream_t s);
 hipError_t launch_heads(const uint64_t *skey, const uint32_t *srank, uint64_t n, uint64_t invalid_key,
                         const uint64_t *rcnt, HeadRec *hrec, hipStream_t s);
+hipError_t launch_heads32(const uint32_t *skey, const uint32_t *srank, uint64_t n, uint32_t invalid_key,
+                          const uint64_t *rcnt, HeadRec *hrec, hipStream_t s);
 hipError_t launch_emit(const EmitArgs &a, hipStream_t s);
-hipError_t launch_merge_prep(const uint64_t *keys, const Agg *vals, uint64_t n, uint64_t *rkey, uint64_t *rord,
-                             uint64_t *rcnt, uint32_t *ridx, hipStream_t s);
+hipError_t launch_merge_prep(const uint64_t *keys, const Agg *vals, uint64_t n, uint64_t *rkey, uint32_t *rkey32,
+                             uint64_t *rord, uint64_t *rcnt, uint32_t *ridx, hipStream_t s);
 hipError_t launch_gather_records(const Record *recs, const uint64_t *key_off, uint64_t n,
                                  const uint8_t *data, uint8_t *out, hipStream_t s);
 hipError_t launch_synth_fastq(uint8_t *out, uint64_t seed, uint64_t first_read, uint64_t n_reads,

@@ -766,59 +766,111 @@ __device__ __forceinline__ uint64_t resolve_hit(const HitArgs &a, const HitRec &
     return key;
 }
 
-// One wave per tile.  Packed mode: lane i takes the tile's i-th stored hit,
-// ranks it among the tile's hits by (line, strand, +-offset) with a 64-lane
-// compare, and writes it at rank out_base + hits-before-tile + local rank --
-// unless its line crosses a tile edge (or the tile overflowed), in which case
-// it goes to the cross list with that natural slot.
-__global__ __launch_bounds__(256) void hit_kernel(HitArgs a) {
-    const uint32_t t = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-    if (t >= a.n_tiles || *a.ovf_count > a.ovf_cap) return;   // overflowed scan: the host redoes the chunk
-    const uint32_t lane = threadIdx.x & 63;
-    const TileSum ts = a.tsum[t];
-    const TileSum tb = a.tscan[t];
-    const uint32_t n = (uint32_t)ts.nh;
-    const uint32_t m = min(n, (uint32_t)HMAX);
-    const bool have = lane < m;
-    const bool over = n > (uint32_t)HMAX;
-    uint64_t order = 0, key = a.invalid_key;
-    uint32_t lk = 0xFFFFFFFFu, c_local = 0;
-    bool lvalid = false;
-    if (have) {
-        const HitRec r = a.hits[(uint64_t)t * HMAX + lane];
-        key = resolve_hit(a, r, tb, &order, &lk, &lvalid);
-        c_local = r.c_local;
-    }
-    if (!a.packed) return;
-    const bool cross = have && (over || !lvalid || c_local == (uint32_t)ts.cnt);
-    // rank among the tile's hits, and among its cross hits (so that the cross
-    // list is in slot order); an overflowed tile uses the in-tile ordinal
-    uint32_t rank = lane, xr = lane;
-    if (!over) {
-        const uint64_t cm = __ballot(cross);
-        rank = 0;
-        xr = 0;
-        for (uint32_t j = 0; j < m; ++j) {
-            const uint32_t less = __shfl(lk, (int)j) < lk ? 1u : 0u;
-            rank += less;
-            xr += less & (uint32_t)(cm >> j);
-        }
-    }
-    if (!have) return;
-    const uint64_t slot = a.out_base + tb.nh + rank;
+// Write one resolved packed hit at its rank slot, or to the cross list.
+__device__ __forceinline__ void place_hit(const HitArgs &a, uint64_t slot, bool cross, uint64_t xi, uint64_t key,
+                                          uint64_t order) {
     a.ridx[slot] = (uint32_t)slot;
     if (!cross) {
-        a.rkey[slot] = key;
+        if (a.rkey32) a.rkey32[slot] = (uint32_t)key;
+        else a.rkey[slot] = key;
         a.rord[slot] = order;
+    } else if (xi < a.xcap) {
+        a.xord[xi] = order;
+        a.xkey[xi] = key;
+        a.xslot[xi] = (uint32_t)slot;
     } else {
-        const uint64_t xi = a.xbase + tb.nx + xr;
-        if (xi < a.xcap) {
-            a.xord[xi] = order;
-            a.xkey[xi] = key;
-            a.xslot[xi] = (uint32_t)slot;
-        } else {
-            atomicOr(a.err, ERR_CROSS_OVERFLOW);
+        atomicOr(a.err, ERR_CROSS_OVERFLOW);
+    }
+}
+
+// Hits of HTPW consecutive tiles per wave, flattened onto the lanes (a tile
+// has ~14 hits at 150 bp reads: one tile per wave would leave most lanes
+// idle).  Phase 1: lane = one hit: resolve it, stage (local order, cross
+// flag, key, order) in LDS.  Phase 2: rank each hit among its tile's hits by
+// (line, strand, +-offset) and place it at out_base + hits-before-tile +
+// rank, or on the cross list (line crosses a tile edge / tile overflowed).
+constexpr uint32_t HTPW = 4;
+constexpr uint32_t HENT = HTPW * HMAX;       // staged hits per wave
+__global__ __launch_bounds__(256) void hit_kernel(HitArgs a) {
+    __shared__ uint32_t s_lk[4][HENT];
+    __shared__ uint8_t s_x[4][HENT];
+    __shared__ uint64_t s_key[4][HENT];
+    __shared__ uint64_t s_ord[4][HENT];
+    const uint32_t wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t t0 = __builtin_amdgcn_readfirstlane((blockIdx.x * 4 + wid) * HTPW);
+    if (t0 >= a.n_tiles || *a.ovf_count > a.ovf_cap) return;   // overflowed scan: the host redoes the chunk
+    TileSum ts[HTPW], tb[HTPW];
+    uint32_t off[HTPW + 1];
+    off[0] = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < HTPW; ++u) {
+        const uint32_t t = min(t0 + u, a.n_tiles - 1);
+        ts[u] = a.tsum[t];
+        tb[u] = a.tscan[t];
+        off[u + 1] = off[u] + (t0 + u < a.n_tiles ? min(ts[u].nh, (uint32_t)HMAX) : 0u);
+    }
+    const uint32_t total = off[HTPW];
+    // phase 1
+    for (uint32_t e0 = 0; e0 < total; e0 += 64) {
+        const uint32_t e = e0 + lane;
+        if (e < total) {
+            uint32_t u = 0;
+#pragma unroll
+            for (uint32_t v = 1; v < HTPW; ++v) u += e >= off[v] ? 1u : 0u;
+            const uint32_t i = e - off[u];
+            TileSum tsu = ts[0], tbu = tb[0];
+#pragma unroll
+            for (uint32_t v = 1; v < HTPW; ++v)
+                if (u == v) {
+                    tsu = ts[v];
+                    tbu = tb[v];
+                }
+            const HitRec r = a.hits[(uint64_t)(t0 + u) * HMAX + i];
+            uint64_t order;
+            uint32_t lk;
+            bool lvalid;
+            const uint64_t key = resolve_hit(a, r, tbu, &order, &lk, &lvalid);
+            s_lk[wid][e] = lk;
+            s_x[wid][e] = (tsu.nh > (uint32_t)HMAX || !lvalid || r.c_local == (uint32_t)tsu.cnt) ? 1 : 0;
+            s_key[wid][e] = key;
+            s_ord[wid][e] = order;
         }
+    }
+    if (!a.packed) return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    // phase 2
+    for (uint32_t e0 = 0; e0 < total; e0 += 64) {
+        const uint32_t e = e0 + lane;
+        if (e >= total) continue;
+        uint32_t u = 0;
+#pragma unroll
+        for (uint32_t v = 1; v < HTPW; ++v) u += e >= off[v] ? 1u : 0u;
+        uint32_t lo = off[0], hi = off[1], nh = ts[0].nh;
+        uint64_t hb = tb[0].nh, xb = tb[0].nx;
+#pragma unroll
+        for (uint32_t v = 1; v < HTPW; ++v)
+            if (u == v) {
+                lo = off[v];
+                hi = off[v + 1];
+                nh = ts[v].nh;
+                hb = tb[v].nh;
+                xb = tb[v].nx;
+            }
+        const uint32_t i = e - lo;
+        const bool cross = s_x[wid][e] != 0;
+        uint32_t rank = i, xr = i;            // overflowed tile: the in-tile ordinal
+        if (nh <= (uint32_t)HMAX) {
+            const uint32_t lk = s_lk[wid][e];
+            rank = 0;
+            xr = 0;
+            for (uint32_t j = lo; j < hi; ++j) {
+                const uint32_t less = s_lk[wid][j] < lk ? 1u : 0u;
+                rank += less;
+                xr += less & (uint32_t)s_x[wid][j];
+            }
+        }
+        place_hit(a, a.out_base + hb + rank, cross, a.xbase + xb + xr, s_key[wid][e], s_ord[wid][e]);
     }
 }
 
@@ -835,16 +887,101 @@ __global__ __launch_bounds__(256) void hit_overflow_kernel(HitArgs a) {
         const uint64_t key = resolve_hit(a, r, tb, &order, &lk, &lvalid);
         if (!a.packed) continue;
         const uint32_t ord = r.qm >> 17;
-        const uint64_t slot = a.out_base + tb.nh + ord;
-        a.ridx[slot] = (uint32_t)slot;
-        const uint64_t xi = a.xbase + tb.nx + ord;
-        if (xi < a.xcap) {
-            a.xord[xi] = order;
-            a.xkey[xi] = key;
-            a.xslot[xi] = (uint32_t)slot;
-        } else {
-            atomicOr(a.err, ERR_CROSS_OVERFLOW);
-        }
+        place_hit(a, a.out_base + tb.nh + ord, true, a.xbase + tb.nx + ord, key, order);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// exclusive scan of the per-tile sums: block reduce, then per-block scan with
+// the prefix of the preceding blocks (in-kernel for up to TSCAN_INLINE_MAX
+// blocks, else from a scanned block-sum array)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ TileSum ts_shfl_up(const TileSum &v, int d) {
+    TileSum r;
+    r.cnt = (uint64_t)__shfl_up((unsigned long long)v.cnt, d);
+    r.nh = (uint32_t)__shfl_up((int)v.nh, d);
+    r.nx = (uint32_t)__shfl_up((int)v.nx, d);
+    r.lnl = (uint64_t)__shfl_up((unsigned long long)v.lnl, d);
+    return r;
+}
+__device__ __forceinline__ TileSum ts_zero() {
+    TileSum z;
+    z.cnt = 0;
+    z.nh = 0;
+    z.nx = 0;
+    z.lnl = 0;
+    return z;
+}
+// inclusive wave scan
+__device__ __forceinline__ TileSum ts_wave_scan(TileSum v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const TileSum o = ts_shfl_up(v, d);
+        if (lane >= d) v = tile_sum_op(o, v);
+    }
+    return v;
+}
+// block (256 threads) exclusive scan of one value per thread; returns the exclusive prefix, *total the sum
+__device__ __forceinline__ TileSum ts_block_scan(TileSum v, TileSum *total) {
+    __shared__ TileSum wsum[4];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const TileSum incl = ts_wave_scan(v);
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    TileSum pre = ts_zero(), tot = ts_zero();
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        if (w < wid) pre = tile_sum_op(pre, wsum[w]);
+        tot = tile_sum_op(tot, wsum[w]);
+    }
+    __syncthreads();
+    *total = tot;
+    const TileSum ex = ts_shfl_up(incl, 1);
+    return lane == 0 ? pre : tile_sum_op(pre, ex);
+}
+
+__global__ __launch_bounds__(256) void tile_reduce_kernel(const TileSum *in, uint32_t n, TileSum *bsum) {
+    const uint32_t base = blockIdx.x * TSCAN_BLOCK;
+    TileSum v = ts_zero();
+#pragma unroll
+    for (uint32_t i = 0; i < TSCAN_BLOCK / 256; ++i) {
+        const uint32_t t = base + i * 256 + threadIdx.x;
+        if (t < n) v = tile_sum_op(v, in[t]);
+    }
+    TileSum tot;
+    (void)ts_block_scan(v, &tot);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(256) void tile_scan_kernel(const TileSum *in, uint32_t n, const TileSum *bsum,
+                                                        uint32_t bsum_scanned, TileSum init, TileSum *out) {
+    const uint32_t b = blockIdx.x;
+    TileSum pre;
+    if (bsum_scanned) {
+        pre = tile_sum_op(init, bsum[b]);
+    } else {
+        TileSum v = ts_zero();
+        for (uint32_t j = threadIdx.x; j < b; j += 256) v = tile_sum_op(v, bsum[j]);
+        TileSum tot;
+        (void)ts_block_scan(v, &tot);
+        pre = tile_sum_op(init, tot);
+    }
+    // 4 consecutive tiles per thread
+    const uint32_t t0 = b * TSCAN_BLOCK + threadIdx.x * 4;
+    TileSum x[4];
+    TileSum acc = ts_zero();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        x[i] = t0 + i < n ? in[t0 + i] : ts_zero();
+        acc = tile_sum_op(acc, x[i]);
+    }
+    TileSum tot;
+    TileSum ex = tile_sum_op(pre, ts_block_scan(acc, &tot));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (t0 + i < n) out[t0 + i] = ex;
+        ex = tile_sum_op(ex, x[i]);
     }
 }
 
@@ -861,10 +998,11 @@ __global__ void set_pos_kernel(StreamPos *pos, uint64_t lines) {
 // advance the running stream position past this chunk; hits of the chunk
 __global__ void pos_update_kernel(StreamPos *pos, const TileSum *tsum, const TileSum *tscan, uint32_t n_tiles,
                                   const uint8_t *data, uint64_t len, unsigned long long *chunk_hits,
-                                  unsigned long long *chunk_cross) {
+                                  unsigned long long *chunk_cross, unsigned long long *ends_open) {
     if (threadIdx.x == 0 && blockIdx.x == 0) {   // (a redo after an overflow restores pos first)
         pos->lines += tscan[n_tiles - 1].cnt + tsum[n_tiles - 1].cnt;
         pos->ends_open = (len > 0 && data[len - 1] != '\n') ? 1 : 0;
+        *ends_open = pos->ends_open;
         *chunk_hits = tscan[n_tiles - 1].nh + tsum[n_tiles - 1].nh;
         *chunk_cross = tscan[n_tiles - 1].nx + tsum[n_tiles - 1].nx;
     }
@@ -959,12 +1097,17 @@ __global__ __launch_bounds__(256) void windows_kernel(WindowArgs a) {
 // Cross entries (in natural-slot order) sorted by order key: the i-th
 // smallest order takes the i-th natural slot.  Large lists: radix-sorted on
 // the host side of the pipeline, then cross_scatter_kernel.
+__device__ __forceinline__ void put_key(uint64_t *rkey, uint32_t *rkey32, uint64_t slot, uint64_t key) {
+    if (rkey32) rkey32[slot] = (uint32_t)key;
+    else rkey[slot] = key;
+}
+
 __global__ __launch_bounds__(256) void cross_scatter_kernel(const uint32_t *slot, const uint64_t *ord,
                                                             const uint64_t *key, uint64_t n, uint64_t *rkey,
-                                                            uint64_t *rord) {
+                                                            uint32_t *rkey32, uint64_t *rord) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t sl = slot[i];
-        rkey[sl] = key[i];
+        put_key(rkey, rkey32, sl, key[i]);
         rord[sl] = ord[i];
     }
 }
@@ -974,7 +1117,7 @@ __global__ __launch_bounds__(256) void cross_scatter_kernel(const uint32_t *slot
 constexpr uint32_t XSMALL = 16384;
 __global__ __launch_bounds__(1024) void cross_sort_small_kernel(const uint32_t *slot, const uint64_t *ord,
                                                                 const uint64_t *key, uint32_t n, uint64_t *rkey,
-                                                                uint64_t *rord) {
+                                                                uint32_t *rkey32, uint64_t *rord) {
     __shared__ uint64_t so[XSMALL];
     __shared__ uint16_t si[XSMALL];
     uint32_t N = 2;
@@ -1005,7 +1148,7 @@ __global__ __launch_bounds__(1024) void cross_sort_small_kernel(const uint32_t *
     }
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
         const uint32_t sl = slot[i];
-        rkey[sl] = key[si[i]];
+        put_key(rkey, rkey32, sl, key[si[i]]);
         rord[sl] = so[i];
     }
 }
@@ -1015,7 +1158,8 @@ __global__ __launch_bounds__(1024) void cross_sort_small_kernel(const uint32_t *
 // (<= 2 * HMAX).  One thread per line segment: insertion sort by order key,
 // then the scatter to the natural slots.
 __global__ __launch_bounds__(256) void cross_segsort_kernel(uint64_t *ord, uint64_t *key, const uint32_t *slot,
-                                                            uint64_t n, uint64_t *rkey, uint64_t *rord) {
+                                                            uint64_t n, uint64_t *rkey, uint32_t *rkey32,
+                                                            uint64_t *rord) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t line = ord[i] >> 24;      // (the line bits of a segment never change while it is sorted)
         if (i > 0 && (ord[i - 1] >> 24) == line) continue;
@@ -1034,14 +1178,15 @@ __global__ __launch_bounds__(256) void cross_segsort_kernel(uint64_t *ord, uint6
         }
         for (uint64_t j = i; j < e; ++j) {
             const uint32_t sl = slot[j];
-            rkey[sl] = key[j];
+            put_key(rkey, rkey32, sl, key[j]);
             rord[sl] = ord[j];
         }
     }
 }
 
 // End of the key group starting at sorted index i: galloping then binary search.
-__device__ __forceinline__ uint64_t group_end(const uint64_t *skey, uint64_t i, uint64_t n, uint64_t key) {
+template <typename K>
+__device__ __forceinline__ uint64_t group_end(const K *skey, uint64_t i, uint64_t n, K key) {
     uint64_t lo = i, step = 1, hi = n;
     for (;;) {
         const uint64_t p = lo + step;
@@ -1063,10 +1208,11 @@ __device__ __forceinline__ uint64_t group_end(const uint64_t *skey, uint64_t i, 
 // After the stable key sort (payload = rank): the first element of each key
 // group has the smallest rank = the key's first occurrence.  Every rank gets
 // its record written (srank is a permutation), so no clearing pass is needed.
-__global__ __launch_bounds__(256) void heads_kernel(const uint64_t *skey, const uint32_t *srank, uint64_t n,
-                                                    uint64_t invalid_key, const uint64_t *rcnt, HeadRec *hrec) {
+template <typename K>
+__global__ __launch_bounds__(256) void heads_kernel(const K *skey, const uint32_t *srank, uint64_t n, K invalid_key,
+                                                    const uint64_t *rcnt, HeadRec *hrec) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = skey[i];
+        const K k = skey[i];
         HeadRec v;
         v.key = 0;
         v.count = 0;
@@ -1135,11 +1281,11 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
 
 // merged partials (in shard order = first-occurrence order) -> rank arrays
 __global__ __launch_bounds__(256) void merge_prep_kernel(const uint64_t *keys, const Agg *vals, uint64_t n,
-                                                         uint64_t *rkey, uint64_t *rord, uint64_t *rcnt,
-                                                         uint32_t *ridx) {
+                                                         uint64_t *rkey, uint32_t *rkey32, uint64_t *rord,
+                                                         uint64_t *rcnt, uint32_t *ridx) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const Agg v = vals[i];
-        rkey[i] = keys[i];
+        put_key(rkey, rkey32, i, keys[i]);
         rord[i] = v.first;
         rcnt[i] = v.count;
         ridx[i] = (uint32_t)i;
@@ -1229,16 +1375,26 @@ hipError_t launch_scan_tiles(const ScanArgs &a, hipStream_t s) {
 }
 
 hipError_t launch_hits(const HitArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(hit_kernel, dim3((a.n_tiles + 3) / 4), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(hit_kernel, dim3((a.n_tiles + 4 * HTPW - 1) / (4 * HTPW)), dim3(256), 0, s, a);
     hipLaunchKernelGGL(hit_overflow_kernel, dim3(64), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_pos_update(StreamPos *pos, const TileSum *tsum, const TileSum *tscan, uint32_t n_tiles,
                              const uint8_t *data, uint64_t len, unsigned long long *chunk_hits,
-                             unsigned long long *chunk_cross, hipStream_t s) {
+                             unsigned long long *chunk_cross, unsigned long long *ends_open, hipStream_t s) {
     hipLaunchKernelGGL(pos_update_kernel, dim3(1), dim3(64), 0, s, pos, tsum, tscan, n_tiles, data, len, chunk_hits,
-                       chunk_cross);
+                       chunk_cross, ends_open);
+    return hipGetLastError();
+}
+hipError_t launch_tile_reduce(const TileSum *in, uint32_t n, TileSum *bsum, hipStream_t s) {
+    hipLaunchKernelGGL(tile_reduce_kernel, dim3((n + TSCAN_BLOCK - 1) / TSCAN_BLOCK), dim3(256), 0, s, in, n, bsum);
+    return hipGetLastError();
+}
+hipError_t launch_tile_scan(const TileSum *in, uint32_t n, const TileSum *bsum, bool bsum_scanned, TileSum init,
+                            TileSum *out, hipStream_t s) {
+    hipLaunchKernelGGL(tile_scan_kernel, dim3((n + TSCAN_BLOCK - 1) / TSCAN_BLOCK), dim3(256), 0, s, in, n, bsum,
+                       bsum_scanned ? 1u : 0u, init, out);
     return hipGetLastError();
 }
 hipError_t launch_set_pos(StreamPos *pos, uint64_t lines, hipStream_t s) {
@@ -1263,33 +1419,47 @@ static uint32_t grid_for(uint64_t n) {
 }
 
 hipError_t launch_cross_scatter(const uint32_t *slot, const uint64_t *ord, const uint64_t *key, uint64_t n,
-                                uint64_t *rkey, uint64_t *rord, hipStream_t s) {
-    if (n) hipLaunchKernelGGL(cross_scatter_kernel, dim3(grid_for(n)), dim3(256), 0, s, slot, ord, key, n, rkey, rord);
+                                uint64_t *rkey, uint32_t *rkey32, uint64_t *rord, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(cross_scatter_kernel, dim3(grid_for(n)), dim3(256), 0, s, slot, ord, key, n, rkey, rkey32,
+                              rord);
     return hipGetLastError();
 }
 hipError_t launch_cross_sort_small(const uint32_t *slot, const uint64_t *ord, const uint64_t *key, uint64_t n,
-                                   uint64_t *rkey, uint64_t *rord, hipStream_t s) {
+                                   uint64_t *rkey, uint32_t *rkey32, uint64_t *rord, hipStream_t s) {
     if (n > XSMALL) return hipErrorInvalidValue;
-    if (n) hipLaunchKernelGGL(cross_sort_small_kernel, dim3(1), dim3(1024), 0, s, slot, ord, key, (uint32_t)n, rkey, rord);
+    if (n) hipLaunchKernelGGL(cross_sort_small_kernel, dim3(1), dim3(1024), 0, s, slot, ord, key, (uint32_t)n, rkey,
+                              rkey32, rord);
     return hipGetLastError();
 }
 hipError_t launch_cross_segsort(uint64_t *ord, uint64_t *key, const uint32_t *slot, uint64_t n, uint64_t *rkey,
-                                uint64_t *rord, hipStream_t s) {
-    if (n) hipLaunchKernelGGL(cross_segsort_kernel, dim3(grid_for(n)), dim3(256), 0, s, ord, key, slot, n, rkey, rord);
+                                uint32_t *rkey32, uint64_t *rord, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(cross_segsort_kernel, dim3(grid_for(n)), dim3(256), 0, s, ord, key, slot, n, rkey, rkey32,
+                              rord);
     return hipGetLastError();
 }
 hipError_t launch_heads(const uint64_t *skey, const uint32_t *srank, uint64_t n, uint64_t invalid_key,
                         const uint64_t *rcnt, HeadRec *hrec, hipStream_t s) {
-    if (n) hipLaunchKernelGGL(heads_kernel, dim3(grid_for(n)), dim3(256), 0, s, skey, srank, n, invalid_key, rcnt, hrec);
+    if (n)
+        hipLaunchKernelGGL(heads_kernel<uint64_t>, dim3(grid_for(n)), dim3(256), 0, s, skey, srank, n, invalid_key, rcnt,
+                           hrec);
+    return hipGetLastError();
+}
+hipError_t launch_heads32(const uint32_t *skey, const uint32_t *srank, uint64_t n, uint32_t invalid_key,
+                          const uint64_t *rcnt, HeadRec *hrec, hipStream_t s) {
+    if (n)
+        hipLaunchKernelGGL(heads_kernel<uint32_t>, dim3(grid_for(n)), dim3(256), 0, s, skey, srank, n, invalid_key, rcnt,
+                           hrec);
     return hipGetLastError();
 }
 hipError_t launch_emit(const EmitArgs &a, hipStream_t s) {
     if (a.n) hipLaunchKernelGGL(emit_kernel, dim3(grid_for(a.n)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
-hipError_t launch_merge_prep(const uint64_t *keys, const Agg *vals, uint64_t n, uint64_t *rkey, uint64_t *rord,
-                             uint64_t *rcnt, uint32_t *ridx, hipStream_t s) {
-    if (n) hipLaunchKernelGGL(merge_prep_kernel, dim3(grid_for(n)), dim3(256), 0, s, keys, vals, n, rkey, rord, rcnt, ridx);
+hipError_t launch_merge_prep(const uint64_t *keys, const Agg *vals, uint64_t n, uint64_t *rkey, uint32_t *rkey32,
+                             uint64_t *rord, uint64_t *rcnt, uint32_t *ridx, hipStream_t s) {
+    if (n)
+        hipLaunchKernelGGL(merge_prep_kernel, dim3(grid_for(n)), dim3(256), 0, s, keys, vals, n, rkey, rkey32, rord, rcnt,
+                           ridx);
     return hipGetLastError();
 }
 hipError_t launch_gather_records(const Record *recs, const uint64_t *key_off, uint64_t n, const uint8_t *data,
