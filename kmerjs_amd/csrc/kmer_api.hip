@@ -103,6 +103,8 @@ struct kmer_ctx {
     DBuf<uint64_t> rkey, rkey2, rord, rcnt;
     DBuf<uint32_t> rkey32, rkey32b;   // narrow keys: 2(k-|P|) + 1 <= 32 bits
     bool narrow = false;
+    bool planes = false;           // ACGT prefix: bit-plane scan kernel
+    PlaneArgs pargs{};
     DBuf<uint32_t> ridx, ridx2, opos;
     DBuf<HeadRec> hrec;
     bool long_seg = false;         // INFO_LONGSEG seen this session
@@ -370,7 +372,8 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
     for (int attempt = 0; attempt < 8; ++attempt) {
         HIPCHK(c, hipMemsetAsync(c->d_scal, 0, 3 * 8, s));   // rec, ovf, cross counts of this chunk
         HIPCHK(c, hipEventRecord(c->ev0, s));
-        HIPCHK(c, launch_scan_tiles(a, s));
+        if (c->planes) HIPCHK(c, launch_scan_planes(a, c->pargs, s));
+        else HIPCHK(c, launch_scan_tiles(a, s));
         HIPCHK(c, hipEventRecord(c->ev1, s));
         HIPCHK(c, launch_tile_reduce(c->tsum.p, n_tiles, c->bsum.p, s));
         if (n_blocks > TSCAN_INLINE_MAX) {
@@ -900,6 +903,18 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
         c->mode = MODE_GENERAL;
     c->kbits = c->mode == MODE_PACKED ? 2 * (k - plen) : 0;
     c->narrow = c->mode == MODE_PACKED && c->kbits <= 31;
+    c->planes = c->mode != MODE_GENERAL && acgt && !(pp->flags & KMER_FLAG_BYTE_SCAN);
+    if (c->planes) {
+        auto code = [](char ch) -> uint32_t { return ch == 'A' ? 0u : ch == 'C' ? 1u : ch == 'G' ? 2u : 3u; };
+        c->pargs.pb = std::min<uint32_t>(plen, 5);
+        for (uint32_t i = 0; i < 5; ++i) {
+            const uint32_t cp = i < plen ? code(c->prefix[i]) : 0u, cr = i < plen ? code(c->rprefix[i]) : 0u;
+            c->pargs.kl[i] = (cp & 1u) ? 0u : ~0u;
+            c->pargs.kh[i] = (cp & 2u) ? 0u : ~0u;
+            c->pargs.rl[i] = (cr & 1u) ? 0u : ~0u;
+            c->pargs.rh[i] = (cr & 2u) ? 0u : ~0u;
+        }
+    }
 
     bool ok = true;
     ok &= dalloc(&c->d_P, std::max<uint32_t>(plen, 1)) == hipSuccess;

@@ -112,6 +112,14 @@ struct ScanArgs {
     uint32_t ablate;               // experiments only: bit0 = drop all candidates
 };
 
+// Bit-plane prefix test (ACGT prefixes): per prefix base i, xor masks that
+// turn the plane bits into "code bit equals P_i's bit" (~0 where P_i's bit is 0).
+struct PlaneArgs {
+    uint32_t kl[5], kh[5];         // P (forward strand)
+    uint32_t rl[5], rh[5];         // rc(P), as a forward-strand string
+    uint32_t pb;                   // bases tested on the planes: min(|P|, 5); the rest byte-exact
+};
+
 // value of a unique packed key: first-occurrence order and count
 struct Agg {
     uint64_t first;
@@ -221,6 +229,7 @@ struct WindowArgs {
 // ---- launchers (kmer_kernels.hip) ------------------------------------------
 hipError_t launch_lines(const TileArgs &a, bool lookback, hipStream_t s);
 hipError_t launch_scan_tiles(const ScanArgs &a, hipStream_t s);
+hipError_t launch_scan_planes(const ScanArgs &a, const PlaneArgs &pa, hipStream_t s);
 hipError_t launch_hits(const HitArgs &a, hipStream_t s);
 // exclusive scan of the per-tile sums (init folded in); bsum / bscan: n_blocks scratch
 hipError_t launch_tile_reduce(const TileSum *in, uint32_t n, TileSum *bsum, hipStream_t s);

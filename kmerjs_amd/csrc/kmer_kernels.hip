@@ -414,6 +414,10 @@ __device__ __forceinline__ int last_newline_in_chunk(const uint8_t *buf, int c, 
 
 // One verified prefix hit (queue entry (q << 1) | strand): window analysis,
 // tile-local line context, hit record.
+// THREAD_MAP: sh.nlmap holds one bit per 64-byte thread region (plane
+// kernel; chunks inside a region are resolved through cpre), else one bit per
+// 16-byte chunk (byte kernel).
+template <bool THREAD_MAP>
 __device__ __forceinline__ void emit_hit(const ScanArgs &a, const uint8_t *buf, ScanShared &sh, uint32_t tile,
                                       uint32_t e) {
     const uint32_t k = a.k, plen = a.plen;
@@ -461,12 +465,29 @@ __device__ __forceinline__ void emit_hit(const ScanArgs &a, const uint8_t *buf, 
         if (last >= 0) {
             lstart = last + 1;
         } else if (c_local > 0) {
-            // the line started in the last earlier chunk that holds a '\n' (chunk bitmap)
-            const int cc = cs - 1;
-            int wi = cc >> 5;
-            uint32_t m = sh.nlmap[wi] & (0xFFFFFFFFu >> (31 - (cc & 31)));
-            while (m == 0) m = sh.nlmap[--wi];
-            lstart = last_newline_in_chunk(buf, 32 * wi + 31 - __clz(m)) + 1;
+            // the line started in the last earlier chunk that holds a '\n'
+            int c;
+            if (THREAD_MAP) {
+                // inside cs's 64-byte region first (chunk c holds a '\n' iff cpre[c+1] > cpre[c])
+                c = cs - 1;
+                const int rb = cs & ~3;
+                while (c >= rb && sh.cpre[c + 1] == sh.cpre[c]) --c;
+                if (c < rb) {
+                    const int rr = (cs >> 2) - 1;        // earlier regions: region bitmap
+                    int wi = rr >> 5;
+                    uint32_t m = sh.nlmap[wi] & (0xFFFFFFFFu >> (31 - (rr & 31)));
+                    while (m == 0) m = sh.nlmap[--wi];
+                    c = 4 * (32 * wi + 31 - __clz(m)) + 3;
+                    while (sh.cpre[c + 1] == sh.cpre[c]) --c;   // (c + 1 <= cs - 1 here)
+                }
+            } else {
+                const int cc = cs - 1;               // chunk bitmap
+                int wi = cc >> 5;
+                uint32_t m = sh.nlmap[wi] & (0xFFFFFFFFu >> (31 - (cc & 31)));
+                while (m == 0) m = sh.nlmap[--wi];
+                c = 32 * wi + 31 - __clz(m);
+            }
+            lstart = last_newline_in_chunk(buf, c) + 1;
         }
     }
     HitRec r;
@@ -516,7 +537,7 @@ __device__ __forceinline__ void scan_word(const ScanArgs &a, const uint8_t *buf,
             const uint32_t mk = n >= 4 ? 0xFFFFFFFFu : ((1u << (8 * n)) - 1u);
             ok = ((lds_word(buf, q + (int)b) ^ pw[(strand ? KMAX_TILE / 4 : 0) + b / 4]) & mk) == 0;
         }
-        if (ok) emit_hit(a, buf, sh, tile, ((uint32_t)q << 1) | strand);
+        if (ok) emit_hit<false>(a, buf, sh, tile, ((uint32_t)q << 1) | strand);
     }
 }
 
@@ -715,6 +736,246 @@ __global__ __launch_bounds__(TPB) void scan_tile_kernel(ScanArgs a) {
     }
 }
 
+
+// Plane-kernel candidate (q << 1) | strand: byte-exact prefix check (the
+// planes alias non-ACGT bytes), then the hit record.
+__device__ __forceinline__ void verify_emit(const ScanArgs &a, const uint8_t *buf, ScanShared &sh, uint32_t tile,
+                                            const uint32_t *pw, uint32_t e) {
+    const uint32_t strand = e & 1u, plen = a.plen;
+    const int q = (int)(e >> 1);
+    bool ok = true;
+#pragma unroll 1
+    for (uint32_t b = 0; b < plen && ok; b += 4) {
+        const uint32_t n = plen - b;
+        const uint32_t mk = n >= 4 ? 0xFFFFFFFFu : ((1u << (8 * n)) - 1u);
+        ok = ((lds_word(buf, q + (int)b) ^ pw[(strand ? KMAX_TILE / 4 : 0) + b / 4]) & mk) == 0;
+    }
+    if (ok) emit_hit<true>(a, buf, sh, tile, e);
+}
+
+// ---------------------------------------------------------------------------
+// Plane kernel (ACGT prefixes).  Same tile staging as scan_tile_kernel, but
+// after the coalesced load each thread works on its own 64 contiguous bytes
+// (+4 look-ahead): the bytes become two bit-planes of 2-bit base codes
+// (A=0 C=1 G=2 T=3; bit 0 = b1^b2, bit 1 = b2^b3 of the byte), 32 positions
+// per 32-bit word, packed with v_dot4_u32_u8.  The prefix (up to 5 bases) is
+// then tested at 32 positions per bit-op on both strands:
+//   match = AND_i (L>>i == P_i.lo) & (H>>i == P_i.hi)     (funnel shifts)
+// Non-ACGT bytes alias to some code, so a candidate is re-checked byte for
+// byte before its hit record is written.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t plane_match(uint32_t L0, uint32_t H0, uint32_t L1, uint32_t H1,
+                                                const uint32_t *kl, const uint32_t *kh, uint32_t pb,
+                                                const uint32_t *SL, const uint32_t *SH) {
+    uint32_t acc = (L0 ^ kl[0]) & (H0 ^ kh[0]);
+#pragma unroll
+    for (uint32_t i = 1; i < 5; ++i) {
+        if (i < pb) acc = acc & (SL[i] ^ kl[i]) & (SH[i] ^ kh[i]);
+    }
+    return acc;
+}
+
+template <bool FULL5>
+__global__ __launch_bounds__(TPB) void scan_planes_kernel(ScanArgs a, PlaneArgs pa) {
+    __shared__ __attribute__((aligned(16))) uint8_t buf[BUFSZ];
+    __shared__ ScanShared sh;
+    __shared__ __attribute__((aligned(16))) uint8_t s_pr[2 * KMAX_TILE];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint64_t len = a.len;
+    const bool halo = tid < NCH_FRONT + NCH_BACK;
+    const int hc = tid < NCH_FRONT ? tid : NCH_FRONT + NCH_MAIN + (tid - NCH_FRONT);
+    const uint32_t tile = blockIdx.x;
+    const int64_t g0 = (int64_t)tile * TILE;
+    {
+        uint4 v[4];
+        uint4 vh = make_uint4(0, 0, 0, 0);
+        if (g0 - FH >= 0 && (uint64_t)(g0 + TILE + BH) <= len) {
+            const uint8_t *src = a.data + g0 + 16 * tid;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = *(const uint4 *)(src + 16 * TPB * i);
+            vh = *(const uint4 *)(a.data + g0 - FH + 16 * (halo ? hc : 0));
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = load_chunk(a.data, g0 + (int64_t)(tid + TPB * i) * 16, len);
+            if (halo) vh = load_chunk(a.data, g0 - FH + (int64_t)hc * 16, len);
+        }
+        if (tid == 0) {
+            sh.last_chunk = -1;
+            sh.nh = 0;
+            sh.nx = 0;
+            sh.qn = 0;
+        }
+        uint32_t orall = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            orall |= v[i].x | v[i].y | v[i].z | v[i].w;
+            *(uint4 *)(buf + FH + (tid + TPB * i) * 16) = v[i];
+        }
+        if (halo) *(uint4 *)(buf + hc * 16) = vh;
+        if (tid < 2 * KMAX_TILE) s_pr[tid] = a.PR[tid];
+        if (orall & 0x80808080u) atomicOr(a.err, ERR_NONASCII);
+    }
+    __syncthreads();
+
+    // ---- this thread's 64 bytes (4 chunks) + 4 look-ahead bytes ----
+    uint32_t w[17];
+    {
+        const uint4 *src = (const uint4 *)(buf + FH + 64 * tid);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint4 x = src[j];
+            w[4 * j] = x.x;
+            w[4 * j + 1] = x.y;
+            w[4 * j + 2] = x.z;
+            w[4 * j + 3] = x.w;
+        }
+        w[16] = *(const uint32_t *)(buf + FH + 64 * tid + 64);
+    }
+    const bool tail_tile = (uint64_t)(g0 + TILE) > len;
+    uint32_t ccnt[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        uint32_t cnt = 0;
+        if (!tail_tile) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) cnt += __popc(nl_flags(w[4 * j + i]));
+        } else {
+            const int64_t gc = g0 + 64 * tid + 16 * j;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int64_t n = (int64_t)len - (gc + 4 * i);
+                uint32_t z = nl_flags(w[4 * j + i]);
+                z = n <= 0 ? 0u : n < 4 ? (z & ((1u << (8 * n)) - 1u)) : z;
+                cnt += __popc(z);
+            }
+        }
+        ccnt[j] = cnt;
+    }
+    const uint32_t ttot = ccnt[0] + ccnt[1] + ccnt[2] + ccnt[3];
+    {
+        const unsigned long long m = __ballot(ttot != 0);
+        if (lane == 0) {
+            sh.nlmap[2 * wid] = (uint32_t)m;
+            sh.nlmap[2 * wid + 1] = (uint32_t)(m >> 32);
+            if (m) atomicMax(&sh.last_chunk, 64 * wid + 63 - (int)__clzll((long long)m));   // (a thread index here)
+        }
+    }
+    const uint32_t incl = wave_incl_sum(ttot);
+    if (lane == 63) sh.wsum[wid][0] = incl;
+
+    // ---- bit-planes of the 68 bytes: gL/gH groups of 8 bases (2 words) ----
+    const uint32_t W0 = 0x08040201u, W1 = 0x80402010u;
+    uint32_t L[3], H[3];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        uint32_t gl[4], gh[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const uint32_t x0 = w[8 * h + 2 * p], x1 = w[8 * h + 2 * p + 1];
+            const uint32_t t0 = x0 ^ (x0 >> 1), t1 = x1 ^ (x1 >> 1);
+            gl[p] = __builtin_amdgcn_udot4(t0 & 0x02020202u, W0, __builtin_amdgcn_udot4(t1 & 0x02020202u, W1, 0u, false), false);
+            gh[p] = __builtin_amdgcn_udot4(t0 & 0x04040404u, W0, __builtin_amdgcn_udot4(t1 & 0x04040404u, W1, 0u, false), false);
+        }
+        // gl: bits 1..8, gh: bits 2..9 for 8 bases
+        L[h] = (gl[0] >> 1) | (gl[1] << 7) | (gl[2] << 15) | (gl[3] << 23);
+        H[h] = (gh[0] >> 2) | (gh[1] << 6) | (gh[2] << 14) | (gh[3] << 22);
+    }
+    {
+        const uint32_t x = w[16], t = x ^ (x >> 1);
+        L[2] = __builtin_amdgcn_udot4(t & 0x02020202u, W0, 0u, false) >> 1;
+        H[2] = __builtin_amdgcn_udot4(t & 0x04040404u, W0, 0u, false) >> 2;
+    }
+    uint32_t mf[2], mr[2];
+    const uint32_t pb = FULL5 ? 5u : pa.pb;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        uint32_t SL[5], SH[5];
+        SL[0] = L[h];
+        SH[0] = H[h];
+#pragma unroll
+        for (uint32_t i = 1; i < 5; ++i) {
+            SL[i] = __builtin_amdgcn_alignbit(L[h + 1], L[h], i);
+            SH[i] = __builtin_amdgcn_alignbit(H[h + 1], H[h], i);
+        }
+        mf[h] = plane_match(L[h], H[h], L[h + 1], H[h + 1], pa.kl, pa.kh, pb, SL, SH);
+        mr[h] = plane_match(L[h], H[h], L[h + 1], H[h + 1], pa.rl, pa.rh, pb, SL, SH);
+    }
+    if (a.k < a.plen || (a.ablate & 1u)) mf[0] = mf[1] = mr[0] = mr[1] = 0;
+
+    // ---- block scan of the per-thread '\\n' counts -> cpre per chunk ----
+    __syncthreads();
+    {
+        uint32_t pre = incl - ttot, tot = 0;
+#pragma unroll
+        for (int ww = 0; ww < TPB / 64; ++ww) {
+            pre += ww < wid ? sh.wsum[ww][0] : 0u;
+            tot += sh.wsum[ww][0];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            sh.cpre[4 * tid + j] = (uint16_t)pre;
+            pre += ccnt[j];
+        }
+        if (tid == 0) {
+            a.tsum[tile].cnt = tot;
+            sh.tcnt = tot;
+        }
+    }
+    __syncthreads();             // cpre visible
+    if (tid == 0) {
+        const int lt = sh.last_chunk;            // highest thread region with a '\\n'
+        int lp = -1;
+        if (lt >= 0) {
+            int c = 4 * lt + 3;
+            while ((c == NCH_MAIN - 1 ? sh.tcnt : (uint32_t)sh.cpre[c + 1]) == sh.cpre[c]) --c;
+            const int64_t lim = (int64_t)len - g0;
+            lp = last_newline_in_chunk(buf, c, lim < TILE ? (int)lim : TILE);
+        }
+        sh.lastpos = lp;
+        a.tsum[tile].lnl = lp >= 0 ? a.abs_offset + (uint64_t)(g0 + lp + 1) : 0;
+    }
+
+    // ---- candidates -> LDS queue (one LDS atomic per wave) ----
+    const uint32_t *pw = (const uint32_t *)s_pr;
+    {
+        const uint32_t nc = __popc(mf[0]) + __popc(mf[1]) + __popc(mr[0]) + __popc(mr[1]);
+        const uint32_t incl_c = wave_incl_sum(nc);
+        const uint32_t wtotal = (uint32_t)__builtin_amdgcn_readlane((int)incl_c, 63);
+        if (wtotal) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&sh.qn, wtotal);
+            uint32_t pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)base, 0)) + incl_c - nc;
+#pragma unroll
+            for (int hs = 0; hs < 4; ++hs) {
+                uint32_t m = hs == 0 ? mf[0] : hs == 1 ? mf[1] : hs == 2 ? mr[0] : mr[1];
+                while (m) {
+                    const uint32_t bit = __ffs(m) - 1;
+                    m &= m - 1;
+                    const uint32_t q = 64u * (uint32_t)tid + 32u * (uint32_t)(hs & 1) + bit;
+                    const uint32_t e = (q << 1) | (uint32_t)(hs >> 1);
+                    if (pos < QCAP) sh.q[pos] = e;
+                    else verify_emit(a, buf, sh, tile, pw, e);   // queue full: process in place
+                    ++pos;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t nq = min(sh.qn, (uint32_t)QCAP);
+    for (uint32_t h = tid; h < nq; h += TPB) verify_emit(a, buf, sh, tile, pw, sh.q[h]);
+    if (nq > 64 || sh.qn > QCAP) {
+        __syncthreads();
+        if (tid == 0) {
+            a.tsum[tile].nh = sh.nh;
+            a.tsum[tile].nx = sh.nh > (uint32_t)HMAX ? sh.nh : sh.nx;
+            if (sh.nh > (uint32_t)HMAX || (sh.nh && sh.tcnt == 0)) atomicOr(a.err, INFO_LONGSEG);
+        }
+    } else if (tid == 0) {
+        a.tsum[tile].nh = sh.nh;
+        a.tsum[tile].nx = sh.nh > (uint32_t)HMAX ? sh.nh : sh.nx;
+        if (sh.nh > (uint32_t)HMAX || (sh.nh && sh.tcnt == 0)) atomicOr(a.err, INFO_LONGSEG);
+    }
+}
 
 // Resolve one hit: global line index / line start from the tile scans, the
 // reference's sequence-line rule (lib/kmers.js:151-155), first-occurrence
@@ -1368,6 +1629,11 @@ hipError_t launch_lines(const TileArgs &a, bool lookback, hipStream_t s) {
     return hipGetLastError();
 }
 
+hipError_t launch_scan_planes(const ScanArgs &a, const PlaneArgs &pa, hipStream_t s) {
+    if (pa.pb >= 5) hipLaunchKernelGGL((scan_planes_kernel<true>), dim3(a.n_tiles), dim3(TPB), 0, s, a, pa);
+    else hipLaunchKernelGGL((scan_planes_kernel<false>), dim3(a.n_tiles), dim3(TPB), 0, s, a, pa);
+    return hipGetLastError();
+}
 hipError_t launch_scan_tiles(const ScanArgs &a, hipStream_t s) {
     if (a.plen >= 4) hipLaunchKernelGGL((scan_tile_kernel<true>), dim3(a.n_tiles), dim3(TPB), 0, s, a);
     else hipLaunchKernelGGL((scan_tile_kernel<false>), dim3(a.n_tiles), dim3(TPB), 0, s, a);

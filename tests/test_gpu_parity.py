@@ -54,6 +54,30 @@ def test_record_path_matches(native, golden, inputs):
     assert not bad, bad[:5]
 
 
+def test_byte_scan_kernel_matches(native, golden, inputs):
+    # the byte-SWAR scan kernel (used for non-ACGT prefixes) on ACGT prefixes too
+    bad = _run_cases(native, golden, inputs, flags=native.FLAG_BYTE_SCAN,
+                     select=lambda c: c["step"] == 1 and c["prefix"] in ("ATGAC", "A", "GTCAT", "AT"))
+    assert not bad, bad[:5]
+
+
+def test_chunks_must_end_at_line_ends(native):
+    import torch
+    data = b"@r\nACGTATGACGGGTTTACGATGACA\n+\nIIIIIIIIIIIIIIIIIIIIIIII\n"
+    t = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    ctr = native.Counter(k=8, prefix=b"ATGAC")
+    ctr.reset()
+    ctr.feed_device(t.data_ptr(), 10)            # ends inside the sequence line
+    torch.cuda.synchronize()
+    with pytest.raises(native.KmerError):
+        ctr.feed_device(t.data_ptr() + 10, len(data) - 10)
+    ctr.reset()
+    ctr.feed_device(t.data_ptr(), len(data))
+    from oracle import oracle
+    assert ctr.finish().entries() == oracle.count_buffer(data, b"ATGAC", 8, 1)
+    ctr.close()
+
+
 def test_small_batches_chain_lines(native, golden, inputs):
     # 4 KiB batches: many chunks per input, lines carried across chunk boundaries
     bad = _run_cases(native, golden, inputs, batch_bytes=4096,
