@@ -750,6 +750,10 @@ __device__ __forceinline__ void verify_emit(const ScanArgs &a, const uint8_t *bu
         const uint32_t mk = n >= 4 ? 0xFFFFFFFFu : ((1u << (8 * n)) - 1u);
         ok = ((lds_word(buf, q + (int)b) ^ pw[(strand ? KMAX_TILE / 4 : 0) + b / 4]) & mk) == 0;
     }
+    if (a.ablate & 4u) {                         // experiments: verified, no record
+        if (ok) atomicAdd(&sh.nx, 0u);
+        return;
+    }
     if (ok) emit_hit<true>(a, buf, sh, tile, e);
 }
 

@@ -23,7 +23,7 @@ for _ in range(10):
     v.sum()
 torch.cuda.synchronize()
 out["torch_sum_GBs"] = n * 317 * 10 / (time.perf_counter() - t0) / 1e9
-modes = (("full", 0), ("no_hits", 1 << 8), ("no_swar", (1 << 8) | (1 << 9)))
+modes = (("full", 0), ("byte_scan", 4), ("no_hits", 1 << 8), ("no_emit", 1 << 10))
 for name, flags in modes:
     ctr = Counter(k=16, prefix=b"ATGAC", flags=flags)
     ts, fs, fin = [], [], []

@@ -7,7 +7,7 @@ path = sys.argv[1]
 which = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 r = list(csv.DictReader(open(path)))
 r.sort(key=lambda x: int(x['Start_Timestamp']))
-idx = [i for i, x in enumerate(r) if 'scan_tile' in x['Kernel_Name']]
+idx = [i for i, x in enumerate(r) if 'scan_tile' in x['Kernel_Name'] or 'scan_planes' in x['Kernel_Name']]
 a, b = idx[which], idx[which + 1]
 t0 = int(r[a]['Start_Timestamp'])
 prev = None
