@@ -34,7 +34,10 @@ using namespace kmerhip;
 
 namespace {
 
-enum Mode { MODE_PACKED, MODE_TILE_REC, MODE_GENERAL };
+// PACKED: tile scan, packed keys; TILE_REC: tile scan, records (host merge);
+// WINDOWS: dense hits (no / 1-3 base prefix), every window ranked; GENERAL:
+// lines + windows kernels, records (any k, step, prefix).
+enum Mode { MODE_PACKED, MODE_TILE_REC, MODE_WINDOWS, MODE_GENERAL };
 
 struct Ent {
     uint64_t count;
@@ -95,6 +98,10 @@ struct kmer_ctx {
     // per tile
     uint64_t tile_cap = 0;
     DBuf<TileSum> tsum, tscan, bsum, bscan;
+    DBuf<uint64_t> wcount, wbase;  // dense-hit path: windows / first rank per sequence line
+    DBuf<uint32_t> tcount;         // dense-hit path: '\n' per tile
+    DBuf<uint64_t> tbase, nlpos;   // ... exclusive scan, chunk-relative '\n' positions
+    uint64_t host_lines = 0;       // StreamPos.lines as last seen by the host (dense-hit path)
     DBuf<HitRec> hits, ovf;
     DBuf<unsigned long long> lb_cnt, lb_lnl;   // general path look-back
     DBuf<uint64_t> tp_cnt, tp_lnl;             // general path, two-pass debug mode
@@ -209,7 +216,7 @@ kmer_status ensure_tiles(kmer_ctx *c, uint64_t n_tiles) {
     if (n_tiles <= c->tile_cap) return KMER_OK;
     const uint64_t cap = std::max<uint64_t>(n_tiles, 1024);
     hipStream_t s = c->stream;
-    if (c->mode == MODE_GENERAL) {
+    if (c->mode == MODE_GENERAL || c->mode == MODE_WINDOWS) {
         HIPCHK(c, c->lb_cnt.ensure(cap, s));
         HIPCHK(c, c->lb_lnl.ensure(cap, s));
         HIPCHK(c, c->tp_cnt.ensure(cap, s));
@@ -475,7 +482,12 @@ kmer_status two_pass_prefix(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_
     return KMER_OK;
 }
 
-kmer_status general_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s) {
+kmer_status read_pos(kmer_ctx *c, StreamPos *pos);
+
+// Sequence-line descriptors of a chunk (lines kernel: decoupled look-back, or
+// the two-pass debug mode); *nlines = descriptors written.
+kmer_status collect_lines(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s,
+                          uint64_t *nlines_out) {
     const bool lookback = !(c->p.flags & KMER_FLAG_TWO_PASS);
     HIPCHK(c, c->lines.ensure(1 << 16, s));
     TileArgs a;
@@ -530,7 +542,14 @@ kmer_status general_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n
         }
         break;
     }
-    const uint64_t nlines = c->h_small[6];
+    *nlines_out = c->h_small[6];
+    return KMER_OK;
+}
+
+kmer_status general_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s) {
+    uint64_t nlines = 0;
+    kmer_status st = collect_lines(c, d, len, n_tiles, s, &nlines);
+    if (st) return st;
     uint64_t nrec = 0;
     if (nlines) {
         WindowArgs w;
@@ -577,6 +596,108 @@ kmer_status general_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n
     return KMER_OK;
 }
 
+// Dense-hit path: every window of every sequence line goes to its rank slot.
+kmer_status windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s) {
+    const uint64_t li0 = c->host_lines;
+    kmer_status st;
+    // newline positions of the chunk (two streaming passes, no look-back)
+    HIPCHK(c, c->tcount.ensure(n_tiles, s));
+    HIPCHK(c, c->tbase.ensure(n_tiles, s));
+    HIPCHK(c, hipEventRecord(c->ev0, s));
+    HIPCHK(c, launch_nl_count(d, len, n_tiles, c->tcount.p, c->d_err, s));
+    ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tcount.p, c->tbase.p, (uint64_t)0, (size_t)n_tiles,
+                                           rocprim::plus<uint64_t>(), s));
+    HIPCHK(c, hipMemcpyAsync(c->h_small + 14, c->tbase.p + n_tiles - 1, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(c->h_small + 15, c->tcount.p + n_tiles - 1, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    st = check_err(c, (uint32_t)c->h_small[5]);
+    if (st) return st;
+    const uint64_t n_nl = c->h_small[14] + (uint32_t)c->h_small[15];
+    HIPCHK(c, c->nlpos.ensure(n_nl + 1, s));
+    HIPCHK(c, launch_nl_write(d, len, n_tiles, c->tbase.p, c->nlpos.p, s));
+    const uint64_t first = (1u - (uint32_t)li0) & 3u;
+    const uint64_t n_seq = n_nl >= first ? (n_nl - first) / 4 + 1 : 0;
+    uint64_t total = 0;
+    if (n_seq) {
+        HIPCHK(c, c->lines.ensure(n_seq, s));
+        HIPCHK(c, c->wcount.ensure(n_seq, s));
+        HIPCHK(c, c->wbase.ensure(n_seq, s));
+        HIPCHK(c, launch_seq_lines(c->nlpos.p, n_nl, len, li0, n_seq, c->p.k, c->lines.p, c->wcount.p, c->d_err, s));
+        ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->wcount.p, c->wbase.p, (uint64_t)0, (size_t)n_seq,
+                                               rocprim::plus<uint64_t>(), s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 14, c->wbase.p + n_seq - 1, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 15, c->wcount.p + n_seq - 1, 8, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(c, launch_pos_after(c->d_pos, li0 + n_nl, d, len, c->d_ends_open, s));
+    HIPCHK(c, hipEventRecord(c->ev1, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    if (n_seq) total = c->h_small[14] + c->h_small[15];
+    c->host_lines = li0 + n_nl;
+    {
+        float ms = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        c->scan_ms += ms;
+        c->feed_ms += ms;
+    }
+    st = ensure_rank_arrays(c, c->n_hits + total, c->n_hits, s);
+    if (st) return st;
+    HIPCHK(c, hipEventRecord(c->ev0, s));
+    WinArgs w;
+    memset(&w, 0, sizeof(w));
+    w.data = d;
+    w.len = len;
+    w.lines = c->lines.p;
+    w.n_lines = n_seq;
+    w.li0 = li0;
+    w.wbase = c->wbase.p;
+    w.k = c->p.k;
+    w.plen = (uint32_t)c->prefix.size();
+    auto code = [](char ch) -> uint64_t { return ch == 'A' ? 0u : ch == 'C' ? 1u : ch == 'G' ? 2u : 3u; };
+    for (char ch : c->prefix) w.pcode = (w.pcode << 2) | code(ch);
+    for (char ch : c->rprefix) w.rcode = (w.rcode << 2) | code(ch);
+    w.smask = (c->kbits >= 64) ? ~0ull : ((1ull << c->kbits) - 1ull);
+    w.invalid_key = c->kbits >= 63 ? ~0ull : (1ull << c->kbits);
+    w.out_base = c->n_hits;
+    w.rkey = c->rkey.p;
+    w.rkey32 = c->narrow ? c->rkey32.p : nullptr;
+    w.rord = c->rord.p;
+    w.ridx = c->ridx.p;
+    w.err = c->d_err;
+    for (int attempt = 0; attempt < 8; ++attempt) {
+        w.recs = c->recs.p;
+        w.rec_count = c->d_rec_count;
+        w.rec_cap = c->recs.cap;
+        HIPCHK(c, hipMemsetAsync(c->d_rec_count, 0, 8, s));
+        HIPCHK(c, launch_windows_packed(w, s));
+        HIPCHK(c, hipEventRecord(c->ev1, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        const uint32_t e = (uint32_t)c->h_small[5];
+        st = check_err(c, e);
+        if (st) return st;
+        float ms = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        c->feed_ms += ms;
+        if (e & ERR_REC_OVERFLOW) {                 // rank slots are rewritten by the redo
+            HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
+            st = ensure_records(c, c->h_small[0] + 1024);
+            if (st) return st;
+            continue;
+        }
+        break;
+    }
+    c->n_hits += total;
+    c->chunk_open = c->h_small[7] != 0;
+    const uint64_t nrec = c->h_small[0];
+    if (nrec) {
+        st = drain_records(c, d, nrec, s);
+        if (st) return st;
+    }
+    c->abs_offset += len;
+    return KMER_OK;
+}
+
 kmer_status feed(kmer_ctx *c, const uint8_t *d, uint64_t len, hipStream_t s) {
     if (len == 0) return KMER_OK;
     const uint64_t n_tiles64 = (len + TILE - 1) / TILE;
@@ -586,7 +707,9 @@ kmer_status feed(kmer_ctx *c, const uint8_t *d, uint64_t len, hipStream_t s) {
         return fail(c, KMER_E_BAD_PARAM, "the previous chunk did not end with '\\n' (chunks must be cut at line ends)");
     kmer_status st = ensure_tiles(c, n_tiles);
     if (st) return st;
-    return c->mode == MODE_GENERAL ? general_feed(c, d, len, n_tiles, s) : scan_feed(c, d, len, n_tiles, s);
+    if (c->mode == MODE_GENERAL) return general_feed(c, d, len, n_tiles, s);
+    if (c->mode == MODE_WINDOWS) return windows_feed(c, d, len, n_tiles, s);
+    return scan_feed(c, d, len, n_tiles, s);
 }
 
 kmer_status reset(kmer_ctx *c) {
@@ -597,6 +720,7 @@ kmer_status reset(kmer_ctx *c) {
     c->abs_offset = 0;
     c->n_hits = 0;
     c->n_cross = 0;
+    c->host_lines = 0;
     c->long_seg = false;
     c->chunk_open = false;
     c->out_pending = false;
@@ -612,8 +736,6 @@ kmer_status reset(kmer_ctx *c) {
 // ---------------------------------------------------------------------------
 // Place the cross entries: sorted by order key they take the natural slots
 // sorted ascending (the slots that tile-local ranking left to them).
-kmer_status read_pos(kmer_ctx *c, StreamPos *pos);
-
 kmer_status apply_cross(kmer_ctx *c) {
     hipStream_t s = c->stream;
     const uint64_t n = c->n_cross;
@@ -793,7 +915,7 @@ kmer_status finish(kmer_ctx *c, kmer_result **out) {
     uint64_t nu = 0;
     c->n_out = 0;
     const bool sync = out || c->p.max_keys;
-    if (c->mode == MODE_PACKED) {
+    if (c->mode == MODE_PACKED || c->mode == MODE_WINDOWS) {
         st = apply_cross(c);
         if (st) return st;
         st = rank_finish(c, c->n_hits, false, false, &nu, sync);
@@ -895,15 +1017,19 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
     const uint32_t k = pp->k, plen = (uint32_t)c->prefix.size();
     bool acgt = plen > 0;
     for (char ch : c->prefix) acgt &= ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T';
-    if (pp->step == 1 && acgt && plen <= k && k <= (uint32_t)KMAX_DENSE && !(pp->flags & KMER_FLAG_NO_DENSE))
+    const bool dense_ok = !(pp->flags & KMER_FLAG_NO_DENSE) && pp->step == 1 && plen <= k;
+    if (dense_ok && (plen == 0 ? k <= 31 : (acgt && plen <= 3 && k <= (uint32_t)KMAX_DENSE)))
+        c->mode = MODE_WINDOWS;
+    else if (dense_ok && acgt && k <= (uint32_t)KMAX_DENSE)
         c->mode = MODE_PACKED;
     else if (pp->step == 1 && plen > 0 && k <= (uint32_t)KMAX_TILE)
         c->mode = MODE_TILE_REC;
     else
         c->mode = MODE_GENERAL;
-    c->kbits = c->mode == MODE_PACKED ? 2 * (k - plen) : 0;
-    c->narrow = c->mode == MODE_PACKED && c->kbits <= 31;
-    c->planes = c->mode != MODE_GENERAL && acgt && !(pp->flags & KMER_FLAG_BYTE_SCAN);
+    const bool packed_keys = c->mode == MODE_PACKED || c->mode == MODE_WINDOWS;
+    c->kbits = packed_keys ? 2 * (k - plen) : 0;
+    c->narrow = packed_keys && c->kbits <= 31;
+    c->planes = (c->mode == MODE_PACKED || c->mode == MODE_TILE_REC) && acgt && !(pp->flags & KMER_FLAG_BYTE_SCAN);
     if (c->planes) {
         auto code = [](char ch) -> uint32_t { return ch == 'A' ? 0u : ch == 'C' ? 1u : ch == 'G' ? 2u : 3u; };
         c->pargs.pb = std::min<uint32_t>(plen, 5);
@@ -961,7 +1087,8 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
 kmer_status kmer_close(kmer_ctx *c) {
     if (!c) return KMER_E_BAD_PARAM;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (auto *b : {&c->tp_cnt, &c->tp_lnl, &c->rkey, &c->rkey2, &c->rord, &c->rcnt, &c->xord, &c->xord2,
+    c->tcount.release();
+    for (auto *b : {&c->tbase, &c->nlpos, &c->wcount, &c->wbase, &c->tp_cnt, &c->tp_lnl, &c->rkey, &c->rkey2, &c->rord, &c->rcnt, &c->xord, &c->xord2,
                     &c->xkey, &c->xkey2, &c->ukey, &c->first, &c->cnt_out, &c->roff})
         b->release();
     for (auto *b : {&c->ridx, &c->ridx2, &c->opos, &c->xslot, &c->rkey32, &c->rkey32b}) b->release();
@@ -1081,7 +1208,8 @@ kmer_status kmer_count_file(kmer_ctx *c, const char *path, kmer_result **out) {
 
 kmer_status kmer_partial_device(kmer_ctx *c, const void **d_keys, const void **d_vals, uint64_t *n) {
     if (!c || !d_keys || !d_vals || !n) return KMER_E_BAD_PARAM;
-    if (c->mode != MODE_PACKED) return fail(c, KMER_E_STATE, "configuration has no packed keys");
+    if (c->mode != MODE_PACKED && c->mode != MODE_WINDOWS)
+        return fail(c, KMER_E_STATE, "configuration has no packed keys");
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
     kmer_status st = apply_cross(c);
     if (st) return st;
@@ -1098,7 +1226,8 @@ kmer_status kmer_partial_device(kmer_ctx *c, const void **d_keys, const void **d
 kmer_status kmer_finish_merged(kmer_ctx *c, const void *d_keys, const void *d_vals, uint64_t n,
                                uint64_t total_lines, kmer_result **out) {
     if (!c || (n && (!d_keys || !d_vals))) return KMER_E_BAD_PARAM;
-    if (c->mode != MODE_PACKED) return fail(c, KMER_E_STATE, "configuration has no packed keys");
+    if (c->mode != MODE_PACKED && c->mode != MODE_WINDOWS)
+        return fail(c, KMER_E_STATE, "configuration has no packed keys");
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
     if (out) *out = nullptr;
     hipStream_t s = c->stream;
@@ -1168,6 +1297,7 @@ kmer_status kmer_set_position(kmer_ctx *c, uint64_t lines_before, uint64_t byte_
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
     HIPCHK(c, launch_set_pos(c->d_pos, lines_before, c->stream));
     c->abs_offset = byte_offset;
+    c->host_lines = lines_before;
     return KMER_OK;
 }
 

@@ -226,6 +226,31 @@ struct WindowArgs {
     unsigned int *err;
 };
 
+// Dense-hit path (empty or 1-2 base ACGT prefix, step 1, k <= 32): every
+// window of every sequence line gets a rank slot -- its position in the
+// first-occurrence order: line base (scan of 2W per sequence line) + s for
+// the forward window at s, + W + (W-1-s) for the reverse strand's.
+struct WinArgs {
+    const uint8_t *data;
+    uint64_t len;
+    const SeqLine *lines;          // by sequence ordinal (len 0: no windows)
+    uint64_t n_lines;
+    uint64_t li0;                  // line index of the chunk's first line
+    const uint64_t *wbase;         // by sequence ordinal: rank of the line's first window (chunk-relative)
+    uint32_t k, plen;
+    uint64_t pcode, rcode;         // P and rc(P) as 2-bit codes (first base most significant)
+    uint64_t smask, invalid_key;
+    uint64_t out_base;
+    uint64_t *rkey;
+    uint32_t *rkey32;
+    uint64_t *rord;
+    uint32_t *ridx;
+    Record *recs;
+    unsigned long long *rec_count;
+    uint64_t rec_cap;
+    unsigned int *err;
+};
+
 // ---- launchers (kmer_kernels.hip) ------------------------------------------
 hipError_t launch_lines(const TileArgs &a, bool lookback, hipStream_t s);
 hipError_t launch_scan_tiles(const ScanArgs &a, hipStream_t s);
@@ -259,6 +284,15 @@ hipError_t launch_merge_prep(const uint64_t *keys, const Agg *vals, uint64_t n, 
                              uint64_t *rord, uint64_t *rcnt, uint32_t *ridx, hipStream_t s);
 hipError_t launch_gather_records(const Record *recs, const uint64_t *key_off, uint64_t n,
                                  const uint8_t *data, uint8_t *out, hipStream_t s);
+hipError_t launch_nl_count(const uint8_t *data, uint64_t len, uint32_t n_tiles, uint32_t *tcount, unsigned int *err,
+                           hipStream_t s);
+hipError_t launch_nl_write(const uint8_t *data, uint64_t len, uint32_t n_tiles, const uint64_t *tbase, uint64_t *nl,
+                           hipStream_t s);
+hipError_t launch_seq_lines(const uint64_t *nl, uint64_t n_nl, uint64_t len, uint64_t li0, uint64_t n_seq, uint32_t k,
+                            SeqLine *lines, uint64_t *wcount, unsigned int *err, hipStream_t s);
+hipError_t launch_pos_after(StreamPos *pos, uint64_t lines, const uint8_t *data, uint64_t len,
+                            unsigned long long *ends_open, hipStream_t s);
+hipError_t launch_windows_packed(const WinArgs &a, hipStream_t s);
 hipError_t launch_synth_fastq(uint8_t *out, uint64_t seed, uint64_t first_read, uint64_t n_reads,
                               hipStream_t s);
 

@@ -1357,6 +1357,218 @@ __global__ __launch_bounds__(256) void windows_kernel(WindowArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// dense-hit path: windows of sequence lines straight into rank slots
+// ---------------------------------------------------------------------------
+// 2-bit code of the k bytes at p (first base most significant); *exotic if a
+// byte is not A/C/G/T.  `safe`: p + k + 4 stays inside the buffer (word loads).
+__device__ __forceinline__ uint64_t window_code(const uint8_t *p, uint32_t k, bool safe, bool *exotic) {
+    uint64_t code = 0;
+    bool ex = false;
+    if (safe) {
+        const uintptr_t ad = (uintptr_t)p;
+        const uint32_t *wp = (const uint32_t *)(ad & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)(ad & 3);
+        uint32_t cur = wp[0];
+#pragma unroll 1
+        for (uint32_t b = 0, i = 0; b < k; b += 4, ++i) {
+            const uint32_t nxt = wp[i + 1];
+            const uint32_t x = align4(nxt, cur, sh);
+            cur = nxt;
+            const uint32_t nb = k - b >= 4 ? 4u : k - b;
+            const uint32_t mk = nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
+            const uint32_t c = ((x >> 1) ^ (x >> 2)) & 0x03030303u;
+            ex |= ((__builtin_amdgcn_perm(0u, 0x54474341u, c) ^ x) & mk) != 0;
+            const uint32_t pk = ((c & 3u) << 6) | (((c >> 8) & 3u) << 4) | (((c >> 16) & 3u) << 2) | ((c >> 24) & 3u);
+            code = (code << (2 * nb)) | (pk >> (2 * (4 - nb)));
+        }
+    } else {
+#pragma unroll 1
+        for (uint32_t b = 0; b < k; ++b) {
+            const uint32_t x = p[b];
+            const uint32_t c = ((x >> 1) ^ (x >> 2)) & 3u;
+            ex |= x != ((0x54474341u >> (8 * c)) & 0xFFu);
+            code = (code << 2) | c;
+        }
+    }
+    *exotic = ex;
+    return code;
+}
+
+__device__ __forceinline__ void win_record(const WinArgs &a, uint64_t order, uint64_t pos, uint32_t strand) {
+    const unsigned long long n = atomicAdd(a.rec_count, 1ull);
+    if (n < a.rec_cap) {
+        Record rec;
+        rec.order = order;
+        rec.pos = pos;
+        rec.len = a.k;
+        rec.strand = strand;
+        a.recs[n] = rec;
+    } else {
+        atomicOr(a.err, ERR_REC_OVERFLOW);
+    }
+}
+
+__device__ __forceinline__ void win_place(const WinArgs &a, uint64_t rank, uint64_t key, uint64_t order) {
+    if (a.rkey32) a.rkey32[rank] = (uint32_t)key;
+    else a.rkey[rank] = key;
+    a.rord[rank] = order;
+    a.ridx[rank] = (uint32_t)rank;
+}
+
+// ---- sequence lines of a chunk without look-back (dense-hit path) ----
+// pass 1: '\n' count per 16 KiB tile; pass 2 (after a scan): the chunk-relative
+// position of every '\n', in order; then sequence line m is read off the
+// newline array directly (line li runs from NL[li-li0-1]+1 to NL[li-li0]).
+__device__ __forceinline__ uint32_t thread_nl_flags(const uint8_t *data, uint64_t len, int64_t g, uint32_t (&z)[16],
+                                                    uint32_t *orall) {
+    uint32_t cnt = 0, o = 0;
+    if ((uint64_t)g + 64 <= len) {
+        const uint4 *src = (const uint4 *)(data + g);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint4 x = src[j];
+            o |= x.x | x.y | x.z | x.w;
+            z[4 * j] = nl_flags(x.x);
+            z[4 * j + 1] = nl_flags(x.y);
+            z[4 * j + 2] = nl_flags(x.z);
+            z[4 * j + 3] = nl_flags(x.w);
+        }
+    } else {
+#pragma unroll 1
+        for (int j = 0; j < 16; ++j) {
+            uint32_t x = 0;
+            for (int b = 0; b < 4; ++b) {
+                const uint64_t p = (uint64_t)g + 4 * j + b;
+                x |= (uint32_t)(p < len ? data[p] : 0u) << (8 * b);
+            }
+            o |= x;
+            z[j] = nl_flags(x);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) cnt += __popc(z[j]);
+    *orall = o;
+    return cnt;
+}
+
+__global__ __launch_bounds__(256) void nl_count_kernel(const uint8_t *data, uint64_t len, uint32_t *tcount,
+                                                       unsigned int *err) {
+    __shared__ uint32_t ws[4];
+    uint32_t z[16], o = 0;
+    const int64_t g = (int64_t)blockIdx.x * TILE + 64 * threadIdx.x;
+    const uint32_t cnt = (uint64_t)g < len ? thread_nl_flags(data, len, g, z, &o) : 0u;
+    if (o & 0x80808080u) atomicOr(err, ERR_NONASCII);
+    const uint32_t incl = wave_incl_sum(cnt);
+    if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) tcount[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ __launch_bounds__(256) void nl_write_kernel(const uint8_t *data, uint64_t len, const uint64_t *tbase,
+                                                       uint64_t *nl) {
+    __shared__ uint32_t ws[4];
+    uint32_t z[16], orall;
+    const int64_t g = (int64_t)blockIdx.x * TILE + 64 * threadIdx.x;
+    const uint32_t cnt = (uint64_t)g < len ? thread_nl_flags(data, len, g, z, &orall) : 0u;
+    const uint32_t incl = wave_incl_sum(cnt);
+    const int wid = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 63) ws[wid] = incl;
+    __syncthreads();
+    uint64_t o = tbase[blockIdx.x] + incl - cnt;
+    for (int w = 0; w < wid; ++w) o += ws[w];
+    if (!cnt) return;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        uint32_t m = z[j];
+        while (m) {
+            const int b = __ffs(m) - 1;          // bit 7 of a byte
+            m &= m - 1;
+            nl[o++] = (uint64_t)g + 4 * j + (b >> 3);
+        }
+    }
+}
+
+// sequence ordinal m -> SeqLine (len 0: no windows) and its window count 2W
+__global__ __launch_bounds__(256) void seq_lines_kernel(const uint64_t *nl, uint64_t n_nl, uint64_t len,
+                                                        uint64_t li0, uint64_t n_seq, uint32_t k, SeqLine *lines,
+                                                        uint64_t *wcount, unsigned int *err) {
+    const uint64_t first = (1u - (uint32_t)li0) & 3u;      // first sequence line, relative to li0
+    for (uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; m < n_seq; m += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t r = first + 4 * m;                  // line index - li0
+        SeqLine sl;
+        sl.line_index = li0 + r;
+        sl.start = 0;
+        sl.len = 0;
+        uint64_t w2 = 0;
+        if (r <= n_nl) {
+            const uint64_t st = r == 0 ? 0 : nl[r - 1] + 1;
+            const uint64_t en = r < n_nl ? nl[r] : len;    // (r == n_nl: the open trailing segment)
+            const uint64_t L = en > st ? en - st : 0;
+            if (L > 1 && L >= k) {
+                sl.start = st;
+                sl.len = L;
+                const uint64_t W = L - k + 1;
+                if (W - 1 > MAXREL) atomicOr(err, ERR_LINE_TOO_LONG);
+                w2 = 2 * W;
+            }
+        }
+        lines[m] = sl;
+        wcount[m] = w2;
+    }
+}
+
+__global__ void pos_after_kernel(StreamPos *pos, uint64_t lines, const uint8_t *data, uint64_t len,
+                                 unsigned long long *ends_open) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        pos->lines = lines;
+        pos->ends_open = (len > 0 && data[len - 1] != '\n') ? 1 : 0;
+        *ends_open = pos->ends_open;
+    }
+}
+
+// one workgroup per sequence line (grid-stride), one thread per window
+__global__ __launch_bounds__(256) void windows_packed_kernel(WinArgs a) {
+    const uint32_t k = a.k, plen = a.plen;
+    const uint32_t tailbits = 2 * (k - plen);
+    for (uint64_t li = blockIdx.x; li < a.n_lines; li += gridDim.x) {
+        const SeqLine sl = a.lines[li];          // dense by sequence ordinal
+        if (sl.len == 0) continue;
+        const uint64_t W = sl.len - k + 1;
+        if (W - 1 > MAXREL) continue;            // reported by seq_lines_kernel
+        const uint64_t base = a.out_base + a.wbase[li];
+        const uint64_t lo = sl.line_index << 24;
+        for (uint64_t s = threadIdx.x; s < W; s += blockDim.x) {
+            const uint64_t pos = sl.start + s;
+            bool exotic;
+            const uint64_t code = window_code(a.data + pos, k, pos + k + 4 <= a.len, &exotic);
+            const uint64_t rc = revcomp_code(code, k);
+            const uint64_t of = lo | s, orr = lo | (1ull << 23) | (uint64_t)(MAXREL - s);
+            // prefix tests on the codes: a non-ACGT byte in the prefix bases never
+            // matches (its code aliases, so exotic windows re-check the bytes)
+            bool mf = plen == 0 || (code >> tailbits) == a.pcode;
+            bool mr = plen == 0 || (rc >> tailbits) == a.pcode;
+            if (exotic && plen) {
+                for (uint32_t b = 0; b < plen; ++b) {
+                    const uint32_t cf = (uint32_t)(a.pcode >> (2 * (plen - 1 - b))) & 3u;
+                    const uint8_t xf = a.data[pos + b];
+                    mf = mf && xf == (uint8_t)((0x54474341u >> (8 * cf)) & 0xFFu);
+                    const uint32_t cr = (uint32_t)(a.rcode >> (2 * (plen - 1 - b))) & 3u;
+                    const uint8_t xr = a.data[pos + k - plen + b];
+                    mr = mr && xr == (uint8_t)((0x54474341u >> (8 * cr)) & 0xFFu);
+                }
+            }
+            const uint64_t rf = base + s, rr = base + W + (W - 1 - s);
+            win_place(a, rf, (mf && !exotic) ? (code & a.smask) : a.invalid_key, of);
+            win_place(a, rr, (mr && !exotic) ? (rc & a.smask) : a.invalid_key, orr);
+            if (exotic) {
+                if (mf) win_record(a, of, pos, 0);
+                if (mr) win_record(a, orr, pos, 1);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // result materialisation
 // ---------------------------------------------------------------------------
 // Cross entries (in natural-slot order) sorted by order key: the i-th
@@ -1741,6 +1953,35 @@ hipError_t launch_gather_records(const Record *recs, const uint64_t *key_off, ui
     return hipGetLastError();
 }
 
+hipError_t launch_nl_count(const uint8_t *data, uint64_t len, uint32_t n_tiles, uint32_t *tcount, unsigned int *err,
+                           hipStream_t s) {
+    hipLaunchKernelGGL(nl_count_kernel, dim3(n_tiles), dim3(256), 0, s, data, len, tcount, err);
+    return hipGetLastError();
+}
+hipError_t launch_nl_write(const uint8_t *data, uint64_t len, uint32_t n_tiles, const uint64_t *tbase, uint64_t *nl,
+                           hipStream_t s) {
+    hipLaunchKernelGGL(nl_write_kernel, dim3(n_tiles), dim3(256), 0, s, data, len, tbase, nl);
+    return hipGetLastError();
+}
+hipError_t launch_seq_lines(const uint64_t *nl, uint64_t n_nl, uint64_t len, uint64_t li0, uint64_t n_seq, uint32_t k,
+                            SeqLine *lines, uint64_t *wcount, unsigned int *err, hipStream_t s) {
+    if (n_seq)
+        hipLaunchKernelGGL(seq_lines_kernel, dim3(grid_for(n_seq)), dim3(256), 0, s, nl, n_nl, len, li0, n_seq, k, lines,
+                           wcount, err);
+    return hipGetLastError();
+}
+hipError_t launch_pos_after(StreamPos *pos, uint64_t lines, const uint8_t *data, uint64_t len,
+                            unsigned long long *ends_open, hipStream_t s) {
+    hipLaunchKernelGGL(pos_after_kernel, dim3(1), dim3(64), 0, s, pos, lines, data, len, ends_open);
+    return hipGetLastError();
+}
+hipError_t launch_windows_packed(const WinArgs &a, hipStream_t s) {
+    if (a.n_lines) {
+        const uint64_t g = a.n_lines < 65536 ? a.n_lines : 65536;
+        hipLaunchKernelGGL(windows_packed_kernel, dim3((uint32_t)g), dim3(256), 0, s, a);
+    }
+    return hipGetLastError();
+}
 hipError_t launch_synth_fastq(uint8_t *out, uint64_t seed, uint64_t first_read, uint64_t n_reads, hipStream_t s) {
     const uint64_t chunks = (n_reads * 317 + 15) / 16;
     uint64_t blocks = (chunks + 255) / 256;

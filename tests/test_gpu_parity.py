@@ -298,3 +298,25 @@ def test_long_lines_and_dense_hits(native):
         ctr.close()
         assert len(got) == len(want), (k, p)
         assert first_diff(got, want) is None, (k, p)
+
+
+@pytest.mark.parametrize("k,prefix", [(31, b""), (21, b""), (16, b"AC"), (12, b"G"), (32, b"AT")])
+def test_dense_hit_path_vs_oracle(native, k, prefix):
+    # empty / 1-3 base prefixes: every window ranked directly (SURVEY.md C3 shape)
+    import torch
+    from kmerjs_amd import synth_fastq_device
+    from oracle import oracle
+    n = 20_000
+    buf = torch.empty(n * 317, dtype=torch.uint8, device="cuda")
+    synth_fastq_device(buf.data_ptr(), 3, 0, n)
+    torch.cuda.synchronize()
+    host = buf.cpu().numpy().tobytes()
+    want = oracle.count_buffer(host, prefix, k, 1)
+    ctr = native.Counter(k=k, prefix=prefix)
+    ctr.reset()
+    ctr.feed_device(buf.data_ptr(), 317 * 7000)          # two record-aligned chunks
+    ctr.feed_device(buf.data_ptr() + 317 * 7000, len(host) - 317 * 7000)
+    got = ctr.finish().entries()
+    ctr.close()
+    assert len(got) == len(want)
+    assert first_diff(got, want) is None
