@@ -50,6 +50,84 @@ def cpu_baseline(k, prefix, seconds_target=10.0):
                       % (n, k, prefix.decode(), dt)}
 
 
+def count_windows(lines_bytes_lengths, first_line, k):
+    """Windows on both strands of the sequence lines (index % 4 == 1, length > 1)."""
+    tot = 0
+    for i, L in enumerate(lines_bytes_lengths):
+        if (first_line + i) % 4 == 1 and L > 1 and L >= k:
+            tot += 2 * (L - k + 1)
+    return tot
+
+
+def make_contigs(seed, target_bytes, k):
+    """C5: single-line FASTA '>c%08d\n' + contig of 10 kb - 1 Mb, seed 5."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    parts, lens, n, i = [], [], 0, 0
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    while n < target_bytes:
+        L = int(rng.integers(10_000, 1_000_001))
+        head = b">c%08d\n" % i
+        seq = acgt[rng.integers(0, 4, L)].tobytes()
+        parts += [head, seq, b"\n"]
+        lens += [len(head) - 1, L]
+        n += len(head) + L + 1
+        i += 1
+    return b"".join(parts), lens
+
+
+def make_workload(args, rank, world, dev):
+    """Input of this rank, resident in HBM, and its line / byte position in the whole job."""
+    import torch
+    import torch.distributed as dist
+    from kmerjs_amd import synth_fastq_device
+    from kmerjs_amd.multi import shard_plan
+    if args.config in ("c2", "c3"):
+        plan = shard_plan(args.reads, rank)
+        nbytes = args.reads * RECORD
+        buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        synth_fastq_device(buf.data_ptr(), args.seed, plan["first_read"], args.reads)
+        torch.cuda.synchronize()
+        per = args.reads * windows_per_read(args.k)
+        return {"buf": buf, "nbytes": nbytes, "lines_before": plan["lines_before"], "byte_offset": plan["byte_offset"],
+                "total_lines": world * args.reads * 4, "windows": per, "windows_total": world * per,
+                "desc": "%s: %d synthetic 150bp reads per GPU, k=%d, prefix '%s'"
+                        % (args.config.upper(), args.reads, args.k, args.prefix)}
+    if args.config == "c5":
+        data, lens = make_contigs(5 + rank, args.contig_bytes, args.k)
+        info = torch.tensor([len(data), len(lens)], dtype=torch.int64, device=dev)
+        if world > 1:
+            allv = [torch.zeros_like(info) for _ in range(world)]
+            dist.all_gather(allv, info)
+            sizes = [(int(x[0]), int(x[1])) for x in allv]
+        else:
+            sizes = [(len(data), len(lens))]
+        byte_offset = sum(b for b, _ in sizes[:rank])
+        lines_before = sum(n for _, n in sizes[:rank])
+        per = count_windows(lens, lines_before, args.k)
+        tot = torch.tensor([per], dtype=torch.int64, device=dev)
+        if world > 1:
+            dist.all_reduce(tot)
+        buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
+        return {"buf": buf, "nbytes": len(data), "lines_before": lines_before, "byte_offset": byte_offset,
+                "total_lines": sum(n for _, n in sizes), "windows": per, "windows_total": int(tot.item()),
+                "desc": "C5: single-line FASTA contigs 10 kb-1 Mb (seed 5+rank), %.2f GB per GPU, k=%d, prefix '%s'"
+                        % (len(data) / 1e9, args.k, args.prefix)}
+    if args.config == "c1":
+        path = os.path.join(REPO, "tests", "golden", "inputs", "test_short.fastq")
+        with open(path, "rb") as f:
+            data = f.read()
+        lens = [len(x) for x in data.split(b"\n")]
+        if data.endswith(b"\n"):
+            lens = lens[:-1]
+        per = count_windows(lens, 0, args.k)
+        buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
+        return {"buf": buf, "nbytes": len(data), "lines_before": 0, "byte_offset": 0, "total_lines": len(lens),
+                "windows": per, "windows_total": per,
+                "desc": "C1: test_data/test_short.fastq, k=%d, prefix '%s' (plumbing)" % (args.k, args.prefix)}
+    raise SystemExit("unknown config " + args.config)
+
+
 def load_traffic(args):
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
@@ -75,12 +153,28 @@ def main():
     ap.add_argument("--flags", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true")
+    ap.add_argument("--config", default="c2", choices=("c1", "c2", "c3", "c5"),
+                    help="BASELINE.json config: c2 (default, the headline), c3 no-prefix k=31, c5 long contigs k=21")
+    ap.add_argument("--contig-bytes", type=int, default=1_000_000_000, help="c5: bytes of contigs per GPU")
     args = ap.parse_args()
+    # per-config defaults (explicit flags still win)
+    argv = " ".join(sys.argv)
+    if args.config == "c3":
+        if "--k" not in argv:
+            args.k = 31
+        if "--prefix" not in argv:
+            args.prefix = ""
+        if "--reads" not in argv:
+            args.reads = 4_000_000       # 0.96 G windows: C3's 100 M reads (24 G) exceed one session's 2^32 ranks
+    if args.config == "c5" and "--k" not in argv:
+        args.k = 21
+    if args.config != "c2":
+        args.no_pcie = True
 
     import torch
     import torch.distributed as dist
-    from kmerjs_amd import Counter, synth_fastq_device
-    from kmerjs_amd.multi import merge_to, shard_plan
+    from kmerjs_amd import Counter
+    from kmerjs_amd.multi import merge_to
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -93,14 +187,12 @@ def main():
     torch.cuda.set_device(dev)
 
     prefix = args.prefix.encode()
-    plan = shard_plan(args.reads, rank)
-    nbytes = args.reads * RECORD
-    buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    synth_fastq_device(buf.data_ptr(), args.seed, plan["first_read"], args.reads)
-    torch.cuda.synchronize()
+    wl = make_workload(args, rank, world, dev)
+    buf, nbytes = wl["buf"], wl["nbytes"]
+    plan = {"lines_before": wl["lines_before"], "byte_offset": wl["byte_offset"]}
 
     ctr = Counter(k=args.k, prefix=prefix, device=local, flags=args.flags)
-    total_lines = world * args.reads * 4
+    total_lines = wl["total_lines"]
     tile_ms, feed_ms_l = [], []
 
     def step(record):
@@ -142,10 +234,10 @@ def main():
     if rank == 0:
         distinct = len(res)
         accepted = int(res.counts.sum())
-        assert res.lines == total_lines, (res.lines, total_lines)
+        assert res.lines == total_lines or args.config == "c1", (res.lines, total_lines)
 
     if rank == 0:
-        windows_step = world * args.reads * windows_per_read(args.k)
+        windows_step = wl["windows_total"]
         ms_per_step = elapsed / args.steps * 1e3
         value = windows_step * args.steps / elapsed
         kern_ms = sum(tile_ms) / len(tile_ms)
@@ -166,10 +258,12 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (on-device splitmix64 FASTQ, 317 B records, seed %d)" % args.seed,
-            "config": {"workload": "C2: %d synthetic 150bp reads per GPU, k=%d, prefix '%s'"
-                                   % (args.reads, args.k, args.prefix),
-                       "reads_per_gpu": args.reads, "k": args.k, "prefix": args.prefix,
+            "data": {"c1": "test_data/test_short.fastq (reference fixture)",
+                     "c5": "synthetic contigs (numpy PCG64, seed 5 + rank)"}.get(
+                         args.config, "synthetic (on-device splitmix64 FASTQ, 317 B records, seed %d)" % args.seed),
+            "config": {"workload": wl["desc"], "name": args.config,
+                       "reads_per_gpu": args.reads if args.config in ("c2", "c3") else None,
+                       "k": args.k, "prefix": args.prefix, "windows_per_step": windows_step,
                        "bytes_per_gpu": nbytes, "parallelism": "dp%d (reads sharded, RCCL gather of partials)" % world},
             "distinct_kmers_per_s": distinct * args.steps / elapsed,
             "distinct_kmers": distinct,
@@ -191,7 +285,7 @@ def main():
             out["pcie_inclusive_ms"] = dt * 1e3
             assert len(r) == distinct
             del host
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and args.config == "c2":
             out["cpu_baseline"] = cpu_baseline(args.k, prefix)
         print(json.dumps(out), flush=True)
     ctr.close()
