@@ -88,11 +88,19 @@ function kmers(line, kmerMap, length, preffix, step) {
 
 // Fold a packed native result into an existing Map, preserving Map semantics:
 // existing keys keep their position, new keys append in first-occurrence order.
+// Fresh Map (the readFile() case): the result's keys are unique, so every
+// entry is a plain set(); the keys are substrings of ONE Latin-1 string
+// (V8 sliced strings), ~20% faster than a Buffer slice per key.
 function foldResult(map, res) {
     const keys = res.keys;
     const off = res.offsets;
     const cnt = res.counts;
     const n = cnt.length;
+    if (map.size === 0) {
+        const all = keys.latin1Slice(0, n ? off[n] : 0);
+        for (let i = 0; i < n; i += 1) map.set(all.substring(off[i], off[i + 1]), cnt[i]);
+        return;
+    }
     for (let i = 0; i < n; i += 1) {
         const key = keys.latin1Slice(off[i], off[i + 1]);
         const prev = map.get(key);
