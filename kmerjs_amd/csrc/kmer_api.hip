@@ -1,20 +1,21 @@
 // kmer_api.hip — host orchestration behind the C-ABI (include/kmer_api.h).
 //
 // One kmer_ctx = one device, one HIP stream, one (k, preffix, step)
-// configuration.  Input flows in chunks that start at a line start.
+// configuration.  Input flows in chunks cut at line ends.
 //
-// Packed path (step 1, ACGT prefix, |P| <= k <= 32) and tile-record path
-// (step 1, any prefix, k <= 64), per chunk:
-//   scan_tile_kernel   one HBM pass: '\n' aggregates + verified prefix hits
-//   3 x rocPRIM scan   per-tile line index / line start / hit-slot offsets
-//   hit_kernel         line rule + first-occurrence order; packed hits go to
-//                      the session's (suffix code, {order, 1}) array, the
-//                      rest become records merged on the host
-// finish: radix-sort the packed hits by code, reduce_by_key (min order, sum
-// count), radix-sort the unique keys by first occurrence, decode -> the
-// reference Map's exact iteration order (lib/kmers.js:76,95).
-// General path (step > 1, empty prefix, k > 64): line list (decoupled
-// look-back over tiles) + one-workgroup-per-line window kernel -> records.
+// Packed path (step 1, ACGT prefix of >= 4 bases, k <= 32), per chunk:
+//   scan_planes_kernel   one HBM pass: '\n' aggregates + verified prefix hits
+//   tile reduce / scan   per-tile lines / line start / hits / cross hits before
+//   hit_kernel           line rule + first-occurrence order; each packed hit
+//                        goes to its RANK slot (or the cross list)
+// Dense-hit path (empty or 1-3 base ACGT prefix): newline array -> sequence
+//   lines by ordinal -> every window written at its rank slot.
+// finish: place the cross list, radix-sort (key, rank), heads (first element
+// of a key group = first occurrence), scan of heads over ranks -> output
+// position, emit decoded keys in the reference Map's exact iteration order
+// (lib/kmers.js:76,95).
+// Tile-record path (non-ACGT prefix, or k in 33..64) and general path
+// (step > 1, k > 64, ...): windows become records merged on the host.
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>

@@ -7,17 +7,18 @@
 // key = substring(ini, ini+k) that startsWith(preffix) is counted (:88-100);
 // Map order = first occurrence (:95).
 //
-// Device pipeline (DESIGN.md §3):
-//   tile_kernel   one 16 KiB tile per workgroup, single pass over HBM:
-//                 stage tile + halos in LDS, count '\n' per thread, block
-//                 scan, decoupled look-back across tiles (line index and line
-//                 start of the tile), SWAR 4-byte scan for P and rc(P) at
-//                 every byte, exact verification of the rare candidates,
-//                 dense-table atomics (count + first-occurrence atomicMin)
-//                 for ACGT windows, records for everything else.
-//   windows_kernel general path (any k, any step, empty prefix): one
-//                 workgroup per sequence line, every window enumerated.
-//   dense_compact / dense_decode / gather_records: result materialisation.
+// Device pipeline (DESIGN.md §4):
+//   scan_planes_kernel / scan_tile_kernel  one 16 KiB tile per workgroup,
+//                 single pass over HBM: stage tile + halos in LDS, '\n'
+//                 counts and block scan, prefix test of every window on both
+//                 strands (bit-planes of 2-bit codes, or byte SWAR), exact
+//                 verification, one hit record per verified window.
+//   hit_kernel    global line index (after a scan of the tile sums), the
+//                 sequence-line rule, order key, rank slot of each hit.
+//   finish        cross-list placement, heads / emit after the key sort.
+//   dense-hit path: newline array, sequence lines, windows_packed_kernel.
+//   general path: lines_kernel (decoupled look-back) + windows_kernel ->
+//                 records for the host merge.
 //
 // Canonical identity used by the tile kernel: the
 // reverse-complement strand's window at j is rc of the forward window at
@@ -52,12 +53,6 @@ __device__ __forceinline__ uint32_t nl_flags(uint32_t x) {
     return ~(t + 0x7F7F7F7Fu) & 0x80808080u;
 }
 
-// 2-bit code, A=0 C=1 G=2 T=3; returns 4 for any other byte
-__device__ __forceinline__ uint32_t base_code(uint32_t b) {
-    uint32_t c = ((b >> 1) ^ (b >> 2)) & 3u;
-    uint32_t expect = (0x54474341u >> (8u * c)) & 0xFFu;  // "ACGT"[c]
-    return b == expect ? c : 4u;
-}
 
 __device__ __forceinline__ uint8_t comp_byte(uint8_t c) {
     return c == 'A' ? 'T' : c == 'T' ? 'A' : c == 'G' ? 'C' : c == 'C' ? 'G' : c;
@@ -184,16 +179,6 @@ __device__ __forceinline__ uint32_t lds_word(const uint8_t *buf, int p) {
     return align4(w[1], w[0], (uint32_t)(a & 3));
 }
 
-// position of the last '\n' inside thread thr's 64 bytes (-1 if none)
-__device__ __forceinline__ int last_newline_in_thread(const uint8_t *buf, int thr) {
-    const uint32_t *lw = (const uint32_t *)(buf + FH + 64 * thr);
-#pragma unroll 1
-    for (int i = 15; i >= 0; --i) {
-        const uint32_t z = nl_flags(lw[i]);
-        if (z) return 64 * thr + 4 * i + ((31 - __clz(z)) >> 3);
-    }
-    return -1;
-}
 
 // reverse complement of a 2-bit code of k bases (A=0 C=1 G=2 T=3)
 __device__ __forceinline__ uint64_t revcomp_code(uint64_t x, uint32_t k) {
