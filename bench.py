@@ -179,10 +179,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (never used by the driver): all ranks on one device, gloo instead of RCCL
+    if os.environ.get("KMERHIP_ONE_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("KMERHIP_DIST_BACKEND", "nccl")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -230,20 +237,37 @@ def main():
     ctr.set_position(plan["lines_before"], plan["byte_offset"])
     ctr.feed_device(buf.data_ptr(), nbytes)
     distinct, accepted = 0, 0
-    res = merge_to(ctr, args.k, len(prefix), total_lines, dst=0) if world > 1 else ctr.finish(want_result=True)
+    if world > 1:
+        merge_to(ctr, args.k, len(prefix), total_lines, dst=0, want_result=False)
+    else:
+        ctr.finish(want_result=False)
     if rank == 0:
-        distinct = len(res)
-        accepted = int(res.counts.sum())
-        assert res.lines == total_lines or args.config == "c1", (res.lines, total_lines)
+        # counted on the device (a C3-sized result has ~10^9 entries): ordered device
+        # entries + the host-side records (non-ACGT windows)
+        from kmerjs_amd.multi import device_u64
+        d_keys, d_cnt, d_first, n_dev = ctr.result_device()
+        dev_sum = int(device_u64(d_cnt, n_dev, dev).sum().item()) if n_dev else 0
+        kb, off, cnts, firsts = ctr.records_export()
+        distinct = n_dev + len(cnts)
+        accepted = dev_sum + int(cnts.sum())
+        if n_dev > 1:
+            f = device_u64(d_first, n_dev, dev)
+            assert bool((f[1:] > f[:-1]).all().item()), "first-occurrence order broken"
 
     if rank == 0:
         windows_step = wl["windows_total"]
         ms_per_step = elapsed / args.steps * 1e3
         value = windows_step * args.steps / elapsed
         kern_ms = sum(tile_ms) / len(tile_ms)
-        # algorithmic bytes per scan launch: the whole FASTQ batch is read
-        # once (B_in) + one 24-B hit record written per accepted window
-        algo_bytes = nbytes + 24 * (accepted / world)
+        if args.config == "c3" or (args.prefix and len(args.prefix) <= 3) or not args.prefix:
+            # dense-hit path: the timed kernels are the two streaming newline passes
+            kern_name = "nl_count_kernel + nl_write_kernel (dense-hit path)"
+            algo_bytes = 2 * nbytes
+        else:
+            # algorithmic bytes per scan launch: the whole FASTQ batch is
+            # read once (B_in) + one 24-B hit record written per accepted window
+            kern_name = "scan_planes_kernel"
+            algo_bytes = nbytes + 24 * (accepted / world)
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
         traffic = load_traffic(args)
         out = {
@@ -271,7 +295,8 @@ def main():
             "scan_kernel_ms": kern_ms,
             "feed_device_ms": sum(feed_ms_l) / len(feed_ms_l),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kern_name,
+                         "algorithmic_bytes_per_launch": algo_bytes, "kernel_ms": kern_ms},
         }
         if not args.no_pcie and world == 1:
             # PCIe-inclusive rate (host bytes -> H2D -> count -> ordered host result); never `value`

@@ -113,7 +113,10 @@ class Result:
             off = np.ctypeslib.as_array(offs, shape=(n + 1,)).copy()
             self.counts = np.ctypeslib.as_array(cnts, shape=(n,)).copy()
             self.firsts = np.ctypeslib.as_array(firsts, shape=(n,)).copy()
-            self.keybuf = ctypes.string_at(keys, int(off[-1]))
+            nbytes = int(off[-1])
+            # (ctypes.string_at takes a C int size: keys of > 2 GiB are copied through an array type)
+            self.keybuf = ctypes.string_at(keys, nbytes) if nbytes < (1 << 31) else \
+                (ctypes.c_char * nbytes).from_address(keys.value).raw
             self.offsets = off
         else:
             self.counts = np.zeros(0, dtype=np.uint64)

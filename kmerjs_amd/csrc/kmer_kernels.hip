@@ -35,6 +35,12 @@ __device__ __forceinline__ uint32_t align4(uint32_t hi, uint32_t lo, uint32_t se
     return __builtin_amdgcn_alignbyte(hi, lo, sel);
 }
 
+// Set a rarely-changing info bit: read first, so that thousands of tiles do
+// not serialise on one device-scope atomic (long contigs flag every tile).
+__device__ __forceinline__ void set_info(unsigned int *err, unsigned int bit) {
+    if (!(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(err, bit);
+}
+
 // Inclusive wave64 prefix sum with DPP (row_shr 1/2/4/8 inside rows of 16,
 // then row_bcast 15 / 31 across rows): no LDS round trips on the critical path.
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
@@ -712,12 +718,12 @@ __global__ __launch_bounds__(TPB) void scan_tile_kernel(ScanArgs a) {
         if (tid == 0) {
             a.tsum[tile].nh = sh.nh;
             a.tsum[tile].nx = sh.nh > (uint32_t)HMAX ? sh.nh : sh.nx;   // overflowed: all hits cross
-            if (sh.nh > (uint32_t)HMAX || (sh.nh && sh.tcnt == 0)) atomicOr(a.err, INFO_LONGSEG);
+            if (sh.nh > (uint32_t)HMAX || (sh.nh && sh.tcnt == 0)) set_info(a.err, INFO_LONGSEG);
         }
     } else if (tid == 0) {                       // wave 0 wrote them all (a word can hold 8 hits)
         a.tsum[tile].nh = sh.nh;
         a.tsum[tile].nx = sh.nh > (uint32_t)HMAX ? sh.nh : sh.nx;
-        if (sh.nh > (uint32_t)HMAX || (sh.nh && sh.tcnt == 0)) atomicOr(a.err, INFO_LONGSEG);
+        if (sh.nh > (uint32_t)HMAX || (sh.nh && sh.tcnt == 0)) set_info(a.err, INFO_LONGSEG);
     }
 }
 
@@ -957,12 +963,12 @@ __global__ __launch_bounds__(TPB) void scan_planes_kernel(ScanArgs a, PlaneArgs 
         if (tid == 0) {
             a.tsum[tile].nh = sh.nh;
             a.tsum[tile].nx = sh.nh > (uint32_t)HMAX ? sh.nh : sh.nx;
-            if (sh.nh > (uint32_t)HMAX || (sh.nh && sh.tcnt == 0)) atomicOr(a.err, INFO_LONGSEG);
+            if (sh.nh > (uint32_t)HMAX || (sh.nh && sh.tcnt == 0)) set_info(a.err, INFO_LONGSEG);
         }
     } else if (tid == 0) {
         a.tsum[tile].nh = sh.nh;
         a.tsum[tile].nx = sh.nh > (uint32_t)HMAX ? sh.nh : sh.nx;
-        if (sh.nh > (uint32_t)HMAX || (sh.nh && sh.tcnt == 0)) atomicOr(a.err, INFO_LONGSEG);
+        if (sh.nh > (uint32_t)HMAX || (sh.nh && sh.tcnt == 0)) set_info(a.err, INFO_LONGSEG);
     }
 }
 

@@ -74,7 +74,8 @@ def gather_partials(keys, vals, pad_key, dst=0, group=None):
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = keys.device
-    n = torch.tensor([keys.numel()], dtype=torch.int64, device=dev)
+    host_coll = dist.get_backend(group) == "gloo"
+    n = torch.tensor([keys.numel()], dtype=torch.int64, device="cpu" if host_coll else dev)
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n, group=group)
     maxn = max(int(x.item()) for x in sizes)
@@ -86,12 +87,16 @@ def gather_partials(keys, vals, pad_key, dst=0, group=None):
     vp[:, 1] = 0
     kp[:keys.numel()] = keys
     vp[:keys.numel()] = vals
+    staged = host_coll and kp.is_cuda     # gloo: gather host tensors
+    if staged:
+        kp, vp = kp.cpu(), vp.cpu()
     if rank == dst:
         kl = [torch.empty_like(kp) for _ in range(world)]
         vl = [torch.empty_like(vp) for _ in range(world)]
         dist.gather(kp, kl, dst=dst, group=group)
         dist.gather(vp, vl, dst=dst, group=group)
-        return torch.cat(kl), torch.cat(vl)
+        gk, gv = torch.cat(kl), torch.cat(vl)
+        return (gk.to(dev), gv.to(dev)) if staged else (gk, gv)
     dist.gather(kp, None, dst=dst, group=group)
     dist.gather(vp, None, dst=dst, group=group)
     return None, None
