@@ -31,9 +31,10 @@ for k, cs in vals.items():
     d = {c: sum(v) / len(v) for c, v in cs.items()}
     d["dispatches"] = max(len(v) for v in cs.values())
     summary[k] = d
-scan = summary.get("scan_tile_kernel", {})
+kname = "scan_planes_kernel" if "scan_planes_kernel" in summary else "scan_tile_kernel"
+scan = summary.get(kname, {})
 entry = {
-    "kernel": "scan_tile_kernel<true>",
+    "kernel": kname,
     "fetch_size_kib_raw": scan.get("FETCH_SIZE"),
     "write_size_kib": scan.get("WRITE_SIZE"),
 }
