@@ -54,6 +54,7 @@ enum {
     KMER_FLAG_TWO_PASS = 1u << 0,  /* debug: exact two-pass line scan instead of single-pass look-back */
     KMER_FLAG_NO_DENSE = 1u << 1,  /* debug: records instead of packed keys (host merge) */
     KMER_FLAG_BYTE_SCAN = 1u << 2, /* debug: byte-SWAR prefix scan instead of the bit-plane scan */
+    KMER_FLAG_SORT_FINISH = 1u << 3, /* debug: radix-sort finish instead of the bucket-table finish */
     /* experiments only (results are WRONG with these set): ablate parts of the tile scan */
     KMER_FLAG_ABLATE_HITS = 1u << 8,   /* drop every prefix candidate */
     KMER_FLAG_ABLATE_SWAR = 1u << 9    /* skip the SWAR prefix scan entirely */

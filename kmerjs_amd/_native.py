@@ -15,6 +15,7 @@ STATUS = {0: "ok", 1: "i/o error", 2: "bad parameter", 3: "out of memory", 4: "d
 FLAG_TWO_PASS = 1
 FLAG_NO_DENSE = 2
 FLAG_BYTE_SCAN = 4
+FLAG_SORT_FINISH = 8
 
 # every symbol the header declares (tests/test_abi.py checks header <-> library)
 EXPORTS = ["kmer_open", "kmer_close", "kmer_count_file", "kmer_count_buffer", "kmer_reset",

@@ -115,6 +115,8 @@ struct kmer_ctx {
     PlaneArgs pargs{};
     DBuf<uint32_t> ridx, ridx2, opos;
     DBuf<HeadRec> hrec;
+    DBuf<uint32_t> bH, bHs;        // bucket finish: per (bucket, block) counts, their scan
+    DBuf<uint16_t> pkey16;         // bucket finish: low key bits, partitioned
     bool long_seg = false;         // INFO_LONGSEG seen this session
     bool chunk_open = false;       // the last chunk did not end with '\n'
     bool out_pending = false;      // unique count of the last finish not yet read back (h_small[13])
@@ -779,6 +781,27 @@ kmer_status sort_and_heads(kmer_ctx *c, K *keys, K *keys2, uint64_t n, bool with
     return KMER_OK;
 }
 
+// bucket partition + per-bucket LDS tables (keys of <= 24 bits)
+kmer_status bucket_heads(kmer_ctx *c, uint64_t n) {
+    hipStream_t s = c->stream;
+    const uint32_t shift = std::min<uint32_t>(c->kbits, BKT_LOW);
+    const uint32_t nb = 1u << (c->kbits - shift);
+    const uint64_t nblk64 = (n + BKT_EPB_HOST - 1) / BKT_EPB_HOST;
+    if (nblk64 > 0x7FFFFFFFull) return fail(c, KMER_E_BAD_PARAM, "too many hits");
+    const uint32_t nblk = (uint32_t)nblk64;
+    const uint32_t invalid = 1u << c->kbits;
+    HIPCHK(c, c->bH.ensure((uint64_t)nb * nblk, s));
+    HIPCHK(c, c->bHs.ensure((uint64_t)nb * nblk, s));
+    HIPCHK(c, c->pkey16.ensure(n, s));
+    HIPCHK(c, c->ridx2.ensure(n, s));
+    HIPCHK(c, hipMemsetAsync(c->hrec.p, 0, n * sizeof(HeadRec), s));
+    HIPCHK(c, launch_bucket_hist(c->rkey32.p, n, invalid, shift, nb, nblk, c->bH.p, s));
+    ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->bH.p, c->bHs.p, 0u, (size_t)nb * nblk, rocprim::plus<uint32_t>(), s));
+    HIPCHK(c, launch_bucket_scatter(c->rkey32.p, n, invalid, shift, nb, nblk, c->bHs.p, c->pkey16.p, c->ridx2.p, s));
+    HIPCHK(c, launch_bucket_heads(c->pkey16.p, c->ridx2.p, c->bHs.p, c->bH.p, nb, nblk, shift, c->hrec.p, s));
+    return KMER_OK;
+}
+
 // resolve a deferred unique count (finish without a host result)
 kmer_status resolve_out(kmer_ctx *c) {
     if (c->out_pending) {
@@ -820,8 +843,14 @@ kmer_status rank_finish(kmer_ctx *c, uint64_t n, bool partial, bool with_counts,
         HIPCHK(c, c->first.ensure(n, s));
     }
     const uint64_t invalid = c->kbits >= 63 ? ~0ull : (1ull << c->kbits);
-    kmer_status st = c->narrow ? sort_and_heads<uint32_t>(c, c->rkey32.p, c->rkey32b.p, n, with_counts)
-                               : sort_and_heads<uint64_t>(c, c->rkey.p, c->rkey2.p, n, with_counts);
+    kmer_status st;
+    // (merged partials carry counts: the sort finish sums them in 64 bits)
+    if (c->narrow && c->kbits <= BKT_LOW + 11 && !with_counts && !(c->p.flags & KMER_FLAG_SORT_FINISH))
+        st = bucket_heads(c, n);
+    else if (c->narrow)
+        st = sort_and_heads<uint32_t>(c, c->rkey32.p, c->rkey32b.p, n, with_counts);
+    else
+        st = sort_and_heads<uint64_t>(c, c->rkey.p, c->rkey2.p, n, with_counts);
     if (st) return st;
     auto is_head = rocprim::make_transform_iterator(c->hrec.p, IsHead());
     ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, is_head, c->opos.p, 0u, (size_t)n, rocprim::plus<uint32_t>(), s));
@@ -1092,7 +1121,8 @@ kmer_status kmer_close(kmer_ctx *c) {
     for (auto *b : {&c->tbase, &c->nlpos, &c->wcount, &c->wbase, &c->tp_cnt, &c->tp_lnl, &c->rkey, &c->rkey2, &c->rord, &c->rcnt, &c->xord, &c->xord2,
                     &c->xkey, &c->xkey2, &c->ukey, &c->first, &c->cnt_out, &c->roff})
         b->release();
-    for (auto *b : {&c->ridx, &c->ridx2, &c->opos, &c->xslot, &c->rkey32, &c->rkey32b}) b->release();
+    for (auto *b : {&c->ridx, &c->ridx2, &c->opos, &c->xslot, &c->rkey32, &c->rkey32b, &c->bH, &c->bHs}) b->release();
+    c->pkey16.release();
     c->bsum.release();
     c->bscan.release();
     c->hrec.release();

@@ -280,6 +280,16 @@ hipError_t launch_heads(const uint64_t *skey, const uint32_t *srank, uint64_t n,
 hipError_t launch_heads32(const uint32_t *skey, const uint32_t *srank, uint64_t n, uint32_t invalid_key,
                           const uint64_t *rcnt, HeadRec *hrec, hipStream_t s);
 hipError_t launch_emit(const EmitArgs &a, hipStream_t s);
+// bucket finish (u32 keys of <= BKT_LOW + 11 bits)
+constexpr uint32_t BKT_LOW = 14;             // keys per bucket table: 2^14 (128 KiB of LDS: min rank, count)
+constexpr uint32_t BKT_MAX = 2048;           // buckets (keys of <= BKT_LOW + 11 bits)
+constexpr uint32_t BKT_EPB_HOST = 4096;      // elements per partition block (= BKT_EPB)
+hipError_t launch_bucket_hist(const uint32_t *key, uint64_t n, uint32_t invalid, uint32_t shift, uint32_t nb,
+                              uint32_t nblk, uint32_t *H, hipStream_t s);
+hipError_t launch_bucket_scatter(const uint32_t *key, uint64_t n, uint32_t invalid, uint32_t shift, uint32_t nb,
+                                 uint32_t nblk, const uint32_t *Hs, uint16_t *pkey, uint32_t *prank, hipStream_t s);
+hipError_t launch_bucket_heads(const uint16_t *pkey, const uint32_t *prank, const uint32_t *Hs, const uint32_t *H,
+                               uint32_t nb, uint32_t nblk, uint32_t shift, HeadRec *hrec, hipStream_t s);
 hipError_t launch_merge_prep(const uint64_t *keys, const Agg *vals, uint64_t n, uint64_t *rkey, uint32_t *rkey32,
                              uint64_t *rord, uint64_t *rcnt, uint32_t *ridx, hipStream_t s);
 hipError_t launch_gather_records(const Record *recs, const uint64_t *key_off, uint64_t n,

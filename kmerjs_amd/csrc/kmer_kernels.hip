@@ -1698,6 +1698,124 @@ __global__ __launch_bounds__(256) void heads_kernel(const K *skey, const uint32_
     }
 }
 
+// ---------------------------------------------------------------------------
+// Bucket finish (u32 keys of <= 24 bits): instead of sorting, partition the
+// ranked hits by key >> BKT_LOW into <= 2048 buckets (LDS-privatised
+// histogram, scan, scatter), then one workgroup per bucket keeps an LDS table
+// of 2^BKT_LOW keys: min rank (= first occurrence) and count, and writes the
+// head record of every key present at its first-occurrence rank.
+// ---------------------------------------------------------------------------
+constexpr uint32_t BKT_EPB = 4096;           // elements per partition block
+
+__global__ __launch_bounds__(256) void bucket_hist_kernel(const uint32_t *key, uint64_t n, uint32_t invalid,
+                                                          uint32_t shift, uint32_t nb, uint32_t nblk,
+                                                          uint32_t *H) {
+    __shared__ uint32_t hist[BKT_MAX];
+    for (uint32_t b = threadIdx.x; b < nb; b += 256) hist[b] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * BKT_EPB;
+#pragma unroll 4
+    for (uint32_t j = threadIdx.x; j < BKT_EPB; j += 256) {
+        const uint64_t i = base + j;
+        if (i < n) {
+            const uint32_t k = key[i];
+            if (k != invalid) atomicAdd(&hist[k >> shift], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += 256) H[(uint64_t)b * nblk + blockIdx.x] = hist[b];
+}
+
+// Scatter with the block's elements first grouped by bucket in LDS, so that
+// each bucket's run goes out as one contiguous (coalesced) piece.
+__global__ __launch_bounds__(256) void bucket_scatter_kernel(const uint32_t *key, uint64_t n, uint32_t invalid,
+                                                             uint32_t shift, uint32_t nb, uint32_t nblk,
+                                                             const uint32_t *Hs, uint16_t *pkey, uint32_t *prank) {
+    __shared__ uint32_t cnt[BKT_MAX];          // per bucket: count, then local start
+    __shared__ uint32_t skey[BKT_EPB];
+    __shared__ uint32_t srank[BKT_EPB];
+    __shared__ uint32_t wtot[4];
+    for (uint32_t b = threadIdx.x; b < nb; b += 256) cnt[b] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * BKT_EPB;
+    uint32_t kk[BKT_EPB / 256], li[BKT_EPB / 256];
+#pragma unroll
+    for (uint32_t u = 0; u < BKT_EPB / 256; ++u) {
+        const uint64_t i = base + u * 256 + threadIdx.x;
+        kk[u] = i < n ? key[i] : invalid;
+        li[u] = kk[u] != invalid ? atomicAdd(&cnt[kk[u] >> shift], 1u) : 0u;
+    }
+    __syncthreads();
+    // exclusive scan of the bucket counts (nb <= BKT_MAX, <= 8 per thread)
+    uint32_t loc[BKT_MAX / 256], sum = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < BKT_MAX / 256; ++u) {
+        const uint32_t b = threadIdx.x * (BKT_MAX / 256) + u;
+        loc[u] = b < nb ? cnt[b] : 0u;
+        sum += loc[u];
+    }
+    const uint32_t incl = wave_incl_sum(sum);
+    if ((threadIdx.x & 63) == 63) wtot[threadIdx.x >> 6] = incl;
+    __syncthreads();
+    uint32_t pre = incl - sum;
+    for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) pre += wtot[w];
+#pragma unroll
+    for (uint32_t u = 0; u < BKT_MAX / 256; ++u) {
+        const uint32_t b = threadIdx.x * (BKT_MAX / 256) + u;
+        if (b < nb) cnt[b] = pre;
+        pre += loc[u];
+    }
+    const uint32_t valid = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+    __syncthreads();
+#pragma unroll
+    for (uint32_t u = 0; u < BKT_EPB / 256; ++u) {
+        if (kk[u] != invalid) {
+            const uint32_t p = cnt[kk[u] >> shift] + li[u];
+            skey[p] = kk[u];
+            srank[p] = (uint32_t)(base + u * 256 + threadIdx.x);
+        }
+    }
+    __syncthreads();
+    const uint32_t lo_mask = (1u << shift) - 1u;
+    for (uint32_t e = threadIdx.x; e < valid; e += 256) {
+        const uint32_t k = skey[e], b = k >> shift;
+        const uint32_t pos = Hs[(uint64_t)b * nblk + blockIdx.x] + (e - cnt[b]);
+        pkey[pos] = (uint16_t)(k & lo_mask);
+        prank[pos] = srank[e];
+    }
+}
+
+__global__ __launch_bounds__(1024) void bucket_heads_kernel(const uint16_t *pkey, const uint32_t *prank,
+                                                            const uint32_t *Hs, const uint32_t *H, uint32_t nb,
+                                                            uint32_t nblk, uint32_t shift, HeadRec *hrec) {
+    __shared__ uint32_t minr[1u << BKT_LOW];
+    __shared__ uint32_t cnt[1u << BKT_LOW];
+    const uint32_t b = blockIdx.x, nk = 1u << shift;
+    for (uint32_t j = threadIdx.x; j < nk; j += blockDim.x) {
+        minr[j] = 0xFFFFFFFFu;
+        cnt[j] = 0;
+    }
+    __syncthreads();
+    const uint64_t last = (uint64_t)nb * nblk - 1;
+    const uint32_t lo = Hs[(uint64_t)b * nblk];
+    const uint32_t hi = b + 1 < nb ? Hs[(uint64_t)(b + 1) * nblk] : Hs[last] + H[last];
+    for (uint32_t e = lo + threadIdx.x; e < hi; e += blockDim.x) {
+        const uint32_t j = pkey[e], r = prank[e];
+        atomicMin(&minr[j], r);
+        atomicAdd(&cnt[j], 1u);
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < nk; j += blockDim.x) {
+        const uint32_t c = cnt[j];
+        if (c) {
+            HeadRec v;
+            v.key = ((uint64_t)b << shift) | j;
+            v.count = c;
+            hrec[minr[j]] = v;
+        }
+    }
+}
+
 // One thread per rank; flagged ranks emit output entry opos[rank]: decoded key
 // (P + suffix, 'ACGT' from the 2-bit code, first base most significant),
 // count, first-occurrence order -- or the packed (code, {first, count}) pair
@@ -1922,6 +2040,22 @@ hipError_t launch_heads32(const uint32_t *skey, const uint32_t *srank, uint64_t 
     if (n)
         hipLaunchKernelGGL(heads_kernel<uint32_t>, dim3(grid_for(n)), dim3(256), 0, s, skey, srank, n, invalid_key, rcnt,
                            hrec);
+    return hipGetLastError();
+}
+hipError_t launch_bucket_hist(const uint32_t *key, uint64_t n, uint32_t invalid, uint32_t shift, uint32_t nb,
+                              uint32_t nblk, uint32_t *H, hipStream_t s) {
+    hipLaunchKernelGGL(bucket_hist_kernel, dim3(nblk), dim3(256), 0, s, key, n, invalid, shift, nb, nblk, H);
+    return hipGetLastError();
+}
+hipError_t launch_bucket_scatter(const uint32_t *key, uint64_t n, uint32_t invalid, uint32_t shift, uint32_t nb,
+                                 uint32_t nblk, const uint32_t *Hs, uint16_t *pkey, uint32_t *prank, hipStream_t s) {
+    hipLaunchKernelGGL(bucket_scatter_kernel, dim3(nblk), dim3(256), 0, s, key, n, invalid, shift, nb, nblk, Hs, pkey,
+                       prank);
+    return hipGetLastError();
+}
+hipError_t launch_bucket_heads(const uint16_t *pkey, const uint32_t *prank, const uint32_t *Hs, const uint32_t *H,
+                               uint32_t nb, uint32_t nblk, uint32_t shift, HeadRec *hrec, hipStream_t s) {
+    hipLaunchKernelGGL(bucket_heads_kernel, dim3(nb), dim3(1024), 0, s, pkey, prank, Hs, H, nb, nblk, shift, hrec);
     return hipGetLastError();
 }
 hipError_t launch_emit(const EmitArgs &a, hipStream_t s) {

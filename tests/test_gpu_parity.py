@@ -61,6 +61,13 @@ def test_byte_scan_kernel_matches(native, golden, inputs):
     assert not bad, bad[:5]
 
 
+def test_sort_finish_matches(native, golden, inputs):
+    # the radix-sort finish (used for keys wider than 24 bits) on narrow keys too
+    bad = _run_cases(native, golden, inputs, flags=native.FLAG_SORT_FINISH,
+                     select=lambda c: c["step"] == 1 and c["k"] <= 16)
+    assert not bad, bad[:5]
+
+
 def test_chunks_must_end_at_line_ends(native):
     import torch
     data = b"@r\nACGTATGACGGGTTTACGATGACA\n+\nIIIIIIIIIIIIIIIIIIIIIIII\n"
