@@ -156,6 +156,9 @@ def main():
     ap.add_argument("--config", default="c2", choices=("c1", "c2", "c3", "c5"),
                     help="BASELINE.json config: c2 (default, the headline), c3 no-prefix k=31, c5 long contigs k=21")
     ap.add_argument("--contig-bytes", type=int, default=1_000_000_000, help="c5: bytes of contigs per GPU")
+    ap.add_argument("--merge", default="alltoall", choices=("alltoall", "gather"),
+                    help="N > 1: key-range all-to-all + per-rank finish (result distributed by key range), "
+                         "or gather of all partials + finish on rank 0")
     args = ap.parse_args()
     # per-config defaults (explicit flags still win)
     argv = " ".join(sys.argv)
@@ -174,7 +177,7 @@ def main():
     import torch
     import torch.distributed as dist
     from kmerjs_amd import Counter
-    from kmerjs_amd.multi import merge_to
+    from kmerjs_amd.multi import device_u64, finish_distributed, merge_to
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -210,10 +213,15 @@ def main():
         if record:
             tile_ms.append(scan_ms)
             feed_ms_l.append(feed_ms)
-        if world > 1:
-            merge_to(ctr, args.k, len(prefix), total_lines, dst=0, want_result=False)
-        else:
+        multi_finish()
+
+    def multi_finish():
+        if world == 1:
             ctr.finish(want_result=False)
+        elif args.merge == "alltoall":
+            finish_distributed(ctr, args.k, len(prefix), total_lines)
+        else:
+            merge_to(ctr, args.k, len(prefix), total_lines, dst=0, want_result=False)
 
     for _ in range(args.warmup):
         step(False)
@@ -237,22 +245,34 @@ def main():
     ctr.set_position(plan["lines_before"], plan["byte_offset"])
     ctr.feed_device(buf.data_ptr(), nbytes)
     distinct, accepted = 0, 0
-    if world > 1:
-        merge_to(ctr, args.k, len(prefix), total_lines, dst=0, want_result=False)
-    else:
-        ctr.finish(want_result=False)
+    multi_finish()
+    # counted on the device (a C3-sized result has ~10^9 entries): ordered device
+    # entries (every rank's key range after the all-to-all, or all on rank 0) +
+    # the host-side records (non-ACGT windows, on rank 0)
+    d_keys, d_cnt, d_first, n_dev = ctr.result_device() if (rank == 0 or args.merge == "alltoall") else (0, 0, 0, 0)
+    dev_sum = int(device_u64(d_cnt, n_dev, dev).sum().item()) if n_dev else 0
+    if n_dev > 1:
+        f = device_u64(d_first, n_dev, dev)
+        assert bool((f[1:] > f[:-1]).all().item()), "first-occurrence order broken"
+    n_rec, rec_sum = 0, 0
     if rank == 0:
-        # counted on the device (a C3-sized result has ~10^9 entries): ordered device
-        # entries + the host-side records (non-ACGT windows)
-        from kmerjs_amd.multi import device_u64
-        d_keys, d_cnt, d_first, n_dev = ctr.result_device()
-        dev_sum = int(device_u64(d_cnt, n_dev, dev).sum().item()) if n_dev else 0
         kb, off, cnts, firsts = ctr.records_export()
-        distinct = n_dev + len(cnts)
-        accepted = dev_sum + int(cnts.sum())
-        if n_dev > 1:
-            f = device_u64(d_first, n_dev, dev)
-            assert bool((f[1:] > f[:-1]).all().item()), "first-occurrence order broken"
+        n_rec, rec_sum = len(cnts), int(cnts.sum())
+    tot = torch.tensor([n_dev + n_rec, dev_sum + rec_sum], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(tot)
+    distinct, accepted = int(tot[0].item()), int(tot[1].item())
+    if os.environ.get("KMERHIP_BENCH_VERIFY") == "1" and args.config in ("c2", "c3") and world > 1:
+        # rehearsal check (never set by the driver): the distributed result, merged
+        # by first occurrence, equals the oracle on the whole job's input
+        from kmerjs_amd.multi import collect_ordered
+        assert args.merge == "alltoall"
+        got = collect_ordered(ctr, args.k)
+        if rank == 0:
+            from oracle import oracle
+            want = oracle.count_buffer(oracle.synth_fastq(args.seed, 0, world * args.reads), prefix, args.k, 1)
+            assert got == want, "distributed result differs from the oracle"
+            print("verify: %d entries equal the oracle" % len(want), file=sys.stderr)
 
     if rank == 0:
         windows_step = wl["windows_total"]
@@ -288,7 +308,9 @@ def main():
             "config": {"workload": wl["desc"], "name": args.config,
                        "reads_per_gpu": args.reads if args.config in ("c2", "c3") else None,
                        "k": args.k, "prefix": args.prefix, "windows_per_step": windows_step,
-                       "bytes_per_gpu": nbytes, "parallelism": "dp%d (reads sharded, RCCL gather of partials)" % world},
+                       "bytes_per_gpu": nbytes, "parallelism": "dp%d (reads sharded; %s)" % (
+                           world, "RCCL all-to-all of partials by key range, per-rank finish" if args.merge == "alltoall"
+                           else "RCCL gather of partials, finish on rank 0")},
             "distinct_kmers_per_s": distinct * args.steps / elapsed,
             "distinct_kmers": distinct,
             "accepted_windows": accepted,

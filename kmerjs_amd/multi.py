@@ -3,12 +3,22 @@
 Reads are independent units (lib/kmers.js:151-155), so an input is split into
 per-rank shards at record boundaries; each rank counts its shard with the
 global line index / byte offset of its first line (kmer_set_position), which
-makes first-occurrence order keys comparable across ranks.  The only exchange
-is one gather of the per-rank partial results to rank 0 (RCCL over xGMI):
-unique packed keys + {first, count} pairs, padded to the largest rank with the
-invalid key (which the merged reduce drops), followed by one reduce/order/
-decode on rank 0 (kmer_finish_merged).  Record (non-ACGT) keys
-are merged on the host with a small object gather.
+makes first-occurrence order keys comparable across ranks.  Each rank reduces
+its shard to a partial result (unique packed keys + {first, count}, in
+first-occurrence order).  Two ways to finish:
+
+* finish_distributed: ONE all-to-all (RCCL over xGMI) by key range -- rank r
+  receives every rank's entries of its key range; the concatenation by source
+  rank is already in first-occurrence order (shards are in line order), so a
+  merged finish (kmer_finish_merged) on each rank yields that rank's key range
+  of the result, ordered by first occurrence.  The global Map order is the
+  merge of the ranks' lists by first occurrence (collect_ordered).  Work per
+  rank stays constant as ranks are added.
+* merge_to: gather every partial to one rank and finish there (one ordered
+  result on one GPU; the gather and the merge grow with the rank count).
+
+Record (non-ACGT) keys are merged on the host of one rank with a small object
+gather.
 """
 import torch
 import torch.distributed as dist
@@ -106,6 +116,12 @@ def gather_records(ctr, dst=0, group=None):
     """Move every rank's host record keys (non-ACGT windows) into rank dst's context."""
     rank = dist.get_rank(group)
     mine = ctr.records_export()
+    # skip the object gather when no rank has records (the common case)
+    dev = "cpu" if dist.get_backend(group) == "gloo" else torch.device("cuda", torch.cuda.current_device())
+    tot = torch.tensor([len(mine[2])], dtype=torch.int64, device=dev)
+    dist.all_reduce(tot, group=group)
+    if int(tot.item()) == 0:
+        return
     payload = (mine[0], mine[1].tolist(), mine[2].tolist(), mine[3].tolist())
     got = [None] * dist.get_world_size(group) if rank == dst else None
     dist.gather_object(payload, got, dst=dst, group=group)
@@ -115,6 +131,84 @@ def gather_records(ctr, dst=0, group=None):
             if r != dst and cnt:
                 ctr.records_import(kb, np.array(off, dtype=np.uint64), np.array(cnt, dtype=np.uint64),
                                    np.array(fst, dtype=np.uint64))
+
+
+def key_owner(keys, kbits, world):
+    """Owning rank of each packed key: equal slices of the key space."""
+    s = max(0, kbits - 40)
+    return (((keys >> s) * world) >> (kbits - s)).clamp_(0, world - 1)
+
+
+def shuffle_partials(keys, vals, kbits, group=None):
+    """All-to-all of partial entries by key range.
+
+    keys int64[n] (packed keys), vals int64[n, 2] ({first, count}), in
+    first-occurrence order.  Returns this rank's key range from every rank,
+    concatenated by source rank -- i.e. still in first-occurrence order."""
+    world = dist.get_world_size(group)
+    dev = keys.device
+    host_coll = dist.get_backend(group) == "gloo"
+    owner = key_owner(keys, kbits, world)
+    order = torch.sort(owner, stable=True).indices       # stable: first order kept per destination
+    ks, vs = keys[order], vals[order]
+    send = torch.bincount(owner, minlength=world).to(torch.int64)
+    recv = torch.empty_like(send)
+    if host_coll:
+        send, recv, ks, vs = send.cpu(), recv.cpu(), ks.cpu(), vs.cpu()
+    dist.all_to_all_single(recv, send, group=group)
+    send_l, recv_l = send.tolist(), recv.tolist()
+    rk = torch.empty(sum(recv_l), dtype=torch.int64, device=ks.device)
+    rv = torch.empty((sum(recv_l), 2), dtype=torch.int64, device=ks.device)
+    dist.all_to_all_single(rk, ks, recv_l, send_l, group=group)
+    dist.all_to_all_single(rv.view(-1), vs.reshape(-1), [2 * x for x in recv_l], [2 * x for x in send_l], group=group)
+    if host_coll:
+        rk, rv = rk.to(dev), rv.to(dev)
+    return rk, rv
+
+
+def finish_distributed(ctr, k, plen, total_lines, group=None, want_result=False, records=True, dst=0):
+    """Finish a sharded count with the key-range all-to-all: afterwards every
+    rank holds its key range of the result, ordered by first occurrence
+    (device, kmer_result_device).  Record keys are merged on rank `dst`."""
+    d_k, d_v, n = ctr.partial_device()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    keys = device_u64(d_k, n, dev) if n else torch.empty(0, dtype=torch.int64, device=dev)
+    vals = device_u64(d_v, 2 * n, dev).view(n, 2) if n else torch.empty((0, 2), dtype=torch.int64, device=dev)
+    rk, rv = shuffle_partials(keys, vals, 2 * (k - plen), group=group)
+    if records:
+        gather_records(ctr, dst=dst, group=group)
+    torch.cuda.synchronize()
+    return ctr.finish_merged(rk.data_ptr(), rv.data_ptr(), rk.numel(), total_lines, want_result=want_result)
+
+
+def collect_ordered(ctr, k, dst=0, group=None):
+    """Gather every rank's ordered key range (after finish_distributed) to `dst`
+    and merge the lists by first occurrence: the whole Map, in reference order.
+    Returns [(key bytes, count)] on dst (device entries + dst's records), None elsewhere."""
+    import numpy as np
+    d_keys, d_cnt, d_first, n = ctr.result_device()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    if n:
+        kb = torch.as_tensor(_CudaArray(d_keys, n * k, "|u1"), device=dev).cpu().numpy().tobytes()
+        cnt = device_u64(d_cnt, n, dev).cpu().numpy().astype(np.uint64)
+        fst = device_u64(d_first, n, dev).cpu().numpy().astype(np.uint64)
+    else:
+        kb, cnt, fst = b"", np.zeros(0, np.uint64), np.zeros(0, np.uint64)
+    got = [None] * dist.get_world_size(group) if dist.get_rank(group) == dst else None
+    dist.gather_object((kb, cnt.tolist(), fst.tolist()), got, dst=dst, group=group)
+    if dist.get_rank(group) != dst:
+        return None
+    keys, counts, firsts = [], [], []
+    for kb_r, cnt_r, fst_r in got:
+        keys += [kb_r[i * k:(i + 1) * k] for i in range(len(cnt_r))]
+        counts += cnt_r
+        firsts += fst_r
+    rk, ro, rc, rf = ctr.records_export()
+    keys += [rk[int(ro[i]):int(ro[i + 1])] for i in range(len(rc))]
+    counts += [int(x) for x in rc]
+    firsts += [int(x) for x in rf]
+    order = sorted(range(len(keys)), key=lambda i: firsts[i])
+    return [(keys[i], counts[i]) for i in order]
 
 
 def merge_to(ctr, k, plen, total_lines, dst=0, group=None, want_result=True, records=True):

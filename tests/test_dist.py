@@ -109,3 +109,59 @@ def test_shard_plan_positions():
 def test_invalid_key_is_past_every_suffix():
     assert multi.invalid_key(16, 5) == 1 << 22
     assert multi.invalid_key(5, 5) == 1
+
+
+def _shuffle_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        kbits = 22
+        g = torch.Generator().manual_seed(rank)
+        n = 1000 + 137 * rank
+        keys = torch.randint(0, 1 << kbits, (n,), generator=g, dtype=torch.int64)
+        # first-occurrence orders of this rank's shard: increasing, above every earlier rank's
+        first = torch.arange(n, dtype=torch.int64) + (rank << 40)
+        vals = torch.stack([first, torch.full((n,), rank + 1, dtype=torch.int64)], dim=1)
+        rk, rv = multi.shuffle_partials(keys, vals, kbits)
+        q.put(("ok", rank, keys.tolist(), rk.tolist(), rv.tolist()))
+    except Exception as e:  # pragma: no cover
+        q.put(("err", rank, repr(e), None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_shuffle_partials_by_key_range_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shuffle_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[0] == "ok" for r in res), res
+    by_rank = {r[1]: r for r in res}
+    sent = sorted(k for r in res for k in r[2])
+    got = []
+    for rank in range(world):
+        _, _, _, rk, rv = by_rank[rank]
+        owners = multi.key_owner(torch.tensor(rk, dtype=torch.int64), 22, world).tolist() if rk else []
+        assert all(o == rank for o in owners)                 # only this rank's key range
+        firsts = [v[0] for v in rv]
+        assert firsts == sorted(firsts)                        # still in first-occurrence order
+        got += rk
+    assert sorted(got) == sent                                 # nothing lost, nothing duplicated
+
+
+def test_key_owner_balanced_and_monotone():
+    keys = torch.arange(0, 1 << 22, 97, dtype=torch.int64)
+    for world in (1, 2, 3, 8):
+        own = multi.key_owner(keys, 22, world)
+        assert int(own.min()) == 0 and int(own.max()) == world - 1
+        assert bool((own[1:] >= own[:-1]).all())
+    big = torch.tensor([(1 << 62) - 1, 0], dtype=torch.int64)
+    assert multi.key_owner(big, 62, 8).tolist() == [7, 0]
