@@ -178,6 +178,9 @@ def finish_distributed(ctr, k, plen, total_lines, group=None, want_result=False,
     if records:
         gather_records(ctr, dst=dst, group=group)
     torch.cuda.synchronize()
+    # the merged finish runs on the context's own stream and may still read the
+    # received buffers after returning: keep them alive until the next finish
+    ctr._keepalive = (rk, rv)
     return ctr.finish_merged(rk.data_ptr(), rv.data_ptr(), rk.numel(), total_lines, want_result=want_result)
 
 
@@ -228,4 +231,5 @@ def merge_to(ctr, k, plen, total_lines, dst=0, group=None, want_result=True, rec
     if dist.get_rank(group) != dst:
         return None
     torch.cuda.synchronize()
+    ctr._keepalive = (gk, gv)                     # (see finish_distributed)
     return ctr.finish_merged(gk.data_ptr(), gv.data_ptr(), gk.numel(), total_lines, want_result=want_result)
