@@ -156,9 +156,9 @@ def main():
     ap.add_argument("--config", default="c2", choices=("c1", "c2", "c3", "c5"),
                     help="BASELINE.json config: c2 (default, the headline), c3 no-prefix k=31, c5 long contigs k=21")
     ap.add_argument("--contig-bytes", type=int, default=1_000_000_000, help="c5: bytes of contigs per GPU")
-    ap.add_argument("--merge", default="alltoall", choices=("alltoall", "gather"),
-                    help="N > 1: key-range all-to-all + per-rank finish (result distributed by key range), "
-                         "or gather of all partials + finish on rank 0")
+    ap.add_argument("--merge", default="hits", choices=("hits", "alltoall", "gather"),
+                    help="N > 1: hits: key-range all-to-all of the hits + per-rank finish (result distributed by "
+                         "key range); alltoall: the same with per-rank partials; gather: all partials to rank 0")
     args = ap.parse_args()
     # per-config defaults (explicit flags still win)
     argv = " ".join(sys.argv)
@@ -177,7 +177,7 @@ def main():
     import torch
     import torch.distributed as dist
     from kmerjs_amd import Counter
-    from kmerjs_amd.multi import device_u64, finish_distributed, merge_to
+    from kmerjs_amd.multi import device_u64, finish_distributed, finish_exchange, merge_to
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -218,6 +218,8 @@ def main():
     def multi_finish():
         if world == 1:
             ctr.finish(want_result=False)
+        elif args.merge == "hits":
+            finish_exchange(ctr, args.k, len(prefix), total_lines)
         elif args.merge == "alltoall":
             finish_distributed(ctr, args.k, len(prefix), total_lines)
         else:
@@ -249,7 +251,7 @@ def main():
     # counted on the device (a C3-sized result has ~10^9 entries): ordered device
     # entries (every rank's key range after the all-to-all, or all on rank 0) +
     # the host-side records (non-ACGT windows, on rank 0)
-    d_keys, d_cnt, d_first, n_dev = ctr.result_device() if (rank == 0 or args.merge == "alltoall") else (0, 0, 0, 0)
+    d_keys, d_cnt, d_first, n_dev = ctr.result_device() if (rank == 0 or args.merge != "gather") else (0, 0, 0, 0)
     dev_sum = int(device_u64(d_cnt, n_dev, dev).sum().item()) if n_dev else 0
     if n_dev > 1:
         f = device_u64(d_first, n_dev, dev)
@@ -266,7 +268,7 @@ def main():
         # rehearsal check (never set by the driver): the distributed result, merged
         # by first occurrence, equals the oracle on the whole job's input
         from kmerjs_amd.multi import collect_ordered
-        assert args.merge == "alltoall"
+        assert args.merge != "gather"
         got = collect_ordered(ctr, args.k)
         if rank == 0:
             from oracle import oracle
@@ -309,8 +311,9 @@ def main():
                        "reads_per_gpu": args.reads if args.config in ("c2", "c3") else None,
                        "k": args.k, "prefix": args.prefix, "windows_per_step": windows_step,
                        "bytes_per_gpu": nbytes, "parallelism": "dp%d (reads sharded; %s)" % (
-                           world, "RCCL all-to-all of partials by key range, per-rank finish" if args.merge == "alltoall"
-                           else "RCCL gather of partials, finish on rank 0")},
+                           world, {"hits": "RCCL all-to-all of hits by key range, per-rank finish",
+                        "alltoall": "RCCL all-to-all of partials by key range, per-rank finish"}.get(
+                            args.merge, "RCCL gather of partials, finish on rank 0"))},
             "distinct_kmers_per_s": distinct * args.steps / elapsed,
             "distinct_kmers": distinct,
             "accepted_windows": accepted,

@@ -105,9 +105,28 @@ kmer_status kmer_finish_device(kmer_ctx *ctx, kmer_result **out);
 kmer_status kmer_partial_device(kmer_ctx *ctx, const void **d_keys, const void **d_vals, uint64_t *n);
 kmer_status kmer_finish_merged(kmer_ctx *ctx, const void *d_keys, const void *d_vals, uint64_t n,
                                uint64_t total_lines, kmer_result **out);
+/* Multi-GPU hit exchange (the default multi-GPU finish).  After the feeds,
+ * kmer_exchange_prepare partitions this session's counting hits by owning
+ * rank -- equal slices of the packed-key space over `world` ranks (world <=
+ * 256) -- into d_send: per owner a contiguous run of 16-byte records {uint64
+ * first-occurrence order key, uint64 packed key}, runs in owner order, each
+ * run in first-occurrence order; counts[o] (host array of `world`) = records
+ * for owner o.  d_send is valid until the next call on the context.  Exchange
+ * the runs (all-to-all over xGMI) and hand each rank's received records,
+ * concatenated in source-rank order, to kmer_finish_exchanged, which counts
+ * them (this rank's key range of the result, in first-occurrence order,
+ * device-resident: kmer_result_device).  `wait_stream` (hipStream_t or NULL):
+ * the context's stream waits for the work queued so far on that stream (the
+ * collective that wrote d_recv) before reading it.  Shards must be fed in
+ * line order (kmer_set_position) so that order keys are global. */
+kmer_status kmer_exchange_prepare(kmer_ctx *ctx, uint32_t world, const void **d_send, uint64_t *counts);
+kmer_status kmer_finish_exchanged(kmer_ctx *ctx, const void *d_recv, uint64_t n, uint64_t total_lines,
+                                  void *wait_stream, kmer_result **out);
 kmer_status kmer_records_export(kmer_ctx *ctx, kmer_result **out);
 kmer_status kmer_records_import(kmer_ctx *ctx, const char *keys, const uint64_t *offsets,
                                 const uint64_t *counts, const uint64_t *firsts, uint64_t n);
+/* Drop this session's record keys (after they were moved to another rank). */
+kmer_status kmer_records_clear(kmer_ctx *ctx);
 /* Ordered result of the last finish, still in device memory (packed path):
  * keys = n * k bytes, counts = uint64[n], firsts = uint64[n]. */
 kmer_status kmer_result_device(kmer_ctx *ctx, const void **d_keys, const void **d_counts,

@@ -20,7 +20,8 @@ FLAG_SORT_FINISH = 8
 # every symbol the header declares (tests/test_abi.py checks header <-> library)
 EXPORTS = ["kmer_open", "kmer_close", "kmer_count_file", "kmer_count_buffer", "kmer_reset",
            "kmer_feed_device", "kmer_finish_device", "kmer_partial_device", "kmer_finish_merged",
-           "kmer_records_export", "kmer_records_import", "kmer_result_device", "kmer_set_position",
+           "kmer_exchange_prepare", "kmer_finish_exchanged",
+           "kmer_records_export", "kmer_records_import", "kmer_records_clear", "kmer_result_device", "kmer_set_position",
            "kmer_lines", "kmer_result_size", "kmer_result_lines", "kmer_result_get",
            "kmer_result_arrays", "kmer_result_firsts", "kmer_result_free", "kmer_synth_fastq_device",
            "kmer_last_timing", "kmer_status_string", "kmer_last_error", "kmer_version"]
@@ -63,7 +64,10 @@ def _load():
         "kmer_finish_device": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
         "kmer_partial_device": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), pu64]),
         "kmer_finish_merged": (ctypes.c_int, [vp, vp, vp, u64, u64, ctypes.POINTER(vp)]),
+        "kmer_exchange_prepare": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.POINTER(vp), pu64]),
+        "kmer_finish_exchanged": (ctypes.c_int, [vp, vp, u64, u64, vp, ctypes.POINTER(vp)]),
         "kmer_records_export": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
+        "kmer_records_clear": (ctypes.c_int, [vp]),
         "kmer_records_import": (ctypes.c_int, [vp, ctypes.c_char_p, pu64, pu64, pu64, u64]),
         "kmer_result_device": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp), pu64]),
         "kmer_result_firsts": (ctypes.c_int, [vp, ctypes.POINTER(pu64)]),
@@ -215,6 +219,21 @@ class Counter:
                                            ctypes.byref(r) if want_result else None), "finish_merged")
         return Result(r) if want_result else None
 
+    def exchange_prepare(self, world):
+        """(d_send, counts): this session's counting hits partitioned by owning
+        rank (16-byte {order key, packed key} records, owner-major, each run in
+        first-occurrence order) and the number of records per owner."""
+        d = ctypes.c_void_p()
+        cnt = (ctypes.c_uint64 * world)()
+        self._check(LIB.kmer_exchange_prepare(self.h, world, ctypes.byref(d), cnt), "exchange_prepare")
+        return d.value or 0, list(cnt)
+
+    def finish_exchanged(self, d_recv, n, total_lines, stream=0, want_result=False):
+        r = ctypes.c_void_p()
+        self._check(LIB.kmer_finish_exchanged(self.h, ctypes.c_void_p(d_recv), n, total_lines, ctypes.c_void_p(stream),
+                                              ctypes.byref(r) if want_result else None), "finish_exchanged")
+        return Result(r) if want_result else None
+
     def records_export(self):
         """Host-side record keys (non-ACGT windows) as (keys, offsets, counts, firsts)."""
         r = ctypes.c_void_p()
@@ -233,6 +252,10 @@ class Counter:
         P = ctypes.POINTER(ctypes.c_uint64)
         self._check(LIB.kmer_records_import(self.h, keybuf, off.ctypes.data_as(P), cnt.ctypes.data_as(P),
                                             fst.ctypes.data_as(P), n), "records_import")
+
+    def records_clear(self):
+        """Drop the host-side record keys (they were moved to another rank)."""
+        self._check(LIB.kmer_records_clear(self.h), "records_clear")
 
     def result_device(self):
         """(d_keys, d_counts, d_firsts, n) of the last finish, in device memory."""

@@ -117,6 +117,10 @@ struct kmer_ctx {
     DBuf<HeadRec> hrec;
     DBuf<uint32_t> bH, bHs;        // bucket finish: per (bucket, block) counts, their scan
     DBuf<uint16_t> pkey16;         // bucket finish: low key bits, partitioned
+    DBuf<XHit> xsend;              // hit exchange: valid hits partitioned by owner rank
+    DBuf<uint32_t> xH, xHs;        // ... per (owner, block) counts, their scan
+    DBuf<uint64_t> xcnt;           // ... per owner totals (device)
+    uint64_t *h_xcnt = nullptr;    // ... pinned host copy (XP_MAXW)
     bool long_seg = false;         // INFO_LONGSEG seen this session
     bool chunk_open = false;       // the last chunk did not end with '\n'
     bool out_pending = false;      // unique count of the last finish not yet read back (h_small[13])
@@ -153,6 +157,7 @@ struct kmer_ctx {
     DBuf<uint8_t> batch;
     // timing (HIP events on the context stream)
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr;
+    hipEvent_t evw = nullptr;      // cross-stream wait (no timing)
     double scan_ms = 0.0, feed_ms = 0.0, finish_ms = 0.0;
 };
 
@@ -1102,7 +1107,8 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
     ok &= hipHostMalloc((void **)&c->h_small, 16 * sizeof(uint64_t), hipHostMallocDefault) == hipSuccess;
     ok &= hipEventCreate(&c->ev0) == hipSuccess && hipEventCreate(&c->ev1) == hipSuccess &&
           hipEventCreate(&c->ev2) == hipSuccess && hipEventCreate(&c->ev3) == hipSuccess &&
-          hipEventCreate(&c->ev4) == hipSuccess;
+          hipEventCreate(&c->ev4) == hipSuccess &&
+          hipEventCreateWithFlags(&c->evw, hipEventDisableTiming) == hipSuccess;
     if (!ok) return cleanup(KMER_E_OOM);
     if (ensure_records(c, 1 << 16) || ensure_tiles(c, 1 << 12)) return cleanup(KMER_E_OOM);
     if (c->ovf.ensure(1 << 16, c->stream) != hipSuccess) return cleanup(KMER_E_OOM);
@@ -1123,6 +1129,11 @@ kmer_status kmer_close(kmer_ctx *c) {
         b->release();
     for (auto *b : {&c->ridx, &c->ridx2, &c->opos, &c->xslot, &c->rkey32, &c->rkey32b, &c->bH, &c->bHs}) b->release();
     c->pkey16.release();
+    c->xsend.release();
+    c->xH.release();
+    c->xHs.release();
+    c->xcnt.release();
+    if (c->h_xcnt) (void)hipHostFree(c->h_xcnt);
     c->bsum.release();
     c->bscan.release();
     c->hrec.release();
@@ -1142,7 +1153,7 @@ kmer_status kmer_close(kmer_ctx *c) {
     dfree(c->d_ticket); dfree(c->d_scal); dfree(c->d_pos); dfree(c->d_pos_saved);
     dfree(c->d_P); dfree(c->d_PR);
     if (c->h_small) (void)hipHostFree(c->h_small);
-    for (hipEvent_t e : {c->ev0, c->ev1, c->ev2, c->ev3, c->ev4})
+    for (hipEvent_t e : {c->ev0, c->ev1, c->ev2, c->ev3, c->ev4, c->evw})
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1290,6 +1301,82 @@ kmer_status kmer_finish_merged(kmer_ctx *c, const void *d_keys, const void *d_va
     return build_result(c, total_lines, out);
 }
 
+kmer_status kmer_exchange_prepare(kmer_ctx *c, uint32_t world, const void **d_send, uint64_t *counts) {
+    if (!c || !d_send || !counts || world == 0 || world > XP_MAXW) return KMER_E_BAD_PARAM;
+    if (c->mode != MODE_PACKED && c->mode != MODE_WINDOWS)
+        return fail(c, KMER_E_STATE, "configuration has no packed keys");
+    if (!c->open_stream) return fail(c, KMER_E_STATE, "exchange without reset/feed");
+    if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
+    hipStream_t s = c->stream;
+    kmer_status st = apply_cross(c);
+    if (st) return st;
+    const uint64_t n = c->n_hits;
+    *d_send = nullptr;
+    for (uint32_t o = 0; o < world; ++o) counts[o] = 0;
+    c->n_hits = 0;           // the rank arrays are handed over (finish_exchanged refills them)
+    if (n == 0) return KMER_OK;
+    const uint64_t nblk64 = (n + XP_EPB_HOST - 1) / XP_EPB_HOST;
+    if ((uint64_t)world * nblk64 >= (1ull << 31)) return fail(c, KMER_E_BAD_PARAM, "too many hits to partition");
+    const uint32_t nblk = (uint32_t)nblk64;
+    const uint64_t invalid = c->kbits >= 63 ? ~0ull : (1ull << c->kbits);
+    HIPCHK(c, c->xsend.ensure(n, s));
+    HIPCHK(c, c->xH.ensure((uint64_t)world * nblk, s));
+    HIPCHK(c, c->xHs.ensure((uint64_t)world * nblk, s));
+    HIPCHK(c, c->xcnt.ensure(world, s));
+    if (!c->h_xcnt) HIPCHK(c, hipHostMalloc((void **)&c->h_xcnt, XP_MAXW * sizeof(uint64_t), hipHostMallocDefault));
+    const uint64_t *rk = c->narrow ? nullptr : c->rkey.p;
+    const uint32_t *rk32 = c->narrow ? c->rkey32.p : nullptr;
+    HIPCHK(c, launch_xpart_hist(rk, rk32, n, invalid, c->kbits, world, nblk, c->xH.p, s));
+    ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->xH.p, c->xHs.p, 0u, (size_t)world * nblk,
+                                           rocprim::plus<uint32_t>(), s));
+    HIPCHK(c, launch_xpart_scatter(rk, rk32, c->rord.p, n, invalid, c->kbits, world, nblk, c->xH.p, c->xHs.p,
+                                   c->xsend.p, c->xcnt.p, s));
+    HIPCHK(c, hipMemcpyAsync(c->h_xcnt, c->xcnt.p, world * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    for (uint32_t o = 0; o < world; ++o) counts[o] = c->h_xcnt[o];
+    *d_send = c->xsend.p;
+    return KMER_OK;
+}
+
+kmer_status kmer_finish_exchanged(kmer_ctx *c, const void *d_recv, uint64_t n, uint64_t total_lines,
+                                  void *wait_stream, kmer_result **out) {
+    if (!c || (n && !d_recv)) return KMER_E_BAD_PARAM;
+    if (c->mode != MODE_PACKED && c->mode != MODE_WINDOWS)
+        return fail(c, KMER_E_STATE, "configuration has no packed keys");
+    if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
+    if (out) *out = nullptr;
+    hipStream_t s = c->stream;
+    if (wait_stream) {
+        // the received buffer was written on the caller's stream (the collective)
+        HIPCHK(c, hipEventRecord(c->evw, (hipStream_t)wait_stream));
+        HIPCHK(c, hipStreamWaitEvent(s, c->evw, 0));
+    }
+    HIPCHK(c, hipEventRecord(c->ev2, s));
+    // the received hits, concatenated by source rank, are in rank order
+    kmer_status st = ensure_rank_arrays(c, n, 0, s);
+    if (st) return st;
+    HIPCHK(c, launch_xprep((const XHit *)d_recv, n, c->rkey.p, c->narrow ? c->rkey32.p : nullptr, c->rord.p,
+                           c->ridx.p, s));
+    uint64_t nu = 0;
+    const bool sync = out || c->p.max_keys;
+    st = rank_finish(c, n, false, false, &nu, sync);
+    if (st) return st;
+    c->n_out = nu;
+    HIPCHK(c, hipEventRecord(c->ev3, s));
+    c->timing_pending = true;
+    c->n_hits = 0;
+    c->n_cross = 0;
+    c->open_stream = false;
+    if (!sync) return KMER_OK;
+    st = resolve_out(c);
+    if (st) return st;
+    const uint64_t total = c->n_out + c->exotic.size();
+    if (c->p.max_keys && total > c->p.max_keys)
+        return fail(c, KMER_E_TOO_MANY_KEYS, "more distinct keys than max_keys (reference Map limit)");
+    if (!out) return KMER_OK;
+    return build_result(c, total_lines, out);
+}
+
 kmer_status kmer_records_export(kmer_ctx *c, kmer_result **out) {
     if (!c || !out) return KMER_E_BAD_PARAM;
     kmer_result *r = new (std::nothrow) kmer_result();
@@ -1320,6 +1407,12 @@ kmer_status kmer_records_import(kmer_ctx *c, const char *keys, const uint64_t *o
             it->second.first = std::min(it->second.first, firsts[i]);
         }
     }
+    return KMER_OK;
+}
+
+kmer_status kmer_records_clear(kmer_ctx *c) {
+    if (!c) return KMER_E_BAD_PARAM;
+    c->exotic.clear();
     return KMER_OK;
 }
 

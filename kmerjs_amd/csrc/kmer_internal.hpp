@@ -290,6 +290,20 @@ hipError_t launch_bucket_scatter(const uint32_t *key, uint64_t n, uint32_t inval
                                  uint32_t nblk, const uint32_t *Hs, uint16_t *pkey, uint32_t *prank, hipStream_t s);
 hipError_t launch_bucket_heads(const uint16_t *pkey, const uint32_t *prank, const uint32_t *Hs, const uint32_t *H,
                                uint32_t nb, uint32_t nblk, uint32_t shift, HeadRec *hrec, hipStream_t s);
+// multi-GPU hit exchange (kmer_exchange_prepare / kmer_finish_exchanged)
+struct XHit {
+    uint64_t ord;                  // first-occurrence order key
+    uint64_t key;                  // packed suffix code
+};
+constexpr uint32_t XP_MAXW = 256;            // most ranks of one exchange
+constexpr uint32_t XP_EPB_HOST = 4096;       // rank slots per partition block (= XP_EPB)
+hipError_t launch_xpart_hist(const uint64_t *rkey, const uint32_t *rkey32, uint64_t n, uint64_t invalid,
+                             uint32_t kbits, uint32_t world, uint32_t nblk, uint32_t *H, hipStream_t s);
+hipError_t launch_xpart_scatter(const uint64_t *rkey, const uint32_t *rkey32, const uint64_t *rord, uint64_t n,
+                                uint64_t invalid, uint32_t kbits, uint32_t world, uint32_t nblk, const uint32_t *H,
+                                const uint32_t *Hs, XHit *out, uint64_t *counts, hipStream_t s);
+hipError_t launch_xprep(const XHit *x, uint64_t n, uint64_t *rkey, uint32_t *rkey32, uint64_t *rord, uint32_t *ridx,
+                        hipStream_t s);
 hipError_t launch_merge_prep(const uint64_t *keys, const Agg *vals, uint64_t n, uint64_t *rkey, uint32_t *rkey32,
                              uint64_t *rord, uint64_t *rcnt, uint32_t *ridx, hipStream_t s);
 hipError_t launch_gather_records(const Record *recs, const uint64_t *key_off, uint64_t n,

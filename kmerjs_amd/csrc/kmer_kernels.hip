@@ -1878,6 +1878,115 @@ __global__ __launch_bounds__(256) void merge_prep_kernel(const uint64_t *keys, c
     }
 }
 
+// ---------------------------------------------------------------------------
+// Multi-GPU hit exchange: the session's ranked hits, partitioned by owning
+// rank (equal slices of the packed-key space, multi.key_owner), stable within
+// each owner so that every destination's run stays in rank (= first
+// occurrence) order.  Non-counting slots (invalid key) are dropped.
+// ---------------------------------------------------------------------------
+constexpr uint32_t XP_EPB = 4096;            // rank slots per partition block
+
+__device__ __forceinline__ uint32_t xkey_owner(uint64_t key, uint32_t kbits, uint32_t world) {
+    const uint32_t s = kbits > 40 ? kbits - 40 : 0;
+    const uint64_t o = ((key >> s) * (uint64_t)world) >> (kbits - s);
+    return o < world ? (uint32_t)o : world - 1u;
+}
+
+__device__ __forceinline__ uint64_t xget_key(const uint64_t *rkey, const uint32_t *rkey32, uint64_t i) {
+    return rkey32 ? (uint64_t)rkey32[i] : rkey[i];
+}
+
+__global__ __launch_bounds__(256) void xpart_hist_kernel(const uint64_t *rkey, const uint32_t *rkey32, uint64_t n,
+                                                         uint64_t invalid, uint32_t kbits, uint32_t world,
+                                                         uint32_t nblk, uint32_t *H) {
+    __shared__ uint32_t hist[XP_MAXW];
+    for (uint32_t o = threadIdx.x; o < world; o += 256) hist[o] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * XP_EPB;
+    for (uint32_t j = threadIdx.x; j < XP_EPB; j += 256) {
+        const uint64_t i = base + j;
+        if (i < n) {
+            const uint64_t k = xget_key(rkey, rkey32, i);
+            if (k != invalid) atomicAdd(&hist[xkey_owner(k, kbits, world)], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t o = threadIdx.x; o < world; o += 256) H[(uint64_t)o * nblk + blockIdx.x] = hist[o];
+}
+
+// Stable scatter: slots are taken in rank order, 256 per round; inside a wave
+// the lanes of one owner are ranked with a ballot, across waves and rounds
+// with per-owner LDS counters.
+__global__ __launch_bounds__(256) void xpart_scatter_kernel(const uint64_t *rkey, const uint32_t *rkey32,
+                                                            const uint64_t *rord, uint64_t n, uint64_t invalid,
+                                                            uint32_t kbits, uint32_t world, uint32_t nblk,
+                                                            const uint32_t *Hs, XHit *out) {
+    __shared__ uint32_t run[XP_MAXW];          // owner's slots taken by earlier rounds (+ block start)
+    __shared__ uint32_t wcnt[4][XP_MAXW];      // this round: per wave, per owner
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint32_t o = threadIdx.x; o < world; o += 256) {
+        run[o] = Hs[(uint64_t)o * nblk + blockIdx.x];
+        wcnt[0][o] = wcnt[1][o] = wcnt[2][o] = wcnt[3][o] = 0;
+    }
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * XP_EPB;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (uint32_t u = 0; u < XP_EPB / 256; ++u) {
+        const uint64_t i = base + u * 256 + threadIdx.x;
+        uint64_t key = invalid;
+        if (i < n) key = xget_key(rkey, rkey32, i);
+        const bool valid = key != invalid;
+        const uint32_t o = valid ? xkey_owner(key, kbits, world) : 0u;
+        uint32_t pre = 0;
+        uint64_t pending = __ballot(valid);
+        while (pending) {
+            const int leader = __ffsll((long long)pending) - 1;
+            const uint32_t lo = __shfl(o, leader);
+            const uint64_t m = __ballot(valid && o == lo);
+            if (valid && o == lo) pre = __popcll(m & lt);
+            if ((int)lane == leader) wcnt[wave][lo] = __popcll(m);
+            pending &= ~m;
+        }
+        __syncthreads();
+        if (valid) {
+            uint32_t p = run[o] + pre;
+            for (uint32_t w = 0; w < wave; ++w) p += wcnt[w][o];
+            XHit h;
+            h.ord = rord[i];
+            h.key = key;
+            out[p] = h;
+        }
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < world; t += 256) {
+            run[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
+            wcnt[0][t] = wcnt[1][t] = wcnt[2][t] = wcnt[3][t] = 0;
+        }
+        __syncthreads();
+    }
+}
+
+// per-owner totals of the partition (exclusive scan Hs of H, owner-major)
+__global__ void xpart_counts_kernel(const uint32_t *H, const uint32_t *Hs, uint32_t world, uint32_t nblk,
+                                    uint64_t *counts) {
+    const uint64_t last = (uint64_t)world * nblk - 1;
+    for (uint32_t o = threadIdx.x; o < world; o += blockDim.x) {
+        const uint64_t lo = Hs[(uint64_t)o * nblk];
+        const uint64_t hi = o + 1 < world ? (uint64_t)Hs[(uint64_t)(o + 1) * nblk] : (uint64_t)Hs[last] + H[last];
+        counts[o] = hi - lo;
+    }
+}
+
+// received hits (concatenated by source rank = rank order) -> rank arrays
+__global__ __launch_bounds__(256) void xprep_kernel(const XHit *x, uint64_t n, uint64_t *rkey, uint32_t *rkey32,
+                                                    uint64_t *rord, uint32_t *ridx) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const XHit h = x[i];
+        put_key(rkey, rkey32, i, h.key);
+        rord[i] = h.ord;
+        ridx[i] = (uint32_t)i;
+    }
+}
+
 __global__ __launch_bounds__(256) void gather_records_kernel(const Record *recs, const uint64_t *key_off,
                                                              uint64_t n, const uint8_t *data, uint8_t *out) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -2067,6 +2176,26 @@ hipError_t launch_merge_prep(const uint64_t *keys, const Agg *vals, uint64_t n, 
     if (n)
         hipLaunchKernelGGL(merge_prep_kernel, dim3(grid_for(n)), dim3(256), 0, s, keys, vals, n, rkey, rkey32, rord, rcnt,
                            ridx);
+    return hipGetLastError();
+}
+hipError_t launch_xpart_hist(const uint64_t *rkey, const uint32_t *rkey32, uint64_t n, uint64_t invalid,
+                             uint32_t kbits, uint32_t world, uint32_t nblk, uint32_t *H, hipStream_t s) {
+    if (world == 0 || world > XP_MAXW || nblk == 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(xpart_hist_kernel, dim3(nblk), dim3(256), 0, s, rkey, rkey32, n, invalid, kbits, world, nblk, H);
+    return hipGetLastError();
+}
+hipError_t launch_xpart_scatter(const uint64_t *rkey, const uint32_t *rkey32, const uint64_t *rord, uint64_t n,
+                                uint64_t invalid, uint32_t kbits, uint32_t world, uint32_t nblk, const uint32_t *H,
+                                const uint32_t *Hs, XHit *out, uint64_t *counts, hipStream_t s) {
+    if (world == 0 || world > XP_MAXW || nblk == 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(xpart_scatter_kernel, dim3(nblk), dim3(256), 0, s, rkey, rkey32, rord, n, invalid, kbits, world,
+                       nblk, Hs, out);
+    hipLaunchKernelGGL(xpart_counts_kernel, dim3(1), dim3(256), 0, s, H, Hs, world, nblk, counts);
+    return hipGetLastError();
+}
+hipError_t launch_xprep(const XHit *x, uint64_t n, uint64_t *rkey, uint32_t *rkey32, uint64_t *rord, uint32_t *ridx,
+                        hipStream_t s) {
+    if (n) hipLaunchKernelGGL(xprep_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, n, rkey, rkey32, rord, ridx);
     return hipGetLastError();
 }
 hipError_t launch_gather_records(const Record *recs, const uint64_t *key_off, uint64_t n, const uint8_t *data,

@@ -7,13 +7,20 @@ makes first-occurrence order keys comparable across ranks.  Each rank reduces
 its shard to a partial result (unique packed keys + {first, count}, in
 first-occurrence order).  Two ways to finish:
 
-* finish_distributed: ONE all-to-all (RCCL over xGMI) by key range -- rank r
-  receives every rank's entries of its key range; the concatenation by source
-  rank is already in first-occurrence order (shards are in line order), so a
-  merged finish (kmer_finish_merged) on each rank yields that rank's key range
-  of the result, ordered by first occurrence.  The global Map order is the
-  merge of the ranks' lists by first occurrence (collect_ordered).  Work per
-  rank stays constant as ranks are added.
+* finish_exchange (the default): no per-rank reduce at all -- the session's
+  counting hits are partitioned by owning rank on the device
+  (kmer_exchange_prepare: equal slices of the packed-key space, stable), ONE
+  all-to-all (RCCL over xGMI) moves each run to its owner, and the owner
+  counts what it received with the single-GPU finish (kmer_finish_exchanged).
+  The received runs, concatenated by source rank, are in first-occurrence
+  order (shards are in line order), so each rank ends with its key range of
+  the result, ordered by first occurrence.  The global Map order is the merge
+  of the ranks' lists by first occurrence (collect_ordered).  Work per rank
+  stays constant as ranks are added.
+* finish_distributed: the same key-range all-to-all, but of per-rank partials
+  (unique keys + {first, count}, kmer_partial_device) merged with
+  kmer_finish_merged -- fewer bytes on the wire when keys repeat a lot within
+  a shard (high coverage), one more reduce per rank.
 * merge_to: gather every partial to one rank and finish there (one ordered
   result on one GPU; the gather and the merge grow with the rank count).
 
@@ -112,19 +119,27 @@ def gather_partials(keys, vals, pad_key, dst=0, group=None):
     return None, None
 
 
-def gather_records(ctr, dst=0, group=None):
-    """Move every rank's host record keys (non-ACGT windows) into rank dst's context."""
+def gather_records(ctr, dst=0, group=None, total=None, mine=None):
+    """Move every rank's host record keys (non-ACGT windows) into rank dst's context.
+
+    total: the number of records over all ranks when the caller already knows
+    it (else one all-reduce finds it); mine: this rank's records_export()."""
     rank = dist.get_rank(group)
-    mine = ctr.records_export()
+    if mine is None:
+        mine = ctr.records_export()
     # skip the object gather when no rank has records (the common case)
-    dev = "cpu" if dist.get_backend(group) == "gloo" else torch.device("cuda", torch.cuda.current_device())
-    tot = torch.tensor([len(mine[2])], dtype=torch.int64, device=dev)
-    dist.all_reduce(tot, group=group)
-    if int(tot.item()) == 0:
+    if total is None:
+        dev = "cpu" if dist.get_backend(group) == "gloo" else torch.device("cuda", torch.cuda.current_device())
+        tot = torch.tensor([len(mine[2])], dtype=torch.int64, device=dev)
+        dist.all_reduce(tot, group=group)
+        total = int(tot.item())
+    if total == 0:
         return
     payload = (mine[0], mine[1].tolist(), mine[2].tolist(), mine[3].tolist())
     got = [None] * dist.get_world_size(group) if rank == dst else None
     dist.gather_object(payload, got, dst=dst, group=group)
+    if rank != dst:
+        ctr.records_clear()          # moved: a later host result of this rank must not repeat them
     if rank == dst:
         import numpy as np
         for r, (kb, off, cnt, fst) in enumerate(got):
@@ -164,6 +179,54 @@ def shuffle_partials(keys, vals, kbits, group=None):
     if host_coll:
         rk, rv = rk.to(dev), rv.to(dev)
     return rk, rv
+
+
+def exchange_counts(counts, n_records, device, group=None):
+    """All-to-all of the per-destination run lengths, with this rank's host
+    record count riding along.  Returns (received run lengths by source rank,
+    record counts by rank) as host lists -- one device->host sync."""
+    world = dist.get_world_size(group)
+    assert len(counts) == world
+    if dist.get_backend(group) == "gloo":
+        device = "cpu"
+    send = torch.tensor([[c, n_records] for c in counts], dtype=torch.int64).to(device, non_blocking=True)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)
+    r = recv.cpu().tolist()
+    return [x[0] for x in r], [x[1] for x in r]
+
+
+def exchange_runs(send, counts, recv_counts, words=2, group=None):
+    """All-to-all of owner-major runs of `words` int64 words per record:
+    send = int64[words * sum(counts)] (run o goes to rank o); returns the
+    received runs concatenated by source rank, int64[words * sum(recv_counts)]."""
+    dev = send.device
+    host_coll = dist.get_backend(group) == "gloo"
+    out = torch.empty(words * sum(recv_counts), dtype=torch.int64, device="cpu" if host_coll else dev)
+    src = send.cpu() if host_coll else send
+    dist.all_to_all_single(out, src, [words * x for x in recv_counts], [words * x for x in counts], group=group)
+    return out.to(dev) if host_coll else out
+
+
+def finish_exchange(ctr, k, plen, total_lines, group=None, want_result=False, records=True, dst=0):
+    """Finish a sharded count by exchanging hits (module docstring): afterwards
+    every rank holds its key range of the result, ordered by first occurrence
+    (device, kmer_result_device).  Record keys are merged on rank `dst`."""
+    world = dist.get_world_size(group)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    d_x, counts = ctr.exchange_prepare(world)
+    mine = ctr.records_export() if records else None
+    recv_counts, rec_counts = exchange_counts(counts, len(mine[2]) if mine else 0, dev, group=group)
+    n_send = sum(counts)
+    send = device_u64(d_x, 2 * n_send, dev) if n_send else torch.empty(0, dtype=torch.int64, device=dev)
+    recv = exchange_runs(send, counts, recv_counts, group=group)
+    if records:
+        gather_records(ctr, dst=dst, group=group, total=sum(rec_counts), mine=mine)
+    # the finish runs on the context's stream after the collective (stream wait,
+    # no host sync) and may read `recv` after returning: keep it alive
+    ctr._keepalive = (recv,)
+    return ctr.finish_exchanged(recv.data_ptr(), recv.numel() // 2, total_lines,
+                                stream=torch.cuda.current_stream(dev).cuda_stream, want_result=want_result)
 
 
 def finish_distributed(ctr, k, plen, total_lines, group=None, want_result=False, records=True, dst=0):

@@ -32,6 +32,9 @@ class _FakeCounter:
         return kb, off, np.array([v[0] for _, v in items], dtype=np.uint64), \
             np.array([v[1] for _, v in items], dtype=np.uint64)
 
+    def records_clear(self):
+        self.recs = {}
+
     def records_import(self, kb, off, cnt, fst):
         for i in range(len(cnt)):
             key = kb[int(off[i]):int(off[i + 1])]
@@ -165,3 +168,47 @@ def test_key_owner_balanced_and_monotone():
         assert bool((own[1:] >= own[:-1]).all())
     big = torch.tensor([(1 << 62) - 1, 0], dtype=torch.int64)
     assert multi.key_owner(big, 62, 8).tolist() == [7, 0]
+
+
+def _exchange_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # owner-major runs of {order, key} records, as kmer_exchange_prepare lays them out
+        counts = [(rank + 1) * (o + 2) % 5 for o in range(world)]
+        recs = []
+        for o in range(world):
+            recs += [[(rank << 40) + 100 * o + i, 1000 * o + i] for i in range(counts[o])]
+        send = torch.tensor(recs, dtype=torch.int64).view(-1) if recs else torch.empty(0, dtype=torch.int64)
+        recv_counts, rec_counts = multi.exchange_counts(counts, 10 + rank, "cpu")
+        recv = multi.exchange_runs(send, counts, recv_counts)
+        q.put(("ok", rank, counts, recv_counts, rec_counts, recv.view(-1, 2).tolist()))
+    except Exception as e:  # pragma: no cover
+        q.put(("err", rank, repr(e), None, None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_hit_exchange_collectives_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exchange_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[0] == "ok" for r in res), res
+    by_rank = {r[1]: r for r in res}
+    for rank in range(world):
+        _, _, counts, recv_counts, rec_counts, recv = by_rank[rank]
+        assert rec_counts == [10 + r for r in range(world)]          # every rank's record count
+        assert recv_counts == [by_rank[src][2][rank] for src in range(world)]
+        # run `rank` of every source, concatenated by source rank: global order kept
+        want = [[(src << 40) + 100 * rank + i, 1000 * rank + i] for src in range(world)
+                for i in range(by_rank[src][2][rank])]
+        assert recv == want

@@ -219,6 +219,72 @@ def _shard_and_merge(native, data, k, prefix, world, batch_bytes=0):
             c.close()
 
 
+def _shard_and_exchange(native, data, k, prefix, world):
+    """Count `data` as `world` record-aligned shards (one context per rank) and
+    finish with the hit exchange (multi.finish_exchange, done in-process): each
+    owner counts the runs every rank sent it.  Returns the whole ordered Map
+    (the owners' lists merged by first occurrence) and the line count."""
+    import torch
+    from kmerjs_amd.multi import device_u64, key_owner, split_at_records
+    shards = split_at_records(data, world)
+    ctrs = [native.Counter(k=k, prefix=prefix) for _ in range(world)]
+    dev = torch.device("cuda")
+    try:
+        runs, recs, total_lines = [], [], 0
+        for ctr, (lo, hi, lines_before) in zip(ctrs, shards):
+            ctr.reset()
+            ctr.set_position(lines_before, lo)
+            part = data[lo:hi]
+            if part:
+                t = torch.frombuffer(bytearray(part), dtype=torch.uint8).cuda()
+                ctr.feed_device(t.data_ptr(), len(part))
+                torch.cuda.synchronize()
+            total_lines = max(total_lines, ctr.lines())
+            d_x, counts = ctr.exchange_prepare(world)
+            x = device_u64(d_x, 2 * sum(counts), dev).clone() if sum(counts) else torch.empty(0, dtype=torch.int64,
+                                                                                               device=dev)
+            offs = np.cumsum([0] + counts)
+            runs.append([x[2 * offs[o]:2 * offs[o + 1]] for o in range(world)])
+            recs.append(ctr.records_export())
+        for c, r in zip(ctrs[1:], recs[1:]):
+            ctrs[0].records_import(*r)
+            c.records_clear()                      # moved to rank 0 (multi.gather_records)
+        kbits = 2 * (k - len(prefix))
+        merged = []
+        for o in range(world):
+            recv = torch.cat([runs[src][o] for src in range(world)])
+            if recv.numel():
+                keys = recv.view(-1, 2)[:, 1]
+                assert bool((key_owner(keys, kbits, world) == o).all())     # only this owner's key range
+                fo = recv.view(-1, 2)[:, 0]
+                assert bool((fo[1:] > fo[:-1]).all())                     # in first-occurrence order
+            r = ctrs[o].finish_exchanged(recv.data_ptr(), recv.numel() // 2, total_lines, want_result=True)
+            merged += [(int(f), kk, c) for f, (kk, c) in zip(r.firsts.tolist(), r.entries())]
+        merged.sort(key=lambda t: t[0])
+        return [(kk, c) for _, kk, c in merged], total_lines
+    finally:
+        for c in ctrs:
+            c.close()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_hit_exchange_matches_oracle(native, world):
+    # default multi-GPU finish (SURVEY.md §8e): hits partitioned by owner, exchanged, counted per owner
+    from oracle import oracle
+    rng = np.random.default_rng(100 + world)
+    arr = np.frombuffer(bytearray(oracle.synth_fastq(9, 0, 20000)), dtype=np.uint8).reshape(-1, 317).copy()
+    seq = arr[:, 13:163]
+    seq[rng.random(seq.shape) < 0.002] = ord("N")
+    arr[:, 13:163] = seq
+    data = arr.tobytes()
+    for k, p, n in ((16, b"ATGAC", 20000), (13, b"AC", 20000), (32, b"ATGAC", 20000), (21, b"", 3000)):
+        part = data[:317 * n]
+        want = oracle.count_buffer(part, p, k, 1)
+        got, lines = _shard_and_exchange(native, part, k, p, world)
+        assert lines == 4 * n
+        assert first_diff(got, want) is None, (world, k, p)
+
+
 @pytest.mark.parametrize("world", [2, 3, 5])
 def test_sharded_merge_matches_oracle(native, world):
     # multi-GPU exchange (SURVEY.md §8e): per-shard partials + merged finish == whole count
