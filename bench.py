@@ -205,14 +205,19 @@ def main():
     total_lines = wl["total_lines"]
     tile_ms, feed_ms_l = [], []
 
+    recorded = [False]
+
     def step(record):
+        if recorded[0]:
+            # kernel times of the previous step's feed (read now: the feed's host
+            # wait returns before its closing event; the finish is not waited for)
+            scan_ms, feed_ms, _ = ctr.last_timing(finish=False)
+            tile_ms.append(scan_ms)
+            feed_ms_l.append(feed_ms)
+        recorded[0] = record
         ctr.reset()
         ctr.set_position(plan["lines_before"], plan["byte_offset"])
         ctr.feed_device(buf.data_ptr(), nbytes)
-        scan_ms, feed_ms, _ = ctr.last_timing()
-        if record:
-            tile_ms.append(scan_ms)
-            feed_ms_l.append(feed_ms)
         multi_finish()
 
     def multi_finish():
@@ -243,6 +248,7 @@ def main():
         elapsed = float(t.item())
 
     # one more pass to read the result size / accepted windows (outside the timed region)
+    step(False)
     ctr.reset()
     ctr.set_position(plan["lines_before"], plan["byte_offset"])
     ctr.feed_device(buf.data_ptr(), nbytes)

@@ -157,7 +157,8 @@ kmer_status kmer_synth_fastq_device(void *d_out, uint64_t seed, uint64_t first_r
 /* Device time (HIP events on the context's stream, ms) since the last reset:
  * scan_ms = the streaming tile-scan kernel(s) alone, feed_ms = every kernel of
  * the feeds (scan + line scans + hit resolution), finish_ms = the last finish
- * (compaction + sort + decode). */
+ * (compaction + sort + decode).  Waits for the last finish only when
+ * finish_ms is non-NULL. */
 kmer_status kmer_last_timing(kmer_ctx *ctx, double *scan_ms, double *feed_ms, double *finish_ms);
 
 const char *kmer_status_string(kmer_status s);

@@ -269,11 +269,13 @@ class Counter:
         self._check(LIB.kmer_lines(self.h, ctypes.byref(n)), "lines")
         return n.value
 
-    def last_timing(self):
-        """(scan_kernel_ms, feed_ms, finish_ms) device times since the last reset."""
+    def last_timing(self, finish=True):
+        """(scan_kernel_ms, feed_ms, finish_ms) device times since the last reset.
+        finish=False: do not wait for a finish still running (finish_ms is None)."""
         a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
-        self._check(LIB.kmer_last_timing(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "last_timing")
-        return a.value, b.value, c.value
+        self._check(LIB.kmer_last_timing(self.h, ctypes.byref(a), ctypes.byref(b),
+                                         ctypes.byref(c) if finish else None), "last_timing")
+        return a.value, b.value, (c.value if finish else None)
 
 
 def synth_fastq_device(ptr: int, seed: int, first_read: int, n_reads: int, stream: int = 0):

@@ -115,6 +115,7 @@ struct kmer_ctx {
     PlaneArgs pargs{};
     DBuf<uint32_t> ridx, ridx2, opos;
     DBuf<HeadRec> hrec;
+    DBuf<uint32_t> hcnt;           // by rank: != 0 iff first occurrence of its key (bucket finish: count)
     DBuf<uint32_t> bH, bHs;        // bucket finish: per (bucket, block) counts, their scan
     DBuf<uint16_t> pkey16;         // bucket finish: low key bits, partitioned
     DBuf<XHit> xsend;              // hit exchange: valid hits partitioned by owner rank
@@ -123,7 +124,7 @@ struct kmer_ctx {
     uint64_t *h_xcnt = nullptr;    // ... pinned host copy (XP_MAXW)
     bool long_seg = false;         // INFO_LONGSEG seen this session
     bool chunk_open = false;       // the last chunk did not end with '\n'
-    bool out_pending = false;      // unique count of the last finish not yet read back (h_small[13])
+    bool out_pending = false;      // unique count of the last finish not yet read back (h_tail[8])
     bool timing_pending = false;   // finish events not yet read
     DBuf<uint64_t> xord, xord2, xkey, xkey2;   // cross list
     DBuf<uint32_t> xslot;
@@ -154,6 +155,13 @@ struct kmer_ctx {
     bool open_stream = false;      // reset called, not finished
     std::unordered_map<std::string, Ent> exotic;
     uint64_t *h_small = nullptr;   // pinned: [0..7] copy of d_scal, [8..11] pos
+    uint64_t *h_tail = nullptr;    // pinned, mapped, coherent: d_scal[0..7] written by the chunk tail kernel
+    uint64_t *d_tail = nullptr;    // ... its device address
+    unsigned int *d_hticket = nullptr;   // chunk tail last-block ticket (d_scal[8])
+    uint64_t tail_seq = 0;         // last chunk sequence number handed to the chunk tail kernel
+    bool feed_timing_pending = false;   // scan / feed events of the last chunk not yet read
+    uint32_t prep_flags = 0;       // PREP_RESET / PREP_SETPOS pending for the next feed's prologue
+    uint64_t prep_lines = 0;
     DBuf<uint8_t> batch;
     // timing (HIP events on the context stream)
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr;
@@ -278,6 +286,51 @@ kmer_status drain_records(kmer_ctx *c, const uint8_t *d_data, uint64_t n, hipStr
     return KMER_OK;
 }
 
+// Wait for the chunk tail (hit_overflow_kernel's last block) to publish the
+// chunk's counters: spin on the sequence word it writes last to mapped host
+// memory, instead of a stream-synchronize round trip.  The stream is polled
+// now and then, so that a failed or finished stream ends the wait.
+kmer_status wait_tail(kmer_ctx *c, uint64_t seq) {
+    volatile uint64_t *flag = c->h_tail + 9;
+    for (uint32_t i = 1;; ++i) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) break;
+        if ((i & 1023) == 0) {
+            const hipError_t e = hipStreamQuery(c->stream);
+            if (e == hipSuccess) {
+                if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) break;
+                return fail(c, KMER_E_DEVICE, "chunk counters were not published");
+            }
+            if (e != hipErrorNotReady) HIPCHK(c, e);
+        }
+        __builtin_ia32_pause();
+    }
+    memcpy(c->h_small, (const void *)c->h_tail, 8 * 8);
+    return KMER_OK;
+}
+
+// Read the scan / feed kernel times of the last chunk (lazily: the chunk's
+// host wait returns before its closing event).
+kmer_status resolve_feed_timing(kmer_ctx *c) {
+    if (!c->feed_timing_pending) return KMER_OK;
+    float ms = 0.f, ms_all = 0.f;
+    HIPCHK(c, hipEventSynchronize(c->ev4));
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    HIPCHK(c, hipEventElapsedTime(&ms_all, c->ev0, c->ev4));
+    c->scan_ms += ms;
+    c->feed_ms += ms_all;
+    c->feed_timing_pending = false;
+    return KMER_OK;
+}
+
+// Apply a pending reset / set_position (and `extra` PREP_* work) on the device.
+kmer_status flush_prep(kmer_ctx *c, hipStream_t s, uint32_t extra) {
+    const uint32_t f = c->prep_flags | extra;
+    if (!f) return KMER_OK;
+    HIPCHK(c, launch_prep(c->d_pos, c->d_pos_saved, c->d_err, c->d_scal, f, c->prep_lines, s));
+    c->prep_flags = 0;
+    return KMER_OK;
+}
+
 kmer_status check_err(kmer_ctx *c, uint32_t e) {
     if (e & ERR_NONASCII) return fail(c, KMER_E_NONASCII, "input contains a byte >= 0x80 (non-ASCII)");
     if (e & ERR_LINE_TOO_LONG) return fail(c, KMER_E_LINE_TOO_LONG, "sequence line longer than 2^23 bytes");
@@ -289,7 +342,7 @@ kmer_status check_err(kmer_ctx *c, uint32_t e) {
 // fast path feed
 // ---------------------------------------------------------------------------
 struct IsHead {
-    __host__ __device__ uint32_t operator()(const HeadRec &h) const { return h.count ? 1u : 0u; }
+    __host__ __device__ uint32_t operator()(uint32_t c) const { return c ? 1u : 0u; }
 };
 
 struct TileSumOp {
@@ -383,9 +436,21 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
     init.lnl = c->abs_offset;
     const uint32_t n_blocks = (n_tiles + TSCAN_BLOCK - 1) / TSCAN_BLOCK;
 
-    HIPCHK(c, hipMemcpyAsync(c->d_pos_saved, c->d_pos, sizeof(StreamPos), hipMemcpyDeviceToDevice, s));
+    h.data = d;
+    h.len = len;
+    h.scal = c->d_scal;
+    h.ticket = c->d_hticket;
+    h.chunk_hits = c->d_chunk_hits;
+    h.chunk_cross = c->d_xcount;
+    h.ends_open = c->d_ends_open;
+    h.host_out = c->d_tail;
+    // prologue: pending reset / position, position snapshot, zeroed chunk counters
+    st = resolve_feed_timing(c);
+    if (st) return st;
+    st = flush_prep(c, s, PREP_SAVE | PREP_ZERO);
+    if (st) return st;
     for (int attempt = 0; attempt < 8; ++attempt) {
-        HIPCHK(c, hipMemsetAsync(c->d_scal, 0, 3 * 8, s));   // rec, ovf, cross counts of this chunk
+        if (attempt) HIPCHK(c, hipMemsetAsync(c->d_scal, 0, 3 * 8, s));   // rec, ovf, cross counts of this chunk
         HIPCHK(c, hipEventRecord(c->ev0, s));
         if (c->planes) HIPCHK(c, launch_scan_planes(a, c->pargs, s));
         else HIPCHK(c, launch_scan_tiles(a, s));
@@ -399,20 +464,19 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
         } else {
             HIPCHK(c, launch_tile_scan(c->tsum.p, n_tiles, c->bsum.p, false, init, c->tscan.p, s));
         }
-        HIPCHK(c, launch_hits(h, s));
-        HIPCHK(c, launch_pos_update(c->d_pos, c->tsum.p, c->tscan.p, n_tiles, d, len, c->d_chunk_hits, c->d_xcount,
-                                    c->d_ends_open, s));
+        h.seq = ++c->tail_seq;
+        HIPCHK(c, launch_hits(h, s));          // (+ the chunk tail: position, counters -> h_tail)
         HIPCHK(c, hipEventRecord(c->ev4, s));
-        HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipStreamSynchronize(s));
+        st = wait_tail(c, h.seq);
+        if (st) return st;
+        c->feed_timing_pending = true;
         const uint32_t e = (uint32_t)c->h_small[5];
         st = check_err(c, e);
         if (st) return st;
-        float ms = 0.f, ms_all = 0.f;
-        HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
-        HIPCHK(c, hipEventElapsedTime(&ms_all, c->ev0, c->ev4));
-        c->scan_ms += ms;
-        c->feed_ms += ms_all;
+        if (e & (ERR_OVF_OVERFLOW | ERR_REC_OVERFLOW | ERR_CROSS_OVERFLOW)) {
+            st = resolve_feed_timing(c);
+            if (st) return st;
+        }
         if (e & (ERR_OVF_OVERFLOW | ERR_REC_OVERFLOW | ERR_CROSS_OVERFLOW)) {
             // grow and redo the chunk from the saved position; hit placement is
             // idempotent (rank slots are rewritten, lists restart at this chunk's base)
@@ -707,6 +771,10 @@ kmer_status windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n
 }
 
 kmer_status feed(kmer_ctx *c, const uint8_t *d, uint64_t len, hipStream_t s) {
+    if (c->mode != MODE_PACKED && c->mode != MODE_TILE_REC) {
+        kmer_status st = flush_prep(c, s, 0);
+        if (st) return st;
+    }
     if (len == 0) return KMER_OK;
     const uint64_t n_tiles64 = (len + TILE - 1) / TILE;
     if (n_tiles64 > 0x7FFFFFFFull) return fail(c, KMER_E_BAD_PARAM, "chunk too large");
@@ -720,10 +788,10 @@ kmer_status feed(kmer_ctx *c, const uint8_t *d, uint64_t len, hipStream_t s) {
     return scan_feed(c, d, len, n_tiles, s);
 }
 
+// (device side deferred to the next feed's prologue kernel: flush_prep)
 kmer_status reset(kmer_ctx *c) {
-    hipStream_t s = c->stream;
-    HIPCHK(c, hipMemsetAsync(c->d_pos, 0, sizeof(StreamPos), s));
-    HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
+    c->prep_flags = PREP_RESET;
+    c->feed_timing_pending = false;
     c->exotic.clear();
     c->abs_offset = 0;
     c->n_hits = 0;
@@ -780,9 +848,9 @@ kmer_status sort_and_heads(kmer_ctx *c, K *keys, K *keys2, uint64_t n, bool with
     ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, kb, vb, (size_t)n, 0, end_bit, s));
     const uint64_t *rcnt = with_counts ? c->rcnt.p : nullptr;
     if (sizeof(K) == 4)
-        HIPCHK(c, launch_heads32((const uint32_t *)kb.current(), vb.current(), n, (uint32_t)invalid, rcnt, c->hrec.p, s));
+        HIPCHK(c, launch_heads32((const uint32_t *)kb.current(), vb.current(), n, (uint32_t)invalid, rcnt, c->hrec.p, c->hcnt.p, s));
     else
-        HIPCHK(c, launch_heads((const uint64_t *)kb.current(), vb.current(), n, invalid, rcnt, c->hrec.p, s));
+        HIPCHK(c, launch_heads((const uint64_t *)kb.current(), vb.current(), n, invalid, rcnt, c->hrec.p, c->hcnt.p, s));
     return KMER_OK;
 }
 
@@ -799,19 +867,20 @@ kmer_status bucket_heads(kmer_ctx *c, uint64_t n) {
     HIPCHK(c, c->bHs.ensure((uint64_t)nb * nblk, s));
     HIPCHK(c, c->pkey16.ensure(n, s));
     HIPCHK(c, c->ridx2.ensure(n, s));
-    HIPCHK(c, hipMemsetAsync(c->hrec.p, 0, n * sizeof(HeadRec), s));
-    HIPCHK(c, launch_bucket_hist(c->rkey32.p, n, invalid, shift, nb, nblk, c->bH.p, s));
+    HIPCHK(c, launch_bucket_hist(c->rkey32.p, n, invalid, shift, nb, nblk, c->bH.p, c->hcnt.p, s));
     ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->bH.p, c->bHs.p, 0u, (size_t)nb * nblk, rocprim::plus<uint32_t>(), s));
     HIPCHK(c, launch_bucket_scatter(c->rkey32.p, n, invalid, shift, nb, nblk, c->bHs.p, c->pkey16.p, c->ridx2.p, s));
-    HIPCHK(c, launch_bucket_heads(c->pkey16.p, c->ridx2.p, c->bHs.p, c->bH.p, nb, nblk, shift, c->hrec.p, s));
+    HIPCHK(c, launch_bucket_heads(c->pkey16.p, c->ridx2.p, c->bHs.p, c->bH.p, nb, nblk, shift, c->hcnt.p, s));
     return KMER_OK;
 }
 
 // resolve a deferred unique count (finish without a host result)
 kmer_status resolve_out(kmer_ctx *c) {
+    kmer_status st = resolve_feed_timing(c);
+    if (st) return st;
     if (c->out_pending) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
-        c->n_out = c->h_small[13];
+        c->n_out = c->h_tail[8];
         c->out_pending = false;
     }
     if (c->timing_pending) {
@@ -838,6 +907,7 @@ kmer_status rank_finish(kmer_ctx *c, uint64_t n, bool partial, bool with_counts,
     else HIPCHK(c, c->rkey2.ensure(n, s));
     HIPCHK(c, c->ridx2.ensure(n, s));
     HIPCHK(c, c->hrec.ensure(n, s));
+    HIPCHK(c, c->hcnt.ensure(n + 4, s));
     HIPCHK(c, c->opos.ensure(n, s));
     if (partial) {
         HIPCHK(c, c->ukey.ensure(n, s));
@@ -850,23 +920,27 @@ kmer_status rank_finish(kmer_ctx *c, uint64_t n, bool partial, bool with_counts,
     const uint64_t invalid = c->kbits >= 63 ? ~0ull : (1ull << c->kbits);
     kmer_status st;
     // (merged partials carry counts: the sort finish sums them in 64 bits)
-    if (c->narrow && c->kbits <= BKT_LOW + 11 && !with_counts && !(c->p.flags & KMER_FLAG_SORT_FINISH))
+    const bool bucket = c->narrow && c->kbits <= BKT_LOW + 11 && !with_counts && !(c->p.flags & KMER_FLAG_SORT_FINISH);
+    if (bucket)
         st = bucket_heads(c, n);
     else if (c->narrow)
         st = sort_and_heads<uint32_t>(c, c->rkey32.p, c->rkey32b.p, n, with_counts);
     else
         st = sort_and_heads<uint64_t>(c, c->rkey.p, c->rkey2.p, n, with_counts);
     if (st) return st;
-    auto is_head = rocprim::make_transform_iterator(c->hrec.p, IsHead());
+    auto is_head = rocprim::make_transform_iterator(c->hcnt.p, IsHead());
     ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, is_head, c->opos.p, 0u, (size_t)n, rocprim::plus<uint32_t>(), s));
     EmitArgs e;
     memset(&e, 0, sizeof(e));
-    e.hrec = c->hrec.p;
+    e.hcnt = c->hcnt.p;
+    e.hrec = bucket ? nullptr : c->hrec.p;
+    e.rkey32 = c->rkey32.p;
     e.opos = c->opos.p;
     e.rord = c->rord.p;
     e.n = n;
     e.invalid_key = invalid;
     e.nuniq = c->d_nuniq;
+    e.nuniq_host = c->d_tail + 8;
     e.k = c->p.k;
     e.plen = (uint32_t)c->prefix.size();
     e.partial = partial ? 1u : 0u;
@@ -877,13 +951,12 @@ kmer_status rank_finish(kmer_ctx *c, uint64_t n, bool partial, bool with_counts,
     e.ukey = c->ukey.p;
     e.uval = c->uval.p;
     HIPCHK(c, launch_emit(e, s));
-    HIPCHK(c, hipMemcpyAsync(c->h_small + 13, c->d_nuniq, 8, hipMemcpyDeviceToHost, s));
     if (!sync) {
         c->out_pending = true;
         return KMER_OK;
     }
     HIPCHK(c, hipStreamSynchronize(s));
-    *nu_out = c->h_small[13];
+    *nu_out = c->h_tail[8];
     return KMER_OK;
 }
 
@@ -935,6 +1008,8 @@ kmer_status build_result(kmer_ctx *c, uint64_t lines, kmer_result **out) {
 }
 
 kmer_status read_pos(kmer_ctx *c, StreamPos *pos) {
+    kmer_status st = flush_prep(c, c->stream, 0);
+    if (st) return st;
     HIPCHK(c, hipMemcpyAsync(c->h_small + 8, c->d_pos, sizeof(StreamPos), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     memcpy(pos, c->h_small + 8, sizeof(StreamPos));
@@ -1090,9 +1165,10 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
         if (ok) ok &= hipMemcpy(c->d_PR, pr.data(), pr.size(), hipMemcpyHostToDevice) == hipSuccess;
     }
     ok &= dalloc(&c->d_ticket, 4) == hipSuccess;
-    ok &= dalloc(&c->d_scal, 8) == hipSuccess;
+    ok &= dalloc(&c->d_scal, 16) == hipSuccess;
     if (ok) {
-        ok &= hipMemset(c->d_scal, 0, 64) == hipSuccess;
+        ok &= hipMemset(c->d_scal, 0, 128) == hipSuccess;
+        c->d_hticket = (unsigned int *)(c->d_scal + 8);
         c->d_rec_count = (unsigned long long *)(c->d_scal + 0);
         c->d_ovf_count = (unsigned long long *)(c->d_scal + 1);
         c->d_xcount = (unsigned long long *)(c->d_scal + 2);
@@ -1105,6 +1181,10 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
     ok &= dalloc(&c->d_pos, 1) == hipSuccess;
     ok &= dalloc(&c->d_pos_saved, 1) == hipSuccess;
     ok &= hipHostMalloc((void **)&c->h_small, 16 * sizeof(uint64_t), hipHostMallocDefault) == hipSuccess;
+    ok &= hipHostMalloc((void **)&c->h_tail, 16 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent) ==
+          hipSuccess;
+    ok &= c->h_tail && hipHostGetDevicePointer((void **)&c->d_tail, c->h_tail, 0) == hipSuccess;
+    if (c->h_tail) memset(c->h_tail, 0, 16 * sizeof(uint64_t));
     ok &= hipEventCreate(&c->ev0) == hipSuccess && hipEventCreate(&c->ev1) == hipSuccess &&
           hipEventCreate(&c->ev2) == hipSuccess && hipEventCreate(&c->ev3) == hipSuccess &&
           hipEventCreate(&c->ev4) == hipSuccess &&
@@ -1137,6 +1217,7 @@ kmer_status kmer_close(kmer_ctx *c) {
     c->bsum.release();
     c->bscan.release();
     c->hrec.release();
+    c->hcnt.release();
     c->tsum.release();
     c->tscan.release();
     c->hits.release();
@@ -1153,6 +1234,7 @@ kmer_status kmer_close(kmer_ctx *c) {
     dfree(c->d_ticket); dfree(c->d_scal); dfree(c->d_pos); dfree(c->d_pos_saved);
     dfree(c->d_P); dfree(c->d_PR);
     if (c->h_small) (void)hipHostFree(c->h_small);
+    if (c->h_tail) (void)hipHostFree(c->h_tail);
     for (hipEvent_t e : {c->ev0, c->ev1, c->ev2, c->ev3, c->ev4, c->evw})
         if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1419,7 +1501,8 @@ kmer_status kmer_records_clear(kmer_ctx *c) {
 kmer_status kmer_set_position(kmer_ctx *c, uint64_t lines_before, uint64_t byte_offset) {
     if (!c) return KMER_E_BAD_PARAM;
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
-    HIPCHK(c, launch_set_pos(c->d_pos, lines_before, c->stream));
+    c->prep_flags |= PREP_SETPOS;      // applied by the next feed's prologue (flush_prep)
+    c->prep_lines = lines_before;
     c->abs_offset = byte_offset;
     c->host_lines = lines_before;
     return KMER_OK;
@@ -1448,7 +1531,8 @@ kmer_status kmer_result_device(kmer_ctx *c, const void **d_keys, const void **d_
 
 kmer_status kmer_last_timing(kmer_ctx *c, double *scan_ms, double *feed_ms, double *finish_ms) {
     if (!c) return KMER_E_BAD_PARAM;
-    kmer_status st = resolve_out(c);
+    // (the finish is waited for only when its time is asked for)
+    kmer_status st = finish_ms ? resolve_out(c) : resolve_feed_timing(c);
     if (st) return st;
     if (scan_ms) *scan_ms = c->scan_ms;
     if (feed_ms) *feed_ms = c->feed_ms;

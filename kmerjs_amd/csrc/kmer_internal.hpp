@@ -156,6 +156,15 @@ struct HitArgs {
     unsigned long long *rec_count;
     uint64_t rec_cap;
     unsigned int *err;
+    // chunk tail (hit_overflow_kernel's last block): stream position update and
+    // the chunk's counters published to host memory
+    const uint8_t *data;
+    uint64_t len;
+    uint64_t *scal;                // device scalars [0..7] (see kmer_ctx::d_scal)
+    unsigned int *ticket;          // last-block ticket (returned to 0 by the last block)
+    unsigned long long *chunk_hits, *chunk_cross, *ends_open;
+    uint64_t *host_out;            // mapped host memory: copy of scal[0..7], then [9] = seq
+    uint64_t seq;                  // chunk sequence number (the host waits for it in host_out[9])
 };
 
 // By rank, after the key sort: the key and its total count if this rank is
@@ -167,12 +176,15 @@ struct HeadRec {
 
 // Ordered output from the rank arrays after the key sort.
 struct EmitArgs {
-    const HeadRec *hrec;           // by rank
-    const uint32_t *opos;          // exclusive scan of (count != 0): output position
+    const uint32_t *hcnt;          // by rank: != 0 iff the first occurrence of its key (bucket finish: the count)
+    const HeadRec *hrec;           // sort finish: by rank, key and count of heads (null: bucket finish)
+    const uint32_t *rkey32;        // bucket finish: key by rank
+    const uint32_t *opos;          // exclusive scan of (hcnt != 0): output position
     const uint64_t *rord;          // by rank: order key
     uint64_t n;
     uint64_t invalid_key;
     uint64_t *nuniq;
+    uint64_t *nuniq_host;          // mapped host copy of *nuniq (or null)
     uint32_t k, plen, partial;
     uint8_t P[32];
     uint8_t *keys_out;             // decode: n * k bytes
@@ -260,10 +272,9 @@ hipError_t launch_hits(const HitArgs &a, hipStream_t s);
 hipError_t launch_tile_reduce(const TileSum *in, uint32_t n, TileSum *bsum, hipStream_t s);
 hipError_t launch_tile_scan(const TileSum *in, uint32_t n, const TileSum *bsum, bool bsum_scanned, TileSum init,
                             TileSum *out, hipStream_t s);
-hipError_t launch_pos_update(StreamPos *pos, const TileSum *tsum, const TileSum *tscan, uint32_t n_tiles,
-                             const uint8_t *data, uint64_t len, unsigned long long *chunk_hits,
-                             unsigned long long *chunk_cross, unsigned long long *ends_open, hipStream_t s);
-hipError_t launch_set_pos(StreamPos *pos, uint64_t lines, hipStream_t s);
+enum : uint32_t { PREP_RESET = 1, PREP_SETPOS = 2, PREP_SAVE = 4, PREP_ZERO = 8 };
+hipError_t launch_prep(StreamPos *pos, StreamPos *saved, unsigned int *err, uint64_t *scal, uint32_t flags,
+                       uint64_t lines, hipStream_t s);
 hipError_t launch_tile_aggregate(const uint8_t *data, uint64_t len, uint32_t n_tiles, uint64_t *agg_cnt,
                                  uint64_t *agg_lnl, unsigned int *err, hipStream_t s);
 hipError_t launch_windows(const WindowArgs &a, uint32_t grid, hipStream_t s);
@@ -276,20 +287,20 @@ constexpr uint64_t XSMALL_MAX = 16384;   // cross lists up to this size: one-wor
 hipError_t launch_cross_segsort(uint64_t *ord, uint64_t *key, const uint32_t *slot, uint64_t n, uint64_t *rkey,
                                 uint32_t *rkey32, uint64_t *rord, hipStream_t s);
 hipError_t launch_heads(const uint64_t *skey, const uint32_t *srank, uint64_t n, uint64_t invalid_key,
-                        const uint64_t *rcnt, HeadRec *hrec, hipStream_t s);
+                        const uint64_t *rcnt, HeadRec *hrec, uint32_t *hcnt, hipStream_t s);
 hipError_t launch_heads32(const uint32_t *skey, const uint32_t *srank, uint64_t n, uint32_t invalid_key,
-                          const uint64_t *rcnt, HeadRec *hrec, hipStream_t s);
+                          const uint64_t *rcnt, HeadRec *hrec, uint32_t *hcnt, hipStream_t s);
 hipError_t launch_emit(const EmitArgs &a, hipStream_t s);
 // bucket finish (u32 keys of <= BKT_LOW + 11 bits)
 constexpr uint32_t BKT_LOW = 14;             // keys per bucket table: 2^14 (128 KiB of LDS: min rank, count)
 constexpr uint32_t BKT_MAX = 2048;           // buckets (keys of <= BKT_LOW + 11 bits)
 constexpr uint32_t BKT_EPB_HOST = 4096;      // elements per partition block (= BKT_EPB)
 hipError_t launch_bucket_hist(const uint32_t *key, uint64_t n, uint32_t invalid, uint32_t shift, uint32_t nb,
-                              uint32_t nblk, uint32_t *H, hipStream_t s);
+                              uint32_t nblk, uint32_t *H, uint32_t *hcnt, hipStream_t s);
 hipError_t launch_bucket_scatter(const uint32_t *key, uint64_t n, uint32_t invalid, uint32_t shift, uint32_t nb,
                                  uint32_t nblk, const uint32_t *Hs, uint16_t *pkey, uint32_t *prank, hipStream_t s);
 hipError_t launch_bucket_heads(const uint16_t *pkey, const uint32_t *prank, const uint32_t *Hs, const uint32_t *H,
-                               uint32_t nb, uint32_t nblk, uint32_t shift, HeadRec *hrec, hipStream_t s);
+                               uint32_t nb, uint32_t nblk, uint32_t shift, uint32_t *hcnt, hipStream_t s);
 // multi-GPU hit exchange (kmer_exchange_prepare / kmer_finish_exchanged)
 struct XHit {
     uint64_t ord;                  // first-occurrence order key

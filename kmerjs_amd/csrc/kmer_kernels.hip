@@ -1132,8 +1132,7 @@ __global__ __launch_bounds__(256) void hit_kernel(HitArgs a) {
 
 // hits that did not fit their tile's slots (their tile is all cross)
 __global__ __launch_bounds__(256) void hit_overflow_kernel(HitArgs a) {
-    if (*a.ovf_count > a.ovf_cap) return;
-    const uint64_t n = *a.ovf_count;
+    const uint64_t n = *a.ovf_count <= a.ovf_cap ? *a.ovf_count : 0;   // overflowed: the host redoes the chunk
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const HitRec r = a.ovf[i];
         const TileSum tb = a.tscan[r.tile];
@@ -1144,6 +1143,33 @@ __global__ __launch_bounds__(256) void hit_overflow_kernel(HitArgs a) {
         if (!a.packed) continue;
         const uint32_t ord = r.qm >> 17;
         place_hit(a, a.out_base + tb.nh + ord, true, a.xbase + tb.nx + ord, key, order);
+    }
+    // chunk tail, by the last block to finish (every hit of the chunk has read
+    // pos by then): advance the stream position past the chunk, publish the
+    // chunk's hit / cross counts and copy the counters to host memory
+    __shared__ bool last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd(a.ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last || threadIdx.x != 0) return;
+    __threadfence();
+    const uint32_t nt = a.n_tiles;
+    StreamPos *pos = (StreamPos *)a.pos;
+    pos->lines += a.tscan[nt - 1].cnt + a.tsum[nt - 1].cnt;
+    pos->ends_open = (a.len > 0 && a.data[a.len - 1] != '\n') ? 1 : 0;
+    *a.ends_open = pos->ends_open;
+    *a.chunk_hits = a.tscan[nt - 1].nh + a.tsum[nt - 1].nh;
+    *a.chunk_cross = a.tscan[nt - 1].nx + a.tsum[nt - 1].nx;
+    *a.ticket = 0;
+    __threadfence();
+    if (a.host_out) {
+        for (int i = 0; i < 8; ++i)
+            a.host_out[i] = __hip_atomic_load(a.scal + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __threadfence_system();
+        __hip_atomic_store(a.host_out + 9, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -1242,26 +1268,23 @@ __global__ __launch_bounds__(256) void tile_scan_kernel(const TileSum *in, uint3
 }
 
 // set the running stream position (kernel argument: no host staging, no sync)
-__global__ void set_pos_kernel(StreamPos *pos, uint64_t lines) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) {
-        pos->lines = lines;
-        pos->unused = 0;
-        pos->ends_open = 0;
-        pos->pad = 0;
+// Feed prologue: the lazy reset / set_position of the host API, the position
+// snapshot for an overflow redo, the chunk's counters -- one launch.
+__global__ void prep_kernel(StreamPos *pos, StreamPos *saved, unsigned int *err, uint64_t *scal, uint32_t flags,
+                            uint64_t lines) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    StreamPos p = *pos;
+    if (flags & PREP_RESET) {
+        p.lines = p.unused = p.ends_open = p.pad = 0;
+        *err = 0;
     }
-}
-
-// advance the running stream position past this chunk; hits of the chunk
-__global__ void pos_update_kernel(StreamPos *pos, const TileSum *tsum, const TileSum *tscan, uint32_t n_tiles,
-                                  const uint8_t *data, uint64_t len, unsigned long long *chunk_hits,
-                                  unsigned long long *chunk_cross, unsigned long long *ends_open) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) {   // (a redo after an overflow restores pos first)
-        pos->lines += tscan[n_tiles - 1].cnt + tsum[n_tiles - 1].cnt;
-        pos->ends_open = (len > 0 && data[len - 1] != '\n') ? 1 : 0;
-        *ends_open = pos->ends_open;
-        *chunk_hits = tscan[n_tiles - 1].nh + tsum[n_tiles - 1].nh;
-        *chunk_cross = tscan[n_tiles - 1].nx + tsum[n_tiles - 1].nx;
+    if (flags & PREP_SETPOS) {
+        p.lines = lines;
+        p.unused = p.ends_open = p.pad = 0;
     }
+    if (flags & (PREP_RESET | PREP_SETPOS)) *pos = p;
+    if (flags & PREP_SAVE) *saved = p;
+    if (flags & PREP_ZERO) scal[0] = scal[1] = scal[2] = 0;   // records, overflow hits, cross hits of the chunk
 }
 
 // Two-pass mode, pass 1: per-tile '\n' count and last '\n' position.
@@ -1678,7 +1701,7 @@ __device__ __forceinline__ uint64_t group_end(const K *skey, uint64_t i, uint64_
 // its record written (srank is a permutation), so no clearing pass is needed.
 template <typename K>
 __global__ __launch_bounds__(256) void heads_kernel(const K *skey, const uint32_t *srank, uint64_t n, K invalid_key,
-                                                    const uint64_t *rcnt, HeadRec *hrec) {
+                                                    const uint64_t *rcnt, HeadRec *hrec, uint32_t *hcnt) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const K k = skey[i];
         HeadRec v;
@@ -1694,7 +1717,9 @@ __global__ __launch_bounds__(256) void heads_kernel(const K *skey, const uint32_
             v.key = k;
             v.count = cnt;
         }
-        hrec[srank[i]] = v;
+        const uint32_t r = srank[i];
+        hrec[r] = v;
+        hcnt[r] = v.count ? 1u : 0u;
     }
 }
 
@@ -1709,11 +1734,17 @@ constexpr uint32_t BKT_EPB = 4096;           // elements per partition block
 
 __global__ __launch_bounds__(256) void bucket_hist_kernel(const uint32_t *key, uint64_t n, uint32_t invalid,
                                                           uint32_t shift, uint32_t nb, uint32_t nblk,
-                                                          uint32_t *H) {
+                                                          uint32_t *H, uint32_t *hcnt) {
     __shared__ uint32_t hist[BKT_MAX];
     for (uint32_t b = threadIdx.x; b < nb; b += 256) hist[b] = 0;
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * BKT_EPB;
+    // clear the head counts of this block's ranks (bucket_heads sets the heads')
+    for (uint32_t j = 4 * threadIdx.x; j < BKT_EPB; j += 4 * 256) {
+        const uint64_t i = base + j;
+        if (i + 4 <= n) *(uint4 *)(hcnt + i) = make_uint4(0, 0, 0, 0);
+        else for (uint64_t t = i; t < n; ++t) hcnt[t] = 0;
+    }
 #pragma unroll 4
     for (uint32_t j = threadIdx.x; j < BKT_EPB; j += 256) {
         const uint64_t i = base + j;
@@ -1787,7 +1818,7 @@ __global__ __launch_bounds__(256) void bucket_scatter_kernel(const uint32_t *key
 
 __global__ __launch_bounds__(1024) void bucket_heads_kernel(const uint16_t *pkey, const uint32_t *prank,
                                                             const uint32_t *Hs, const uint32_t *H, uint32_t nb,
-                                                            uint32_t nblk, uint32_t shift, HeadRec *hrec) {
+                                                            uint32_t nblk, uint32_t shift, uint32_t *hcnt) {
     __shared__ uint32_t minr[1u << BKT_LOW];
     __shared__ uint32_t cnt[1u << BKT_LOW];
     const uint32_t b = blockIdx.x, nk = 1u << shift;
@@ -1807,12 +1838,7 @@ __global__ __launch_bounds__(1024) void bucket_heads_kernel(const uint16_t *pkey
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < nk; j += blockDim.x) {
         const uint32_t c = cnt[j];
-        if (c) {
-            HeadRec v;
-            v.key = ((uint64_t)b << shift) | j;
-            v.count = c;
-            hrec[minr[j]] = v;
-        }
+        if (c) hcnt[minr[j]] = c;       // (the key is rkey32 at that rank)
     }
 }
 
@@ -1823,11 +1849,27 @@ __global__ __launch_bounds__(1024) void bucket_heads_kernel(const uint16_t *pkey
 __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
     const uint64_t n = a.n;
     for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
-        const HeadRec v = a.hrec[r];
+        const uint32_t hc = a.hcnt[r];
+        const uint32_t f = hc ? 1u : 0u;
+        if (r == n - 1) {
+            const uint64_t nu = (uint64_t)a.opos[r] + f;
+            *a.nuniq = nu;
+            if (a.nuniq_host) {
+                *a.nuniq_host = nu;
+                __threadfence_system();
+            }
+        }
+        if (!f) continue;
+        uint64_t key, cnt;
+        if (a.hrec) {
+            const HeadRec v = a.hrec[r];
+            key = v.key;
+            cnt = v.count;
+        } else {
+            key = a.rkey32[r];
+            cnt = hc;
+        }
         const uint32_t o = a.opos[r];
-        if (r == n - 1) *a.nuniq = (uint64_t)o + (v.count ? 1u : 0u);
-        if (!v.count) continue;
-        const uint64_t key = v.key, cnt = v.count;
         const uint64_t first = a.rord[r];
         if (a.partial) {
             a.ukey[o] = key;
@@ -2080,13 +2122,6 @@ hipError_t launch_hits(const HitArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_pos_update(StreamPos *pos, const TileSum *tsum, const TileSum *tscan, uint32_t n_tiles,
-                             const uint8_t *data, uint64_t len, unsigned long long *chunk_hits,
-                             unsigned long long *chunk_cross, unsigned long long *ends_open, hipStream_t s) {
-    hipLaunchKernelGGL(pos_update_kernel, dim3(1), dim3(64), 0, s, pos, tsum, tscan, n_tiles, data, len, chunk_hits,
-                       chunk_cross, ends_open);
-    return hipGetLastError();
-}
 hipError_t launch_tile_reduce(const TileSum *in, uint32_t n, TileSum *bsum, hipStream_t s) {
     hipLaunchKernelGGL(tile_reduce_kernel, dim3((n + TSCAN_BLOCK - 1) / TSCAN_BLOCK), dim3(256), 0, s, in, n, bsum);
     return hipGetLastError();
@@ -2097,8 +2132,9 @@ hipError_t launch_tile_scan(const TileSum *in, uint32_t n, const TileSum *bsum, 
                        bsum_scanned ? 1u : 0u, init, out);
     return hipGetLastError();
 }
-hipError_t launch_set_pos(StreamPos *pos, uint64_t lines, hipStream_t s) {
-    hipLaunchKernelGGL(set_pos_kernel, dim3(1), dim3(64), 0, s, pos, lines);
+hipError_t launch_prep(StreamPos *pos, StreamPos *saved, unsigned int *err, uint64_t *scal, uint32_t flags,
+                       uint64_t lines, hipStream_t s) {
+    hipLaunchKernelGGL(prep_kernel, dim3(1), dim3(64), 0, s, pos, saved, err, scal, flags, lines);
     return hipGetLastError();
 }
 hipError_t launch_tile_aggregate(const uint8_t *data, uint64_t len, uint32_t n_tiles, uint64_t *agg_cnt,
@@ -2138,22 +2174,22 @@ hipError_t launch_cross_segsort(uint64_t *ord, uint64_t *key, const uint32_t *sl
     return hipGetLastError();
 }
 hipError_t launch_heads(const uint64_t *skey, const uint32_t *srank, uint64_t n, uint64_t invalid_key,
-                        const uint64_t *rcnt, HeadRec *hrec, hipStream_t s) {
+                        const uint64_t *rcnt, HeadRec *hrec, uint32_t *hcnt, hipStream_t s) {
     if (n)
         hipLaunchKernelGGL(heads_kernel<uint64_t>, dim3(grid_for(n)), dim3(256), 0, s, skey, srank, n, invalid_key, rcnt,
-                           hrec);
+                           hrec, hcnt);
     return hipGetLastError();
 }
 hipError_t launch_heads32(const uint32_t *skey, const uint32_t *srank, uint64_t n, uint32_t invalid_key,
-                          const uint64_t *rcnt, HeadRec *hrec, hipStream_t s) {
+                          const uint64_t *rcnt, HeadRec *hrec, uint32_t *hcnt, hipStream_t s) {
     if (n)
         hipLaunchKernelGGL(heads_kernel<uint32_t>, dim3(grid_for(n)), dim3(256), 0, s, skey, srank, n, invalid_key, rcnt,
-                           hrec);
+                           hrec, hcnt);
     return hipGetLastError();
 }
 hipError_t launch_bucket_hist(const uint32_t *key, uint64_t n, uint32_t invalid, uint32_t shift, uint32_t nb,
-                              uint32_t nblk, uint32_t *H, hipStream_t s) {
-    hipLaunchKernelGGL(bucket_hist_kernel, dim3(nblk), dim3(256), 0, s, key, n, invalid, shift, nb, nblk, H);
+                              uint32_t nblk, uint32_t *H, uint32_t *hcnt, hipStream_t s) {
+    hipLaunchKernelGGL(bucket_hist_kernel, dim3(nblk), dim3(256), 0, s, key, n, invalid, shift, nb, nblk, H, hcnt);
     return hipGetLastError();
 }
 hipError_t launch_bucket_scatter(const uint32_t *key, uint64_t n, uint32_t invalid, uint32_t shift, uint32_t nb,
@@ -2163,8 +2199,8 @@ hipError_t launch_bucket_scatter(const uint32_t *key, uint64_t n, uint32_t inval
     return hipGetLastError();
 }
 hipError_t launch_bucket_heads(const uint16_t *pkey, const uint32_t *prank, const uint32_t *Hs, const uint32_t *H,
-                               uint32_t nb, uint32_t nblk, uint32_t shift, HeadRec *hrec, hipStream_t s) {
-    hipLaunchKernelGGL(bucket_heads_kernel, dim3(nb), dim3(1024), 0, s, pkey, prank, Hs, H, nb, nblk, shift, hrec);
+                               uint32_t nb, uint32_t nblk, uint32_t shift, uint32_t *hcnt, hipStream_t s) {
+    hipLaunchKernelGGL(bucket_heads_kernel, dim3(nb), dim3(1024), 0, s, pkey, prank, Hs, H, nb, nblk, shift, hcnt);
     return hipGetLastError();
 }
 hipError_t launch_emit(const EmitArgs &a, hipStream_t s) {
