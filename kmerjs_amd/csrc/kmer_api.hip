@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 #include <rocprim/iterator/transform_iterator.hpp>
 
 #include <algorithm>
@@ -837,16 +838,29 @@ kmer_status apply_cross(kmer_ctx *c) {
     return KMER_OK;
 }
 
-// stable radix sort of (key, rank), then one head record per rank
+// stable radix sort of (key, rank), then the heads.  Without per-entry
+// counts the by-rank keys are kept (the sort writes a copy), hcnt is
+// prefilled with 1 and only repeated / invalid keys are scattered
+// (heads_sparse); merged partials (with_counts) sum u64 counts into HeadRecs.
 template <typename K>
 kmer_status sort_and_heads(kmer_ctx *c, K *keys, K *keys2, uint64_t n, bool with_counts) {
     hipStream_t s = c->stream;
     const uint64_t invalid = c->kbits >= 63 ? ~0ull : (1ull << c->kbits);
+    const int end_bit = std::min<int>(8 * (int)sizeof(K), (int)c->kbits + 1);   // + the invalid-key bit
+    if (!with_counts) {
+        rocprim::counting_iterator<uint32_t> iota(0u);
+        ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, keys, keys2, iota, c->ridx2.p, (size_t)n, 0, end_bit, s));
+        HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)c->hcnt.p, 1, n, s));
+        if (sizeof(K) == 4)
+            HIPCHK(c, launch_heads_sparse(nullptr, (const uint32_t *)keys2, c->ridx2.p, n, invalid, c->hcnt.p, s));
+        else
+            HIPCHK(c, launch_heads_sparse((const uint64_t *)keys2, nullptr, c->ridx2.p, n, invalid, c->hcnt.p, s));
+        return KMER_OK;
+    }
     rocprim::double_buffer<K> kb(keys, keys2);
     rocprim::double_buffer<uint32_t> vb(c->ridx.p, c->ridx2.p);
-    const int end_bit = std::min<int>(8 * (int)sizeof(K), (int)c->kbits + 1);   // + the invalid-key bit
     ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, kb, vb, (size_t)n, 0, end_bit, s));
-    const uint64_t *rcnt = with_counts ? c->rcnt.p : nullptr;
+    const uint64_t *rcnt = c->rcnt.p;
     if (sizeof(K) == 4)
         HIPCHK(c, launch_heads32((const uint32_t *)kb.current(), vb.current(), n, (uint32_t)invalid, rcnt, c->hrec.p, c->hcnt.p, s));
     else
@@ -906,7 +920,7 @@ kmer_status rank_finish(kmer_ctx *c, uint64_t n, bool partial, bool with_counts,
     if (c->narrow) HIPCHK(c, c->rkey32b.ensure(n, s));
     else HIPCHK(c, c->rkey2.ensure(n, s));
     HIPCHK(c, c->ridx2.ensure(n, s));
-    HIPCHK(c, c->hrec.ensure(n, s));
+    if (with_counts) HIPCHK(c, c->hrec.ensure(n, s));
     HIPCHK(c, c->hcnt.ensure(n + 4, s));
     HIPCHK(c, c->opos.ensure(n, s));
     if (partial) {
@@ -933,8 +947,9 @@ kmer_status rank_finish(kmer_ctx *c, uint64_t n, bool partial, bool with_counts,
     EmitArgs e;
     memset(&e, 0, sizeof(e));
     e.hcnt = c->hcnt.p;
-    e.hrec = bucket ? nullptr : c->hrec.p;
-    e.rkey32 = c->rkey32.p;
+    e.hrec = with_counts ? c->hrec.p : nullptr;
+    e.rkey32 = c->narrow ? c->rkey32.p : nullptr;
+    e.rkey64 = c->narrow ? nullptr : c->rkey.p;
     e.opos = c->opos.p;
     e.rord = c->rord.p;
     e.n = n;

@@ -15,6 +15,7 @@ constexpr int BPT = 64;                  // bytes scanned per thread
 constexpr int TILE = TPB * BPT;          // 16384
 constexpr int FH = 64;                   // front halo bytes
 constexpr int BH = 80;                   // back halo bytes (>= KMAX_TILE - 1 + 3, x16)
+constexpr int KMAX_PACKED = 32;          // longest k of a 2-bit packed (u64) key
 constexpr int KMAX_TILE = 64;            // longest k handled by the tile kernel
 constexpr int KMAX_DENSE = 32;           // longest k packed into 2-bit codes
 constexpr uint32_t MAXREL = (1u << 23) - 1;  // longest sequence line (bytes - 1)
@@ -176,9 +177,10 @@ struct HeadRec {
 
 // Ordered output from the rank arrays after the key sort.
 struct EmitArgs {
-    const uint32_t *hcnt;          // by rank: != 0 iff the first occurrence of its key (bucket finish: the count)
-    const HeadRec *hrec;           // sort finish: by rank, key and count of heads (null: bucket finish)
-    const uint32_t *rkey32;        // bucket finish: key by rank
+    const uint32_t *hcnt;          // by rank: the key's count at its first occurrence, else 0
+    const HeadRec *hrec;           // merged finish (summed counts): by rank, key and u64 count of heads; else null
+    const uint32_t *rkey32;        // hrec == null: key by rank (narrow keys) ...
+    const uint64_t *rkey64;        // ... or (wide keys)
     const uint32_t *opos;          // exclusive scan of (hcnt != 0): output position
     const uint64_t *rord;          // by rank: order key
     uint64_t n;
@@ -288,6 +290,9 @@ hipError_t launch_cross_segsort(uint64_t *ord, uint64_t *key, const uint32_t *sl
                                 uint32_t *rkey32, uint64_t *rord, hipStream_t s);
 hipError_t launch_heads(const uint64_t *skey, const uint32_t *srank, uint64_t n, uint64_t invalid_key,
                         const uint64_t *rcnt, HeadRec *hrec, uint32_t *hcnt, hipStream_t s);
+// sort finish without per-entry counts: hcnt prefilled with 1, only groups of >= 2 and invalid keys written
+hipError_t launch_heads_sparse(const uint64_t *skey64, const uint32_t *skey32, const uint32_t *srank, uint64_t n,
+                               uint64_t invalid_key, uint32_t *hcnt, hipStream_t s);
 hipError_t launch_heads32(const uint32_t *skey, const uint32_t *srank, uint64_t n, uint32_t invalid_key,
                           const uint64_t *rcnt, HeadRec *hrec, uint32_t *hcnt, hipStream_t s);
 hipError_t launch_emit(const EmitArgs &a, hipStream_t s);

@@ -1723,6 +1723,25 @@ __global__ __launch_bounds__(256) void heads_kernel(const K *skey, const uint32_
     }
 }
 
+// Sort finish without per-entry counts: hcnt is prefilled with 1 (every rank
+// a singleton head), so only members of key groups of >= 2 and invalid keys
+// are scattered: the head (smallest rank, stable sort) gets the group size,
+// the others 0.  Where keys are mostly unique (k=31, no prefix) almost
+// nothing is written at random.
+template <typename K>
+__global__ __launch_bounds__(256) void heads_sparse_kernel(const K *skey, const uint32_t *srank, uint64_t n,
+                                                           K invalid_key, uint32_t *hcnt) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const K k = skey[i];
+        const bool dp = i > 0 && skey[i - 1] == k;
+        const bool dn = i + 1 < n && skey[i + 1] == k;
+        if (k != invalid_key && !dp && !dn) continue;
+        uint32_t v = 0;
+        if (k != invalid_key && !dp) v = (uint32_t)(group_end(skey, i, n, k) - i);
+        hcnt[srank[i]] = v;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Bucket finish (u32 keys of <= 24 bits): instead of sorting, partition the
 // ranked hits by key >> BKT_LOW into <= 2048 buckets (LDS-privatised
@@ -1847,63 +1866,98 @@ __global__ __launch_bounds__(1024) void bucket_heads_kernel(const uint16_t *pkey
 // count, first-occurrence order -- or the packed (code, {first, count}) pair
 // for a partial result.
 __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
+    // decoded keys of this block's heads, staged so that the block's output
+    // range [o0 * k, o_end * k) is written with coalesced dword stores
+    __shared__ __attribute__((aligned(16))) uint8_t kbuf[256 * KMAX_PACKED];
+    __shared__ uint32_t s_o0, s_oend;
     const uint64_t n = a.n;
-    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t hc = a.hcnt[r];
+    const uint32_t k = a.k, plen = a.plen;
+    for (uint64_t base = (uint64_t)blockIdx.x * 256; base < n; base += (uint64_t)gridDim.x * 256) {
+        const uint64_t r = base + threadIdx.x;
+        const uint64_t last = (base + 256 < n ? base + 256 : n) - 1;
+        uint32_t hc = 0, o = 0;
+        if (r < n) {
+            hc = a.hcnt[r];
+            o = a.opos[r];
+        }
         const uint32_t f = hc ? 1u : 0u;
-        if (r == n - 1) {
-            const uint64_t nu = (uint64_t)a.opos[r] + f;
-            *a.nuniq = nu;
-            if (a.nuniq_host) {
-                *a.nuniq_host = nu;
-                __threadfence_system();
+        if (threadIdx.x == 0) s_o0 = o;
+        if (r == last) {
+            s_oend = o + f;
+            if (r == n - 1) {
+                *a.nuniq = (uint64_t)o + f;
+                if (a.nuniq_host) {
+                    *a.nuniq_host = (uint64_t)o + f;
+                    __threadfence_system();
+                }
             }
         }
-        if (!f) continue;
-        uint64_t key, cnt;
-        if (a.hrec) {
-            const HeadRec v = a.hrec[r];
-            key = v.key;
-            cnt = v.count;
-        } else {
-            key = a.rkey32[r];
-            cnt = hc;
-        }
-        const uint32_t o = a.opos[r];
-        const uint64_t first = a.rord[r];
-        if (a.partial) {
-            a.ukey[o] = key;
-            Agg v;
-            v.first = first;
-            v.count = cnt;
-            a.uval[o] = v;
-            continue;
-        }
-        a.cnt_out[o] = cnt;
-        a.first_out[o] = first;
-        const uint32_t k = a.k, plen = a.plen;
-        uint8_t *out = a.keys_out + (uint64_t)o * k;
-        uint32_t words[8];
-#pragma unroll
-        for (int w = 0; w < 8; ++w) {
-            uint32_t v = 0;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t pos = 4 * w + j;
-                uint32_t ch = 0;
-                if (pos < plen) ch = a.P[pos];
-                else if (pos < k) ch = (0x54474341u >> (8 * ((uint32_t)(key >> (2 * (k - 1 - pos))) & 3u))) & 0xFFu;
-                v |= ch << (8 * j);
+        __syncthreads();
+        const uint32_t o0 = s_o0, oend = s_oend;
+        if (f) {
+            uint64_t key, cnt;
+            if (a.hrec) {
+                const HeadRec v = a.hrec[r];
+                key = v.key;
+                cnt = v.count;
+            } else {
+                key = a.rkey32 ? (uint64_t)a.rkey32[r] : a.rkey64[r];
+                cnt = hc;
             }
-            words[w] = v;
+            const uint64_t first = a.rord[r];
+            if (a.partial) {
+                a.ukey[o] = key;
+                Agg v;
+                v.first = first;
+                v.count = cnt;
+                a.uval[o] = v;
+            } else {
+                a.cnt_out[o] = cnt;
+                a.first_out[o] = first;
+                uint8_t *out = kbuf + (o - o0) * k;
+                uint32_t words[8];
+#pragma unroll
+                for (int w = 0; w < 8; ++w) {
+                    uint32_t v = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t pos = 4 * w + j;
+                        uint32_t ch = 0;
+                        if (pos < plen) ch = a.P[pos];
+                        else if (pos < k)
+                            ch = (0x54474341u >> (8 * ((uint32_t)(key >> (2 * (k - 1 - pos))) & 3u))) & 0xFFu;
+                        v |= ch << (8 * j);
+                    }
+                    words[w] = v;
+                }
+                if (k == 16) {
+                    *(uint4 *)out = make_uint4(words[0], words[1], words[2], words[3]);
+                } else if ((k & 3) == 0) {
+                    for (uint32_t w = 0; w < k / 4; ++w) *(uint32_t *)(out + 4 * w) = words[w];
+                } else {
+                    for (uint32_t b = 0; b < k; ++b) out[b] = (uint8_t)(words[b >> 2] >> (8 * (b & 3)));
+                }
+            }
         }
-        if (k == 16) {
-            *(uint4 *)out = make_uint4(words[0], words[1], words[2], words[3]);
-        } else if ((k & 3) == 0) {
-            for (uint32_t w = 0; w < k / 4; ++w) *(uint32_t *)(out + 4 * w) = words[w];
+        if (a.partial) continue;      // (uniform: no barrier skipped by part of the block)
+        __syncthreads();
+        const uint64_t g0 = (uint64_t)o0 * k, g1 = (uint64_t)oend * k;
+        const uint64_t a0 = (g0 + 3) & ~3ull, a1 = g1 & ~3ull;
+        if (a0 >= a1) {
+            for (uint64_t g = g0 + threadIdx.x; g < g1; g += 256) a.keys_out[g] = kbuf[g - g0];
         } else {
-            for (uint32_t b = 0; b < k; ++b) out[b] = (uint8_t)(words[b >> 2] >> (8 * (b & 3)));
+            if (threadIdx.x < a0 - g0) a.keys_out[g0 + threadIdx.x] = kbuf[threadIdx.x];
+            if (threadIdx.x < g1 - a1) a.keys_out[a1 + threadIdx.x] = kbuf[a1 - g0 + threadIdx.x];
+            const uint32_t sh = (uint32_t)(a0 - g0);
+            for (uint64_t g = a0 + 4 * threadIdx.x; g < a1; g += 4 * 256) {
+                const uint32_t l = (uint32_t)(g - g0);
+                const uint32_t v = sh == 0 ? *(const uint32_t *)(kbuf + l)
+                                           : (uint32_t)kbuf[l] | ((uint32_t)kbuf[l + 1] << 8) |
+                                                 ((uint32_t)kbuf[l + 2] << 16) | ((uint32_t)kbuf[l + 3] << 24);
+                *(uint32_t *)(a.keys_out + g) = v;
+            }
         }
+        __syncthreads();              // kbuf / s_o0 are reused by the next range
     }
 }
 
@@ -2178,6 +2232,17 @@ hipError_t launch_heads(const uint64_t *skey, const uint32_t *srank, uint64_t n,
     if (n)
         hipLaunchKernelGGL(heads_kernel<uint64_t>, dim3(grid_for(n)), dim3(256), 0, s, skey, srank, n, invalid_key, rcnt,
                            hrec, hcnt);
+    return hipGetLastError();
+}
+hipError_t launch_heads_sparse(const uint64_t *skey64, const uint32_t *skey32, const uint32_t *srank, uint64_t n,
+                               uint64_t invalid_key, uint32_t *hcnt, hipStream_t s) {
+    if (!n) return hipSuccess;
+    if (skey32)
+        hipLaunchKernelGGL(heads_sparse_kernel<uint32_t>, dim3(grid_for(n)), dim3(256), 0, s, skey32, srank, n,
+                           (uint32_t)invalid_key, hcnt);
+    else
+        hipLaunchKernelGGL(heads_sparse_kernel<uint64_t>, dim3(grid_for(n)), dim3(256), 0, s, skey64, srank, n,
+                           invalid_key, hcnt);
     return hipGetLastError();
 }
 hipError_t launch_heads32(const uint32_t *skey, const uint32_t *srank, uint64_t n, uint32_t invalid_key,
