@@ -374,7 +374,7 @@ __global__ __launch_bounds__(TPB) void lines_kernel(TileArgs a) {
 // ---------------------------------------------------------------------------
 constexpr int QCAP = 256;
 
-struct ScanShared {
+struct alignas(16) ScanShared {
     uint16_t cpre[NCH_MAIN];     // exclusive '\n' count per 16-byte chunk inside the tile
     uint32_t nlmap[NCH_MAIN / 32];   // bit c: chunk c holds a real '\n' 
     uint32_t wsum[TPB / 64][4];  // per-wave totals of the four packed chunk columns
@@ -384,7 +384,7 @@ struct ScanShared {
     uint32_t nx;                 // ... of which on lines that cross a tile edge
     uint32_t tcnt;               // real '\n' count of the tile
     uint32_t qn;                 // verified-hit queue fill
-    uint32_t q[QCAP];            // candidate words: tile position of the word's first window
+    alignas(8) uint32_t q[QCAP]; // candidate words (byte kernel) / QCAP/2 {entry, mask} pairs (plane kernel)
 };
 
 // last '\n' (tile-relative) inside 16-byte chunk c at a position < limit, -1 if none
@@ -431,15 +431,28 @@ __device__ __forceinline__ void emit_hit(const ScanArgs &a, const uint8_t *buf, 
                             ((c >> 24) & 3u);                // first byte most significant
         code = (code << (2 * nb)) | (pk >> (2 * (4 - nb)));
     }
-    if (hasnl) return;            // crosses a line end (or the end of input)
-    if (k == 1 && buf[FH + s0 - 1] == '\n' && buf[FH + s0 + 1] == '\n') return;   // line.length > 1
+    // crosses a line end (or the end of input); k == 1: line.length > 1
+    const bool valid = !hasnl && !(k == 1 && buf[FH + s0 - 1] == '\n' && buf[FH + s0 + 1] == '\n');
     // tile-local line context of the window start: '\n' count before s0 and
-    // the start of its line if that lies inside this tile
+    // the start of its line if that lies inside this tile.  The reads that
+    // only depend on s0 (chunk, cpre of its region, region bitmap word) go
+    // out together; at most two more dependent rounds follow.
     uint32_t c_local = 0;
     int lstart = -1;
-    if (s0 > 0) {
+    if (valid && s0 > 0) {
         const int cs = (s0 - 1) >> 4;               // chunk holding byte s0-1
         const uint4 x4 = *(const uint4 *)(buf + FH + 16 * cs);
+        uint32_t cp[4] = {0, 0, 0, 0};              // THREAD_MAP: cpre of cs's 64-byte region
+        uint32_t mw = 0;
+        const int rb = cs & ~3;
+        if (THREAD_MAP) {
+            const uint2 c2 = *(const uint2 *)(sh.cpre + rb);
+            cp[0] = c2.x & 0xFFFFu;
+            cp[1] = c2.x >> 16;
+            cp[2] = c2.y & 0xFFFFu;
+            cp[3] = c2.y >> 16;
+            if (rb > 0) mw = sh.nlmap[((rb >> 2) - 1) >> 5];
+        }
         const uint32_t xs[4] = {x4.x, x4.y, x4.z, x4.w};
         uint32_t cnt = 0;
         int last = -1;
@@ -452,24 +465,29 @@ __device__ __forceinline__ void emit_hit(const ScanArgs &a, const uint8_t *buf, 
             cnt += __popc(z);
             last = z ? pos + ((31 - __clz(z)) >> 3) : last;
         }
-        c_local = sh.cpre[cs] + cnt;
+        const uint32_t ccs = THREAD_MAP ? cp[cs - rb] : (uint32_t)sh.cpre[cs];
+        c_local = ccs + cnt;
         if (last >= 0) {
             lstart = last + 1;
         } else if (c_local > 0) {
             // the line started in the last earlier chunk that holds a '\n'
-            int c;
+            int c = -1;
             if (THREAD_MAP) {
-                // inside cs's 64-byte region first (chunk c holds a '\n' iff cpre[c+1] > cpre[c])
-                c = cs - 1;
-                const int rb = cs & ~3;
-                while (c >= rb && sh.cpre[c + 1] == sh.cpre[c]) --c;
-                if (c < rb) {
-                    const int rr = (cs >> 2) - 1;        // earlier regions: region bitmap
+                // inside cs's region first: chunk rb + j holds a '\n' iff cpre rises after it
+                if (ccs > cp[0]) {
+#pragma unroll
+                    for (int j = 2; j >= 0; --j)
+                        if (c < 0 && rb + j < cs && cp[j] < ccs) c = rb + j;
+                } else {
+                    const int rr = (rb >> 2) - 1;        // earlier regions: region bitmap
                     int wi = rr >> 5;
-                    uint32_t m = sh.nlmap[wi] & (0xFFFFFFFFu >> (31 - (rr & 31)));
+                    uint32_t m = mw & (0xFFFFFFFFu >> (31 - (rr & 31)));
                     while (m == 0) m = sh.nlmap[--wi];
-                    c = 4 * (32 * wi + 31 - __clz(m)) + 3;
-                    while (sh.cpre[c + 1] == sh.cpre[c]) --c;   // (c + 1 <= cs - 1 here)
+                    const int rg = 4 * (32 * wi + 31 - __clz(m));
+                    const uint2 d2 = *(const uint2 *)(sh.cpre + rg);
+                    const uint32_t nxt = sh.cpre[rg + 4];      // (rg + 4 <= rb <= cs)
+                    const uint32_t d[4] = {d2.x & 0xFFFFu, d2.x >> 16, d2.y & 0xFFFFu, d2.y >> 16};
+                    c = d[3] < nxt ? rg + 3 : d[2] < d[3] ? rg + 2 : d[1] < d[2] ? rg + 1 : rg;
                 }
             } else {
                 const int cc = cs - 1;               // chunk bitmap
@@ -481,17 +499,26 @@ __device__ __forceinline__ void emit_hit(const ScanArgs &a, const uint8_t *buf, 
             lstart = last_newline_in_chunk(buf, c) + 1;
         }
     }
+    // slots and the cross count: one LDS atomic per wave, not per hit.  The
+    // hit kernel ranks hits of lines inside the tile; lines that cross a tile
+    // edge are placed at finish (same predicate there).
+    const bool cross = valid && (lstart < 0 || c_local == sh.tcnt);
+    const unsigned long long vm = __ballot(valid), xm = __ballot(cross), act = __ballot(1);
+    const int lane = threadIdx.x & 63, leader = __ffsll((long long)act) - 1;
+    uint32_t base = 0;
+    if (lane == leader) {
+        if (vm) base = atomicAdd(&sh.nh, (uint32_t)__popcll(vm));
+        if (xm) atomicAdd(&sh.nx, (uint32_t)__popcll(xm));
+    }
+    base = (uint32_t)__shfl((int)base, leader);
+    if (!valid) return;
+    const uint32_t slot = base + (uint32_t)__popcll(vm & ((1ull << lane) - 1ull));   // < 2 * TILE: fits qm[31:17]
     HitRec r;
     r.code = code;
     r.tile = tile;
-    r.qm = (uint32_t)q | (strand << 14) | ((exotic ? 1u : 0u) << 15) | ((lstart >= 0 ? 1u : 0u) << 16);
+    r.qm = (uint32_t)q | (strand << 14) | ((exotic ? 1u : 0u) << 15) | ((lstart >= 0 ? 1u : 0u) << 16) | (slot << 17);
     r.c_local = c_local;
     r.lstart = lstart >= 0 ? (uint32_t)lstart : 0u;
-    const uint32_t slot = atomicAdd(&sh.nh, 1u);     // < 2 * TILE: fits qm[31:17]
-    r.qm |= slot << 17;
-    // the hit kernel ranks hits of lines inside the tile; lines that cross a
-    // tile edge are placed at finish (same predicate there)
-    if (lstart < 0 || c_local == sh.tcnt) atomicAdd(&sh.nx, 1u);
     if (slot < HMAX) {
         a.hits[(uint64_t)tile * HMAX + slot] = r;
     } else {
@@ -930,35 +957,61 @@ __global__ __launch_bounds__(TPB) void scan_planes_kernel(ScanArgs a, PlaneArgs 
         a.tsum[tile].lnl = lp >= 0 ? a.abs_offset + (uint64_t)(g0 + lp + 1) : 0;
     }
 
-    // ---- candidates -> LDS queue (one LDS atomic per wave) ----
+    // ---- candidates -> LDS queue: one {first window, mask} entry per nonzero
+    //      32-position mask (ballot + mbcnt, one LDS atomic per wave); the
+    //      rare, branchy verification runs once per tile in as few waves as
+    //      possible ----
     const uint32_t *pw = (const uint32_t *)s_pr;
+    uint2 *qe = (uint2 *)sh.q;
+    constexpr uint32_t QE = QCAP / 2;
     {
-        const uint32_t nc = __popc(mf[0]) + __popc(mf[1]) + __popc(mr[0]) + __popc(mr[1]);
-        const uint32_t incl_c = wave_incl_sum(nc);
-        const uint32_t wtotal = (uint32_t)__builtin_amdgcn_readlane((int)incl_c, 63);
-        if (wtotal) {
+        const uint32_t mm[4] = {mf[0], mf[1], mr[0], mr[1]};
+        unsigned long long bl[4];
+        uint32_t tot = 0;
+#pragma unroll
+        for (int hs = 0; hs < 4; ++hs) {
+            bl[hs] = __ballot(mm[hs] != 0);
+            tot += (uint32_t)__popcll(bl[hs]);
+        }
+        if (tot) {
             uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(&sh.qn, wtotal);
-            uint32_t pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)__shfl((int)base, 0)) + incl_c - nc;
+            if (lane == 0) base = atomicAdd(&sh.qn, tot);
+            base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
 #pragma unroll
             for (int hs = 0; hs < 4; ++hs) {
-                uint32_t m = hs == 0 ? mf[0] : hs == 1 ? mf[1] : hs == 2 ? mr[0] : mr[1];
-                while (m) {
-                    const uint32_t bit = __ffs(m) - 1;
-                    m &= m - 1;
-                    const uint32_t q = 64u * (uint32_t)tid + 32u * (uint32_t)(hs & 1) + bit;
-                    const uint32_t e = (q << 1) | (uint32_t)(hs >> 1);
-                    if (pos < QCAP) sh.q[pos] = e;
-                    else verify_emit(a, buf, sh, tile, pw, e);   // queue full: process in place
-                    ++pos;
+                if (bl[hs]) {
+                    if (mm[hs]) {
+                        const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(bl[hs] >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)bl[hs], 0u));
+                        const uint32_t e0 = ((64u * (uint32_t)tid + 32u * (uint32_t)(hs & 1)) << 1) | (uint32_t)(hs >> 1);
+                        if (pos < QE) {
+                            qe[pos] = make_uint2(e0, mm[hs]);
+                        } else {                 // queue full: process in place
+                            uint32_t m = mm[hs];
+                            while (m) {
+                                const uint32_t bit = __ffs(m) - 1;
+                                m &= m - 1;
+                                verify_emit(a, buf, sh, tile, pw, e0 + (bit << 1));
+                            }
+                        }
+                    }
+                    base += (uint32_t)__popcll(bl[hs]);
                 }
             }
         }
     }
     __syncthreads();
-    const uint32_t nq = min(sh.qn, (uint32_t)QCAP);
-    for (uint32_t h = tid; h < nq; h += TPB) verify_emit(a, buf, sh, tile, pw, sh.q[h]);
-    if (nq > 64 || sh.qn > QCAP) {
+    const uint32_t nq = min(sh.qn, QE);
+    for (uint32_t h = tid; h < nq; h += TPB) {
+        const uint2 en = qe[h];
+        uint32_t m = en.y;
+        while (m) {
+            const uint32_t bit = __ffs(m) - 1;
+            m &= m - 1;
+            verify_emit(a, buf, sh, tile, pw, en.x + (bit << 1));
+        }
+    }
+    if (nq > 64 || sh.qn > QE) {
         __syncthreads();
         if (tid == 0) {
             a.tsum[tile].nh = sh.nh;
@@ -1872,6 +1925,7 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
     __shared__ uint32_t s_o0, s_oend;
     const uint64_t n = a.n;
     const uint32_t k = a.k, plen = a.plen;
+    const bool staged = !a.partial && (k & 3);     // else: aligned direct stores
     for (uint64_t base = (uint64_t)blockIdx.x * 256; base < n; base += (uint64_t)gridDim.x * 256) {
         const uint64_t r = base + threadIdx.x;
         const uint64_t last = (base + 256 < n ? base + 256 : n) - 1;
@@ -1881,18 +1935,18 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
             o = a.opos[r];
         }
         const uint32_t f = hc ? 1u : 0u;
-        if (threadIdx.x == 0) s_o0 = o;
-        if (r == last) {
-            s_oend = o + f;
-            if (r == n - 1) {
-                *a.nuniq = (uint64_t)o + f;
-                if (a.nuniq_host) {
-                    *a.nuniq_host = (uint64_t)o + f;
-                    __threadfence_system();
-                }
+        if (r == n - 1) {
+            *a.nuniq = (uint64_t)o + f;
+            if (a.nuniq_host) {
+                *a.nuniq_host = (uint64_t)o + f;
+                __threadfence_system();
             }
         }
-        __syncthreads();
+        if (staged) {
+            if (threadIdx.x == 0) s_o0 = o;
+            if (r == last) s_oend = o + f;
+            __syncthreads();
+        }
         const uint32_t o0 = s_o0, oend = s_oend;
         if (f) {
             uint64_t key, cnt;
@@ -1914,7 +1968,7 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
             } else {
                 a.cnt_out[o] = cnt;
                 a.first_out[o] = first;
-                uint8_t *out = kbuf + (o - o0) * k;
+                uint8_t *out = staged ? kbuf + (o - o0) * k : a.keys_out + (uint64_t)o * k;
                 uint32_t words[8];
 #pragma unroll
                 for (int w = 0; w < 8; ++w) {
@@ -1939,7 +1993,7 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
                 }
             }
         }
-        if (a.partial) continue;      // (uniform: no barrier skipped by part of the block)
+        if (!staged) continue;        // (uniform: no barrier skipped by part of the block)
         __syncthreads();
         const uint64_t g0 = (uint64_t)o0 * k, g1 = (uint64_t)oend * k;
         const uint64_t a0 = (g0 + 3) & ~3ull, a1 = g1 & ~3ull;
