@@ -153,6 +153,8 @@ def main():
     ap.add_argument("--flags", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="sessions in rotation (>= 2: a step's finish overlaps the next steps' scans)")
     ap.add_argument("--config", default="c2", choices=("c1", "c2", "c3", "c5"),
                     help="BASELINE.json config: c2 (default, the headline), c3 no-prefix k=31, c5 long contigs k=21")
     ap.add_argument("--contig-bytes", type=int, default=1_000_000_000, help="c5: bytes of contigs per GPU")
@@ -201,43 +203,64 @@ def main():
     buf, nbytes = wl["buf"], wl["nbytes"]
     plan = {"lines_before": wl["lines_before"], "byte_offset": wl["byte_offset"]}
 
-    ctr = Counter(k=args.k, prefix=prefix, device=local, flags=args.flags)
+    # --pipeline N (N >= 2): N sessions in rotation.  Step i's chunk is queued
+    # (kmer_feed_device returns without waiting), then the oldest session in
+    # flight is settled and its finish queued on its high-priority stream, so
+    # finishes (chains of small latency-bound kernels) overlap the following
+    # scans instead of idling the chip.  Every step still does all of its work
+    # inside the timed region: the sessions in flight are drained before the
+    # clock stops.  Default: one session, steps strictly in sequence.
+    nctx = max(1, args.pipeline)
+    ctrs = [Counter(k=args.k, prefix=prefix, device=local, flags=args.flags) for _ in range(nctx)]
+    ctr = ctrs[0]
     total_lines = wl["total_lines"]
     tile_ms, feed_ms_l = [], []
+    inflight = []                 # (session, recorded) fed, finish not yet queued
 
-    recorded = [False]
+    def feed(c):
+        c.reset()
+        c.set_position(plan["lines_before"], plan["byte_offset"])
+        c.feed_device(buf.data_ptr(), nbytes)
 
-    def step(record):
-        if recorded[0]:
-            # kernel times of the previous step's feed (read now: the feed's host
-            # wait returns before its closing event; the finish is not waited for)
-            scan_ms, feed_ms, _ = ctr.last_timing(finish=False)
+    def retire():
+        c, rec = inflight.pop(0)
+        c.sync()                  # its scan is done: chunk counters read back
+        if rec:
+            scan_ms, feed_ms, _ = c.last_timing(finish=False)
             tile_ms.append(scan_ms)
             feed_ms_l.append(feed_ms)
-        recorded[0] = record
-        ctr.reset()
-        ctr.set_position(plan["lines_before"], plan["byte_offset"])
-        ctr.feed_device(buf.data_ptr(), nbytes)
-        multi_finish()
+        multi_finish(c)
 
-    def multi_finish():
+    def step(i, record):
+        feed(ctrs[i % nctx])      # (its previous finish is ahead of it on its stream)
+        inflight.append((ctrs[i % nctx], record))
+        while len(inflight) > nctx - 1:
+            retire()
+
+    def drain():
+        while inflight:
+            retire()
+
+    def multi_finish(c):
         if world == 1:
-            ctr.finish(want_result=False)
+            c.finish(want_result=False)
         elif args.merge == "hits":
-            finish_exchange(ctr, args.k, len(prefix), total_lines)
+            finish_exchange(c, args.k, len(prefix), total_lines)
         elif args.merge == "alltoall":
-            finish_distributed(ctr, args.k, len(prefix), total_lines)
+            finish_distributed(c, args.k, len(prefix), total_lines)
         else:
-            merge_to(ctr, args.k, len(prefix), total_lines, dst=0, want_result=False)
+            merge_to(c, args.k, len(prefix), total_lines, dst=0, want_result=False)
 
-    for _ in range(args.warmup):
-        step(False)
+    for i in range(args.warmup):
+        step(i, False)
+    drain()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
+    for i in range(args.steps):
+        step(i, True)
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -248,12 +271,9 @@ def main():
         elapsed = float(t.item())
 
     # one more pass to read the result size / accepted windows (outside the timed region)
-    step(False)
-    ctr.reset()
-    ctr.set_position(plan["lines_before"], plan["byte_offset"])
-    ctr.feed_device(buf.data_ptr(), nbytes)
+    feed(ctr)
     distinct, accepted = 0, 0
-    multi_finish()
+    multi_finish(ctr)
     # counted on the device (a C3-sized result has ~10^9 entries): ordered device
     # entries (every rank's key range after the all-to-all, or all on rank 0) +
     # the host-side records (non-ACGT windows, on rank 0)
@@ -316,7 +336,10 @@ def main():
             "config": {"workload": wl["desc"], "name": args.config,
                        "reads_per_gpu": args.reads if args.config in ("c2", "c3") else None,
                        "k": args.k, "prefix": args.prefix, "windows_per_step": windows_step,
-                       "bytes_per_gpu": nbytes, "parallelism": "dp%d (reads sharded; %s)" % (
+                       "bytes_per_gpu": nbytes,
+                       "pipeline": ("%d sessions in rotation: finishes overlap later scans" % nctx if nctx > 1
+                                    else "off (steps in sequence)"),
+                       "parallelism": "dp%d (reads sharded; %s)" % (
                            world, {"hits": "RCCL all-to-all of hits by key range, per-rank finish",
                         "alltoall": "RCCL all-to-all of partials by key range, per-rank finish"}.get(
                             args.merge, "RCCL gather of partials, finish on rank 0"))},
@@ -344,7 +367,8 @@ def main():
         if not args.no_cpu_baseline and world == 1 and args.config == "c2":
             out["cpu_baseline"] = cpu_baseline(args.k, prefix)
         print(json.dumps(out), flush=True)
-    ctr.close()
+    for c in ctrs:
+        c.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -91,6 +91,15 @@ kmer_status kmer_count_buffer(kmer_ctx *ctx, const uint8_t *bytes, size_t len, k
 kmer_status kmer_reset(kmer_ctx *ctx);
 kmer_status kmer_feed_device(kmer_ctx *ctx, const void *d_bytes, size_t len, void *stream);
 kmer_status kmer_finish_device(kmer_ctx *ctx, kmer_result **out);
+/* kmer_feed_device returns once the chunk is queued on the context's stream
+ * (packed paths); the chunk is settled -- its counters read back, an overflow
+ * of the hit lists redone, its errors reported -- by the next call on the
+ * context, or explicitly by kmer_sync.  The bytes must stay valid and
+ * unchanged until then.  While a chunk is in flight the caller may queue
+ * work on other contexts (e.g. another session's finish), which then
+ * overlaps the scan on the device.  (lib/kmers.js:148-171 reads the stream
+ * chunk by chunk; errors surface at the next call instead of the feed.) */
+kmer_status kmer_sync(kmer_ctx *ctx);
 
 /* Multi-GPU merge.  kmer_partial_device reduces this context's session to its
  * unique packed keys: keys = uint64[n] 2-bit suffix codes (the k-|P| bases

@@ -18,7 +18,7 @@ FLAG_BYTE_SCAN = 4
 FLAG_SORT_FINISH = 8
 
 # every symbol the header declares (tests/test_abi.py checks header <-> library)
-EXPORTS = ["kmer_open", "kmer_close", "kmer_count_file", "kmer_count_buffer", "kmer_reset",
+EXPORTS = ["kmer_open", "kmer_close", "kmer_count_file", "kmer_count_buffer", "kmer_reset", "kmer_sync",
            "kmer_feed_device", "kmer_finish_device", "kmer_partial_device", "kmer_finish_merged",
            "kmer_exchange_prepare", "kmer_finish_exchanged",
            "kmer_records_export", "kmer_records_import", "kmer_records_clear", "kmer_result_device", "kmer_set_position",
@@ -60,6 +60,7 @@ def _load():
         "kmer_count_file": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.POINTER(vp)]),
         "kmer_count_buffer": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(vp)]),
         "kmer_reset": (ctypes.c_int, [vp]),
+        "kmer_sync": (ctypes.c_int, [vp]),
         "kmer_feed_device": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp]),
         "kmer_finish_device": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
         "kmer_partial_device": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), pu64]),
@@ -191,6 +192,10 @@ class Counter:
     # ---- device-resident streaming ----
     def reset(self):
         self._check(LIB.kmer_reset(self.h), "reset")
+
+    def sync(self):
+        """Settle the chunk in flight (feed_device returns once it is queued)."""
+        self._check(LIB.kmer_sync(self.h), "sync")
 
     def set_position(self, lines_before, byte_offset):
         self._check(LIB.kmer_set_position(self.h, lines_before, byte_offset), "set_position")

@@ -93,7 +93,9 @@ struct kmer_ctx {
     std::string prefix, rprefix;
     Mode mode = MODE_GENERAL;
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;  // high priority: finish, exchange, copies, everything but the scan chain
+    hipStream_t sstream = nullptr; // low priority: a packed-path chunk (scan, tile scan, hit resolution)
+    hipEvent_t evq = nullptr;      // orders sstream after stream
     std::string err;
     uint32_t kbits = 0;            // packed key bits = 2*(k - |P|)
 
@@ -162,6 +164,18 @@ struct kmer_ctx {
     uint64_t tail_seq = 0;         // last chunk sequence number handed to the chunk tail kernel
     bool feed_timing_pending = false;   // scan / feed events of the last chunk not yet read
     uint32_t prep_flags = 0;       // PREP_RESET / PREP_SETPOS pending for the next feed's prologue
+    // the last packed-path chunk, launched but not yet settled (its tail read,
+    // overflows redone, counters applied): settle() before any other use
+    struct Pending {
+        bool active = false;
+        ScanArgs a;
+        HitArgs h;
+        uint32_t n_tiles = 0, n_blocks = 0;
+        TileSum init;
+        const uint8_t *d = nullptr;
+        uint64_t len = 0;
+        hipStream_t s = nullptr;
+    } pend;
     uint64_t prep_lines = 0;
     DBuf<uint8_t> batch;
     // timing (HIP events on the context stream)
@@ -291,12 +305,12 @@ kmer_status drain_records(kmer_ctx *c, const uint8_t *d_data, uint64_t n, hipStr
 // chunk's counters: spin on the sequence word it writes last to mapped host
 // memory, instead of a stream-synchronize round trip.  The stream is polled
 // now and then, so that a failed or finished stream ends the wait.
-kmer_status wait_tail(kmer_ctx *c, uint64_t seq) {
+kmer_status wait_tail(kmer_ctx *c, uint64_t seq, hipStream_t qs) {
     volatile uint64_t *flag = c->h_tail + 9;
     for (uint32_t i = 1;; ++i) {
         if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) break;
         if ((i & 1023) == 0) {
-            const hipError_t e = hipStreamQuery(c->stream);
+            const hipError_t e = hipStreamQuery(qs);
             if (e == hipSuccess) {
                 if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) break;
                 return fail(c, KMER_E_DEVICE, "chunk counters were not published");
@@ -367,6 +381,49 @@ kmer_status ensure_cross(kmer_ctx *c, uint64_t need, hipStream_t s) {
     return KMER_OK;
 }
 
+// session arrays the hit kernels write (they move when grown)
+void bind_hits(kmer_ctx *c, HitArgs &h) {
+    h.rkey = c->rkey.p;
+    h.rkey32 = c->narrow ? c->rkey32.p : nullptr;
+    h.rord = c->rord.p;
+    h.ridx = c->ridx.p;
+    h.xord = c->xord.p;
+    h.xkey = c->xkey.p;
+    h.xslot = c->xslot.p;
+    h.xbase = c->n_cross;
+    h.xcap = c->xord.cap;
+}
+
+// One attempt at the pending chunk: scan, tile scan, hit resolution and the
+// chunk tail (position, counters -> mapped host memory), all on the stream.
+kmer_status launch_chunk(kmer_ctx *c) {
+    auto &p = c->pend;
+    const hipStream_t s = p.s;
+    HIPCHK(c, hipEventRecord(c->ev0, s));
+    if (c->planes) HIPCHK(c, launch_scan_planes(p.a, c->pargs, s));
+    else HIPCHK(c, launch_scan_tiles(p.a, s));
+    HIPCHK(c, hipEventRecord(c->ev1, s));
+    HIPCHK(c, launch_tile_reduce(c->tsum.p, p.n_tiles, c->bsum.p, s));
+    if (p.n_blocks > TSCAN_INLINE_MAX) {
+        TileSum zero;
+        memset(&zero, 0, sizeof(zero));
+        ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->bsum.p, c->bscan.p, zero, (size_t)p.n_blocks, TileSumOp(), s));
+        HIPCHK(c, launch_tile_scan(c->tsum.p, p.n_tiles, c->bscan.p, true, p.init, c->tscan.p, s));
+    } else {
+        HIPCHK(c, launch_tile_scan(c->tsum.p, p.n_tiles, c->bsum.p, false, p.init, c->tscan.p, s));
+    }
+    p.h.seq = ++c->tail_seq;
+    HIPCHK(c, launch_hits(p.h, s));          // (+ the chunk tail: position, counters -> h_tail)
+    HIPCHK(c, hipEventRecord(c->ev4, s));
+    if (s != c->stream) HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev4, 0));   // later work follows the chunk
+    c->feed_timing_pending = true;
+    return KMER_OK;
+}
+
+// Launch one chunk on the packed path and return: the host does not wait
+// for it.  settle() (called by the next use of the context) reads its tail,
+// redoes it after an overflow and applies its counters, so a caller can
+// queue work elsewhere -- e.g. another context's finish -- meanwhile.
 kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s) {
     const bool packed = c->mode == MODE_PACKED;
     kmer_status st;
@@ -377,7 +434,8 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
         st = ensure_cross(c, c->n_cross + std::max<uint64_t>(n_tiles / 4, 4096), s);
         if (st) return st;
     }
-    ScanArgs a;
+    auto &p = c->pend;
+    ScanArgs &a = p.a;
     memset(&a, 0, sizeof(a));
     a.data = d;
     a.len = len;
@@ -397,7 +455,7 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
     a.err = c->d_err;
     a.ablate = (c->p.flags >> 8) & 0xFFu;   // KMER_FLAG_ABLATE_* (experiments only)
 
-    HitArgs h;
+    HitArgs &h = p.h;
     memset(&h, 0, sizeof(h));
     h.hits = c->hits.p;
     h.tsum = c->tsum.p;
@@ -418,25 +476,7 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
     h.rec_count = c->d_rec_count;
     h.rec_cap = c->recs.cap;
     h.err = c->d_err;
-    auto bind_session = [&]() {
-        h.rkey = c->rkey.p;
-        h.rkey32 = c->narrow ? c->rkey32.p : nullptr;
-        h.rord = c->rord.p;
-        h.ridx = c->ridx.p;
-        h.xord = c->xord.p;
-        h.xkey = c->xkey.p;
-        h.xslot = c->xslot.p;
-        h.xbase = c->n_cross;
-        h.xcap = c->xord.cap;
-    };
-    bind_session();
-    TileSum init;
-    init.cnt = 0;
-    init.nh = 0;
-    init.nx = 0;
-    init.lnl = c->abs_offset;
-    const uint32_t n_blocks = (n_tiles + TSCAN_BLOCK - 1) / TSCAN_BLOCK;
-
+    bind_hits(c, h);
     h.data = d;
     h.len = len;
     h.scal = c->d_scal;
@@ -445,68 +485,76 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
     h.chunk_cross = c->d_xcount;
     h.ends_open = c->d_ends_open;
     h.host_out = c->d_tail;
+    p.init.cnt = 0;
+    p.init.nh = 0;
+    p.init.nx = 0;
+    p.init.lnl = c->abs_offset;
+    p.n_tiles = n_tiles;
+    p.n_blocks = (n_tiles + TSCAN_BLOCK - 1) / TSCAN_BLOCK;
+    p.d = d;
+    p.len = len;
+    // the chunk runs on the low-priority stream, after everything queued so far
+    p.s = c->sstream;
+    HIPCHK(c, hipEventRecord(c->evq, s));
+    HIPCHK(c, hipStreamWaitEvent(p.s, c->evq, 0));
     // prologue: pending reset / position, position snapshot, zeroed chunk counters
     st = resolve_feed_timing(c);
     if (st) return st;
-    st = flush_prep(c, s, PREP_SAVE | PREP_ZERO);
+    st = flush_prep(c, p.s, PREP_SAVE | PREP_ZERO);
     if (st) return st;
-    for (int attempt = 0; attempt < 8; ++attempt) {
-        if (attempt) HIPCHK(c, hipMemsetAsync(c->d_scal, 0, 3 * 8, s));   // rec, ovf, cross counts of this chunk
-        HIPCHK(c, hipEventRecord(c->ev0, s));
-        if (c->planes) HIPCHK(c, launch_scan_planes(a, c->pargs, s));
-        else HIPCHK(c, launch_scan_tiles(a, s));
-        HIPCHK(c, hipEventRecord(c->ev1, s));
-        HIPCHK(c, launch_tile_reduce(c->tsum.p, n_tiles, c->bsum.p, s));
-        if (n_blocks > TSCAN_INLINE_MAX) {
-            TileSum zero;
-            memset(&zero, 0, sizeof(zero));
-            ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->bsum.p, c->bscan.p, zero, (size_t)n_blocks, TileSumOp(), s));
-            HIPCHK(c, launch_tile_scan(c->tsum.p, n_tiles, c->bscan.p, true, init, c->tscan.p, s));
-        } else {
-            HIPCHK(c, launch_tile_scan(c->tsum.p, n_tiles, c->bsum.p, false, init, c->tscan.p, s));
-        }
-        h.seq = ++c->tail_seq;
-        HIPCHK(c, launch_hits(h, s));          // (+ the chunk tail: position, counters -> h_tail)
-        HIPCHK(c, hipEventRecord(c->ev4, s));
-        st = wait_tail(c, h.seq);
+    p.active = true;
+    c->abs_offset += len;
+    return launch_chunk(c);
+}
+
+// Settle the pending chunk: wait for its tail (published to mapped host
+// memory, no stream sync), check errors; after an overflow grow the lists
+// and redo it from the saved position (hit placement is idempotent: rank
+// slots are rewritten, lists restart at this chunk's base); then apply its
+// hit / cross counts and drain its records.
+kmer_status settle(kmer_ctx *c) {
+    auto &p = c->pend;
+    if (!p.active) return KMER_OK;
+    p.active = false;                            // (an error abandons the chunk)
+    const bool packed = c->mode == MODE_PACKED;
+    const hipStream_t s = p.s;
+    kmer_status st;
+    for (int attempt = 0;; ++attempt) {
+        st = wait_tail(c, p.h.seq, s);
         if (st) return st;
-        c->feed_timing_pending = true;
         const uint32_t e = (uint32_t)c->h_small[5];
         st = check_err(c, e);
         if (st) return st;
-        if (e & (ERR_OVF_OVERFLOW | ERR_REC_OVERFLOW | ERR_CROSS_OVERFLOW)) {
-            st = resolve_feed_timing(c);
+        if (!(e & (ERR_OVF_OVERFLOW | ERR_REC_OVERFLOW | ERR_CROSS_OVERFLOW))) break;
+        if (attempt == 7) return fail(c, KMER_E_OOM, "hit lists kept overflowing");
+        st = resolve_feed_timing(c);
+        if (st) return st;
+        HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
+        HIPCHK(c, hipMemcpyAsync(c->d_pos, c->d_pos_saved, sizeof(StreamPos), hipMemcpyDeviceToDevice, s));
+        if (e & ERR_OVF_OVERFLOW) {
+            HIPCHK(c, c->ovf.ensure(c->h_small[1] + 1024, s));
+            p.a.ovf = c->ovf.p;
+            p.h.ovf = c->ovf.p;
+            p.a.ovf_cap = p.h.ovf_cap = c->ovf.cap;
+            if (packed) {
+                st = ensure_rank_arrays(c, c->n_hits + (uint64_t)p.n_tiles * HMAX + c->ovf.cap, c->n_hits, s);
+                if (st) return st;
+            }
+        }
+        if (e & ERR_CROSS_OVERFLOW) {
+            st = ensure_cross(c, c->n_cross + c->h_small[2] + 1024, s);
             if (st) return st;
         }
-        if (e & (ERR_OVF_OVERFLOW | ERR_REC_OVERFLOW | ERR_CROSS_OVERFLOW)) {
-            // grow and redo the chunk from the saved position; hit placement is
-            // idempotent (rank slots are rewritten, lists restart at this chunk's base)
-            HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
-            HIPCHK(c, hipMemcpyAsync(c->d_pos, c->d_pos_saved, sizeof(StreamPos), hipMemcpyDeviceToDevice, s));
-            if (e & ERR_OVF_OVERFLOW) {
-                HIPCHK(c, c->ovf.ensure(c->h_small[1] + 1024, s));
-                a.ovf = c->ovf.p;
-                h.ovf = c->ovf.p;
-                a.ovf_cap = h.ovf_cap = c->ovf.cap;
-                if (packed) {
-                    st = ensure_rank_arrays(c, c->n_hits + (uint64_t)n_tiles * HMAX + c->ovf.cap, c->n_hits, s);
-                    if (st) return st;
-                }
-            }
-            if (e & ERR_CROSS_OVERFLOW) {
-                st = ensure_cross(c, c->n_cross + c->h_small[2] + 1024, s);
-                if (st) return st;
-            }
-            if (e & ERR_REC_OVERFLOW) {
-                st = ensure_records(c, c->h_small[0] + 1024);
-                if (st) return st;
-                h.recs = c->recs.p;
-                h.rec_cap = c->recs.cap;
-            }
-            bind_session();
-            continue;
+        if (e & ERR_REC_OVERFLOW) {
+            st = ensure_records(c, c->h_small[0] + 1024);
+            if (st) return st;
+            p.h.recs = c->recs.p;
+            p.h.rec_cap = c->recs.cap;
         }
-        break;
+        bind_hits(c, p.h);
+        HIPCHK(c, hipMemsetAsync(c->d_scal, 0, 3 * 8, s));   // rec, ovf, cross counts of this chunk
+        st = launch_chunk(c);
+        if (st) return st;
     }
     if (packed) {
         c->n_hits += c->h_small[3];
@@ -516,12 +564,17 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
     c->chunk_open = c->h_small[7] != 0;
     const uint64_t nrec = c->h_small[0];
     if (nrec) {
-        st = drain_records(c, d, nrec, s);
+        st = drain_records(c, p.d, nrec, s);
         if (st) return st;
     }
-    c->abs_offset += len;
     return KMER_OK;
 }
+
+#define SETTLE(ctx)                          \
+    do {                                     \
+        const kmer_status st_ = settle(ctx); \
+        if (st_) return st_;                 \
+    } while (0)
 
 // ---------------------------------------------------------------------------
 // general path feed
@@ -772,6 +825,8 @@ kmer_status windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n
 }
 
 kmer_status feed(kmer_ctx *c, const uint8_t *d, uint64_t len, hipStream_t s) {
+    kmer_status st0 = settle(c);
+    if (st0) return st0;
     if (c->mode != MODE_PACKED && c->mode != MODE_TILE_REC) {
         kmer_status st = flush_prep(c, s, 0);
         if (st) return st;
@@ -791,6 +846,7 @@ kmer_status feed(kmer_ctx *c, const uint8_t *d, uint64_t len, hipStream_t s) {
 
 // (device side deferred to the next feed's prologue kernel: flush_prep)
 kmer_status reset(kmer_ctx *c) {
+    (void)settle(c);                             // (a chunk abandoned by the reset: its errors do not matter)
     c->prep_flags = PREP_RESET;
     c->feed_timing_pending = false;
     c->exotic.clear();
@@ -1023,7 +1079,9 @@ kmer_status build_result(kmer_ctx *c, uint64_t lines, kmer_result **out) {
 }
 
 kmer_status read_pos(kmer_ctx *c, StreamPos *pos) {
-    kmer_status st = flush_prep(c, c->stream, 0);
+    kmer_status st = settle(c);
+    if (st) return st;
+    st = flush_prep(c, c->stream, 0);
     if (st) return st;
     HIPCHK(c, hipMemcpyAsync(c->h_small + 8, c->d_pos, sizeof(StreamPos), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1035,7 +1093,8 @@ kmer_status read_pos(kmer_ctx *c, StreamPos *pos) {
 // for the device: the unique count and the timing are read back lazily.
 kmer_status finish(kmer_ctx *c, kmer_result **out) {
     if (!c->open_stream) return fail(c, KMER_E_STATE, "finish without reset/feed");
-    kmer_status st;
+    kmer_status st = settle(c);
+    if (st) return st;
     HIPCHK(c, hipEventRecord(c->ev2, c->stream));
     uint64_t nu = 0;
     c->n_out = 0;
@@ -1082,6 +1141,8 @@ kmer_status feed_host(kmer_ctx *c, const uint8_t *bytes, uint64_t len) {
             }
         }
         const uint64_t n = end - pos;
+        kmer_status st0 = settle(c);            // the previous batch is done with the staging buffer
+        if (st0) return st0;
         HIPCHK(c, c->batch.ensure(n, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->batch.p, bytes + pos, n, hipMemcpyHostToDevice, c->stream));
         kmer_status st = feed(c, c->batch.p, n, c->stream);
@@ -1137,7 +1198,17 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
         return s;
     };
     if (hipSetDevice(c->device) != hipSuccess) return cleanup(KMER_E_DEVICE);
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return cleanup(KMER_E_DEVICE);
+    {
+        // two priorities: another session's finish (short, latency-bound
+        // kernels) is dispatched ahead of the remaining workgroups of a
+        // running scan instead of queueing behind all of them
+        int lo = 0, hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
+        if (hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi) != hipSuccess ||
+            hipStreamCreateWithPriority(&c->sstream, hipStreamNonBlocking, lo) != hipSuccess ||
+            hipEventCreateWithFlags(&c->evq, hipEventDisableTiming) != hipSuccess)
+            return cleanup(KMER_E_DEVICE);
+    }
 
     const uint32_t k = pp->k, plen = (uint32_t)c->prefix.size();
     bool acgt = plen > 0;
@@ -1217,6 +1288,8 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
 
 kmer_status kmer_close(kmer_ctx *c) {
     if (!c) return KMER_E_BAD_PARAM;
+    (void)hipSetDevice(c->device);
+    (void)settle(c);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->tcount.release();
     for (auto *b : {&c->tbase, &c->nlpos, &c->wcount, &c->wbase, &c->tp_cnt, &c->tp_lnl, &c->rkey, &c->rkey2, &c->rord, &c->rcnt, &c->xord, &c->xord2,
@@ -1252,9 +1325,18 @@ kmer_status kmer_close(kmer_ctx *c) {
     if (c->h_tail) (void)hipHostFree(c->h_tail);
     for (hipEvent_t e : {c->ev0, c->ev1, c->ev2, c->ev3, c->ev4, c->evw})
         if (e) (void)hipEventDestroy(e);
+    if (c->sstream) (void)hipStreamSynchronize(c->sstream);
+    if (c->evq) (void)hipEventDestroy(c->evq);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->sstream) (void)hipStreamDestroy(c->sstream);
     delete c;
     return KMER_OK;
+}
+
+kmer_status kmer_sync(kmer_ctx *c) {
+    if (!c) return KMER_E_BAD_PARAM;
+    if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
+    return settle(c);
 }
 
 kmer_status kmer_reset(kmer_ctx *c) {
@@ -1265,6 +1347,7 @@ kmer_status kmer_reset(kmer_ctx *c) {
 
 kmer_status kmer_feed_device(kmer_ctx *c, const void *d_bytes, size_t len, void *stream) {
     if (!c || (!d_bytes && len)) return KMER_E_BAD_PARAM;
+    SETTLE(c);
     if (!c->open_stream) return fail(c, KMER_E_STATE, "feed without reset");
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
     hipStream_t s = (hipStream_t)stream;
@@ -1281,6 +1364,7 @@ kmer_status kmer_feed_device(kmer_ctx *c, const void *d_bytes, size_t len, void 
 
 kmer_status kmer_finish_device(kmer_ctx *c, kmer_result **out) {
     if (!c) return KMER_E_BAD_PARAM;
+    SETTLE(c);
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
     if (out) *out = nullptr;
     return finish(c, out);
@@ -1347,6 +1431,7 @@ kmer_status kmer_count_file(kmer_ctx *c, const char *path, kmer_result **out) {
 
 kmer_status kmer_partial_device(kmer_ctx *c, const void **d_keys, const void **d_vals, uint64_t *n) {
     if (!c || !d_keys || !d_vals || !n) return KMER_E_BAD_PARAM;
+    SETTLE(c);
     if (c->mode != MODE_PACKED && c->mode != MODE_WINDOWS)
         return fail(c, KMER_E_STATE, "configuration has no packed keys");
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
@@ -1365,6 +1450,7 @@ kmer_status kmer_partial_device(kmer_ctx *c, const void **d_keys, const void **d
 kmer_status kmer_finish_merged(kmer_ctx *c, const void *d_keys, const void *d_vals, uint64_t n,
                                uint64_t total_lines, kmer_result **out) {
     if (!c || (n && (!d_keys || !d_vals))) return KMER_E_BAD_PARAM;
+    SETTLE(c);
     if (c->mode != MODE_PACKED && c->mode != MODE_WINDOWS)
         return fail(c, KMER_E_STATE, "configuration has no packed keys");
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
@@ -1400,6 +1486,7 @@ kmer_status kmer_finish_merged(kmer_ctx *c, const void *d_keys, const void *d_va
 
 kmer_status kmer_exchange_prepare(kmer_ctx *c, uint32_t world, const void **d_send, uint64_t *counts) {
     if (!c || !d_send || !counts || world == 0 || world > XP_MAXW) return KMER_E_BAD_PARAM;
+    SETTLE(c);
     if (c->mode != MODE_PACKED && c->mode != MODE_WINDOWS)
         return fail(c, KMER_E_STATE, "configuration has no packed keys");
     if (!c->open_stream) return fail(c, KMER_E_STATE, "exchange without reset/feed");
@@ -1438,6 +1525,7 @@ kmer_status kmer_exchange_prepare(kmer_ctx *c, uint32_t world, const void **d_se
 kmer_status kmer_finish_exchanged(kmer_ctx *c, const void *d_recv, uint64_t n, uint64_t total_lines,
                                   void *wait_stream, kmer_result **out) {
     if (!c || (n && !d_recv)) return KMER_E_BAD_PARAM;
+    SETTLE(c);
     if (c->mode != MODE_PACKED && c->mode != MODE_WINDOWS)
         return fail(c, KMER_E_STATE, "configuration has no packed keys");
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
@@ -1476,6 +1564,7 @@ kmer_status kmer_finish_exchanged(kmer_ctx *c, const void *d_recv, uint64_t n, u
 
 kmer_status kmer_records_export(kmer_ctx *c, kmer_result **out) {
     if (!c || !out) return KMER_E_BAD_PARAM;
+    SETTLE(c);
     kmer_result *r = new (std::nothrow) kmer_result();
     if (!r) return KMER_E_OOM;
     std::vector<std::pair<uint64_t, const std::pair<const std::string, Ent> *>> ex;
@@ -1494,6 +1583,7 @@ kmer_status kmer_records_export(kmer_ctx *c, kmer_result **out) {
 kmer_status kmer_records_import(kmer_ctx *c, const char *keys, const uint64_t *offsets, const uint64_t *counts,
                                 const uint64_t *firsts, uint64_t n) {
     if (!c || (n && (!keys || !offsets || !counts || !firsts))) return KMER_E_BAD_PARAM;
+    SETTLE(c);
     for (uint64_t i = 0; i < n; ++i) {
         std::string key(keys + offsets[i], offsets[i + 1] - offsets[i]);
         auto it = c->exotic.find(key);
@@ -1509,12 +1599,14 @@ kmer_status kmer_records_import(kmer_ctx *c, const char *keys, const uint64_t *o
 
 kmer_status kmer_records_clear(kmer_ctx *c) {
     if (!c) return KMER_E_BAD_PARAM;
+    SETTLE(c);
     c->exotic.clear();
     return KMER_OK;
 }
 
 kmer_status kmer_set_position(kmer_ctx *c, uint64_t lines_before, uint64_t byte_offset) {
     if (!c) return KMER_E_BAD_PARAM;
+    SETTLE(c);
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
     c->prep_flags |= PREP_SETPOS;      // applied by the next feed's prologue (flush_prep)
     c->prep_lines = lines_before;
@@ -1525,6 +1617,7 @@ kmer_status kmer_set_position(kmer_ctx *c, uint64_t lines_before, uint64_t byte_
 
 kmer_status kmer_lines(kmer_ctx *c, uint64_t *lines) {
     if (!c || !lines) return KMER_E_BAD_PARAM;
+    SETTLE(c);
     StreamPos pos;
     kmer_status st = read_pos(c, &pos);
     if (st) return st;
@@ -1535,6 +1628,7 @@ kmer_status kmer_lines(kmer_ctx *c, uint64_t *lines) {
 kmer_status kmer_result_device(kmer_ctx *c, const void **d_keys, const void **d_counts, const void **d_firsts,
                                uint64_t *n) {
     if (!c || !n) return KMER_E_BAD_PARAM;
+    SETTLE(c);
     kmer_status st = resolve_out(c);
     if (st) return st;
     if (d_keys) *d_keys = c->keys_out.p;
@@ -1546,6 +1640,7 @@ kmer_status kmer_result_device(kmer_ctx *c, const void **d_keys, const void **d_
 
 kmer_status kmer_last_timing(kmer_ctx *c, double *scan_ms, double *feed_ms, double *finish_ms) {
     if (!c) return KMER_E_BAD_PARAM;
+    SETTLE(c);
     // (the finish is waited for only when its time is asked for)
     kmer_status st = finish_ms ? resolve_out(c) : resolve_feed_timing(c);
     if (st) return st;
