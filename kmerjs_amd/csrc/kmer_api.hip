@@ -1227,7 +1227,8 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
     c->narrow = packed_keys && c->kbits <= 31;
     c->planes = (c->mode == MODE_PACKED || c->mode == MODE_TILE_REC) && acgt && !(pp->flags & KMER_FLAG_BYTE_SCAN);
     if (c->planes) {
-        auto code = [](char ch) -> uint32_t { return ch == 'A' ? 0u : ch == 'C' ? 1u : ch == 'G' ? 2u : 3u; };
+        // plane bits of a base: bit 1 (plane L) and bit 2 (plane H) of its ASCII byte
+        auto code = [](char ch) -> uint32_t { return (((uint8_t)ch >> 1) & 1u) | ((((uint8_t)ch >> 2) & 1u) << 1); };
         c->pargs.pb = std::min<uint32_t>(plen, 5);
         for (uint32_t i = 0; i < 5; ++i) {
             const uint32_t cp = i < plen ? code(c->prefix[i]) : 0u, cr = i < plen ? code(c->rprefix[i]) : 0u;

@@ -778,9 +778,9 @@ __device__ __forceinline__ void verify_emit(const ScanArgs &a, const uint8_t *bu
 // ---------------------------------------------------------------------------
 // Plane kernel (ACGT prefixes).  Same tile staging as scan_tile_kernel, but
 // after the coalesced load each thread works on its own 64 contiguous bytes
-// (+4 look-ahead): the bytes become two bit-planes of 2-bit base codes
-// (A=0 C=1 G=2 T=3; bit 0 = b1^b2, bit 1 = b2^b3 of the byte), 32 positions
-// per 32-bit word, packed with v_dot4_u32_u8.  The prefix (up to 5 bases) is
+// (+4 look-ahead): the bytes become two bit-planes, bits 1 and 2 of each
+// byte, which already tell A (00) C (10) G (11) T (01) apart -- 32 positions
+// per 32-bit word, packed with v_dot4_u32_u8, no per-byte recoding.  The prefix (up to 5 bases) is
 // then tested at 32 positions per bit-op on both strands:
 //   match = AND_i (L>>i == P_i.lo) & (H>>i == P_i.hi)     (funnel shifts)
 // Non-ACGT bytes alias to some code, so a candidate is re-checked byte for
@@ -894,18 +894,17 @@ __global__ __launch_bounds__(TPB) void scan_planes_kernel(ScanArgs a, PlaneArgs 
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             const uint32_t x0 = w[8 * h + 2 * p], x1 = w[8 * h + 2 * p + 1];
-            const uint32_t t0 = x0 ^ (x0 >> 1), t1 = x1 ^ (x1 >> 1);
-            gl[p] = __builtin_amdgcn_udot4(t0 & 0x02020202u, W0, __builtin_amdgcn_udot4(t1 & 0x02020202u, W1, 0u, false), false);
-            gh[p] = __builtin_amdgcn_udot4(t0 & 0x04040404u, W0, __builtin_amdgcn_udot4(t1 & 0x04040404u, W1, 0u, false), false);
+            gl[p] = __builtin_amdgcn_udot4(x0 & 0x02020202u, W0, __builtin_amdgcn_udot4(x1 & 0x02020202u, W1, 0u, false), false);
+            gh[p] = __builtin_amdgcn_udot4(x0 & 0x04040404u, W0, __builtin_amdgcn_udot4(x1 & 0x04040404u, W1, 0u, false), false);
         }
         // gl: bits 1..8, gh: bits 2..9 for 8 bases
         L[h] = (gl[0] >> 1) | (gl[1] << 7) | (gl[2] << 15) | (gl[3] << 23);
         H[h] = (gh[0] >> 2) | (gh[1] << 6) | (gh[2] << 14) | (gh[3] << 22);
     }
     {
-        const uint32_t x = w[16], t = x ^ (x >> 1);
-        L[2] = __builtin_amdgcn_udot4(t & 0x02020202u, W0, 0u, false) >> 1;
-        H[2] = __builtin_amdgcn_udot4(t & 0x04040404u, W0, 0u, false) >> 2;
+        const uint32_t x = w[16];
+        L[2] = __builtin_amdgcn_udot4(x & 0x02020202u, W0, 0u, false) >> 1;
+        H[2] = __builtin_amdgcn_udot4(x & 0x04040404u, W0, 0u, false) >> 2;
     }
     uint32_t mf[2], mr[2];
     const uint32_t pb = FULL5 ? 5u : pa.pb;
