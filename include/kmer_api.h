@@ -55,6 +55,12 @@ enum {
     KMER_FLAG_NO_DENSE = 1u << 1,  /* debug: records instead of packed keys (host merge) */
     KMER_FLAG_BYTE_SCAN = 1u << 2, /* debug: byte-SWAR prefix scan instead of the bit-plane scan */
     KMER_FLAG_SORT_FINISH = 1u << 3, /* debug: radix-sort finish instead of the bucket-table finish */
+    /* Table mode: the result need not be in Map insertion order.  For step 1,
+     * k <= 32 and an empty or A/C/G/T prefix the counts go to a hash-partitioned
+     * table of canonical k-mers in HBM (no 2^32-hit session limit; host results
+     * sorted by key bytes); other configurations keep the ordered paths. */
+    KMER_FLAG_UNORDERED = 1u << 4,
+    KMER_FLAG_TABLE_SPLIT_TEST = 1u << 5, /* debug: table mode with 64-key LDS ranges (exercises range splits) */
     /* experiments only (results are WRONG with these set): ablate parts of the tile scan */
     KMER_FLAG_ABLATE_HITS = 1u << 8,   /* drop every prefix candidate */
     KMER_FLAG_ABLATE_SWAR = 1u << 9    /* skip the SWAR prefix scan entirely */
@@ -162,6 +168,22 @@ void kmer_result_free(kmer_result *r);
  * §8d generator, splitmix64 of (seed, read index)) to device memory. */
 kmer_status kmer_synth_fastq_device(void *d_out, uint64_t seed, uint64_t first_read, uint64_t n_reads,
                                     void *stream);
+
+/* Table mode (KMER_FLAG_UNORDERED), after a finish.  The counts replace the
+ * reference Map (lib/kmers.js:95) when it would be too large to build:
+ *   canonical = distinct canonical k-mers in the table,
+ *   keys      = distinct Map keys (both orientations, prefix-filtered, + records),
+ *   total     = sum of the Map's counts (= counted windows on both strands). */
+kmer_status kmer_table_stats(kmer_ctx *ctx, uint64_t *canonical, uint64_t *keys, uint64_t *total);
+/* The table itself, in device memory.  2^20 buckets; bucket q holds
+ * bucket_len[q] (uint32) entries at entries[bucket_start[q] ..] (uint64 each:
+ * remainder << 20 | count, count == 0xFFFFF meaning "see the big list").
+ * h = q << 44 | remainder is a bijective mix (murmur3 fmix64) of the canonical
+ * planar code c = min(code(w), code(rc w)) with code = hi_plane << k | lo_plane,
+ * base i of the k-mer at bit i of each plane, A/C/G/T = (hi,lo) 00/01/10/11.
+ * big = n_big {uint64 h, uint64 count} pairs.  Valid until the next reset. */
+kmer_status kmer_table_device(kmer_ctx *ctx, const void **d_entries, const void **d_bucket_start,
+                              const void **d_bucket_len, const void **d_big, uint64_t *n_big);
 
 /* Device time (HIP events on the context's stream, ms) since the last reset:
  * scan_ms = the streaming tile-scan kernel(s) alone, feed_ms = every kernel of

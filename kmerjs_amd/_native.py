@@ -16,6 +16,8 @@ FLAG_TWO_PASS = 1
 FLAG_NO_DENSE = 2
 FLAG_BYTE_SCAN = 4
 FLAG_SORT_FINISH = 8
+FLAG_UNORDERED = 16
+FLAG_TABLE_SPLIT_TEST = 32
 
 # every symbol the header declares (tests/test_abi.py checks header <-> library)
 EXPORTS = ["kmer_open", "kmer_close", "kmer_count_file", "kmer_count_buffer", "kmer_reset", "kmer_sync",
@@ -24,7 +26,8 @@ EXPORTS = ["kmer_open", "kmer_close", "kmer_count_file", "kmer_count_buffer", "k
            "kmer_records_export", "kmer_records_import", "kmer_records_clear", "kmer_result_device", "kmer_set_position",
            "kmer_lines", "kmer_result_size", "kmer_result_lines", "kmer_result_get",
            "kmer_result_arrays", "kmer_result_firsts", "kmer_result_free", "kmer_synth_fastq_device",
-           "kmer_last_timing", "kmer_status_string", "kmer_last_error", "kmer_version"]
+           "kmer_last_timing", "kmer_table_stats", "kmer_table_device",
+           "kmer_status_string", "kmer_last_error", "kmer_version"]
 
 
 class Params(ctypes.Structure):
@@ -84,6 +87,9 @@ def _load():
         "kmer_synth_fastq_device": (ctypes.c_int, [vp, u64, u64, u64, vp]),
         "kmer_last_timing": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                             ctypes.POINTER(ctypes.c_double)]),
+        "kmer_table_stats": (ctypes.c_int, [vp, pu64, pu64, pu64]),
+        "kmer_table_device": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                             ctypes.POINTER(vp), pu64]),
         "kmer_status_string": (ctypes.c_char_p, [ctypes.c_int]),
         "kmer_last_error": (ctypes.c_char_p, [vp]),
         "kmer_version": (ctypes.c_char_p, []),
@@ -268,6 +274,19 @@ class Counter:
         self._check(LIB.kmer_result_device(self.h, ctypes.byref(k), ctypes.byref(c), ctypes.byref(f),
                                            ctypes.byref(n)), "result_device")
         return k.value or 0, c.value or 0, f.value or 0, n.value
+
+    def table_stats(self):
+        """Table mode: (distinct canonical k-mers, distinct Map keys, sum of Map counts)."""
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(LIB.kmer_table_stats(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "table_stats")
+        return a.value, b.value, c.value
+
+    def table_device(self):
+        """Table mode: (d_entries, d_bucket_start, d_bucket_len, d_big, n_big) in device memory."""
+        e, st, ln, bg, nb = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+        self._check(LIB.kmer_table_device(self.h, ctypes.byref(e), ctypes.byref(st), ctypes.byref(ln),
+                                          ctypes.byref(bg), ctypes.byref(nb)), "table_device")
+        return e.value or 0, st.value or 0, ln.value or 0, bg.value or 0, nb.value
 
     def lines(self):
         n = ctypes.c_uint64()

@@ -38,8 +38,9 @@ namespace {
 
 // PACKED: tile scan, packed keys; TILE_REC: tile scan, records (host merge);
 // WINDOWS: dense hits (no / 1-3 base prefix), every window ranked; GENERAL:
-// lines + windows kernels, records (any k, step, prefix).
-enum Mode { MODE_PACKED, MODE_TILE_REC, MODE_WINDOWS, MODE_GENERAL };
+// lines + windows kernels, records (any k, step, prefix); TABLE: unordered
+// canonical counts in a hash-partitioned table (KMER_FLAG_UNORDERED).
+enum Mode { MODE_PACKED, MODE_TILE_REC, MODE_WINDOWS, MODE_GENERAL, MODE_TABLE };
 
 struct Ent {
     uint64_t count;
@@ -178,6 +179,20 @@ struct kmer_ctx {
     } pend;
     uint64_t prep_lines = 0;
     DBuf<uint8_t> batch;
+    // table mode (kmer_table.hip)
+    DBuf<uint64_t> tb1, tb2;       // pass-1 keys (session, partition-major per chunk); final entries -> tb1
+    DBuf<uint32_t> tH, tnd;        // pass-1 / pass-2 histograms; distinct entries per bucket
+    DBuf<uint64_t> tHs, tstart;    // their scans; bucket starts (TAB_NQ + 1)
+    DBuf<uint64_t> tp1;            // pass-1 partition starts of the last chunk (TAB_NB)
+    DBuf<TabUnit> tunits;          // pass-2 units, then TAB_NB partition heads
+    DBuf<TabBig> tbig;             // entries with counts >= TAB_CMAX
+    DBuf<unsigned long long> tstats;   // [0..2] final statistics, [3] big-list count
+    uint64_t t_keys = 0;           // pass-1 keys of the session
+    std::vector<uint64_t> t_cbase; // per chunk: first key in tb1
+    std::vector<std::vector<uint64_t>> t_coff;   // per chunk: TAB_NB + 1 partition starts (chunk-relative)
+    uint64_t t_canon = 0, t_nkeys = 0, t_sum = 0, t_nbig = 0;   // last finish
+    bool t_done = false;           // a table finish holds results
+    int n_cu = 0;
     // timing (HIP events on the context stream)
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr;
     hipEvent_t evw = nullptr;      // cross-stream wait (no timing)
@@ -247,7 +262,9 @@ kmer_status ensure_tiles(kmer_ctx *c, uint64_t n_tiles) {
     if (n_tiles <= c->tile_cap) return KMER_OK;
     const uint64_t cap = std::max<uint64_t>(n_tiles, 1024);
     hipStream_t s = c->stream;
-    if (c->mode == MODE_GENERAL || c->mode == MODE_WINDOWS) {
+    if (c->mode == MODE_TABLE) {
+        // (table mode keeps no per-tile state beyond the newline counts)
+    } else if (c->mode == MODE_GENERAL || c->mode == MODE_WINDOWS) {
         HIPCHK(c, c->lb_cnt.ensure(cap, s));
         HIPCHK(c, c->lb_lnl.ensure(cap, s));
         HIPCHK(c, c->tp_cnt.ensure(cap, s));
@@ -722,14 +739,15 @@ kmer_status general_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n
     return KMER_OK;
 }
 
-// Dense-hit path: every window of every sequence line goes to its rank slot.
-kmer_status windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s) {
+// Sequence lines of a chunk: newline positions (two streaming passes, no
+// look-back), then one descriptor per sequence ordinal (c->lines, window
+// counts in c->wcount).  check_len: lines whose windows exceed the order
+// key's 2^23 positions are an error (ordered paths only).
+kmer_status chunk_lines(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s, bool check_len,
+                        uint64_t *n_nl_out, uint64_t *n_seq_out) {
     const uint64_t li0 = c->host_lines;
-    kmer_status st;
-    // newline positions of the chunk (two streaming passes, no look-back)
     HIPCHK(c, c->tcount.ensure(n_tiles, s));
     HIPCHK(c, c->tbase.ensure(n_tiles, s));
-    HIPCHK(c, hipEventRecord(c->ev0, s));
     HIPCHK(c, launch_nl_count(d, len, n_tiles, c->tcount.p, c->d_err, s));
     ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tcount.p, c->tbase.p, (uint64_t)0, (size_t)n_tiles,
                                            rocprim::plus<uint64_t>(), s));
@@ -737,19 +755,35 @@ kmer_status windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n
     HIPCHK(c, hipMemcpyAsync(c->h_small + 15, c->tcount.p + n_tiles - 1, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
-    st = check_err(c, (uint32_t)c->h_small[5]);
+    kmer_status st = check_err(c, (uint32_t)c->h_small[5]);
     if (st) return st;
     const uint64_t n_nl = c->h_small[14] + (uint32_t)c->h_small[15];
     HIPCHK(c, c->nlpos.ensure(n_nl + 1, s));
     HIPCHK(c, launch_nl_write(d, len, n_tiles, c->tbase.p, c->nlpos.p, s));
     const uint64_t first = (1u - (uint32_t)li0) & 3u;
     const uint64_t n_seq = n_nl >= first ? (n_nl - first) / 4 + 1 : 0;
-    uint64_t total = 0;
     if (n_seq) {
         HIPCHK(c, c->lines.ensure(n_seq, s));
         HIPCHK(c, c->wcount.ensure(n_seq, s));
+        HIPCHK(c, launch_seq_lines(c->nlpos.p, n_nl, len, li0, n_seq, c->p.k, c->lines.p, c->wcount.p,
+                                   check_len ? c->d_err : nullptr, s));
+    }
+    *n_nl_out = n_nl;
+    *n_seq_out = n_seq;
+    return KMER_OK;
+}
+
+// Dense-hit path: every window of every sequence line goes to its rank slot.
+kmer_status windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s) {
+    const uint64_t li0 = c->host_lines;
+    kmer_status st;
+    HIPCHK(c, hipEventRecord(c->ev0, s));
+    uint64_t n_nl = 0, n_seq = 0;
+    st = chunk_lines(c, d, len, n_tiles, s, true, &n_nl, &n_seq);
+    if (st) return st;
+    uint64_t total = 0;
+    if (n_seq) {
         HIPCHK(c, c->wbase.ensure(n_seq, s));
-        HIPCHK(c, launch_seq_lines(c->nlpos.p, n_nl, len, li0, n_seq, c->p.k, c->lines.p, c->wcount.p, c->d_err, s));
         ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->wcount.p, c->wbase.p, (uint64_t)0, (size_t)n_seq,
                                                rocprim::plus<uint64_t>(), s));
         HIPCHK(c, hipMemcpyAsync(c->h_small + 14, c->wbase.p + n_seq - 1, 8, hipMemcpyDeviceToHost, s));
@@ -824,6 +858,260 @@ kmer_status windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n
     return KMER_OK;
 }
 
+// ---------------------------------------------------------------------------
+// table mode feed (kernels: kmer_table.hip)
+// ---------------------------------------------------------------------------
+// Pass 1 of one chunk: its sequence lines, then per workgroup share of lines
+// a histogram of keys by partition, a scan, and the scatter into tb1 after
+// the session's earlier keys.  Non-ACGT windows go to the host map.
+kmer_status table_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s) {
+    const uint64_t li0 = c->host_lines;
+    HIPCHK(c, hipEventRecord(c->ev0, s));
+    uint64_t n_nl = 0, n_seq = 0;
+    kmer_status st = chunk_lines(c, d, len, n_tiles, s, false, &n_nl, &n_seq);
+    if (st) return st;
+    HIPCHK(c, launch_pos_after(c->d_pos, li0 + n_nl, d, len, c->d_ends_open, s));
+    c->host_lines = li0 + n_nl;
+    if (n_seq) {
+        TabArgs a;
+        memset(&a, 0, sizeof(a));
+        a.data = d;
+        a.len = len;
+        a.lines = c->lines.p;
+        a.n_lines = n_seq;
+        const uint64_t nwg0 = std::min<uint64_t>(8192, (n_seq + 63) / 64);
+        a.lpw = (n_seq + nwg0 - 1) / nwg0;
+        a.nwg = (uint32_t)((n_seq + a.lpw - 1) / a.lpw);
+        a.k = c->p.k;
+        for (size_t i = 0; i < c->prefix.size(); ++i) {
+            const uint8_t ch = (uint8_t)c->prefix[i];
+            a.plo |= ((((uint32_t)ch >> 1) ^ ((uint32_t)ch >> 2)) & 1u) << i;
+            a.phi |= (((uint32_t)ch >> 2) & 1u) << i;
+        }
+        a.pmask = c->prefix.size() >= 32 ? ~0u : ((1u << c->prefix.size()) - 1u);
+        a.err = c->d_err;
+        const uint64_t nh = (uint64_t)TAB_NB * a.nwg;
+        HIPCHK(c, c->tH.ensure(nh, s));
+        HIPCHK(c, c->tHs.ensure(nh, s));
+        HIPCHK(c, c->tp1.ensure(TAB_NB, s));
+        a.H1 = c->tH.p;
+        HIPCHK(c, launch_tab_hist1(a, s));
+        ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tH.p, c->tHs.p, (uint64_t)0, (size_t)nh,
+                                               rocprim::plus<uint64_t>(), s));
+        HIPCHK(c, launch_tab_p1_offsets(c->tHs.p, a.nwg, c->tp1.p, s));
+        std::vector<uint64_t> off(TAB_NB + 1);
+        HIPCHK(c, hipMemcpyAsync(off.data(), c->tp1.p, TAB_NB * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 14, c->tHs.p + nh - 1, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 15, c->tH.p + nh - 1, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        const uint64_t n_c = c->h_small[14] + (uint32_t)c->h_small[15];
+        off[TAB_NB] = n_c;
+        HIPCHK(c, c->tb1.ensure(c->t_keys + n_c, s, true, c->t_keys));
+        a.H1s = c->tHs.p;
+        a.base = c->t_keys;
+        a.B1 = c->tb1.p;
+        for (int attempt = 0;; ++attempt) {
+            a.recs = c->recs.p;
+            a.rec_count = c->d_rec_count;
+            a.rec_cap = c->recs.cap;
+            HIPCHK(c, hipMemsetAsync(c->d_rec_count, 0, 8, s));
+            HIPCHK(c, launch_tab_scatter1(a, s));
+            HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            const uint32_t e = (uint32_t)c->h_small[5];
+            st = check_err(c, e);
+            if (st) return st;
+            if (!(e & ERR_REC_OVERFLOW)) break;     // (a redo rewrites the same key ranges)
+            if (attempt == 7) return fail(c, KMER_E_OOM, "record list kept overflowing");
+            HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
+            st = ensure_records(c, c->h_small[0] + 1024);
+            if (st) return st;
+        }
+        const uint64_t nrec = c->h_small[0];
+        if (nrec) {
+            st = drain_records(c, d, nrec, s);
+            if (st) return st;
+        }
+        c->t_cbase.push_back(c->t_keys);
+        c->t_coff.push_back(std::move(off));
+        c->t_keys += n_c;
+    }
+    HIPCHK(c, hipEventRecord(c->ev1, s));
+    HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    c->scan_ms += ms;
+    c->feed_ms += ms;
+    c->chunk_open = c->h_small[7] != 0;
+    c->abs_offset += len;
+    return KMER_OK;
+}
+
+uint64_t inv_odd(uint64_t a) {   // inverse of an odd number mod 2^64 (Newton)
+    uint64_t x = a;
+    for (int i = 0; i < 5; ++i) x *= 2 - a * x;
+    return x;
+}
+
+// Pass 2 + final of the session: pass-1 partitions (one run per chunk) are
+// cut into units; each unit's keys go to their 2^20 buckets in tb2; the
+// final kernel merges each bucket in LDS and writes its entries into tb1.
+kmer_status table_finish(kmer_ctx *c) {
+    hipStream_t s = c->stream;
+    c->t_canon = c->t_nkeys = c->t_sum = c->t_nbig = 0;
+    c->t_done = true;
+    const uint64_t n = c->t_keys;
+    if (n == 0) return KMER_OK;
+    std::vector<TabUnit> units;
+    std::vector<TabUnit> heads(TAB_NB);
+    uint64_t ubase = 0;
+    for (uint32_t p = 0; p < TAB_NB; ++p) {
+        const size_t first = units.size();
+        for (size_t ch = 0; ch < c->t_cbase.size(); ++ch) {
+            const uint64_t a0 = c->t_coff[ch][p], a1 = c->t_coff[ch][p + 1];
+            for (uint64_t o = a0; o < a1; o += TAB_UNIT) {
+                TabUnit u{};
+                u.start = c->t_cbase[ch] + o;
+                u.len = (uint32_t)std::min<uint64_t>(TAB_UNIT, a1 - o);
+                units.push_back(u);
+            }
+        }
+        if (units.size() == first) units.push_back(TabUnit{});   // empty partition: zero histogram row
+        const uint32_t nun = (uint32_t)(units.size() - first);
+        for (size_t i = first; i < units.size(); ++i) {
+            units[i].u = (uint32_t)(i - first);
+            units[i].nunits = nun;
+            units[i].hbase = ubase * TAB_NB;
+        }
+        heads[p] = units[first];
+        ubase += nun;
+    }
+    const uint64_t n_units = units.size();
+    if (n_units >= (1ull << 31)) return fail(c, KMER_E_BAD_PARAM, "too many table units");
+    units.insert(units.end(), heads.begin(), heads.end());
+    HIPCHK(c, c->tunits.ensure(units.size(), s));
+    HIPCHK(c, hipMemcpyAsync(c->tunits.p, units.data(), units.size() * sizeof(TabUnit), hipMemcpyHostToDevice, s));
+    const uint64_t nh = n_units * TAB_NB;
+    HIPCHK(c, c->tH.ensure(nh, s));
+    HIPCHK(c, c->tHs.ensure(nh, s));
+    HIPCHK(c, c->tb2.ensure(n, s));
+    HIPCHK(c, c->tstart.ensure(TAB_NQ + 1, s));
+    HIPCHK(c, c->tnd.ensure(TAB_NQ, s));
+    HIPCHK(c, c->tbig.ensure(1 << 16, s));
+    HIPCHK(c, c->tstats.ensure(4, s));
+    HIPCHK(c, launch_tab_hist2(c->tb1.p, c->tunits.p, (uint32_t)n_units, c->tH.p, s));
+    ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tH.p, c->tHs.p, (uint64_t)0, (size_t)nh,
+                                           rocprim::plus<uint64_t>(), s));
+    HIPCHK(c, launch_tab_scatter2(c->tb1.p, c->tunits.p, (uint32_t)n_units, c->tHs.p, c->tb2.p, s));
+    HIPCHK(c, launch_tab_starts(c->tHs.p, c->tunits.p + n_units, n, c->tstart.p, s));
+    HIPCHK(c, hipMemsetAsync(c->tstats.p, 0, 4 * sizeof(unsigned long long), s));
+    TabFinal f;
+    memset(&f, 0, sizeof(f));
+    f.B2 = c->tb2.p;
+    f.start = c->tstart.p;
+    f.out = c->tb1.p;                        // (pass-1 keys are dead after pass 2)
+    f.nd = c->tnd.p;
+    const uint64_t mean = n / TAB_NQ;
+    while (f.sub_bits < 16 && (mean >> f.sub_bits) > 6000) ++f.sub_bits;
+    f.cap = (c->p.flags & KMER_FLAG_TABLE_SPLIT_TEST) ? 64 : TAB_CAP;
+    f.big = c->tbig.p;
+    f.big_count = c->tstats.p + 3;
+    f.big_cap = c->tbig.cap;
+    f.err = c->d_err;
+    f.k = c->p.k;
+    for (size_t i = 0; i < c->prefix.size(); ++i) {
+        const uint8_t ch = (uint8_t)c->prefix[i];
+        f.plo |= ((((uint32_t)ch >> 1) ^ ((uint32_t)ch >> 2)) & 1u) << i;
+        f.phi |= (((uint32_t)ch >> 2) & 1u) << i;
+    }
+    f.pmask = c->prefix.size() >= 32 ? ~0u : ((1u << c->prefix.size()) - 1u);
+    f.inv1 = inv_odd(0xff51afd7ed558ccdull);
+    f.inv2 = inv_odd(0xc4ceb9fe1a85ec53ull);
+    f.stats = c->tstats.p;
+    HIPCHK(c, launch_tab_final(f, (uint32_t)std::max(c->n_cu, 1), s));
+    HIPCHK(c, hipMemcpyAsync(c->h_small + 8, c->tstats.p, 4 * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    const uint32_t e = (uint32_t)c->h_small[5];
+    if (e & ERR_COUNT_OVERFLOW) return fail(c, KMER_E_TOO_MANY_KEYS, "a k-mer count exceeds 2^32 - 1");
+    if (e & ERR_BIG_OVERFLOW) return fail(c, KMER_E_OOM, "too many k-mers with counts >= 2^20");
+    if (e & ERR_TAB_SPLIT) return fail(c, KMER_E_DEVICE, "table bucket could not be split");
+    c->t_canon = c->h_small[8];
+    c->t_nkeys = c->h_small[9];
+    c->t_sum = c->h_small[10];
+    c->t_nbig = c->h_small[11];
+    c->n_out = c->t_nkeys;
+    return KMER_OK;
+}
+
+// Host result of a table finish: every canonical entry expanded into its Map
+// keys (c and rc c, prefix-filtered; palindromes counted twice), plus the
+// record keys; entries sorted by key bytes (the table has no order).
+kmer_status build_table_result(kmer_ctx *c, uint64_t lines, kmer_result **out) {
+    kmer_result *r = new (std::nothrow) kmer_result();
+    if (!r) return fail(c, KMER_E_OOM, "host allocation failed");
+    r->lines = lines;
+    std::vector<std::pair<std::string, uint64_t>> ents;
+    const uint32_t k = c->p.k;
+    if (c->t_keys) {
+        hipStream_t s = c->stream;
+        std::vector<uint64_t> start(TAB_NQ + 1), ent(c->t_keys);
+        std::vector<uint32_t> nd(TAB_NQ);
+        std::vector<TabBig> big(c->t_nbig);
+        bool ok = hipMemcpyAsync(start.data(), c->tstart.p, start.size() * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
+                  hipMemcpyAsync(nd.data(), c->tnd.p, nd.size() * 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
+                  hipMemcpyAsync(ent.data(), c->tb1.p, ent.size() * 8, hipMemcpyDeviceToHost, s) == hipSuccess;
+        if (ok && !big.empty())
+            ok = hipMemcpyAsync(big.data(), c->tbig.p, big.size() * sizeof(TabBig), hipMemcpyDeviceToHost, s) == hipSuccess;
+        if (!ok || hipStreamSynchronize(s) != hipSuccess) {
+            delete r;
+            return fail(c, KMER_E_DEVICE, "result copy failed");
+        }
+        std::unordered_map<uint64_t, uint64_t> bigc;
+        for (auto &b : big) bigc[b.h] = b.count;
+        const uint64_t inv1 = inv_odd(0xff51afd7ed558ccdull), inv2 = inv_odd(0xc4ceb9fe1a85ec53ull);
+        const uint64_t kmask = k >= 32 ? 0xFFFFFFFFull : ((1ull << k) - 1);
+        std::string key(k, 'A'), rkey(k, 'A');
+        for (uint32_t q = 0; q < TAB_NQ; ++q) {
+            for (uint32_t i = 0; i < nd[q]; ++i) {
+                const uint64_t w = ent[start[q] + i];
+                const uint64_t h = ((uint64_t)q << TAB_RBITS) | (w >> 20);
+                uint64_t cnt = w & TAB_CMAX;
+                if (cnt == TAB_CMAX) cnt = bigc[h];
+                uint64_t x = h;                      // tab_mix^-1
+                x ^= x >> 33;
+                x *= inv2;
+                x ^= x >> 33;
+                x *= inv1;
+                x ^= x >> 33;
+                const uint64_t lo = x & kmask, hi = (x >> k) & kmask;
+                for (uint32_t j = 0; j < k; ++j) {
+                    const uint32_t v = (uint32_t)(((hi >> j) & 1u) << 1 | ((lo >> j) & 1u));
+                    key[j] = "ACGT"[v];
+                    rkey[k - 1 - j] = "TGCA"[v];
+                }
+                const bool pal = key == rkey;
+                if (key.compare(0, c->prefix.size(), c->prefix) == 0) ents.emplace_back(key, pal ? 2 * cnt : cnt);
+                if (!pal && rkey.compare(0, c->prefix.size(), c->prefix) == 0) ents.emplace_back(rkey, cnt);
+            }
+        }
+    }
+    for (auto &kv : c->exotic) ents.emplace_back(kv.first, kv.second.count);
+    std::sort(ents.begin(), ents.end());
+    r->keys.reserve(ents.size() * k);
+    r->offsets.reserve(ents.size() + 1);
+    r->counts.reserve(ents.size());
+    for (auto &e : ents) {
+        r->keys.insert(r->keys.end(), e.first.begin(), e.first.end());
+        r->offsets.push_back(r->keys.size());
+        r->counts.push_back(e.second);
+        r->firsts.push_back(0);
+    }
+    *out = r;
+    return KMER_OK;
+}
+
 kmer_status feed(kmer_ctx *c, const uint8_t *d, uint64_t len, hipStream_t s) {
     kmer_status st0 = settle(c);
     if (st0) return st0;
@@ -841,6 +1129,7 @@ kmer_status feed(kmer_ctx *c, const uint8_t *d, uint64_t len, hipStream_t s) {
     if (st) return st;
     if (c->mode == MODE_GENERAL) return general_feed(c, d, len, n_tiles, s);
     if (c->mode == MODE_WINDOWS) return windows_feed(c, d, len, n_tiles, s);
+    if (c->mode == MODE_TABLE) return table_feed(c, d, len, n_tiles, s);
     return scan_feed(c, d, len, n_tiles, s);
 }
 
@@ -859,6 +1148,10 @@ kmer_status reset(kmer_ctx *c) {
     c->out_pending = false;
     c->timing_pending = false;
     c->n_out = 0;
+    c->t_keys = 0;
+    c->t_cbase.clear();
+    c->t_coff.clear();
+    c->t_done = false;
     c->scan_ms = c->feed_ms = c->finish_ms = 0.0;
     c->open_stream = true;
     return KMER_OK;
@@ -1105,6 +1398,9 @@ kmer_status finish(kmer_ctx *c, kmer_result **out) {
         st = rank_finish(c, c->n_hits, false, false, &nu, sync);
         if (st) return st;
         c->n_out = nu;
+    } else if (c->mode == MODE_TABLE) {
+        st = table_finish(c);
+        if (st) return st;
     }
     HIPCHK(c, hipEventRecord(c->ev3, c->stream));
     c->timing_pending = true;
@@ -1119,6 +1415,7 @@ kmer_status finish(kmer_ctx *c, kmer_result **out) {
     StreamPos pos;
     st = read_pos(c, &pos);
     if (st) return st;
+    if (c->mode == MODE_TABLE) return build_table_result(c, pos.lines + pos.ends_open, out);
     return build_result(c, pos.lines + pos.ends_open, out);
 }
 
@@ -1198,6 +1495,7 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
         return s;
     };
     if (hipSetDevice(c->device) != hipSuccess) return cleanup(KMER_E_DEVICE);
+    if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) c->n_cu = 256;
     {
         // two priorities: another session's finish (short, latency-bound
         // kernels) is dispatched ahead of the remaining workgroups of a
@@ -1214,7 +1512,10 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
     bool acgt = plen > 0;
     for (char ch : c->prefix) acgt &= ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T';
     const bool dense_ok = !(pp->flags & KMER_FLAG_NO_DENSE) && pp->step == 1 && plen <= k;
-    if (dense_ok && (plen == 0 ? k <= 31 : (acgt && plen <= 3 && k <= (uint32_t)KMAX_DENSE)))
+    if ((pp->flags & KMER_FLAG_UNORDERED) && pp->step == 1 && plen <= k && k <= (uint32_t)KMAX_PACKED &&
+        (plen == 0 || acgt))
+        c->mode = MODE_TABLE;
+    else if (dense_ok && (plen == 0 ? k <= 31 : (acgt && plen <= 3 && k <= (uint32_t)KMAX_DENSE)))
         c->mode = MODE_WINDOWS;
     else if (dense_ok && acgt && k <= (uint32_t)KMAX_DENSE)
         c->mode = MODE_PACKED;
@@ -1320,6 +1621,12 @@ kmer_status kmer_close(kmer_ctx *c) {
     c->rec_keys.release();
     c->tmp.release();
     c->batch.release();
+    for (auto *b : {&c->tb1, &c->tb2, &c->tHs, &c->tstart, &c->tp1}) b->release();
+    c->tH.release();
+    c->tnd.release();
+    c->tunits.release();
+    c->tbig.release();
+    c->tstats.release();
     dfree(c->d_ticket); dfree(c->d_scal); dfree(c->d_pos); dfree(c->d_pos_saved);
     dfree(c->d_P); dfree(c->d_PR);
     if (c->h_small) (void)hipHostFree(c->h_small);
@@ -1636,6 +1943,37 @@ kmer_status kmer_result_device(kmer_ctx *c, const void **d_keys, const void **d_
     if (d_counts) *d_counts = c->cnt_out.p;
     if (d_firsts) *d_firsts = c->first.p;
     *n = c->n_out;
+    return KMER_OK;
+}
+
+kmer_status kmer_table_stats(kmer_ctx *c, uint64_t *canonical, uint64_t *keys, uint64_t *total) {
+    if (!c) return KMER_E_BAD_PARAM;
+    SETTLE(c);
+    if (c->mode != MODE_TABLE) return fail(c, KMER_E_STATE, "not a table-mode context (KMER_FLAG_UNORDERED)");
+    if (!c->t_done) return fail(c, KMER_E_STATE, "no table finish yet");
+    uint64_t rk = 0, rs = 0;
+    for (auto &kv : c->exotic) {
+        rk += 1;
+        rs += kv.second.count;
+    }
+    if (canonical) *canonical = c->t_canon;
+    if (keys) *keys = c->t_nkeys + rk;
+    if (total) *total = c->t_sum + rs;
+    return KMER_OK;
+}
+
+kmer_status kmer_table_device(kmer_ctx *c, const void **d_entries, const void **d_bucket_start,
+                              const void **d_bucket_len, const void **d_big, uint64_t *n_big) {
+    if (!c) return KMER_E_BAD_PARAM;
+    SETTLE(c);
+    if (c->mode != MODE_TABLE) return fail(c, KMER_E_STATE, "not a table-mode context (KMER_FLAG_UNORDERED)");
+    if (!c->t_done) return fail(c, KMER_E_STATE, "no table finish yet");
+    const bool any = c->t_keys != 0;
+    if (d_entries) *d_entries = any ? c->tb1.p : nullptr;
+    if (d_bucket_start) *d_bucket_start = any ? c->tstart.p : nullptr;
+    if (d_bucket_len) *d_bucket_len = any ? c->tnd.p : nullptr;
+    if (d_big) *d_big = any ? c->tbig.p : nullptr;
+    if (n_big) *n_big = c->t_nbig;
     return KMER_OK;
 }
 

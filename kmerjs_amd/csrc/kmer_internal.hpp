@@ -29,6 +29,9 @@ enum : uint32_t {
     ERR_LINE_OVERFLOW = 1u << 4,
     ERR_OVF_OVERFLOW = 1u << 5,
     ERR_CROSS_OVERFLOW = 1u << 6,
+    ERR_COUNT_OVERFLOW = 1u << 7,    // table mode: one key counted 2^32 times in one bucket
+    ERR_BIG_OVERFLOW = 1u << 8,      // table mode: big-count list full
+    ERR_TAB_SPLIT = 1u << 9,         // table mode: bucket range could not be split further
     // not an error: a tile without '\n' had hits, or a tile overflowed its hit
     // slots -- cross segments may be long (finish sorts the whole cross list)
     INFO_LONGSEG = 1u << 16,
@@ -333,6 +336,87 @@ hipError_t launch_seq_lines(const uint64_t *nl, uint64_t n_nl, uint64_t len, uin
 hipError_t launch_pos_after(StreamPos *pos, uint64_t lines, const uint8_t *data, uint64_t len,
                             unsigned long long *ends_open, hipStream_t s);
 hipError_t launch_windows_packed(const WinArgs &a, hipStream_t s);
+
+// ---- table mode (kmer_table.hip): unordered canonical counts ---------------
+// Every counted forward window w contributes its canonical planar code
+// c = min(code(w), code(rc w)) (planar code: low plane bits of the k bases,
+// then the high plane bits, base 0 least significant; A=00 C=01 G=10 T=11 as
+// (hi, lo)); h = tab_mix(c) is a bijection.  h's top 10 bits pick the pass-1
+// partition, the next 10 the bucket (2^20 buckets), the low 44 bits are the
+// remainder kept in the table.  count(x) = C[c] for x in {c, rc c} when x
+// starts with P (palindromes: 2 C[c]) -- SURVEY.md App. A.6.
+constexpr uint32_t TAB_L1 = 10, TAB_L2 = 10;           // bits per partition level
+constexpr uint32_t TAB_NB = 1u << 10;                  // bins per level
+constexpr uint32_t TAB_NQ = 1u << (TAB_L1 + TAB_L2);   // buckets
+constexpr uint32_t TAB_RBITS = 64 - TAB_L1 - TAB_L2;   // remainder bits (44)
+constexpr uint64_t TAB_CMAX = 0xFFFFFull;              // entry count field (20 bits); larger -> big list
+constexpr uint64_t TAB_UNIT = 1ull << 18;              // pass-2 keys per workgroup
+constexpr uint32_t TAB_SLOTS = 8192;                   // final LDS table slots (96 KiB)
+constexpr uint32_t TAB_CAP = 7000;                     // distinct keys per range before it is split (+1024 in flight)
+
+__host__ __device__ inline uint64_t tab_mix(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
+}
+
+struct TabArgs {
+    const uint8_t *data;
+    uint64_t len;
+    const SeqLine *lines;          // by sequence ordinal (len 0: no windows)
+    uint64_t n_lines;
+    uint64_t lpw;                  // sequence lines per pass-1 workgroup
+    uint32_t nwg;                  // pass-1 workgroups
+    uint32_t k;
+    uint32_t plo, phi, pmask;      // prefix planes (base i at bit i), mask of |P| bits
+    uint32_t *H1;                  // hist: [p * nwg + g]
+    const uint64_t *H1s;           // scatter: exclusive scan of H1 (chunk-relative)
+    uint64_t base;                 // scatter: session keys before this chunk
+    uint64_t *B1;                  // scatter: hashed keys, partition-major
+    Record *recs;                  // non-ACGT windows
+    unsigned long long *rec_count;
+    uint64_t rec_cap;
+    unsigned int *err;
+};
+
+struct TabUnit {                   // pass 2: a run of one pass-1 partition's keys
+    uint64_t start;                // first key in B1
+    uint64_t hbase;                // H2 index of (bin 0, unit 0) of the partition
+    uint32_t len, u, nunits, pad;  // keys, unit index within the partition, units of the partition
+};
+
+struct TabBig {                    // entries whose count does not fit the 20-bit field
+    uint64_t h, count;
+};
+
+struct TabFinal {
+    const uint64_t *B2;            // keys by bucket
+    const uint64_t *start;         // TAB_NQ + 1 bucket starts in B2 (and in out)
+    uint64_t *out;                 // per bucket: nd[q] entries (rem << 20 | min(count, TAB_CMAX))
+    uint32_t *nd;
+    uint32_t sub_bits;             // initial split of a bucket's remainder range
+    uint32_t cap;                  // claims per range before it is split (<= TAB_CAP)
+    TabBig *big;
+    unsigned long long *big_count;
+    uint64_t big_cap;
+    unsigned int *err;
+    uint32_t k, plo, phi, pmask;
+    uint64_t inv1, inv2;           // inverses of tab_mix's multipliers
+    unsigned long long *stats;     // [0] canonical entries [1] Map keys [2] sum of Map counts
+};
+
+hipError_t launch_tab_hist1(const TabArgs &a, hipStream_t s);
+hipError_t launch_tab_scatter1(const TabArgs &a, hipStream_t s);
+hipError_t launch_tab_p1_offsets(const uint64_t *H1s, uint32_t nwg, uint64_t *out, hipStream_t s);
+hipError_t launch_tab_hist2(const uint64_t *B1, const TabUnit *units, uint32_t n_units, uint32_t *H2, hipStream_t s);
+hipError_t launch_tab_scatter2(const uint64_t *B1, const TabUnit *units, uint32_t n_units, const uint64_t *H2s,
+                               uint64_t *B2, hipStream_t s);
+hipError_t launch_tab_starts(const uint64_t *H2s, const TabUnit *pfirst, uint64_t total, uint64_t *start,
+                             hipStream_t s);
+hipError_t launch_tab_final(const TabFinal &a, uint32_t grid, hipStream_t s);
 hipError_t launch_synth_fastq(uint8_t *out, uint64_t seed, uint64_t first_read, uint64_t n_reads,
                               hipStream_t s);
 

@@ -1574,7 +1574,7 @@ __global__ __launch_bounds__(256) void seq_lines_kernel(const uint64_t *nl, uint
                 sl.start = st;
                 sl.len = L;
                 const uint64_t W = L - k + 1;
-                if (W - 1 > MAXREL) atomicOr(err, ERR_LINE_TOO_LONG);
+                if (err && W - 1 > MAXREL) atomicOr(err, ERR_LINE_TOO_LONG);   // (null: no order key, no limit)
                 w2 = 2 * W;
             }
         }

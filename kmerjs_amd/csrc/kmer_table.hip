@@ -1,0 +1,534 @@
+// kmer_table.hip — table mode: unordered canonical k-mer counts for
+// configurations whose result is too large for an ordered Map (BASELINE C3:
+// 100 M reads, k = 31, no prefix -> ~12 G distinct canonical keys; the
+// reference Map stops at 2^24 keys, lib/kmers.js:95).
+//
+// Same counting rule as the ordered paths (lib/kmers.js:88-100 on every
+// sequence line and on its complement, :151-155), stored canonically (SURVEY.md
+// App. A.6): a forward window w counts toward c = min(w, rc w) when w or rc(w)
+// starts with the prefix; the Map is recovered as {c: C, rc c: C} (filtered
+// by the prefix; palindromes 2 C).
+//
+// Pipeline (hash-partitioned, every write pass coalesced; no global atomics
+// on the data path):
+//   pass 1  per sequence line, one window per lane: 2-bit planes by ballot,
+//           canonical code, h = tab_mix(code).  hist1 counts keys per
+//           (workgroup, top-10-bit partition) in LDS; scatter1 re-reads the
+//           input (1.3 B/window, cheaper than a key buffer), ranks each key in
+//           its partition with an LDS atomic, sorts a round of 16 K keys in LDS
+//           and writes each partition's run contiguously.
+//   pass 2  per run of a partition: the next 10 bits, same LDS sort -> B2 in
+//           2^20 buckets, contiguous per bucket.
+//   final   one persistent workgroup per CU, bucket by bucket: an LDS
+//           open-addressing table (8 K slots, CAS claim, atomic count) merges
+//           the bucket's keys across the workgroup's 16 waves; ranges that do
+//           not fit are split and redone.  Entries (remainder, count) are
+//           written back to the bucket's range; Map statistics on the fly.
+#include "kmer_internal.hpp"
+
+namespace kmerhip {
+
+namespace {
+
+constexpr int TAB_RPL = 16;                  // segments (keys) per lane per round
+constexpr int TAB_WG1 = 1024;                // scatter workgroup (16 waves)
+constexpr int TAB_ROUND = TAB_RPL * TAB_WG1; // keys sorted in LDS per round
+constexpr uint64_t TAB_EMPTY = 1ull << 63;   // empty slot (remainders are < 2^44)
+constexpr uint64_t TAB_RMASK = (1ull << TAB_RBITS) - 1;
+
+__device__ __forceinline__ uint32_t tab_incl_sum(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
+}
+
+// Exclusive scan of one value per thread over a 1024-thread workgroup;
+// `ws` = 16 words of LDS scratch.  Returns the exclusive prefix, *total the sum.
+__device__ __forceinline__ uint32_t block_excl_1024(uint32_t v, uint32_t *ws, uint32_t *total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t inc = tab_incl_sum(v);
+    if (lane == 63) ws[wid] = inc;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+        const uint32_t x = ws[w];
+        before += w < wid ? x : 0u;
+        all += x;
+    }
+    *total = all;
+    return before + inc - v;
+}
+
+__device__ __forceinline__ uint32_t readlane32(uint32_t v, uint32_t i) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)i);
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t i) {
+    return (uint64_t)readlane32((uint32_t)v, i) | ((uint64_t)readlane32((uint32_t)(v >> 32), i) << 32);
+}
+
+// bits [s, s + 32) of the 128-bit value (hi:lo), s in [0, 64)
+__device__ __forceinline__ uint32_t funnel(uint64_t lo, uint64_t hi, uint32_t s) {
+    const uint64_t x = s ? (lo >> s) | (hi << (64 - s)) : lo;
+    return (uint32_t)x;
+}
+
+__device__ __forceinline__ bool is_acgt(uint32_t b) { return b == 'A' || b == 'C' || b == 'G' || b == 'T'; }
+
+// A wave's position in its workgroup's share of sequence lines.
+struct TabCur {
+    uint64_t m, end;               // next sequence ordinal of this wave, end of the workgroup's share
+    uint64_t seg;                  // first window of the next segment in line m
+    uint32_t stride;               // waves per workgroup
+};
+
+__device__ __forceinline__ void tab_record(const TabArgs &a, uint64_t pos, uint32_t strand) {
+    const unsigned long long i = atomicAdd(a.rec_count, 1ull);
+    if (i < a.rec_cap) {
+        Record r;
+        r.order = 0;
+        r.pos = pos;
+        r.len = a.k;
+        r.strand = strand;
+        a.recs[i] = r;
+    } else {
+        atomicOr(a.err, ERR_REC_OVERFLOW);
+    }
+}
+
+// One round of a wave: up to TAB_RPL segments of 64 windows (one window per
+// lane) from this wave's lines.  Phase 1 finds the segments (descriptors of
+// the next 16 lines prefetched by lanes 0..15) and issues every byte load;
+// phase 2 forms the windows.  key[j] = h of the lane's window in segment j,
+// bit j of the result set iff that window is counted.  Non-ACGT windows
+// become records (rec).  Each lane loads bytes seg + lane and seg + 64 + lane
+// of the line (a window needs <= 64 + 31 bytes after seg).
+template <int NS, int OFF>
+__device__ __forceinline__ uint32_t tab_round(const TabArgs &a, TabCur &c, bool rec, uint64_t (&key)[TAB_RPL]) {
+    const int lane = threadIdx.x & 63;
+    SeqLine d;
+    d.start = 0;
+    d.len = 0;
+    {
+        const uint64_t mi = c.m + (uint64_t)c.stride * (uint32_t)(lane & 15);
+        if (lane < 16 && mi < c.end) d = a.lines[mi];
+    }
+    const uint32_t k = a.k;
+    uint32_t li = 0;
+    uint64_t seg = c.seg;
+    uint32_t b0[NS], b1[NS], sli[NS];
+    uint64_t sseg[NS];
+    uint32_t have = 0;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        // next line (from li on) that still has a segment at `seg`
+        uint64_t L = 0;
+        while (li < 16) {
+            if (c.m + (uint64_t)c.stride * li >= c.end) {
+                li = 16;
+                break;
+            }
+            L = readlane64(d.len, li);
+            if (L >= k && seg < L - k + 1) break;
+            ++li;
+            seg = 0;
+        }
+        b0[j] = b1[j] = 'A';
+        sli[j] = li;
+        sseg[j] = seg;
+        if (li < 16) {
+            const uint64_t st = readlane64(d.start, li);
+            have |= 1u << j;
+            const uint64_t i0 = seg + (uint32_t)lane, i1 = i0 + 64;
+            if (i0 < L) b0[j] = a.data[st + i0];
+            if (i1 < L) b1[j] = a.data[st + i1];
+            seg += 64;
+        }
+    }
+    if (li >= 16) {
+        c.m += (uint64_t)c.stride * 16;
+        c.seg = 0;
+    } else {
+        c.m += (uint64_t)c.stride * li;
+        c.seg = seg;
+    }
+    const uint32_t kmask = k >= 32 ? ~0u : ((1u << k) - 1u);
+    const uint32_t sh = 32 - k;
+    uint32_t valid = 0;
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        if (!(have & (1u << j))) continue;      // (wave-uniform)
+        const uint32_t x0 = b0[j], x1 = b1[j];
+        const uint64_t l0 = __ballot(((x0 >> 1) ^ (x0 >> 2)) & 1u), l1 = __ballot(((x1 >> 1) ^ (x1 >> 2)) & 1u);
+        const uint64_t h0 = __ballot((x0 >> 2) & 1u), h1 = __ballot((x1 >> 2) & 1u);
+        const uint64_t e0 = __ballot(!is_acgt(x0)), e1 = __ballot(!is_acgt(x1));
+        const uint64_t s = sseg[j] + (uint32_t)lane;
+        if (s >= readlane64(d.len, sli[j]) - k + 1) continue;   // past the line's last window
+        const uint32_t flo = funnel(l0, l1, lane) & kmask, fhi = funnel(h0, h1, lane) & kmask;
+        const uint32_t fx = funnel(e0, e1, lane) & kmask;
+        const uint32_t rlo = __brev(~flo & kmask) >> sh, rhi = __brev(~fhi & kmask) >> sh, rx = __brev(fx) >> sh;
+        const bool fm = (((flo ^ a.plo) | (fhi ^ a.phi) | fx) & a.pmask) == 0;   // w starts with P
+        const bool rm = (((rlo ^ a.plo) | (rhi ^ a.phi) | rx) & a.pmask) == 0;   // rc(w) starts with P
+        if (fx == 0) {
+            if (fm || rm) {
+                const uint64_t cf = ((uint64_t)fhi << k) | flo, cr = ((uint64_t)rhi << k) | rlo;
+                key[OFF + j] = tab_mix(cf < cr ? cf : cr);
+                valid |= 1u << j;
+            }
+        } else if (rec) {
+            const uint64_t pos = readlane64(d.start, sli[j]) + s;
+            if (fm) tab_record(a, pos, 0);
+            if (rm) tab_record(a, pos, 1);
+        }
+    }
+    return valid << OFF;
+}
+
+__device__ __forceinline__ TabCur tab_cursor(const TabArgs &a, uint32_t waves) {
+    TabCur c;
+    const uint64_t m0 = (uint64_t)blockIdx.x * a.lpw;
+    c.end = m0 + a.lpw < a.n_lines ? m0 + a.lpw : a.n_lines;
+    c.m = m0 + (threadIdx.x >> 6);
+    c.seg = 0;
+    c.stride = waves;
+    return c;
+}
+
+}  // namespace
+
+// pass 1, histogram: keys per (workgroup, partition)
+__global__ __launch_bounds__(256) void tab_hist1_kernel(TabArgs a) {
+    __shared__ uint32_t hist[TAB_NB];
+    for (uint32_t i = threadIdx.x; i < TAB_NB; i += 256) hist[i] = 0;
+    __syncthreads();
+    TabCur c = tab_cursor(a, 4);
+    while (c.m < c.end) {
+        uint64_t key[TAB_RPL];
+        uint32_t v = tab_round<TAB_RPL, 0>(a, c, false, key);
+#pragma unroll
+        for (int j = 0; j < TAB_RPL; ++j)
+            if (v & (1u << j)) atomicAdd(&hist[key[j] >> (64 - TAB_L1)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < TAB_NB; i += 256) a.H1[(uint64_t)i * a.nwg + blockIdx.x] = hist[i];
+}
+
+// pass 1, scatter: the same keys, LDS-sorted by partition in rounds of 16 K,
+// written as one contiguous run per partition and round
+__global__ __launch_bounds__(TAB_WG1) void tab_scatter1_kernel(TabArgs a) {
+    __shared__ uint64_t srt[TAB_ROUND];
+    __shared__ uint64_t cur[TAB_NB];
+    __shared__ uint32_t bcnt[TAB_NB], bst[TAB_NB];
+    __shared__ uint32_t ws[16];
+    const uint32_t t = threadIdx.x;
+    cur[t] = a.base + a.H1s[(uint64_t)t * a.nwg + blockIdx.x];
+    bcnt[t] = 0;
+    __syncthreads();
+    TabCur c = tab_cursor(a, TAB_WG1 / 64);
+    while (true) {
+        uint64_t key[TAB_RPL];
+        uint32_t rank[TAB_RPL];
+        uint32_t v = 0;
+        if (c.m < c.end) v = tab_round<TAB_RPL / 2, 0>(a, c, true, key);
+        if (c.m < c.end) v |= tab_round<TAB_RPL / 2, TAB_RPL / 2>(a, c, true, key);
+#pragma unroll
+        for (int j = 0; j < TAB_RPL; ++j)
+            rank[j] = (v & (1u << j)) ? atomicAdd(&bcnt[key[j] >> (64 - TAB_L1)], 1u) : 0u;
+        __syncthreads();
+        uint32_t total;
+        const uint32_t cnt = bcnt[t];
+        bst[t] = block_excl_1024(cnt, ws, &total);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < TAB_RPL; ++j)
+            if (v & (1u << j)) srt[bst[key[j] >> (64 - TAB_L1)] + rank[j]] = key[j];
+        __syncthreads();
+        for (uint32_t i = t; i < total; i += TAB_WG1) {
+            const uint64_t h = srt[i];
+            const uint32_t p = (uint32_t)(h >> (64 - TAB_L1));
+            a.B1[cur[p] + (i - bst[p])] = h;
+        }
+        __syncthreads();
+        cur[t] += cnt;
+        bcnt[t] = 0;
+        if (!__syncthreads_or(c.m < c.end)) break;
+    }
+}
+
+// chunk-relative start of every pass-1 partition (+ the chunk's key total)
+__global__ void tab_p1_offsets_kernel(const uint64_t *H1s, uint32_t nwg, uint64_t *out) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < TAB_NB) out[p] = H1s[(uint64_t)p * nwg];
+}
+
+// pass 2, histogram: keys per (unit, bucket bin)
+__global__ __launch_bounds__(256) void tab_hist2_kernel(const uint64_t *B1, const TabUnit *units, uint32_t *H2) {
+    __shared__ uint32_t hist[TAB_NB];
+    for (uint32_t i = threadIdx.x; i < TAB_NB; i += 256) hist[i] = 0;
+    __syncthreads();
+    const TabUnit un = units[blockIdx.x];
+    const uint64_t *src = B1 + un.start;
+    for (uint32_t i = threadIdx.x; i < un.len; i += 256)
+        atomicAdd(&hist[(uint32_t)(src[i] >> TAB_RBITS) & (TAB_NB - 1)], 1u);
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < TAB_NB; b += 256) H2[un.hbase + (uint64_t)b * un.nunits + un.u] = hist[b];
+}
+
+// pass 2, scatter: a unit's keys into their buckets (LDS sort per round)
+__global__ __launch_bounds__(TAB_WG1) void tab_scatter2_kernel(const uint64_t *B1, const TabUnit *units,
+                                                               const uint64_t *H2s, uint64_t *B2) {
+    __shared__ uint64_t srt[TAB_ROUND];
+    __shared__ uint64_t cur[TAB_NB];
+    __shared__ uint32_t bcnt[TAB_NB], bst[TAB_NB];
+    __shared__ uint32_t ws[16];
+    const uint32_t t = threadIdx.x;
+    const TabUnit un = units[blockIdx.x];
+    const uint64_t *src = B1 + un.start;
+    cur[t] = H2s[un.hbase + (uint64_t)t * un.nunits + un.u];
+    bcnt[t] = 0;
+    __syncthreads();
+    for (uint32_t r0 = 0; r0 < un.len; r0 += TAB_ROUND) {
+        uint64_t key[TAB_RPL];
+        uint32_t rank[TAB_RPL];
+#pragma unroll
+        for (int j = 0; j < TAB_RPL; ++j) {
+            const uint32_t i = r0 + j * TAB_WG1 + t;
+            key[j] = i < un.len ? src[i] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < TAB_RPL; ++j) {
+            const uint32_t i = r0 + j * TAB_WG1 + t;
+            rank[j] = i < un.len ? atomicAdd(&bcnt[(uint32_t)(key[j] >> TAB_RBITS) & (TAB_NB - 1)], 1u) : 0u;
+        }
+        __syncthreads();
+        uint32_t total;
+        const uint32_t cnt = bcnt[t];
+        bst[t] = block_excl_1024(cnt, ws, &total);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < TAB_RPL; ++j) {
+            const uint32_t i = r0 + j * TAB_WG1 + t;
+            if (i < un.len) srt[bst[(uint32_t)(key[j] >> TAB_RBITS) & (TAB_NB - 1)] + rank[j]] = key[j];
+        }
+        __syncthreads();
+        for (uint32_t i = t; i < total; i += TAB_WG1) {
+            const uint64_t h = srt[i];
+            const uint32_t b = (uint32_t)(h >> TAB_RBITS) & (TAB_NB - 1);
+            B2[cur[b] + (i - bst[b])] = h;
+        }
+        __syncthreads();
+        cur[t] += cnt;
+        bcnt[t] = 0;
+        __syncthreads();
+    }
+}
+
+// bucket q = (p, b) starts at the scanned H2 entry of (p, b, unit 0)
+__global__ __launch_bounds__(256) void tab_starts_kernel(const uint64_t *H2s, const TabUnit *pfirst, uint64_t total,
+                                                         uint64_t *start) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < TAB_NQ) {
+        const TabUnit u = pfirst[q >> TAB_L2];
+        start[q] = H2s[u.hbase + (uint64_t)(q & (TAB_NB - 1)) * u.nunits];
+    }
+    if (q == 0) start[TAB_NQ] = total;
+}
+
+namespace {
+
+// Insert a remainder into the LDS table (linear probing).  More than `cap`
+// distinct keys (or a full probe) set *ovf: the range is redone in halves.
+// Inserts stop once *ovf is seen, so at most cap + 1024 slots are taken.
+__device__ __forceinline__ void tab_insert(uint64_t *tkey, uint32_t *tcnt, uint32_t *occ, volatile uint32_t *ovf,
+                                           uint64_t rem, uint32_t cap, unsigned int *err) {
+    uint32_t s = (uint32_t)rem & (TAB_SLOTS - 1);
+    for (uint32_t probe = 0; probe < TAB_SLOTS; ++probe) {
+        uint64_t cur = __hip_atomic_load(&tkey[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (cur == TAB_EMPTY) {
+            cur = atomicCAS((unsigned long long *)&tkey[s], (unsigned long long)TAB_EMPTY, (unsigned long long)rem);
+            if (cur == TAB_EMPTY) {                   // claimed: one more distinct key
+                cur = rem;
+                if (atomicAdd(occ, 1u) >= cap) *ovf = 1u;
+            }
+        }
+        if (cur == rem) {
+            if (atomicAdd(&tcnt[s], 1u) == 0xFFFFFFFFu) atomicOr(err, ERR_COUNT_OVERFLOW);
+            return;
+        }
+        s = (s + 1) & (TAB_SLOTS - 1);
+    }
+    *ovf = 1u;
+}
+
+__device__ __forceinline__ uint64_t tab_unmix(uint64_t x, uint64_t inv1, uint64_t inv2) {
+    x ^= x >> 33;
+    x *= inv2;
+    x ^= x >> 33;
+    x *= inv1;
+    x ^= x >> 33;
+    return x;
+}
+
+}  // namespace
+
+// final: per bucket, LDS hash table -> (remainder, count) entries in place of
+// the bucket's keys (into `out`), distinct count per bucket, Map statistics
+__global__ __launch_bounds__(TAB_WG1) void tab_final_kernel(TabFinal a) {
+    __shared__ uint64_t tkey[TAB_SLOTS];
+    __shared__ uint32_t tcnt[TAB_SLOTS];
+    __shared__ uint64_t stk[2 * 64];          // range stack [lo, hi) of remainders
+    __shared__ uint32_t occ, nout, sp;
+    __shared__ volatile uint32_t ovf;
+    const uint32_t t = threadIdx.x, lane = t & 63;
+    const uint32_t k = a.k;
+    const uint32_t kmask = k >= 32 ? ~0u : ((1u << k) - 1u), sh = 32 - k;
+    uint64_t st_canon = 0, st_keys = 0, st_sum = 0;
+    for (uint32_t q = blockIdx.x; q < TAB_NQ; q += gridDim.x) {
+        const uint64_t s0 = a.start[q], n = a.start[q + 1] - s0;
+        if (n == 0) {
+            if (t == 0) a.nd[q] = 0;
+            continue;
+        }
+        if (t == 0) {
+            const uint32_t nsub = 1u << a.sub_bits;
+            const uint64_t w = (1ull << TAB_RBITS) >> a.sub_bits;
+            for (uint32_t i = 0; i < nsub; ++i) {      // popped in ascending order
+                stk[2 * i] = (uint64_t)(nsub - 1 - i) * w;
+                stk[2 * i + 1] = (uint64_t)(nsub - i) * w;
+            }
+            sp = nsub;
+            nout = 0;
+        }
+        while (true) {
+            __syncthreads();
+            const uint32_t top = sp;
+            if (top == 0) break;
+            const uint64_t rlo = stk[2 * (top - 1)], rhi = stk[2 * (top - 1) + 1];
+            for (uint32_t i = t; i < TAB_SLOTS; i += TAB_WG1) {
+                tkey[i] = TAB_EMPTY;
+                tcnt[i] = 0;
+            }
+            __syncthreads();
+            if (t == 0) {
+                sp = top - 1;
+                occ = 0;
+                ovf = 0;
+            }
+            __syncthreads();
+            const uint64_t *src = a.B2 + s0;
+            for (uint64_t i = t; i < n; i += TAB_WG1) {
+                if (ovf) break;
+                const uint64_t rem = src[i] & TAB_RMASK;
+                if (rem >= rlo && rem < rhi) tab_insert(tkey, tcnt, &occ, &ovf, rem, a.cap, a.err);
+            }
+            __syncthreads();
+            if (ovf) {
+                if (t == 0) {
+                    if (rhi - rlo < 2 || sp + 2 > 64) {
+                        atomicOr(a.err, ERR_TAB_SPLIT);
+                    } else {
+                        const uint64_t mid = rlo + (rhi - rlo) / 2;
+                        stk[2 * sp] = mid;
+                        stk[2 * sp + 1] = rhi;
+                        stk[2 * sp + 2] = rlo;
+                        stk[2 * sp + 3] = mid;
+                        sp += 2;
+                    }
+                }
+                continue;
+            }
+            // emit the occupied slots (one LDS counter bump per wave and pass)
+            for (uint32_t i = t; i < TAB_SLOTS; i += TAB_WG1) {
+                const uint64_t rem = tkey[i];
+                const bool v = rem != TAB_EMPTY;
+                const uint64_t m = __ballot(v);
+                if (!m) continue;
+                uint32_t base = 0;
+                if (lane == (uint32_t)(__ffsll((long long)m) - 1)) base = atomicAdd(&nout, (uint32_t)__popcll(m));
+                base = __shfl(base, __ffsll((long long)m) - 1);
+                if (!v) continue;
+                const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                const uint64_t cnt = tcnt[i];
+                a.out[s0 + pos] = (rem << 20) | (cnt < TAB_CMAX ? cnt : TAB_CMAX);
+                const uint64_t h = ((uint64_t)q << TAB_RBITS) | rem;
+                if (cnt >= TAB_CMAX) {
+                    const unsigned long long bi = atomicAdd(a.big_count, 1ull);
+                    if (bi < a.big_cap) {
+                        a.big[bi].h = h;
+                        a.big[bi].count = cnt;
+                    } else {
+                        atomicOr(a.err, ERR_BIG_OVERFLOW);
+                    }
+                }
+                // Map view of this canonical entry (App. A.6)
+                const uint64_t code = tab_unmix(h, a.inv1, a.inv2);
+                const uint32_t lo = (uint32_t)code & kmask, hi = (uint32_t)(code >> k) & kmask;
+                const uint32_t rlo2 = __brev(~lo & kmask) >> sh, rhi2 = __brev(~hi & kmask) >> sh;
+                const bool pal = lo == rlo2 && hi == rhi2;
+                const bool fs = (((lo ^ a.plo) | (hi ^ a.phi)) & a.pmask) == 0;
+                const bool rs = !pal && (((rlo2 ^ a.plo) | (rhi2 ^ a.phi)) & a.pmask) == 0;
+                st_canon += 1;
+                st_keys += (fs ? 1u : 0u) + (rs ? 1u : 0u);
+                st_sum += (fs ? (pal ? 2 * cnt : cnt) : 0) + (rs ? cnt : 0);
+            }
+        }
+        if (t == 0) a.nd[q] = nout;
+    }
+    // workgroup totals -> one atomic per wave
+    for (int d = 32; d >= 1; d >>= 1) {
+        st_canon += __shfl_xor(st_canon, d);
+        st_keys += __shfl_xor(st_keys, d);
+        st_sum += __shfl_xor(st_sum, d);
+    }
+    if (lane == 0 && st_canon) {
+        atomicAdd(&a.stats[0], (unsigned long long)st_canon);
+        atomicAdd(&a.stats[1], (unsigned long long)st_keys);
+        atomicAdd(&a.stats[2], (unsigned long long)st_sum);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+hipError_t launch_tab_hist1(const TabArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(tab_hist1_kernel, dim3(a.nwg), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_tab_scatter1(const TabArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(tab_scatter1_kernel, dim3(a.nwg), dim3(TAB_WG1), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_tab_p1_offsets(const uint64_t *H1s, uint32_t nwg, uint64_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(tab_p1_offsets_kernel, dim3(TAB_NB / 256), dim3(256), 0, s, H1s, nwg, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_tab_hist2(const uint64_t *B1, const TabUnit *units, uint32_t n_units, uint32_t *H2, hipStream_t s) {
+    hipLaunchKernelGGL(tab_hist2_kernel, dim3(n_units), dim3(256), 0, s, B1, units, H2);
+    return hipGetLastError();
+}
+
+hipError_t launch_tab_scatter2(const uint64_t *B1, const TabUnit *units, uint32_t n_units, const uint64_t *H2s,
+                               uint64_t *B2, hipStream_t s) {
+    hipLaunchKernelGGL(tab_scatter2_kernel, dim3(n_units), dim3(TAB_WG1), 0, s, B1, units, H2s, B2);
+    return hipGetLastError();
+}
+
+hipError_t launch_tab_starts(const uint64_t *H2s, const TabUnit *pfirst, uint64_t total, uint64_t *start,
+                             hipStream_t s) {
+    hipLaunchKernelGGL(tab_starts_kernel, dim3(TAB_NQ / 256), dim3(256), 0, s, H2s, pfirst, total, start);
+    return hipGetLastError();
+}
+
+hipError_t launch_tab_final(const TabFinal &a, uint32_t grid, hipStream_t s) {
+    hipLaunchKernelGGL(tab_final_kernel, dim3(grid), dim3(TAB_WG1), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace kmerhip

@@ -1,0 +1,160 @@
+"""GPU parity of table mode (KMER_FLAG_UNORDERED, kmer_table.hip): the same
+k-mer -> count Map as the reference (lib/kmers.js:88-100, :151-155), entries
+sorted by key bytes instead of insertion order.  Checked against the goldens
+(size, sum, lines; full entries where the golden holds them) and the oracle
+(every entry, sorted)."""
+import numpy as np
+import pytest
+
+from tests.util import first_diff
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def native():
+    from kmerjs_amd import _native
+    return _native
+
+
+def _table_ok(c):
+    p = c["prefix"]
+    return c["step"] == 1 and c["k"] <= 32 and len(p) <= c["k"] and all(ch in "ACGT" for ch in p)
+
+
+def _check_cases(native, golden, inputs, flags):
+    from oracle import oracle
+    bad = []
+    by_cfg = {}
+    for c in golden["cases"]:
+        if _table_ok(c):
+            by_cfg.setdefault((c["prefix"], c["k"]), []).append(c)
+    for (p, k), cases in by_cfg.items():
+        ctr = native.Counter(k=k, prefix=p.encode(), flags=native.FLAG_UNORDERED | flags)
+        try:
+            for c in cases:
+                r = ctr.count_buffer(inputs[c["input"]])
+                e = r.entries()
+                ok = len(e) == c["size"] and sum(v for _, v in e) == c["sum"] and r.lines == c["lines"]
+                if ok and "entries" in c:
+                    ok = e == sorted((kk.encode("latin-1"), v) for kk, v in c["entries"])
+                if ok and "entries" not in c:
+                    ok = e == sorted(oracle.count_buffer(inputs[c["input"]], p.encode(), k, 1))
+                if ok:
+                    _, keys, total = ctr.table_stats()
+                    ok = keys == c["size"] and total == c["sum"]
+                if not ok:
+                    bad.append((c["input"], p, k, len(e), c["size"], r.lines, c["lines"]))
+        finally:
+            ctr.close()
+    return bad
+
+
+def test_table_every_golden_case(native, golden, inputs):
+    assert sum(_table_ok(c) for c in golden["cases"]) >= 455
+    bad = _check_cases(native, golden, inputs, 0)
+    assert not bad, bad[:5]
+
+
+def test_table_range_splits(native, golden, inputs):
+    # 64-key LDS ranges: every bucket with more keys is split (and redone)
+    bad = _check_cases(native, golden, inputs, native.FLAG_TABLE_SPLIT_TEST)
+    assert not bad, bad[:5]
+
+
+def _device_input(n, seed=3):
+    import torch
+    from kmerjs_amd import synth_fastq_device
+    buf = torch.empty(n * 317, dtype=torch.uint8, device="cuda")
+    synth_fastq_device(buf.data_ptr(), seed, 0, n)
+    torch.cuda.synchronize()
+    return buf
+
+
+@pytest.mark.parametrize("k,prefix", [(31, b""), (16, b""), (21, b"A"), (16, b"ATGAC"), (32, b"GT")])
+def test_table_synthetic_vs_oracle(native, k, prefix):
+    from oracle import oracle
+    buf = _device_input(100_000)
+    host = buf.cpu().numpy().tobytes()
+    want = sorted(oracle.count_buffer(host, prefix, k, 1))
+    ctr = native.Counter(k=k, prefix=prefix, flags=native.FLAG_UNORDERED)
+    ctr.reset()
+    ctr.feed_device(buf.data_ptr(), len(host))
+    got = ctr.finish().entries()
+    canon, keys, total = ctr.table_stats()
+    ctr.close()
+    assert len(got) == len(want)
+    assert first_diff(got, want) is None
+    assert keys == len(want) and total == sum(v for _, v in want)
+
+
+def test_table_chunked_feeds_match_one_feed(native):
+    import torch
+    buf = _device_input(60_000, seed=9)
+    n = buf.numel()
+    ctr = native.Counter(k=31, prefix=b"", flags=native.FLAG_UNORDERED)
+    one = ctr.count_buffer(buf.cpu().numpy().tobytes()).entries()
+    ctr.reset()
+    cuts = [0, 317 * 7, 317 * 20_000, 317 * 20_001, 317 * 45_000, n]
+    for lo, hi in zip(cuts, cuts[1:]):
+        ctr.feed_device(buf.data_ptr() + lo, hi - lo)
+    torch.cuda.synchronize()
+    many = ctr.finish().entries()
+    ctr.close()
+    assert many == one
+
+
+def test_table_realistic_reads_with_n(native):
+    from oracle import oracle
+    rng = np.random.default_rng(12)
+    arr = np.frombuffer(bytearray(oracle.synth_fastq(4, 0, 20000)), dtype=np.uint8).reshape(-1, 317).copy()
+    seq = arr[:, 13:163]
+    seq[rng.random(seq.shape) < 0.002] = ord("N")
+    seq[rng.random(len(seq)) < 0.8, 0] = ord("N")
+    arr[:, 13:163] = seq
+    data = arr.tobytes()
+    for k, p in ((16, b""), (31, b""), (21, b"GT")):
+        want = sorted(oracle.count_buffer(data, p, k, 1))
+        ctr = native.Counter(k=k, prefix=p, flags=native.FLAG_UNORDERED)
+        got = ctr.count_buffer(data).entries()
+        ctr.close()
+        assert first_diff(got, want) is None, (k, p)
+
+
+def test_table_big_counts(native):
+    # one canonical k-mer seen > 2^20 times (count beyond the entry's 20-bit
+    # field -> big list), plus palindromes (even k: AT-repeats)
+    from oracle import oracle
+    polya = b"".join(b"@r%010d\n%s\n+\n%s\n" % (i, b"A" * 150, b"I" * 150) for i in range(9000))
+    at = b"".join(b"@s%010d\n%s\n+\n%s\n" % (i, b"AT" * 75, b"I" * 150) for i in range(300))
+    data = polya + at
+    for k, p in ((16, b""), (16, b"A"), (15, b"T"), (15, b"")):
+        want = sorted(oracle.count_buffer(data, p, k, 1))
+        ctr = native.Counter(k=k, prefix=p, flags=native.FLAG_UNORDERED)
+        got = ctr.count_buffer(data).entries()
+        ctr.close()
+        assert got == want, (k, p, got[:4], want[:4])
+    assert dict(want).get(b"A" * 15) == 9000 * 136
+
+
+def test_table_matches_ordered_path_at_scale(native):
+    # 2 M reads, k = 31, no prefix (C3's configuration): the table's Map keys
+    # and counts equal the ordered dense path's result (960 windows per 2 reads)
+    buf = _device_input(2_000_000, seed=3)
+    ctr = native.Counter(k=31, prefix=b"", flags=native.FLAG_UNORDERED)
+    ctr.reset()
+    ctr.feed_device(buf.data_ptr(), buf.numel())
+    ctr.finish(want_result=False)
+    canon, keys, total = ctr.table_stats()
+    ctr.close()
+    assert total == 2_000_000 * 2 * 120
+    assert keys == 2 * canon            # odd k: no palindromes
+    ordered = native.Counter(k=31, prefix=b"")
+    ordered.reset()
+    ordered.feed_device(buf.data_ptr(), buf.numel())
+    ordered.finish(want_result=False)
+    _, d_counts, _, n = ordered.result_device()
+    from kmerjs_amd.multi import device_u64
+    ordered_sum = int(device_u64(d_counts, n, buf.device).sum().item())
+    ordered.close()
+    assert n == keys and ordered_sum == total
