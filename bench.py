@@ -32,8 +32,11 @@ def windows_per_read(k):
     return 2 * max(0, READ_LEN - k + 1)
 
 
-def cpu_baseline(k, prefix, seconds_target=10.0):
-    """Oracle (C restatement, 1 thread) on a bounded sample of the same workload."""
+def cpu_baseline(k, prefix, seconds_target=8.0):
+    """Oracle (C restatement) on a bounded sample of the same workload: one
+    thread, and one thread per host core on record-aligned shards whose
+    per-shard Maps are then merged (whole-job time, merge included)."""
+    from concurrent.futures import ThreadPoolExecutor
     from oracle import oracle
     n = 20000
     data = oracle.synth_fastq(1, 0, n)
@@ -44,10 +47,27 @@ def cpu_baseline(k, prefix, seconds_target=10.0):
     data = oracle.synth_fastq(1, 0, n)
     t0 = time.perf_counter()
     oracle.count_buffer(data, prefix, k, 1)
-    dt = time.perf_counter() - t0
-    return {"value": n * windows_per_read(k) / dt, "unit": "k-mers/s", "cores": 1, "kind": "port",
+    dt1 = time.perf_counter() - t0
+    # one thread per core (the box's CPU share is 16; ctypes calls release the GIL)
+    cores = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    nt = n * cores
+    data = oracle.synth_fastq(1, 0, nt)
+    per = (nt + cores - 1) // cores
+    shards = [data[i * per * RECORD:min(nt, (i + 1) * per) * RECORD] for i in range(cores)]
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(cores) as ex:
+        parts = list(ex.map(lambda b: oracle.count_buffer(b, prefix, k, 1), shards))
+    merged = {}
+    for part in parts:                       # shard order = read order: first occurrence kept
+        for key, v in part:
+            merged[key] = merged.get(key, 0) + v
+    dtn = time.perf_counter() - t0
+    return {"value": n * windows_per_read(k) / dt1, "unit": "k-mers/s", "cores": 1, "kind": "port",
             "sample": "%d synthetic reads (seed 1), k=%d, prefix %r, oracle/kmer_oracle.c single-threaded, %.1f s"
-                      % (n, k, prefix.decode(), dt)}
+                      % (n, k, prefix.decode(), dt1),
+            "threads": {"value": nt * windows_per_read(k) / dtn, "unit": "k-mers/s", "cores": cores, "kind": "port",
+                        "sample": "%d reads in %d record-aligned shards, one thread each, + merge of the per-shard "
+                                  "Maps; %.1f s" % (nt, cores, dtn)}}
 
 
 def count_windows(lines_bytes_lengths, first_line, k):
@@ -82,7 +102,7 @@ def make_workload(args, rank, world, dev):
     import torch.distributed as dist
     from kmerjs_amd import synth_fastq_device
     from kmerjs_amd.multi import shard_plan
-    if args.config in ("c2", "c3"):
+    if args.config in ("c2", "c3", "c4"):
         plan = shard_plan(args.reads, rank)
         nbytes = args.reads * RECORD
         buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
@@ -128,17 +148,29 @@ def make_workload(args, rank, world, dev):
     raise SystemExit("unknown config " + args.config)
 
 
-def load_traffic(args):
+def load_traffic(args, kernel):
+    """HBM bytes per launch of `kernel` in this config, from the committed PMC
+    passes (profiles/pmc_traffic.json, keyed by config name and kernel)."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     try:
         with open(path) as f:
             d = json.load(f)
-        key = "k%d_%s_r%d" % (args.k, args.prefix, args.reads)
-        return d.get(key, {}).get("hbm_bytes_per_launch")
+        e = d.get(args.config, {})
+        if e.get("reads") not in (None, args.reads) or e.get("k") not in (None, args.k) or \
+                e.get("prefix") not in (None, args.prefix):
+            return None
+        return e.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
     except Exception:
         return None
+
+
+# table mode (C3): algorithmic bytes of each phase per launch, from the
+# pass-1 key count n (8-B keys) -- DESIGN.md §4
+def table_phase_bytes(nbytes, n_keys, canonical, sub_bits):
+    return {"lines": 2 * nbytes, "hist1": nbytes, "scatter1": nbytes + 8 * n_keys, "hist2": 8 * n_keys,
+            "scatter2": 16 * n_keys, "final": 8 * n_keys * (1 << sub_bits) + 8 * canonical}
 
 
 def main():
@@ -155,8 +187,9 @@ def main():
     ap.add_argument("--no-pcie", action="store_true")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="sessions in rotation (>= 2: a step's finish overlaps the next steps' scans)")
-    ap.add_argument("--config", default="c2", choices=("c1", "c2", "c3", "c5"),
-                    help="BASELINE.json config: c2 (default, the headline), c3 no-prefix k=31, c5 long contigs k=21")
+    ap.add_argument("--config", default="c2", choices=("c1", "c2", "c3", "c4", "c5"),
+                    help="BASELINE.json config: c2 (default, the headline); c3 100 M reads, k=31, no prefix "
+                         "(table mode); c4 125 M reads per GPU (1 B on 8), k=16; c5 long contigs k=21")
     ap.add_argument("--contig-bytes", type=int, default=1_000_000_000, help="c5: bytes of contigs per GPU")
     ap.add_argument("--merge", default="hits", choices=("hits", "alltoall", "gather"),
                     help="N > 1: hits: key-range all-to-all of the hits + per-rank finish (result distributed by "
@@ -164,13 +197,28 @@ def main():
     args = ap.parse_args()
     # per-config defaults (explicit flags still win)
     argv = " ".join(sys.argv)
+    from kmerjs_amd._native import FLAG_UNORDERED
     if args.config == "c3":
+        # hash-table pressure: 24 G windows, ~12 G distinct canonical 31-mers -- far
+        # beyond an ordered Map (the reference stops at 2^24 keys), so table mode
         if "--k" not in argv:
             args.k = 31
         if "--prefix" not in argv:
             args.prefix = ""
         if "--reads" not in argv:
-            args.reads = 4_000_000       # 0.96 G windows: C3's 100 M reads (24 G) exceed one session's 2^32 ranks
+            args.reads = 100_000_000
+        if "--seed" not in argv:
+            args.seed = 3
+        args.flags |= FLAG_UNORDERED
+    if args.config == "c4":
+        # 1 B reads over 8 GPUs: 125 M per GPU (39.6 GB shard), seed 4
+        if "--reads" not in argv:
+            args.reads = 125_000_000
+        if "--seed" not in argv:
+            args.seed = 4
+    table = bool(args.flags & FLAG_UNORDERED)
+    if table and args.gpus > 1:
+        raise SystemExit("table mode is single-GPU in this build (see DESIGN.md)")
     if args.config == "c5" and "--k" not in argv:
         args.k = 21
     if args.config != "c2":
@@ -215,6 +263,7 @@ def main():
     ctr = ctrs[0]
     total_lines = wl["total_lines"]
     tile_ms, feed_ms_l = [], []
+    phase_ms = []                 # table mode: per-step phase times
     inflight = []                 # (session, recorded) fed, finish not yet queued
 
     def feed(c):
@@ -229,7 +278,7 @@ def main():
             scan_ms, feed_ms, _ = c.last_timing(finish=False)
             tile_ms.append(scan_ms)
             feed_ms_l.append(feed_ms)
-        multi_finish(c)
+        multi_finish(c, rec)
 
     def step(i, record):
         feed(ctrs[i % nctx])      # (its previous finish is ahead of it on its stream)
@@ -241,9 +290,11 @@ def main():
         while inflight:
             retire()
 
-    def multi_finish(c):
+    def multi_finish(c, record=False):
         if world == 1:
             c.finish(want_result=False)
+            if table and record:
+                phase_ms.append(c.phase_times())
         elif args.merge == "hits":
             finish_exchange(c, args.k, len(prefix), total_lines)
         elif args.merge == "alltoall":
@@ -277,15 +328,20 @@ def main():
     # counted on the device (a C3-sized result has ~10^9 entries): ordered device
     # entries (every rank's key range after the all-to-all, or all on rank 0) +
     # the host-side records (non-ACGT windows, on rank 0)
-    d_keys, d_cnt, d_first, n_dev = ctr.result_device() if (rank == 0 or args.merge != "gather") else (0, 0, 0, 0)
-    dev_sum = int(device_u64(d_cnt, n_dev, dev).sum().item()) if n_dev else 0
-    if n_dev > 1:
-        f = device_u64(d_first, n_dev, dev)
-        assert bool((f[1:] > f[:-1]).all().item()), "first-occurrence order broken"
-    n_rec, rec_sum = 0, 0
-    if rank == 0:
-        kb, off, cnts, firsts = ctr.records_export()
-        n_rec, rec_sum = len(cnts), int(cnts.sum())
+    canonical = None
+    if table:
+        canonical, n_keys_map, map_sum = ctr.table_stats()
+        n_dev, dev_sum, n_rec, rec_sum = n_keys_map, map_sum, 0, 0
+    else:
+        d_keys, d_cnt, d_first, n_dev = ctr.result_device() if (rank == 0 or args.merge != "gather") else (0, 0, 0, 0)
+        dev_sum = int(device_u64(d_cnt, n_dev, dev).sum().item()) if n_dev else 0
+        if n_dev > 1:
+            f = device_u64(d_first, n_dev, dev)
+            assert bool((f[1:] > f[:-1]).all().item()), "first-occurrence order broken"
+        n_rec, rec_sum = 0, 0
+        if rank == 0:
+            kb, off, cnts, firsts = ctr.records_export()
+            n_rec, rec_sum = len(cnts), int(cnts.sum())
     tot = torch.tensor([n_dev + n_rec, dev_sum + rec_sum], dtype=torch.int64, device=dev)
     if world > 1:
         dist.all_reduce(tot)
@@ -307,7 +363,33 @@ def main():
         ms_per_step = elapsed / args.steps * 1e3
         value = windows_step * args.steps / elapsed
         kern_ms = sum(tile_ms) / len(tile_ms)
-        if args.config == "c3" or (args.prefix and len(args.prefix) <= 3) or not args.prefix:
+        # step-level fraction: SURVEY.md §8d algorithmic bytes per window (input
+        # B_in + table B_table) x windows of the step / step time
+        b_in = RECORD / windows_per_read(args.k) if args.config in ("c2", "c3", "c4") else nbytes / max(1, wl["windows"])
+        if table:
+            b_table = 16.0      # SURVEY §8d hash path: 16-B slot read + write per forward position / 2 windows
+        else:
+            b_table = 24.0 * accepted / max(1, windows_step)  # one slot update per accepted window
+        step_bytes = (b_in + b_table) * windows_step / world
+        step_frac = step_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS
+        phases = None
+        if table:
+            # the dominant phase of the table pipeline (HIP events on the library's stream)
+            phases = {kname: sum(p[kname] for p in phase_ms) / len(phase_ms) for kname in phase_ms[0]}
+            n_keys = accepted // 2 if not args.prefix else None
+            mean = (n_keys or 0) >> 20
+            sub_bits = 0
+            while sub_bits < 16 and (mean >> sub_bits) > 6000:
+                sub_bits += 1
+            pbytes = table_phase_bytes(nbytes, n_keys or 0, canonical, sub_bits)
+            kern_name = max(phases, key=lambda x: phases[x])
+            kern_ms = phases[kern_name]
+            algo_bytes = pbytes[kern_name]
+            kern_name = {"lines": "nl_count_kernel + nl_write_kernel + seq_lines_kernel",
+                         "hist1": "tab_hist1_kernel (+ scan)", "scatter1": "tab_scatter1_kernel",
+                         "hist2": "tab_hist2_kernel (+ scan)", "scatter2": "tab_scatter2_kernel",
+                         "final": "tab_final_kernel"}[kern_name]
+        elif (args.prefix and len(args.prefix) <= 3) or not args.prefix:
             # dense-hit path: the timed kernels are the two streaming newline passes
             kern_name = "nl_count_kernel + nl_write_kernel (dense-hit path)"
             algo_bytes = 2 * nbytes
@@ -317,7 +399,7 @@ def main():
             kern_name = "scan_planes_kernel"
             algo_bytes = nbytes + 24 * (accepted / world)
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
-        traffic = load_traffic(args)
+        traffic = load_traffic(args, kern_name.split(" ")[0])
         out = {
             "metric": "k-mers/sec + distinct-kmers/sec, k=%d 150bp synthetic FASTQ, 1/2/4/8 GPU" % args.k,
             "value": value,
@@ -334,7 +416,9 @@ def main():
                      "c5": "synthetic contigs (numpy PCG64, seed 5 + rank)"}.get(
                          args.config, "synthetic (on-device splitmix64 FASTQ, 317 B records, seed %d)" % args.seed),
             "config": {"workload": wl["desc"], "name": args.config,
-                       "reads_per_gpu": args.reads if args.config in ("c2", "c3") else None,
+                       "reads_per_gpu": args.reads if args.config in ("c2", "c3", "c4") else None,
+                       "mode": "table (unordered canonical counts, KMER_FLAG_UNORDERED)" if table
+                               else "ordered (reference Map insertion order)",
                        "k": args.k, "prefix": args.prefix, "windows_per_step": windows_step,
                        "bytes_per_gpu": nbytes,
                        "pipeline": ("%d sessions in rotation: finishes overlap later scans" % nctx if nctx > 1
@@ -350,8 +434,12 @@ def main():
             "feed_device_ms": sum(feed_ms_l) / len(feed_ms_l),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kern_name,
-                         "algorithmic_bytes_per_launch": algo_bytes, "kernel_ms": kern_ms},
+                         "algorithmic_bytes_per_launch": algo_bytes, "kernel_ms": kern_ms,
+                         "step_frac": step_frac, "step_bytes_per_window": b_in + b_table},
         }
+        if phases is not None:
+            out["table_phase_ms"] = phases
+            out["canonical_kmers"] = canonical
         if not args.no_pcie and world == 1:
             # PCIe-inclusive rate (host bytes -> H2D -> count -> ordered host result); never `value`
             host = buf.cpu().numpy().tobytes()

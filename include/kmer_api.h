@@ -178,7 +178,7 @@ kmer_status kmer_table_stats(kmer_ctx *ctx, uint64_t *canonical, uint64_t *keys,
 /* The table itself, in device memory.  2^20 buckets; bucket q holds
  * bucket_len[q] (uint32) entries at entries[bucket_start[q] ..] (uint64 each:
  * remainder << 20 | count, count == 0xFFFFF meaning "see the big list").
- * h = q << 44 | remainder is a bijective mix (murmur3 fmix64) of the canonical
+ * h = q << 44 | remainder = c * 0x9E3779B97F4A7C15 (mod 2^64), a bijection of the canonical
  * planar code c = min(code(w), code(rc w)) with code = hi_plane << k | lo_plane,
  * base i of the k-mer at bit i of each plane, A/C/G/T = (hi,lo) 00/01/10/11.
  * big = n_big {uint64 h, uint64 count} pairs.  Valid until the next reset. */
@@ -191,6 +191,13 @@ kmer_status kmer_table_device(kmer_ctx *ctx, const void **d_entries, const void 
  * (compaction + sort + decode).  Waits for the last finish only when
  * finish_ms is non-NULL. */
 kmer_status kmer_last_timing(kmer_ctx *ctx, double *scan_ms, double *feed_ms, double *finish_ms);
+
+/* Device time per phase since the last reset (HIP events on the context's
+ * stream, ms; feeds summed).  Table mode: "lines" (newline array, sequence
+ * lines), "hist1" (+ its scan), "scatter1", "hist2" (+ scan), "scatter2",
+ * "final"; ordered modes: "scan", "feed", "finish" as kmer_last_timing.
+ * Up to `max` entries are written; *n = the number of phases. */
+kmer_status kmer_phase_times(kmer_ctx *ctx, uint32_t max, const char **names, double *ms, uint32_t *n);
 
 const char *kmer_status_string(kmer_status s);
 const char *kmer_last_error(const kmer_ctx *ctx);

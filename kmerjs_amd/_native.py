@@ -7,7 +7,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libkmerhip.so")
+LIB_PATH = os.environ.get("KMERHIP_LIB_EXPERIMENT") or os.path.join(HERE, "libkmerhip.so")   # (A/B builds only)
 
 KMER_OK = 0
 STATUS = {0: "ok", 1: "i/o error", 2: "bad parameter", 3: "out of memory", 4: "device error",
@@ -26,7 +26,7 @@ EXPORTS = ["kmer_open", "kmer_close", "kmer_count_file", "kmer_count_buffer", "k
            "kmer_records_export", "kmer_records_import", "kmer_records_clear", "kmer_result_device", "kmer_set_position",
            "kmer_lines", "kmer_result_size", "kmer_result_lines", "kmer_result_get",
            "kmer_result_arrays", "kmer_result_firsts", "kmer_result_free", "kmer_synth_fastq_device",
-           "kmer_last_timing", "kmer_table_stats", "kmer_table_device",
+           "kmer_last_timing", "kmer_phase_times", "kmer_table_stats", "kmer_table_device",
            "kmer_status_string", "kmer_last_error", "kmer_version"]
 
 
@@ -87,6 +87,8 @@ def _load():
         "kmer_synth_fastq_device": (ctypes.c_int, [vp, u64, u64, u64, vp]),
         "kmer_last_timing": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                             ctypes.POINTER(ctypes.c_double)]),
+        "kmer_phase_times": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_char_p),
+                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32)]),
         "kmer_table_stats": (ctypes.c_int, [vp, pu64, pu64, pu64]),
         "kmer_table_device": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp),
                                              ctypes.POINTER(vp), pu64]),
@@ -274,6 +276,14 @@ class Counter:
         self._check(LIB.kmer_result_device(self.h, ctypes.byref(k), ctypes.byref(c), ctypes.byref(f),
                                            ctypes.byref(n)), "result_device")
         return k.value or 0, c.value or 0, f.value or 0, n.value
+
+    def phase_times(self):
+        """{phase: device ms since the last reset} (table mode: lines, hist1, scatter1, hist2, scatter2, final)."""
+        names = (ctypes.c_char_p * 16)()
+        ms = (ctypes.c_double * 16)()
+        n = ctypes.c_uint32()
+        self._check(LIB.kmer_phase_times(self.h, 16, names, ms, ctypes.byref(n)), "phase_times")
+        return {names[i].decode(): ms[i] for i in range(min(n.value, 16))}
 
     def table_stats(self):
         """Table mode: (distinct canonical k-mers, distinct Map keys, sum of Map counts)."""

@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -192,6 +193,8 @@ struct kmer_ctx {
     std::vector<std::vector<uint64_t>> t_coff;   // per chunk: TAB_NB + 1 partition starts (chunk-relative)
     uint64_t t_canon = 0, t_nkeys = 0, t_sum = 0, t_nbig = 0;   // last finish
     bool t_done = false;           // a table finish holds results
+    hipEvent_t tev[8] = {};        // table phase events
+    double t_ms[6] = {};           // table phase times since the reset: lines, hist1, scatter1, hist2, scatter2, final
     int n_cu = 0;
     // timing (HIP events on the context stream)
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr;
@@ -864,13 +867,21 @@ kmer_status windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n
 // Pass 1 of one chunk: its sequence lines, then per workgroup share of lines
 // a histogram of keys by partition, a scan, and the scatter into tb1 after
 // the session's earlier keys.  Non-ACGT windows go to the host map.
+float ev_ms(kmer_ctx *c, hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) ms = 0.f;
+    return ms;
+}
+
 kmer_status table_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s) {
     const uint64_t li0 = c->host_lines;
     HIPCHK(c, hipEventRecord(c->ev0, s));
+    HIPCHK(c, hipEventRecord(c->tev[0], s));
     uint64_t n_nl = 0, n_seq = 0;
     kmer_status st = chunk_lines(c, d, len, n_tiles, s, false, &n_nl, &n_seq);
     if (st) return st;
     HIPCHK(c, launch_pos_after(c->d_pos, li0 + n_nl, d, len, c->d_ends_open, s));
+    HIPCHK(c, hipEventRecord(c->tev[1], s));
     c->host_lines = li0 + n_nl;
     if (n_seq) {
         TabArgs a;
@@ -903,7 +914,10 @@ kmer_status table_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_t
         HIPCHK(c, hipMemcpyAsync(off.data(), c->tp1.p, TAB_NB * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipMemcpyAsync(c->h_small + 14, c->tHs.p + nh - 1, 8, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipMemcpyAsync(c->h_small + 15, c->tH.p + nh - 1, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipEventRecord(c->tev[2], s));
         HIPCHK(c, hipStreamSynchronize(s));
+        c->t_ms[0] += ev_ms(c, c->tev[0], c->tev[1]);
+        c->t_ms[1] += ev_ms(c, c->tev[1], c->tev[2]);
         const uint64_t n_c = c->h_small[14] + (uint32_t)c->h_small[15];
         off[TAB_NB] = n_c;
         HIPCHK(c, c->tb1.ensure(c->t_keys + n_c, s, true, c->t_keys));
@@ -915,13 +929,19 @@ kmer_status table_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_t
             a.rec_count = c->d_rec_count;
             a.rec_cap = c->recs.cap;
             HIPCHK(c, hipMemsetAsync(c->d_rec_count, 0, 8, s));
+            HIPCHK(c, hipEventRecord(c->tev[2], s));
             HIPCHK(c, launch_tab_scatter1(a, s));
+            HIPCHK(c, hipEventRecord(c->tev[3], s));
             HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
             HIPCHK(c, hipStreamSynchronize(s));
+            const float ms_s1 = ev_ms(c, c->tev[2], c->tev[3]);
             const uint32_t e = (uint32_t)c->h_small[5];
             st = check_err(c, e);
             if (st) return st;
-            if (!(e & ERR_REC_OVERFLOW)) break;     // (a redo rewrites the same key ranges)
+            if (!(e & ERR_REC_OVERFLOW)) {         // (a redo rewrites the same key ranges)
+                c->t_ms[2] += ms_s1;
+                break;
+            }
             if (attempt == 7) return fail(c, KMER_E_OOM, "record list kept overflowing");
             HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
             st = ensure_records(c, c->h_small[0] + 1024);
@@ -1000,10 +1020,13 @@ kmer_status table_finish(kmer_ctx *c) {
     HIPCHK(c, c->tnd.ensure(TAB_NQ, s));
     HIPCHK(c, c->tbig.ensure(1 << 16, s));
     HIPCHK(c, c->tstats.ensure(4, s));
+    HIPCHK(c, hipEventRecord(c->tev[4], s));
     HIPCHK(c, launch_tab_hist2(c->tb1.p, c->tunits.p, (uint32_t)n_units, c->tH.p, s));
     ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tH.p, c->tHs.p, (uint64_t)0, (size_t)nh,
                                            rocprim::plus<uint64_t>(), s));
+    HIPCHK(c, hipEventRecord(c->tev[5], s));
     HIPCHK(c, launch_tab_scatter2(c->tb1.p, c->tunits.p, (uint32_t)n_units, c->tHs.p, c->tb2.p, s));
+    HIPCHK(c, hipEventRecord(c->tev[6], s));
     HIPCHK(c, launch_tab_starts(c->tHs.p, c->tunits.p + n_units, n, c->tstart.p, s));
     HIPCHK(c, hipMemsetAsync(c->tstats.p, 0, 4 * sizeof(unsigned long long), s));
     TabFinal f;
@@ -1013,8 +1036,11 @@ kmer_status table_finish(kmer_ctx *c) {
     f.out = c->tb1.p;                        // (pass-1 keys are dead after pass 2)
     f.nd = c->tnd.p;
     const uint64_t mean = n / TAB_NQ;
-    while (f.sub_bits < 16 && (mean >> f.sub_bits) > 6000) ++f.sub_bits;
+    uint64_t range_keys = 3000;               // mean keys per LDS range (load ~0.37: short probes; measured best at C3)
+    if (const char *rk = getenv("KMERHIP_TAB_RANGE")) range_keys = std::max<uint64_t>(64, strtoull(rk, nullptr, 10));
+    while (f.sub_bits < 16 && (mean >> f.sub_bits) > range_keys) ++f.sub_bits;
     f.cap = (c->p.flags & KMER_FLAG_TABLE_SPLIT_TEST) ? 64 : TAB_CAP;
+    if (const char *ab = getenv("KMERHIP_TAB_ABLATE")) f.ablate = (uint32_t)atoi(ab);   // experiments only
     f.big = c->tbig.p;
     f.big_count = c->tstats.p + 3;
     f.big_cap = c->tbig.cap;
@@ -1026,13 +1052,17 @@ kmer_status table_finish(kmer_ctx *c) {
         f.phi |= (((uint32_t)ch >> 2) & 1u) << i;
     }
     f.pmask = c->prefix.size() >= 32 ? ~0u : ((1u << c->prefix.size()) - 1u);
-    f.inv1 = inv_odd(0xff51afd7ed558ccdull);
-    f.inv2 = inv_odd(0xc4ceb9fe1a85ec53ull);
+    f.inv = inv_odd(TAB_MUL);
     f.stats = c->tstats.p;
+    HIPCHK(c, hipEventRecord(c->tev[2], s));
     HIPCHK(c, launch_tab_final(f, (uint32_t)std::max(c->n_cu, 1), s));
+    HIPCHK(c, hipEventRecord(c->tev[7], s));
     HIPCHK(c, hipMemcpyAsync(c->h_small + 8, c->tstats.p, 4 * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
+    c->t_ms[3] += ev_ms(c, c->tev[4], c->tev[5]);
+    c->t_ms[4] += ev_ms(c, c->tev[5], c->tev[6]);
+    c->t_ms[5] += ev_ms(c, c->tev[2], c->tev[7]);
     const uint32_t e = (uint32_t)c->h_small[5];
     if (e & ERR_COUNT_OVERFLOW) return fail(c, KMER_E_TOO_MANY_KEYS, "a k-mer count exceeds 2^32 - 1");
     if (e & ERR_BIG_OVERFLOW) return fail(c, KMER_E_OOM, "too many k-mers with counts >= 2^20");
@@ -1070,7 +1100,7 @@ kmer_status build_table_result(kmer_ctx *c, uint64_t lines, kmer_result **out) {
         }
         std::unordered_map<uint64_t, uint64_t> bigc;
         for (auto &b : big) bigc[b.h] = b.count;
-        const uint64_t inv1 = inv_odd(0xff51afd7ed558ccdull), inv2 = inv_odd(0xc4ceb9fe1a85ec53ull);
+        const uint64_t inv = inv_odd(TAB_MUL);
         const uint64_t kmask = k >= 32 ? 0xFFFFFFFFull : ((1ull << k) - 1);
         std::string key(k, 'A'), rkey(k, 'A');
         for (uint32_t q = 0; q < TAB_NQ; ++q) {
@@ -1079,12 +1109,7 @@ kmer_status build_table_result(kmer_ctx *c, uint64_t lines, kmer_result **out) {
                 const uint64_t h = ((uint64_t)q << TAB_RBITS) | (w >> 20);
                 uint64_t cnt = w & TAB_CMAX;
                 if (cnt == TAB_CMAX) cnt = bigc[h];
-                uint64_t x = h;                      // tab_mix^-1
-                x ^= x >> 33;
-                x *= inv2;
-                x ^= x >> 33;
-                x *= inv1;
-                x ^= x >> 33;
+                const uint64_t x = h * inv;          // tab_mix^-1
                 const uint64_t lo = x & kmask, hi = (x >> k) & kmask;
                 for (uint32_t j = 0; j < k; ++j) {
                     const uint32_t v = (uint32_t)(((hi >> j) & 1u) << 1 | ((lo >> j) & 1u));
@@ -1152,6 +1177,7 @@ kmer_status reset(kmer_ctx *c) {
     c->t_cbase.clear();
     c->t_coff.clear();
     c->t_done = false;
+    for (double &x : c->t_ms) x = 0.0;
     c->scan_ms = c->feed_ms = c->finish_ms = 0.0;
     c->open_stream = true;
     return KMER_OK;
@@ -1573,6 +1599,7 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
           hipSuccess;
     ok &= c->h_tail && hipHostGetDevicePointer((void **)&c->d_tail, c->h_tail, 0) == hipSuccess;
     if (c->h_tail) memset(c->h_tail, 0, 16 * sizeof(uint64_t));
+    for (hipEvent_t &e : c->tev) ok &= hipEventCreate(&e) == hipSuccess;
     ok &= hipEventCreate(&c->ev0) == hipSuccess && hipEventCreate(&c->ev1) == hipSuccess &&
           hipEventCreate(&c->ev2) == hipSuccess && hipEventCreate(&c->ev3) == hipSuccess &&
           hipEventCreate(&c->ev4) == hipSuccess &&
@@ -1632,6 +1659,8 @@ kmer_status kmer_close(kmer_ctx *c) {
     if (c->h_small) (void)hipHostFree(c->h_small);
     if (c->h_tail) (void)hipHostFree(c->h_tail);
     for (hipEvent_t e : {c->ev0, c->ev1, c->ev2, c->ev3, c->ev4, c->evw})
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->tev)
         if (e) (void)hipEventDestroy(e);
     if (c->sstream) (void)hipStreamSynchronize(c->sstream);
     if (c->evq) (void)hipEventDestroy(c->evq);
@@ -1974,6 +2003,30 @@ kmer_status kmer_table_device(kmer_ctx *c, const void **d_entries, const void **
     if (d_bucket_len) *d_bucket_len = any ? c->tnd.p : nullptr;
     if (d_big) *d_big = any ? c->tbig.p : nullptr;
     if (n_big) *n_big = c->t_nbig;
+    return KMER_OK;
+}
+
+kmer_status kmer_phase_times(kmer_ctx *c, uint32_t max, const char **names, double *ms, uint32_t *n) {
+    if (!c || !n || (max && (!names || !ms))) return KMER_E_BAD_PARAM;
+    SETTLE(c);
+    static const char *tab_names[6] = {"lines", "hist1", "scatter1", "hist2", "scatter2", "final"};
+    static const char *ord_names[3] = {"scan", "feed", "finish"};
+    if (c->mode == MODE_TABLE) {
+        *n = 6;
+        for (uint32_t i = 0; i < 6 && i < max; ++i) {
+            names[i] = tab_names[i];
+            ms[i] = c->t_ms[i];
+        }
+        return KMER_OK;
+    }
+    kmer_status st = resolve_out(c);
+    if (st) return st;
+    const double v[3] = {c->scan_ms, c->feed_ms, c->finish_ms};
+    *n = 3;
+    for (uint32_t i = 0; i < 3 && i < max; ++i) {
+        names[i] = ord_names[i];
+        ms[i] = v[i];
+    }
     return KMER_OK;
 }
 

@@ -351,17 +351,14 @@ constexpr uint32_t TAB_NQ = 1u << (TAB_L1 + TAB_L2);   // buckets
 constexpr uint32_t TAB_RBITS = 64 - TAB_L1 - TAB_L2;   // remainder bits (44)
 constexpr uint64_t TAB_CMAX = 0xFFFFFull;              // entry count field (20 bits); larger -> big list
 constexpr uint64_t TAB_UNIT = 1ull << 18;              // pass-2 keys per workgroup
+constexpr uint32_t TAB_FWG = 1024;                     // final workgroup (16 waves, one per CU)
 constexpr uint32_t TAB_SLOTS = 8192;                   // final LDS table slots (96 KiB)
 constexpr uint32_t TAB_CAP = 7000;                     // distinct keys per range before it is split (+1024 in flight)
 
-__host__ __device__ inline uint64_t tab_mix(uint64_t x) {
-    x ^= x >> 33;
-    x *= 0xff51afd7ed558ccdull;
-    x ^= x >> 33;
-    x *= 0xc4ceb9fe1a85ec53ull;
-    x ^= x >> 33;
-    return x;
-}
+// multiplicative hash: a bijection of the 64-bit code (odd multiplier) whose
+// top bits -- partition and bucket -- depend on every bit of the code
+constexpr uint64_t TAB_MUL = 0x9E3779B97F4A7C15ull;
+__host__ __device__ inline uint64_t tab_mix(uint64_t x) { return x * TAB_MUL; }
 
 struct TabArgs {
     const uint8_t *data;
@@ -399,12 +396,13 @@ struct TabFinal {
     uint32_t *nd;
     uint32_t sub_bits;             // initial split of a bucket's remainder range
     uint32_t cap;                  // claims per range before it is split (<= TAB_CAP)
+    uint32_t ablate;               // experiments only (results WRONG): 1 no insert, 2 no emit
     TabBig *big;
     unsigned long long *big_count;
     uint64_t big_cap;
     unsigned int *err;
     uint32_t k, plo, phi, pmask;
-    uint64_t inv1, inv2;           // inverses of tab_mix's multipliers
+    uint64_t inv;                  // inverse of TAB_MUL mod 2^64 (tab_mix^-1)
     unsigned long long *stats;     // [0] canonical entries [1] Map keys [2] sum of Map counts
 };
 

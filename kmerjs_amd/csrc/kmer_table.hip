@@ -340,59 +340,128 @@ __global__ __launch_bounds__(256) void tab_starts_kernel(const uint64_t *H2s, co
 
 namespace {
 
-// Insert a remainder into the LDS table (linear probing).  More than `cap`
-// distinct keys (or a full probe) set *ovf: the range is redone in halves.
-// Inserts stop once *ovf is seen, so at most cap + 1024 slots are taken.
-__device__ __forceinline__ void tab_insert(uint64_t *tkey, uint32_t *tcnt, uint32_t *occ, volatile uint32_t *ovf,
-                                           uint64_t rem, uint32_t cap, unsigned int *err) {
-    uint32_t s = (uint32_t)rem & (TAB_SLOTS - 1);
-    for (uint32_t probe = 0; probe < TAB_SLOTS; ++probe) {
-        uint64_t cur = __hip_atomic_load(&tkey[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (cur == TAB_EMPTY) {
-            cur = atomicCAS((unsigned long long *)&tkey[s], (unsigned long long)TAB_EMPTY, (unsigned long long)rem);
-            if (cur == TAB_EMPTY) {                   // claimed: one more distinct key
-                cur = rem;
-                if (atomicAdd(occ, 1u) >= cap) *ovf = 1u;
-            }
-        }
-        if (cur == rem) {
-            if (atomicAdd(&tcnt[s], 1u) == 0xFFFFFFFFu) atomicOr(err, ERR_COUNT_OVERFLOW);
-            return;
-        }
-        s = (s + 1) & (TAB_SLOTS - 1);
-    }
-    *ovf = 1u;
+// LDS slot of a remainder: its low bits are weak (a product's low bits see
+// only the code's low bits), so the slot comes from a second multiply's top bits
+__device__ __forceinline__ uint32_t tab_slot(uint64_t rem) {
+    return (uint32_t)((rem * TAB_MUL) >> 51) & (TAB_SLOTS - 1);
 }
 
-__device__ __forceinline__ uint64_t tab_unmix(uint64_t x, uint64_t inv1, uint64_t inv2) {
-    x ^= x >> 33;
-    x *= inv2;
-    x ^= x >> 33;
-    x *= inv1;
-    x ^= x >> 33;
-    return x;
+__device__ __forceinline__ bool lds_flag(uint32_t *f) {
+    return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
 }
+
+constexpr uint32_t TAB_PROBE_MAX = 256;      // a longer probe marks the range as overflowing
+
+// Insert N of a lane's held keys (key[OFF + j] takes part iff bit OFF + j of
+// `pend` is set) together:
+// every step issues one CAS per pending key (independent, so their LDS round
+// trips overlap) instead of walking each key's probe sequence in turn, which
+// serialises the wave on its longest probe for every key.  CAS(EMPTY -> rem)
+// returning EMPTY claims the slot, returning rem finds it; the count add needs
+// no return.  Returns the slots this lane claimed.
+template <int N, int M>
+__device__ __forceinline__ uint32_t tab_insert_grp(uint64_t *tkey, uint32_t *tcnt, const uint64_t (&key)[M], int g,
+                                                   uint32_t pend, uint32_t *ovf) {
+    // (g is a constant once the caller's loop is unrolled: key[g + j] stays in registers)
+    pend = (pend >> g) & ((1u << N) - 1u);
+    uint64_t rem[N];
+    uint32_t slot[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+        rem[j] = key[g + j];
+        slot[j] = tab_slot(rem[j]);
+    }
+    uint32_t claimed = 0;
+    for (uint32_t step = 0; __any(pend != 0); ++step) {
+        if (step == TAB_PROBE_MAX) {
+            if (pend) __hip_atomic_store(ovf, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            break;
+        }
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            if (!(pend & (1u << j))) continue;
+            const uint64_t old = atomicCAS((unsigned long long *)&tkey[slot[j]], (unsigned long long)TAB_EMPTY,
+                                           (unsigned long long)rem[j]);
+            if (old == TAB_EMPTY || old == rem[j]) {
+                __hip_atomic_fetch_add(&tcnt[slot[j]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                claimed += old == TAB_EMPTY ? 1u : 0u;
+                pend &= ~(1u << j);
+            } else {
+                slot[j] = (slot[j] + 1) & (TAB_SLOTS - 1);
+            }
+        }
+    }
+    return claimed;
+}
+
 
 }  // namespace
 
-// final: per bucket, LDS hash table -> (remainder, count) entries in place of
-// the bucket's keys (into `out`), distinct count per bucket, Map statistics
-__global__ __launch_bounds__(TAB_WG1) void tab_final_kernel(TabFinal a) {
+constexpr int TAB_KPT = 12;                   // bucket keys held per thread (register path)
+constexpr uint32_t TAB_REG_MAX = TAB_KPT * TAB_FWG;
+constexpr uint32_t TAB_SC = 1024;             // bucket starts cached in LDS per refill
+
+// final: each workgroup merges a contiguous range of buckets, one at a time,
+// in an LDS hash table; entries (remainder, count) go to `out` at the
+// bucket's start, the distinct count to nd[q], Map statistics on the fly.
+// Latency: bucket starts come from an LDS cache refilled every 1024 buckets;
+// a bucket of <= 12 K keys is held in registers (12 per thread), and the next
+// bucket's keys are loaded as soon as the current one's last range is merged,
+// in flight while it is emitted.  Larger buckets (repeated keys, inputs
+// beyond ~130 M reads) stream from HBM once per range.  The table is clean
+// between buckets: emission clears the slots it reads.
+__global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
     __shared__ uint64_t tkey[TAB_SLOTS];
     __shared__ uint32_t tcnt[TAB_SLOTS];
     __shared__ uint64_t stk[2 * 64];          // range stack [lo, hi) of remainders
-    __shared__ uint32_t occ, nout, sp;
-    __shared__ volatile uint32_t ovf;
+    __shared__ uint64_t sc[TAB_SC + 2];       // start[cbase .. cbase + TAB_SC + 1]
+    __shared__ uint32_t occ, nout, sp, ovf;
     const uint32_t t = threadIdx.x, lane = t & 63;
     const uint32_t k = a.k;
     const uint32_t kmask = k >= 32 ? ~0u : ((1u << k) - 1u), sh = 32 - k;
+    const uint32_t per = (TAB_NQ + gridDim.x - 1) / gridDim.x;
+    const uint32_t q0 = blockIdx.x * per, q1 = q0 + per < TAB_NQ ? q0 + per : TAB_NQ;
     uint64_t st_canon = 0, st_keys = 0, st_sum = 0;
-    for (uint32_t q = blockIdx.x; q < TAB_NQ; q += gridDim.x) {
-        const uint64_t s0 = a.start[q], n = a.start[q + 1] - s0;
+    uint64_t kn[TAB_KPT];
+    // a bucket's keys, as remainders (lanes past its end re-read its first key
+    // and are masked at use): unconditional loads, all in flight together
+    auto load_keys = [&](uint64_t s0x, uint64_t nx) {
+        if (nx - 1 < (uint64_t)TAB_REG_MAX) {
+            // (lane tests as t < nx - 1024 j: immediates, no per-j index registers)
+            const uint64_t *src = a.B2 + s0x;
+            const int left = (int)nx - (int)t;
+#pragma unroll
+            for (int j = 0; j < TAB_KPT; ++j) kn[j] = src[left > j * (int)TAB_FWG ? j * TAB_FWG + t : 0u];
+        }
+    };
+    auto refill = [&](uint32_t cb) {
+        __syncthreads();
+        for (uint32_t i = t; i < TAB_SC + 2; i += TAB_FWG) sc[i] = a.start[cb + i < TAB_NQ ? cb + i : TAB_NQ];
+        __syncthreads();
+    };
+    for (uint32_t i = t; i < TAB_SLOTS; i += TAB_FWG) {
+        tkey[i] = TAB_EMPTY;
+        tcnt[i] = 0;
+    }
+    uint32_t cbase = q0;
+    refill(cbase);
+    if (q0 < q1) load_keys(sc[0], sc[1] - sc[0]);
+    for (uint32_t q = q0; q < q1; ++q) {
+        if (q - cbase == TAB_SC) {
+            cbase = q;
+            refill(cbase);
+        }
+        const uint64_t s0 = sc[q - cbase], n = sc[q - cbase + 1] - s0;
+        const uint64_t s0n = sc[q - cbase + 1], nn = sc[q - cbase + 2] - s0n;   // bucket q + 1
+        const bool more = q + 1 < q1;
+        const bool inreg = n <= TAB_REG_MAX;
         if (n == 0) {
             if (t == 0) a.nd[q] = 0;
+            if (more) load_keys(s0n, nn);
             continue;
         }
+        if (n >= (1ull << 32) && t == 0) atomicOr(a.err, ERR_COUNT_OVERFLOW);   // (u32 counts)
+        __syncthreads();                         // the previous bucket is done with the LDS state
         if (t == 0) {
             const uint32_t nsub = 1u << a.sub_bits;
             const uint64_t w = (1ull << TAB_RBITS) >> a.sub_bits;
@@ -403,15 +472,13 @@ __global__ __launch_bounds__(TAB_WG1) void tab_final_kernel(TabFinal a) {
             sp = nsub;
             nout = 0;
         }
+#pragma unroll
+        for (int j = 0; j < TAB_KPT; ++j) kn[j] &= TAB_RMASK;
         while (true) {
             __syncthreads();
             const uint32_t top = sp;
             if (top == 0) break;
             const uint64_t rlo = stk[2 * (top - 1)], rhi = stk[2 * (top - 1) + 1];
-            for (uint32_t i = t; i < TAB_SLOTS; i += TAB_WG1) {
-                tkey[i] = TAB_EMPTY;
-                tcnt[i] = 0;
-            }
             __syncthreads();
             if (t == 0) {
                 sp = top - 1;
@@ -419,14 +486,38 @@ __global__ __launch_bounds__(TAB_WG1) void tab_final_kernel(TabFinal a) {
                 ovf = 0;
             }
             __syncthreads();
-            const uint64_t *src = a.B2 + s0;
-            for (uint64_t i = t; i < n; i += TAB_WG1) {
-                if (ovf) break;
-                const uint64_t rem = src[i] & TAB_RMASK;
-                if (rem >= rlo && rem < rhi) tab_insert(tkey, tcnt, &occ, &ovf, rem, a.cap, a.err);
+            if (inreg) {
+                uint32_t pend = 0;
+                const int left = (int)n - (int)t;
+#pragma unroll
+                for (int j = 0; j < TAB_KPT; ++j)
+                    if (left > j * (int)TAB_FWG && kn[j] >= rlo && kn[j] < rhi && !(a.ablate & 1)) pend |= 1u << j;
+                // (groups of four keys: enough CAS round trips in flight
+                // without spilling the held keys)
+                uint32_t cl = 0;
+#pragma unroll
+                for (int g = 0; g < TAB_KPT; g += 4) cl += tab_insert_grp<4>(tkey, tcnt, kn, g, pend, &ovf);
+                for (int d = 32; d >= 1; d >>= 1) cl += __shfl_xor(cl, d);
+                if (lane == 0 && cl) atomicAdd(&occ, cl);
+            } else {
+                const uint64_t *src = a.B2 + s0;
+                for (uint64_t i = t; i < n; i += TAB_FWG) {
+                    if (lds_flag(&ovf)) break;
+                    uint64_t r1[1] = {src[i] & TAB_RMASK};
+                    if (r1[0] >= rlo && r1[0] < rhi) {
+                        uint32_t cl = tab_insert_grp<1>(tkey, tcnt, r1, 0, 1u, &ovf);
+                        if (cl) atomicAdd(&occ, cl);
+                    }
+                }
             }
             __syncthreads();
+            if (t == 0 && occ > a.cap) ovf = 1u;     // more distinct keys than the range may hold
+            __syncthreads();
             if (ovf) {
+                for (uint32_t i = t; i < TAB_SLOTS; i += TAB_FWG) {
+                    tkey[i] = TAB_EMPTY;
+                    tcnt[i] = 0;
+                }
                 if (t == 0) {
                     if (rhi - rlo < 2 || sp + 2 > 64) {
                         atomicOr(a.err, ERR_TAB_SPLIT);
@@ -441,8 +532,12 @@ __global__ __launch_bounds__(TAB_WG1) void tab_final_kernel(TabFinal a) {
                 }
                 continue;
             }
-            // emit the occupied slots (one LDS counter bump per wave and pass)
-            for (uint32_t i = t; i < TAB_SLOTS; i += TAB_WG1) {
+            // the bucket's last range is merged: load the next bucket's keys
+            // now, in flight while this one is emitted
+            if (top == 1 && more) load_keys(s0n, nn);
+            // emit (and clear) the occupied slots, one LDS counter bump per wave and pass
+#pragma unroll 1
+            for (uint32_t i = t; i < TAB_SLOTS && !(a.ablate & 2); i += TAB_FWG) {
                 const uint64_t rem = tkey[i];
                 const bool v = rem != TAB_EMPTY;
                 const uint64_t m = __ballot(v);
@@ -453,6 +548,8 @@ __global__ __launch_bounds__(TAB_WG1) void tab_final_kernel(TabFinal a) {
                 if (!v) continue;
                 const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
                 const uint64_t cnt = tcnt[i];
+                tkey[i] = TAB_EMPTY;
+                tcnt[i] = 0;
                 a.out[s0 + pos] = (rem << 20) | (cnt < TAB_CMAX ? cnt : TAB_CMAX);
                 const uint64_t h = ((uint64_t)q << TAB_RBITS) | rem;
                 if (cnt >= TAB_CMAX) {
@@ -465,7 +562,7 @@ __global__ __launch_bounds__(TAB_WG1) void tab_final_kernel(TabFinal a) {
                     }
                 }
                 // Map view of this canonical entry (App. A.6)
-                const uint64_t code = tab_unmix(h, a.inv1, a.inv2);
+                const uint64_t code = h * a.inv;
                 const uint32_t lo = (uint32_t)code & kmask, hi = (uint32_t)(code >> k) & kmask;
                 const uint32_t rlo2 = __brev(~lo & kmask) >> sh, rhi2 = __brev(~hi & kmask) >> sh;
                 const bool pal = lo == rlo2 && hi == rhi2;
@@ -527,7 +624,7 @@ hipError_t launch_tab_starts(const uint64_t *H2s, const TabUnit *pfirst, uint64_
 }
 
 hipError_t launch_tab_final(const TabFinal &a, uint32_t grid, hipStream_t s) {
-    hipLaunchKernelGGL(tab_final_kernel, dim3(grid), dim3(TAB_WG1), 0, s, a);
+    hipLaunchKernelGGL(tab_final_kernel, dim3(grid), dim3(TAB_FWG), 0, s, a);
     return hipGetLastError();
 }
 
