@@ -70,6 +70,34 @@ def cpu_baseline(k, prefix, seconds_target=8.0):
                                   "Maps; %.1f s" % (nt, cores, dtn)}}
 
 
+def end_to_end(buf, args):
+    """readFile() -> Map through the Node drop-in on the same input written to
+    a file: a child `node` process, timed inside it."""
+    import shutil
+    import subprocess
+    import tempfile
+    node = shutil.which("node")
+    if node is None:
+        return {"skipped": "node not installed"}
+    fd, path = tempfile.mkstemp(suffix=".fastq", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        with os.fdopen(fd, "wb") as f:
+            step = 1 << 30
+            for lo in range(0, buf.numel(), step):
+                f.write(buf[lo:lo + step].cpu().numpy().tobytes())
+        p = subprocess.run([node, os.path.join(REPO, "tools", "e2e_readfile.js"), path, args.prefix, str(args.k)],
+                           capture_output=True, text=True, timeout=600)
+        if p.returncode != 0:
+            return {"error": p.stderr[-500:]}
+        r = json.loads(p.stdout.strip().splitlines()[-1])
+        r["what"] = ("Node KmerJS.readFile() on a %.2f GB FASTQ file: host read + H2D + GPU count + ordered result "
+                     "+ N-API + lazy KmerMap; iterate = one full for..of; first_get = index build on the first "
+                     "keyed access; eager_map = new Map(map) for comparison" % (buf.numel() / 1e9))
+        return r
+    finally:
+        os.unlink(path)
+
+
 def count_windows(lines_bytes_lengths, first_line, k):
     """Windows on both strands of the sequence lines (index % 4 == 1, length > 1)."""
     tot = 0
@@ -185,6 +213,7 @@ def main():
     ap.add_argument("--flags", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the Node readFile() -> Map end-to-end run")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="sessions in rotation (>= 2: a step's finish overlaps the next steps' scans)")
     ap.add_argument("--config", default="c2", choices=("c1", "c2", "c3", "c4", "c5"),
@@ -452,6 +481,8 @@ def main():
             out["pcie_inclusive_ms"] = dt * 1e3
             assert len(r) == distinct
             del host
+        if not args.no_e2e and world == 1 and args.config == "c2":
+            out["end_to_end"] = end_to_end(buf, args)
         if not args.no_cpu_baseline and world == 1 and args.config == "c2":
             out["cpu_baseline"] = cpu_baseline(args.k, prefix)
         print(json.dumps(out), flush=True)

@@ -85,6 +85,8 @@ kmer_status kmer_open(const kmer_params *params, kmer_ctx **out);
 kmer_status kmer_close(kmer_ctx *ctx);
 
 /* Whole-input calls (replace readFile(), lib/kmers.js:106-185). */
+/* kmer_count_file also reads gzip-compressed FASTQ (magic 1f 8b) through zlib:
+ * the count is that of the decompressed bytes. */
 kmer_status kmer_count_file(kmer_ctx *ctx, const char *path, kmer_result **out);
 kmer_status kmer_count_buffer(kmer_ctx *ctx, const uint8_t *bytes, size_t len, kmer_result **out);
 
@@ -162,6 +164,11 @@ kmer_status kmer_result_arrays(const kmer_result *r, const char **keys, const ui
                                const uint64_t **counts);
 /* First-occurrence order key of every entry (monotone in Map order). */
 kmer_status kmer_result_firsts(const kmer_result *r, const uint64_t **firsts);
+/* Write a result to a file, in Map order: KMER_WRITE_JSON = JSON.stringify of
+ * mapToJSON(map) (lib/kmers.js:46-54); KMER_WRITE_LEGACY = the npm main's
+ * "{\n key: count, ... }\n" dump (lib/index.js:381-388). */
+enum { KMER_WRITE_JSON = 0, KMER_WRITE_LEGACY = 1 };
+kmer_status kmer_result_write(const kmer_result *r, const char *path, uint32_t format);
 void kmer_result_free(kmer_result *r);
 
 /* Benchmark utility: write n_reads synthetic 317-byte FASTQ records (SURVEY.md

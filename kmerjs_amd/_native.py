@@ -18,6 +18,8 @@ FLAG_BYTE_SCAN = 4
 FLAG_SORT_FINISH = 8
 FLAG_UNORDERED = 16
 FLAG_TABLE_SPLIT_TEST = 32
+WRITE_JSON = 0      # JSON.stringify(mapToJSON(map)), lib/kmers.js:46-54
+WRITE_LEGACY = 1    # "{\nkey: count,...}\n", lib/index.js:381-388
 
 # every symbol the header declares (tests/test_abi.py checks header <-> library)
 EXPORTS = ["kmer_open", "kmer_close", "kmer_count_file", "kmer_count_buffer", "kmer_reset", "kmer_sync",
@@ -25,7 +27,8 @@ EXPORTS = ["kmer_open", "kmer_close", "kmer_count_file", "kmer_count_buffer", "k
            "kmer_exchange_prepare", "kmer_finish_exchanged",
            "kmer_records_export", "kmer_records_import", "kmer_records_clear", "kmer_result_device", "kmer_set_position",
            "kmer_lines", "kmer_result_size", "kmer_result_lines", "kmer_result_get",
-           "kmer_result_arrays", "kmer_result_firsts", "kmer_result_free", "kmer_synth_fastq_device",
+           "kmer_result_arrays", "kmer_result_firsts", "kmer_result_write", "kmer_result_free",
+           "kmer_synth_fastq_device",
            "kmer_last_timing", "kmer_phase_times", "kmer_table_stats", "kmer_table_device",
            "kmer_status_string", "kmer_last_error", "kmer_version"]
 
@@ -83,6 +86,7 @@ def _load():
                                            ctypes.POINTER(ctypes.c_uint32), pu64]),
         "kmer_result_arrays": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(pu64),
                                               ctypes.POINTER(pu64)]),
+        "kmer_result_write": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_uint32]),
         "kmer_result_free": (None, [vp]),
         "kmer_synth_fastq_device": (ctypes.c_int, [vp, u64, u64, u64, vp]),
         "kmer_last_timing": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
@@ -192,9 +196,16 @@ class Counter:
         self._check(LIB.kmer_count_buffer(self.h, data, len(data), ctypes.byref(r)), "count_buffer")
         return Result(r)
 
-    def count_file(self, path) -> Result:
+    def count_file(self, path, write=None, fmt=WRITE_JSON) -> Result:
+        """Count a FASTQ file (plain or gzip).  write: also serialise the result
+        to this path (natively, in Map order; fmt WRITE_JSON or WRITE_LEGACY)."""
         r = ctypes.c_void_p()
         self._check(LIB.kmer_count_file(self.h, os.fsencode(path), ctypes.byref(r)), "count_file")
+        if write is not None:
+            st = LIB.kmer_result_write(r, os.fsencode(write), fmt)
+            if st != KMER_OK:
+                LIB.kmer_result_free(r)
+                raise KmerError(st, "kmer_result_write(%s)" % write)
         return Result(r)
 
     # ---- device-resident streaming ----

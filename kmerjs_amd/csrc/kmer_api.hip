@@ -26,12 +26,17 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <unordered_map>
 #include <vector>
 
 #include "../../include/kmer_api.h"
 #include "kmer_internal.hpp"
+
+#include <sys/stat.h>
+#include <unistd.h>
+#include <zlib.h>
 
 using namespace kmerhip;
 
@@ -1731,19 +1736,77 @@ kmer_status kmer_count_file(kmer_ctx *c, const char *path, kmer_result **out) {
         return KMER_E_DEVICE;
     }
     kmer_status st = reset(c);
-    const uint64_t batch = c->p.batch_bytes ? c->p.batch_bytes : DEFAULT_BATCH;
-    std::vector<uint8_t> buf;
+    // staging: one batch, but no larger than the file (a small FASTQ does not
+    // commit a 1 GiB buffer); not zero-filled; grown only for a line longer
+    // than the batch
+    uint64_t batch = c->p.batch_bytes ? c->p.batch_bytes : DEFAULT_BATCH;
+    struct stat sb;
+    if (fstat(fileno(f), &sb) == 0 && S_ISREG(sb.st_mode)) batch = std::min<uint64_t>(batch, (uint64_t)sb.st_size + 1);
+    batch = std::max<uint64_t>(batch, 1);
+    // gzip input (magic 1f 8b): read through zlib; the count is that of the
+    // decompressed FASTQ (the reference reads raw bytes only)
+    gzFile gz = nullptr;
+    {
+        unsigned char magic[2] = {0, 0};
+        const size_t m = fread(magic, 1, 2, f);
+        rewind(f);
+        if (m == 2 && magic[0] == 0x1f && magic[1] == 0x8b) {
+            gz = gzdopen(dup(fileno(f)), "rb");
+            if (!gz) {
+                fclose(f);
+                return fail(c, KMER_E_IO, std::string("cannot read gzip stream ") + path);
+            }
+            gzbuffer(gz, 1 << 20);
+            batch = std::max<uint64_t>(batch, 64ull << 20);   // (file size is the compressed size)
+            batch = std::min<uint64_t>(batch, c->p.batch_bytes ? c->p.batch_bytes : DEFAULT_BATCH);
+        }
+    }
+    uint64_t cap = batch;
+    std::unique_ptr<uint8_t[]> buf(new (std::nothrow) uint8_t[cap]);
+    if (!buf) {
+        if (gz) gzclose(gz);
+        fclose(f);
+        return fail(c, KMER_E_OOM, "host staging buffer");
+    }
     uint64_t carry = 0;
     bool eof = false;
     while (!st && !eof) {
-        buf.resize(carry + batch);
-        const size_t got = fread(buf.data() + carry, 1, batch, f);
-        if (got < batch) {
-            if (ferror(f)) {
-                st = fail(c, KMER_E_IO, std::string("read error on ") + path);
+        if (carry + batch > cap) {                // (a line longer than the batch)
+            const uint64_t nc = std::max(carry + batch, cap * 2);
+            std::unique_ptr<uint8_t[]> nb(new (std::nothrow) uint8_t[nc]);
+            if (!nb) {
+                st = fail(c, KMER_E_OOM, "host staging buffer");
                 break;
             }
-            eof = true;
+            memcpy(nb.get(), buf.get(), carry);
+            buf = std::move(nb);
+            cap = nc;
+        }
+        size_t got = 0;
+        if (gz) {
+            while (got < batch) {                 // (gzread takes an unsigned int count)
+                const unsigned want = (unsigned)std::min<uint64_t>(batch - got, 1u << 30);
+                const int r = gzread(gz, buf.get() + carry + got, want);
+                if (r < 0) break;
+                got += (size_t)r;
+                if ((unsigned)r < want) break;
+            }
+            int zerr = 0;
+            gzerror(gz, &zerr);
+            if (zerr != Z_OK && zerr != Z_BUF_ERROR) {
+                st = fail(c, KMER_E_IO, std::string("gzip read error on ") + path);
+                break;
+            }
+            if (got < batch) eof = true;
+        } else {
+            got = fread(buf.get() + carry, 1, batch, f);
+            if (got < batch) {
+                if (ferror(f)) {
+                    st = fail(c, KMER_E_IO, std::string("read error on ") + path);
+                    break;
+                }
+                eof = true;
+            }
         }
         const uint64_t have = carry + got;
         uint64_t cut = have;
@@ -1754,10 +1817,11 @@ kmer_status kmer_count_file(kmer_ctx *c, const char *path, kmer_result **out) {
                 continue;
             }
         }
-        st = feed_host(c, buf.data(), cut);
+        st = feed_host(c, buf.get(), cut);
         carry = have - cut;
-        if (carry) memmove(buf.data(), buf.data() + cut, carry);
+        if (carry) memmove(buf.get(), buf.get() + cut, carry);
     }
+    if (gz) gzclose(gz);
     fclose(f);
     if (st) {
         c->open_stream = false;
@@ -2074,6 +2138,69 @@ kmer_status kmer_result_firsts(const kmer_result *r, const uint64_t **firsts) {
     if (!r || !firsts) return KMER_E_BAD_PARAM;
     *firsts = r->firsts.data();
     return KMER_OK;
+}
+
+// Serialise a result in Map order.  KMER_WRITE_JSON: JSON.stringify of
+// mapToJSON(map) (lib/kmers.js:46-54): {"key":count,...}, keys escaped as
+// JSON.stringify does (\" \\ \b \f \n \r \t, other bytes < 0x20 as \u00XX).
+// KMER_WRITE_LEGACY: the npm main's dump (lib/index.js:381-388):
+// "{\n" then "key: count," per entry, then "}\n".
+kmer_status kmer_result_write(const kmer_result *r, const char *path, uint32_t format) {
+    if (!r || !path || format > KMER_WRITE_LEGACY) return KMER_E_BAD_PARAM;
+    FILE *f = fopen(path, "wb");
+    if (!f) return KMER_E_IO;
+    std::string out;
+    out.reserve(1 << 22);
+    const uint64_t n = r->counts.size();
+    char num[32];
+    auto flush = [&]() -> bool {
+        const bool ok = fwrite(out.data(), 1, out.size(), f) == out.size();
+        out.clear();
+        return ok;
+    };
+    bool ok = true;
+    out += format == KMER_WRITE_JSON ? "{" : "{\n";
+    for (uint64_t i = 0; i < n && ok; ++i) {
+        const char *k = r->keys.data() + r->offsets[i];
+        const uint64_t kl = r->offsets[i + 1] - r->offsets[i];
+        const int nl = snprintf(num, sizeof(num), "%llu", (unsigned long long)r->counts[i]);
+        if (format == KMER_WRITE_JSON) {
+            if (i) out += ',';
+            out += '"';
+            for (uint64_t j = 0; j < kl; ++j) {
+                const unsigned char ch = (unsigned char)k[j];
+                switch (ch) {
+                case '"': out += "\\\""; break;
+                case '\\': out += "\\\\"; break;
+                case '\b': out += "\\b"; break;
+                case '\f': out += "\\f"; break;
+                case '\n': out += "\\n"; break;
+                case '\r': out += "\\r"; break;
+                case '\t': out += "\\t"; break;
+                default:
+                    if (ch < 0x20) {
+                        char u[8];
+                        snprintf(u, sizeof(u), "\\u%04x", ch);
+                        out += u;
+                    } else {
+                        out += (char)ch;
+                    }
+                }
+            }
+            out += "\":";
+            out.append(num, nl);
+        } else {
+            out.append(k, kl);
+            out += ": ";
+            out.append(num, nl);
+            out += ',';
+        }
+        if (out.size() > (1u << 22)) ok = flush();
+    }
+    out += format == KMER_WRITE_JSON ? "}" : "}\n";
+    ok = ok && flush();
+    ok = (fclose(f) == 0) && ok;
+    return ok ? KMER_OK : KMER_E_IO;
 }
 
 void kmer_result_free(kmer_result *r) { delete r; }

@@ -1,0 +1,134 @@
+/* kmer_map.js — KmerMap: a Map over a packed native result, built lazily.
+ *
+ * readFile() resolves to the reference's Map<kmer, count> in first-occurrence
+ * order (lib/kmers.js:76, :95, :178).  Inserting ~2 M string keys into a V8
+ * Map costs ~1 us each on node 12 (SURVEY.md §6: ~1.2 us/entry), i.e. seconds
+ * at C2 against ~1 ms on the GPU.  KmerMap extends Map (instanceof Map, every
+ * Map method) but keeps the counter's packed result -- one Latin-1 string of
+ * all keys, offsets, counts -- and builds nothing up front:
+ *   - iteration (for..of, keys(), values(), entries(), forEach, spread) walks
+ *     the packed entries in order, cutting each key out of the one string;
+ *   - size is a field;
+ *   - get / has / set / delete build a key -> index Map on their first use;
+ *   - the consumers' mutations (lib/kmerFinderClient.js:132-133 set 'db' /
+ *     'collection', :223-225 and lib/kmerFinderServer.js:781-783 delete) follow
+ *     Map semantics exactly: set on a present key keeps its position, a new (or
+ *     deleted and re-set) key goes to the end, delete removes it.
+ * Packed entries live in this object; keys added later live in the Map base
+ * (super), which therefore holds exactly the entries appended after the
+ * packed block, in insertion order.
+ */
+'use strict';
+
+class KmerMap extends Map {
+    // keys: a Latin-1 string of all keys back to back; off: n + 1 offsets;
+    // cnt: n values (array-like)
+    constructor(keys, off, cnt) {
+        super();
+        this._all = keys;
+        this._off = off;
+        this._cnt = cnt;
+        this._n = cnt.length;
+        this._idx = null;        // key -> packed index (built on first keyed access)
+        this._mod = null;        // packed index -> value set since (Map)
+        this._del = null;        // Uint8Array: packed index deleted
+        this._ndel = 0;
+    }
+
+    static fromNative(res) {
+        const n = res.counts.length;
+        const all = n ? res.keys.latin1Slice(0, res.offsets[n]) : '';
+        return new KmerMap(all, res.offsets, res.counts);
+    }
+
+    _key(i) { return this._all.substring(this._off[i], this._off[i + 1]); }
+
+    _value(i) {
+        if (this._mod !== null) {
+            const v = this._mod.get(i);
+            if (v !== undefined || this._mod.has(i)) return v;
+        }
+        return this._cnt[i];
+    }
+
+    _live(i) { return this._del === null || this._del[i] === 0; }
+
+    _index() {
+        if (this._idx === null) {
+            const m = new Map();
+            for (let i = 0; i < this._n; i += 1) m.set(this._key(i), i);
+            this._idx = m;
+        }
+        return this._idx;
+    }
+
+    // packed index of a live packed key, else -1
+    _find(key) {
+        const i = this._index().get(key);
+        return i !== undefined && this._live(i) ? i : -1;
+    }
+
+    get size() { return this._n - this._ndel + super.size; }
+
+    get(key) {
+        const i = this._find(key);
+        return i >= 0 ? this._value(i) : super.get(key);
+    }
+
+    has(key) { return this._find(key) >= 0 || super.has(key); }
+
+    set(key, value) {
+        const i = this._find(key);
+        if (i >= 0) {
+            if (this._mod === null) this._mod = new Map();
+            this._mod.set(i, value);
+        } else {
+            super.set(key, value);
+        }
+        return this;
+    }
+
+    delete(key) {
+        const i = this._find(key);
+        if (i < 0) return super.delete(key);
+        if (this._del === null) this._del = new Uint8Array(this._n);
+        this._del[i] = 1;
+        this._ndel += 1;
+        if (this._mod !== null) this._mod.delete(i);
+        return true;
+    }
+
+    clear() {
+        this._n = 0;
+        this._ndel = 0;
+        this._all = '';
+        this._idx = null;
+        this._mod = null;
+        this._del = null;
+        super.clear();
+    }
+
+    * entries() {
+        for (let i = 0; i < this._n; i += 1) if (this._live(i)) yield [this._key(i), this._value(i)];
+        yield* super.entries();
+    }
+
+    * keys() {
+        for (let i = 0; i < this._n; i += 1) if (this._live(i)) yield this._key(i);
+        yield* super.keys();
+    }
+
+    * values() {
+        for (let i = 0; i < this._n; i += 1) if (this._live(i)) yield this._value(i);
+        yield* super.values();
+    }
+
+    [Symbol.iterator]() { return this.entries(); }
+
+    forEach(fn, thisArg) {
+        for (let i = 0; i < this._n; i += 1) if (this._live(i)) fn.call(thisArg, this._value(i), this._key(i), this);
+        super.forEach((v, k) => fn.call(thisArg, v, k, this));
+    }
+}
+
+module.exports = { KmerMap };

@@ -31,12 +31,14 @@ namespace {
 struct Handle {
     kmer_ctx *ctx = nullptr;
     bool busy = false;
+    bool close_pending = false;   // close() while a call was in flight: closed when it completes
 };
 
 struct Work {
     napi_async_work work = nullptr;
     napi_ref cb = nullptr;
     napi_ref keep = nullptr;   // keeps the input Buffer alive
+    napi_ref href = nullptr;   // keeps the handle's external alive while Execute uses it
     Handle *h = nullptr;
     std::string path;
     const uint8_t *bytes = nullptr;
@@ -144,6 +146,10 @@ napi_value make_f64_array(napi_env env, const uint64_t *src, size_t n) {
 void Complete(napi_env env, napi_status, void *data) {
     Work *w = static_cast<Work *>(data);
     w->h->busy = false;
+    if (w->h->close_pending && w->h->ctx) {
+        kmer_close(w->h->ctx);
+        w->h->ctx = nullptr;
+    }
     napi_value cb, undef, args[2];
     napi_get_reference_value(env, w->cb, &cb);
     napi_get_undefined(env, &undef);
@@ -175,14 +181,16 @@ void Complete(napi_env env, napi_status, void *data) {
     napi_call_function(env, undef, cb, 2, args, nullptr);
     napi_delete_reference(env, w->cb);
     if (w->keep) napi_delete_reference(env, w->keep);
+    if (w->href) napi_delete_reference(env, w->href);
     napi_delete_async_work(env, w->work);
     delete w;
 }
 
-napi_value queue(napi_env env, Work *w, napi_value cb) {
+napi_value queue(napi_env env, Work *w, napi_value handle, napi_value cb) {
     napi_value name;
     napi_create_string_utf8(env, "kmerhip.count", NAPI_AUTO_LENGTH, &name);
     NAPI_CALL(env, napi_create_reference(env, cb, 1, &w->cb));
+    NAPI_CALL(env, napi_create_reference(env, handle, 1, &w->href));
     NAPI_CALL(env, napi_create_async_work(env, nullptr, name, Execute, Complete, w, &w->work));
     w->h->busy = true;
     NAPI_CALL(env, napi_queue_async_work(env, w->work));
@@ -197,8 +205,9 @@ napi_value CountFile(napi_env env, napi_callback_info info) {
     NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
     Handle *h = get_handle(env, argv[0]);
     if (!h) return nullptr;
-    if (h->busy) {
-        napi_throw_error(env, nullptr, "kmerhip handle busy (one in-flight call per context)");
+    if (h->busy || !h->ctx) {
+        napi_throw_error(env, nullptr, h->ctx ? "kmerhip handle busy (one in-flight call per context)"
+                                              : "kmerhip handle closed");
         return nullptr;
     }
     size_t n = 0;
@@ -209,7 +218,7 @@ napi_value CountFile(napi_env env, napi_callback_info info) {
     w->path.resize(n);
     w->h = h;
     w->is_file = true;
-    return queue(env, w, argv[2]);
+    return queue(env, w, argv[0], argv[2]);
 }
 
 napi_value CountBuffer(napi_env env, napi_callback_info info) {
@@ -218,8 +227,9 @@ napi_value CountBuffer(napi_env env, napi_callback_info info) {
     NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
     Handle *h = get_handle(env, argv[0]);
     if (!h) return nullptr;
-    if (h->busy) {
-        napi_throw_error(env, nullptr, "kmerhip handle busy (one in-flight call per context)");
+    if (h->busy || !h->ctx) {
+        napi_throw_error(env, nullptr, h->ctx ? "kmerhip handle busy (one in-flight call per context)"
+                                              : "kmerhip handle closed");
         return nullptr;
     }
     void *data = nullptr;
@@ -230,7 +240,7 @@ napi_value CountBuffer(napi_env env, napi_callback_info info) {
     w->bytes = (const uint8_t *)data;
     w->len = len;
     NAPI_CALL(env, napi_create_reference(env, argv[1], 1, &w->keep));
-    return queue(env, w, argv[2]);
+    return queue(env, w, argv[0], argv[2]);
 }
 
 napi_value Close(napi_env env, napi_callback_info info) {
@@ -239,7 +249,9 @@ napi_value Close(napi_env env, napi_callback_info info) {
     NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
     Handle *h = get_handle(env, argv[0]);
     if (!h) return nullptr;
-    if (h->ctx && !h->busy) {
+    if (h->busy) {
+        h->close_pending = true;          // closed by the in-flight call's completion
+    } else if (h->ctx) {
         kmer_close(h->ctx);
         h->ctx = nullptr;
     }

@@ -9,9 +9,12 @@
  * plus the legacy npm-main loop `kmers(line, kmerMap, length, preffix, step)`
  * (lib/index.js:60-73).
  *
- * readFile() resolves to this.kmerMap: a real, mutable JS Map whose
- * iteration order is the reference's first-occurrence order (consumers rely on
- * it: lib/kmerFinderServer.js:175,742).  kmersInLine() stays a synchronous CPU
+ * readFile() resolves to this.kmerMap: a mutable JS Map (a KmerMap, which
+ * extends Map and is filled lazily from the packed native result, when the
+ * Map was empty) whose iteration order is the reference's first-occurrence
+ * order (consumers rely on it: lib/kmerFinderServer.js:175,742).  More than
+ * this.maxKeys (2^24, the reference Map's limit) distinct keys reject the
+ * promise with a RangeError, as Map.set throws in the reference.  kmersInLine() stays a synchronous CPU
  * loop over one line, as in the reference (lib/kmers.js:88-100).
  *
  * Documented divergences (error/diagnostic paths only): a missing file
@@ -22,6 +25,12 @@
 'use strict';
 const EventEmitter = require('events');
 const path = require('path');
+const { KmerMap } = require('./kmer_map.js');
+
+// the reference Map's capacity: Map.set throws RangeError beyond 2^24 keys
+// (lib/kmers.js:95); the native count is told the same limit and rejects
+const MAP_MAX_KEYS = 16777216;
+const KMER_E_TOO_MANY_KEYS = 5;
 
 let addon = null;
 function native() {
@@ -86,26 +95,26 @@ function kmers(line, kmerMap, length, preffix, step) {
     return true;
 }
 
-// Fold a packed native result into an existing Map, preserving Map semantics:
-// existing keys keep their position, new keys append in first-occurrence order.
-// Fresh Map (the readFile() case): the result's keys are unique, so every
-// entry is a plain set(); the keys are substrings of ONE Latin-1 string
-// (V8 sliced strings), ~20% faster than a Buffer slice per key.
+// Fold a packed native result into an existing, non-empty Map, preserving
+// Map semantics: existing keys keep their position, new keys append in
+// first-occurrence order.  (An empty Map is replaced by a KmerMap instead.)
 function foldResult(map, res) {
     const keys = res.keys;
     const off = res.offsets;
     const cnt = res.counts;
     const n = cnt.length;
-    if (map.size === 0) {
-        const all = keys.latin1Slice(0, n ? off[n] : 0);
-        for (let i = 0; i < n; i += 1) map.set(all.substring(off[i], off[i + 1]), cnt[i]);
-        return;
-    }
+    const all = keys.latin1Slice(0, n ? off[n] : 0);
     for (let i = 0; i < n; i += 1) {
-        const key = keys.latin1Slice(off[i], off[i + 1]);
+        const key = all.substring(off[i], off[i + 1]);
         const prev = map.get(key);
         map.set(key, prev === undefined ? cnt[i] : prev + cnt[i]);
     }
+}
+
+function tooManyKeys(msg) {
+    const e = new RangeError(msg);
+    e.status = KMER_E_TOO_MANY_KEYS;
+    return e;
 }
 
 class KmerJS {
@@ -121,6 +130,7 @@ class KmerJS {
         this.kmerMap = new Map();
         this.kmerMapSize = 0;
         this.env = env;
+        this.maxKeys = MAP_MAX_KEYS;     // the reference Map's limit (lib/kmers.js:95)
         if (env === 'browser') this.fileDataRead = 0;
     }
 
@@ -149,8 +159,10 @@ class KmerJS {
             }
             let handle;
             try {
+                // (the native result alone may not exceed the limit; a pre-filled
+                // Map is checked again after the fold)
                 handle = native().open(kmerObj.kmerLength, Buffer.from(String(kmerObj.preffix), 'latin1'),
-                    kmerObj.step, Number(process.env.KMERHIP_DEVICE || 0));
+                    kmerObj.step, Number(process.env.KMERHIP_DEVICE || 0), 0, kmerObj.maxKeys);
             } catch (e) {
                 reject(e);
                 return;
@@ -158,10 +170,20 @@ class KmerJS {
             native().countFile(handle, String(kmerObj.fastq), (err, res) => {
                 native().close(handle);
                 if (err) {
-                    reject(err);
+                    reject(err.status === KMER_E_TOO_MANY_KEYS ? tooManyKeys(err.message) : err);
                     return;
                 }
-                foldResult(kmerObj.kmerMap, res);
+                try {
+                    if (kmerObj.kmerMap.size === 0 && !(kmerObj.kmerMap instanceof KmerMap)) {
+                        kmerObj.kmerMap = KmerMap.fromNative(res);      // built lazily (kmer_map.js)
+                    } else {
+                        foldResult(kmerObj.kmerMap, res);
+                        if (kmerObj.kmerMap.size > kmerObj.maxKeys) throw tooManyKeys('Map maximum size exceeded');
+                    }
+                } catch (e) {
+                    reject(e);        // (never an exception escaping the completion callback)
+                    return;
+                }
                 kmerObj.lines = res.lines;
                 event.emit('progress', { percentage: 100, transferred: 0, length: 0 });
                 if (kmerObj.progress) {
@@ -183,5 +205,5 @@ function kmerjs(fastq, preffix = 'ATGAC', length = 16, step = 1) {
 
 module.exports = {
     complementMap, jsonToStrMap, complement, stringToMap, objectToMap, mapToJSON, KmerJS,
-    kmers, kmerjs, version: () => native().version(),
+    kmers, kmerjs, KmerMap, version: () => native().version(), native,
 };

@@ -57,6 +57,63 @@ function cpuTests() {
     check('addon loads', () => {
         assert.ok(/gfx950/.test(lib.version()));
     });
+    check('KmerMap follows Map semantics (random operations vs a real Map)', () => {
+        // packed result of n distinct keys, as the addon hands it over
+        const n = 500;
+        const keys = [];
+        for (let i = 0; i < n; i += 1) keys.push('K' + ((i * 7919) % 100003).toString(36) + 'x'.repeat(i % 5));
+        const buf = Buffer.from(keys.join(''), 'latin1');
+        const off = new Float64Array(n + 1);
+        for (let i = 0; i < n; i += 1) off[i + 1] = off[i] + keys[i].length;
+        const cnt = new Float64Array(n);
+        for (let i = 0; i < n; i += 1) cnt[i] = (i % 13) + 1;
+        const km = lib.KmerMap.fromNative({ keys: buf, offsets: off, counts: cnt });
+        const ref = new Map();
+        for (let i = 0; i < n; i += 1) ref.set(keys[i], cnt[i]);
+        assert.ok(km instanceof Map);
+        const same = () => {
+            assert.strictEqual(km.size, ref.size);
+            assert.deepStrictEqual([...km], [...ref]);
+            assert.deepStrictEqual([...km.keys()], [...ref.keys()]);
+            assert.deepStrictEqual([...km.values()], [...ref.values()]);
+            const a = []; km.forEach((v, k, m) => { assert.strictEqual(m, km); a.push([k, v]); });
+            assert.deepStrictEqual(a, [...ref]);
+        };
+        same();                                     // before any keyed access (lazy)
+        let x = 1;
+        const rnd = (m) => { x = (x * 1103515245 + 12345) % 2147483648; return x % m; };
+        for (let step = 0; step < 3000; step += 1) {
+            const op = rnd(6);
+            const key = rnd(3) === 0 ? 'new' + rnd(40) : keys[rnd(n)];
+            if (op === 0) { km.set(key, step); ref.set(key, step); }
+            else if (op === 1) assert.strictEqual(km.delete(key), ref.delete(key));
+            else if (op === 2) assert.strictEqual(km.get(key), ref.get(key));
+            else if (op === 3) assert.strictEqual(km.has(key), ref.has(key));
+            else if (op === 4) { km.set('db', 'Kmers'); ref.set('db', 'Kmers'); }
+            else { km.delete('db'); ref.delete('db'); }
+            if (step % 500 === 0) same();
+        }
+        same();
+        assert.strictEqual(lib.mapToJSON(km)[keys[1]], ref.get(keys[1]));
+        km.clear(); ref.clear();
+        same();
+    });
+    check('legacy npm main (lib/index.js) exports and fields', () => {
+        const legacy = require(path.join(repo, 'kmerjs_amd', 'node', 'index.js'));
+        for (const name of ['kmers', 'complement', 'KmerJSClient', 'KmerJSServer']) assert.ok(name in legacy, name);
+        const s = new legacy.KmerJSServer('x.fastq');
+        assert.strictEqual(s.preffix, 'ATGAC');
+        assert.strictEqual(s.length, 16);
+        assert.strictEqual(s.step, 1);
+        assert.strictEqual(s.uKmers, 0);
+        assert.deepStrictEqual(s.db, { type: 'mongo', url: 'mongodb://localhost:27017/Kmers' });
+        assert.strictEqual(s.evalue.cmp(0.05), 0);
+        assert.strictEqual(s.mapToJSON(new Map([['a', 1]])), '{"a":1}');
+        const c = new legacy.KmerJSClient('x.fastq', 'AT', 5, 1, 1, '', 'json');
+        assert.strictEqual(c.url, 'http://localhost:3000/kmers');
+        assert.strictEqual(c.db.url, '../test_data/db.json');
+        assert.strictEqual(legacy.complement('ATGACCTGAGAGCCTT'), 'AAGGCTCTCAGGTCAT');
+    });
 }
 
 function sha(s) { return crypto.createHash('sha256').update(s, 'utf8').digest('hex'); }
@@ -95,7 +152,66 @@ async function gpuTests() {
     }
     // the Map is a real mutable Map, consumers may add / delete keys
     short.set('db', 'Kmers'); short.delete('ATGACGCAATACTCCT');
-    results.push({ name: 'result Map is mutable', ok: short.size === 2 && short.get('db') === 'Kmers' });
+    results.push({ name: 'result Map is mutable', ok: short.size === 2 && short.get('db') === 'Kmers'
+        && short instanceof Map && [...short][1][0] === 'db' });
+    // more distinct keys than the Map may hold: the promise rejects with a
+    // RangeError (the reference's Map.set throws, lib/kmers.js:95)
+    {
+        const kj = new KmerJS(path.join(repo, 'tests', 'golden', 'inputs', 'test_long.kmer.fastq'), 'ATGAC', 16, 1, 1, false);
+        kj.maxKeys = 100;
+        try {
+            await kj.readFile().promise;
+            results.push({ name: 'too many keys rejects', ok: false });
+        } catch (e) {
+            results.push({ name: 'too many keys rejects', ok: e instanceof RangeError && e.status === 5 });
+        }
+        // a pre-filled Map: the fold checks the limit after merging
+        const kp = new KmerJS(path.join(repo, 'tests', 'golden', 'inputs', 'test_long.kmer.fastq'), 'ATGAC', 16, 1, 1, false);
+        kp.maxKeys = 401;
+        kp.kmerMap.set('pre', 1);
+        try {
+            await kp.readFile().promise;
+            results.push({ name: 'pre-filled Map over the limit rejects', ok: false });
+        } catch (e) {
+            results.push({ name: 'pre-filled Map over the limit rejects', ok: e instanceof RangeError });
+        }
+        const kq = new KmerJS(path.join(repo, 'tests', 'golden', 'inputs', 'test_long.kmer.fastq'), 'ATGAC', 16, 1, 1, false);
+        kq.kmerMap.set('pre', 1);
+        const mq = await kq.readFile().promise;
+        results.push({ name: 'pre-filled Map folds', ok: mq.size === 402 && [...mq][0][0] === 'pre' && mq === kq.kmerMap });
+    }
+    // legacy npm main: KmerJSServer/KmerJSClient.findKmers (lib/index.js:250-306, :402-408, :327-332)
+    {
+        const legacy = require(path.join(repo, 'kmerjs_amd', 'node', 'index.js'));
+        const cases = golden.cases.filter((c) => c.step === 1 && [16, 31].includes(c.k) && ['ATGAC', ''].includes(c.prefix));
+        for (const c of cases) {
+            const file = path.join(repo, 'tests', 'golden', 'inputs', c.input);
+            for (const Cls of [legacy.KmerJSServer, legacy.KmerJSClient]) {
+                const o = new Cls(file, c.prefix, c.k, c.step);
+                try {
+                    const m = await o.findKmers();
+                    const ok = sha(JSON.stringify([...m])) === c.digest && o.uKmers === c.size;
+                    results.push({ name: `${Cls.name}.findKmers ${c.input} '${c.prefix}' k=${c.k}`, ok });
+                } catch (e) {
+                    results.push({ name: `${Cls.name}.findKmers ${c.input}`, ok: false, err: String(e) });
+                }
+            }
+        }
+    }
+    // close() while a count is in flight: closed when it completes (no use after free)
+    {
+        const nat = lib.native();
+        const h = nat.open(16, Buffer.from('ATGAC', 'latin1'), 1, 0);
+        const done = new Promise((resolve) => {
+            nat.countFile(h, path.join(repo, 'tests', 'golden', 'inputs', 'test_long.kmer.fastq'), (err, res) => {
+                resolve(!err && res.counts.length === 401);
+            });
+        });
+        nat.close(h);
+        let reuse = false;
+        try { nat.countFile(h, 'x', () => {}); } catch (e) { reuse = true; }
+        results.push({ name: 'close while busy is deferred', ok: (await done) && reuse });
+    }
 }
 
 (async () => {

@@ -393,3 +393,27 @@ def test_dense_hit_path_vs_oracle(native, k, prefix):
     ctr.close()
     assert len(got) == len(want)
     assert first_diff(got, want) is None
+
+
+def test_gzip_input_and_result_writers(native, tmp_path, inputs, golden):
+    # gzip FASTQ is read through zlib (count = that of the decompressed bytes);
+    # the native writers match JSON.stringify(mapToJSON(map)) (lib/kmers.js:46-54)
+    # and the npm main's text dump (lib/index.js:381-388)
+    import gzip
+    import json
+    for name in ("test_kmers.fastq", "edge_crlf.fastq", "test_long.kmer.fastq"):
+        plain = tmp_path / name
+        plain.write_bytes(inputs[name])
+        gz = tmp_path / (name + ".gz")
+        gz.write_bytes(gzip.compress(inputs[name]))
+        for p in (b"ATGAC", b""):
+            ctr = native.Counter(k=16, prefix=p)
+            a = ctr.count_file(str(plain), write=str(tmp_path / "a.json"), fmt=native.WRITE_JSON)
+            b = ctr.count_file(str(gz), write=str(tmp_path / "b.txt"), fmt=native.WRITE_LEGACY)
+            ctr.close()
+            assert a.entries() == b.entries() and a.lines == b.lines
+            obj = {k.decode("latin-1"): v for k, v in a.entries()}
+            assert (tmp_path / "a.json").read_bytes().decode("latin-1") == \
+                json.dumps(obj, separators=(",", ":"), ensure_ascii=False)
+            legacy = "{\n" + "".join("%s: %d," % (k.decode("latin-1"), v) for k, v in a.entries()) + "}\n"
+            assert (tmp_path / "b.txt").read_bytes().decode("latin-1") == legacy   # (keys may hold '\r')
