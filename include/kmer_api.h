@@ -75,6 +75,17 @@ typedef struct {
     uint32_t flags;           /* KMER_FLAG_* */
     uint64_t max_keys;        /* 0 = unlimited; 16777216 reproduces the reference Map cap */
     uint64_t batch_bytes;     /* host->device batch size for file/buffer input; 0 = default (1 GiB) */
+    /* Multi-GPU (SURVEY.md §8b `ndev`): ndev > 1 makes a group context over
+     * `devices` (ndev HIP ordinals; NULL = 0..ndev-1; an ordinal may repeat).
+     * kmer_count_file / kmer_count_buffer then split the input into ndev
+     * line-aligned shards counted concurrently, one per device, and merge the
+     * per-device partials (copied to devices[0] over xGMI) into one result in
+     * Map order -- bit-exact with a single-device count.  Configurations
+     * without packed keys (non-ACGT prefix, step > 1, k > 32, table mode) run
+     * on devices[0] alone.  The device-resident entry points are single-device
+     * only (KMER_E_STATE on a group).  0 or 1 = single device `device`. */
+    uint32_t ndev;
+    const int32_t *devices;
 } kmer_params;
 
 typedef struct kmer_ctx kmer_ctx;

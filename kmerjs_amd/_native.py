@@ -37,7 +37,8 @@ class Params(ctypes.Structure):
     _fields_ = [("k", ctypes.c_uint32), ("step", ctypes.c_uint32),
                 ("prefix", ctypes.c_char_p), ("prefix_len", ctypes.c_uint32),
                 ("device", ctypes.c_int32), ("flags", ctypes.c_uint32),
-                ("max_keys", ctypes.c_uint64), ("batch_bytes", ctypes.c_uint64)]
+                ("max_keys", ctypes.c_uint64), ("batch_bytes", ctypes.c_uint64),
+                ("ndev", ctypes.c_uint32), ("devices", ctypes.POINTER(ctypes.c_int32))]
 
 
 class KmerError(RuntimeError):
@@ -163,12 +164,19 @@ class Result:
 class Counter:
     """One kmer_ctx (device, configuration)."""
 
-    def __init__(self, k=16, prefix=b"ATGAC", step=1, device=0, flags=0, max_keys=0, batch_bytes=0):
+    def __init__(self, k=16, prefix=b"ATGAC", step=1, device=0, flags=0, max_keys=0, batch_bytes=0, devices=None):
+        """devices: a list of HIP ordinals (ordinals may repeat) -> a multi-GPU
+        group context: count_buffer / count_file shard the input over them and
+        merge into one result (kmer_params.ndev)."""
         if isinstance(prefix, str):
             prefix = prefix.encode("latin-1")
         self._prefix = prefix
         p = Params(k=k, step=step, prefix=prefix, prefix_len=len(prefix), device=device, flags=flags,
                    max_keys=max_keys, batch_bytes=batch_bytes)
+        if devices is not None and len(devices) > 1:
+            self._devs = (ctypes.c_int32 * len(devices))(*devices)
+            p.ndev = len(devices)
+            p.devices = self._devs
         h = ctypes.c_void_p()
         st = LIB.kmer_open(ctypes.byref(p), ctypes.byref(h))
         if st != KMER_OK:

@@ -28,6 +28,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -199,6 +200,12 @@ struct kmer_ctx {
     uint64_t t_canon = 0, t_nkeys = 0, t_sum = 0, t_nbig = 0;   // last finish
     bool t_done = false;           // a table finish holds results
     hipEvent_t tev[8] = {};        // table phase events
+    // multi-device group (kmer_params.ndev > 1): one child context per device;
+    // the group itself owns no device state beyond the merge buffers on
+    // devices[0] (allocated through child 0)
+    std::vector<kmer_ctx *> group;
+    DBuf<uint64_t> gkeys;
+    DBuf<Agg> gvals;
     double t_ms[6] = {};           // table phase times since the reset: lines, hist1, scatter1, hist2, scatter2, final
     int n_cu = 0;
     // timing (HIP events on the context stream)
@@ -595,10 +602,11 @@ kmer_status settle(kmer_ctx *c) {
     return KMER_OK;
 }
 
-#define SETTLE(ctx)                          \
-    do {                                     \
-        const kmer_status st_ = settle(ctx); \
-        if (st_) return st_;                 \
+#define SETTLE(ctx)                                                                       \
+    do {                                                                                  \
+        if (!(ctx)->group.empty()) return fail(ctx, KMER_E_STATE, "single-device call on a group context"); \
+        const kmer_status st_ = settle(ctx);                                              \
+        if (st_) return st_;                                                              \
     } while (0)
 
 // ---------------------------------------------------------------------------
@@ -1480,6 +1488,161 @@ kmer_status feed_host(kmer_ctx *c, const uint8_t *bytes, uint64_t len) {
     return KMER_OK;
 }
 
+// ---------------------------------------------------------------------------
+// multi-device group (kmer_params.ndev > 1)
+// ---------------------------------------------------------------------------
+// Count `bytes` on every child in line-aligned shards and merge on child 0:
+// shard i starts after a '\n' near i/ndev of the input; its first line index
+// (newlines before it) comes from a threaded host count; each child resets,
+// takes its position, feeds its shard and reduces it to unique packed keys
+// {first, count} (kmer_partial_device); the partials are copied in shard
+// order to devices[0] (peer copies over xGMI) and finished there
+// (kmer_finish_merged: min first, sum counts, Map order).  Record keys
+// (non-ACGT windows) move from every child to child 0 on the host.
+kmer_status group_count_buffer(kmer_ctx *g, const uint8_t *bytes, uint64_t len, kmer_result **out) {
+    const size_t N = g->group.size();
+    kmer_ctx *c0 = g->group[0];
+    if (c0->mode != MODE_PACKED && c0->mode != MODE_WINDOWS) {
+        // no packed partials to merge: the whole input on devices[0]
+        kmer_status st = kmer_count_buffer(c0, bytes, len, out);
+        if (st) g->err = c0->err;
+        return st;
+    }
+    std::vector<uint64_t> cut(N + 1, len);
+    cut[0] = 0;
+    for (size_t i = 1; i < N; ++i) {
+        uint64_t p = std::max<uint64_t>(cut[i - 1], len / N * i);
+        if (p > 0 && p < len) {
+            const void *nl = memchr(bytes + p - 1, '\n', len - (p - 1));
+            p = nl ? (uint64_t)((const uint8_t *)nl - bytes) + 1 : len;
+        }
+        cut[i] = std::min<uint64_t>(p, len);
+    }
+    std::vector<uint64_t> nls(N, 0);
+    {
+        std::vector<std::thread> th;
+        for (size_t i = 0; i < N; ++i)
+            th.emplace_back([&, i]() {
+                uint64_t n = 0;
+                const uint8_t *p = bytes + cut[i], *e = bytes + cut[i + 1];
+                while (p < e) {
+                    const void *q = memchr(p, '\n', (size_t)(e - p));
+                    if (!q) break;
+                    ++n;
+                    p = (const uint8_t *)q + 1;
+                }
+                nls[i] = n;
+            });
+        for (auto &t : th) t.join();
+    }
+    std::vector<uint64_t> before(N, 0);
+    for (size_t i = 1; i < N; ++i) before[i] = before[i - 1] + nls[i - 1];
+    const uint64_t total_lines = before[N - 1] + nls[N - 1] + ((len > 0 && bytes[len - 1] != '\n') ? 1 : 0);
+    std::vector<kmer_status> sts(N, KMER_OK);
+    std::vector<const void *> pk(N, nullptr), pv(N, nullptr);
+    std::vector<uint64_t> pn(N, 0);
+    {
+        std::vector<std::thread> th;
+        for (size_t i = 0; i < N; ++i)
+            th.emplace_back([&, i]() {
+                kmer_ctx *c = g->group[i];
+                if (hipSetDevice(c->device) != hipSuccess) {
+                    sts[i] = KMER_E_DEVICE;
+                    return;
+                }
+                kmer_status st = reset(c);
+                if (!st) st = kmer_set_position(c, before[i], cut[i]);
+                if (!st) st = feed_host(c, bytes + cut[i], cut[i + 1] - cut[i]);
+                if (!st) st = kmer_partial_device(c, &pk[i], &pv[i], &pn[i]);
+                if (st) c->open_stream = false;
+                sts[i] = st;
+            });
+        for (auto &t : th) t.join();
+    }
+    for (size_t i = 0; i < N; ++i)
+        if (sts[i]) return fail(g, sts[i], "device " + std::to_string(g->group[i]->device) + ": " + g->group[i]->err);
+    // partials -> devices[0], in shard order
+    uint64_t n = 0;
+    for (size_t i = 0; i < N; ++i) n += pn[i];
+    if (hipSetDevice(c0->device) != hipSuccess) return fail(g, KMER_E_DEVICE, "hipSetDevice");
+    hipStream_t s = c0->stream;
+    HIPCHK(g, g->gkeys.ensure(n, s));
+    HIPCHK(g, g->gvals.ensure(n, s));
+    uint64_t o = 0;
+    for (size_t i = 0; i < N; ++i) {
+        if (!pn[i]) continue;
+        kmer_ctx *c = g->group[i];
+        if (c->device == c0->device) {
+            HIPCHK(g, hipMemcpyAsync(g->gkeys.p + o, pk[i], pn[i] * 8, hipMemcpyDeviceToDevice, s));
+            HIPCHK(g, hipMemcpyAsync(g->gvals.p + o, pv[i], pn[i] * sizeof(Agg), hipMemcpyDeviceToDevice, s));
+        } else {
+            HIPCHK(g, hipMemcpyPeerAsync(g->gkeys.p + o, c0->device, pk[i], c->device, pn[i] * 8, s));
+            HIPCHK(g, hipMemcpyPeerAsync(g->gvals.p + o, c0->device, pv[i], c->device, pn[i] * sizeof(Agg), s));
+        }
+        o += pn[i];
+    }
+    HIPCHK(g, hipStreamSynchronize(s));
+    for (size_t i = 1; i < N; ++i) {
+        kmer_result *r = nullptr;
+        kmer_status st = kmer_records_export(g->group[i], &r);
+        if (st) return fail(g, st, "records export");
+        const uint64_t m = kmer_result_size(r);
+        if (m) {
+            const char *kb = nullptr;
+            const uint64_t *off = nullptr, *cnt = nullptr, *fst = nullptr;
+            kmer_result_arrays(r, &kb, &off, &cnt);
+            kmer_result_firsts(r, &fst);
+            st = kmer_records_import(c0, kb, off, cnt, fst, m);
+        }
+        kmer_result_free(r);
+        if (st) return fail(g, st, "records import");
+    }
+    kmer_status st = kmer_finish_merged(c0, g->gkeys.p, g->gvals.p, n, total_lines, out);
+    if (st) return fail(g, st, c0->err);
+    return KMER_OK;
+}
+
+// A whole file into host memory (mmap when plain, zlib when gzip), then the group count.
+kmer_status group_count_file(kmer_ctx *g, const char *path, kmer_result **out) {
+    gzFile gz = gzopen(path, "rb");
+    if (!gz) return fail(g, KMER_E_IO, std::string("cannot open ") + path);
+    gzbuffer(gz, 1 << 20);
+    std::vector<uint8_t> data;
+    size_t cap = 1 << 24, len = 0;
+    {
+        struct stat sb;
+        if (stat(path, &sb) == 0 && S_ISREG(sb.st_mode)) cap = std::max<size_t>(cap, (size_t)sb.st_size + 1);
+    }
+    std::unique_ptr<uint8_t[]> buf(new (std::nothrow) uint8_t[cap]);
+    if (!buf) {
+        gzclose(gz);
+        return fail(g, KMER_E_OOM, "host buffer");
+    }
+    while (true) {                             // (gzread passes plain files through)
+        if (len == cap) {
+            const size_t nc = cap * 2;
+            std::unique_ptr<uint8_t[]> nb(new (std::nothrow) uint8_t[nc]);
+            if (!nb) {
+                gzclose(gz);
+                return fail(g, KMER_E_OOM, "host buffer");
+            }
+            memcpy(nb.get(), buf.get(), len);
+            buf = std::move(nb);
+            cap = nc;
+        }
+        const unsigned want = (unsigned)std::min<size_t>(cap - len, 1u << 30);
+        const int r = gzread(gz, buf.get() + len, want);
+        if (r < 0) {
+            gzclose(gz);
+            return fail(g, KMER_E_IO, std::string("read error on ") + path);
+        }
+        len += (size_t)r;
+        if (r == 0) break;
+    }
+    gzclose(gz);
+    return group_count_buffer(g, buf.get(), len, out);
+}
+
 }  // namespace
 
 extern "C" {
@@ -1507,6 +1670,32 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
     if (!pp || !out) return KMER_E_BAD_PARAM;
     if (pp->k == 0 || pp->step == 0 || (pp->prefix_len && !pp->prefix)) return KMER_E_BAD_PARAM;
     *out = nullptr;
+    if (pp->ndev > 1) {
+        if (pp->ndev > 64) return KMER_E_BAD_PARAM;
+        kmer_ctx *g = new (std::nothrow) kmer_ctx();
+        if (!g) return KMER_E_OOM;
+        g->p = *pp;
+        g->p.prefix = nullptr;
+        g->p.devices = nullptr;
+        g->prefix.assign((const char *)pp->prefix, pp->prefix_len);
+        for (uint32_t i = 0; i < pp->ndev; ++i) {
+            kmer_params cp = *pp;
+            cp.ndev = 1;
+            cp.devices = nullptr;
+            cp.device = pp->devices ? pp->devices[i] : (int32_t)i;
+            kmer_ctx *c = nullptr;
+            const kmer_status st = kmer_open(&cp, &c);
+            if (st) {
+                kmer_close(g);
+                return st;
+            }
+            g->group.push_back(c);
+        }
+        g->device = g->group[0]->device;
+        g->mode = g->group[0]->mode;
+        *out = g;
+        return KMER_OK;
+    }
     kmer_ctx *c = new (std::nothrow) kmer_ctx();
     if (!c) return KMER_E_OOM;
     c->p = *pp;
@@ -1622,6 +1811,15 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
 
 kmer_status kmer_close(kmer_ctx *c) {
     if (!c) return KMER_E_BAD_PARAM;
+    if (!c->group.empty()) {
+        if (hipSetDevice(c->group[0]->device) == hipSuccess) {
+            c->gkeys.release();
+            c->gvals.release();
+        }
+        for (kmer_ctx *x : c->group) kmer_close(x);
+        delete c;
+        return KMER_OK;
+    }
     (void)hipSetDevice(c->device);
     (void)settle(c);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
@@ -1677,12 +1875,14 @@ kmer_status kmer_close(kmer_ctx *c) {
 
 kmer_status kmer_sync(kmer_ctx *c) {
     if (!c) return KMER_E_BAD_PARAM;
+    if (!c->group.empty()) return fail(c, KMER_E_STATE, "single-device call on a group context");
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
     return settle(c);
 }
 
 kmer_status kmer_reset(kmer_ctx *c) {
     if (!c) return KMER_E_BAD_PARAM;
+    if (!c->group.empty()) return fail(c, KMER_E_STATE, "single-device call on a group context");
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
     return reset(c);
 }
@@ -1715,6 +1915,7 @@ kmer_status kmer_finish_device(kmer_ctx *c, kmer_result **out) {
 kmer_status kmer_count_buffer(kmer_ctx *c, const uint8_t *bytes, size_t len, kmer_result **out) {
     if (!c || !out || (!bytes && len)) return KMER_E_BAD_PARAM;
     *out = nullptr;
+    if (!c->group.empty()) return group_count_buffer(c, bytes, len, out);
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
     kmer_status st = reset(c);
     if (st) return st;
@@ -1729,6 +1930,7 @@ kmer_status kmer_count_buffer(kmer_ctx *c, const uint8_t *bytes, size_t len, kme
 kmer_status kmer_count_file(kmer_ctx *c, const char *path, kmer_result **out) {
     if (!c || !path || !out) return KMER_E_BAD_PARAM;
     *out = nullptr;
+    if (!c->group.empty()) return group_count_file(c, path, out);
     FILE *f = fopen(path, "rb");
     if (!f) return fail(c, KMER_E_IO, std::string("cannot open ") + path);
     if (hipSetDevice(c->device) != hipSuccess) {

@@ -46,7 +46,7 @@ function countPath(kmerObj, fastq) {
         let handle;
         try {
             handle = drop.native().open(kmerObj.length, Buffer.from(String(kmerObj.preffix), 'latin1'),
-                kmerObj.step, Number(process.env.KMERHIP_DEVICE || 0), 0, kmerObj.maxKeys);
+                kmerObj.step, Number(process.env.KMERHIP_DEVICE || 0), 0, kmerObj.maxKeys, 0, drop.devices(kmerObj));
         } catch (e) {
             reject(e);
             return;

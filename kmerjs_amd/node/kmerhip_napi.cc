@@ -4,7 +4,8 @@
 // where kmers.js builds the Map in the reference's insertion order.
 //
 // JS surface (used by kmers.js only):
-//   open(k, prefixBuffer, step, device, flags, maxKeys, batchBytes) -> handle
+//   open(k, prefixBuffer, step, device, flags, maxKeys, batchBytes, devices[]) -> handle
+//     (devices: >= 2 HIP ordinals -> a multi-GPU group context, kmer_params.ndev)
 //   countFile(handle, path, cb(err, {keys, offsets, counts, lines}))
 //   countBuffer(handle, buffer, cb(err, {...}))
 //   close(handle)
@@ -74,8 +75,8 @@ uint32_t get_u32(napi_env env, napi_value v, uint32_t dflt) {
 }
 
 napi_value Open(napi_env env, napi_callback_info info) {
-    size_t argc = 7;
-    napi_value argv[7];
+    size_t argc = 8;
+    napi_value argv[8];
     NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
     if (argc < 3) {
         napi_throw_type_error(env, nullptr, "open(k, prefix, step, ...)");
@@ -105,6 +106,24 @@ napi_value Open(napi_env env, napi_callback_info info) {
     if (argc > 6) {
         double d = 0;
         if (napi_get_value_double(env, argv[6], &d) == napi_ok && d > 0) p.batch_bytes = (uint64_t)d;
+    }
+    std::vector<int32_t> devs;
+    if (argc > 7) {                      // devices: an array of HIP ordinals -> multi-GPU group
+        bool arr = false;
+        napi_is_array(env, argv[7], &arr);
+        if (arr) {
+            uint32_t n = 0;
+            napi_get_array_length(env, argv[7], &n);
+            for (uint32_t i = 0; i < n; ++i) {
+                napi_value e;
+                napi_get_element(env, argv[7], i, &e);
+                devs.push_back((int32_t)get_u32(env, e, 0));
+            }
+        }
+    }
+    if (devs.size() > 1) {
+        p.ndev = (uint32_t)devs.size();
+        p.devices = devs.data();
     }
     Handle *h = new Handle();
     kmer_status st = kmer_open(&p, &h->ctx);

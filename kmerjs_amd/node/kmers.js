@@ -111,6 +111,15 @@ function foldResult(map, res) {
     }
 }
 
+// GPUs of one count: this.devices (an array of HIP ordinals) or
+// KMERHIP_DEVICES="0,1,..."; two or more shard the file over them (one
+// result, merged over xGMI; kmer_params.ndev)
+function devices(kmerObj) {
+    if (Array.isArray(kmerObj.devices)) return kmerObj.devices;
+    const env = process.env.KMERHIP_DEVICES;
+    return env ? env.split(',').map(Number) : [];
+}
+
 function tooManyKeys(msg) {
     const e = new RangeError(msg);
     e.status = KMER_E_TOO_MANY_KEYS;
@@ -162,7 +171,7 @@ class KmerJS {
                 // (the native result alone may not exceed the limit; a pre-filled
                 // Map is checked again after the fold)
                 handle = native().open(kmerObj.kmerLength, Buffer.from(String(kmerObj.preffix), 'latin1'),
-                    kmerObj.step, Number(process.env.KMERHIP_DEVICE || 0), 0, kmerObj.maxKeys);
+                    kmerObj.step, Number(process.env.KMERHIP_DEVICE || 0), 0, kmerObj.maxKeys, 0, devices(kmerObj));
             } catch (e) {
                 reject(e);
                 return;
@@ -205,5 +214,5 @@ function kmerjs(fastq, preffix = 'ATGAC', length = 16, step = 1) {
 
 module.exports = {
     complementMap, jsonToStrMap, complement, stringToMap, objectToMap, mapToJSON, KmerJS,
-    kmers, kmerjs, KmerMap, version: () => native().version(), native,
+    kmers, kmerjs, KmerMap, version: () => native().version(), native, devices,
 };

@@ -198,6 +198,19 @@ async function gpuTests() {
             }
         }
     }
+    // multi-GPU through readFile(): two shards on a device group (ordinal 0 twice
+    // on a one-GPU box), merged into the same ordered Map
+    for (const c of golden.cases.filter((x) => x.step === 1 && x.k === 16 && ['ATGAC', ''].includes(x.prefix))) {
+        const kj = new KmerJS(path.join(repo, 'tests', 'golden', 'inputs', c.input), c.prefix, c.k, 1, 1, false);
+        kj.devices = [0, 0];
+        try {
+            const m = await kj.readFile().promise;
+            const ok = sha(JSON.stringify([...m])) === c.digest && kj.lines === c.lines;
+            results.push({ name: `readFile on devices [0,0] ${c.input} '${c.prefix}'`, ok });
+        } catch (e) {
+            results.push({ name: `readFile on devices [0,0] ${c.input}`, ok: false, err: String(e) });
+        }
+    }
     // close() while a count is in flight: closed when it completes (no use after free)
     {
         const nat = lib.native();

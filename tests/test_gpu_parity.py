@@ -417,3 +417,39 @@ def test_gzip_input_and_result_writers(native, tmp_path, inputs, golden):
                 json.dumps(obj, separators=(",", ":"), ensure_ascii=False)
             legacy = "{\n" + "".join("%s: %d," % (k.decode("latin-1"), v) for k, v in a.entries()) + "}\n"
             assert (tmp_path / "b.txt").read_bytes().decode("latin-1") == legacy   # (keys may hold '\r')
+
+
+@pytest.mark.parametrize("devs", [[0, 0], [0, 0, 0]])
+def test_device_group_through_the_c_abi(native, golden, inputs, devs, tmp_path):
+    # kmer_params.ndev: line-aligned shards counted on a device group (an
+    # ordinal repeated on a one-GPU box), partials merged on devices[0] --
+    # the same ordered Map as one device (goldens: ordered digest + lines)
+    sel = lambda c: c["step"] == 1 and c["k"] in (5, 16, 31) and c["prefix"] in ("ATGAC", "", "A", "N")
+    by_cfg = collections.defaultdict(list)
+    for c in golden["cases"]:
+        if sel(c):
+            by_cfg[(c["prefix"], c["k"])].append(c)
+    bad = []
+    for (p, k), cases in by_cfg.items():
+        ctr = native.Counter(k=k, prefix=p.encode(), devices=devs)
+        try:
+            for c in cases:
+                r = ctr.count_buffer(inputs[c["input"]])
+                if digest(r.entries()) != c["digest"] or r.lines != c["lines"]:
+                    bad.append((c["input"], p, k, len(r), c["size"], r.lines, c["lines"]))
+        finally:
+            ctr.close()
+    assert not bad, bad[:5]
+    # a larger synthetic input (many tiles per shard) and a gzip file
+    from oracle import oracle
+    import gzip
+    data = oracle.synth_fastq(7, 0, 150_000)
+    want = oracle.count_buffer(data, b"ATGAC", 16, 1)
+    ctr = native.Counter(k=16, prefix=b"ATGAC", devices=devs)
+    assert first_diff(ctr.count_buffer(data).entries(), want) is None
+    f = tmp_path / "s.fastq.gz"
+    f.write_bytes(gzip.compress(data))
+    assert ctr.count_file(str(f)).entries() == want
+    with pytest.raises(native.KmerError):          # device-resident calls are single-device only
+        ctr.reset()
+    ctr.close()
