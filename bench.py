@@ -220,6 +220,9 @@ def main():
                     help="BASELINE.json config: c2 (default, the headline); c3 100 M reads, k=31, no prefix "
                          "(table mode); c4 125 M reads per GPU (1 B on 8), k=16; c5 long contigs k=21")
     ap.add_argument("--contig-bytes", type=int, default=1_000_000_000, help="c5: bytes of contigs per GPU")
+    ap.add_argument("--collect", action="store_true",
+                    help="N > 1: the timed step also gathers every rank's ordered key range to rank 0 and merges "
+                         "them on the device into ONE result in Map order (kmer_merge_ordered)")
     ap.add_argument("--merge", default="hits", choices=("hits", "alltoall", "gather"),
                     help="N > 1: hits: key-range all-to-all of the hits + per-rank finish (result distributed by "
                          "key range); alltoall: the same with per-rank partials; gather: all partials to rank 0")
@@ -256,7 +259,7 @@ def main():
     import torch
     import torch.distributed as dist
     from kmerjs_amd import Counter
-    from kmerjs_amd.multi import device_u64, finish_distributed, finish_exchange, merge_to
+    from kmerjs_amd.multi import collect_ordered_device, device_u64, finish_distributed, finish_exchange, merge_to
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -307,7 +310,7 @@ def main():
             scan_ms, feed_ms, _ = c.last_timing(finish=False)
             tile_ms.append(scan_ms)
             feed_ms_l.append(feed_ms)
-        multi_finish(c, rec)
+        multi_finish(c, rec, collect=args.collect)
 
     def step(i, record):
         feed(ctrs[i % nctx])      # (its previous finish is ahead of it on its stream)
@@ -319,7 +322,7 @@ def main():
         while inflight:
             retire()
 
-    def multi_finish(c, record=False):
+    def multi_finish(c, record=False, collect=False):
         if world == 1:
             c.finish(want_result=False)
             if table and record:
@@ -330,6 +333,8 @@ def main():
             finish_distributed(c, args.k, len(prefix), total_lines)
         else:
             merge_to(c, args.k, len(prefix), total_lines, dst=0, want_result=False)
+        if collect and world > 1 and args.merge != "gather":
+            collect_ordered_device(c, args.k, total_lines, dst=0)
 
     for i in range(args.warmup):
         step(i, False)
@@ -375,12 +380,12 @@ def main():
     if world > 1:
         dist.all_reduce(tot)
     distinct, accepted = int(tot[0].item()), int(tot[1].item())
-    if os.environ.get("KMERHIP_BENCH_VERIFY") == "1" and args.config in ("c2", "c3") and world > 1:
+    if os.environ.get("KMERHIP_BENCH_VERIFY") == "1" and args.config in ("c2", "c4") and world > 1:
         # rehearsal check (never set by the driver): the distributed result, merged
         # by first occurrence, equals the oracle on the whole job's input
         from kmerjs_amd.multi import collect_ordered
         assert args.merge != "gather"
-        got = collect_ordered(ctr, args.k)
+        got = collect_ordered(ctr, args.k, total_lines)
         if rank == 0:
             from oracle import oracle
             want = oracle.count_buffer(oracle.synth_fastq(args.seed, 0, world * args.reads), prefix, args.k, 1)
@@ -452,10 +457,12 @@ def main():
                        "bytes_per_gpu": nbytes,
                        "pipeline": ("%d sessions in rotation: finishes overlap later scans" % nctx if nctx > 1
                                     else "off (steps in sequence)"),
-                       "parallelism": "dp%d (reads sharded; %s)" % (
+                       "parallelism": "dp%d (reads sharded; %s%s)" % (
                            world, {"hits": "RCCL all-to-all of hits by key range, per-rank finish",
                         "alltoall": "RCCL all-to-all of partials by key range, per-rank finish"}.get(
-                            args.merge, "RCCL gather of partials, finish on rank 0"))},
+                            args.merge, "RCCL gather of partials, finish on rank 0"),
+                           "; + alltoallv gather of the ordered ranges to rank 0 and device merge into one "
+                           "Map-order result" if args.collect and world > 1 else "")},
             "distinct_kmers_per_s": distinct * args.steps / elapsed,
             "distinct_kmers": distinct,
             "accepted_windows": accepted,

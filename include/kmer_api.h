@@ -103,8 +103,9 @@ kmer_status kmer_count_buffer(kmer_ctx *ctx, const uint8_t *bytes, size_t len, k
 
 /* Device-resident streaming: bytes already in HBM.  Each fed chunk must start
  * at a line start (offset 0 of the input, or just after a '\n'); all chunks
- * but the last must end with '\n'.  `stream` is a hipStream_t (NULL = the
- * context's own stream).  kmer_finish_device leaves the ordered result in
+ * but the last must end with '\n'.  `stream` is the hipStream_t that produced
+ * the bytes (NULL = the legacy default stream): the count waits for the work
+ * queued on it so far.  kmer_finish_device leaves the ordered result in
  * device memory (kmer_result_device) and also returns it as a host result
  * when `out` is non-NULL. */
 kmer_status kmer_reset(kmer_ctx *ctx);
@@ -143,13 +144,22 @@ kmer_status kmer_finish_merged(kmer_ctx *ctx, const void *d_keys, const void *d_
  * the runs (all-to-all over xGMI) and hand each rank's received records,
  * concatenated in source-rank order, to kmer_finish_exchanged, which counts
  * them (this rank's key range of the result, in first-occurrence order,
- * device-resident: kmer_result_device).  `wait_stream` (hipStream_t or NULL):
- * the context's stream waits for the work queued so far on that stream (the
- * collective that wrote d_recv) before reading it.  Shards must be fed in
+ * device-resident: kmer_result_device).  `wait_stream` (hipStream_t; NULL =
+ * the legacy default stream): the context's stream waits for the work queued
+ * so far on that stream (the collective that wrote d_recv) before reading it.  Shards must be fed in
  * line order (kmer_set_position) so that order keys are global. */
 kmer_status kmer_exchange_prepare(kmer_ctx *ctx, uint32_t world, const void **d_send, uint64_t *counts);
 kmer_status kmer_finish_exchanged(kmer_ctx *ctx, const void *d_recv, uint64_t n, uint64_t total_lines,
                                   void *wait_stream, kmer_result **out);
+/* One result in Map order from every rank's ordered key range (the device
+ * result of kmer_finish_exchanged on each rank), gathered to this context's
+ * device and concatenated (any order): n rows of keys (n * k bytes), counts
+ * (uint64) and first-occurrence keys (uint64).  Re-orders them by first
+ * occurrence into this context's device result (kmer_result_device) and,
+ * when `out` is non-NULL, returns the host result with this context's record
+ * keys merged in (import the other ranks' records first). */
+kmer_status kmer_merge_ordered(kmer_ctx *ctx, const void *d_keys, const void *d_counts, const void *d_firsts,
+                               uint64_t n, uint64_t total_lines, kmer_result **out);
 kmer_status kmer_records_export(kmer_ctx *ctx, kmer_result **out);
 kmer_status kmer_records_import(kmer_ctx *ctx, const char *keys, const uint64_t *offsets,
                                 const uint64_t *counts, const uint64_t *firsts, uint64_t n);

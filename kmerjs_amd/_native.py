@@ -24,7 +24,7 @@ WRITE_LEGACY = 1    # "{\nkey: count,...}\n", lib/index.js:381-388
 # every symbol the header declares (tests/test_abi.py checks header <-> library)
 EXPORTS = ["kmer_open", "kmer_close", "kmer_count_file", "kmer_count_buffer", "kmer_reset", "kmer_sync",
            "kmer_feed_device", "kmer_finish_device", "kmer_partial_device", "kmer_finish_merged",
-           "kmer_exchange_prepare", "kmer_finish_exchanged",
+           "kmer_exchange_prepare", "kmer_finish_exchanged", "kmer_merge_ordered",
            "kmer_records_export", "kmer_records_import", "kmer_records_clear", "kmer_result_device", "kmer_set_position",
            "kmer_lines", "kmer_result_size", "kmer_result_lines", "kmer_result_get",
            "kmer_result_arrays", "kmer_result_firsts", "kmer_result_write", "kmer_result_free",
@@ -74,6 +74,7 @@ def _load():
         "kmer_finish_merged": (ctypes.c_int, [vp, vp, vp, u64, u64, ctypes.POINTER(vp)]),
         "kmer_exchange_prepare": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.POINTER(vp), pu64]),
         "kmer_finish_exchanged": (ctypes.c_int, [vp, vp, u64, u64, vp, ctypes.POINTER(vp)]),
+        "kmer_merge_ordered": (ctypes.c_int, [vp, vp, vp, vp, u64, u64, ctypes.POINTER(vp)]),
         "kmer_records_export": (ctypes.c_int, [vp, ctypes.POINTER(vp)]),
         "kmer_records_clear": (ctypes.c_int, [vp]),
         "kmer_records_import": (ctypes.c_int, [vp, ctypes.c_char_p, pu64, pu64, pu64, u64]),
@@ -264,6 +265,15 @@ class Counter:
         r = ctypes.c_void_p()
         self._check(LIB.kmer_finish_exchanged(self.h, ctypes.c_void_p(d_recv), n, total_lines, ctypes.c_void_p(stream),
                                               ctypes.byref(r) if want_result else None), "finish_exchanged")
+        return Result(r) if want_result else None
+
+    def merge_ordered(self, d_keys, d_counts, d_firsts, n, total_lines, want_result=False):
+        """One Map-order result from gathered per-rank ordered lists (device
+        pointers: n * k key bytes, uint64 counts, uint64 first-occurrence keys)."""
+        r = ctypes.c_void_p()
+        self._check(LIB.kmer_merge_ordered(self.h, ctypes.c_void_p(d_keys), ctypes.c_void_p(d_counts),
+                                           ctypes.c_void_p(d_firsts), n, total_lines,
+                                           ctypes.byref(r) if want_result else None), "merge_ordered")
         return Result(r) if want_result else None
 
     def records_export(self):

@@ -1893,13 +1893,12 @@ kmer_status kmer_feed_device(kmer_ctx *c, const void *d_bytes, size_t len, void 
     if (!c->open_stream) return fail(c, KMER_E_STATE, "feed without reset");
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
     hipStream_t s = (hipStream_t)stream;
-    if (s && s != c->stream) {
-        // order the context's own stream after the caller's work
-        hipEvent_t ev;
-        HIPCHK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        HIPCHK(c, hipEventRecord(ev, s));
-        HIPCHK(c, hipStreamWaitEvent(c->stream, ev, 0));
-        HIPCHK(c, hipEventDestroy(ev));
+    if (s != c->stream) {
+        // order the context's own (non-blocking) stream after the caller's
+        // work; NULL is the legacy default stream, which a non-blocking stream
+        // does not otherwise wait for
+        HIPCHK(c, hipEventRecord(c->evw, s));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->evw, 0));
     }
     return feed(c, (const uint8_t *)d_bytes, len, c->stream);
 }
@@ -2087,6 +2086,52 @@ kmer_status kmer_finish_merged(kmer_ctx *c, const void *d_keys, const void *d_va
     return build_result(c, total_lines, out);
 }
 
+// One ordered result from the ranks' ordered key ranges (after
+// kmer_finish_exchanged), gathered to one device: a stable radix sort of the
+// first-occurrence keys (each list is sorted; their union is re-ordered),
+// then keys / counts / firsts permuted into the context's result arrays.
+kmer_status kmer_merge_ordered(kmer_ctx *c, const void *d_keys, const void *d_counts, const void *d_firsts,
+                               uint64_t n, uint64_t total_lines, kmer_result **out) {
+    if (!c || (n && (!d_keys || !d_counts || !d_firsts))) return KMER_E_BAD_PARAM;
+    SETTLE(c);
+    if (c->mode != MODE_PACKED && c->mode != MODE_WINDOWS)
+        return fail(c, KMER_E_STATE, "configuration has no packed keys");
+    if (n >= (1ull << 32)) return fail(c, KMER_E_TOO_MANY_KEYS, "more than 2^32 entries to merge");
+    if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
+    if (out) *out = nullptr;
+    hipStream_t s = c->stream;
+    HIPCHK(c, hipEventRecord(c->ev2, s));
+    const uint64_t k = c->p.k;
+    if (n) {
+        HIPCHK(c, c->xord.ensure(n, s));
+        HIPCHK(c, c->xord2.ensure(n, s));
+        HIPCHK(c, c->ridx.ensure(n, s));
+        HIPCHK(c, c->ridx2.ensure(n, s));
+        HIPCHK(c, c->keys_out.ensure(n * k, s));
+        HIPCHK(c, c->cnt_out.ensure(n, s));
+        HIPCHK(c, c->first.ensure(n, s));
+        HIPCHK(c, hipMemcpyAsync(c->xord.p, d_firsts, n * 8, hipMemcpyDeviceToDevice, s));
+        rocprim::counting_iterator<uint32_t> iota(0u);
+        ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, c->xord.p, c->xord2.p, iota, c->ridx2.p, (size_t)n, 0, 64, s));
+        HIPCHK(c, launch_permute_rows((const uint8_t *)d_keys, (const uint64_t *)d_counts, (const uint64_t *)d_firsts,
+                                      c->ridx2.p, n, (uint32_t)k, c->keys_out.p, c->cnt_out.p, c->first.p, s));
+    }
+    c->n_out = n;
+    c->out_pending = false;
+    HIPCHK(c, hipEventRecord(c->ev3, s));
+    c->timing_pending = true;
+    c->open_stream = false;
+    const bool sync = out || c->p.max_keys;
+    if (!sync) return KMER_OK;
+    kmer_status st = resolve_out(c);
+    if (st) return st;
+    const uint64_t total = c->n_out + c->exotic.size();
+    if (c->p.max_keys && total > c->p.max_keys)
+        return fail(c, KMER_E_TOO_MANY_KEYS, "more distinct keys than max_keys (reference Map limit)");
+    if (!out) return KMER_OK;
+    return build_result(c, total_lines, out);
+}
+
 kmer_status kmer_exchange_prepare(kmer_ctx *c, uint32_t world, const void **d_send, uint64_t *counts) {
     if (!c || !d_send || !counts || world == 0 || world > XP_MAXW) return KMER_E_BAD_PARAM;
     SETTLE(c);
@@ -2134,11 +2179,11 @@ kmer_status kmer_finish_exchanged(kmer_ctx *c, const void *d_recv, uint64_t n, u
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
     if (out) *out = nullptr;
     hipStream_t s = c->stream;
-    if (wait_stream) {
-        // the received buffer was written on the caller's stream (the collective)
-        HIPCHK(c, hipEventRecord(c->evw, (hipStream_t)wait_stream));
-        HIPCHK(c, hipStreamWaitEvent(s, c->evw, 0));
-    }
+    // the received buffer was written on the caller's stream (the collective);
+    // NULL is the legacy default stream, which the context's non-blocking
+    // stream does not otherwise wait for
+    HIPCHK(c, hipEventRecord(c->evw, (hipStream_t)wait_stream));
+    HIPCHK(c, hipStreamWaitEvent(s, c->evw, 0));
     HIPCHK(c, hipEventRecord(c->ev2, s));
     // the received hits, concatenated by source rank, are in rank order
     kmer_status st = ensure_rank_arrays(c, n, 0, s);

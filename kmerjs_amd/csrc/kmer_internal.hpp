@@ -417,5 +417,8 @@ hipError_t launch_tab_starts(const uint64_t *H2s, const TabUnit *pfirst, uint64_
 hipError_t launch_tab_final(const TabFinal &a, uint32_t grid, hipStream_t s);
 hipError_t launch_synth_fastq(uint8_t *out, uint64_t seed, uint64_t first_read, uint64_t n_reads,
                               hipStream_t s);
+hipError_t launch_permute_rows(const uint8_t *keys, const uint64_t *cnt, const uint64_t *first, const uint32_t *idx,
+                               uint64_t n, uint32_t k, uint8_t *okeys, uint64_t *ocnt, uint64_t *ofirst,
+                               hipStream_t s);
 
 }  // namespace kmerhip

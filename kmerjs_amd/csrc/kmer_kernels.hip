@@ -2151,6 +2151,38 @@ __global__ __launch_bounds__(256) void gather_records_kernel(const Record *recs,
     }
 }
 
+// Ordered merge of per-rank result lists: row i of the output is source row
+// idx[i] (k-byte key, count, first-occurrence key).  One thread per row; keys
+// copied 4 bytes at a time when k allows.
+__global__ __launch_bounds__(256) void permute_rows_kernel(const uint8_t *keys, const uint64_t *cnt,
+                                                           const uint64_t *first, const uint32_t *idx, uint64_t n,
+                                                           uint32_t k, uint8_t *okeys, uint64_t *ocnt,
+                                                           uint64_t *ofirst) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t j = idx[i];
+        ocnt[i] = cnt[j];
+        ofirst[i] = first[j];
+        const uint8_t *src = keys + j * k;
+        uint8_t *dst = okeys + i * k;
+        if ((k & 3) == 0) {
+            for (uint32_t b = 0; b < k; b += 4) *(uint32_t *)(dst + b) = *(const uint32_t *)(src + b);
+        } else {
+            for (uint32_t b = 0; b < k; ++b) dst[b] = src[b];
+        }
+    }
+}
+
+hipError_t launch_permute_rows(const uint8_t *keys, const uint64_t *cnt, const uint64_t *first, const uint32_t *idx,
+                               uint64_t n, uint32_t k, uint8_t *okeys, uint64_t *ocnt, uint64_t *ofirst,
+                               hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    uint64_t blocks = (n + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(permute_rows_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, keys, cnt, first, idx, n, k,
+                       okeys, ocnt, ofirst);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // synthetic FASTQ: record i = "@r%010d\n" + 150 bases + "\n+\n"
 // + 150 x 'I' + "\n" (317 B), base b = "ACGT"[(mix(seed*G + i*8 + b/32) >> 2(b%32)) & 3]

@@ -15,8 +15,9 @@ first-occurrence order).  Two ways to finish:
   The received runs, concatenated by source rank, are in first-occurrence
   order (shards are in line order), so each rank ends with its key range of
   the result, ordered by first occurrence.  The global Map order is the merge
-  of the ranks' lists by first occurrence (collect_ordered).  Work per rank
-  stays constant as ranks are added.
+  of the ranks' lists by first occurrence: collect_ordered_device gathers the
+  lists to one rank (alltoallv over RCCL) and re-orders them on the device
+  (kmer_merge_ordered).  Work per rank stays constant as ranks are added.
 * finish_distributed: the same key-range all-to-all, but of per-rank partials
   (unique keys + {first, count}, kmer_partial_device) merged with
   kmer_finish_merged -- fewer bytes on the wire when keys repeat a lot within
@@ -247,34 +248,67 @@ def finish_distributed(ctr, k, plen, total_lines, group=None, want_result=False,
     return ctr.finish_merged(rk.data_ptr(), rv.data_ptr(), rk.numel(), total_lines, want_result=want_result)
 
 
-def collect_ordered(ctr, k, dst=0, group=None):
-    """Gather every rank's ordered key range (after finish_distributed) to `dst`
-    and merge the lists by first occurrence: the whole Map, in reference order.
-    Returns [(key bytes, count)] on dst (device entries + dst's records), None elsewhere."""
-    import numpy as np
+def gather_rows(tensors, n, dst=0, group=None):
+    """Gather variable-length row blocks to `dst` with one all-to-all per
+    tensor (alltoallv: only dst receives, no padding).  tensors: list of
+    (tensor, elements per row); returns (received tensors concatenated by
+    source rank, total rows) on dst, (None, 0) elsewhere."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    host_coll = dist.get_backend(group) == "gloo"
+    dev = tensors[0][0].device
+    cnt_dev = "cpu" if host_coll else dev
+    send = torch.zeros(world, dtype=torch.int64, device=cnt_dev)
+    send[dst] = n
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)
+    recv_l = recv.cpu().tolist() if rank == dst else [0] * world
+    total = sum(recv_l)
+    out = []
+    for t, per in tensors:
+        src = t.cpu() if host_coll else t
+        split_out = [per * x for x in recv_l]
+        split_in = [per * n if r == dst else 0 for r in range(world)]
+        o = torch.empty(per * total, dtype=t.dtype, device=src.device)
+        dist.all_to_all_single(o, src, split_out, split_in, group=group)
+        out.append(o.to(dev) if host_coll else o)
+    return (out, total) if rank == dst else (None, 0)
+
+
+def collect_ordered_device(ctr, k, total_lines, dst=0, group=None, want_result=False):
+    """One result in Map order on rank `dst` after finish_exchange /
+    finish_distributed (each rank holds its key range, ordered by first
+    occurrence): every rank's (keys, counts, firsts) go to dst in one
+    alltoallv each (RCCL over xGMI), and dst re-orders the union by first
+    occurrence on the device (kmer_merge_ordered).  The record keys were
+    already merged on dst.  Returns dst's Result when want_result (host
+    entries, records merged in), else None; the ordered device result is
+    dst's kmer_result_device."""
     d_keys, d_cnt, d_first, n = ctr.result_device()
     dev = torch.device("cuda", torch.cuda.current_device())
     if n:
-        kb = torch.as_tensor(_CudaArray(d_keys, n * k, "|u1"), device=dev).cpu().numpy().tobytes()
-        cnt = device_u64(d_cnt, n, dev).cpu().numpy().astype(np.uint64)
-        fst = device_u64(d_first, n, dev).cpu().numpy().astype(np.uint64)
+        keys = torch.as_tensor(_CudaArray(d_keys, n * k, "|u1"), device=dev)
+        cnt = device_u64(d_cnt, n, dev)
+        fst = device_u64(d_first, n, dev)
     else:
-        kb, cnt, fst = b"", np.zeros(0, np.uint64), np.zeros(0, np.uint64)
-    got = [None] * dist.get_world_size(group) if dist.get_rank(group) == dst else None
-    dist.gather_object((kb, cnt.tolist(), fst.tolist()), got, dst=dst, group=group)
-    if dist.get_rank(group) != dst:
+        keys = torch.empty(0, dtype=torch.uint8, device=dev)
+        cnt = torch.empty(0, dtype=torch.int64, device=dev)
+        fst = torch.empty(0, dtype=torch.int64, device=dev)
+    got, total = gather_rows([(keys, k), (cnt, 1), (fst, 1)], n, dst=dst, group=group)
+    if got is None:
         return None
-    keys, counts, firsts = [], [], []
-    for kb_r, cnt_r, fst_r in got:
-        keys += [kb_r[i * k:(i + 1) * k] for i in range(len(cnt_r))]
-        counts += cnt_r
-        firsts += fst_r
-    rk, ro, rc, rf = ctr.records_export()
-    keys += [rk[int(ro[i]):int(ro[i + 1])] for i in range(len(rc))]
-    counts += [int(x) for x in rc]
-    firsts += [int(x) for x in rf]
-    order = sorted(range(len(keys)), key=lambda i: firsts[i])
-    return [(keys[i], counts[i]) for i in order]
+    torch.cuda.synchronize()                  # (the merge runs on the context's stream)
+    rk, rc, rf = got
+    ctr._keepalive = (rk, rc, rf)
+    return ctr.merge_ordered(rk.data_ptr(), rc.data_ptr(), rf.data_ptr(), total, total_lines,
+                             want_result=want_result)
+
+
+def collect_ordered(ctr, k, total_lines, dst=0, group=None):
+    """The whole Map in reference order on `dst` (device gather + device merge,
+    collect_ordered_device): [(key bytes, count)] on dst, None elsewhere."""
+    r = collect_ordered_device(ctr, k, total_lines, dst=dst, group=group, want_result=True)
+    return r.entries() if r is not None else None
 
 
 def merge_to(ctr, k, plen, total_lines, dst=0, group=None, want_result=True, records=True):

@@ -212,3 +212,52 @@ def test_hit_exchange_collectives_gloo(world):
         want = [[(src << 40) + 100 * rank + i, 1000 * rank + i] for src in range(world)
                 for i in range(by_rank[src][2][rank])]
         assert recv == want
+
+
+def _gather_rows_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # an ordered key range per rank, as collect_ordered_device sends it:
+        # n rows of k key bytes, counts, first-occurrence keys
+        k, n = 4, [3, 0, 2][rank]
+        keys = torch.tensor([[65 + rank, 67, 71, 84 + i % 2] for i in range(n)], dtype=torch.uint8).view(-1) \
+            if n else torch.empty(0, dtype=torch.uint8)
+        cnt = torch.arange(n, dtype=torch.int64) + 10 * rank
+        fst = torch.arange(n, dtype=torch.int64) * world + rank
+        got, total = multi.gather_rows([(keys, k), (cnt, 1), (fst, 1)], n, dst=0)
+        if rank == 0:
+            q.put(("ok", total, got[0].view(-1, k).tolist(), got[1].tolist(), got[2].tolist()))
+        else:
+            q.put(("ok", total, got, None, None))
+    except Exception as e:  # pragma: no cover
+        q.put(("err", repr(e), None, None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_rows_alltoallv_gloo(world):
+    # the collective of the device-side ordered collect (multi.collect_ordered_device):
+    # variable-length row blocks to rank 0 in one alltoallv per tensor, no padding
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_rows_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[0] == "ok" for r in res), res
+    root = [r for r in res if r[1] != 0 or r[2] is not None]
+    ns = [[3, 0, 2][r] for r in range(world)]
+    main = [r for r in res if r[3] is not None][0]
+    _, total, keys, cnt, fst = main
+    assert total == sum(ns)
+    assert keys == [[65 + r, 67, 71, 84 + i % 2] for r in range(world) for i in range(ns[r])]
+    assert cnt == [i + 10 * r for r in range(world) for i in range(ns[r])]
+    assert fst == [i * world + r for r in range(world) for i in range(ns[r])]
+    assert root

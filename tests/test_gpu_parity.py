@@ -219,13 +219,15 @@ def _shard_and_merge(native, data, k, prefix, world, batch_bytes=0):
             c.close()
 
 
-def _shard_and_exchange(native, data, k, prefix, world):
+def _shard_and_exchange(native, data, k, prefix, world, device_merge=False):
     """Count `data` as `world` record-aligned shards (one context per rank) and
     finish with the hit exchange (multi.finish_exchange, done in-process): each
     owner counts the runs every rank sent it.  Returns the whole ordered Map
-    (the owners' lists merged by first occurrence) and the line count."""
+    (the owners' lists merged by first occurrence: on the host, or with
+    device_merge by kmer_merge_ordered on rank 0 as multi.collect_ordered_device
+    does after its gather) and the line count."""
     import torch
-    from kmerjs_amd.multi import device_u64, key_owner, split_at_records
+    from kmerjs_amd.multi import _CudaArray, device_u64, key_owner, split_at_records
     shards = split_at_records(data, world)
     ctrs = [native.Counter(k=k, prefix=prefix) for _ in range(world)]
     dev = torch.device("cuda")
@@ -258,8 +260,30 @@ def _shard_and_exchange(native, data, k, prefix, world):
                 assert bool((key_owner(keys, kbits, world) == o).all())     # only this owner's key range
                 fo = recv.view(-1, 2)[:, 0]
                 assert bool((fo[1:] > fo[:-1]).all())                     # in first-occurrence order
+            if device_merge:
+                ctrs[o].finish_exchanged(recv.data_ptr(), recv.numel() // 2, total_lines)
+                dk, dc, df, n = ctrs[o].result_device()
+                if n:
+                    kb = torch.as_tensor(_CudaArray(dk, n * k, "|u1"), device=dev).clone()
+                    merged.append((kb, device_u64(dc, n, dev).clone(), device_u64(df, n, dev).clone()))
+                continue
             r = ctrs[o].finish_exchanged(recv.data_ptr(), recv.numel() // 2, total_lines, want_result=True)
             merged += [(int(f), kk, c) for f, (kk, c) in zip(r.firsts.tolist(), r.entries())]
+        if device_merge:
+            # the owners' lists gathered to rank 0 (any order) and re-ordered there
+            if merged:
+                gk = torch.cat([m[0] for m in reversed(merged)])
+                gc = torch.cat([m[1] for m in reversed(merged)])
+                gf = torch.cat([m[2] for m in reversed(merged)])
+            else:
+                gk = torch.empty(0, dtype=torch.uint8, device=dev)
+                gc = gf = torch.empty(0, dtype=torch.int64, device=dev)
+            torch.cuda.synchronize()
+            r = ctrs[0].merge_ordered(gk.data_ptr(), gc.data_ptr(), gf.data_ptr(), gc.numel(), total_lines,
+                                      want_result=True)
+            fs = r.firsts.tolist()
+            assert all(a < b for a, b in zip(fs, fs[1:]))
+            return r.entries(), r.lines
         merged.sort(key=lambda t: t[0])
         return [(kk, c) for _, kk, c in merged], total_lines
     finally:
@@ -283,6 +307,10 @@ def test_hit_exchange_matches_oracle(native, world):
         got, lines = _shard_and_exchange(native, part, k, p, world)
         assert lines == 4 * n
         assert first_diff(got, want) is None, (world, k, p)
+        # the device-side collect (multi.collect_ordered_device's merge)
+        got, lines = _shard_and_exchange(native, part, k, p, world, device_merge=True)
+        assert lines == 4 * n
+        assert first_diff(got, want) is None, ("device merge", world, k, p)
 
 
 @pytest.mark.parametrize("world", [2, 3, 5])
@@ -453,3 +481,75 @@ def test_device_group_through_the_c_abi(native, golden, inputs, devs, tmp_path):
     with pytest.raises(native.KmerError):          # device-resident calls are single-device only
         ctr.reset()
     ctr.close()
+
+
+def test_c4_shard_full_size_properties(native):
+    # BASELINE configs[3] per-GPU shard: 125 M reads (39.6 GB, seed 4) -- the
+    # 1 B-read job's share of one of 8 GPUs -- properties that need no oracle,
+    # checked on the device; then the shard as 2 ranks' worth, hit exchange +
+    # device-side ordered collect (kmer_merge_ordered) == the one-pass result
+    import torch
+    from kmerjs_amd import synth_fastq_device
+    from kmerjs_amd.multi import _CudaArray, device_u64
+    n, k, prefix = 125_000_000, 16, b"ATGAC"
+    dev = torch.device("cuda")
+    buf = torch.empty(n * 317, dtype=torch.uint8, device=dev)
+    synth_fastq_device(buf.data_ptr(), 4, 0, n)
+    torch.cuda.synchronize()
+    ctr = native.Counter(k=k, prefix=prefix)
+    ctr.reset()
+    ctr.set_position(0, 0)
+    ctr.feed_device(buf.data_ptr(), buf.numel())
+    ctr.finish(want_result=False)
+    assert ctr.lines() == 4 * n
+    dk, dc, df, m = ctr.result_device()
+    keys = torch.as_tensor(_CudaArray(dk, m * k, "|u1"), device=dev).view(m, k).clone()
+    cnt = device_u64(dc, m, dev).clone()
+    fst = device_u64(df, m, dev).clone()
+    # accepted windows counted independently, 10 M reads at a time
+    accepted = 0
+    for lo in range(0, n, 10_000_000):
+        seq = buf.view(n, 317)[lo:lo + 10_000_000, 13:163]
+        fwd = torch.ones((seq.shape[0], 146), dtype=torch.bool, device=dev)
+        rev = torch.ones_like(fwd)
+        for i in range(5):
+            fwd &= seq[:, i:146 + i] == prefix[i]
+            rev &= seq[:, i:146 + i] == b"GTCAT"[i]
+        accepted += int(fwd[:, :150 - k + 1].sum()) + int(rev[:, k - 5:].sum())
+        del fwd, rev, seq
+    assert int(cnt.sum()) == accepted
+    assert m <= 4 ** 11 and bool((keys[:, :5] == torch.tensor(list(prefix), dtype=torch.uint8, device=dev)).all())
+    assert bool((fst[1:] > fst[:-1]).all())
+    # 2 ranks' worth on the same device: exchange by key range, per-owner finish,
+    # then the owners' ordered lists merged by first occurrence on "rank 0"
+    half = n // 2
+    ctrs = [native.Counter(k=k, prefix=prefix) for _ in range(2)]
+    runs = []
+    for r, c in enumerate(ctrs):
+        c.reset()
+        c.set_position(4 * half * r, 317 * half * r)
+        c.feed_device(buf.data_ptr() + 317 * half * r, 317 * half)
+        d_x, counts = c.exchange_prepare(2)
+        x = device_u64(d_x, 2 * sum(counts), dev).clone()
+        runs.append((x[:2 * counts[0]], x[2 * counts[0]:]))
+    del buf
+    parts = []
+    for o, c in enumerate(ctrs):
+        recv = torch.cat([runs[0][o], runs[1][o]])
+        c.finish_exchanged(recv.data_ptr(), recv.numel() // 2, 4 * n,
+                           stream=torch.cuda.current_stream().cuda_stream)   # (after the cat)
+        ok, oc, of, om = c.result_device()
+        parts.append((torch.as_tensor(_CudaArray(ok, om * k, "|u1"), device=dev).clone(),
+                      device_u64(oc, om, dev).clone(), device_u64(of, om, dev).clone()))
+    del runs
+    gk = torch.cat([p[0] for p in parts])
+    gc = torch.cat([p[1] for p in parts])
+    gf = torch.cat([p[2] for p in parts])
+    torch.cuda.synchronize()
+    ctrs[0].merge_ordered(gk.data_ptr(), gc.data_ptr(), gf.data_ptr(), gc.numel(), 4 * n)
+    mk, mc, mf, mm = ctrs[0].result_device()
+    assert mm == m
+    assert torch.equal(device_u64(mc, mm, dev), cnt) and torch.equal(device_u64(mf, mm, dev), fst)
+    assert torch.equal(torch.as_tensor(_CudaArray(mk, mm * k, "|u1"), device=dev).view(mm, k), keys)
+    for c in ctrs + [ctr]:
+        c.close()
