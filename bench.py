@@ -220,6 +220,7 @@ def main():
                     help="BASELINE.json config: c2 (default, the headline); c3 100 M reads, k=31, no prefix "
                          "(table mode); c4 125 M reads per GPU (1 B on 8), k=16; c5 long contigs k=21")
     ap.add_argument("--contig-bytes", type=int, default=1_000_000_000, help="c5: bytes of contigs per GPU")
+    ap.add_argument("--ordered", action="store_true", help="c5: the reference's ordered Map instead of canonical")
     ap.add_argument("--collect", action="store_true",
                     help="N > 1: the timed step also gathers every rank's ordered key range to rank 0 and merges "
                          "them on the device into ONE result in Map order (kmer_merge_ordered)")
@@ -248,13 +249,23 @@ def main():
             args.reads = 125_000_000
         if "--seed" not in argv:
             args.seed = 4
-    table = bool(args.flags & FLAG_UNORDERED)
-    if table and args.gpus > 1:
-        raise SystemExit("table mode is single-GPU in this build (see DESIGN.md)")
-    if args.config == "c5" and "--k" not in argv:
-        args.k = 21
+    if args.config == "c5":
+        # long contigs, k = 21, canonical k-mers (BASELINE configs[4]): table
+        # mode with KMER_FLAG_CANONICAL, no prefix (an extension: the reference
+        # Map has no canonical form; parity of the underlying counts is tested)
+        from kmerjs_amd._native import FLAG_CANONICAL
+        if "--k" not in argv:
+            args.k = 21
+        if "--prefix" not in argv:
+            args.prefix = ""
+        if "--ordered" not in argv:
+            args.flags |= FLAG_CANONICAL
     if args.config != "c2":
         args.no_pcie = True
+    from kmerjs_amd._native import FLAG_CANONICAL as _FC
+    table = bool(args.flags & (FLAG_UNORDERED | _FC))
+    if table and args.gpus > 1:
+        raise SystemExit("table mode is single-GPU in this build (see DESIGN.md)")
 
     import torch
     import torch.distributed as dist
@@ -410,7 +421,9 @@ def main():
         if table:
             # the dominant phase of the table pipeline (HIP events on the library's stream)
             phases = {kname: sum(p[kname] for p in phase_ms) / len(phase_ms) for kname in phase_ms[0]}
-            n_keys = accepted // 2 if not args.prefix else None
+            # pass-1 keys = forward windows counted (no prefix): the Map sum is
+            # twice that, the canonical sum once
+            n_keys = (accepted if args.flags & _FC else accepted // 2) if not args.prefix else None
             mean = (n_keys or 0) >> 20
             sub_bits = 0
             while sub_bits < 16 and (mean >> sub_bits) > 6000:
@@ -451,7 +464,8 @@ def main():
                          args.config, "synthetic (on-device splitmix64 FASTQ, 317 B records, seed %d)" % args.seed),
             "config": {"workload": wl["desc"], "name": args.config,
                        "reads_per_gpu": args.reads if args.config in ("c2", "c3", "c4") else None,
-                       "mode": "table (unordered canonical counts, KMER_FLAG_UNORDERED)" if table
+                       "mode": ("table, canonical k-mers (KMER_FLAG_CANONICAL)" if args.flags & _FC else
+                                "table (unordered canonical counts, KMER_FLAG_UNORDERED)") if table
                                else "ordered (reference Map insertion order)",
                        "k": args.k, "prefix": args.prefix, "windows_per_step": windows_step,
                        "bytes_per_gpu": nbytes,

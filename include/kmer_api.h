@@ -61,6 +61,12 @@ enum {
      * sorted by key bytes); other configurations keep the ordered paths. */
     KMER_FLAG_UNORDERED = 1u << 4,
     KMER_FLAG_TABLE_SPLIT_TEST = 1u << 5, /* debug: table mode with 64-key LDS ranges (exercises range splits) */
+    /* Canonical k-mers (BASELINE C5; an extension, not the reference's Map):
+     * table mode whose result holds one key per {x, rc x} class -- the
+     * lexicographically smaller string -- counted once per forward window of
+     * the class (jellyfish -C).  Step 1, k <= 32, empty or A/C/G/T prefix
+     * (tested on the canonical key); KMER_E_BAD_PARAM otherwise. */
+    KMER_FLAG_CANONICAL = 1u << 6,
     /* experiments only (results are WRONG with these set): ablate parts of the tile scan */
     KMER_FLAG_ABLATE_HITS = 1u << 8,   /* drop every prefix candidate */
     KMER_FLAG_ABLATE_SWAR = 1u << 9    /* skip the SWAR prefix scan entirely */

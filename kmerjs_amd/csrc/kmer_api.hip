@@ -193,6 +193,9 @@ struct kmer_ctx {
     DBuf<uint64_t> tp1;            // pass-1 partition starts of the last chunk (TAB_NB)
     DBuf<TabUnit> tunits;          // pass-2 units, then TAB_NB partition heads
     DBuf<TabBig> tbig;             // entries with counts >= TAB_CMAX
+    DBuf<uint32_t> tpc;            // pieces per sequence line (long lines)
+    DBuf<uint64_t> tpb;            // ... their scan
+    DBuf<SeqLine> tpieces;         // long lines cut into pieces of <= TAB_PIECE windows
     DBuf<unsigned long long> tstats;   // [0..2] final statistics, [3] big-list count
     uint64_t t_keys = 0;           // pass-1 keys of the session
     std::vector<uint64_t> t_cbase; // per chunk: first key in tb1
@@ -894,18 +897,40 @@ kmer_status table_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_t
     kmer_status st = chunk_lines(c, d, len, n_tiles, s, false, &n_nl, &n_seq);
     if (st) return st;
     HIPCHK(c, launch_pos_after(c->d_pos, li0 + n_nl, d, len, c->d_ends_open, s));
-    HIPCHK(c, hipEventRecord(c->tev[1], s));
     c->host_lines = li0 + n_nl;
+    // long lines -> pieces of <= TAB_PIECE windows (balance pass 1's shares)
+    const SeqLine *plines = c->lines.p;
+    uint64_t n_items = n_seq;
     if (n_seq) {
+        HIPCHK(c, c->tpc.ensure(n_seq, s));
+        HIPCHK(c, c->tpb.ensure(n_seq, s));
+        HIPCHK(c, launch_tab_piece_count(c->wcount.p, n_seq, c->tpc.p, s));
+        ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tpc.p, c->tpb.p, (uint64_t)0, (size_t)n_seq,
+                                               rocprim::plus<uint64_t>(), s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 12, c->tpb.p + n_seq - 1, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 13, c->tpc.p + n_seq - 1, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        const uint64_t n_pieces = c->h_small[12] + (uint32_t)c->h_small[13];
+        if (n_pieces == 0) {
+            n_items = 0;                          // no line holds a window
+        } else if (n_pieces != n_seq) {           // long lines (or empty ones, dropped on the way)
+            HIPCHK(c, c->tpieces.ensure(std::max<uint64_t>(n_pieces, 1), s));
+            HIPCHK(c, launch_tab_piece_write(c->lines.p, c->wcount.p, c->tpb.p, n_seq, c->p.k, c->tpieces.p, s));
+            plines = c->tpieces.p;
+            n_items = n_pieces;
+        }
+    }
+    HIPCHK(c, hipEventRecord(c->tev[1], s));
+    if (n_items) {
         TabArgs a;
         memset(&a, 0, sizeof(a));
         a.data = d;
         a.len = len;
-        a.lines = c->lines.p;
-        a.n_lines = n_seq;
-        const uint64_t nwg0 = std::min<uint64_t>(8192, (n_seq + 63) / 64);
-        a.lpw = (n_seq + nwg0 - 1) / nwg0;
-        a.nwg = (uint32_t)((n_seq + a.lpw - 1) / a.lpw);
+        a.lines = plines;
+        a.n_lines = n_items;
+        const uint64_t nwg0 = std::min<uint64_t>(8192, (n_items + 63) / 64);
+        a.lpw = (n_items + nwg0 - 1) / nwg0;
+        a.nwg = (uint32_t)((n_items + a.lpw - 1) / a.lpw);
         a.k = c->p.k;
         for (size_t i = 0; i < c->prefix.size(); ++i) {
             const uint8_t ch = (uint8_t)c->prefix[i];
@@ -913,6 +938,7 @@ kmer_status table_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_t
             a.phi |= (((uint32_t)ch >> 2) & 1u) << i;
         }
         a.pmask = c->prefix.size() >= 32 ? ~0u : ((1u << c->prefix.size()) - 1u);
+        a.canonical = (c->p.flags & KMER_FLAG_CANONICAL) ? 1u : 0u;
         a.err = c->d_err;
         const uint64_t nh = (uint64_t)TAB_NB * a.nwg;
         HIPCHK(c, c->tH.ensure(nh, s));
@@ -1066,6 +1092,7 @@ kmer_status table_finish(kmer_ctx *c) {
     }
     f.pmask = c->prefix.size() >= 32 ? ~0u : ((1u << c->prefix.size()) - 1u);
     f.inv = inv_odd(TAB_MUL);
+    f.canonical = (c->p.flags & KMER_FLAG_CANONICAL) ? 1u : 0u;
     f.stats = c->tstats.p;
     HIPCHK(c, hipEventRecord(c->tev[2], s));
     HIPCHK(c, launch_tab_final(f, (uint32_t)std::max(c->n_cu, 1), s));
@@ -1086,6 +1113,17 @@ kmer_status table_finish(kmer_ctx *c) {
     c->t_nbig = c->h_small[11];
     c->n_out = c->t_nkeys;
     return KMER_OK;
+}
+
+// Canonical classes of the record keys (KMER_FLAG_CANONICAL: forward windows)
+std::unordered_map<std::string, uint64_t> canonical_records(const kmer_ctx *c) {
+    std::unordered_map<std::string, uint64_t> cls;
+    for (auto &kv : c->exotic) {
+        std::string r(kv.first.rbegin(), kv.first.rend());
+        for (char &ch : r) ch = (char)comp((uint8_t)ch);
+        cls[std::min(kv.first, r)] += kv.second.count;
+    }
+    return cls;
 }
 
 // Host result of a table finish: every canonical entry expanded into its Map
@@ -1114,6 +1152,7 @@ kmer_status build_table_result(kmer_ctx *c, uint64_t lines, kmer_result **out) {
         std::unordered_map<uint64_t, uint64_t> bigc;
         for (auto &b : big) bigc[b.h] = b.count;
         const uint64_t inv = inv_odd(TAB_MUL);
+        const bool canon = (c->p.flags & KMER_FLAG_CANONICAL) != 0;
         const uint64_t kmask = k >= 32 ? 0xFFFFFFFFull : ((1ull << k) - 1);
         std::string key(k, 'A'), rkey(k, 'A');
         for (uint32_t q = 0; q < TAB_NQ; ++q) {
@@ -1130,12 +1169,24 @@ kmer_status build_table_result(kmer_ctx *c, uint64_t lines, kmer_result **out) {
                     rkey[k - 1 - j] = "TGCA"[v];
                 }
                 const bool pal = key == rkey;
+                if (canon) {                          // one key per class, counted once per window
+                    const std::string &ck = key < rkey ? key : rkey;
+                    if (ck.compare(0, c->prefix.size(), c->prefix) == 0) ents.emplace_back(ck, cnt);
+                    continue;
+                }
                 if (key.compare(0, c->prefix.size(), c->prefix) == 0) ents.emplace_back(key, pal ? 2 * cnt : cnt);
                 if (!pal && rkey.compare(0, c->prefix.size(), c->prefix) == 0) ents.emplace_back(rkey, cnt);
             }
         }
     }
-    for (auto &kv : c->exotic) ents.emplace_back(kv.first, kv.second.count);
+    if (c->p.flags & KMER_FLAG_CANONICAL) {
+        // record keys (non-ACGT windows; forward windows only, unfiltered):
+        // classed under min(x, rc x), then the prefix is tested on that key
+        for (auto &kv : canonical_records(c))
+            if (kv.first.compare(0, c->prefix.size(), c->prefix) == 0) ents.emplace_back(kv.first, kv.second);
+    } else {
+        for (auto &kv : c->exotic) ents.emplace_back(kv.first, kv.second.count);
+    }
     std::sort(ents.begin(), ents.end());
     r->keys.reserve(ents.size() * k);
     r->offsets.reserve(ents.size() + 1);
@@ -1732,8 +1783,13 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
     bool acgt = plen > 0;
     for (char ch : c->prefix) acgt &= ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T';
     const bool dense_ok = !(pp->flags & KMER_FLAG_NO_DENSE) && pp->step == 1 && plen <= k;
-    if ((pp->flags & KMER_FLAG_UNORDERED) && pp->step == 1 && plen <= k && k <= (uint32_t)KMAX_PACKED &&
-        (plen == 0 || acgt))
+    if ((pp->flags & KMER_FLAG_CANONICAL) &&
+        !(pp->step == 1 && plen <= k && k <= (uint32_t)KMAX_PACKED && (plen == 0 || acgt))) {
+        delete c;                               // (canonical counts exist in table mode only)
+        return KMER_E_BAD_PARAM;
+    }
+    if ((pp->flags & (KMER_FLAG_UNORDERED | KMER_FLAG_CANONICAL)) && pp->step == 1 && plen <= k &&
+        k <= (uint32_t)KMAX_PACKED && (plen == 0 || acgt))
         c->mode = MODE_TABLE;
     else if (dense_ok && (plen == 0 ? k <= 31 : (acgt && plen <= 3 && k <= (uint32_t)KMAX_DENSE)))
         c->mode = MODE_WINDOWS;
@@ -1851,7 +1907,9 @@ kmer_status kmer_close(kmer_ctx *c) {
     c->rec_keys.release();
     c->tmp.release();
     c->batch.release();
-    for (auto *b : {&c->tb1, &c->tb2, &c->tHs, &c->tstart, &c->tp1}) b->release();
+    for (auto *b : {&c->tb1, &c->tb2, &c->tHs, &c->tstart, &c->tp1, &c->tpb}) b->release();
+    c->tpc.release();
+    c->tpieces.release();
     c->tH.release();
     c->tnd.release();
     c->tunits.release();
@@ -2277,6 +2335,7 @@ kmer_status kmer_result_device(kmer_ctx *c, const void **d_keys, const void **d_
                                uint64_t *n) {
     if (!c || !n) return KMER_E_BAD_PARAM;
     SETTLE(c);
+    if (c->mode == MODE_TABLE) return fail(c, KMER_E_STATE, "table mode: use kmer_table_device");
     kmer_status st = resolve_out(c);
     if (st) return st;
     if (d_keys) *d_keys = c->keys_out.p;
@@ -2292,9 +2351,17 @@ kmer_status kmer_table_stats(kmer_ctx *c, uint64_t *canonical, uint64_t *keys, u
     if (c->mode != MODE_TABLE) return fail(c, KMER_E_STATE, "not a table-mode context (KMER_FLAG_UNORDERED)");
     if (!c->t_done) return fail(c, KMER_E_STATE, "no table finish yet");
     uint64_t rk = 0, rs = 0;
-    for (auto &kv : c->exotic) {
-        rk += 1;
-        rs += kv.second.count;
+    if (c->p.flags & KMER_FLAG_CANONICAL) {
+        for (auto &kv : canonical_records(c))
+            if (kv.first.compare(0, c->prefix.size(), c->prefix) == 0) {
+                rk += 1;
+                rs += kv.second;
+            }
+    } else {
+        for (auto &kv : c->exotic) {
+            rk += 1;
+            rs += kv.second.count;
+        }
     }
     if (canonical) *canonical = c->t_canon;
     if (keys) *keys = c->t_nkeys + rk;

@@ -369,6 +369,7 @@ struct TabArgs {
     uint32_t nwg;                  // pass-1 workgroups
     uint32_t k;
     uint32_t plo, phi, pmask;      // prefix planes (base i at bit i), mask of |P| bits
+    uint32_t canonical;            // non-ACGT windows: forward-strand records, unfiltered (KMER_FLAG_CANONICAL)
     uint32_t *H1;                  // hist: [p * nwg + g]
     const uint64_t *H1s;           // scatter: exclusive scan of H1 (chunk-relative)
     uint64_t base;                 // scatter: session keys before this chunk
@@ -402,10 +403,15 @@ struct TabFinal {
     uint64_t big_cap;
     unsigned int *err;
     uint32_t k, plo, phi, pmask;
+    uint32_t canonical;            // statistics of the canonical-k-mer view (KMER_FLAG_CANONICAL)
     uint64_t inv;                  // inverse of TAB_MUL mod 2^64 (tab_mix^-1)
     unsigned long long *stats;     // [0] canonical entries [1] Map keys [2] sum of Map counts
 };
 
+constexpr uint64_t TAB_PIECE = 4096;                   // windows per piece of a long line (pass 1)
+hipError_t launch_tab_piece_count(const uint64_t *wcount, uint64_t n, uint32_t *pc, hipStream_t s);
+hipError_t launch_tab_piece_write(const SeqLine *lines, const uint64_t *wcount, const uint64_t *pbase, uint64_t n,
+                                  uint32_t k, SeqLine *out, hipStream_t s);
 hipError_t launch_tab_hist1(const TabArgs &a, hipStream_t s);
 hipError_t launch_tab_scatter1(const TabArgs &a, hipStream_t s);
 hipError_t launch_tab_p1_offsets(const uint64_t *H1s, uint32_t nwg, uint64_t *out, hipStream_t s);

@@ -181,8 +181,12 @@ __device__ __forceinline__ uint32_t tab_round(const TabArgs &a, TabCur &c, bool 
             }
         } else if (rec) {
             const uint64_t pos = readlane64(d.start, sli[j]) + s;
-            if (fm) tab_record(a, pos, 0);
-            if (rm) tab_record(a, pos, 1);
+            if (a.canonical) {
+                tab_record(a, pos, 0);           // every forward window: classed on the host
+            } else {
+                if (fm) tab_record(a, pos, 0);
+                if (rm) tab_record(a, pos, 1);
+            }
         }
     }
     return valid << OFF;
@@ -256,6 +260,35 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter1_kernel(TabArgs a) {
         cur[t] += cnt;
         bcnt[t] = 0;
         if (!__syncthreads_or(c.m < c.end)) break;
+    }
+}
+
+// Long lines (contigs) are cut into pieces of <= TAB_PIECE windows, so that
+// pass 1's per-workgroup shares of lines carry similar work: table mode has no
+// order, so a piece is just a shorter line (its k-1 byte overlap with the next
+// piece holds no window start of its own).  wcount = 2 W per line.
+__global__ __launch_bounds__(256) void tab_piece_count_kernel(const uint64_t *wcount, uint64_t n, uint32_t *pc) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t w = wcount[i] / 2;
+        pc[i] = (uint32_t)((w + TAB_PIECE - 1) / TAB_PIECE);
+    }
+}
+
+__global__ __launch_bounds__(256) void tab_piece_write_kernel(const SeqLine *lines, const uint64_t *wcount,
+                                                              const uint64_t *pbase, uint64_t n, uint32_t k,
+                                                              SeqLine *out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t w = wcount[i] / 2;
+        const SeqLine sl = lines[i];
+        uint64_t o = pbase[i];
+        for (uint64_t s0 = 0; s0 < w; s0 += TAB_PIECE) {
+            const uint64_t pw = w - s0 < TAB_PIECE ? w - s0 : TAB_PIECE;
+            SeqLine p;
+            p.start = sl.start + s0;
+            p.len = pw + k - 1;
+            p.line_index = sl.line_index;
+            out[o++] = p;
+        }
     }
 }
 
@@ -566,11 +599,25 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
                 const uint32_t lo = (uint32_t)code & kmask, hi = (uint32_t)(code >> k) & kmask;
                 const uint32_t rlo2 = __brev(~lo & kmask) >> sh, rhi2 = __brev(~hi & kmask) >> sh;
                 const bool pal = lo == rlo2 && hi == rhi2;
-                const bool fs = (((lo ^ a.plo) | (hi ^ a.phi)) & a.pmask) == 0;
-                const bool rs = !pal && (((rlo2 ^ a.plo) | (rhi2 ^ a.phi)) & a.pmask) == 0;
                 st_canon += 1;
-                st_keys += (fs ? 1u : 0u) + (rs ? 1u : 0u);
-                st_sum += (fs ? (pal ? 2 * cnt : cnt) : 0) + (rs ? cnt : 0);
+                if (a.canonical) {
+                    // one key per class: the lexicographically smaller of w, rc w
+                    // (first differing base decides), counted C times
+                    const uint32_t dif = (lo ^ rlo2) | (hi ^ rhi2);
+                    const uint32_t j = dif ? __ffs(dif) - 1 : 0;
+                    const uint32_t bw = (((hi >> j) & 1u) << 1) | ((lo >> j) & 1u);
+                    const uint32_t br = (((rhi2 >> j) & 1u) << 1) | ((rlo2 >> j) & 1u);
+                    const bool wmin = dif == 0 || bw < br;
+                    const uint32_t clo = wmin ? lo : rlo2, chi = wmin ? hi : rhi2;
+                    const bool cs = (((clo ^ a.plo) | (chi ^ a.phi)) & a.pmask) == 0;
+                    st_keys += cs ? 1u : 0u;
+                    st_sum += cs ? cnt : 0;
+                } else {
+                    const bool fs = (((lo ^ a.plo) | (hi ^ a.phi)) & a.pmask) == 0;
+                    const bool rs = !pal && (((rlo2 ^ a.plo) | (rhi2 ^ a.phi)) & a.pmask) == 0;
+                    st_keys += (fs ? 1u : 0u) + (rs ? 1u : 0u);
+                    st_sum += (fs ? (pal ? 2 * cnt : cnt) : 0) + (rs ? cnt : 0);
+                }
             }
         }
         if (t == 0) a.nd[q] = nout;
@@ -603,6 +650,22 @@ hipError_t launch_tab_scatter1(const TabArgs &a, hipStream_t s) {
 
 hipError_t launch_tab_p1_offsets(const uint64_t *H1s, uint32_t nwg, uint64_t *out, hipStream_t s) {
     hipLaunchKernelGGL(tab_p1_offsets_kernel, dim3(TAB_NB / 256), dim3(256), 0, s, H1s, nwg, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_tab_piece_count(const uint64_t *wcount, uint64_t n, uint32_t *pc, hipStream_t s) {
+    uint64_t blocks = (n + 255) / 256;
+    blocks = blocks < 1 ? 1 : blocks > 16384 ? 16384 : blocks;
+    hipLaunchKernelGGL(tab_piece_count_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, wcount, n, pc);
+    return hipGetLastError();
+}
+
+hipError_t launch_tab_piece_write(const SeqLine *lines, const uint64_t *wcount, const uint64_t *pbase, uint64_t n,
+                                  uint32_t k, SeqLine *out, hipStream_t s) {
+    uint64_t blocks = (n + 255) / 256;
+    blocks = blocks < 1 ? 1 : blocks > 16384 ? 16384 : blocks;
+    hipLaunchKernelGGL(tab_piece_write_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, lines, wcount, pbase, n, k,
+                       out);
     return hipGetLastError();
 }
 

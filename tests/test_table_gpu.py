@@ -82,6 +82,8 @@ def test_table_synthetic_vs_oracle(native, k, prefix):
     ctr.feed_device(buf.data_ptr(), len(host))
     got = ctr.finish().entries()
     canon, keys, total = ctr.table_stats()
+    with pytest.raises(native.KmerError):          # no ordered device result in table mode
+        ctr.result_device()
     ctr.close()
     assert len(got) == len(want)
     assert first_diff(got, want) is None
@@ -158,3 +160,40 @@ def test_table_matches_ordered_path_at_scale(native):
     ordered_sum = int(device_u64(d_counts, n, buf.device).sum().item())
     ordered.close()
     assert n == keys and ordered_sum == total
+
+
+def _canonical_from_map(entries):
+    """Canonical counts derived from the reference Map (App. A.6: Map(x) =
+    fwd(x) + fwd(rc x)): class {x, rc x} under min(x, rc x) counts its forward
+    windows = Map(c), or Map(c) / 2 for a self-complementary c."""
+    from oracle import oracle
+    m = dict(entries)
+    out = []
+    for key, v in m.items():
+        rc = oracle.complement(key)
+        if key <= rc:
+            out.append((key, v // 2 if key == rc else v))
+    return sorted(out)
+
+
+@pytest.mark.parametrize("k,prefix", [(21, b""), (16, b"A"), (31, b""), (12, b"GT")])
+def test_canonical_mode_vs_oracle(native, golden, inputs, k, prefix):
+    # KMER_FLAG_CANONICAL (BASELINE C5's "canonical k-mers"): one key per
+    # {x, rc x} class, counted once per forward window
+    from oracle import oracle
+    rng = np.random.default_rng(k)
+    arr = np.frombuffer(bytearray(oracle.synth_fastq(6, 0, 20000)), dtype=np.uint8).reshape(-1, 317).copy()
+    seq = arr[:, 13:163]
+    seq[rng.random(seq.shape) < 0.002] = ord("N")
+    arr[:, 13:163] = seq
+    datas = [arr.tobytes(), inputs["test_kmers.fastq"], inputs["test_long.kmer.fastq"], inputs["edge_contigs.fsa"]]
+    ctr = native.Counter(k=k, prefix=prefix, flags=native.FLAG_CANONICAL)
+    for data in datas:
+        want = _canonical_from_map(oracle.count_buffer(data, prefix, k, 1))
+        got = ctr.count_buffer(data).entries()
+        assert first_diff(got, want) is None, (k, prefix)
+        _, keys, total = ctr.table_stats()
+        assert keys == len(want) and total == sum(v for _, v in want)
+    ctr.close()
+    with pytest.raises(native.KmerError):          # canonical counts need a table-mode configuration
+        native.Counter(k=16, prefix=b"N", flags=native.FLAG_CANONICAL)
