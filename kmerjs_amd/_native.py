@@ -32,6 +32,19 @@ EXPORTS = ["kmer_open", "kmer_close", "kmer_count_file", "kmer_count_buffer", "k
            "kmer_synth_fastq_device",
            "kmer_last_timing", "kmer_phase_times", "kmer_table_stats", "kmer_table_device",
            "kmer_status_string", "kmer_last_error", "kmer_version"]
+# include/kmer_match.h (the template matcher, same library)
+MATCH_EXPORTS = ["kmer_db_open", "kmer_db_info", "kmer_db_close", "kmer_match_open", "kmer_match_open_device",
+                 "kmer_match_info", "kmer_match_templates", "kmer_match_winner", "kmer_match_remove",
+                 "kmer_match_removed", "kmer_match_close", "kmer_match_last_error"]
+EXPORTS = EXPORTS + MATCH_EXPORTS
+ORDER_FIRST_HIT = 0    # kmer_match_templates: the Redis path's templates Map order
+ORDER_DB = 1           # the Mongo aggregation's (DB) order
+
+
+class Winner(ctypes.Structure):
+    _fields_ = [("tmpl", ctypes.c_uint32), ("reserved", ctypes.c_uint32), ("uscore", ctypes.c_uint64),
+                ("tscore", ctypes.c_uint64), ("hits", ctypes.c_uint64), ("first_uscore", ctypes.c_uint64),
+                ("first_tscore", ctypes.c_uint64)]
 
 
 class Params(ctypes.Structure):
@@ -102,6 +115,21 @@ def _load():
         "kmer_status_string": (ctypes.c_char_p, [ctypes.c_int]),
         "kmer_last_error": (ctypes.c_char_p, [vp]),
         "kmer_version": (ctypes.c_char_p, []),
+        "kmer_db_open": (ctypes.c_int, [ctypes.c_int32, ctypes.c_uint32, vp, u64, pu64, ctypes.c_uint32,
+                                        ctypes.POINTER(vp)]),
+        "kmer_db_info": (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32), pu64,
+                                        pu64]),
+        "kmer_db_close": (ctypes.c_int, [vp]),
+        "kmer_match_open": (ctypes.c_int, [vp, vp, pu64, pu64, u64, ctypes.POINTER(vp)]),
+        "kmer_match_open_device": (ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, u64, vp, ctypes.POINTER(vp)]),
+        "kmer_match_info": (ctypes.c_int, [vp, pu64, ctypes.POINTER(ctypes.c_uint32)]),
+        "kmer_match_templates": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
+                                                pu64, pu64, ctypes.POINTER(ctypes.c_uint32)]),
+        "kmer_match_winner": (ctypes.c_int, [vp, ctypes.POINTER(Winner)]),
+        "kmer_match_remove": (ctypes.c_int, [vp, ctypes.c_uint32, pu64]),
+        "kmer_match_removed": (ctypes.c_int, [vp, vp]),
+        "kmer_match_close": (ctypes.c_int, [vp]),
+        "kmer_match_last_error": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -1,0 +1,725 @@
+// kmer_match.hip — k-mer -> template matching on the GPU (include/kmer_match.h).
+//
+// kmerFinder scores reference genomes ("templates") by the query k-mers they
+// share (lib/kmerFinderServer.js:171-226, :736-849).  The reference does one
+// Redis lrange per query k-mer and folds the lists into a JS Map, then loops
+// winner-takes-all: the template with the most shared k-mers wins, its k-mers
+// leave the query, everything is re-scored.  Here:
+//
+//   DB (once):  k-mers packed to 2-bit codes, (code, template) pairs radix
+//               sorted (stable: a k-mer's templates stay in DB order), dedup,
+//               CSR: U[m] sorted distinct codes, O[m + 1] list offsets, T[] templates.
+//   round 1:    each query key packed and binary-searched in U; hits expanded to
+//               (template, query) pairs in (query, list) order, radix sorted by
+//               template (stable) -> per-template segments of query indices:
+//               uScore = segment length, tScore = sum of counts (one wave per
+//               template), first hit = the segment's first query.  Templates
+//               ranked by (first query, template) = the Redis Map's insertion order.
+//   winner:     one workgroup: max of uScore << 32 | ~rank.
+//   remove:     the winner's segment: each query k-mer still present is
+//               removed (atomic exchange) and its templates' scores drop.
+//
+// All integer work; the join is a few random reads per query key and the
+// remove touches only the winner's k-mers.
+#include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/kmer_match.h"
+
+namespace {
+
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+thread_local std::string g_err;
+
+kmer_status set_err(kmer_status s, const std::string &msg) {
+    g_err = msg;
+    return s;
+}
+
+#define MCHK(x)                                                                      \
+    do {                                                                             \
+        hipError_t e_ = (x);                                                         \
+        if (e_ != hipSuccess) return set_err(KMER_E_DEVICE, std::string("HIP error: ") + hipGetErrorString(e_) + " at " #x); \
+    } while (0)
+
+template <typename T>
+hipError_t dalloc(T **p, uint64_t n) {
+    return hipMalloc((void **)p, std::max<uint64_t>(n, 1) * sizeof(T));
+}
+
+struct Temp {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc(&p, n);
+        if (e == hipSuccess) cap = n;
+        return e;
+    }
+    ~Temp() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+#define MROC(tmp, CALL)                       \
+    do {                                      \
+        size_t b = 0;                         \
+        void *t = nullptr;                    \
+        MCHK(CALL);                           \
+        MCHK((tmp).ensure(b + 16));           \
+        t = (tmp).p;                          \
+        MCHK(CALL);                           \
+    } while (0)
+
+int bit_width64(uint64_t x) {
+    int b = 0;
+    while (x) {
+        ++b;
+        x >>= 1;
+    }
+    return b;
+}
+
+__device__ __forceinline__ int base2(uint32_t c) {
+    return c == 'A' ? 0 : c == 'C' ? 1 : c == 'G' ? 2 : c == 'T' ? 3 : -1;
+}
+
+__device__ __forceinline__ bool pack_key(const uint8_t *p, uint32_t k, uint64_t *code) {
+    uint64_t v = 0;
+    bool ok = true;
+    for (uint32_t i = 0; i < k; ++i) {
+        const int b = base2(p[i]);
+        ok &= b >= 0;
+        v = (v << 2) | (uint64_t)(b & 3);
+    }
+    *code = v;
+    return ok;
+}
+
+// ---------------------------------------------------------------------------
+// DB kernels
+// ---------------------------------------------------------------------------
+__global__ void db_pack_kernel(const uint8_t *keys, uint64_t n, uint32_t k, uint64_t *codes, uint32_t *bad) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t c;
+        if (!pack_key(keys + i * k, k, &c)) atomicOr(bad, 1u);
+        codes[i] = c;
+    }
+}
+
+// entry -> template (template t owns [ts[t], ts[t + 1]))
+__global__ void db_tmpl_kernel(const uint64_t *ts, uint32_t nt, uint32_t *tmpl) {
+    for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x)
+        for (uint64_t i = ts[t] + threadIdx.x; i < ts[t + 1]; i += blockDim.x) tmpl[i] = t;
+}
+
+// after the (code, template) sort: keep = not a repeated pair, head = first of its code
+struct KeepHead {
+    const uint64_t *c;
+    const uint32_t *t;
+    __device__ uint64_t operator()(uint64_t i) const {
+        const bool head = i == 0 || c[i] != c[i - 1];
+        const bool keep = head || t[i] != t[i - 1];
+        return (keep ? 1ull : 0ull) | (head ? 1ull << 32 : 0ull);
+    }
+};
+
+__global__ void db_csr_kernel(const uint64_t *c, const uint32_t *t, uint64_t n, const uint64_t *pos, uint64_t *U,
+                              uint64_t *O, uint32_t *T) {
+    KeepHead kh{c, t};
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t f = kh(i), p = pos[i];
+        const uint64_t e = p & 0xFFFFFFFFull, u = p >> 32;
+        if (f & 1) T[e] = t[i];
+        if (f >> 32) {
+            U[u] = c[i];
+            O[u] = e;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// query kernels
+// ---------------------------------------------------------------------------
+// pack + binary search: qidx = DB k-mer index or NONE, hc = its list length
+__global__ void q_lookup_kernel(const uint8_t *keys, const uint64_t *offs, uint32_t klen, uint64_t n, uint32_t k,
+                                const uint64_t *U, uint64_t m, const uint64_t *O, uint32_t *qidx, uint64_t *hc,
+                                uint32_t *present) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t b = offs ? offs[i] : i * klen;
+        const uint64_t len = offs ? offs[i + 1] - b : klen;
+        uint32_t idx = NONE;
+        uint64_t code;
+        if (len == k && m && pack_key(keys + b, k, &code)) {
+            uint64_t lo = 0, hi = m;           // first U[j] >= code
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) >> 1;
+                if (U[mid] < code) lo = mid + 1;
+                else hi = mid;
+            }
+            if (lo < m && U[lo] == code) idx = (uint32_t)lo;
+        }
+        qidx[i] = idx;
+        hc[i] = idx == NONE ? 0 : O[idx + 1] - O[idx];
+        present[i] = idx == NONE ? 0u : 1u;
+    }
+}
+
+// hits in (query, list) order as (template, query) pairs
+__global__ void q_emit_kernel(const uint32_t *qidx, const uint64_t *H, uint64_t n, const uint64_t *O,
+                              const uint32_t *T, uint32_t *pt, uint32_t *pq) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t idx = qidx[i];
+        if (idx == NONE) continue;
+        const uint64_t o = O[idx], len = O[idx + 1] - o, h = H[i];
+        for (uint64_t j = 0; j < len; ++j) {
+            pt[h + j] = T[o + j];
+            pq[h + j] = (uint32_t)i;
+        }
+    }
+}
+
+// seg[t] = first sorted hit of template >= t (t = 0 .. nt)
+__global__ void q_seg_kernel(const uint32_t *st, uint64_t hits, uint32_t nt, uint64_t *seg) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t <= nt; t += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t lo = 0, hi = hits;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (st[mid] < t) lo = mid + 1;
+            else hi = mid;
+        }
+        seg[t] = lo;
+    }
+}
+
+// one wave per template: round-1 scores and its first-hit sort key
+__global__ __launch_bounds__(256) void q_score_kernel(const uint64_t *seg, const uint32_t *sq, const uint64_t *cnt,
+                                                      uint32_t nt, uint32_t *u0, uint64_t *t0, uint32_t *cu,
+                                                      uint64_t *ct, uint64_t *fkey, uint32_t *nh) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint64_t t = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6; t < nt;
+         t += ((uint64_t)gridDim.x * blockDim.x) >> 6) {
+        const uint64_t a = seg[t], b = seg[t + 1];
+        uint64_t s = 0;
+        for (uint64_t e = a + lane; e < b; e += 64) s += cnt[sq[e]];
+        for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
+        if (lane == 0) {
+            const uint32_t u = (uint32_t)(b - a);
+            u0[t] = u;
+            cu[t] = u;
+            t0[t] = s;
+            ct[t] = s;
+            fkey[t] = u ? ((uint64_t)sq[a] << 32) | t : ~0ull;
+            if (u) atomicAdd(nh, 1u);
+        }
+    }
+}
+
+__global__ void q_order_kernel(const uint64_t *skey, uint32_t nh, uint32_t *order, uint32_t *rank) {
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < nh; r += gridDim.x * blockDim.x) {
+        const uint32_t t = (uint32_t)skey[r];
+        order[r] = t;
+        rank[t] = r;
+    }
+}
+
+// scal: [0] hits left; winner written to *w
+__global__ __launch_bounds__(1024) void winner_kernel(const uint32_t *order, uint32_t nh, const uint32_t *cu,
+                                                      const uint64_t *ct, const uint32_t *u0, const uint64_t *t0,
+                                                      const uint64_t *scal, kmer_winner *w) {
+    __shared__ uint64_t part[16];
+    uint64_t best = 0;
+    for (uint32_t r = threadIdx.x; r < nh; r += blockDim.x) {
+        const uint32_t u = cu[order[r]];
+        const uint64_t key = u ? ((uint64_t)u << 32) | (0xFFFFFFFFu - r) : 0;
+        best = key > best ? key : best;
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint64_t o = __shfl_xor(best, d);
+        best = o > best ? o : best;
+    }
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (uint32_t i = 1; i < blockDim.x / 64; ++i) best = part[i] > best ? part[i] : best;
+        kmer_winner o;
+        memset(&o, 0, sizeof(o));
+        o.tmpl = NONE;
+        o.hits = scal[0];
+        if (best) {
+            const uint32_t t = order[0xFFFFFFFFu - (uint32_t)best];
+            o.tmpl = t;
+            o.uscore = cu[t];
+            o.tscore = ct[t];
+            o.first_uscore = u0[t];
+            o.first_tscore = t0[t];
+        }
+        *w = o;
+    }
+}
+
+// removeWinnerKmers: the winner's query k-mers still present leave the query
+__global__ void remove_kernel(const uint64_t *seg, const uint32_t *sq, uint32_t w, uint32_t *present,
+                              const uint32_t *qidx, const uint64_t *O, const uint32_t *T, const uint64_t *cnt,
+                              uint32_t *cu, uint64_t *ct, uint64_t *scal) {
+    const uint64_t a = seg[w], b = seg[w + 1];
+    for (uint64_t e = a + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < b;
+         e += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t q = sq[e];
+        if (atomicExch(&present[q], 0u) == 0u) continue;
+        const uint32_t idx = qidx[q];
+        const uint64_t o = O[idx], len = O[idx + 1] - o, c = cnt[q];
+        for (uint64_t j = 0; j < len; ++j) {
+            const uint32_t t = T[o + j];
+            atomicSub(&cu[t], 1u);
+            atomicAdd((unsigned long long *)&ct[t], (unsigned long long)(0ull - c));
+        }
+        atomicAdd((unsigned long long *)&scal[0], (unsigned long long)(0ull - len));
+    }
+}
+
+__global__ void removed_kernel(const uint32_t *qidx, const uint32_t *present, uint64_t n, uint8_t *flags) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        flags[i] = qidx[i] != NONE && present[i] == 0u ? 1 : 0;
+}
+
+uint32_t grid_for(uint64_t n, uint32_t block = 256, uint32_t cap = 65536) {
+    const uint64_t g = (n + block - 1) / block;
+    return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(g, cap));
+}
+
+}  // namespace
+
+struct kmer_db {
+    int device = 0;
+    uint32_t k = 0, nt = 0;
+    uint64_t m = 0, entries = 0;
+    hipStream_t s = nullptr;
+    uint64_t *U = nullptr, *O = nullptr;
+    uint32_t *T = nullptr;
+};
+
+struct kmer_match {
+    kmer_db *db = nullptr;
+    uint64_t n = 0, hits0 = 0;
+    uint32_t nh = 0;
+    uint64_t *cnt = nullptr, *H = nullptr, *seg = nullptr, *t0 = nullptr, *ct = nullptr, *scal = nullptr;
+    uint32_t *qidx = nullptr, *present = nullptr, *sq = nullptr, *u0 = nullptr, *cu = nullptr, *order = nullptr,
+             *rank = nullptr;
+    kmer_winner *dw = nullptr, *hw = nullptr;
+    void release() {
+        for (void *p : {(void *)cnt, (void *)H, (void *)seg, (void *)t0, (void *)ct, (void *)scal, (void *)qidx,
+                        (void *)present, (void *)sq, (void *)u0, (void *)cu, (void *)order, (void *)rank, (void *)dw})
+            if (p) (void)hipFree(p);
+        if (hw) (void)hipHostFree(hw);
+    }
+};
+
+namespace {
+
+void free_db(kmer_db *db) {
+    if (!db) return;
+    (void)hipSetDevice(db->device);
+    if (db->U) (void)hipFree(db->U);
+    if (db->O) (void)hipFree(db->O);
+    if (db->T) (void)hipFree(db->T);
+    if (db->s) (void)hipStreamDestroy(db->s);
+    delete db;
+}
+
+kmer_status build_db(kmer_db *db, const char *keys, uint64_t n, const uint64_t *ts) {
+    hipStream_t s = db->s;
+    Temp tmp;
+    uint8_t *dkeys = nullptr;
+    uint64_t *c = nullptr, *c2 = nullptr, *dts = nullptr, *pos = nullptr;
+    uint32_t *t = nullptr, *t2 = nullptr, *bad = nullptr;
+    auto cleanup = [&]() {
+        for (void *p : {(void *)dkeys, (void *)c, (void *)c2, (void *)dts, (void *)pos, (void *)t, (void *)t2,
+                        (void *)bad})
+            if (p) (void)hipFree(p);
+    };
+    struct Guard {
+        decltype(cleanup) &f;
+        ~Guard() { f(); }
+    } guard{cleanup};
+    MCHK(dalloc(&dkeys, n * db->k));
+    MCHK(dalloc(&c, n));
+    MCHK(dalloc(&c2, n));
+    MCHK(dalloc(&t, n));
+    MCHK(dalloc(&t2, n));
+    MCHK(dalloc(&dts, (uint64_t)db->nt + 1));
+    MCHK(dalloc(&pos, n));
+    MCHK(dalloc(&bad, 1));
+    MCHK(hipMemsetAsync(bad, 0, 4, s));
+    MCHK(hipMemcpyAsync(dkeys, keys, n * db->k, hipMemcpyHostToDevice, s));
+    MCHK(hipMemcpyAsync(dts, ts, ((uint64_t)db->nt + 1) * 8, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(db_pack_kernel, dim3(grid_for(n)), dim3(256), 0, s, dkeys, n, db->k, c, bad);
+    hipLaunchKernelGGL(db_tmpl_kernel, dim3(std::min<uint32_t>(std::max<uint32_t>(db->nt, 1), 65536)), dim3(256), 0,
+                       s, dts, db->nt, t);
+    MCHK(hipGetLastError());
+    uint32_t hbad = 0;
+    MCHK(hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, s));
+    MCHK(hipStreamSynchronize(s));
+    if (hbad) return set_err(KMER_E_BAD_PARAM, "kmer_db_open: a template k-mer has a byte outside A/C/G/T");
+    rocprim::double_buffer<uint64_t> kb(c, c2);
+    rocprim::double_buffer<uint32_t> vb(t, t2);
+    MROC(tmp, rocprim::radix_sort_pairs(t, b, kb, vb, (size_t)n, 0, 2 * db->k, s));
+    const uint64_t *sc = kb.current();
+    const uint32_t *stt = vb.current();
+    rocprim::counting_iterator<uint64_t> iota(0);
+    auto flags = rocprim::make_transform_iterator(iota, KeepHead{sc, stt});
+    MROC(tmp, rocprim::exclusive_scan(t, b, flags, pos, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s));
+    uint64_t last[2] = {0, 0};
+    MCHK(hipMemcpyAsync(&last[0], pos + n - 1, 8, hipMemcpyDeviceToHost, s));
+    MCHK(hipStreamSynchronize(s));
+    // (the last entry's own flags: recomputed on the host from the two sorted tails)
+    uint64_t tail_c[2] = {0, 0};
+    uint32_t tail_t[2] = {0, 0};
+    MCHK(hipMemcpy(tail_c, sc + (n >= 2 ? n - 2 : 0), 8 * std::min<uint64_t>(n, 2), hipMemcpyDeviceToHost));
+    MCHK(hipMemcpy(tail_t, stt + (n >= 2 ? n - 2 : 0), 4 * std::min<uint64_t>(n, 2), hipMemcpyDeviceToHost));
+    bool head = n == 1 || tail_c[1] != tail_c[0];
+    bool keep = head || tail_t[1] != tail_t[0];
+    db->entries = (last[0] & 0xFFFFFFFFull) + (keep ? 1 : 0);
+    db->m = (last[0] >> 32) + (head ? 1 : 0);
+    if (db->entries >= NONE || db->m >= NONE)
+        return set_err(KMER_E_BAD_PARAM, "kmer_db_open: more than 2^32 - 2 DB entries");
+    MCHK(dalloc(&db->U, db->m));
+    MCHK(dalloc(&db->O, db->m + 1));
+    MCHK(dalloc(&db->T, db->entries));
+    hipLaunchKernelGGL(db_csr_kernel, dim3(grid_for(n)), dim3(256), 0, s, sc, stt, n, pos, db->U, db->O, db->T);
+    MCHK(hipGetLastError());
+    MCHK(hipMemcpyAsync(db->O + db->m, &db->entries, 8, hipMemcpyHostToDevice, s));
+    MCHK(hipStreamSynchronize(s));
+    return KMER_OK;
+}
+
+kmer_status match_build(kmer_match *m, const uint8_t *dkeys, const uint64_t *doffs, uint32_t klen) {
+    kmer_db *db = m->db;
+    hipStream_t s = db->s;
+    const uint64_t n = m->n;
+    const uint32_t nt = db->nt;
+    Temp tmp;
+    uint32_t *pt = nullptr, *pt2 = nullptr, *pq2 = nullptr, *nhd = nullptr;
+    uint64_t *fkey = nullptr, *fkey2 = nullptr;
+    auto cleanup = [&]() {
+        for (void *p : {(void *)pt, (void *)pt2, (void *)pq2, (void *)nhd, (void *)fkey, (void *)fkey2})
+            if (p) (void)hipFree(p);
+    };
+    struct Guard {
+        decltype(cleanup) &f;
+        ~Guard() { f(); }
+    } guard{cleanup};
+    MCHK(dalloc(&m->qidx, n));
+    MCHK(dalloc(&m->present, n));
+    MCHK(dalloc(&m->H, n));
+    MCHK(dalloc(&m->seg, (uint64_t)nt + 1));
+    MCHK(dalloc(&m->u0, nt));
+    MCHK(dalloc(&m->cu, nt));
+    MCHK(dalloc(&m->t0, nt));
+    MCHK(dalloc(&m->ct, nt));
+    MCHK(dalloc(&m->order, nt));
+    MCHK(dalloc(&m->rank, nt));
+    MCHK(dalloc(&m->scal, 2));
+    MCHK(dalloc(&m->dw, 1));
+    MCHK(hipHostMalloc((void **)&m->hw, sizeof(kmer_winner), hipHostMallocDefault));
+    MCHK(dalloc(&nhd, 1));
+    MCHK(dalloc(&fkey, nt));
+    MCHK(dalloc(&fkey2, nt));
+    // hit counts per query key (m->H holds the counts, then their scan in place)
+    uint64_t *hc = nullptr;
+    MCHK(dalloc(&hc, n));
+    hipLaunchKernelGGL(q_lookup_kernel, dim3(grid_for(n)), dim3(256), 0, s, dkeys, doffs, klen, n, db->k, db->U,
+                       db->m, db->O, m->qidx, hc, m->present);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) {
+        size_t b = 0;
+        e = rocprim::exclusive_scan(nullptr, b, hc, m->H, (uint64_t)0, (size_t)std::max<uint64_t>(n, 1),
+                                    rocprim::plus<uint64_t>(), s);
+        if (e == hipSuccess) e = tmp.ensure(b + 16);
+        if (e == hipSuccess && n)
+            e = rocprim::exclusive_scan(tmp.p, b, hc, m->H, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s);
+    }
+    uint64_t tail[2] = {0, 0};
+    if (e == hipSuccess && n) e = hipMemcpyAsync(&tail[0], m->H + n - 1, 8, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess && n) e = hipMemcpyAsync(&tail[1], hc + n - 1, 8, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFree(hc);
+    MCHK(e);
+    const uint64_t hits = tail[0] + tail[1];
+    m->hits0 = hits;
+    MCHK(hipMemcpyAsync(m->scal, &m->hits0, 8, hipMemcpyHostToDevice, s));
+    MCHK(hipMemsetAsync(nhd, 0, 4, s));
+    if (hits >= NONE) return set_err(KMER_E_BAD_PARAM, "kmer_match_open: more than 2^32 - 2 hits");
+    MCHK(dalloc(&pt, hits));
+    MCHK(dalloc(&pt2, hits));
+    MCHK(dalloc(&m->sq, hits));
+    MCHK(dalloc(&pq2, hits));
+    if (hits) {
+        hipLaunchKernelGGL(q_emit_kernel, dim3(grid_for(n)), dim3(256), 0, s, m->qidx, m->H, n, db->O, db->T, pt,
+                           pq2);
+        MCHK(hipGetLastError());
+        rocprim::double_buffer<uint32_t> kb(pt, pt2);
+        rocprim::double_buffer<uint32_t> vb(pq2, m->sq);
+        MROC(tmp, rocprim::radix_sort_pairs(t, b, kb, vb, (size_t)hits, 0, std::max(1, bit_width64(nt)), s));
+        if (vb.current() != m->sq) MCHK(hipMemcpyAsync(m->sq, vb.current(), hits * 4, hipMemcpyDeviceToDevice, s));
+        hipLaunchKernelGGL(q_seg_kernel, dim3(grid_for((uint64_t)nt + 1)), dim3(256), 0, s, kb.current(), hits, nt,
+                           m->seg);
+    } else {
+        MCHK(hipMemsetAsync(m->seg, 0, ((uint64_t)nt + 1) * 8, s));
+    }
+    hipLaunchKernelGGL(q_score_kernel, dim3(grid_for((uint64_t)nt * 64)), dim3(256), 0, s, m->seg, m->sq, m->cnt, nt,
+                       m->u0, m->t0, m->cu, m->ct, fkey, nhd);
+    MCHK(hipGetLastError());
+    MROC(tmp, rocprim::radix_sort_keys(t, b, fkey, fkey2, (size_t)std::max<uint32_t>(nt, 1), 0, 64, s));
+    MCHK(hipMemcpyAsync(&m->nh, nhd, 4, hipMemcpyDeviceToHost, s));
+    MCHK(hipStreamSynchronize(s));
+    hipLaunchKernelGGL(q_order_kernel, dim3(grid_for(std::max<uint32_t>(m->nh, 1))), dim3(256), 0, s, fkey2, m->nh,
+                       m->order, m->rank);
+    MCHK(hipGetLastError());
+    MCHK(hipStreamSynchronize(s));
+    return KMER_OK;
+}
+
+kmer_status match_open_common(kmer_db *db, uint64_t n, kmer_match **out, kmer_match **mm) {
+    if (!db || !out) return set_err(KMER_E_BAD_PARAM, "kmer_match_open: NULL argument");
+    if (n >= NONE) return set_err(KMER_E_BAD_PARAM, "kmer_match_open: more than 2^32 - 2 query keys");
+    *out = nullptr;
+    MCHK(hipSetDevice(db->device));
+    kmer_match *m = new kmer_match();
+    m->db = db;
+    m->n = n;
+    *mm = m;
+    return KMER_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+kmer_status kmer_db_open(int32_t device, uint32_t k, const char *keys, uint64_t n_keys,
+                         const uint64_t *template_start, uint32_t n_templates, kmer_db **out) {
+    if (!out || (!keys && n_keys) || !template_start) return set_err(KMER_E_BAD_PARAM, "kmer_db_open: NULL argument");
+    *out = nullptr;
+    if (k == 0 || k > 32) return set_err(KMER_E_BAD_PARAM, "kmer_db_open: k must be 1..32");
+    if (n_templates >= 0x7FFFFFFFu) return set_err(KMER_E_BAD_PARAM, "kmer_db_open: too many templates");
+    if (template_start[0] != 0 || template_start[n_templates] != n_keys)
+        return set_err(KMER_E_BAD_PARAM, "kmer_db_open: template_start must run from 0 to n_keys");
+    for (uint32_t t = 0; t < n_templates; ++t)
+        if (template_start[t + 1] < template_start[t])
+            return set_err(KMER_E_BAD_PARAM, "kmer_db_open: template_start must not decrease");
+    if (n_keys >= NONE) return set_err(KMER_E_BAD_PARAM, "kmer_db_open: more than 2^32 - 2 k-mers");
+    MCHK(hipSetDevice(device));
+    kmer_db *db = new kmer_db();
+    db->device = device;
+    db->k = k;
+    db->nt = n_templates;
+    hipError_t e = hipStreamCreateWithFlags(&db->s, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete db;
+        MCHK(e);
+    }
+    kmer_status st = KMER_OK;
+    if (n_keys) {
+        st = build_db(db, keys, n_keys, template_start);
+    } else {
+        e = dalloc(&db->O, 1);
+        if (e == hipSuccess) e = hipMemset(db->O, 0, 8);
+        if (e != hipSuccess) st = set_err(KMER_E_DEVICE, "kmer_db_open: allocation failed");
+    }
+    if (st != KMER_OK) {
+        free_db(db);
+        return st;
+    }
+    *out = db;
+    return KMER_OK;
+}
+
+kmer_status kmer_db_info(const kmer_db *db, uint32_t *k, uint32_t *n_templates, uint64_t *distinct,
+                         uint64_t *entries) {
+    if (!db) return set_err(KMER_E_BAD_PARAM, "kmer_db_info: NULL db");
+    if (k) *k = db->k;
+    if (n_templates) *n_templates = db->nt;
+    if (distinct) *distinct = db->m;
+    if (entries) *entries = db->entries;
+    return KMER_OK;
+}
+
+kmer_status kmer_db_close(kmer_db *db) {
+    free_db(db);
+    return KMER_OK;
+}
+
+kmer_status kmer_match_open(kmer_db *db, const char *keys, const uint64_t *offsets, const uint64_t *counts,
+                            uint64_t n, kmer_match **out) {
+    if (n && (!keys || !offsets || !counts)) return set_err(KMER_E_BAD_PARAM, "kmer_match_open: NULL argument");
+    kmer_match *m = nullptr;
+    kmer_status st = match_open_common(db, n, out, &m);
+    if (st != KMER_OK) return st;
+    const uint64_t nbytes = n ? offsets[n] : 0;
+    uint8_t *dk = nullptr;
+    uint64_t *doff = nullptr;
+    hipError_t e = dalloc(&dk, nbytes);
+    if (e == hipSuccess) e = dalloc(&doff, n + 1);
+    if (e == hipSuccess) e = dalloc(&m->cnt, n);
+    if (e == hipSuccess && nbytes) e = hipMemcpyAsync(dk, keys, nbytes, hipMemcpyHostToDevice, db->s);
+    if (e == hipSuccess && n) e = hipMemcpyAsync(doff, offsets, (n + 1) * 8, hipMemcpyHostToDevice, db->s);
+    if (e == hipSuccess && n) e = hipMemcpyAsync(m->cnt, counts, n * 8, hipMemcpyHostToDevice, db->s);
+    st = e == hipSuccess ? match_build(m, dk, doff, 0)
+                         : set_err(KMER_E_DEVICE, std::string("HIP error: ") + hipGetErrorString(e));
+    (void)hipStreamSynchronize(db->s);
+    if (dk) (void)hipFree(dk);
+    if (doff) (void)hipFree(doff);
+    if (st != KMER_OK) {
+        m->release();
+        delete m;
+        return st;
+    }
+    *out = m;
+    return KMER_OK;
+}
+
+kmer_status kmer_match_open_device(kmer_db *db, const void *d_keys, uint32_t klen, const void *d_counts, uint64_t n,
+                                   void *stream, kmer_match **out) {
+    if (n && (!d_keys || !d_counts || klen == 0))
+        return set_err(KMER_E_BAD_PARAM, "kmer_match_open_device: NULL argument");
+    kmer_match *m = nullptr;
+    kmer_status st = match_open_common(db, n, out, &m);
+    if (st != KMER_OK) return st;
+    hipEvent_t ev = nullptr;
+    hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventRecord(ev, (hipStream_t)stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(db->s, ev, 0);
+    if (e == hipSuccess) e = dalloc(&m->cnt, n);
+    if (e == hipSuccess && n) e = hipMemcpyAsync(m->cnt, d_counts, n * 8, hipMemcpyDeviceToDevice, db->s);
+    st = e == hipSuccess ? match_build(m, (const uint8_t *)d_keys, nullptr, klen)
+                         : set_err(KMER_E_DEVICE, std::string("HIP error: ") + hipGetErrorString(e));
+    if (ev) (void)hipEventDestroy(ev);
+    if (st != KMER_OK) {
+        m->release();
+        delete m;
+        return st;
+    }
+    *out = m;
+    return KMER_OK;
+}
+
+kmer_status kmer_match_info(kmer_match *m, uint64_t *hits, uint32_t *n_templates) {
+    if (!m) return set_err(KMER_E_BAD_PARAM, "kmer_match_info: NULL match");
+    MCHK(hipSetDevice(m->db->device));
+    kmer_winner w;
+    kmer_status st = kmer_match_winner(m, &w);
+    if (st != KMER_OK) return st;
+    if (hits) *hits = w.hits;
+    if (n_templates) {
+        uint32_t n = 0;
+        st = kmer_match_templates(m, KMER_ORDER_DB, 0, nullptr, nullptr, nullptr, &n);
+        if (st != KMER_OK) return st;
+        *n_templates = n;
+    }
+    return KMER_OK;
+}
+
+kmer_status kmer_match_templates(kmer_match *m, uint32_t order, uint32_t cap, uint32_t *tmpl, uint64_t *uscore,
+                                 uint64_t *tscore, uint32_t *n) {
+    if (!m || !n || (cap && (!tmpl || !uscore || !tscore)) || order > KMER_ORDER_DB)
+        return set_err(KMER_E_BAD_PARAM, "kmer_match_templates: bad argument");
+    MCHK(hipSetDevice(m->db->device));
+    const uint32_t nt = m->db->nt, nh = m->nh;
+    std::vector<uint32_t> ord(nh), cu(nt);
+    std::vector<uint64_t> ct(nt);
+    hipStream_t s = m->db->s;
+    if (nh) MCHK(hipMemcpyAsync(ord.data(), m->order, nh * 4ull, hipMemcpyDeviceToHost, s));
+    if (nt) MCHK(hipMemcpyAsync(cu.data(), m->cu, nt * 4ull, hipMemcpyDeviceToHost, s));
+    if (nt) MCHK(hipMemcpyAsync(ct.data(), m->ct, nt * 8ull, hipMemcpyDeviceToHost, s));
+    MCHK(hipStreamSynchronize(s));
+    uint32_t c = 0;
+    auto put = [&](uint32_t t) {
+        if (!cu[t]) return;
+        if (c < cap) {
+            tmpl[c] = t;
+            uscore[c] = cu[t];
+            tscore[c] = ct[t];
+        }
+        ++c;
+    };
+    if (order == KMER_ORDER_FIRST_HIT) {
+        for (uint32_t r = 0; r < nh; ++r) put(ord[r]);
+    } else {
+        for (uint32_t t = 0; t < nt; ++t) put(t);
+    }
+    *n = c;
+    return KMER_OK;
+}
+
+kmer_status kmer_match_winner(kmer_match *m, kmer_winner *w) {
+    if (!m || !w) return set_err(KMER_E_BAD_PARAM, "kmer_match_winner: NULL argument");
+    MCHK(hipSetDevice(m->db->device));
+    hipStream_t s = m->db->s;
+    hipLaunchKernelGGL(winner_kernel, dim3(1), dim3(1024), 0, s, m->order, m->nh, m->cu, m->ct, m->u0, m->t0,
+                       m->scal, m->dw);
+    MCHK(hipGetLastError());
+    MCHK(hipMemcpyAsync(m->hw, m->dw, sizeof(kmer_winner), hipMemcpyDeviceToHost, s));
+    MCHK(hipStreamSynchronize(s));
+    *w = *m->hw;
+    return KMER_OK;
+}
+
+kmer_status kmer_match_remove(kmer_match *m, uint32_t tmpl, uint64_t *hits) {
+    if (!m || tmpl >= m->db->nt) return set_err(KMER_E_BAD_PARAM, "kmer_match_remove: bad template");
+    MCHK(hipSetDevice(m->db->device));
+    hipStream_t s = m->db->s;
+    uint64_t ab[2];
+    MCHK(hipMemcpyAsync(ab, m->seg + tmpl, 16, hipMemcpyDeviceToHost, s));
+    MCHK(hipStreamSynchronize(s));
+    const uint64_t len = ab[1] - ab[0];
+    if (len) {
+        hipLaunchKernelGGL(remove_kernel, dim3(grid_for(len)), dim3(256), 0, s, m->seg, m->sq, tmpl, m->present,
+                           m->qidx, m->db->O, m->db->T, m->cnt, m->cu, m->ct, m->scal);
+        MCHK(hipGetLastError());
+    }
+    uint64_t h = 0;
+    MCHK(hipMemcpyAsync(&h, m->scal, 8, hipMemcpyDeviceToHost, s));
+    MCHK(hipStreamSynchronize(s));
+    if (hits) *hits = h;
+    return KMER_OK;
+}
+
+kmer_status kmer_match_removed(kmer_match *m, uint8_t *flags) {
+    if (!m || (m->n && !flags)) return set_err(KMER_E_BAD_PARAM, "kmer_match_removed: NULL argument");
+    if (!m->n) return KMER_OK;
+    MCHK(hipSetDevice(m->db->device));
+    hipStream_t s = m->db->s;
+    uint8_t *d = nullptr;
+    MCHK(dalloc(&d, m->n));
+    hipLaunchKernelGGL(removed_kernel, dim3(grid_for(m->n)), dim3(256), 0, s, m->qidx, m->present, m->n, d);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(flags, d, m->n, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFree(d);
+    MCHK(e);
+    return KMER_OK;
+}
+
+kmer_status kmer_match_close(kmer_match *m) {
+    if (!m) return KMER_OK;
+    (void)hipSetDevice(m->db->device);
+    (void)hipStreamSynchronize(m->db->s);
+    m->release();
+    delete m;
+    return KMER_OK;
+}
+
+const char *kmer_match_last_error(void) { return g_err.c_str(); }
+
+}  // extern "C"

@@ -1,0 +1,346 @@
+"""K-mer -> template matching (kmerFinder's findMatches) over the GPU matcher
+(include/kmer_match.h) -- the Python mirror of kmerjs_amd/node/kmerfinder.js.
+
+Reference: lib/kmerFinderServer.js -- findKmersMatchesRedis (:171-226),
+winnerScoring (:736-849: findWinner, removeWinnerKmers, getMatches, loop),
+standardScoring (:857-874) over findMatchesMongoAggregation (:452-522),
+matchSummary (:625-676); lib/stats.js zScore (:19-45) and fastp (:52-115).
+The joins and re-scoring run on the GPU; the statistics of a winner are
+scalar decimal arithmetic done here with bignumber.js 2.x semantics
+(package.json:61): dividedBy and sqrt round to 20 decimal places half up,
+plus / minus / times are exact, round(dp, 6) is half-even, toNumber parses the
+decimal string.
+
+A template is a dict {'sequence', 'lengths', 'ulength', 'species', 'kmers'}
+(the ETL's Mongo document, src/kmerPyToMongo.py:36-42, with `reads` as
+`kmers`); summary = {'templates', 'totalLen', 'uniqueLens'}
+(test_data/summary.json).  Errors: NoHits carries the reference's messages.
+"""
+import ctypes
+import math
+
+import numpy as np
+
+from . import _native
+from ._native import LIB, KmerError
+
+DP = 20
+
+
+class NoHits(Exception):
+    """`throw new Error('No hits were found! ...')` of the reference."""
+
+
+# -- decimals: (integer, scale) = integer / 10**scale --------------------------
+class Dec:
+    __slots__ = ("n", "s")
+
+    def __init__(self, n, s=0):
+        self.n, self.s = n, s
+
+    @staticmethod
+    def of(x):
+        if isinstance(x, Dec):
+            return x
+        if isinstance(x, int):
+            return Dec(x, 0)
+        t = repr(float(x)) if isinstance(x, float) else str(x)    # like new BigNumber(number): its string form
+        mant, _, ex = t.lower().partition("e")
+        ip, _, fp = mant.partition(".")
+        n = int((ip + fp) or "0")
+        return Dec(n, len(fp) - int(ex or 0)) if len(fp) - int(ex or 0) >= 0 else Dec(n * 10 ** (int(ex) - len(fp)), 0)
+
+    def _al(self, o):
+        o = Dec.of(o)
+        s = max(self.s, o.s)
+        return self.n * 10 ** (s - self.s), o.n * 10 ** (s - o.s), s
+
+    def __add__(self, o):
+        a, b, s = self._al(o)
+        return Dec(a + b, s)
+
+    def __sub__(self, o):
+        a, b, s = self._al(o)
+        return Dec(a - b, s)
+
+    def __rsub__(self, o):
+        return Dec.of(o) - self
+
+    def __mul__(self, o):
+        o = Dec.of(o)
+        return Dec(self.n * o.n, self.s + o.s)
+
+    def cmp(self, o):
+        a, b, _ = self._al(o)
+        return (a > b) - (a < b)
+
+    def div(self, o, dp=DP):
+        """dividedBy: rounded to dp places, half away from zero."""
+        o = Dec.of(o)
+        num, den = self.n * 10 ** (dp + o.s), o.n * 10 ** self.s
+        neg = (num < 0) != (den < 0)
+        q, r = divmod(abs(num), abs(den))
+        if 2 * r >= abs(den):
+            q += 1
+        return Dec(-q if neg else q, dp)
+
+    def sqrt(self, dp=DP):
+        """sqrt rounded to dp places, half up (self >= 0)."""
+        # y = self * 10^(2 dp) = n * 10^(2dp - s); t = floor(sqrt(y))
+        e = 2 * dp - self.s
+        num, den = (self.n * 10 ** e, 1) if e >= 0 else (self.n, 10 ** -e)
+        t = math.isqrt(num // den)
+        if 4 * num >= (2 * t + 1) ** 2 * den:       # sqrt(y) >= t + 1/2
+            t += 1
+        return Dec(t, dp)
+
+    def round(self, dp, half_even=False):
+        if self.s <= dp:
+            return self
+        d = 10 ** (self.s - dp)
+        neg = self.n < 0
+        q, r = divmod(abs(self.n), d)
+        if 2 * r > d or (2 * r == d and (not half_even or q % 2 == 1)):
+            q += 1
+        return Dec(-q if neg else q, dp)
+
+    def to_number(self):
+        return float(self.n) if self.s == 0 else float("%de-%d" % (self.n, self.s))
+
+
+ETTA = Dec(1, 8)                      # lib/stats.js:6
+EVALUE = Dec(5, 2)                    # lib/kmers.js:75
+_FASTP = [(Dec.of(a), Dec.of(b)) for a, b in (
+    ("10.7016", "1e-26"), ("10.4862", "1e-25"), ("10.2663", "1e-24"), ("10.0416", "1e-23"), ("9.81197", "1e-22"),
+    ("9.5769", "1e-21"), ("9.33604", "1e-20"), ("9.08895", "1e-19"), ("8.83511", "1e-18"), ("8.57394", "1e-17"),
+    ("8.30479", "1e-16"), ("8.02686", "1e-15"), ("7.73926", "1e-14"), ("7.4409", "1e-13"), ("7.13051", "1e-12"),
+    ("6.8065", "1e-11"), ("6.46695", "1e-10"), ("6.10941", "1e-9"), ("5.73073", "1e-8"), ("5.32672", "1e-7"),
+    ("4.89164", "1e-6"), ("4.41717", "1e-5"), ("3.89059", "1e-4"), ("3.29053", "1e-3"), ("2.57583", "0.01"),
+    ("1.95996", "0.05"), ("1.64485", "0.1"))]
+
+
+def fastp(z):
+    """lib/stats.js:52-115."""
+    for thr, p in _FASTP:
+        if z.cmp(thr) > 0:
+            return p
+    return Dec(1)
+
+
+def z_score(r1, n1, r2, n2):
+    """lib/stats.js:19-45."""
+    p1 = Dec.of(r1).div(n1) + ETTA
+    p2 = Dec.of(r2).div(n2) + ETTA
+    p = (Dec.of(r1) + r2).div(Dec.of(n1) + n2 + ETTA)
+    q = Dec(1) - p
+    sq = (p * q * (Dec(1).div(Dec.of(n1) + ETTA) + Dec(1).div(Dec.of(n2) + ETTA)) + ETTA).sqrt()
+    return (p1 - p2).div(sq)
+
+
+def match_summary(query_size, name, t, u, ts, first_u, first_t, hits, summary):
+    """matchSummary (lib/kmerFinderServer.js:625-676) -> [(key, value)] or None."""
+    if not u > 0:
+        return None
+    z = z_score(u, t["ulength"], hits, summary["uniqueLens"])
+    prob = fastp(z) * summary["templates"]
+    if EVALUE.cmp(prob) < 0:
+        return None
+    qs = Dec.of(query_size) + ETTA
+    ul = Dec.of(t["ulength"]) + ETTA
+    r2 = lambda x: x.round(2, True).to_number()            # noqa: E731
+    return [("template", name), ("score", u),
+            ("expected", (Dec.of(hits) * t["ulength"]).div(summary["uniqueLens"]).round(0, True).to_number()),
+            ("z", z.round(2).to_number()), ("probability", prob.to_number()),
+            ("frac-q", r2(Dec(200 * u).div(qs))), ("frac-d", r2(Dec(100 * u).div(ul))),
+            ("depth", r2(Dec.of(ts).div(t["lengths"]))), ("kmers-template", t["ulength"]),
+            ("total-frac-q", r2(Dec(200 * first_u).div(qs))), ("total-frac-d", r2(Dec(100 * first_u).div(ul))),
+            ("total-temp-cover", r2(Dec.of(first_t).div(t["lengths"]))), ("species", t["species"])]
+
+
+def _check(st, what):
+    if st != 0:
+        raise KmerError(st, "%s: %s" % (what, (LIB.kmer_match_last_error() or b"").decode()))
+
+
+class TemplateDB:
+    """The template database on one GPU (kmer_db_open)."""
+
+    def __init__(self, templates, k, summary=None, device=0):
+        self.templates = list(templates)
+        self.k = k
+        self.device = device
+        nt = len(self.templates)
+        starts = np.zeros(nt + 1, dtype=np.uint64)
+        for i, t in enumerate(self.templates):
+            starts[i + 1] = starts[i] + len(t["kmers"])
+        keys = b"".join(km.encode("latin-1") if isinstance(km, str) else bytes(km)
+                        for t in self.templates for km in t["kmers"])
+        if len(keys) != int(starts[-1]) * k:
+            raise KmerError(2, "TemplateDB: every template k-mer must have length k")
+        self._open(keys, starts)
+        self.summary = summary or default_summary(self.templates)
+
+    @classmethod
+    def from_arrays(cls, k, keys, starts, meta, summary, device=0):
+        """keys: bytes of n * k; starts: uint64[nt + 1]; meta: per-template dicts
+        without 'kmers' (the bulk path used by the benchmark)."""
+        self = cls.__new__(cls)
+        self.templates, self.k, self.device, self.summary = list(meta), k, device, summary
+        self._open(keys, np.ascontiguousarray(starts, dtype=np.uint64))
+        return self
+
+    def _open(self, keys, starts):
+        h = ctypes.c_void_p()
+        _check(LIB.kmer_db_open(self.device, self.k, keys, int(starts[-1]),
+                                starts.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), len(starts) - 1,
+                                ctypes.byref(h)), "kmer_db_open")
+        self.handle = h
+
+    def info(self):
+        k, nt = ctypes.c_uint32(), ctypes.c_uint32()
+        d, e = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(LIB.kmer_db_info(self.handle, ctypes.byref(k), ctypes.byref(nt), ctypes.byref(d), ctypes.byref(e)),
+               "kmer_db_info")
+        return {"k": k.value, "templates": nt.value, "distinct": d.value, "entries": e.value}
+
+    def close(self):
+        if getattr(self, "handle", None):
+            LIB.kmer_db_close(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        self.close()
+
+
+def default_summary(templates):
+    """The DB's Summary entry: template count, total and unique k-mer lengths."""
+    return {"templates": len(templates), "totalLen": sum(int(t["lengths"]) for t in templates),
+            "uniqueLens": sum(int(t["ulength"]) for t in templates)}
+
+
+class Match:
+    """One query joined against a TemplateDB (kmer_match_open*)."""
+
+    def __init__(self, db, keys=None, counts=None, device_result=None, stream=0):
+        self.db = db
+        h = ctypes.c_void_p()
+        if device_result is not None:
+            d_keys, klen, d_counts, n = device_result
+            _check(LIB.kmer_match_open_device(db.handle, d_keys, klen, d_counts, n, stream, ctypes.byref(h)),
+                   "kmer_match_open_device")
+            self.n = n
+        else:
+            enc = [k.encode("latin-1") if isinstance(k, str) else bytes(k) for k in keys]
+            off = np.zeros(len(enc) + 1, dtype=np.uint64)
+            np.cumsum([len(x) for x in enc], out=off[1:]) if enc else None
+            cnt = np.ascontiguousarray(counts, dtype=np.uint64)
+            blob = b"".join(enc)
+            pu = ctypes.POINTER(ctypes.c_uint64)
+            _check(LIB.kmer_match_open(db.handle, blob, off.ctypes.data_as(pu), cnt.ctypes.data_as(pu), len(enc),
+                                       ctypes.byref(h)), "kmer_match_open")
+            self.n = len(enc)
+        self.handle = h
+
+    def templates(self, order=_native.ORDER_FIRST_HIT):
+        n = ctypes.c_uint32()
+        _check(LIB.kmer_match_templates(self.handle, order, 0, None, None, None, ctypes.byref(n)),
+               "kmer_match_templates")
+        cap = n.value
+        t = (ctypes.c_uint32 * max(cap, 1))()
+        u = (ctypes.c_uint64 * max(cap, 1))()
+        s = (ctypes.c_uint64 * max(cap, 1))()
+        _check(LIB.kmer_match_templates(self.handle, order, cap, t, u, s, ctypes.byref(n)), "kmer_match_templates")
+        return [(t[i], u[i], s[i]) for i in range(cap)]
+
+    def winner(self):
+        w = _native.Winner()
+        _check(LIB.kmer_match_winner(self.handle, ctypes.byref(w)), "kmer_match_winner")
+        return w
+
+    def remove(self, tmpl):
+        h = ctypes.c_uint64()
+        _check(LIB.kmer_match_remove(self.handle, tmpl, ctypes.byref(h)), "kmer_match_remove")
+        return h.value
+
+    def removed(self):
+        f = np.zeros(max(self.n, 1), dtype=np.uint8)
+        _check(LIB.kmer_match_removed(self.handle, f.ctypes.data_as(ctypes.c_void_p)), "kmer_match_removed")
+        return f[:self.n]
+
+    def close(self):
+        if getattr(self, "handle", None):
+            LIB.kmer_match_close(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        self.close()
+
+
+class KmerFinder:
+    """findMatches of KmerFinderServer (lib/kmerFinderServer.js:920-928) over a
+    TemplateDB.  method 'winner' (Redis path) or 'standard' (Mongo path)."""
+
+    def __init__(self, db, method="winner", max_hits=100):
+        if method not in ("winner", "standard"):
+            raise ValueError("Scoring scheme unknown")
+        self.db, self.method, self.max_hits = db, method, max_hits
+
+    def _summary(self, m, query_size, ti, u, ts, fu, ft, hits):
+        t = self.db.templates[ti]
+        return match_summary(query_size, t["sequence"], t, u, ts, fu, ft, hits, self.db.summary)
+
+    def find_matches(self, query, query_size=None, match=None):
+        """query: dict key -> count in Map order (winner: MUTATED, winners'
+        k-mers deleted, like the reference's kmerMap), or None with `match`
+        given (an open Match, e.g. over a device result).  query_size =
+        kmerObject.kmerMapSize (default len(query)).  Returns the list of
+        summaries (lists of (key, value) pairs); 'standard' keeps the
+        reference's trailing None (JS undefined) entries."""
+        own = match is None
+        if own:
+            keys = list(query.keys())
+            match = Match(self.db, keys, [query[k] for k in keys])
+        if query_size is None:
+            query_size = len(query) if query is not None else match.n
+        try:
+            return self._standard(match, query_size) if self.method == "standard" else \
+                self._winner(match, query, query_size)
+        finally:
+            if own:
+                match.close()
+
+    def _standard(self, m, query_size):
+        tl = m.templates(_native.ORDER_DB)
+        hits = sum(u for _, u, _ in tl)
+        if hits == 0:
+            raise NoHits("No hits were found!")
+        out = [self._summary(m, query_size, ti, u, ts, u, ts, hits) for ti, u, ts in tl]
+        kept = sorted([x for x in out if x is not None], key=lambda w: -w[1][1])
+        return kept + [None] * (len(out) - len(kept))
+
+    def _winner(self, m, query, query_size):
+        results = []
+        w = m.winner()
+        if w.hits == 0:
+            raise NoHits("No hits were found!")
+        try:
+            while True:
+                s = self._summary(m, query_size, w.tmpl, w.uscore, w.tscore, w.first_uscore, w.first_tscore, w.hits)
+                if s is None or EVALUE.cmp(Dec.of(s[4][1])) < 0:
+                    break
+                results.append(s)
+                m.remove(w.tmpl)                  # removeWinnerKmers + getMatches
+                if len(results) >= self.max_hits:
+                    break
+                w = m.winner()
+                if w.hits == 0:
+                    raise NoHits("No hits were found! (nHits === 0)")
+        finally:
+            # the reference deleted the winners' k-mers from the caller's Map as it went
+            if query is not None and results:
+                keys = list(query.keys())
+                for i in np.nonzero(m.removed())[0]:
+                    del query[keys[i]]
+        if not results:
+            raise NoHits("No hits were found! (kmerResults.length === 0)")
+        return results

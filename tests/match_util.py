@@ -1,0 +1,76 @@
+"""Synthetic template databases and queries for the matcher tests and bench.
+
+The reference's template DB (kmerFinder's complete-genome k-mer sets, Redis /
+MongoDB) is not in the tree, so the DB is synthetic: templates grouped in
+clades that share part of their k-mers (related genomes), each template's
+k-mers unique; the query mixes k-mers of a few "present" templates with
+random noise, non-ACGT keys and keys of another length.
+"""
+import numpy as np
+
+BASES = np.frombuffer(b"ACGT", dtype=np.uint8)
+
+
+def kmer_strings(codes, k):
+    """uint64 2-bit codes (first base most significant) -> list of str."""
+    codes = np.asarray(codes, dtype=np.uint64)
+    shifts = np.arange(2 * (k - 1), -1, -2, dtype=np.uint64)
+    mat = BASES[((codes[:, None] >> shifts[None, :]) & np.uint64(3)).astype(np.int64)]
+    raw = mat.tobytes()
+    return [raw[i * k:(i + 1) * k].decode("latin-1") for i in range(len(codes))]
+
+
+def kmer_codes(rng, n, k, prefix="ATGAC"):
+    """n random k-mer codes that start with `prefix`."""
+    pl = len(prefix)
+    pc = 0
+    for ch in prefix:
+        pc = pc * 4 + "ACGT".index(ch)
+    free = 2 * (k - pl)
+    lo = rng.integers(0, 1 << free, size=n, dtype=np.uint64) if free else np.zeros(n, dtype=np.uint64)
+    return (np.uint64(pc) << np.uint64(free)) | lo
+
+
+def make_db(seed, n_templates, per_template, k=16, prefix="ATGAC", clades=4, shared=0.5):
+    """Templates as dicts (sequence, lengths, ulength, species, kmers: [str])."""
+    rng = np.random.default_rng(seed)
+    pools = [kmer_codes(rng, per_template * 2, k, prefix) for _ in range(clades)]
+    out = []
+    for t in range(n_templates):
+        c = t % clades
+        ns = int(per_template * shared)
+        sh = rng.choice(pools[c], size=ns, replace=False)
+        own = kmer_codes(rng, per_template - ns, k, prefix)
+        codes = np.unique(np.concatenate([sh, own]))
+        rng.shuffle(codes)
+        kms = kmer_strings(codes, k)
+        out.append({"sequence": "NC_%06d" % t, "lengths": int(len(kms) * 2 + rng.integers(0, 50)),
+                    "ulength": len(kms), "species": "Species clade%d strain%d" % (c, t), "kmers": kms})
+    return out
+
+
+def make_query(seed, templates, present, frac=0.6, noise=200, k=16, prefix="ATGAC", extras=True, background=0.03):
+    """Ordered dict key -> count: k-mers of the `present` templates (a fraction
+    of each), a `background` fraction of every template's k-mers (so that the
+    winner loop ends on an insignificant winner, not on exhausted hits),
+    random noise k-mers, and (extras) keys that can never match."""
+    rng = np.random.default_rng(seed)
+    q = {}
+    for t in templates:
+        kms = t["kmers"]
+        for i in rng.choice(len(kms), size=int(len(kms) * background), replace=False):
+            q.setdefault(kms[i], int(rng.integers(1, 3)))
+    for t in present:
+        kms = templates[t]["kmers"]
+        pick = rng.choice(len(kms), size=int(len(kms) * frac), replace=False)
+        for i in pick:
+            q.setdefault(kms[i], int(rng.integers(1, 6)))
+    for km in kmer_strings(kmer_codes(rng, noise, k, prefix), k):
+        q.setdefault(km, int(rng.integers(1, 4)))
+    if extras:
+        q.setdefault("ATGAC" + "N" * (k - 5), 3)
+        q.setdefault("ATGAC" + "A" * (k - 4), 2)       # length k + 1
+        q.setdefault("atgac" + "a" * (k - 5), 1)
+    items = list(q.items())
+    rng.shuffle(items)
+    return dict(items)

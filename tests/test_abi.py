@@ -8,8 +8,10 @@ from tests.conftest import REPO
 
 
 def header_symbols():
-    with open(os.path.join(REPO, "include", "kmer_api.h")) as f:
-        text = f.read()
+    text = ""
+    for h in ("kmer_api.h", "kmer_match.h"):
+        with open(os.path.join(REPO, "include", h)) as f:
+            text += f.read()
     return sorted(set(re.findall(r"\b(kmer_[a-z_]+)\s*\(", text)))
 
 
