@@ -195,10 +195,12 @@ def load_traffic(args, kernel):
 
 
 # table mode (C3): algorithmic bytes of each phase per launch, from the
-# pass-1 key count n (8-B keys) -- DESIGN.md §4
-def table_phase_bytes(nbytes, n_keys, canonical, sub_bits):
+# pass-1 key count n (8-B keys) -- DESIGN.md §5.  final: every key read once
+# (a bucket is held in registers across its LDS ranges) + one 8-B entry written
+# per distinct canonical k-mer.
+def table_phase_bytes(nbytes, n_keys, canonical):
     return {"lines": 2 * nbytes, "hist1": nbytes, "scatter1": nbytes + 8 * n_keys, "hist2": 8 * n_keys,
-            "scatter2": 16 * n_keys, "final": 8 * n_keys * (1 << sub_bits) + 8 * canonical}
+            "scatter2": 16 * n_keys, "final": 8 * n_keys + 8 * canonical}
 
 
 def main():
@@ -424,11 +426,7 @@ def main():
             # pass-1 keys = forward windows counted (no prefix): the Map sum is
             # twice that, the canonical sum once
             n_keys = (accepted if args.flags & _FC else accepted // 2) if not args.prefix else None
-            mean = (n_keys or 0) >> 20
-            sub_bits = 0
-            while sub_bits < 16 and (mean >> sub_bits) > 6000:
-                sub_bits += 1
-            pbytes = table_phase_bytes(nbytes, n_keys or 0, canonical, sub_bits)
+            pbytes = table_phase_bytes(nbytes, n_keys or 0, canonical)
             kern_name = max(phases, key=lambda x: phases[x])
             kern_ms = phases[kern_name]
             algo_bytes = pbytes[kern_name]

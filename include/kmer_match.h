@@ -78,6 +78,11 @@ enum { KMER_ORDER_FIRST_HIT = 0, KMER_ORDER_DB = 1 };
 kmer_status kmer_match_templates(kmer_match *m, uint32_t order, uint32_t cap, uint32_t *tmpl, uint64_t *uscore,
                                  uint64_t *tscore, uint32_t *n);
 
+/* The round-1 query k-mers of template `tmpl` as query indices, ascending
+ * (the `kmers` Set of its templates-Map entry, lib/kmerFinderServer.js:190-198).
+ * Up to `cap` entries; *n = their number. */
+kmer_status kmer_match_template_kmers(kmer_match *m, uint32_t tmpl, uint64_t cap, uint32_t *qidx, uint64_t *n);
+
 typedef struct {
     uint32_t tmpl;          /* template index; UINT32_MAX when no template has hits */
     uint32_t reserved;

@@ -34,7 +34,7 @@ EXPORTS = ["kmer_open", "kmer_close", "kmer_count_file", "kmer_count_buffer", "k
            "kmer_status_string", "kmer_last_error", "kmer_version"]
 # include/kmer_match.h (the template matcher, same library)
 MATCH_EXPORTS = ["kmer_db_open", "kmer_db_info", "kmer_db_close", "kmer_match_open", "kmer_match_open_device",
-                 "kmer_match_info", "kmer_match_templates", "kmer_match_winner", "kmer_match_remove",
+                 "kmer_match_info", "kmer_match_templates", "kmer_match_template_kmers", "kmer_match_winner", "kmer_match_remove",
                  "kmer_match_removed", "kmer_match_close", "kmer_match_last_error"]
 EXPORTS = EXPORTS + MATCH_EXPORTS
 ORDER_FIRST_HIT = 0    # kmer_match_templates: the Redis path's templates Map order
@@ -125,6 +125,8 @@ def _load():
         "kmer_match_info": (ctypes.c_int, [vp, pu64, ctypes.POINTER(ctypes.c_uint32)]),
         "kmer_match_templates": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32),
                                                 pu64, pu64, ctypes.POINTER(ctypes.c_uint32)]),
+        "kmer_match_template_kmers": (ctypes.c_int, [vp, ctypes.c_uint32, u64, ctypes.POINTER(ctypes.c_uint32),
+                                                     pu64]),
         "kmer_match_winner": (ctypes.c_int, [vp, ctypes.POINTER(Winner)]),
         "kmer_match_remove": (ctypes.c_int, [vp, ctypes.c_uint32, pu64]),
         "kmer_match_removed": (ctypes.c_int, [vp, vp]),

@@ -662,6 +662,23 @@ kmer_status kmer_match_templates(kmer_match *m, uint32_t order, uint32_t cap, ui
     return KMER_OK;
 }
 
+kmer_status kmer_match_template_kmers(kmer_match *m, uint32_t tmpl, uint64_t cap, uint32_t *qidx, uint64_t *n) {
+    if (!m || !n || tmpl >= m->db->nt || (cap && !qidx))
+        return set_err(KMER_E_BAD_PARAM, "kmer_match_template_kmers: bad argument");
+    MCHK(hipSetDevice(m->db->device));
+    hipStream_t s = m->db->s;
+    uint64_t ab[2];
+    MCHK(hipMemcpyAsync(ab, m->seg + tmpl, 16, hipMemcpyDeviceToHost, s));
+    MCHK(hipStreamSynchronize(s));
+    const uint64_t len = ab[1] - ab[0];
+    if (cap && len) {
+        MCHK(hipMemcpyAsync(qidx, m->sq + ab[0], std::min(cap, len) * 4, hipMemcpyDeviceToHost, s));
+        MCHK(hipStreamSynchronize(s));
+    }
+    *n = len;
+    return KMER_OK;
+}
+
 kmer_status kmer_match_winner(kmer_match *m, kmer_winner *w) {
     if (!m || !w) return set_err(KMER_E_BAD_PARAM, "kmer_match_winner: NULL argument");
     MCHK(hipSetDevice(m->db->device));

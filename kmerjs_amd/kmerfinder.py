@@ -252,6 +252,16 @@ class Match:
         _check(LIB.kmer_match_templates(self.handle, order, cap, t, u, s, ctypes.byref(n)), "kmer_match_templates")
         return [(t[i], u[i], s[i]) for i in range(cap)]
 
+    def template_kmers(self, tmpl):
+        """Round-1 query indices of template `tmpl`, ascending."""
+        n = ctypes.c_uint64()
+        _check(LIB.kmer_match_template_kmers(self.handle, tmpl, 0, None, ctypes.byref(n)), "kmer_match_template_kmers")
+        out = np.zeros(max(n.value, 1), dtype=np.uint32)
+        _check(LIB.kmer_match_template_kmers(self.handle, tmpl, n.value,
+                                             out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(n)),
+               "kmer_match_template_kmers")
+        return out[:n.value]
+
     def winner(self):
         w = _native.Winner()
         _check(LIB.kmer_match_winner(self.handle, ctypes.byref(w)), "kmer_match_winner")

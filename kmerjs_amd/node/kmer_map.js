@@ -9,7 +9,10 @@
  *   - iteration (for..of, keys(), values(), entries(), forEach, spread) walks
  *     the packed entries in order, cutting each key out of the one string;
  *   - size is a field;
- *   - get / has / set / delete build a key -> index Map on their first use;
+ *   - get / has / set / delete build a key -> index hash table on their first
+ *     use: open addressing in one Int32Array, FNV-1a over the key's character
+ *     codes read straight from the packed string, candidates confirmed with
+ *     startsWith at their offset -- no per-key string or Map entry is created;
  *   - the consumers' mutations (lib/kmerFinderClient.js:132-133 set 'db' /
  *     'collection', :223-225 and lib/kmerFinderServer.js:781-783 delete) follow
  *     Map semantics exactly: set on a present key keeps its position, a new (or
@@ -29,7 +32,8 @@ class KmerMap extends Map {
         this._off = off;
         this._cnt = cnt;
         this._n = cnt.length;
-        this._idx = null;        // key -> packed index (built on first keyed access)
+        this._tab = null;        // hash table of packed indices (built on first keyed access)
+        this._mask = 0;
         this._mod = null;        // packed index -> value set since (Map)
         this._del = null;        // Uint8Array: packed index deleted
         this._ndel = 0;
@@ -53,19 +57,59 @@ class KmerMap extends Map {
 
     _live(i) { return this._del === null || this._del[i] === 0; }
 
+    _hashAt(a, b) {
+        const s = this._all;
+        let h = 0x811c9dc5 | 0;
+        for (let j = a; j < b; j += 1) h = Math.imul(h ^ s.charCodeAt(j), 16777619);
+        return h;
+    }
+
     _index() {
-        if (this._idx === null) {
-            const m = new Map();
-            for (let i = 0; i < this._n; i += 1) m.set(this._key(i), i);
-            this._idx = m;
+        if (this._tab === null) {
+            const n = this._n;
+            const off = this._off;
+            let cap = 16;
+            while (cap < 2 * n) cap *= 2;
+            const tab = new Int32Array(cap).fill(-1);
+            const mask = cap - 1;
+            for (let i = 0; i < n; i += 1) {
+                let h = this._hashAt(off[i], off[i + 1]) & mask;
+                while (tab[h] !== -1) h = (h + 1) & mask;
+                tab[h] = i;
+            }
+            this._tab = tab;
+            this._mask = mask;
         }
-        return this._idx;
+        return this._tab;
     }
 
     // packed index of a live packed key, else -1
     _find(key) {
-        const i = this._index().get(key);
-        return i !== undefined && this._live(i) ? i : -1;
+        if (typeof key !== 'string' || this._n === 0) return -1;
+        const tab = this._index();
+        const off = this._off;
+        const all = this._all;
+        let h = 0x811c9dc5 | 0;
+        for (let j = 0; j < key.length; j += 1) h = Math.imul(h ^ key.charCodeAt(j), 16777619);
+        h &= this._mask;
+        for (let i = tab[h]; i !== -1; i = tab[h]) {
+            if (off[i + 1] - off[i] === key.length && all.startsWith(key, off[i])) return this._live(i) ? i : -1;
+            h = (h + 1) & this._mask;
+        }
+        return -1;
+    }
+
+    // the packed entries alone, unmodified (the matcher can take them as they are)
+    _packedOnly() { return this._ndel === 0 && this._mod === null && super.size === 0; }
+
+    // delete packed entry i (kmerfinder.js: the winners' k-mers, by index)
+    _deletePacked(i) {
+        if (!this._live(i)) return false;
+        if (this._del === null) this._del = new Uint8Array(this._n);
+        this._del[i] = 1;
+        this._ndel += 1;
+        if (this._mod !== null) this._mod.delete(i);
+        return true;
     }
 
     get size() { return this._n - this._ndel + super.size; }
@@ -102,7 +146,7 @@ class KmerMap extends Map {
         this._n = 0;
         this._ndel = 0;
         this._all = '';
-        this._idx = null;
+        this._tab = null;
         this._mod = null;
         this._del = null;
         super.clear();

@@ -10,6 +10,15 @@
 //   countBuffer(handle, buffer, cb(err, {...}))
 //   close(handle)
 //   version() -> string
+// Template matching (include/kmer_match.h; used by kmerfinder.js), synchronous:
+//   dbOpen(k, keysBuffer, startsFloat64Array, device) -> db
+//   dbInfo(db) -> {k, templates, distinct, entries};  dbClose(db)
+//   matchOpen(db, keysBuffer, offsetsFloat64Array, countsFloat64Array) -> match
+//   matchTemplates(match, order) -> {tmpl: Uint32Array, u: Float64Array, t: Float64Array}
+//   matchTemplateKmers(match, tmpl) -> Uint32Array (round-1 query indices of tmpl)
+//   matchWinner(match) -> {tmpl (-1: none), uscore, tscore, hits, firstU, firstT}
+//   matchRemove(match, tmpl) -> hits left;  matchRemoved(match) -> Uint8Array
+//   matchClose(match)
 #include <node_api.h>
 
 #include <cstdlib>
@@ -18,6 +27,7 @@
 #include <vector>
 
 #include "../../include/kmer_api.h"
+#include "../../include/kmer_match.h"
 
 namespace {
 
@@ -285,6 +295,307 @@ napi_value Version(napi_env env, napi_callback_info) {
     return v;
 }
 
+
+// ---------------------------------------------------------------------------
+// template matching
+// ---------------------------------------------------------------------------
+struct DbHandle {
+    kmer_db *db = nullptr;
+};
+struct MatchHandle {
+    kmer_match *m = nullptr;
+    napi_ref dbref = nullptr;     // the DB outlives the match
+};
+
+void finalize_db(napi_env, void *data, void *) {
+    DbHandle *h = static_cast<DbHandle *>(data);
+    if (h->db) kmer_db_close(h->db);
+    delete h;
+}
+
+void finalize_match(napi_env env, void *data, void *) {
+    MatchHandle *h = static_cast<MatchHandle *>(data);
+    if (h->m) kmer_match_close(h->m);
+    if (h->dbref) napi_delete_reference(env, h->dbref);
+    delete h;
+}
+
+napi_value throw_match(napi_env env, kmer_status st, const char *what) {
+    std::string msg = std::string(what) + ": " + kmer_status_string(st) + ": " + kmer_match_last_error();
+    napi_value err, code, m;
+    napi_create_string_utf8(env, msg.c_str(), NAPI_AUTO_LENGTH, &m);
+    napi_create_error(env, nullptr, m, &err);
+    napi_create_int32(env, (int)st, &code);
+    napi_set_named_property(env, err, "status", code);
+    napi_throw(env, err);
+    return nullptr;
+}
+
+bool get_f64_as_u64(napi_env env, napi_value v, std::vector<uint64_t> &out) {
+    bool is = false;
+    napi_is_typedarray(env, v, &is);
+    if (!is) return false;
+    napi_typedarray_type t;
+    size_t n = 0;
+    void *data = nullptr;
+    napi_value ab;
+    size_t off = 0;
+    if (napi_get_typedarray_info(env, v, &t, &n, &data, &ab, &off) != napi_ok || t != napi_float64_array) return false;
+    const double *d = static_cast<const double *>(data);
+    out.resize(n);
+    for (size_t i = 0; i < n; ++i) out[i] = (uint64_t)d[i];
+    return true;
+}
+
+template <typename T>
+T *get_ext(napi_env env, napi_value v, const char *what) {
+    void *p = nullptr;
+    if (napi_get_value_external(env, v, &p) != napi_ok || !p) {
+        napi_throw_type_error(env, nullptr, what);
+        return nullptr;
+    }
+    return static_cast<T *>(p);
+}
+
+napi_value DbOpen(napi_env env, napi_callback_info info) {
+    size_t argc = 4;
+    napi_value argv[4];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    if (argc < 3) {
+        napi_throw_type_error(env, nullptr, "dbOpen(k, keys, starts, device)");
+        return nullptr;
+    }
+    const uint32_t k = get_u32(env, argv[0], 16);
+    void *kd = nullptr;
+    size_t klen = 0;
+    bool isbuf = false;
+    napi_is_buffer(env, argv[1], &isbuf);
+    std::vector<uint64_t> starts;
+    if (!isbuf || !get_f64_as_u64(env, argv[2], starts) || starts.empty()) {
+        napi_throw_type_error(env, nullptr, "dbOpen: keys must be a Buffer, starts a Float64Array");
+        return nullptr;
+    }
+    NAPI_CALL(env, napi_get_buffer_info(env, argv[1], &kd, &klen));
+    const int32_t dev = argc > 3 ? (int32_t)get_u32(env, argv[3], 0) : 0;
+    DbHandle *h = new DbHandle();
+    kmer_status st = kmer_db_open(dev, k, (const char *)kd, starts.back(), starts.data(),
+                                  (uint32_t)(starts.size() - 1), &h->db);
+    if (st != KMER_OK) {
+        delete h;
+        return throw_match(env, st, "kmer_db_open");
+    }
+    if (k && (uint64_t)klen != starts.back() * k) {
+        kmer_db_close(h->db);
+        delete h;
+        napi_throw_range_error(env, nullptr, "dbOpen: keys length != n * k");
+        return nullptr;
+    }
+    napi_value ext;
+    NAPI_CALL(env, napi_create_external(env, h, finalize_db, nullptr, &ext));
+    return ext;
+}
+
+napi_value DbInfo(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    DbHandle *h = get_ext<DbHandle>(env, argv[0], "invalid db handle");
+    if (!h) return nullptr;
+    if (!h->db) {
+        napi_throw_error(env, nullptr, "db closed");
+        return nullptr;
+    }
+    uint32_t k = 0, nt = 0;
+    uint64_t d = 0, e = 0;
+    kmer_db_info(h->db, &k, &nt, &d, &e);
+    napi_value o, v;
+    napi_create_object(env, &o);
+    napi_create_double(env, k, &v);
+    napi_set_named_property(env, o, "k", v);
+    napi_create_double(env, nt, &v);
+    napi_set_named_property(env, o, "templates", v);
+    napi_create_double(env, (double)d, &v);
+    napi_set_named_property(env, o, "distinct", v);
+    napi_create_double(env, (double)e, &v);
+    napi_set_named_property(env, o, "entries", v);
+    return o;
+}
+
+napi_value DbClose(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    DbHandle *h = get_ext<DbHandle>(env, argv[0], "invalid db handle");
+    if (!h) return nullptr;
+    // matches hold a reference to the db's JS object, not to kmer_db: the
+    // caller closes its matches first (kmerfinder.js does)
+    if (h->db) kmer_db_close(h->db);
+    h->db = nullptr;
+    napi_value u;
+    napi_get_undefined(env, &u);
+    return u;
+}
+
+napi_value MatchOpen(napi_env env, napi_callback_info info) {
+    size_t argc = 4;
+    napi_value argv[4];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    if (argc < 4) {
+        napi_throw_type_error(env, nullptr, "matchOpen(db, keys, offsets, counts)");
+        return nullptr;
+    }
+    DbHandle *dh = get_ext<DbHandle>(env, argv[0], "invalid db handle");
+    if (!dh) return nullptr;
+    if (!dh->db) {
+        napi_throw_error(env, nullptr, "db closed");
+        return nullptr;
+    }
+    void *kd = nullptr;
+    size_t klen = 0;
+    bool isbuf = false;
+    napi_is_buffer(env, argv[1], &isbuf);
+    std::vector<uint64_t> offs, cnts;
+    if (!isbuf || !get_f64_as_u64(env, argv[2], offs) || !get_f64_as_u64(env, argv[3], cnts) ||
+        offs.size() < cnts.size() + 1) {
+        napi_throw_type_error(env, nullptr, "matchOpen: keys Buffer, offsets / counts Float64Array");
+        return nullptr;
+    }
+    NAPI_CALL(env, napi_get_buffer_info(env, argv[1], &kd, &klen));
+    if (offs[cnts.size()] > klen) {
+        napi_throw_range_error(env, nullptr, "matchOpen: offsets beyond the keys buffer");
+        return nullptr;
+    }
+    MatchHandle *h = new MatchHandle();
+    kmer_status st = kmer_match_open(dh->db, (const char *)kd, offs.data(), cnts.data(), cnts.size(), &h->m);
+    if (st != KMER_OK) {
+        delete h;
+        return throw_match(env, st, "kmer_match_open");
+    }
+    napi_create_reference(env, argv[0], 1, &h->dbref);
+    napi_value ext;
+    NAPI_CALL(env, napi_create_external(env, h, finalize_match, nullptr, &ext));
+    return ext;
+}
+
+MatchHandle *get_match(napi_env env, napi_value v) {
+    MatchHandle *h = get_ext<MatchHandle>(env, v, "invalid match handle");
+    if (h && !h->m) {
+        napi_throw_error(env, nullptr, "match closed");
+        return nullptr;
+    }
+    return h;
+}
+
+napi_value MatchTemplates(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    MatchHandle *h = get_match(env, argv[0]);
+    if (!h) return nullptr;
+    const uint32_t order = argc > 1 ? get_u32(env, argv[1], 0) : 0;
+    uint32_t n = 0;
+    kmer_status st = kmer_match_templates(h->m, order, 0, nullptr, nullptr, nullptr, &n);
+    if (st != KMER_OK) return throw_match(env, st, "kmer_match_templates");
+    std::vector<uint32_t> t(n);
+    std::vector<uint64_t> u(n), s(n);
+    st = kmer_match_templates(h->m, order, n, t.data(), u.data(), s.data(), &n);
+    if (st != KMER_OK) return throw_match(env, st, "kmer_match_templates");
+    napi_value o, ab, ta;
+    napi_create_object(env, &o);
+    void *data = nullptr;
+    napi_create_arraybuffer(env, (size_t)n * 4, &data, &ab);
+    if (n) memcpy(data, t.data(), (size_t)n * 4);
+    napi_create_typedarray(env, napi_uint32_array, n, ab, 0, &ta);
+    napi_set_named_property(env, o, "tmpl", ta);
+    napi_set_named_property(env, o, "u", make_f64_array(env, u.data(), n));
+    napi_set_named_property(env, o, "t", make_f64_array(env, s.data(), n));
+    return o;
+}
+
+napi_value MatchTemplateKmers(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    MatchHandle *h = get_match(env, argv[0]);
+    if (!h) return nullptr;
+    const uint32_t t = get_u32(env, argv[1], 0);
+    uint64_t n = 0;
+    kmer_status st = kmer_match_template_kmers(h->m, t, 0, nullptr, &n);
+    if (st != KMER_OK) return throw_match(env, st, "kmer_match_template_kmers");
+    napi_value ab, ta;
+    void *data = nullptr;
+    napi_create_arraybuffer(env, (size_t)n * 4, &data, &ab);
+    st = kmer_match_template_kmers(h->m, t, n, static_cast<uint32_t *>(data), &n);
+    if (st != KMER_OK) return throw_match(env, st, "kmer_match_template_kmers");
+    napi_create_typedarray(env, napi_uint32_array, (size_t)n, ab, 0, &ta);
+    return ta;
+}
+
+napi_value MatchWinner(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    MatchHandle *h = get_match(env, argv[0]);
+    if (!h) return nullptr;
+    kmer_winner w;
+    kmer_status st = kmer_match_winner(h->m, &w);
+    if (st != KMER_OK) return throw_match(env, st, "kmer_match_winner");
+    napi_value o, v;
+    napi_create_object(env, &o);
+    napi_create_double(env, w.tmpl == 0xFFFFFFFFu ? -1.0 : (double)w.tmpl, &v);
+    napi_set_named_property(env, o, "tmpl", v);
+    const std::pair<const char *, uint64_t> f[] = {{"uscore", w.uscore}, {"tscore", w.tscore}, {"hits", w.hits},
+                                                   {"firstU", w.first_uscore}, {"firstT", w.first_tscore}};
+    for (const auto &x : f) {
+        napi_create_double(env, (double)x.second, &v);
+        napi_set_named_property(env, o, x.first, v);
+    }
+    return o;
+}
+
+napi_value MatchRemove(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    MatchHandle *h = get_match(env, argv[0]);
+    if (!h) return nullptr;
+    uint64_t hits = 0;
+    kmer_status st = kmer_match_remove(h->m, get_u32(env, argv[1], 0), &hits);
+    if (st != KMER_OK) return throw_match(env, st, "kmer_match_remove");
+    napi_value v;
+    napi_create_double(env, (double)hits, &v);
+    return v;
+}
+
+napi_value MatchRemoved(napi_env env, napi_callback_info info) {
+    size_t argc = 2;
+    napi_value argv[2];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    MatchHandle *h = get_match(env, argv[0]);
+    if (!h) return nullptr;
+    const uint32_t n = argc > 1 ? get_u32(env, argv[1], 0) : 0;     // the query size
+    napi_value ab, ta;
+    void *data = nullptr;
+    napi_create_arraybuffer(env, n, &data, &ab);
+    kmer_status st = kmer_match_removed(h->m, static_cast<uint8_t *>(data));
+    if (st != KMER_OK) return throw_match(env, st, "kmer_match_removed");
+    napi_create_typedarray(env, napi_uint8_array, n, ab, 0, &ta);
+    return ta;
+}
+
+napi_value MatchClose(napi_env env, napi_callback_info info) {
+    size_t argc = 1;
+    napi_value argv[1];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    MatchHandle *h = get_ext<MatchHandle>(env, argv[0], "invalid match handle");
+    if (!h) return nullptr;
+    if (h->m) kmer_match_close(h->m);
+    h->m = nullptr;
+    napi_value u;
+    napi_get_undefined(env, &u);
+    return u;
+}
+
 napi_value Init(napi_env env, napi_value exports) {
     napi_property_descriptor props[] = {
         {"open", nullptr, Open, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
@@ -292,6 +603,16 @@ napi_value Init(napi_env env, napi_value exports) {
         {"countBuffer", nullptr, CountBuffer, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"close", nullptr, Close, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"version", nullptr, Version, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"dbOpen", nullptr, DbOpen, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"dbInfo", nullptr, DbInfo, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"dbClose", nullptr, DbClose, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"matchOpen", nullptr, MatchOpen, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"matchTemplates", nullptr, MatchTemplates, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"matchTemplateKmers", nullptr, MatchTemplateKmers, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"matchWinner", nullptr, MatchWinner, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"matchRemove", nullptr, MatchRemove, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"matchRemoved", nullptr, MatchRemoved, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"matchClose", nullptr, MatchClose, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
     };
     napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
     return exports;

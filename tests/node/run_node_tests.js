@@ -98,6 +98,27 @@ function cpuTests() {
         km.clear(); ref.clear();
         same();
     });
+    check('KmerMap hash index at scale, delete by packed index', () => {
+        const n = 50000;
+        const keys = [];
+        for (let i = 0; i < n; i += 1) keys.push('ATGAC' + ((i * 2654435761) >>> 0).toString(4).padStart(11, 'A'));
+        const uniq = [...new Set(keys)];
+        const buf = Buffer.from(uniq.join(''), 'latin1');
+        const off = new Float64Array(uniq.length + 1);
+        for (let i = 0; i < uniq.length; i += 1) off[i + 1] = off[i] + uniq[i].length;
+        const cnt = new Float64Array(uniq.length).map((_, i) => i + 1);
+        const km = lib.KmerMap.fromNative({ keys: buf, offsets: off, counts: cnt });
+        assert.ok(km._packedOnly());
+        for (let i = 0; i < uniq.length; i += 97) assert.strictEqual(km.get(uniq[i]), i + 1);
+        assert.strictEqual(km.get('ATGACZZZZZZZZZZZ'), undefined);
+        assert.strictEqual(km.has(uniq[5].slice(0, 15)), false);
+        assert.strictEqual(km.has(42), false);
+        assert.ok(km._deletePacked(7) && !km._deletePacked(7));
+        assert.strictEqual(km.has(uniq[7]), false);
+        assert.strictEqual(km.size, uniq.length - 1);
+        assert.ok(!km._packedOnly());
+        assert.strictEqual([...km.keys()][7], uniq[8]);
+    });
     check('legacy npm main (lib/index.js) exports and fields', () => {
         const legacy = require(path.join(repo, 'kmerjs_amd', 'node', 'index.js'));
         for (const name of ['kmers', 'complement', 'KmerJSClient', 'KmerJSServer']) assert.ok(name in legacy, name);

@@ -30,3 +30,94 @@ def test_node_dropin_cpu():
 def test_node_dropin_gpu_parity(golden):
     res = _run("gpu", 600)
     assert len(res) > 20
+
+
+KF_RUNNER = os.path.join(REPO, "tests", "node", "run_kmerfinder.js")
+
+
+def _kf(mode, spec, tmp_path, timeout):
+    f = tmp_path / "spec.json"
+    f.write_text(json.dumps(spec))
+    p = subprocess.run([NODE, KF_RUNNER, mode, str(f)], capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+def _pairs(r):
+    return None if r is None else [list(x) for x in r]
+
+
+def test_node_match_summary_matches_oracle(tmp_path):
+    # kmerfinder.js's BigInt decimals (bignumber.js 2.x semantics) against the
+    # oracle's Fraction restatement of lib/stats.js + matchSummary, no GPU
+    import random
+    from oracle import kmerfinder_oracle as ko
+    rng = random.Random(17)
+    summary = {"templates": 5030, "totalLen": 16525500, "uniqueLens": 8076292}   # test_data/summary.json
+    cases = []
+    for _ in range(300):
+        ul = rng.randint(1, 20000)
+        u = rng.randint(1, ul)
+        ts = u * rng.randint(1, 9)
+        cases.append({"u": u, "ts": ts, "lengths": ul * 2 + rng.randint(0, 99), "ulength": ul,
+                      "fu": u + rng.randint(0, 50), "ft": ts + rng.randint(0, 500),
+                      "hits": u + rng.randint(0, 10 ** 6), "qsize": rng.randint(u, 2 * 10 ** 6), "summary": summary})
+    got = _kf("stats", {"cases": cases}, tmp_path, 60)
+    seen = 0
+    for c, g in zip(cases, got):
+        m = {"uScore": c["u"], "tScore": c["ts"], "lengths": c["lengths"], "ulength": c["ulength"], "species": "s"}
+        want = ko.match_summary(c["qsize"], "NC_1", m, {"uScore": c["fu"], "tScore": c["ft"]}, c["hits"], summary)
+        assert _pairs(g) == _pairs(want), c
+        seen += want is not None
+    assert seen > 40
+
+
+@pytest.mark.gpu
+def test_node_kmerfinder_matches_oracle(tmp_path):
+    """KmerFinderServer.findMatches through Node on the GPU matcher against the
+    oracle (lib/kmerFinderServer.js:736-874): winner and standard scoring, the
+    exhausted-hits rejection, and a query Map that comes from readFile()
+    (a KmerMap: the winners' k-mers are deleted from it, by index)."""
+    from oracle import kmerfinder_oracle as ko
+    from oracle import oracle
+    from tests.match_util import make_db, make_query
+
+    def summ(db):
+        return {"templates": len(db), "totalLen": sum(t["lengths"] for t in db),
+                "uniqueLens": sum(t["ulength"] for t in db)}
+    cases, want = [], []
+    for seed, method, bg in ((31, "winner", 0.03), (32, "winner", 0.0), (33, "standard", 0.03)):
+        db = make_db(seed, 50, 400)
+        q = make_query(seed + 1, db, [3, 17, 40], background=bg)
+        s = summ(db)
+        spec_db = [{"sequence": t["sequence"], "lengths": t["lengths"], "ulenght": t["ulength"],
+                    "species": t["species"], "reads": t["kmers"]} for t in db]       # the ETL's document shape
+        cases.append({"templates": spec_db, "summary": s, "method": method, "query": list(q.items())})
+        qo = dict(q)
+        try:
+            r = (ko.winner_scoring(qo, db, s, len(q)) if method == "winner" else
+                 ko.standard_scoring(qo, db, s, len(q)))
+            want.append({"results": [_pairs(x) for x in r], "remaining": [list(x) for x in qo.items()]})
+        except ko.NoHits as e:
+            want.append({"error": str(e), "remaining": [list(x) for x in qo.items()]})
+    # a readFile() query: templates made of the file's own k-mers
+    path = os.path.join(REPO, "tests", "golden", "inputs", "test_long.kmer.fastq")
+    ents = oracle.count_buffer(open(path, "rb").read(), b"ATGAC", 16, 1)
+    q = {k.decode("latin-1"): v for k, v in ents}
+    keys = list(q)
+    db = [{"sequence": "T%d" % t, "lengths": 300, "ulength": len(keys[t::7][:60]), "species": "x",
+           "kmers": keys[t::7][:60]} for t in range(7)]
+    s = summ(db)
+    cases.append({"templates": db, "summary": s, "method": "winner", "maxHits": 3,
+                  "file": {"path": path, "prefix": "ATGAC", "k": 16}})
+    qo = dict(q)
+    r = ko.winner_scoring(qo, db, s, len(q), max_hits=3)
+    want.append({"results": [_pairs(x) for x in r], "remaining": [list(x) for x in qo.items()]})
+    got = _kf("match", {"cases": cases}, tmp_path, 300)
+    for g, w in zip(got, want):
+        if "error" in w:
+            assert g.get("error") == w["error"]
+        else:
+            assert g.get("error") is None, g.get("error")
+            assert [_pairs(x) for x in g["results"]] == w["results"]
+        assert g["remaining"] == w["remaining"]
