@@ -80,7 +80,8 @@ def test_node_kmerfinder_matches_oracle(tmp_path):
     (a KmerMap: the winners' k-mers are deleted from it, by index)."""
     from oracle import kmerfinder_oracle as ko
     from oracle import oracle
-    from tests.match_util import make_db, make_query
+    import numpy as np
+    from tests.match_util import kmer_codes, kmer_strings, make_db, make_query
 
     def summ(db):
         return {"templates": len(db), "totalLen": sum(t["lengths"] for t in db),
@@ -105,13 +106,18 @@ def test_node_kmerfinder_matches_oracle(tmp_path):
     ents = oracle.count_buffer(open(path, "rb").read(), b"ATGAC", 16, 1)
     q = {k.decode("latin-1"): v for k, v in ents}
     keys = list(q)
-    db = [{"sequence": "T%d" % t, "lengths": 300, "ulength": len(keys[t::7][:60]), "species": "x",
-           "kmers": keys[t::7][:60]} for t in range(7)]
+    # T0 holds most of the file's k-mers, T1 a few more, T2.. k-mers the file lacks
+    other = kmer_strings(kmer_codes(np.random.default_rng(5), 400, 16, "CCCCC"), 16)
+    lists = [keys[:250], keys[250:330]] + [other[i * 40:(i + 1) * 40] + keys[330 + i * 10:340 + i * 10]
+                                          for i in range(5)]
+    db = [{"sequence": "T%d" % t, "lengths": 2 * len(l), "ulength": len(l), "species": "x", "kmers": l}
+          for t, l in enumerate(lists)]
     s = summ(db)
     cases.append({"templates": db, "summary": s, "method": "winner", "maxHits": 3,
                   "file": {"path": path, "prefix": "ATGAC", "k": 16}})
     qo = dict(q)
     r = ko.winner_scoring(qo, db, s, len(q), max_hits=3)
+    assert len(r) >= 2
     want.append({"results": [_pairs(x) for x in r], "remaining": [list(x) for x in qo.items()]})
     got = _kf("match", {"cases": cases}, tmp_path, 300)
     for g, w in zip(got, want):
