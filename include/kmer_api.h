@@ -46,7 +46,7 @@ typedef enum {
     KMER_E_DEVICE = 4,        /* HIP runtime error */
     KMER_E_TOO_MANY_KEYS = 5, /* more than max_keys distinct keys (reference: RangeError at 2^24, lib/kmers.js:95) */
     KMER_E_NONASCII = 6,      /* input byte >= 0x80 (reference decodes UTF-8, lib/kmers.js:116) */
-    KMER_E_LINE_TOO_LONG = 7, /* a sequence line longer than 2^23 bytes */
+    KMER_E_LINE_TOO_LONG = 7, /* a sequence line longer than the order key holds (KMER_FLAG_LONG_LINES) */
     KMER_E_STATE = 8          /* call out of sequence (e.g. finish without reset) */
 } kmer_status;
 
@@ -67,6 +67,14 @@ enum {
      * the class (jellyfish -C).  Step 1, k <= 32, empty or A/C/G/T prefix
      * (tested on the canonical key); KMER_E_BAD_PARAM otherwise. */
     KMER_FLAG_CANONICAL = 1u << 6,
+    /* Long-line mode: order keys with a 40-bit position field, so ordered
+     * counts take sequence lines up to 2^40 bytes (FASTA contigs and
+     * chromosomes; the reference has no limit, lib/kmers.js:88-100) at up to
+     * 2^23 lines.  Default: lines up to 2^23 bytes, 2^40 lines.
+     * kmer_count_file / kmer_count_buffer switch to it by themselves when a
+     * longer line turns up (the count is redone once); the device-resident
+     * calls and multi-GPU group contexts need the flag. */
+    KMER_FLAG_LONG_LINES = 1u << 7,
     /* experiments only (results are WRONG with these set): ablate parts of the tile scan */
     KMER_FLAG_ABLATE_HITS = 1u << 8,   /* drop every prefix candidate */
     KMER_FLAG_ABLATE_SWAR = 1u << 9    /* skip the SWAR prefix scan entirely */

@@ -19,6 +19,7 @@ FLAG_SORT_FINISH = 8
 FLAG_UNORDERED = 16
 FLAG_TABLE_SPLIT_TEST = 32
 FLAG_CANONICAL = 64
+FLAG_LONG_LINES = 128
 WRITE_JSON = 0      # JSON.stringify(mapToJSON(map)), lib/kmers.js:46-54
 WRITE_LEGACY = 1    # "{\nkey: count,...}\n", lib/index.js:381-388
 

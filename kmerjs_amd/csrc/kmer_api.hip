@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <functional>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -101,6 +102,7 @@ struct kmer_ctx {
     std::string prefix, rprefix;
     Mode mode = MODE_GENERAL;
     int device = 0;
+    uint32_t pbits = PBITS_DEFAULT;       // order-key position bits (PBITS_LONG: long-line mode)
     hipStream_t stream = nullptr;  // high priority: finish, exchange, copies, everything but the scan chain
     hipStream_t sstream = nullptr; // low priority: a packed-path chunk (scan, tile scan, hit resolution)
     hipEvent_t evq = nullptr;      // orders sstream after stream
@@ -383,7 +385,10 @@ kmer_status flush_prep(kmer_ctx *c, hipStream_t s, uint32_t extra) {
 
 kmer_status check_err(kmer_ctx *c, uint32_t e) {
     if (e & ERR_NONASCII) return fail(c, KMER_E_NONASCII, "input contains a byte >= 0x80 (non-ASCII)");
-    if (e & ERR_LINE_TOO_LONG) return fail(c, KMER_E_LINE_TOO_LONG, "sequence line longer than 2^23 bytes");
+    if (e & ERR_LINE_TOO_LONG)
+        return fail(c, KMER_E_LINE_TOO_LONG,
+                    c->pbits == PBITS_DEFAULT ? "sequence line longer than 2^23 bytes (KMER_FLAG_LONG_LINES)"
+                                              : "long-line mode: a line longer than 2^40 bytes or more than 2^23 lines");
     if (e & ERR_LOOKBACK_TIMEOUT) return fail(c, KMER_E_DEVICE, "tile look-back timed out");
     return KMER_OK;
 }
@@ -504,6 +509,7 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
     h.abs_offset = c->abs_offset;
     h.pos = c->d_pos;
     h.packed = packed;
+    h.pbits = c->pbits;
     h.smask = (c->kbits >= 64) ? ~0ull : ((1ull << c->kbits) - 1ull);
     h.invalid_key = c->kbits >= 63 ? ~0ull : (1ull << c->kbits);
     h.out_base = c->n_hits;
@@ -721,6 +727,7 @@ kmer_status general_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n
         w.n_lines = c->d_line_count;
         w.k = c->p.k;
         w.step = c->p.step;
+        w.pbits = c->pbits;
         w.plen = (uint32_t)c->prefix.size();
         w.P = c->d_PR + 2 * KMAX_TILE;
         w.err = c->d_err;
@@ -785,7 +792,7 @@ kmer_status chunk_lines(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_
         HIPCHK(c, c->lines.ensure(n_seq, s));
         HIPCHK(c, c->wcount.ensure(n_seq, s));
         HIPCHK(c, launch_seq_lines(c->nlpos.p, n_nl, len, li0, n_seq, c->p.k, c->lines.p, c->wcount.p,
-                                   check_len ? c->d_err : nullptr, s));
+                                   check_len ? c->d_err : nullptr, (1ull << c->pbits) - 1ull, s));
     }
     *n_nl_out = n_nl;
     *n_seq_out = n_seq;
@@ -831,6 +838,7 @@ kmer_status windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n
     w.li0 = li0;
     w.wbase = c->wbase.p;
     w.k = c->p.k;
+    w.pbits = c->pbits;
     w.plen = (uint32_t)c->prefix.size();
     auto code = [](char ch) -> uint64_t { return ch == 'A' ? 0u : ch == 'C' ? 1u : ch == 'G' ? 2u : 3u; };
     for (char ch : c->prefix) w.pcode = (w.pcode << 2) | code(ch);
@@ -1094,9 +1102,35 @@ kmer_status table_finish(kmer_ctx *c) {
     f.inv = inv_odd(TAB_MUL);
     f.canonical = (c->p.flags & KMER_FLAG_CANONICAL) ? 1u : 0u;
     f.stats = c->tstats.p;
+    const uint32_t fgrid = (uint32_t)std::max(c->n_cu, 1);
+    std::vector<uint64_t> hprof;
+#ifdef TAB_PROF
+    if (getenv("KMERHIP_TAB_PROF")) {         // experiments (-DTAB_PROF build): per-phase clocks of the final kernel
+#else
+    if (false) {
+#endif
+        HIPCHK(c, hipMalloc((void **)&f.prof, fgrid * 64ull));
+        HIPCHK(c, hipMemsetAsync(f.prof, 0, fgrid * 64ull, s));
+        hprof.resize(fgrid * 8ull);
+    }
     HIPCHK(c, hipEventRecord(c->tev[2], s));
-    HIPCHK(c, launch_tab_final(f, (uint32_t)std::max(c->n_cu, 1), s));
+    HIPCHK(c, launch_tab_final(f, fgrid, s));
     HIPCHK(c, hipEventRecord(c->tev[7], s));
+    if (f.prof) {
+        HIPCHK(c, hipMemcpyAsync(hprof.data(), f.prof, fgrid * 64ull, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        (void)hipFree(f.prof);
+        double ph[6] = {0, 0, 0, 0, 0, 0};
+        uint64_t ranges = 0, buckets = 0;
+        for (uint32_t g = 0; g < fgrid; ++g) {
+            for (int i = 0; i < 6; ++i) ph[i] += i == 4 ? 0 : (double)hprof[g * 8 + i] * 0.01 / fgrid;   // us
+            ranges += hprof[g * 8 + 4] >> 32;
+            buckets += hprof[g * 8 + 4] & 0xFFFFFFFFull;
+        }
+        fprintf(stderr, "tab_final prof (us per workgroup): load+setup %.0f range-syncs %.0f insert %.0f emit %.0f "
+                        "empty %.0f | buckets %llu ranges %llu sub_bits %u\n", ph[0], ph[1], ph[2], ph[3], ph[5],
+                (unsigned long long)buckets, (unsigned long long)ranges, f.sub_bits);
+    }
     HIPCHK(c, hipMemcpyAsync(c->h_small + 8, c->tstats.p, 4 * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
@@ -1258,7 +1292,7 @@ kmer_status apply_cross(kmer_ctx *c) {
     if (n == 0) return KMER_OK;
     uint32_t *k32 = c->narrow ? c->rkey32.p : nullptr;
     if (!c->long_seg) {
-        HIPCHK(c, launch_cross_segsort(c->xord.p, c->xkey.p, c->xslot.p, n, c->rkey.p, k32, c->rord.p, s));
+        HIPCHK(c, launch_cross_segsort(c->xord.p, c->xkey.p, c->xslot.p, n, c->rkey.p, k32, c->rord.p, c->pbits, s));
     } else if (n <= XSMALL_MAX) {
         HIPCHK(c, launch_cross_sort_small(c->xslot.p, c->xord.p, c->xkey.p, n, c->rkey.p, k32, c->rord.p, s));
     } else {
@@ -1269,7 +1303,7 @@ kmer_status apply_cross(kmer_ctx *c) {
         HIPCHK(c, c->xkey2.ensure(n, s));
         rocprim::double_buffer<uint64_t> ob(c->xord.p, c->xord2.p);
         rocprim::double_buffer<uint64_t> kb(c->xkey.p, c->xkey2.p);
-        const int obits = std::min(64, bit_width(((pos.lines + 1) << 24) | 0xFFFFFFull));
+        const int obits = std::min(64, bit_width(((pos.lines + 1) << (c->pbits + 1)) | ((2ull << c->pbits) - 1ull)));
         ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, ob, kb, (size_t)n, 0, obits, s));
         HIPCHK(c, launch_cross_scatter(c->xslot.p, ob.current(), kb.current(), n, c->rkey.p, k32, c->rord.p, s));
     }
@@ -1779,6 +1813,7 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
             return cleanup(KMER_E_DEVICE);
     }
 
+    c->pbits = (pp->flags & KMER_FLAG_LONG_LINES) ? PBITS_LONG : PBITS_DEFAULT;
     const uint32_t k = pp->k, plen = (uint32_t)c->prefix.size();
     bool acgt = plen > 0;
     for (char ch : c->prefix) acgt &= ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T';
@@ -1969,11 +2004,22 @@ kmer_status kmer_finish_device(kmer_ctx *c, kmer_result **out) {
     return finish(c, out);
 }
 
-kmer_status kmer_count_buffer(kmer_ctx *c, const uint8_t *bytes, size_t len, kmer_result **out) {
-    if (!c || !out || (!bytes && len)) return KMER_E_BAD_PARAM;
-    *out = nullptr;
-    if (!c->group.empty()) return group_count_buffer(c, bytes, len, out);
-    if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
+namespace {
+
+// A whole-input count that met a sequence line longer than the default
+// order key's position field (2^23 bytes: a FASTA contig or chromosome) is
+// redone once in long-line mode (2^40-byte lines, up to 2^23 lines).
+kmer_status with_long_line_retry(kmer_ctx *c, const std::function<kmer_status()> &count) {
+    kmer_status st = count();
+    if (st == KMER_E_LINE_TOO_LONG && c->pbits == PBITS_DEFAULT && c->mode != MODE_TABLE) {
+        c->pbits = PBITS_LONG;
+        st = count();
+        c->pbits = PBITS_DEFAULT;
+    }
+    return st;
+}
+
+kmer_status count_buffer_once(kmer_ctx *c, const uint8_t *bytes, size_t len, kmer_result **out) {
     kmer_status st = reset(c);
     if (st) return st;
     st = feed_host(c, bytes, len);
@@ -1984,10 +2030,28 @@ kmer_status kmer_count_buffer(kmer_ctx *c, const uint8_t *bytes, size_t len, kme
     return finish(c, out);
 }
 
+kmer_status count_file_once(kmer_ctx *c, const char *path, kmer_result **out);
+
+}  // namespace
+
+kmer_status kmer_count_buffer(kmer_ctx *c, const uint8_t *bytes, size_t len, kmer_result **out) {
+    if (!c || !out || (!bytes && len)) return KMER_E_BAD_PARAM;
+    *out = nullptr;
+    if (!c->group.empty()) return group_count_buffer(c, bytes, len, out);
+    if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
+    return with_long_line_retry(c, [&] { return count_buffer_once(c, bytes, len, out); });
+}
+
 kmer_status kmer_count_file(kmer_ctx *c, const char *path, kmer_result **out) {
     if (!c || !path || !out) return KMER_E_BAD_PARAM;
     *out = nullptr;
     if (!c->group.empty()) return group_count_file(c, path, out);
+    return with_long_line_retry(c, [&] { return count_file_once(c, path, out); });
+}
+
+namespace {
+
+kmer_status count_file_once(kmer_ctx *c, const char *path, kmer_result **out) {
     FILE *f = fopen(path, "rb");
     if (!f) return fail(c, KMER_E_IO, std::string("cannot open ") + path);
     if (hipSetDevice(c->device) != hipSuccess) {
@@ -2088,6 +2152,8 @@ kmer_status kmer_count_file(kmer_ctx *c, const char *path, kmer_result **out) {
     }
     return finish(c, out);
 }
+
+}  // namespace
 
 kmer_status kmer_partial_device(kmer_ctx *c, const void **d_keys, const void **d_vals, uint64_t *n) {
     if (!c || !d_keys || !d_vals || !n) return KMER_E_BAD_PARAM;

@@ -18,7 +18,12 @@ constexpr int BH = 80;                   // back halo bytes (>= KMAX_TILE - 1 + 
 constexpr int KMAX_PACKED = 32;          // longest k of a 2-bit packed (u64) key
 constexpr int KMAX_TILE = 64;            // longest k handled by the tile kernel
 constexpr int KMAX_DENSE = 32;           // longest k packed into 2-bit codes
-constexpr uint32_t MAXREL = (1u << 23) - 1;  // longest sequence line (bytes - 1)
+constexpr uint32_t MAXREL = (1u << 23) - 1;  // longest sequence line (bytes - 1), default order-key layout
+// Order key = line << (pbits + 1) | strand << pbits | position field (pbits
+// bits).  Default 23 (lines up to 8 MiB, 2^40 lines); long-line mode 40
+// (lines up to 1 TiB, 2^23 lines) -- KMER_FLAG_LONG_LINES, or the automatic
+// retry of kmer_count_file / kmer_count_buffer.
+constexpr uint32_t PBITS_DEFAULT = 23, PBITS_LONG = 40;
 
 // error bits (device-side, OR-ed into ctx->d_err)
 enum : uint32_t {
@@ -146,6 +151,7 @@ struct HitArgs {
     uint64_t abs_offset;
     const StreamPos *pos;
     uint32_t packed;               // ACGT windows (k <= 32) are ranked packed keys
+    uint32_t pbits;                // order-key position bits (PBITS_*)
     uint64_t smask;                // suffix mask: 2*(k - |P|) bits
     uint64_t invalid_key;          // 2^(2*(k-|P|)): sorts after every real key
     uint64_t out_base;             // session hits before this chunk
@@ -236,6 +242,7 @@ struct WindowArgs {
     const SeqLine *lines;
     const unsigned long long *n_lines;
     uint32_t k, step, plen;
+    uint32_t pbits;                // order-key position bits (PBITS_*)
     const uint8_t *P;              // device copy of the prefix
     Record *recs;
     unsigned long long *rec_count;
@@ -255,6 +262,7 @@ struct WinArgs {
     uint64_t li0;                  // line index of the chunk's first line
     const uint64_t *wbase;         // by sequence ordinal: rank of the line's first window (chunk-relative)
     uint32_t k, plen;
+    uint32_t pbits;                // order-key position bits (PBITS_*)
     uint64_t pcode, rcode;         // P and rc(P) as 2-bit codes (first base most significant)
     uint64_t smask, invalid_key;
     uint64_t out_base;
@@ -290,7 +298,7 @@ hipError_t launch_cross_sort_small(const uint32_t *slot, const uint64_t *ord, co
                                    uint64_t *rkey, uint32_t *rkey32, uint64_t *rord, hipStream_t s);
 constexpr uint64_t XSMALL_MAX = 16384;   // cross lists up to this size: one-workgroup sort
 hipError_t launch_cross_segsort(uint64_t *ord, uint64_t *key, const uint32_t *slot, uint64_t n, uint64_t *rkey,
-                                uint32_t *rkey32, uint64_t *rord, hipStream_t s);
+                                uint32_t *rkey32, uint64_t *rord, uint32_t pbits, hipStream_t s);
 hipError_t launch_heads(const uint64_t *skey, const uint32_t *srank, uint64_t n, uint64_t invalid_key,
                         const uint64_t *rcnt, HeadRec *hrec, uint32_t *hcnt, hipStream_t s);
 // sort finish without per-entry counts: hcnt prefilled with 1, only groups of >= 2 and invalid keys written
@@ -332,7 +340,7 @@ hipError_t launch_nl_count(const uint8_t *data, uint64_t len, uint32_t n_tiles, 
 hipError_t launch_nl_write(const uint8_t *data, uint64_t len, uint32_t n_tiles, const uint64_t *tbase, uint64_t *nl,
                            hipStream_t s);
 hipError_t launch_seq_lines(const uint64_t *nl, uint64_t n_nl, uint64_t len, uint64_t li0, uint64_t n_seq, uint32_t k,
-                            SeqLine *lines, uint64_t *wcount, unsigned int *err, hipStream_t s);
+                            SeqLine *lines, uint64_t *wcount, unsigned int *err, uint64_t maxrel, hipStream_t s);
 hipError_t launch_pos_after(StreamPos *pos, uint64_t lines, const uint8_t *data, uint64_t len,
                             unsigned long long *ends_open, hipStream_t s);
 hipError_t launch_windows_packed(const WinArgs &a, hipStream_t s);
@@ -406,6 +414,7 @@ struct TabFinal {
     uint32_t canonical;            // statistics of the canonical-k-mer view (KMER_FLAG_CANONICAL)
     uint64_t inv;                  // inverse of TAB_MUL mod 2^64 (tab_mix^-1)
     unsigned long long *stats;     // [0] canonical entries [1] Map keys [2] sum of Map counts
+    uint64_t *prof;                // experiments only (KMERHIP_TAB_PROF): per-workgroup phase clocks, 8 each
 };
 
 constexpr uint64_t TAB_PIECE = 4096;                   // windows per piece of a long line (pass 1)

@@ -1026,7 +1026,7 @@ __global__ __launch_bounds__(TPB) void scan_planes_kernel(ScanArgs a, PlaneArgs 
 
 // Resolve one hit: global line index / line start from the tile scans, the
 // reference's sequence-line rule (lib/kmers.js:151-155), first-occurrence
-// order key (line << 24 | strand << 23 | strand ? MAXREL - rel : rel).
+// order key (line << (pbits + 1) | strand << pbits | strand ? maxrel - rel : rel).
 // Returns the packed key (invalid_key when the hit does not count as a packed
 // key: non-sequence line, or a record) and writes records for exotic windows
 // / record mode.  *lk = order of the hit among its tile's hits (local).
@@ -1044,11 +1044,13 @@ __device__ __forceinline__ uint64_t resolve_hit(const HitArgs &a, const HitRec &
     const uint64_t sabs = tile_abs + (uint64_t)(int64_t)s0;
     uint64_t rel = sabs - lstart;
     const bool seq = (li & 3) == 1;
-    if (rel > MAXREL) {
+    const uint64_t maxrel = (1ull << a.pbits) - 1ull;
+    if (rel > maxrel) {
         if (seq) atomicOr(a.err, ERR_LINE_TOO_LONG);
-        rel = MAXREL;                            // (non-sequence lines only need a consistent order)
+        rel = maxrel;                            // (non-sequence lines only need a consistent order)
     }
-    const uint64_t order = (li << 24) | ((uint64_t)strand << 23) | (strand ? (uint64_t)(MAXREL - rel) : rel);
+    if (li >> (63 - a.pbits)) atomicOr(a.err, ERR_LINE_TOO_LONG);   // (line field full: long-line mode)
+    const uint64_t order = (li << (a.pbits + 1)) | ((uint64_t)strand << a.pbits) | (strand ? maxrel - rel : rel);
     *order_out = order;
     const uint32_t sp = (uint32_t)(s0 + 64);     // < 2^15
     *lk = (r.c_local << 17) | (strand << 16) | (strand ? 0xFFFFu - sp : sp);
@@ -1389,7 +1391,7 @@ __global__ __launch_bounds__(256) void windows_kernel(WindowArgs a) {
         const uint8_t *line = a.data + sl.start;
         const uint64_t L = sl.len;
         const uint64_t nwin = L - k + 1;       // sl.len >= k guaranteed
-        if (nwin - 1 > MAXREL) {
+        if (nwin - 1 > (1ull << a.pbits) - 1ull || (sl.line_index >> (63 - a.pbits))) {
             if (threadIdx.x == 0) atomicOr(a.err, ERR_LINE_TOO_LONG);
             continue;
         }
@@ -1409,7 +1411,7 @@ __global__ __launch_bounds__(256) void windows_kernel(WindowArgs a) {
                 unsigned long long n = atomicAdd(a.rec_count, 1ull);
                 if (n < a.rec_cap) {
                     Record r;
-                    r.order = (sl.line_index << 24) | ((uint64_t)strand << 23) | j;
+                    r.order = (sl.line_index << (a.pbits + 1)) | ((uint64_t)strand << a.pbits) | j;
                     r.pos = strand ? sl.start + (L - hi) : sl.start + lo;
                     r.len = (uint32_t)klen;
                     r.strand = strand;
@@ -1557,7 +1559,8 @@ __global__ __launch_bounds__(256) void nl_write_kernel(const uint8_t *data, uint
 // sequence ordinal m -> SeqLine (len 0: no windows) and its window count 2W
 __global__ __launch_bounds__(256) void seq_lines_kernel(const uint64_t *nl, uint64_t n_nl, uint64_t len,
                                                         uint64_t li0, uint64_t n_seq, uint32_t k, SeqLine *lines,
-                                                        uint64_t *wcount, unsigned int *err) {
+                                                        uint64_t *wcount, unsigned int *err, uint64_t maxrel) {
+    const uint32_t lsh = 64 - __popcll(maxrel);            // line index bits: 63 - pbits
     const uint64_t first = (1u - (uint32_t)li0) & 3u;      // first sequence line, relative to li0
     for (uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; m < n_seq; m += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t r = first + 4 * m;                  // line index - li0
@@ -1574,7 +1577,8 @@ __global__ __launch_bounds__(256) void seq_lines_kernel(const uint64_t *nl, uint
                 sl.start = st;
                 sl.len = L;
                 const uint64_t W = L - k + 1;
-                if (err && W - 1 > MAXREL) atomicOr(err, ERR_LINE_TOO_LONG);   // (null: no order key, no limit)
+                // (err null: no order key, no limit)
+                if (err && (W - 1 > maxrel || (sl.line_index >> (lsh - 1)))) atomicOr(err, ERR_LINE_TOO_LONG);
                 w2 = 2 * W;
             }
         }
@@ -1600,15 +1604,16 @@ __global__ __launch_bounds__(256) void windows_packed_kernel(WinArgs a) {
         const SeqLine sl = a.lines[li];          // dense by sequence ordinal
         if (sl.len == 0) continue;
         const uint64_t W = sl.len - k + 1;
-        if (W - 1 > MAXREL) continue;            // reported by seq_lines_kernel
+        const uint64_t maxrel = (1ull << a.pbits) - 1ull;
+        if (W - 1 > maxrel) continue;            // reported by seq_lines_kernel
         const uint64_t base = a.out_base + a.wbase[li];
-        const uint64_t lo = sl.line_index << 24;
+        const uint64_t lo = sl.line_index << (a.pbits + 1);
         for (uint64_t s = threadIdx.x; s < W; s += blockDim.x) {
             const uint64_t pos = sl.start + s;
             bool exotic;
             const uint64_t code = window_code(a.data + pos, k, pos + k + 4 <= a.len, &exotic);
             const uint64_t rc = revcomp_code(code, k);
-            const uint64_t of = lo | s, orr = lo | (1ull << 23) | (uint64_t)(MAXREL - s);
+            const uint64_t of = lo | s, orr = lo | (1ull << a.pbits) | (maxrel - s);
             // prefix tests on the codes: a non-ACGT byte in the prefix bases never
             // matches (its code aliases, so exotic windows re-check the bytes)
             bool mf = plen == 0 || (code >> tailbits) == a.pcode;
@@ -1702,12 +1707,12 @@ __global__ __launch_bounds__(1024) void cross_sort_small_kernel(const uint32_t *
 // then the scatter to the natural slots.
 __global__ __launch_bounds__(256) void cross_segsort_kernel(uint64_t *ord, uint64_t *key, const uint32_t *slot,
                                                             uint64_t n, uint64_t *rkey, uint32_t *rkey32,
-                                                            uint64_t *rord) {
+                                                            uint64_t *rord, uint32_t lsh) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t line = ord[i] >> 24;      // (the line bits of a segment never change while it is sorted)
-        if (i > 0 && (ord[i - 1] >> 24) == line) continue;
+        const uint64_t line = ord[i] >> lsh;     // (the line bits of a segment never change while it is sorted)
+        if (i > 0 && (ord[i - 1] >> lsh) == line) continue;
         uint64_t e = i + 1;
-        while (e < n && (ord[e] >> 24) == line) ++e;
+        while (e < n && (ord[e] >> lsh) == line) ++e;
         for (uint64_t j = i + 1; j < e; ++j) {
             const uint64_t v = ord[j], kv = key[j];
             uint64_t p = j;
@@ -2307,9 +2312,9 @@ hipError_t launch_cross_sort_small(const uint32_t *slot, const uint64_t *ord, co
     return hipGetLastError();
 }
 hipError_t launch_cross_segsort(uint64_t *ord, uint64_t *key, const uint32_t *slot, uint64_t n, uint64_t *rkey,
-                                uint32_t *rkey32, uint64_t *rord, hipStream_t s) {
+                                uint32_t *rkey32, uint64_t *rord, uint32_t pbits, hipStream_t s) {
     if (n) hipLaunchKernelGGL(cross_segsort_kernel, dim3(grid_for(n)), dim3(256), 0, s, ord, key, slot, n, rkey, rkey32,
-                              rord);
+                              rord, pbits + 1);
     return hipGetLastError();
 }
 hipError_t launch_heads(const uint64_t *skey, const uint32_t *srank, uint64_t n, uint64_t invalid_key,
@@ -2404,10 +2409,10 @@ hipError_t launch_nl_write(const uint8_t *data, uint64_t len, uint32_t n_tiles, 
     return hipGetLastError();
 }
 hipError_t launch_seq_lines(const uint64_t *nl, uint64_t n_nl, uint64_t len, uint64_t li0, uint64_t n_seq, uint32_t k,
-                            SeqLine *lines, uint64_t *wcount, unsigned int *err, hipStream_t s) {
+                            SeqLine *lines, uint64_t *wcount, unsigned int *err, uint64_t maxrel, hipStream_t s) {
     if (n_seq)
         hipLaunchKernelGGL(seq_lines_kernel, dim3(grid_for(n_seq)), dim3(256), 0, s, nl, n_nl, len, li0, n_seq, k, lines,
-                           wcount, err);
+                           wcount, err, maxrel);
     return hipGetLastError();
 }
 hipError_t launch_pos_after(StreamPos *pos, uint64_t lines, const uint8_t *data, uint64_t len,

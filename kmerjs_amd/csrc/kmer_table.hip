@@ -456,6 +456,20 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
     const uint32_t q0 = blockIdx.x * per, q1 = q0 + per < TAB_NQ ? q0 + per : TAB_NQ;
     uint64_t st_canon = 0, st_keys = 0, st_sum = 0;
     uint64_t kn[TAB_KPT];
+    // (experiments: phase clocks of wave 0, 100 MHz, in a -DTAB_PROF build only)
+#ifdef TAB_PROF
+    const bool prof = a.prof != nullptr && t == 0;
+#else
+    constexpr bool prof = false;
+#endif
+    uint64_t pt[6] = {0, 0, 0, 0, 0, 0}, tm = prof ? wall_clock64() : 0;
+    auto mark = [&](int p) {
+        if (prof) {
+            const uint64_t x = wall_clock64();
+            pt[p] += x - tm;
+            tm = x;
+        }
+    };
     // a bucket's keys, as remainders (lanes past its end re-read its first key
     // and are masked at use): unconditional loads, all in flight together
     auto load_keys = [&](uint64_t s0x, uint64_t nx) {
@@ -491,6 +505,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
         if (n == 0) {
             if (t == 0) a.nd[q] = 0;
             if (more) load_keys(s0n, nn);
+            mark(5);
             continue;
         }
         if (n >= (1ull << 32) && t == 0) atomicOr(a.err, ERR_COUNT_OVERFLOW);   // (u32 counts)
@@ -507,6 +522,9 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
         }
 #pragma unroll
         for (int j = 0; j < TAB_KPT; ++j) kn[j] &= TAB_RMASK;
+        if (prof)
+            for (int j = 0; j < TAB_KPT; ++j) asm volatile("" ::"v"(kn[j]));   // (clock after the key loads)
+        mark(0);
         while (true) {
             __syncthreads();
             const uint32_t top = sp;
@@ -519,6 +537,8 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
                 ovf = 0;
             }
             __syncthreads();
+            mark(1);
+            if (prof) pt[4] += 1ull << 32;       // ranges
             if (inreg) {
                 uint32_t pend = 0;
                 const int left = (int)n - (int)t;
@@ -546,6 +566,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
             __syncthreads();
             if (t == 0 && occ > a.cap) ovf = 1u;     // more distinct keys than the range may hold
             __syncthreads();
+            mark(2);
             if (ovf) {
                 for (uint32_t i = t; i < TAB_SLOTS; i += TAB_FWG) {
                     tkey[i] = TAB_EMPTY;
@@ -619,9 +640,13 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
                     st_sum += (fs ? (pal ? 2 * cnt : cnt) : 0) + (rs ? cnt : 0);
                 }
             }
+            mark(3);
         }
         if (t == 0) a.nd[q] = nout;
+        if (prof) pt[4] += 1;                    // buckets
     }
+    if (prof)
+        for (int i = 0; i < 6; ++i) a.prof[blockIdx.x * 8 + i] = pt[i];
     // workgroup totals -> one atomic per wave
     for (int d = 32; d >= 1; d >>= 1) {
         st_canon += __shfl_xor(st_canon, d);

@@ -48,6 +48,11 @@ def test_two_pass_mode_matches(native, golden, inputs):
     assert not bad, bad[:5]
 
 
+def test_long_line_mode_matches(native, golden, inputs):
+    # long-line order keys (40-bit position field) must not change any result
+    assert not _run_cases(native, golden, inputs, flags=native.FLAG_LONG_LINES)
+
+
 def test_record_path_matches(native, golden, inputs):
     bad = _run_cases(native, golden, inputs, flags=native.FLAG_NO_DENSE,
                      select=lambda c: c["prefix"] == "ATGAC" and c["step"] == 1)

@@ -1,0 +1,62 @@
+"""Sequence lines longer than 2^23 bytes on the ordered paths (long-line
+mode, KMER_FLAG_LONG_LINES / the automatic retry of kmer_count_file and
+kmer_count_buffer): the reference has no line limit (lib/kmers.js:88-100), so
+a 12 MB contig must count exactly like the oracle, in Map order, on every
+ordered path (tile scan + packed keys, dense hits, tile records, general)."""
+import numpy as np
+import pytest
+
+from tests.util import first_diff
+
+pytestmark = pytest.mark.gpu
+
+
+def _contig_input(seed, n_big=12_000_000):
+    rng = np.random.default_rng(seed)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    big = acgt[rng.integers(0, 4, size=n_big)]
+    big[rng.integers(0, n_big, size=50)] = ord("N")            # a few exotic windows
+    small = acgt[rng.integers(0, 4, size=150)].tobytes()
+    return (b">contig1\n" + big.tobytes() + b"\n+\nIIII\n" + b"@r2\n" + small + b"\n+\n" + b"I" * 150 + b"\n")
+
+
+@pytest.fixture(scope="module")
+def data():
+    return _contig_input(21)
+
+
+@pytest.mark.parametrize("k,prefix,step", [(21, b"ATGAC", 1), (21, b"AT", 1), (21, b"", 1), (21, b"ANG", 1),
+                                           (21, b"ACG", 2)])
+def test_long_contig_matches_oracle(data, k, prefix, step, tmp_path):
+    from kmerjs_amd import _native
+    from oracle import oracle
+    want = oracle.count_buffer(data, prefix, k, step)
+    c = _native.Counter(k=k, prefix=prefix, step=step)
+    got = c.count_buffer(data).entries()                 # retried in long-line mode
+    assert len(got) == len(want)
+    assert first_diff(got, want) is None
+    p = tmp_path / "contig.fastq"
+    p.write_bytes(data)
+    got2 = c.count_file(str(p)).entries()
+    assert first_diff(got2, want) is None
+    c.close()
+
+
+def test_device_feed_needs_the_flag(data):
+    import torch
+    from kmerjs_amd import _native
+    from oracle import oracle
+    buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    c = _native.Counter(k=21, prefix=b"ATGAC")
+    c.reset()
+    with pytest.raises(_native.KmerError) as e:
+        c.feed_device(buf.data_ptr(), buf.numel())
+        c.finish()
+    assert e.value.status == 7
+    c.close()
+    c = _native.Counter(k=21, prefix=b"ATGAC", flags=_native.FLAG_LONG_LINES)
+    c.reset()
+    c.feed_device(buf.data_ptr(), buf.numel())
+    got = c.finish().entries()
+    c.close()
+    assert first_diff(got, oracle.count_buffer(data, b"ATGAC", 21, 1)) is None
