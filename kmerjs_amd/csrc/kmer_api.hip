@@ -1086,6 +1086,7 @@ kmer_status table_finish(kmer_ctx *c) {
     uint64_t range_keys = 3000;               // mean keys per LDS range (load ~0.37: short probes; measured best at C3)
     if (const char *rk = getenv("KMERHIP_TAB_RANGE")) range_keys = std::max<uint64_t>(64, strtoull(rk, nullptr, 10));
     while (f.sub_bits < 16 && (mean >> f.sub_bits) > range_keys) ++f.sub_bits;
+    f.range_keys = (uint32_t)std::min<uint64_t>(range_keys, TAB_CAP);
     f.cap = (c->p.flags & KMER_FLAG_TABLE_SPLIT_TEST) ? 64 : TAB_CAP;
     if (const char *ab = getenv("KMERHIP_TAB_ABLATE")) f.ablate = (uint32_t)atoi(ab);   // experiments only
     f.big = c->tbig.p;

@@ -403,7 +403,8 @@ struct TabFinal {
     const uint64_t *start;         // TAB_NQ + 1 bucket starts in B2 (and in out)
     uint64_t *out;                 // per bucket: nd[q] entries (rem << 20 | min(count, TAB_CMAX))
     uint32_t *nd;
-    uint32_t sub_bits;             // initial split of a bucket's remainder range
+    uint32_t sub_bits;             // (unused: ranges are sized per unit from range_keys)
+    uint32_t range_keys;           // target keys per LDS range (small buckets are grouped up to it)
     uint32_t cap;                  // claims per range before it is split (<= TAB_CAP)
     uint32_t ablate;               // experiments only (results WRONG): 1 no insert, 2 no emit
     TabBig *big;

@@ -434,26 +434,36 @@ constexpr int TAB_KPT = 12;                   // bucket keys held per thread (re
 constexpr uint32_t TAB_REG_MAX = TAB_KPT * TAB_FWG;
 constexpr uint32_t TAB_SC = 1024;             // bucket starts cached in LDS per refill
 
-// final: each workgroup merges a contiguous range of buckets, one at a time,
-// in an LDS hash table; entries (remainder, count) go to `out` at the
-// bucket's start, the distinct count to nd[q], Map statistics on the fly.
+// final: each workgroup merges a contiguous range of buckets in an LDS hash
+// table, one UNIT at a time: a run of consecutive small buckets whose keys
+// together fit one LDS range (<= range_keys), or one large bucket split into
+// 2^sb remainder ranges.  A key enters the table as h - (first bucket of the
+// unit << 44) = (bucket offset << 44) | remainder (offset < 64, so never the
+// empty marker).  Entries (remainder, count) go to `out` at their bucket's
+// start, the distinct count to nd[q], the Map statistics on the fly.
 // Latency: bucket starts come from an LDS cache refilled every 1024 buckets;
-// a bucket of <= 12 K keys is held in registers (12 per thread), and the next
-// bucket's keys are loaded as soon as the current one's last range is merged,
+// a unit of <= 12 K keys is held in registers (12 per thread), and the next
+// unit's keys are loaded as soon as the current one's last range is merged,
 // in flight while it is emitted.  Larger buckets (repeated keys, inputs
 // beyond ~130 M reads) stream from HBM once per range.  The table is clean
-// between buckets: emission clears the slots it reads.
+// between ranges: emission clears the slots it reads.  Grouping small buckets
+// divides the per-range fixed cost (barriers, key latency, the slot scan) by
+// the group size (canonical C5: ~1 K keys per bucket).
+constexpr uint32_t TAB_GMAX = 64;             // buckets per unit
+
 __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
     __shared__ uint64_t tkey[TAB_SLOTS];
     __shared__ uint32_t tcnt[TAB_SLOTS];
-    __shared__ uint64_t stk[2 * 64];          // range stack [lo, hi) of remainders
+    __shared__ uint64_t stk[2 * 64];          // range stack [lo, hi) of unit keys
     __shared__ uint64_t sc[TAB_SC + 2];       // start[cbase .. cbase + TAB_SC + 1]
-    __shared__ uint32_t occ, nout, sp, ovf;
+    __shared__ uint32_t nout[TAB_GMAX];       // entries emitted per bucket of the unit
+    __shared__ uint32_t occ, sp, ovf;
     const uint32_t t = threadIdx.x, lane = t & 63;
     const uint32_t k = a.k;
     const uint32_t kmask = k >= 32 ? ~0u : ((1u << k) - 1u), sh = 32 - k;
     const uint32_t per = (TAB_NQ + gridDim.x - 1) / gridDim.x;
     const uint32_t q0 = blockIdx.x * per, q1 = q0 + per < TAB_NQ ? q0 + per : TAB_NQ;
+    const uint64_t rk = a.range_keys;
     uint64_t st_canon = 0, st_keys = 0, st_sum = 0;
     uint64_t kn[TAB_KPT];
     // (experiments: phase clocks of wave 0, 100 MHz, in a -DTAB_PROF build only)
@@ -470,8 +480,8 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
             tm = x;
         }
     };
-    // a bucket's keys, as remainders (lanes past its end re-read its first key
-    // and are masked at use): unconditional loads, all in flight together
+    // a unit's keys (lanes past its end re-read its first key and are masked
+    // at use): unconditional loads, all in flight together
     auto load_keys = [&](uint64_t s0x, uint64_t nx) {
         if (nx - 1 < (uint64_t)TAB_REG_MAX) {
             // (lane tests as t < nx - 1024 j: immediates, no per-j index registers)
@@ -486,42 +496,68 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
         for (uint32_t i = t; i < TAB_SC + 2; i += TAB_FWG) sc[i] = a.start[cb + i < TAB_NQ ? cb + i : TAB_NQ];
         __syncthreads();
     };
+    uint32_t cbase = q0;
+    // the unit starting at bucket u: its end (uniform over the workgroup; the
+    // start cache must hold u's start, i.e. u <= cbase + TAB_SC)
+    auto unit_end = [&](uint32_t u) -> uint32_t {
+        uint32_t e = u + 1;
+        uint64_t tot = sc[u + 1 - cbase] - sc[u - cbase];
+        if (tot > rk) return e;
+        while (e < q1 && e - cbase < TAB_SC && e - u < TAB_GMAX) {
+            const uint64_t ne = sc[e + 1 - cbase] - sc[e - cbase];
+            if (tot + ne > rk) break;
+            tot += ne;
+            ++e;
+        }
+        return e;
+    };
     for (uint32_t i = t; i < TAB_SLOTS; i += TAB_FWG) {
         tkey[i] = TAB_EMPTY;
         tcnt[i] = 0;
     }
-    uint32_t cbase = q0;
     refill(cbase);
-    if (q0 < q1) load_keys(sc[0], sc[1] - sc[0]);
-    for (uint32_t q = q0; q < q1; ++q) {
-        if (q - cbase == TAB_SC) {
+    uint32_t q = q0, qe = q0 < q1 ? unit_end(q0) : q0;
+    if (q0 < q1) load_keys(sc[0], sc[qe - cbase] - sc[0]);
+    while (q < q1) {
+        if (q - cbase >= TAB_SC) {
             cbase = q;
             refill(cbase);
         }
-        const uint64_t s0 = sc[q - cbase], n = sc[q - cbase + 1] - s0;
-        const uint64_t s0n = sc[q - cbase + 1], nn = sc[q - cbase + 2] - s0n;   // bucket q + 1
-        const bool more = q + 1 < q1;
+        const uint32_t g = qe - q;                        // buckets in the unit
+        const uint64_t s0 = sc[q - cbase], n = sc[qe - cbase] - s0;
+        const uint64_t qbase = (uint64_t)q << TAB_RBITS;
+        // the next unit (its keys are loaded while this one is emitted)
+        const uint32_t qn = qe, qne = qn < q1 ? unit_end(qn) : qn;
+        const bool more = qn < q1;
+        const uint64_t s0n = more ? sc[qn - cbase] : 0, nn = more ? sc[qne - cbase] - s0n : 0;
         const bool inreg = n <= TAB_REG_MAX;
         if (n == 0) {
-            if (t == 0) a.nd[q] = 0;
+            for (uint32_t i = t; i < g; i += TAB_FWG) a.nd[q + i] = 0;
             if (more) load_keys(s0n, nn);
             mark(5);
+            q = qn;
+            qe = qne;
             continue;
         }
         if (n >= (1ull << 32) && t == 0) atomicOr(a.err, ERR_COUNT_OVERFLOW);   // (u32 counts)
-        __syncthreads();                         // the previous bucket is done with the LDS state
+        __syncthreads();                         // the previous unit is done with the LDS state
         if (t == 0) {
-            const uint32_t nsub = 1u << a.sub_bits;
-            const uint64_t w = (1ull << TAB_RBITS) >> a.sub_bits;
+            // a group: one range over its keys; a large bucket: 2^sb remainder ranges
+            // (<= 16 initial ranges: the stack holds 64, and a range with more
+            // distinct keys than the table takes is split on demand)
+            uint32_t sb = 0;
+            while (g == 1 && sb < 4 && (n >> sb) > rk) ++sb;
+            const uint32_t nsub = 1u << sb;
+            const uint64_t w = ((uint64_t)g << TAB_RBITS) >> sb;
             for (uint32_t i = 0; i < nsub; ++i) {      // popped in ascending order
                 stk[2 * i] = (uint64_t)(nsub - 1 - i) * w;
                 stk[2 * i + 1] = (uint64_t)(nsub - i) * w;
             }
             sp = nsub;
-            nout = 0;
         }
+        for (uint32_t i = t; i < g; i += TAB_FWG) nout[i] = 0;
 #pragma unroll
-        for (int j = 0; j < TAB_KPT; ++j) kn[j] &= TAB_RMASK;
+        for (int j = 0; j < TAB_KPT; ++j) kn[j] -= qbase;
         if (prof)
             for (int j = 0; j < TAB_KPT; ++j) asm volatile("" ::"v"(kn[j]));   // (clock after the key loads)
         mark(0);
@@ -549,14 +585,14 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
                 // without spilling the held keys)
                 uint32_t cl = 0;
 #pragma unroll
-                for (int g = 0; g < TAB_KPT; g += 4) cl += tab_insert_grp<4>(tkey, tcnt, kn, g, pend, &ovf);
+                for (int gi = 0; gi < TAB_KPT; gi += 4) cl += tab_insert_grp<4>(tkey, tcnt, kn, gi, pend, &ovf);
                 for (int d = 32; d >= 1; d >>= 1) cl += __shfl_xor(cl, d);
                 if (lane == 0 && cl) atomicAdd(&occ, cl);
             } else {
                 const uint64_t *src = a.B2 + s0;
                 for (uint64_t i = t; i < n; i += TAB_FWG) {
                     if (lds_flag(&ovf)) break;
-                    uint64_t r1[1] = {src[i] & TAB_RMASK};
+                    uint64_t r1[1] = {src[i] - qbase};
                     if (r1[0] >= rlo && r1[0] < rhi) {
                         uint32_t cl = tab_insert_grp<1>(tkey, tcnt, r1, 0, 1u, &ovf);
                         if (cl) atomicAdd(&occ, cl);
@@ -586,26 +622,47 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
                 }
                 continue;
             }
-            // the bucket's last range is merged: load the next bucket's keys
-            // now, in flight while this one is emitted
+            // the unit's last range is merged: load the next unit's keys now,
+            // in flight while this one is emitted
             if (top == 1 && more) load_keys(s0n, nn);
-            // emit (and clear) the occupied slots, one LDS counter bump per wave and pass
+            // emit (and clear) the occupied slots: per wave, one LDS counter
+            // bump per bucket present among the wave's entries
 #pragma unroll 1
             for (uint32_t i = t; i < TAB_SLOTS && !(a.ablate & 2); i += TAB_FWG) {
-                const uint64_t rem = tkey[i];
-                const bool v = rem != TAB_EMPTY;
-                const uint64_t m = __ballot(v);
+                const uint64_t key = tkey[i];
+                const bool v = key != TAB_EMPTY;
+                uint64_t m = __ballot(v);
                 if (!m) continue;
-                uint32_t base = 0;
-                if (lane == (uint32_t)(__ffsll((long long)m) - 1)) base = atomicAdd(&nout, (uint32_t)__popcll(m));
-                base = __shfl(base, __ffsll((long long)m) - 1);
+                const uint32_t ql = v ? (uint32_t)(key >> TAB_RBITS) : 0u;
+                uint32_t pos = 0;
+                uint64_t obase = s0;
+                if (g == 1) {                            // (uniform) one bucket: one counter bump per wave
+                    const int ld = __ffsll((long long)m) - 1;
+                    uint32_t base = 0;
+                    if (lane == (uint32_t)ld) base = atomicAdd(&nout[0], (uint32_t)__popcll(m));
+                    base = (uint32_t)__shfl((int)base, ld);
+                    pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                } else {
+                    while (m) {                          // one pass per distinct bucket in the wave
+                        const int ld = __ffsll((long long)m) - 1;
+                        const uint32_t qx = (uint32_t)__shfl((int)ql, ld);
+                        const uint64_t mq = __ballot(v && ql == qx);
+                        uint32_t base = 0;
+                        if (lane == (uint32_t)ld) base = atomicAdd(&nout[qx], (uint32_t)__popcll(mq));
+                        base = (uint32_t)__shfl((int)base, ld);
+                        if (v && ql == qx) pos = base + (uint32_t)__popcll(mq & ((1ull << lane) - 1ull));
+                        m &= ~mq;
+                    }
+                    if (v) obase = sc[q + ql - cbase];
+                }
                 if (!v) continue;
-                const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                const uint64_t rem = key & TAB_RMASK;
                 const uint64_t cnt = tcnt[i];
                 tkey[i] = TAB_EMPTY;
                 tcnt[i] = 0;
-                a.out[s0 + pos] = (rem << 20) | (cnt < TAB_CMAX ? cnt : TAB_CMAX);
-                const uint64_t h = ((uint64_t)q << TAB_RBITS) | rem;
+                const uint32_t qq = q + ql;
+                a.out[obase + pos] = (rem << 20) | (cnt < TAB_CMAX ? cnt : TAB_CMAX);
+                const uint64_t h = ((uint64_t)qq << TAB_RBITS) | rem;
                 if (cnt >= TAB_CMAX) {
                     const unsigned long long bi = atomicAdd(a.big_count, 1ull);
                     if (bi < a.big_cap) {
@@ -642,8 +699,11 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
             }
             mark(3);
         }
-        if (t == 0) a.nd[q] = nout;
-        if (prof) pt[4] += 1;                    // buckets
+        // (the range loop left after a barrier: every emission bump is in nout)
+        for (uint32_t i = t; i < g; i += TAB_FWG) a.nd[q + i] = nout[i];
+        if (prof) pt[4] += g;                        // buckets
+        q = qn;
+        qe = qne;
     }
     if (prof)
         for (int i = 0; i < 6; ++i) a.prof[blockIdx.x * 8 + i] = pt[i];
