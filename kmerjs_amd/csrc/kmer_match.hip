@@ -72,6 +72,28 @@ struct Temp {
     }
 };
 
+// grow-only device array (buffers are reused by the next match on the DB)
+template <typename T>
+struct DArr {
+    T *p = nullptr;
+    uint64_t cap = 0;
+    hipError_t ensure(uint64_t n) {
+        n = std::max<uint64_t>(n, 1);
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc((void **)&p, std::max(n, cap + cap / 2) * sizeof(T));
+        if (e == hipSuccess) cap = std::max(n, cap + cap / 2);
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
 #define MROC(tmp, CALL)                       \
     do {                                      \
         size_t b = 0;                         \
@@ -149,20 +171,37 @@ __global__ void db_csr_kernel(const uint64_t *c, const uint32_t *t, uint64_t n, 
     }
 }
 
+// dir[p] = first U index whose code >> dsh is >= (dlo >> dsh) + p (p = 0 .. np)
+__global__ void db_dir_kernel(const uint64_t *U, uint64_t m, uint64_t dlo, uint32_t dsh, uint64_t np, uint32_t *dir) {
+    for (uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; p <= np; p += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t cell = (dlo >> dsh) + p;
+        uint64_t lo = 0, hi = m;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if ((U[mid] >> dsh) < cell) lo = mid + 1;
+            else hi = mid;
+        }
+        dir[p] = (uint32_t)lo;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // query kernels
 // ---------------------------------------------------------------------------
-// pack + binary search: qidx = DB k-mer index or NONE, hc = its list length
+// pack + directory + binary search: qidx = DB k-mer index or NONE, hc = its
+// list length.  The directory cell of a code (its bits above dsh, relative to
+// the smallest DB code) bounds the search to a few entries.
 __global__ void q_lookup_kernel(const uint8_t *keys, const uint64_t *offs, uint32_t klen, uint64_t n, uint32_t k,
-                                const uint64_t *U, uint64_t m, const uint64_t *O, uint32_t *qidx, uint64_t *hc,
-                                uint32_t *present) {
+                                const uint64_t *U, uint64_t m, const uint64_t *O, const uint32_t *dir, uint64_t dlo,
+                                uint64_t dhi, uint32_t dsh, uint32_t *qidx, uint64_t *hc, uint32_t *present) {
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t b = offs ? offs[i] : i * klen;
         const uint64_t len = offs ? offs[i + 1] - b : klen;
         uint32_t idx = NONE;
         uint64_t code;
-        if (len == k && m && pack_key(keys + b, k, &code)) {
-            uint64_t lo = 0, hi = m;           // first U[j] >= code
+        if (len == k && m && pack_key(keys + b, k, &code) && code >= dlo && code <= dhi) {
+            const uint64_t p = (code >> dsh) - (dlo >> dsh);
+            uint64_t lo = dir[p], hi = dir[p + 1];      // first U[j] >= code, inside its directory cell
             while (lo < hi) {
                 const uint64_t mid = (lo + hi) >> 1;
                 if (U[mid] < code) lo = mid + 1;
@@ -176,16 +215,40 @@ __global__ void q_lookup_kernel(const uint8_t *keys, const uint64_t *offs, uint3
     }
 }
 
-// hits in (query, list) order as (template, query) pairs
-__global__ void q_emit_kernel(const uint32_t *qidx, const uint64_t *H, uint64_t n, const uint64_t *O,
-                              const uint32_t *T, uint32_t *pt, uint32_t *pq) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t idx = qidx[i];
-        if (idx == NONE) continue;
-        const uint64_t o = O[idx], len = O[idx + 1] - o, h = H[i];
-        for (uint64_t j = 0; j < len; ++j) {
-            pt[h + j] = T[o + j];
-            pq[h + j] = (uint32_t)i;
+// hits in (query, list) order as (template, query) pairs, load-balanced: a
+// wave takes 64 consecutive query keys and its lanes walk the wave's hits in
+// order (lane-strided), each finding its owner key by a 6-step search over
+// the lanes' hit offsets -- coalesced stores, no per-key loop imbalance.
+__global__ __launch_bounds__(256) void q_emit_kernel(const uint32_t *qidx, const uint64_t *H, uint64_t n,
+                                                     const uint64_t *O, const uint32_t *T, uint32_t *pt, uint32_t *pq) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint64_t w0 = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) & ~63ull; w0 < n;
+         w0 += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = w0 + lane;
+        const uint32_t idx = i < n ? qidx[i] : NONE;
+        const uint64_t o = idx == NONE ? 0 : O[idx], c = idx == NONE ? 0 : O[idx + 1] - o;
+        const uint64_t h = i < n ? H[i] : ~0ull;                // (past the end: never an owner)
+        uint64_t end = i < n ? h + c : 0;
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint64_t x = __shfl_xor(end, d);
+            end = x > end ? x : end;
+        }
+        const uint64_t start = __shfl(h, 0);
+        // (wave-uniform trip count: every lane takes part in the shuffles)
+        for (uint64_t r = start; r < end; r += 64) {
+            const uint64_t e = r + lane;
+            int lo = 0, hi = 63;                                // the last lane with h <= e owns e
+#pragma unroll
+            for (int it = 0; it < 6; ++it) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (__shfl(h, mid) <= e) lo = mid;
+                else hi = mid - 1;
+            }
+            const uint64_t hl = __shfl(h, lo), ol = __shfl(o, lo);
+            if (e < end) {
+                pt[e] = T[ol + (e - hl)];
+                pq[e] = (uint32_t)(w0 + (uint64_t)lo);
+            }
         }
     }
 }
@@ -301,6 +364,21 @@ uint32_t grid_for(uint64_t n, uint32_t block = 256, uint32_t cap = 65536) {
 
 }  // namespace
 
+// Per-match arrays; a closed match hands them to its DB for the next one.
+struct MatchBufs {
+    DArr<uint64_t> cnt, H, seg, t0, ct, scal;
+    DArr<uint32_t> qidx, present, sq, u0, cu, order, rank;
+    DArr<kmer_winner> dw;
+    kmer_winner *hw = nullptr;
+    void release() {
+        cnt.release(), H.release(), seg.release(), t0.release(), ct.release(), scal.release();
+        qidx.release(), present.release(), sq.release(), u0.release(), cu.release(), order.release(), rank.release();
+        dw.release();
+        if (hw) (void)hipHostFree(hw);
+        hw = nullptr;
+    }
+};
+
 struct kmer_db {
     int device = 0;
     uint32_t k = 0, nt = 0;
@@ -308,21 +386,35 @@ struct kmer_db {
     hipStream_t s = nullptr;
     uint64_t *U = nullptr, *O = nullptr;
     uint32_t *T = nullptr;
+    uint32_t *dir = nullptr;                   // directory over the codes' high bits
+    uint64_t dlo = ~0ull, dhi = 0;
+    uint32_t dsh = 0;
+    // scratch of a match build (matches of one DB are built one at a time)
+    DArr<uint8_t> qkeys;
+    DArr<uint64_t> qoffs, hc, fkey, fkey2;
+    DArr<uint32_t> pt, pt2, pq2, nhd;
+    Temp tmp;
+    MatchBufs spare;                           // buffers of the last closed match
+    bool has_spare = false;
 };
 
 struct kmer_match {
     kmer_db *db = nullptr;
     uint64_t n = 0, hits0 = 0;
     uint32_t nh = 0;
+    MatchBufs b;
     uint64_t *cnt = nullptr, *H = nullptr, *seg = nullptr, *t0 = nullptr, *ct = nullptr, *scal = nullptr;
     uint32_t *qidx = nullptr, *present = nullptr, *sq = nullptr, *u0 = nullptr, *cu = nullptr, *order = nullptr,
              *rank = nullptr;
     kmer_winner *dw = nullptr, *hw = nullptr;
     void release() {
-        for (void *p : {(void *)cnt, (void *)H, (void *)seg, (void *)t0, (void *)ct, (void *)scal, (void *)qidx,
-                        (void *)present, (void *)sq, (void *)u0, (void *)cu, (void *)order, (void *)rank, (void *)dw})
-            if (p) (void)hipFree(p);
-        if (hw) (void)hipHostFree(hw);
+        if (!db->has_spare) {                  // keep the buffers for the DB's next match
+            db->spare = b;
+            db->has_spare = true;
+        } else {
+            b.release();
+        }
+        b = MatchBufs();
     }
 };
 
@@ -334,6 +426,10 @@ void free_db(kmer_db *db) {
     if (db->U) (void)hipFree(db->U);
     if (db->O) (void)hipFree(db->O);
     if (db->T) (void)hipFree(db->T);
+    if (db->dir) (void)hipFree(db->dir);
+    db->qkeys.release(), db->qoffs.release(), db->hc.release(), db->fkey.release(), db->fkey2.release();
+    db->pt.release(), db->pt2.release(), db->pq2.release(), db->nhd.release();
+    if (db->has_spare) db->spare.release();
     if (db->s) (void)hipStreamDestroy(db->s);
     delete db;
 }
@@ -400,6 +496,17 @@ kmer_status build_db(kmer_db *db, const char *keys, uint64_t n, const uint64_t *
     hipLaunchKernelGGL(db_csr_kernel, dim3(grid_for(n)), dim3(256), 0, s, sc, stt, n, pos, db->U, db->O, db->T);
     MCHK(hipGetLastError());
     MCHK(hipMemcpyAsync(db->O + db->m, &db->entries, 8, hipMemcpyHostToDevice, s));
+    // directory: up to 2^20 cells over the bits below the codes' common prefix
+    MCHK(hipMemcpyAsync(&db->dlo, db->U, 8, hipMemcpyDeviceToHost, s));
+    MCHK(hipMemcpyAsync(&db->dhi, db->U + db->m - 1, 8, hipMemcpyDeviceToHost, s));
+    MCHK(hipStreamSynchronize(s));
+    const int span = bit_width64(db->dlo ^ db->dhi);
+    db->dsh = (uint32_t)std::max(0, span - 20);
+    const uint64_t np = (db->dhi >> db->dsh) - (db->dlo >> db->dsh) + 1;
+    MCHK(dalloc(&db->dir, np + 1));
+    hipLaunchKernelGGL(db_dir_kernel, dim3(grid_for(np + 1)), dim3(256), 0, s, db->U, db->m, db->dlo, db->dsh, np,
+                       db->dir);
+    MCHK(hipGetLastError());
     MCHK(hipStreamSynchronize(s));
     return KMER_OK;
 }
@@ -409,68 +516,55 @@ kmer_status match_build(kmer_match *m, const uint8_t *dkeys, const uint64_t *dof
     hipStream_t s = db->s;
     const uint64_t n = m->n;
     const uint32_t nt = db->nt;
-    Temp tmp;
-    uint32_t *pt = nullptr, *pt2 = nullptr, *pq2 = nullptr, *nhd = nullptr;
-    uint64_t *fkey = nullptr, *fkey2 = nullptr;
-    auto cleanup = [&]() {
-        for (void *p : {(void *)pt, (void *)pt2, (void *)pq2, (void *)nhd, (void *)fkey, (void *)fkey2})
-            if (p) (void)hipFree(p);
-    };
-    struct Guard {
-        decltype(cleanup) &f;
-        ~Guard() { f(); }
-    } guard{cleanup};
-    MCHK(dalloc(&m->qidx, n));
-    MCHK(dalloc(&m->present, n));
-    MCHK(dalloc(&m->H, n));
-    MCHK(dalloc(&m->seg, (uint64_t)nt + 1));
-    MCHK(dalloc(&m->u0, nt));
-    MCHK(dalloc(&m->cu, nt));
-    MCHK(dalloc(&m->t0, nt));
-    MCHK(dalloc(&m->ct, nt));
-    MCHK(dalloc(&m->order, nt));
-    MCHK(dalloc(&m->rank, nt));
-    MCHK(dalloc(&m->scal, 2));
-    MCHK(dalloc(&m->dw, 1));
-    MCHK(hipHostMalloc((void **)&m->hw, sizeof(kmer_winner), hipHostMallocDefault));
-    MCHK(dalloc(&nhd, 1));
-    MCHK(dalloc(&fkey, nt));
-    MCHK(dalloc(&fkey2, nt));
-    // hit counts per query key (m->H holds the counts, then their scan in place)
-    uint64_t *hc = nullptr;
-    MCHK(dalloc(&hc, n));
+    Temp &tmp = db->tmp;
+    MatchBufs &b = m->b;
+    MCHK(b.qidx.ensure(n));
+    MCHK(b.present.ensure(n));
+    MCHK(b.H.ensure(n));
+    MCHK(b.seg.ensure((uint64_t)nt + 1));
+    MCHK(b.u0.ensure(nt));
+    MCHK(b.cu.ensure(nt));
+    MCHK(b.t0.ensure(nt));
+    MCHK(b.ct.ensure(nt));
+    MCHK(b.order.ensure(nt));
+    MCHK(b.rank.ensure(nt));
+    MCHK(b.scal.ensure(2));
+    MCHK(b.dw.ensure(1));
+    if (!b.hw) MCHK(hipHostMalloc((void **)&b.hw, sizeof(kmer_winner), hipHostMallocDefault));
+    MCHK(db->nhd.ensure(1));
+    MCHK(db->fkey.ensure(nt));
+    MCHK(db->fkey2.ensure(nt));
+    MCHK(db->hc.ensure(n));
+    m->qidx = b.qidx.p, m->present = b.present.p, m->H = b.H.p, m->seg = b.seg.p, m->u0 = b.u0.p;
+    m->cu = b.cu.p, m->t0 = b.t0.p, m->ct = b.ct.p, m->order = b.order.p, m->rank = b.rank.p;
+    m->scal = b.scal.p, m->dw = b.dw.p, m->hw = b.hw;
+    uint32_t *nhd = db->nhd.p;
+    uint64_t *fkey = db->fkey.p, *fkey2 = db->fkey2.p, *hc = db->hc.p;
+    // hit counts per query key -> their exclusive scan
     hipLaunchKernelGGL(q_lookup_kernel, dim3(grid_for(n)), dim3(256), 0, s, dkeys, doffs, klen, n, db->k, db->U,
-                       db->m, db->O, m->qidx, hc, m->present);
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess) {
-        size_t b = 0;
-        e = rocprim::exclusive_scan(nullptr, b, hc, m->H, (uint64_t)0, (size_t)std::max<uint64_t>(n, 1),
-                                    rocprim::plus<uint64_t>(), s);
-        if (e == hipSuccess) e = tmp.ensure(b + 16);
-        if (e == hipSuccess && n)
-            e = rocprim::exclusive_scan(tmp.p, b, hc, m->H, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s);
-    }
+                       db->m, db->O, db->dir, db->dlo, db->dhi, db->dsh, m->qidx, hc, m->present);
+    MCHK(hipGetLastError());
+    if (n) MROC(tmp, rocprim::exclusive_scan(t, b, hc, m->H, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s));
     uint64_t tail[2] = {0, 0};
-    if (e == hipSuccess && n) e = hipMemcpyAsync(&tail[0], m->H + n - 1, 8, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess && n) e = hipMemcpyAsync(&tail[1], hc + n - 1, 8, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    (void)hipFree(hc);
-    MCHK(e);
+    if (n) MCHK(hipMemcpyAsync(&tail[0], m->H + n - 1, 8, hipMemcpyDeviceToHost, s));
+    if (n) MCHK(hipMemcpyAsync(&tail[1], hc + n - 1, 8, hipMemcpyDeviceToHost, s));
+    MCHK(hipStreamSynchronize(s));
     const uint64_t hits = tail[0] + tail[1];
     m->hits0 = hits;
     MCHK(hipMemcpyAsync(m->scal, &m->hits0, 8, hipMemcpyHostToDevice, s));
     MCHK(hipMemsetAsync(nhd, 0, 4, s));
     if (hits >= NONE) return set_err(KMER_E_BAD_PARAM, "kmer_match_open: more than 2^32 - 2 hits");
-    MCHK(dalloc(&pt, hits));
-    MCHK(dalloc(&pt2, hits));
-    MCHK(dalloc(&m->sq, hits));
-    MCHK(dalloc(&pq2, hits));
+    MCHK(db->pt.ensure(hits));
+    MCHK(db->pt2.ensure(hits));
+    MCHK(db->pq2.ensure(hits));
+    MCHK(b.sq.ensure(hits));
+    m->sq = b.sq.p;
     if (hits) {
-        hipLaunchKernelGGL(q_emit_kernel, dim3(grid_for(n)), dim3(256), 0, s, m->qidx, m->H, n, db->O, db->T, pt,
-                           pq2);
+        hipLaunchKernelGGL(q_emit_kernel, dim3(grid_for(n)), dim3(256), 0, s, m->qidx, m->H, n, db->O, db->T,
+                           db->pt.p, db->pq2.p);
         MCHK(hipGetLastError());
-        rocprim::double_buffer<uint32_t> kb(pt, pt2);
-        rocprim::double_buffer<uint32_t> vb(pq2, m->sq);
+        rocprim::double_buffer<uint32_t> kb(db->pt.p, db->pt2.p);
+        rocprim::double_buffer<uint32_t> vb(db->pq2.p, m->sq);
         MROC(tmp, rocprim::radix_sort_pairs(t, b, kb, vb, (size_t)hits, 0, std::max(1, bit_width64(nt)), s));
         if (vb.current() != m->sq) MCHK(hipMemcpyAsync(m->sq, vb.current(), hits * 4, hipMemcpyDeviceToDevice, s));
         hipLaunchKernelGGL(q_seg_kernel, dim3(grid_for((uint64_t)nt + 1)), dim3(256), 0, s, kb.current(), hits, nt,
@@ -499,6 +593,11 @@ kmer_status match_open_common(kmer_db *db, uint64_t n, kmer_match **out, kmer_ma
     kmer_match *m = new kmer_match();
     m->db = db;
     m->n = n;
+    if (db->has_spare) {                        // the last closed match's buffers
+        m->b = db->spare;
+        db->spare = MatchBufs();
+        db->has_spare = false;
+    }
     *mm = m;
     return KMER_OK;
 }
@@ -567,19 +666,16 @@ kmer_status kmer_match_open(kmer_db *db, const char *keys, const uint64_t *offse
     kmer_status st = match_open_common(db, n, out, &m);
     if (st != KMER_OK) return st;
     const uint64_t nbytes = n ? offsets[n] : 0;
-    uint8_t *dk = nullptr;
-    uint64_t *doff = nullptr;
-    hipError_t e = dalloc(&dk, nbytes);
-    if (e == hipSuccess) e = dalloc(&doff, n + 1);
-    if (e == hipSuccess) e = dalloc(&m->cnt, n);
-    if (e == hipSuccess && nbytes) e = hipMemcpyAsync(dk, keys, nbytes, hipMemcpyHostToDevice, db->s);
-    if (e == hipSuccess && n) e = hipMemcpyAsync(doff, offsets, (n + 1) * 8, hipMemcpyHostToDevice, db->s);
+    hipError_t e = db->qkeys.ensure(nbytes);
+    if (e == hipSuccess) e = db->qoffs.ensure(n + 1);
+    if (e == hipSuccess) e = m->b.cnt.ensure(n);
+    m->cnt = m->b.cnt.p;
+    if (e == hipSuccess && nbytes) e = hipMemcpyAsync(db->qkeys.p, keys, nbytes, hipMemcpyHostToDevice, db->s);
+    if (e == hipSuccess && n) e = hipMemcpyAsync(db->qoffs.p, offsets, (n + 1) * 8, hipMemcpyHostToDevice, db->s);
     if (e == hipSuccess && n) e = hipMemcpyAsync(m->cnt, counts, n * 8, hipMemcpyHostToDevice, db->s);
-    st = e == hipSuccess ? match_build(m, dk, doff, 0)
+    st = e == hipSuccess ? match_build(m, db->qkeys.p, db->qoffs.p, 0)
                          : set_err(KMER_E_DEVICE, std::string("HIP error: ") + hipGetErrorString(e));
     (void)hipStreamSynchronize(db->s);
-    if (dk) (void)hipFree(dk);
-    if (doff) (void)hipFree(doff);
     if (st != KMER_OK) {
         m->release();
         delete m;
@@ -600,7 +696,8 @@ kmer_status kmer_match_open_device(kmer_db *db, const void *d_keys, uint32_t kle
     hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventRecord(ev, (hipStream_t)stream);
     if (e == hipSuccess) e = hipStreamWaitEvent(db->s, ev, 0);
-    if (e == hipSuccess) e = dalloc(&m->cnt, n);
+    if (e == hipSuccess) e = m->b.cnt.ensure(n);
+    m->cnt = m->b.cnt.p;
     if (e == hipSuccess && n) e = hipMemcpyAsync(m->cnt, d_counts, n * 8, hipMemcpyDeviceToDevice, db->s);
     st = e == hipSuccess ? match_build(m, (const uint8_t *)d_keys, nullptr, klen)
                          : set_err(KMER_E_DEVICE, std::string("HIP error: ") + hipGetErrorString(e));

@@ -33,13 +33,7 @@ namespace {
 constexpr int TAB_RPL = 16;                  // segments (keys) per lane per round
 constexpr int TAB_WG1 = 1024;                // scatter workgroup (16 waves)
 constexpr int TAB_ROUND = TAB_RPL * TAB_WG1; // keys sorted in LDS per round
-// Final-kernel LDS slot: unit key << TAB_CB | count (a unit key = bucket
-// offset << 44 | remainder, < 2^50).  Register-held units add to the slot word
-// itself (a range holds <= 12 K keys, so a count never leaves its 14 bits);
-// streamed buckets count in tcnt.  ~0 is never a slot word (its count field
-// would be 16383 > 12288).
-constexpr uint32_t TAB_CB = 14;
-constexpr uint64_t TAB_EMPTY = ~0ull;
+constexpr uint64_t TAB_EMPTY = 1ull << 63;   // empty slot (remainders are < 2^44)
 constexpr uint64_t TAB_RMASK = (1ull << TAB_RBITS) - 1;
 
 __device__ __forceinline__ uint32_t tab_incl_sum(uint32_t x) {
@@ -395,19 +389,21 @@ constexpr uint32_t TAB_PROBE_MAX = 256;      // a longer probe marks the range a
 // `pend` is set) together:
 // every step issues one CAS per pending key (independent, so their LDS round
 // trips overlap) instead of walking each key's probe sequence in turn, which
-// serialises the wave on its longest probe for every key.  CAS(EMPTY ->
-// key << TAB_CB | INC) returning EMPTY claims the slot with its first count
-// (one LDS atomic for a new key); returning a word of the same key finds it,
-// and the count is added without a return (to the word when INC, else to
-// tcnt).  Returns the slots this lane claimed.
-template <int N, int M, bool INC>
+// serialises the wave on its longest probe for every key.  CAS(EMPTY -> rem)
+// returning EMPTY claims the slot, returning rem finds it; the count add needs
+// no return.  Returns the slots this lane claimed.
+template <int N, int M>
 __device__ __forceinline__ uint32_t tab_insert_grp(uint64_t *tkey, uint32_t *tcnt, const uint64_t (&key)[M], int g,
                                                    uint32_t pend, uint32_t *ovf) {
     // (g is a constant once the caller's loop is unrolled: key[g + j] stays in registers)
     pend = (pend >> g) & ((1u << N) - 1u);
+    uint64_t rem[N];
     uint32_t slot[N];
 #pragma unroll
-    for (int j = 0; j < N; ++j) slot[j] = tab_slot(key[g + j]);
+    for (int j = 0; j < N; ++j) {
+        rem[j] = key[g + j];
+        slot[j] = tab_slot(rem[j]);
+    }
     uint32_t claimed = 0;
     for (uint32_t step = 0; __any(pend != 0); ++step) {
         if (step == TAB_PROBE_MAX) {
@@ -418,17 +414,10 @@ __device__ __forceinline__ uint32_t tab_insert_grp(uint64_t *tkey, uint32_t *tcn
         for (int j = 0; j < N; ++j) {
             if (!(pend & (1u << j))) continue;
             const uint64_t old = atomicCAS((unsigned long long *)&tkey[slot[j]], (unsigned long long)TAB_EMPTY,
-                                           (unsigned long long)((key[g + j] << TAB_CB) | (INC ? 1u : 0u)));
-            if (old == TAB_EMPTY) {
-                if (!INC) __hip_atomic_fetch_add(&tcnt[slot[j]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                claimed += 1u;
-                pend &= ~(1u << j);
-            } else if ((old >> TAB_CB) == key[g + j]) {
-                if (INC)
-                    __hip_atomic_fetch_add((unsigned long long *)&tkey[slot[j]], 1ull, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-                else
-                    __hip_atomic_fetch_add(&tcnt[slot[j]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                           (unsigned long long)rem[j]);
+            if (old == TAB_EMPTY || old == rem[j]) {
+                __hip_atomic_fetch_add(&tcnt[slot[j]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                claimed += old == TAB_EMPTY ? 1u : 0u;
                 pend &= ~(1u << j);
             } else {
                 slot[j] = (slot[j] + 1) & (TAB_SLOTS - 1);
@@ -596,7 +585,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
                 // without spilling the held keys)
                 uint32_t cl = 0;
 #pragma unroll
-                for (int gi = 0; gi < TAB_KPT; gi += 4) cl += tab_insert_grp<4, TAB_KPT, true>(tkey, tcnt, kn, gi, pend, &ovf);
+                for (int gi = 0; gi < TAB_KPT; gi += 4) cl += tab_insert_grp<4>(tkey, tcnt, kn, gi, pend, &ovf);
                 for (int d = 32; d >= 1; d >>= 1) cl += __shfl_xor(cl, d);
                 if (lane == 0 && cl) atomicAdd(&occ, cl);
             } else {
@@ -605,7 +594,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
                     if (lds_flag(&ovf)) break;
                     uint64_t r1[1] = {src[i] - qbase};
                     if (r1[0] >= rlo && r1[0] < rhi) {
-                        uint32_t cl = tab_insert_grp<1, 1, false>(tkey, tcnt, r1, 0, 1u, &ovf);
+                        uint32_t cl = tab_insert_grp<1>(tkey, tcnt, r1, 0, 1u, &ovf);
                         if (cl) atomicAdd(&occ, cl);
                     }
                 }
@@ -640,9 +629,8 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
             // bump per bucket present among the wave's entries
 #pragma unroll 1
             for (uint32_t i = t; i < TAB_SLOTS && !(a.ablate & 2); i += TAB_FWG) {
-                const uint64_t word = tkey[i];
-                const bool v = word != TAB_EMPTY;
-                const uint64_t key = word >> TAB_CB;
+                const uint64_t key = tkey[i];
+                const bool v = key != TAB_EMPTY;
                 uint64_t m = __ballot(v);
                 if (!m) continue;
                 const uint32_t ql = v ? (uint32_t)(key >> TAB_RBITS) : 0u;
@@ -669,7 +657,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
                 }
                 if (!v) continue;
                 const uint64_t rem = key & TAB_RMASK;
-                const uint64_t cnt = (word & ((1ull << TAB_CB) - 1ull)) + tcnt[i];
+                const uint64_t cnt = tcnt[i];
                 tkey[i] = TAB_EMPTY;
                 tcnt[i] = 0;
                 const uint32_t qq = q + ql;
