@@ -216,6 +216,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the Node readFile() -> Map end-to-end run")
+    ap.add_argument("--no-match", action="store_true",
+                    help="skip the template-matching record (C2's result joined against a synthetic kmerFinder DB)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="sessions in rotation (>= 2: a step's finish overlaps the next steps' scans)")
     ap.add_argument("--config", default="c2", choices=("c1", "c2", "c3", "c4", "c5"),
@@ -504,6 +506,15 @@ def main():
             out["end_to_end"] = end_to_end(buf, args)
         if not args.no_cpu_baseline and world == 1 and args.config == "c2":
             out["cpu_baseline"] = cpu_baseline(args.k, prefix)
+        if (not args.no_match and world == 1 and args.config == "c2" and args.pipeline == 1 and args.k == 16
+                and args.prefix == "ATGAC"):
+            # §8(f3): the count just measured, still in HBM, joined against a
+            # synthetic template DB (tools/bench_match.py)
+            sys.path.insert(0, os.path.join(REPO, "tools"))
+            import bench_match
+            d_keys, d_cnt, _, nq = ctr.result_device()
+            out["template_matching"] = bench_match.measure(d_keys, d_cnt, nq, args.k, args.reads,
+                                                           cpu_baseline=not args.no_cpu_baseline)
         print(json.dumps(out), flush=True)
     for c in ctrs:
         c.close()

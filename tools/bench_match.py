@@ -29,33 +29,14 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--reads", type=int, default=10_000_000)
-    ap.add_argument("--templates", type=int, default=5030)
-    ap.add_argument("--per", type=int, default=3285)
-    ap.add_argument("--present", type=int, default=8)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    args = ap.parse_args()
-
+def measure(d_keys, d_cnt, nq, k=16, reads=10_000_000, templates=5030, per=3285, present=8, steps=3,
+            cpu_baseline=True):
+    """Matcher benchmark on a count already in HBM (kmer_result_device of a
+    C2 count): returns the JSON-able record (also used by bench.py)."""
     import torch
-    from kmerjs_amd import _native, synth_fastq_device
     from kmerjs_amd import kmerfinder as kf
     from tests.match_util import kmer_codes, BASES
-
-    dev = torch.device("cuda", 0)
-    k = 16
-    buf = torch.empty(args.reads * 317, dtype=torch.uint8, device=dev)
-    synth_fastq_device(buf.data_ptr(), 1, 0, args.reads)
-    torch.cuda.synchronize()
-    ctr = _native.Counter(k=k, prefix=b"ATGAC")
-    ctr.reset()
-    ctr.feed_device(buf.data_ptr(), buf.numel())
-    ctr.finish(want_result=False)
-    d_keys, d_cnt, _, nq = ctr.result_device()
-    del buf
-
+    dev = torch.device("cuda", torch.cuda.current_device())
     # query codes on the host (for the DB's present templates and the CPU baseline)
     from kmerjs_amd.multi import _CudaArray
     kt = torch.as_tensor(_CudaArray(d_keys, nq * k, "|u1"), device=dev).cpu().numpy().reshape(nq, k)
@@ -67,18 +48,21 @@ def main():
         qc = (qc << np.uint64(2)) | lut[kt[:, i]]
 
     rng = np.random.default_rng(7)
-    nt, per = args.templates, args.per
+    nt, per = templates, per
     codes = kmer_codes(rng, nt * per * 2, k)
     allc = np.empty(nt * per, dtype=np.uint64)
     for t in range(nt):
         c = np.unique(codes[t * per * 2:(t + 1) * per * 2])[:per]
-        if t < args.present:
+        if t < present:
             take = int(per * 0.6)
             c = np.unique(np.concatenate([rng.choice(qc, size=take, replace=False), c]))[:per]
         allc[t * per:(t + 1) * per] = c
     starts = np.arange(nt + 1, dtype=np.uint64) * np.uint64(per)
-    shifts = np.arange(2 * (k - 1), -1, -2, dtype=np.uint64)
-    keys = BASES[((allc[:, None] >> shifts[None, :]) & np.uint64(3)).astype(np.int64)].tobytes()
+    mat = np.empty((allc.size, k), dtype=np.uint8)
+    for j in range(k):                         # (column by column: no n x k 64-bit temporaries)
+        mat[:, j] = BASES[((allc >> np.uint64(2 * (k - 1 - j))) & np.uint64(3)).astype(np.uint8)]
+    keys = mat.tobytes()
+    del mat
     meta = [{"sequence": "NC_%06d" % t, "lengths": 2 * per, "ulength": per, "species": "synthetic"}
             for t in range(nt)]
     summary = {"templates": nt, "totalLen": 2 * per * nt, "uniqueLens": per * nt}
@@ -101,7 +85,7 @@ def main():
 
     one_step()            # warmup
     r1, loop, res = [], [], None
-    for _ in range(args.steps):
+    for _ in range(steps):
         a, b, res, _ = one_step()
         r1.append(a)
         loop.append(b)
@@ -117,16 +101,16 @@ def main():
 
     out = {"metric": "template matching (kmerFinder findMatches 'winner') per query", "unit": "ms",
            "value": float(np.median(r1) + np.median(loop)), "higher_is_better": False,
-           "config": {"workload": "C2 result (%d reads, k=16, ATGAC) vs synthetic DB" % args.reads,
+           "config": {"workload": "C2 result (%d reads, k=16, ATGAC) vs synthetic DB" % reads,
                       "query_kmers": int(nq), "templates": nt, "db_entries": info["entries"],
-                      "db_distinct": info["distinct"], "present": args.present},
+                      "db_distinct": info["distinct"], "present": present},
            "round1_ms": float(np.median(r1)), "winner_loop_ms": float(np.median(loop)),
            "winners": len(res), "winner_names": [dict(x)["template"] for x in res][:12],
            "hits_round1": hits, "templates_hit": len(tl), "db_build_ms": db_ms, "standard_ms": std_ms,
            "standard_significant": sum(x is not None for x in std),
            "round1_hits_per_s": hits / (np.median(r1) / 1e3), "query_kmers_per_s": nq / (np.median(r1) / 1e3),
            "data": "synthetic"}
-    if not args.no_cpu_baseline:
+    if cpu_baseline:
         from oracle import kmerfinder_oracle as ko
         tix = np.repeat(np.arange(nt, dtype=np.int64), per)
         t0 = time.perf_counter()
@@ -139,8 +123,37 @@ def main():
         out["cpu_baseline"] = {"value": cpu_ms, "unit": "ms (round 1 only)", "cores": 1, "kind": "port",
                                "sample": "the full workload, round 1 (numpy restatement, oracle/kmerfinder_oracle.py)"}
         out["round1_verified_vs_oracle"] = bool(ok)
-    ctr.close()
     db.close()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reads", type=int, default=10_000_000)
+    ap.add_argument("--templates", type=int, default=5030)
+    ap.add_argument("--per", type=int, default=3285)
+    ap.add_argument("--present", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    from kmerjs_amd import _native, synth_fastq_device
+
+    dev = torch.device("cuda", 0)
+    k = 16
+    buf = torch.empty(args.reads * 317, dtype=torch.uint8, device=dev)
+    synth_fastq_device(buf.data_ptr(), 1, 0, args.reads)
+    torch.cuda.synchronize()
+    ctr = _native.Counter(k=k, prefix=b"ATGAC")
+    ctr.reset()
+    ctr.feed_device(buf.data_ptr(), buf.numel())
+    ctr.finish(want_result=False)
+    d_keys, d_cnt, _, nq = ctr.result_device()
+    del buf
+    out = measure(d_keys, d_cnt, nq, k, args.reads, args.templates, args.per, args.present, args.steps,
+                  not args.no_cpu_baseline)
+    ctr.close()
     print(json.dumps(out))
 
 
