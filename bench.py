@@ -216,6 +216,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the Node readFile() -> Map end-to-end run")
+    ap.add_argument("--no-pipelined", action="store_true",
+                    help="skip the extra two-session (double-buffered) throughput measurement")
     ap.add_argument("--no-match", action="store_true",
                     help="skip the template-matching record (C2's result joined against a synthetic kmerFinder DB)")
     ap.add_argument("--pipeline", type=int, default=1,
@@ -320,12 +322,14 @@ def main():
 
     def retire():
         c, rec = inflight.pop(0)
-        c.sync()                  # its scan is done: chunk counters read back
+        # the finish first (it settles the chunk itself), so that its kernels
+        # are queued as soon as the scan's counters are back; the scan's own
+        # time is read afterwards (those events are complete by then)
+        multi_finish(c, rec, collect=args.collect)
         if rec:
             scan_ms, feed_ms, _ = c.last_timing(finish=False)
             tile_ms.append(scan_ms)
             feed_ms_l.append(feed_ms)
-        multi_finish(c, rec, collect=args.collect)
 
     def step(i, record):
         feed(ctrs[i % nctx])      # (its previous finish is ahead of it on its stream)
@@ -369,6 +373,31 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    # Also measured (single GPU, ordered paths): the same K steps with two
+    # sessions in rotation, each step's finish overlapping the next step's
+    # scan -- the double-buffered throughput of a batch pipeline.  Reported
+    # beside `value`, which (like the roofline) comes from the steps above, run
+    # strictly in sequence.
+    pipelined = None
+    if world == 1 and nctx == 1 and not table and not args.no_pipelined:
+        extra = Counter(k=args.k, prefix=prefix, device=local, flags=args.flags)
+        saved = ctrs
+        ctrs, nctx = [ctr, extra], 2
+        for i in range(2):
+            step(i, False)
+        drain()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for i in range(args.steps):
+            step(i, False)
+        drain()
+        torch.cuda.synchronize()
+        pel = time.perf_counter() - t1
+        ctrs, nctx = saved, 1
+        extra.close()
+        pipelined = {"sessions": 2, "ms_per_step": pel * 1e3 / args.steps,
+                     "value": wl["windows_total"] * args.steps / pel, "unit": "k-mers/s"}
 
     # one more pass to read the result size / accepted windows (outside the timed region)
     feed(ctr)
@@ -490,6 +519,8 @@ def main():
         if phases is not None:
             out["table_phase_ms"] = phases
             out["canonical_kmers"] = canonical
+        if pipelined is not None:
+            out["pipelined"] = pipelined
         if not args.no_pcie and world == 1:
             # PCIe-inclusive rate (host bytes -> H2D -> count -> ordered host result); never `value`
             host = buf.cpu().numpy().tobytes()
