@@ -127,3 +127,25 @@ def test_node_kmerfinder_matches_oracle(tmp_path):
             assert g.get("error") is None, g.get("error")
             assert [_pairs(x) for x in g["results"]] == w["results"]
         assert g["remaining"] == w["remaining"]
+
+
+@pytest.mark.gpu
+def test_node_readfile_long_contig(tmp_path):
+    """readFile() on a FASTA-like file with a 9 MB sequence line (beyond the
+    default order key's 2^23 bytes): kmer_count_file redoes the count in
+    long-line mode and the Map equals the oracle's (lib/kmers.js has no line
+    limit, :88-100)."""
+    import numpy as np
+    from oracle import oracle
+    from tests.util import digest
+    rng = np.random.default_rng(9)
+    big = np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, size=9_000_000)].tobytes()
+    data = b">contig\n" + big + b"\n+\nIIII\n@r2\nACGTATGACGTTAGCATGACCATGACAAAT\n+\nIIII\n"
+    f = tmp_path / "contig.fa"
+    f.write_bytes(data)
+    want = oracle.count_buffer(data, b"ATGAC", 21, 1)
+    p = subprocess.run([NODE, os.path.join(REPO, "tests", "node", "run_readfile.js"), str(f), "ATGAC", "21"],
+                       capture_output=True, text=True, timeout=300)
+    got = json.loads(p.stdout.strip().splitlines()[-1])
+    assert got.get("digest") == digest(want), got
+    assert got["size"] == len(want)
