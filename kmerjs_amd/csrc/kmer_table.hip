@@ -451,9 +451,16 @@ constexpr uint32_t TAB_SC = 1024;             // bucket starts cached in LDS per
 // the group size (canonical C5: ~1 K keys per bucket).
 constexpr uint32_t TAB_GMAX = 64;             // buckets per unit
 
+constexpr uint32_t TAB_SB = 4096;             // sort path: bins (top 12 remainder bits)
+constexpr uint32_t TAB_SORT_RUN = 128;        // sort path: largest 4-bin run a thread dedupes
+
 __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
-    __shared__ uint64_t tkey[TAB_SLOTS];
-    __shared__ uint32_t tcnt[TAB_SLOTS];
+    // hash table (8,192 slots of u64 key + u32 count) = the sort path's key array (12,288 u64)
+    __shared__ uint64_t lbuf[TAB_SLOTS + TAB_SLOTS / 2];
+    uint64_t *const tkey = lbuf;
+    uint32_t *const tcnt = (uint32_t *)(lbuf + TAB_SLOTS);
+    __shared__ uint32_t scnt[TAB_SB], sst[TAB_SB];
+    __shared__ uint32_t sws[16], sws2[16], smax;
     __shared__ uint64_t stk[2 * 64];          // range stack [lo, hi) of unit keys
     __shared__ uint64_t sc[TAB_SC + 2];       // start[cbase .. cbase + TAB_SC + 1]
     __shared__ uint32_t nout[TAB_GMAX];       // entries emitted per bucket of the unit
@@ -495,6 +502,32 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
         __syncthreads();
         for (uint32_t i = t; i < TAB_SC + 2; i += TAB_FWG) sc[i] = a.start[cb + i < TAB_NQ ? cb + i : TAB_NQ];
         __syncthreads();
+    };
+    // Map statistics of one canonical entry h (App. A.6)
+    auto account = [&](uint64_t h, uint64_t cnt) {
+        const uint64_t code = h * a.inv;
+        const uint32_t lo = (uint32_t)code & kmask, hi = (uint32_t)(code >> k) & kmask;
+        const uint32_t rlo2 = __brev(~lo & kmask) >> sh, rhi2 = __brev(~hi & kmask) >> sh;
+        const bool pal = lo == rlo2 && hi == rhi2;
+        st_canon += 1;
+        if (a.canonical) {
+            // one key per class: the lexicographically smaller of w, rc w
+            // (first differing base decides), counted C times
+            const uint32_t dif = (lo ^ rlo2) | (hi ^ rhi2);
+            const uint32_t j = dif ? __ffs(dif) - 1 : 0;
+            const uint32_t bw = (((hi >> j) & 1u) << 1) | ((lo >> j) & 1u);
+            const uint32_t br = (((rhi2 >> j) & 1u) << 1) | ((rlo2 >> j) & 1u);
+            const bool wmin = dif == 0 || bw < br;
+            const uint32_t clo = wmin ? lo : rlo2, chi = wmin ? hi : rhi2;
+            const bool cs = (((clo ^ a.plo) | (chi ^ a.phi)) & a.pmask) == 0;
+            st_keys += cs ? 1u : 0u;
+            st_sum += cs ? cnt : 0;
+        } else {
+            const bool fs = (((lo ^ a.plo) | (hi ^ a.phi)) & a.pmask) == 0;
+            const bool rs = !pal && (((rlo2 ^ a.plo) | (rhi2 ^ a.phi)) & a.pmask) == 0;
+            st_keys += (fs ? 1u : 0u) + (rs ? 1u : 0u);
+            st_sum += (fs ? (pal ? 2 * cnt : cnt) : 0) + (rs ? cnt : 0);
+        }
     };
     uint32_t cbase = q0;
     // the unit starting at bucket u: its end (uniform over the workgroup; the
@@ -561,6 +594,97 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
         if (prof)
             for (int j = 0; j < TAB_KPT; ++j) asm volatile("" ::"v"(kn[j]));   // (clock after the key loads)
         mark(0);
+        // Sort path (one bucket held in registers: C3's common case).  A
+        // counting sort of the bucket's remainders into 4,096 LDS bins by
+        // their top 12 bits, then every thread dedupes its 4 adjacent bins
+        // (~11 keys at C3) by comparison: one returning LDS atomic per key and
+        // plain LDS stores, instead of a CAS + a count add per key (plus
+        // probes) and a slot scan per range.  A bucket with a crowded run of
+        // bins (many copies of one key) takes the hash path below.
+        if (g == 1 && inreg && !(a.ablate & 4)) {
+            for (uint32_t i = t; i < TAB_SB; i += TAB_FWG) scnt[i] = 0;
+            if (t == 0) smax = 0;
+            __syncthreads();
+            uint32_t rank[TAB_KPT];
+            {
+                const int left = (int)n - (int)t;
+#pragma unroll
+                for (int j = 0; j < TAB_KPT; ++j)
+                    rank[j] = left > j * (int)TAB_FWG
+                                  ? atomicAdd(&scnt[(uint32_t)(kn[j] >> (TAB_RBITS - 12)) & (TAB_SB - 1)], 1u)
+                                  : 0u;
+            }
+            __syncthreads();
+            uint32_t c4[4], st4[4], s4 = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                c4[i] = scnt[4 * t + i];
+                s4 += c4[i];
+            }
+            uint32_t tot = 0;
+            uint32_t run = block_excl_1024(s4, sws, &tot);
+            {
+                uint32_t mx = s4;
+                for (int d = 32; d >= 1; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d));
+                if (lane == 0) atomicMax(&smax, mx);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                st4[i] = run;
+                sst[4 * t + i] = run;
+                run += c4[i];
+            }
+            __syncthreads();
+            if (smax <= TAB_SORT_RUN) {                 // (uniform)
+                {
+                    const int left = (int)n - (int)t;
+#pragma unroll
+                    for (int j = 0; j < TAB_KPT; ++j)
+                        if (left > j * (int)TAB_FWG)
+                            lbuf[sst[(uint32_t)(kn[j] >> (TAB_RBITS - 12)) & (TAB_SB - 1)] + rank[j]] = kn[j];
+                }
+                // the registers are free: the next unit's keys load during the dedupe
+                if (more) load_keys(s0n, nn);
+                __syncthreads();
+                // pass 1: distinct keys of this thread's bins (a key's copies share its bin)
+                uint32_t d = 0;
+#pragma unroll 1
+                for (int b = 0; b < 4; ++b)
+                    for (uint32_t i = st4[b]; i < st4[b] + c4[b]; ++i) {
+                        const uint64_t x = lbuf[i];
+                        bool first = true;
+                        for (uint32_t j = st4[b]; j < i; ++j) first &= lbuf[j] != x;
+                        d += first ? 1u : 0u;
+                    }
+                uint32_t dtot = 0;
+                uint32_t pos = block_excl_1024(d, sws2, &dtot);
+                // pass 2: each distinct key once, with the count of its copies
+#pragma unroll 1
+                for (int b = 0; b < 4; ++b)
+                    for (uint32_t i = st4[b]; i < st4[b] + c4[b]; ++i) {
+                        const uint64_t x = lbuf[i];
+                        bool first = true;
+                        for (uint32_t j = st4[b]; j < i; ++j) first &= lbuf[j] != x;
+                        if (!first) continue;
+                        uint32_t cnt = 1;
+                        for (uint32_t j = i + 1; j < st4[b] + c4[b]; ++j) cnt += lbuf[j] == x ? 1u : 0u;
+                        a.out[s0 + pos] = (x << 20) | cnt;
+                        ++pos;
+                        account(qbase | x, cnt);
+                    }
+                if (t == 0) a.nd[q] = dtot;
+                __syncthreads();
+                // the hash path's invariant: an empty table between ranges
+                for (uint32_t i = t; i < TAB_SLOTS; i += TAB_FWG) {
+                    tkey[i] = TAB_EMPTY;
+                    tcnt[i] = 0;
+                }
+                if (prof) pt[4] += 1;
+                q = qn;
+                qe = qne;
+                continue;
+            }
+        }
         while (true) {
             __syncthreads();
             const uint32_t top = sp;
@@ -672,30 +796,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
                         atomicOr(a.err, ERR_BIG_OVERFLOW);
                     }
                 }
-                // Map view of this canonical entry (App. A.6)
-                const uint64_t code = h * a.inv;
-                const uint32_t lo = (uint32_t)code & kmask, hi = (uint32_t)(code >> k) & kmask;
-                const uint32_t rlo2 = __brev(~lo & kmask) >> sh, rhi2 = __brev(~hi & kmask) >> sh;
-                const bool pal = lo == rlo2 && hi == rhi2;
-                st_canon += 1;
-                if (a.canonical) {
-                    // one key per class: the lexicographically smaller of w, rc w
-                    // (first differing base decides), counted C times
-                    const uint32_t dif = (lo ^ rlo2) | (hi ^ rhi2);
-                    const uint32_t j = dif ? __ffs(dif) - 1 : 0;
-                    const uint32_t bw = (((hi >> j) & 1u) << 1) | ((lo >> j) & 1u);
-                    const uint32_t br = (((rhi2 >> j) & 1u) << 1) | ((rlo2 >> j) & 1u);
-                    const bool wmin = dif == 0 || bw < br;
-                    const uint32_t clo = wmin ? lo : rlo2, chi = wmin ? hi : rhi2;
-                    const bool cs = (((clo ^ a.plo) | (chi ^ a.phi)) & a.pmask) == 0;
-                    st_keys += cs ? 1u : 0u;
-                    st_sum += cs ? cnt : 0;
-                } else {
-                    const bool fs = (((lo ^ a.plo) | (hi ^ a.phi)) & a.pmask) == 0;
-                    const bool rs = !pal && (((rlo2 ^ a.plo) | (rhi2 ^ a.phi)) & a.pmask) == 0;
-                    st_keys += (fs ? 1u : 0u) + (rs ? 1u : 0u);
-                    st_sum += (fs ? (pal ? 2 * cnt : cnt) : 0) + (rs ? cnt : 0);
-                }
+                account(h, cnt);
             }
             mark(3);
         }
