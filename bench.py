@@ -270,13 +270,20 @@ def main():
         args.no_pcie = True
     from kmerjs_amd._native import FLAG_CANONICAL as _FC
     table = bool(args.flags & (FLAG_UNORDERED | _FC))
-    if table and args.gpus > 1:
-        raise SystemExit("table mode is single-GPU in this build (see DESIGN.md)")
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    strong = False
+    if args.config == "c3" and world_env > 1 and "--reads" not in argv:
+        # C3 names a job (100 M reads), not a per-GPU size; one rank's 100 M reads
+        # plus the exchange's send and receive key buffers would not fit 288 GB:
+        # N ranks split the 100 M reads (strong scaling)
+        args.reads = 100_000_000 // world_env
+        strong = True
 
     import torch
     import torch.distributed as dist
     from kmerjs_amd import Counter
-    from kmerjs_amd.multi import collect_ordered_device, device_u64, finish_distributed, finish_exchange, merge_to
+    from kmerjs_amd.multi import (collect_ordered_device, device_u64, finish_distributed, finish_exchange,
+                                  finish_table_exchange, merge_to)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -344,15 +351,23 @@ def main():
     def multi_finish(c, record=False, collect=False):
         if world == 1:
             c.finish(want_result=False)
-            if table and record:
+        elif table:
+            # pass-1 keys to the owners of their hash-space slices (one RCCL
+            # all-to-all), pass 2 + final on each owner's buckets
+            finish_table_exchange(c)
+        if table:
+            if record:
                 phase_ms.append(c.phase_times())
-        elif args.merge == "hits":
+            return
+        if world == 1:
+            return
+        if args.merge == "hits":
             finish_exchange(c, args.k, len(prefix), total_lines)
         elif args.merge == "alltoall":
             finish_distributed(c, args.k, len(prefix), total_lines)
         else:
             merge_to(c, args.k, len(prefix), total_lines, dst=0, want_result=False)
-        if collect and world > 1 and args.merge != "gather":
+        if collect and args.merge != "gather":
             collect_ordered_device(c, args.k, total_lines, dst=0)
 
     for i in range(args.warmup):
@@ -410,6 +425,10 @@ def main():
     if table:
         canonical, n_keys_map, map_sum = ctr.table_stats()
         n_dev, dev_sum, n_rec, rec_sum = n_keys_map, map_sum, 0, 0
+        if world > 1:                     # the ranks' shares of the table add up
+            tc = torch.tensor([canonical], dtype=torch.int64, device=dev)
+            dist.all_reduce(tc)
+            canonical = int(tc.item())
     else:
         d_keys, d_cnt, d_first, n_dev = ctr.result_device() if (rank == 0 or args.merge != "gather") else (0, 0, 0, 0)
         dev_sum = int(device_u64(d_cnt, n_dev, dev).sum().item()) if n_dev else 0
@@ -497,7 +516,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": {"c1": "test_data/test_short.fastq (reference fixture)",
@@ -513,7 +532,8 @@ def main():
                        "pipeline": ("%d sessions in rotation: finishes overlap later scans" % nctx if nctx > 1
                                     else "off (steps in sequence)"),
                        "parallelism": "dp%d (reads sharded; %s%s)" % (
-                           world, {"hits": "RCCL all-to-all of hits by key range, per-rank finish",
+                           world, "RCCL all-to-all of pass-1 keys by hash-space slice, per-rank table finish"
+                           if table else {"hits": "RCCL all-to-all of hits by key range, per-rank finish",
                         "alltoall": "RCCL all-to-all of partials by key range, per-rank finish"}.get(
                             args.merge, "RCCL gather of partials, finish on rank 0"),
                            "; + alltoallv gather of the ordered ranges to rank 0 and device merge into one "

@@ -226,6 +226,27 @@ kmer_status kmer_table_stats(kmer_ctx *ctx, uint64_t *canonical, uint64_t *keys,
  * big = n_big {uint64 h, uint64 count} pairs.  Valid until the next reset. */
 kmer_status kmer_table_device(kmer_ctx *ctx, const void **d_entries, const void **d_bucket_start,
                               const void **d_bucket_len, const void **d_big, uint64_t *n_big);
+/* Table mode across ranks (replaces the one Map.set stream of lib/kmers.js:95
+ * when the count is sharded over GPUs; reads are independent, :151-155).
+ * Rank o (of `world` <= 1024) owns the pass-1 partitions [o*1024/world,
+ * (o+1)*1024/world) -- a contiguous slice of the hash space h and its
+ * buckets.  After the feeds, kmer_table_exchange_prepare returns in d_send,
+ * per owner, a contiguous run of uint64 pass-1 keys (runs in owner order, each
+ * partition-major); counts[o] (host, `world`) = keys for owner o; parts[p]
+ * (host, 1024) = this session's keys per partition.  d_send is valid until the
+ * next call on the context.  Exchange the runs (all-to-all over xGMI) and the
+ * parts tables (all-gather), then hand the received runs, concatenated in
+ * source-rank order (n keys), and parts (world x 1024, source-rank order) to
+ * kmer_table_finish_exchanged: pass 2 + final over this rank's buckets
+ * (others empty).  The table is written over d_recv, which must stay alive
+ * until the next reset; kmer_table_stats / kmer_table_device then describe
+ * this rank's share (the ranks' stats add up: partitions are disjoint; move
+ * record keys to one rank first, kmer_records_export / _import / _clear).
+ * `wait_stream` as for kmer_finish_exchanged. */
+kmer_status kmer_table_exchange_prepare(kmer_ctx *ctx, uint32_t world, const void **d_send, uint64_t *counts,
+                                        uint64_t *parts);
+kmer_status kmer_table_finish_exchanged(kmer_ctx *ctx, void *d_recv, uint64_t n, const uint64_t *parts,
+                                        uint32_t world, uint32_t rank, void *wait_stream);
 
 /* Device time (HIP events on the context's stream, ms) since the last reset:
  * scan_ms = the streaming tile-scan kernel(s) alone, feed_ms = every kernel of

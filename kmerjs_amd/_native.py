@@ -20,6 +20,7 @@ FLAG_UNORDERED = 16
 FLAG_TABLE_SPLIT_TEST = 32
 FLAG_CANONICAL = 64
 FLAG_LONG_LINES = 128
+TAB_PARTS = 1024    # table mode: pass-1 partitions (ownership unit across ranks)
 WRITE_JSON = 0      # JSON.stringify(mapToJSON(map)), lib/kmers.js:46-54
 WRITE_LEGACY = 1    # "{\nkey: count,...}\n", lib/index.js:381-388
 
@@ -32,6 +33,7 @@ EXPORTS = ["kmer_open", "kmer_close", "kmer_count_file", "kmer_count_buffer", "k
            "kmer_result_arrays", "kmer_result_firsts", "kmer_result_write", "kmer_result_free",
            "kmer_synth_fastq_device",
            "kmer_last_timing", "kmer_phase_times", "kmer_table_stats", "kmer_table_device",
+           "kmer_table_exchange_prepare", "kmer_table_finish_exchanged",
            "kmer_status_string", "kmer_last_error", "kmer_version"]
 # include/kmer_match.h (the template matcher, same library)
 MATCH_EXPORTS = ["kmer_db_open", "kmer_db_info", "kmer_db_close", "kmer_match_open", "kmer_match_open_device",
@@ -113,6 +115,8 @@ def _load():
         "kmer_table_stats": (ctypes.c_int, [vp, pu64, pu64, pu64]),
         "kmer_table_device": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp),
                                              ctypes.POINTER(vp), pu64]),
+        "kmer_table_exchange_prepare": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.POINTER(vp), pu64, pu64]),
+        "kmer_table_finish_exchanged": (ctypes.c_int, [vp, vp, u64, pu64, ctypes.c_uint32, ctypes.c_uint32, vp]),
         "kmer_status_string": (ctypes.c_char_p, [ctypes.c_int]),
         "kmer_last_error": (ctypes.c_char_p, [vp]),
         "kmer_version": (ctypes.c_char_p, []),
@@ -358,6 +362,28 @@ class Counter:
         self._check(LIB.kmer_table_device(self.h, ctypes.byref(e), ctypes.byref(st), ctypes.byref(ln),
                                           ctypes.byref(bg), ctypes.byref(nb)), "table_device")
         return e.value or 0, st.value or 0, ln.value or 0, bg.value or 0, nb.value
+
+    def table_exchange_prepare(self, world):
+        """Table mode across ranks: (d_send, counts, parts) -- this session's
+        pass-1 keys as per-owner runs (uint64, owner-major), the keys per
+        owner, and the keys per pass-1 partition (TAB_PARTS of them)."""
+        d = ctypes.c_void_p()
+        cnt = (ctypes.c_uint64 * world)()
+        parts = (ctypes.c_uint64 * TAB_PARTS)()
+        self._check(LIB.kmer_table_exchange_prepare(self.h, world, ctypes.byref(d), cnt, parts),
+                    "table_exchange_prepare")
+        return d.value or 0, list(cnt), list(parts)
+
+    def table_finish_exchanged(self, d_recv, n, parts, world, rank, stream=0):
+        """Pass 2 + final over the received keys (runs by source rank); parts =
+        world x TAB_PARTS partition counts by source rank.  The table is
+        written over d_recv: keep it alive until the next reset."""
+        import numpy as np
+        pa = np.ascontiguousarray(np.asarray(parts, dtype=np.uint64).reshape(-1))
+        assert pa.size == world * TAB_PARTS
+        self._check(LIB.kmer_table_finish_exchanged(self.h, ctypes.c_void_p(d_recv), n,
+                                                    pa.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), world, rank,
+                                                    ctypes.c_void_p(stream)), "table_finish_exchanged")
 
     def lines(self):
         n = ctypes.c_uint64()

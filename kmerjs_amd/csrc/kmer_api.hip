@@ -204,6 +204,9 @@ struct kmer_ctx {
     std::vector<std::vector<uint64_t>> t_coff;   // per chunk: TAB_NB + 1 partition starts (chunk-relative)
     uint64_t t_canon = 0, t_nkeys = 0, t_sum = 0, t_nbig = 0;   // last finish
     bool t_done = false;           // a table finish holds results
+    uint64_t *t_ent = nullptr;     // the table's entries (tb1, or the received keys' buffer after an exchange)
+    DBuf<uint64_t> tsend;          // table exchange: send runs (sessions of several chunks)
+    DBuf<TabSeg> tseg;             // ... and their segment table
     hipEvent_t tev[8] = {};        // table phase events
     // multi-device group (kmer_params.ndev > 1): one child context per device;
     // the group itself owns no device state beyond the merge buffers on
@@ -1024,12 +1027,17 @@ uint64_t inv_odd(uint64_t a) {   // inverse of an odd number mod 2^64 (Newton)
 // Pass 2 + final of the session: pass-1 partitions (one run per chunk) are
 // cut into units; each unit's keys go to their 2^20 buckets in tb2; the
 // final kernel merges each bucket in LDS and writes its entries into tb1.
-kmer_status table_finish(kmer_ctx *c) {
+// B1: the pass-1 keys (default: this session's, tb1); [qlo, qhi): the buckets
+// present (multi-GPU: this rank's partitions; the others are left empty).
+kmer_status table_finish(kmer_ctx *c, const uint64_t *B1 = nullptr, uint32_t qlo = 0, uint32_t qhi = TAB_NQ) {
     hipStream_t s = c->stream;
     c->t_canon = c->t_nkeys = c->t_sum = c->t_nbig = 0;
     c->t_done = true;
     const uint64_t n = c->t_keys;
     if (n == 0) return KMER_OK;
+    // the table is written over the pass-1 keys (dead after pass 2)
+    if (!B1) B1 = c->tb1.p;
+    c->t_ent = const_cast<uint64_t *>(B1);
     std::vector<TabUnit> units;
     std::vector<TabUnit> heads(TAB_NB);
     uint64_t ubase = 0;
@@ -1068,11 +1076,11 @@ kmer_status table_finish(kmer_ctx *c) {
     HIPCHK(c, c->tbig.ensure(1 << 16, s));
     HIPCHK(c, c->tstats.ensure(4, s));
     HIPCHK(c, hipEventRecord(c->tev[4], s));
-    HIPCHK(c, launch_tab_hist2(c->tb1.p, c->tunits.p, (uint32_t)n_units, c->tH.p, s));
+    HIPCHK(c, launch_tab_hist2(B1, c->tunits.p, (uint32_t)n_units, c->tH.p, s));
     ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tH.p, c->tHs.p, (uint64_t)0, (size_t)nh,
                                            rocprim::plus<uint64_t>(), s));
     HIPCHK(c, hipEventRecord(c->tev[5], s));
-    HIPCHK(c, launch_tab_scatter2(c->tb1.p, c->tunits.p, (uint32_t)n_units, c->tHs.p, c->tb2.p, s));
+    HIPCHK(c, launch_tab_scatter2(B1, c->tunits.p, (uint32_t)n_units, c->tHs.p, c->tb2.p, s));
     HIPCHK(c, hipEventRecord(c->tev[6], s));
     HIPCHK(c, launch_tab_starts(c->tHs.p, c->tunits.p + n_units, n, c->tstart.p, s));
     HIPCHK(c, hipMemsetAsync(c->tstats.p, 0, 4 * sizeof(unsigned long long), s));
@@ -1080,7 +1088,7 @@ kmer_status table_finish(kmer_ctx *c) {
     memset(&f, 0, sizeof(f));
     f.B2 = c->tb2.p;
     f.start = c->tstart.p;
-    f.out = c->tb1.p;                        // (pass-1 keys are dead after pass 2)
+    f.out = c->t_ent;
     f.nd = c->tnd.p;
     const uint64_t mean = n / TAB_NQ;
     uint64_t range_keys = 3000;               // mean keys per LDS range (load ~0.37: short probes; measured best at C3)
@@ -1103,6 +1111,9 @@ kmer_status table_finish(kmer_ctx *c) {
     f.inv = inv_odd(TAB_MUL);
     f.canonical = (c->p.flags & KMER_FLAG_CANONICAL) ? 1u : 0u;
     f.stats = c->tstats.p;
+    f.qlo = qlo;
+    f.qhi = qhi;
+    if (qlo != 0 || qhi != TAB_NQ) HIPCHK(c, hipMemsetAsync(c->tnd.p, 0, TAB_NQ * sizeof(uint32_t), s));
     const uint32_t fgrid = (uint32_t)std::max(c->n_cu, 1);
     std::vector<uint64_t> hprof;
 #ifdef TAB_PROF
@@ -1177,7 +1188,7 @@ kmer_status build_table_result(kmer_ctx *c, uint64_t lines, kmer_result **out) {
         std::vector<TabBig> big(c->t_nbig);
         bool ok = hipMemcpyAsync(start.data(), c->tstart.p, start.size() * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
                   hipMemcpyAsync(nd.data(), c->tnd.p, nd.size() * 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
-                  hipMemcpyAsync(ent.data(), c->tb1.p, ent.size() * 8, hipMemcpyDeviceToHost, s) == hipSuccess;
+                  hipMemcpyAsync(ent.data(), c->t_ent, ent.size() * 8, hipMemcpyDeviceToHost, s) == hipSuccess;
         if (ok && !big.empty())
             ok = hipMemcpyAsync(big.data(), c->tbig.p, big.size() * sizeof(TabBig), hipMemcpyDeviceToHost, s) == hipSuccess;
         if (!ok || hipStreamSynchronize(s) != hipSuccess) {
@@ -1276,6 +1287,7 @@ kmer_status reset(kmer_ctx *c) {
     c->t_cbase.clear();
     c->t_coff.clear();
     c->t_done = false;
+    c->t_ent = nullptr;
     for (double &x : c->t_ms) x = 0.0;
     c->scan_ms = c->feed_ms = c->finish_ms = 0.0;
     c->open_stream = true;
@@ -1943,7 +1955,8 @@ kmer_status kmer_close(kmer_ctx *c) {
     c->rec_keys.release();
     c->tmp.release();
     c->batch.release();
-    for (auto *b : {&c->tb1, &c->tb2, &c->tHs, &c->tstart, &c->tp1, &c->tpb}) b->release();
+    for (auto *b : {&c->tb1, &c->tb2, &c->tHs, &c->tstart, &c->tp1, &c->tpb, &c->tsend}) b->release();
+    c->tseg.release();
     c->tpc.release();
     c->tpieces.release();
     c->tH.release();
@@ -2335,6 +2348,96 @@ kmer_status kmer_finish_exchanged(kmer_ctx *c, const void *d_recv, uint64_t n, u
     return build_result(c, total_lines, out);
 }
 
+// Table mode across ranks: rank o owns the pass-1 partitions [o * TAB_NB /
+// world, (o + 1) * TAB_NB / world), i.e. a contiguous slice of the hash space
+// and its buckets.  The send buffer holds, per owner, that owner's
+// partitions in partition order (one chunk: tb1 as it is).
+uint32_t tab_part_lo(uint32_t o, uint32_t world) { return (uint32_t)((uint64_t)o * TAB_NB / world); }
+
+kmer_status kmer_table_exchange_prepare(kmer_ctx *c, uint32_t world, const void **d_send, uint64_t *counts,
+                                        uint64_t *parts) {
+    if (!c || !d_send || !counts || !parts || world == 0 || world > TAB_NB) return KMER_E_BAD_PARAM;
+    SETTLE(c);
+    if (c->mode != MODE_TABLE) return fail(c, KMER_E_STATE, "not a table-mode context (KMER_FLAG_UNORDERED)");
+    if (!c->open_stream) return fail(c, KMER_E_STATE, "exchange without reset/feed");
+    if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
+    hipStream_t s = c->stream;
+    const size_t nch = c->t_cbase.size();
+    for (uint32_t p = 0; p < TAB_NB; ++p) {
+        uint64_t x = 0;
+        for (size_t ch = 0; ch < nch; ++ch) x += c->t_coff[ch][p + 1] - c->t_coff[ch][p];
+        parts[p] = x;
+    }
+    for (uint32_t o = 0; o < world; ++o) {
+        uint64_t x = 0;
+        for (uint32_t p = tab_part_lo(o, world); p < tab_part_lo(o + 1, world); ++p) x += parts[p];
+        counts[o] = x;
+    }
+    *d_send = nullptr;
+    const uint64_t n = c->t_keys;
+    if (n == 0) return KMER_OK;
+    if (nch == 1 && c->t_cbase[0] == 0) {
+        *d_send = c->tb1.p;
+        return KMER_OK;
+    }
+    std::vector<TabSeg> segs;
+    uint64_t dst = 0;
+    for (uint32_t p = 0; p < TAB_NB; ++p)
+        for (size_t ch = 0; ch < nch; ++ch) {
+            const uint64_t a0 = c->t_coff[ch][p], a1 = c->t_coff[ch][p + 1];
+            if (a1 > a0) segs.push_back(TabSeg{c->t_cbase[ch] + a0, dst, a1 - a0});
+            dst += a1 - a0;
+        }
+    if (segs.size() >= (1ull << 31)) return fail(c, KMER_E_BAD_PARAM, "too many table segments");
+    HIPCHK(c, c->tsend.ensure(n, s));
+    HIPCHK(c, c->tseg.ensure(segs.size(), s));
+    HIPCHK(c, hipMemcpyAsync(c->tseg.p, segs.data(), segs.size() * sizeof(TabSeg), hipMemcpyHostToDevice, s));
+    HIPCHK(c, launch_tab_segcopy(c->tb1.p, c->tseg.p, (uint32_t)segs.size(), c->tsend.p, s));
+    HIPCHK(c, hipStreamSynchronize(s));        // (segs is a host temporary; the caller's collective follows)
+    *d_send = c->tsend.p;
+    return KMER_OK;
+}
+
+kmer_status kmer_table_finish_exchanged(kmer_ctx *c, void *d_recv, uint64_t n, const uint64_t *parts,
+                                        uint32_t world, uint32_t rank, void *wait_stream) {
+    if (!c || (n && !d_recv) || !parts || world == 0 || world > TAB_NB || rank >= world) return KMER_E_BAD_PARAM;
+    SETTLE(c);
+    if (c->mode != MODE_TABLE) return fail(c, KMER_E_STATE, "not a table-mode context (KMER_FLAG_UNORDERED)");
+    if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
+    const uint32_t plo = tab_part_lo(rank, world), phi = tab_part_lo(rank + 1, world);
+    // the received runs, by source rank: source r's keys of this rank's
+    // partitions, partition-major -- one "chunk" per source
+    std::vector<uint64_t> cbase;
+    std::vector<std::vector<uint64_t>> coff;
+    uint64_t base = 0;
+    for (uint32_t r = 0; r < world; ++r) {
+        std::vector<uint64_t> off(TAB_NB + 1, 0);
+        uint64_t x = 0;
+        for (uint32_t p = 0; p < TAB_NB; ++p) {
+            off[p] = x;
+            if (p >= plo && p < phi) x += parts[(uint64_t)r * TAB_NB + p];
+        }
+        off[TAB_NB] = x;
+        cbase.push_back(base);
+        coff.push_back(std::move(off));
+        base += x;
+    }
+    if (base != n) return fail(c, KMER_E_BAD_PARAM, "received key count does not match the partition counts");
+    hipStream_t s = c->stream;
+    HIPCHK(c, hipEventRecord(c->evw, (hipStream_t)wait_stream));
+    HIPCHK(c, hipStreamWaitEvent(s, c->evw, 0));
+    c->t_cbase = std::move(cbase);
+    c->t_coff = std::move(coff);
+    c->t_keys = n;
+    HIPCHK(c, hipEventRecord(c->ev2, s));
+    kmer_status st = table_finish(c, n ? (const uint64_t *)d_recv : nullptr, plo << TAB_L2, phi << TAB_L2);
+    if (st) return st;
+    HIPCHK(c, hipEventRecord(c->ev3, s));
+    c->timing_pending = true;
+    c->open_stream = false;
+    return KMER_OK;
+}
+
 kmer_status kmer_records_export(kmer_ctx *c, kmer_result **out) {
     if (!c || !out) return KMER_E_BAD_PARAM;
     SETTLE(c);
@@ -2443,7 +2546,7 @@ kmer_status kmer_table_device(kmer_ctx *c, const void **d_entries, const void **
     if (c->mode != MODE_TABLE) return fail(c, KMER_E_STATE, "not a table-mode context (KMER_FLAG_UNORDERED)");
     if (!c->t_done) return fail(c, KMER_E_STATE, "no table finish yet");
     const bool any = c->t_keys != 0;
-    if (d_entries) *d_entries = any ? c->tb1.p : nullptr;
+    if (d_entries) *d_entries = any ? c->t_ent : nullptr;
     if (d_bucket_start) *d_bucket_start = any ? c->tstart.p : nullptr;
     if (d_bucket_len) *d_bucket_len = any ? c->tnd.p : nullptr;
     if (d_big) *d_big = any ? c->tbig.p : nullptr;

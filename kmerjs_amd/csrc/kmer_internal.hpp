@@ -416,6 +416,7 @@ struct TabFinal {
     uint64_t inv;                  // inverse of TAB_MUL mod 2^64 (tab_mix^-1)
     unsigned long long *stats;     // [0] canonical entries [1] Map keys [2] sum of Map counts
     uint64_t *prof;                // experiments only (KMERHIP_TAB_PROF): per-workgroup phase clocks, 8 each
+    uint32_t qlo, qhi;             // buckets [qlo, qhi) of this table (multi-GPU: the rank's partitions)
 };
 
 constexpr uint64_t TAB_PIECE = 4096;                   // windows per piece of a long line (pass 1)
@@ -431,6 +432,12 @@ hipError_t launch_tab_scatter2(const uint64_t *B1, const TabUnit *units, uint32_
 hipError_t launch_tab_starts(const uint64_t *H2s, const TabUnit *pfirst, uint64_t total, uint64_t *start,
                              hipStream_t s);
 hipError_t launch_tab_final(const TabFinal &a, uint32_t grid, hipStream_t s);
+// multi-GPU table exchange: copy n segments {src offset, dst offset, length}
+// of u64 keys (one workgroup per segment, grid-strided)
+struct TabSeg {
+    uint64_t src, dst, len;
+};
+hipError_t launch_tab_segcopy(const uint64_t *src, const TabSeg *segs, uint32_t n, uint64_t *dst, hipStream_t s);
 hipError_t launch_synth_fastq(uint8_t *out, uint64_t seed, uint64_t first_read, uint64_t n_reads,
                               hipStream_t s);
 hipError_t launch_permute_rows(const uint8_t *keys, const uint64_t *cnt, const uint64_t *first, const uint32_t *idx,

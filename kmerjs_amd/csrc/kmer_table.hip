@@ -460,7 +460,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
     uint64_t *const tkey = lbuf;
     uint32_t *const tcnt = (uint32_t *)(lbuf + TAB_SLOTS);
     __shared__ uint32_t scnt[TAB_SB], sst[TAB_SB];
-    __shared__ uint32_t sws[16], sws2[16], smax;
+    __shared__ uint32_t sws[16], smax;
     __shared__ uint64_t stk[2 * 64];          // range stack [lo, hi) of unit keys
     __shared__ uint64_t sc[TAB_SC + 2];       // start[cbase .. cbase + TAB_SC + 1]
     __shared__ uint32_t nout[TAB_GMAX];       // entries emitted per bucket of the unit
@@ -468,8 +468,8 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
     const uint32_t t = threadIdx.x, lane = t & 63;
     const uint32_t k = a.k;
     const uint32_t kmask = k >= 32 ? ~0u : ((1u << k) - 1u), sh = 32 - k;
-    const uint32_t per = (TAB_NQ + gridDim.x - 1) / gridDim.x;
-    const uint32_t q0 = blockIdx.x * per, q1 = q0 + per < TAB_NQ ? q0 + per : TAB_NQ;
+    const uint32_t per = (a.qhi - a.qlo + gridDim.x - 1) / gridDim.x;
+    const uint32_t q0 = min(a.qlo + blockIdx.x * per, a.qhi), q1 = q0 + per < a.qhi ? q0 + per : a.qhi;
     const uint64_t rk = a.range_keys;
     uint64_t st_canon = 0, st_keys = 0, st_sum = 0;
     uint64_t kn[TAB_KPT];
@@ -549,6 +549,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
         tcnt[i] = 0;
     }
     refill(cbase);
+    bool dirty = false;
     uint32_t q = q0, qe = q0 < q1 ? unit_end(q0) : q0;
     if (q0 < q1) load_keys(sc[0], sc[qe - cbase] - sc[0]);
     while (q < q1) {
@@ -646,44 +647,47 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
                 // the registers are free: the next unit's keys load during the dedupe
                 if (more) load_keys(s0n, nn);
                 __syncthreads();
-                // pass 1: distinct keys of this thread's bins (a key's copies share its bin)
-                uint32_t d = 0;
+                // each distinct key once, with the count of its copies (a
+                // key's copies share its bin); output slots from one LDS
+                // counter bump per wave and key round (order inside a bucket
+                // is free)
 #pragma unroll 1
                 for (int b = 0; b < 4; ++b)
                     for (uint32_t i = st4[b]; i < st4[b] + c4[b]; ++i) {
                         const uint64_t x = lbuf[i];
                         bool first = true;
                         for (uint32_t j = st4[b]; j < i; ++j) first &= lbuf[j] != x;
-                        d += first ? 1u : 0u;
-                    }
-                uint32_t dtot = 0;
-                uint32_t pos = block_excl_1024(d, sws2, &dtot);
-                // pass 2: each distinct key once, with the count of its copies
-#pragma unroll 1
-                for (int b = 0; b < 4; ++b)
-                    for (uint32_t i = st4[b]; i < st4[b] + c4[b]; ++i) {
-                        const uint64_t x = lbuf[i];
-                        bool first = true;
-                        for (uint32_t j = st4[b]; j < i; ++j) first &= lbuf[j] != x;
-                        if (!first) continue;
                         uint32_t cnt = 1;
-                        for (uint32_t j = i + 1; j < st4[b] + c4[b]; ++j) cnt += lbuf[j] == x ? 1u : 0u;
-                        a.out[s0 + pos] = (x << 20) | cnt;
-                        ++pos;
-                        account(qbase | x, cnt);
+                        if (first)
+                            for (uint32_t j = i + 1; j < st4[b] + c4[b]; ++j) cnt += lbuf[j] == x ? 1u : 0u;
+                        const unsigned long long fm = __ballot(first);
+                        if (fm) {
+                            const int ld = __ffsll((long long)fm) - 1;
+                            uint32_t base = 0;
+                            if (lane == (uint32_t)ld) base = atomicAdd(&nout[0], (uint32_t)__popcll(fm));
+                            base = (uint32_t)__shfl((int)base, ld);
+                            if (first) {
+                                const uint32_t pos = base + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
+                                a.out[s0 + pos] = (x << 20) | cnt;
+                                account(qbase | x, cnt);
+                            }
+                        }
                     }
-                if (t == 0) a.nd[q] = dtot;
                 __syncthreads();
-                // the hash path's invariant: an empty table between ranges
-                for (uint32_t i = t; i < TAB_SLOTS; i += TAB_FWG) {
-                    tkey[i] = TAB_EMPTY;
-                    tcnt[i] = 0;
-                }
+                if (t == 0) a.nd[q] = nout[0];
+                dirty = true;                    // the hash path clears the table before use
                 if (prof) pt[4] += 1;
                 q = qn;
                 qe = qne;
                 continue;
             }
+        }
+        if (dirty) {                             // (uniform) lbuf held sort-path keys
+            for (uint32_t i = t; i < TAB_SLOTS; i += TAB_FWG) {
+                tkey[i] = TAB_EMPTY;
+                tcnt[i] = 0;
+            }
+            dirty = false;                       // (the range loop's barrier publishes it)
         }
         while (true) {
             __syncthreads();
@@ -869,6 +873,17 @@ hipError_t launch_tab_scatter2(const uint64_t *B1, const TabUnit *units, uint32_
 hipError_t launch_tab_starts(const uint64_t *H2s, const TabUnit *pfirst, uint64_t total, uint64_t *start,
                              hipStream_t s) {
     hipLaunchKernelGGL(tab_starts_kernel, dim3(TAB_NQ / 256), dim3(256), 0, s, H2s, pfirst, total, start);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void tab_segcopy_kernel(const uint64_t *src, const TabSeg *segs, uint64_t *dst) {
+    const TabSeg g = segs[blockIdx.x];
+    for (uint64_t i = threadIdx.x; i < g.len; i += 256) dst[g.dst + i] = src[g.src + i];
+}
+
+hipError_t launch_tab_segcopy(const uint64_t *src, const TabSeg *segs, uint32_t n, uint64_t *dst, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(tab_segcopy_kernel, dim3(n), dim3(256), 0, s, src, segs, dst);
     return hipGetLastError();
 }
 

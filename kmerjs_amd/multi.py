@@ -25,6 +25,14 @@ first-occurrence order).  Two ways to finish:
 * merge_to: gather every partial to one rank and finish there (one ordered
   result on one GPU; the gather and the merge grow with the rank count).
 
+Table mode (KMER_FLAG_UNORDERED / _CANONICAL, C3) shards the same way:
+finish_table_exchange sends each rank's pass-1 keys to the rank owning their
+slice of the hash space (kmer_table_exchange_prepare: 1024 partitions, rank o
+owns a contiguous 1024/world of them), ONE all-to-all of the keys plus an
+all-gather of the per-partition counts, and each owner runs pass 2 + the
+final kernel over its buckets (kmer_table_finish_exchanged).  Partitions are
+disjoint, so the ranks' table statistics add up (table_stats_all).
+
 Record (non-ACGT) keys are merged on the host of one rank with a small object
 gather.
 """
@@ -228,6 +236,58 @@ def finish_exchange(ctr, k, plen, total_lines, group=None, want_result=False, re
     ctr._keepalive = (recv,)
     return ctr.finish_exchanged(recv.data_ptr(), recv.numel() // 2, total_lines,
                                 stream=torch.cuda.current_stream(dev).cuda_stream, want_result=want_result)
+
+
+def table_part_range(o, world, parts=1024):
+    """Pass-1 partitions [lo, hi) owned by rank o (tab_part_lo, kmer_api.hip)."""
+    return o * parts // world, (o + 1) * parts // world
+
+
+def exchange_table_keys(send, counts, parts, group=None):
+    """The collectives of the table exchange: per-destination run lengths
+    (all-to-all), every rank's per-partition counts (all-gather), and the key
+    runs (all-to-all).  send = int64[sum(counts)] (runs in owner order);
+    returns (received runs by source rank, int64[world, len(parts)])."""
+    world = dist.get_world_size(group)
+    host_coll = dist.get_backend(group) == "gloo"
+    cdev = "cpu" if host_coll else send.device
+    send_n = torch.tensor(counts, dtype=torch.int64).to(cdev)
+    recv_n = torch.empty_like(send_n)
+    dist.all_to_all_single(recv_n, send_n, group=group)
+    mine = torch.tensor(parts, dtype=torch.int64).to(cdev)
+    allp = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(allp, mine, group=group)
+    recv_l = recv_n.cpu().tolist()
+    recv = exchange_runs(send, counts, recv_l, words=1, group=group)
+    return recv, torch.stack(allp).cpu()
+
+
+def finish_table_exchange(ctr, group=None, records=True, dst=0):
+    """Finish a sharded table-mode count (module docstring): afterwards every
+    rank holds its buckets of the table (kmer_table_device).  Record keys are
+    moved to rank `dst`, so table_stats_all counts each once."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    d_x, counts, parts = ctr.table_exchange_prepare(world)
+    n_send = sum(counts)
+    send = device_u64(d_x, n_send, dev) if n_send else torch.empty(0, dtype=torch.int64, device=dev)
+    recv, parts_all = exchange_table_keys(send, counts, parts, group=group)
+    if records:
+        gather_records(ctr, dst=dst, group=group)
+    # the table is written over `recv` (and read from it) on the context's
+    # stream after the collective: keep it alive until the next reset
+    ctr._keepalive = (recv,)
+    ctr.table_finish_exchanged(recv.data_ptr() if recv.numel() else 0, recv.numel(), parts_all.numpy(),
+                               world, rank, stream=torch.cuda.current_stream(dev).cuda_stream)
+
+
+def table_stats_all(ctr, group=None):
+    """(canonical, keys, total) of the whole sharded table: the ranks' shares summed."""
+    dev = "cpu" if dist.get_backend(group) == "gloo" else torch.device("cuda", torch.cuda.current_device())
+    t = torch.tensor(list(ctr.table_stats()), dtype=torch.int64, device=dev)
+    dist.all_reduce(t, group=group)
+    return tuple(int(x) for x in t.tolist())
 
 
 def finish_distributed(ctr, k, plen, total_lines, group=None, want_result=False, records=True, dst=0):

@@ -261,3 +261,61 @@ def test_gather_rows_alltoallv_gloo(world):
     assert cnt == [i + 10 * r for r in range(world) for i in range(ns[r])]
     assert fst == [i * world + r for r in range(world) for i in range(ns[r])]
     assert root
+
+
+def _table_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # a session's pass-1 keys: h grouped by partition (top 10 bits), as
+        # kmer_table_exchange_prepare lays them out (owner-major = partition-major)
+        rng = np.random.default_rng(7 + rank)
+        h = rng.integers(0, 1 << 63, size=5000 + 1000 * rank, dtype=np.int64) * 2 + rng.integers(0, 2, 1)
+        part = (h.view(np.uint64) >> np.uint64(54)).astype(np.int64)
+        order = np.argsort(part, kind="stable")
+        hs, ps = h[order], part[order]
+        parts = np.bincount(ps, minlength=1024)
+        counts = [int(parts[slice(*multi.table_part_range(o, world))].sum()) for o in range(world)]
+        recv, parts_all = multi.exchange_table_keys(torch.from_numpy(hs), counts, parts.tolist())
+        q.put(("ok", rank, recv.numpy().tolist(), parts_all.numpy().tolist()))
+    except Exception as e:  # pragma: no cover - surfaced through the queue
+        q.put(("err", rank, repr(e), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_table_exchange_collectives_gloo(world):
+    """Each rank receives exactly the pass-1 keys of its partitions, source
+    rank by source rank, partition-major, and every rank's partition table."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_table_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        status, rank, recv, parts_all = q.get(timeout=120)
+        assert status == "ok", recv
+        got[rank] = (recv, parts_all)
+    for p in procs:
+        p.join(timeout=60)
+    sent = []
+    for r in range(world):
+        rng = np.random.default_rng(7 + r)
+        h = rng.integers(0, 1 << 63, size=5000 + 1000 * r, dtype=np.int64) * 2 + rng.integers(0, 2, 1)
+        part = (h.view(np.uint64) >> np.uint64(54)).astype(np.int64)
+        order = np.argsort(part, kind="stable")
+        sent.append((h[order], part[order]))
+    for o in range(world):
+        lo, hi = multi.table_part_range(o, world)
+        want = np.concatenate([hs[(ps >= lo) & (ps < hi)] for hs, ps in sent])
+        recv, parts_all = got[o]
+        assert recv == want.tolist()
+        assert parts_all == [np.bincount(ps, minlength=1024).tolist() for _, ps in sent]
+    # the owners' ranges tile the 1024 partitions
+    assert [multi.table_part_range(o, world)[0] for o in range(world)] + [1024] == \
+        [0] + [multi.table_part_range(o, world)[1] for o in range(world)]

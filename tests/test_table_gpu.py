@@ -197,3 +197,112 @@ def test_canonical_mode_vs_oracle(native, golden, inputs, k, prefix):
     ctr.close()
     with pytest.raises(native.KmerError):          # canonical counts need a table-mode configuration
         native.Counter(k=16, prefix=b"N", flags=native.FLAG_CANONICAL)
+
+
+def _table_dump(native, ctr):
+    """The device table as sorted (h, count) arrays (kmer_table_device layout)."""
+    import torch
+    from kmerjs_amd.multi import _CudaArray, device_u64
+    nq = 1 << 20
+    e, st, ln, bg, nb = ctr.table_device()
+    if not e:
+        return np.zeros(0, np.uint64), np.zeros(0, np.uint64)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    start = device_u64(st, nq + 1, dev).cpu().numpy().view(np.uint64)
+    lens = torch.as_tensor(_CudaArray(ln, nq, "<i4"), device=dev).cpu().numpy().astype(np.int64)
+    tot = int(lens.sum())
+    ent = device_u64(e, int(start[-1]), dev).cpu().numpy().view(np.uint64)
+    q = np.repeat(np.arange(nq, dtype=np.uint64), lens)
+    first = np.cumsum(lens) - lens
+    idx = np.repeat(start[:-1].astype(np.int64), lens) + (np.arange(tot) - np.repeat(first, lens))
+    x = ent[idx]
+    h = (q << np.uint64(44)) | (x >> np.uint64(20))
+    cnt = x & np.uint64(0xFFFFF)
+    if nb:
+        big = device_u64(bg, 2 * nb, dev).cpu().numpy().view(np.uint64).reshape(-1, 2)
+        bigmap = dict(zip(big[:, 0].tolist(), big[:, 1].tolist()))
+        for i in np.nonzero(cnt == np.uint64(0xFFFFF))[0]:
+            cnt[i] = bigmap[int(h[i])]
+    o = np.argsort(h)
+    return h[o], cnt[o]
+
+
+@pytest.mark.parametrize("world,k,flags_name,with_n", [(2, 31, "FLAG_UNORDERED", False), (3, 21, "FLAG_CANONICAL", True),
+                                                       (1, 16, "FLAG_UNORDERED", True)])
+def test_table_exchange_matches_one_table(native, world, k, flags_name, with_n):
+    """Multi-GPU table mode in one process: `world` contexts count record-aligned
+    shards, their pass-1 keys are exchanged by owning partition range
+    (kmer_table_exchange_prepare / _finish_exchanged, the all-to-all done with
+    device copies), and the union of the owners' tables equals the one-context
+    table entry for entry; the ranks' statistics add up to its statistics."""
+    import torch
+    from kmerjs_amd import multi
+    from oracle import oracle
+    flags = getattr(native, flags_name)
+    n_reads = 150_000
+    if with_n:
+        rng = np.random.default_rng(k)
+        arr = np.frombuffer(bytearray(oracle.synth_fastq(5, 0, n_reads)), dtype=np.uint8).reshape(-1, 317).copy()
+        seq = arr[:, 13:163]
+        seq[rng.random(seq.shape) < 0.001] = ord("N")
+        arr[:, 13:163] = seq
+        buf = torch.from_numpy(arr.reshape(-1)).cuda()
+    else:
+        buf = _device_input(n_reads, seed=5)
+    one = native.Counter(k=k, prefix=b"", flags=flags)
+    one.reset()
+    one.feed_device(buf.data_ptr(), buf.numel())
+    one.finish(want_result=False)
+    want_h, want_c = _table_dump(native, one)
+    want_stats = one.table_stats()
+    one.close()
+    cuts = [317 * (n_reads * r // world) for r in range(world + 1)]
+    ctrs = [native.Counter(k=k, prefix=b"", flags=flags) for _ in range(world)]
+    sends = []
+    for r, c in enumerate(ctrs):
+        c.reset()
+        lo, hi = cuts[r], cuts[r + 1]
+        if r == 0:                                    # two chunks: the segment-copy path
+            mid = lo + 317 * ((hi - lo) // 634)
+            c.feed_device(buf.data_ptr() + lo, mid - lo)
+            c.feed_device(buf.data_ptr() + mid, hi - mid)
+        else:
+            c.feed_device(buf.data_ptr() + lo, hi - lo)
+        d, counts, parts = c.table_exchange_prepare(world)
+        assert sum(counts) == sum(parts)
+        from kmerjs_amd.multi import device_u64
+        keys = device_u64(d, sum(counts), buf.device).clone() if sum(counts) else torch.empty(0, dtype=torch.int64,
+                                                                                           device=buf.device)
+        sends.append((keys, counts, parts))
+    parts_all = np.array([p for _, _, p in sends], dtype=np.uint64)
+    # records (non-ACGT windows) move to rank 0, as multi.gather_records does
+    for c in ctrs[1:]:
+        kb, off, cnt, fst = c.records_export()
+        ctrs[0].records_import(kb, off, cnt, fst)
+        c.records_clear()
+    recvs = []
+    for o, c in enumerate(ctrs):
+        runs = []
+        for keys, counts, _ in sends:
+            a = sum(counts[:o])
+            runs.append(keys[a:a + counts[o]])
+        recv = torch.cat(runs) if runs else torch.empty(0, dtype=torch.int64, device=buf.device)
+        recvs.append(recv)
+        c.table_finish_exchanged(recv.data_ptr() if recv.numel() else 0, recv.numel(), parts_all, world, o,
+                                 stream=torch.cuda.current_stream().cuda_stream)
+    hs, cs, stats = [], [], np.zeros(3, dtype=np.int64)
+    for o, c in enumerate(ctrs):
+        h, cnt = _table_dump(native, c)
+        lo, hi = multi.table_part_range(o, world)
+        assert ((h >> np.uint64(54)) >= lo).all() and ((h >> np.uint64(54)) < hi).all()
+        hs.append(h)
+        cs.append(cnt)
+        stats += np.array(c.table_stats(), dtype=np.int64)
+    h = np.concatenate(hs)
+    cnt = np.concatenate(cs)
+    o = np.argsort(h)
+    assert np.array_equal(h[o], want_h) and np.array_equal(cnt[o], want_c)
+    assert tuple(stats.tolist()) == want_stats
+    for c in ctrs:
+        c.close()
+    del recvs
