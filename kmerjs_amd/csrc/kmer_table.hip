@@ -449,6 +449,9 @@ constexpr uint32_t TAB_SC = 1024;             // bucket starts cached in LDS per
 // between ranges: emission clears the slots it reads.  Grouping small buckets
 // divides the per-range fixed cost (barriers, key latency, the slot scan) by
 // the group size (canonical C5: ~1 K keys per bucket).
+#ifndef TAB_GROUPSORT
+#define TAB_GROUPSORT 0   // (experiment) the sort path for groups of small buckets too
+#endif
 constexpr uint32_t TAB_GMAX = 64;             // buckets per unit
 
 constexpr uint32_t TAB_SB = 4096;             // sort path: bins (top 12 remainder bits)
@@ -532,13 +535,16 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
     uint32_t cbase = q0;
     // the unit starting at bucket u: its end (uniform over the workgroup; the
     // start cache must hold u's start, i.e. u <= cbase + TAB_SC)
+    // (groups for the sort path fill the registers; the hash path's ranges
+    // split a group whose distinct keys overflow the table)
+    const uint64_t gk = TAB_GROUPSORT && !(a.ablate & 4) ? (uint64_t)TAB_REG_MAX : rk;
     auto unit_end = [&](uint32_t u) -> uint32_t {
         uint32_t e = u + 1;
         uint64_t tot = sc[u + 1 - cbase] - sc[u - cbase];
-        if (tot > rk) return e;
+        if (tot > gk) return e;
         while (e < q1 && e - cbase < TAB_SC && e - u < TAB_GMAX) {
             const uint64_t ne = sc[e + 1 - cbase] - sc[e - cbase];
-            if (tot + ne > rk) break;
+            if (tot + ne > gk) break;
             tot += ne;
             ++e;
         }
@@ -602,7 +608,10 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
         // plain LDS stores, instead of a CAS + a count add per key (plus
         // probes) and a slot scan per range.  A bucket with a crowded run of
         // bins (many copies of one key) takes the hash path below.
-        if (g == 1 && inreg && !(a.ablate & 4)) {
+        if ((TAB_GROUPSORT || g == 1) && inreg && !(a.ablate & 4)) {
+            // bins: the top 12 bits of (bucket offset << 44 | remainder), so a
+            // group's buckets occupy consecutive bin ranges
+            const uint32_t bsh = TAB_RBITS + (g > 1 ? 32 - __clz(g - 1) : 0) - 12;
             for (uint32_t i = t; i < TAB_SB; i += TAB_FWG) scnt[i] = 0;
             if (t == 0) smax = 0;
             __syncthreads();
@@ -612,7 +621,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
 #pragma unroll
                 for (int j = 0; j < TAB_KPT; ++j)
                     rank[j] = left > j * (int)TAB_FWG
-                                  ? atomicAdd(&scnt[(uint32_t)(kn[j] >> (TAB_RBITS - 12)) & (TAB_SB - 1)], 1u)
+                                  ? atomicAdd(&scnt[(uint32_t)(kn[j] >> bsh) & (TAB_SB - 1)], 1u)
                                   : 0u;
             }
             __syncthreads();
@@ -642,7 +651,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
 #pragma unroll
                     for (int j = 0; j < TAB_KPT; ++j)
                         if (left > j * (int)TAB_FWG)
-                            lbuf[sst[(uint32_t)(kn[j] >> (TAB_RBITS - 12)) & (TAB_SB - 1)] + rank[j]] = kn[j];
+                            lbuf[sst[(uint32_t)(kn[j] >> bsh) & (TAB_SB - 1)] + rank[j]] = kn[j];
                 }
                 // the registers are free: the next unit's keys load during the dedupe
                 if (more) load_keys(s0n, nn);
@@ -660,21 +669,27 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
                         uint32_t cnt = 1;
                         if (first)
                             for (uint32_t j = i + 1; j < st4[b] + c4[b]; ++j) cnt += lbuf[j] == x ? 1u : 0u;
-                        const unsigned long long fm = __ballot(first);
-                        if (fm) {
+                        // one counter bump per wave, key round and bucket present
+                        const uint32_t ql = (uint32_t)(x >> TAB_RBITS);
+                        unsigned long long fm = __ballot(first);
+                        uint32_t pos = 0;
+                        while (fm) {
                             const int ld = __ffsll((long long)fm) - 1;
+                            const uint32_t qx = (uint32_t)__shfl((int)ql, ld);
+                            const unsigned long long mq = __ballot(first && ql == qx);
                             uint32_t base = 0;
-                            if (lane == (uint32_t)ld) base = atomicAdd(&nout[0], (uint32_t)__popcll(fm));
+                            if (lane == (uint32_t)ld) base = atomicAdd(&nout[qx], (uint32_t)__popcll(mq));
                             base = (uint32_t)__shfl((int)base, ld);
-                            if (first) {
-                                const uint32_t pos = base + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
-                                a.out[s0 + pos] = (x << 20) | cnt;
-                                account(qbase | x, cnt);
-                            }
+                            if (first && ql == qx) pos = base + (uint32_t)__popcll(mq & ((1ull << lane) - 1ull));
+                            fm &= ~mq;
+                        }
+                        if (first) {
+                            a.out[sc[q + ql - cbase] + pos] = ((x & TAB_RMASK) << 20) | cnt;
+                            account(qbase + x, cnt);
                         }
                     }
                 __syncthreads();
-                if (t == 0) a.nd[q] = nout[0];
+                for (uint32_t i = t; i < g; i += TAB_FWG) a.nd[q + i] = nout[i];
                 dirty = true;                    // the hash path clears the table before use
                 if (prof) pt[4] += 1;
                 q = qn;
