@@ -449,9 +449,6 @@ constexpr uint32_t TAB_SC = 1024;             // bucket starts cached in LDS per
 // between ranges: emission clears the slots it reads.  Grouping small buckets
 // divides the per-range fixed cost (barriers, key latency, the slot scan) by
 // the group size (canonical C5: ~1 K keys per bucket).
-#ifndef TAB_GROUPSORT
-#define TAB_GROUPSORT 0   // (experiment) the sort path for groups of small buckets too
-#endif
 constexpr uint32_t TAB_GMAX = 64;             // buckets per unit
 
 constexpr uint32_t TAB_SB = 4096;             // sort path: bins (top 12 remainder bits)
@@ -537,7 +534,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
     // start cache must hold u's start, i.e. u <= cbase + TAB_SC)
     // (groups for the sort path fill the registers; the hash path's ranges
     // split a group whose distinct keys overflow the table)
-    const uint64_t gk = TAB_GROUPSORT && !(a.ablate & 4) ? (uint64_t)TAB_REG_MAX : rk;
+    const uint64_t gk = !(a.ablate & 4) ? (uint64_t)TAB_REG_MAX : rk;
     auto unit_end = [&](uint32_t u) -> uint32_t {
         uint32_t e = u + 1;
         uint64_t tot = sc[u + 1 - cbase] - sc[u - cbase];
@@ -601,14 +598,14 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
         if (prof)
             for (int j = 0; j < TAB_KPT; ++j) asm volatile("" ::"v"(kn[j]));   // (clock after the key loads)
         mark(0);
-        // Sort path (one bucket held in registers: C3's common case).  A
-        // counting sort of the bucket's remainders into 4,096 LDS bins by
-        // their top 12 bits, then every thread dedupes its 4 adjacent bins
-        // (~11 keys at C3) by comparison: one returning LDS atomic per key and
-        // plain LDS stores, instead of a CAS + a count add per key (plus
-        // probes) and a slot scan per range.  A bucket with a crowded run of
-        // bins (many copies of one key) takes the hash path below.
-        if ((TAB_GROUPSORT || g == 1) && inreg && !(a.ablate & 4)) {
+        // Sort path (any unit held in registers: one bucket at C3, a group of
+        // up to 64 small buckets at C5).  A counting sort of the unit's keys
+        // into 4,096 LDS bins by their top 12 bits, then every thread dedupes
+        // its 4 adjacent bins (~11 keys at C3) by comparison: one returning
+        // LDS atomic per key and plain LDS stores, instead of a CAS + a count
+        // add per key (plus probes) and a slot scan per range.  A unit with a
+        // crowded run of bins (many copies of one key) takes the hash path below.
+        if (inreg && !(a.ablate & 4)) {
             // bins: the top 12 bits of (bucket offset << 44 | remainder), so a
             // group's buckets occupy consecutive bin ranges
             const uint32_t bsh = TAB_RBITS + (g > 1 ? 32 - __clz(g - 1) : 0) - 12;
@@ -673,6 +670,14 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
                         const uint32_t ql = (uint32_t)(x >> TAB_RBITS);
                         unsigned long long fm = __ballot(first);
                         uint32_t pos = 0;
+                        if (g == 1 && fm) {              // (uniform) one bucket: one bump
+                            const int ld = __ffsll((long long)fm) - 1;
+                            uint32_t base = 0;
+                            if (lane == (uint32_t)ld) base = atomicAdd(&nout[0], (uint32_t)__popcll(fm));
+                            base = (uint32_t)__shfl((int)base, ld);
+                            pos = base + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
+                            fm = 0;
+                        }
                         while (fm) {
                             const int ld = __ffsll((long long)fm) - 1;
                             const uint32_t qx = (uint32_t)__shfl((int)ql, ld);
@@ -684,7 +689,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
                             fm &= ~mq;
                         }
                         if (first) {
-                            a.out[sc[q + ql - cbase] + pos] = ((x & TAB_RMASK) << 20) | cnt;
+                            a.out[(g == 1 ? s0 : sc[q + ql - cbase]) + pos] = ((x & TAB_RMASK) << 20) | cnt;
                             account(qbase + x, cnt);
                         }
                     }
