@@ -11,19 +11,22 @@
 //
 // Pipeline (hash-partitioned, every write pass coalesced; no global atomics
 // on the data path):
-//   pass 1  per sequence line, one window per lane: 2-bit planes by ballot,
-//           canonical code, h = tab_mix(code).  hist1 counts keys per
+//   pass 1  per sequence line, a run of 16 consecutive windows per lane: bit
+//           planes of the run's bytes (v_dot4 of aligned dwords), each window
+//           a shift of them, canonical code, h = tab_mix(code).  hist1 counts keys per
 //           (workgroup, top-10-bit partition) in LDS; scatter1 re-reads the
 //           input (1.3 B/window, cheaper than a key buffer), ranks each key in
 //           its partition with an LDS atomic, sorts a round of 16 K keys in LDS
 //           and writes each partition's run contiguously.
 //   pass 2  per run of a partition: the next 10 bits, same LDS sort -> B2 in
 //           2^20 buckets, contiguous per bucket.
-//   final   one persistent workgroup per CU, bucket by bucket: an LDS
-//           open-addressing table (8 K slots, CAS claim, atomic count) merges
-//           the bucket's keys across the workgroup's 16 waves; ranges that do
-//           not fit are split and redone.  Entries (remainder, count) are
-//           written back to the bucket's range; Map statistics on the fly.
+//   final   one persistent workgroup per CU, unit by unit (a bucket, or a
+//           group of small buckets): a counting sort of the unit's keys into
+//           4,096 LDS bins and a per-thread dedupe of adjacent bins; crowded
+//           units use an LDS open-addressing table (8 K slots, CAS claim,
+//           atomic count) with ranges split and redone when they do not fit.
+//           Entries (remainder, count) are written back to the bucket's range;
+//           Map statistics on the fly.
 #include "kmer_internal.hpp"
 
 namespace kmerhip {
@@ -67,17 +70,8 @@ __device__ __forceinline__ uint32_t block_excl_1024(uint32_t v, uint32_t *ws, ui
 __device__ __forceinline__ uint32_t readlane32(uint32_t v, uint32_t i) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)i);
 }
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t i) {
-    return (uint64_t)readlane32((uint32_t)v, i) | ((uint64_t)readlane32((uint32_t)(v >> 32), i) << 32);
-}
 
-// bits [s, s + 32) of the 128-bit value (hi:lo), s in [0, 64)
-__device__ __forceinline__ uint32_t funnel(uint64_t lo, uint64_t hi, uint32_t s) {
-    const uint64_t x = s ? (lo >> s) | (hi << (64 - s)) : lo;
-    return (uint32_t)x;
-}
 
-__device__ __forceinline__ bool is_acgt(uint32_t b) { return b == 'A' || b == 'C' || b == 'G' || b == 'T'; }
 
 // A wave's position in its workgroup's share of sequence lines.
 struct TabCur {
@@ -100,89 +94,103 @@ __device__ __forceinline__ void tab_record(const TabArgs &a, uint64_t pos, uint3
     }
 }
 
-// One round of a wave: up to TAB_RPL segments of 64 windows (one window per
-// lane) from this wave's lines.  Phase 1 finds the segments (descriptors of
-// the next 16 lines prefetched by lanes 0..15) and issues every byte load;
-// phase 2 forms the windows.  key[j] = h of the lane's window in segment j,
-// bit j of the result set iff that window is counted.  Non-ACGT windows
-// become records (rec).  Each lane loads bytes seg + lane and seg + 64 + lane
-// of the line (a window needs <= 64 + 31 bytes after seg).
+// One round of a wave: a lane takes NS CONSECUTIVE windows of one line.  Lanes are dealt out over the wave's next 16 lines
+// (ceil(windows left / NS) lanes per line); a lane loads the line bytes its
+// windows span as aligned dwords, turns them into three bit planes (lo / hi
+// base bits, non-ACGT) of up to 52 positions with v_dot4, and every window is
+// then a shift of the planes (a window-per-lane formation with six ballots and
+// funnels per window issued 2.5x the instructions: hist1 41.6 -> 23.1 ms,
+// scatter1 84.4 -> 64.2 ms at C3).  key[OFF + m] = h of the lane's window m,
+// bit m of the result set iff it is counted; non-ACGT windows become records
+// (rec).
 template <int NS, int OFF>
 __device__ __forceinline__ uint32_t tab_round(const TabArgs &a, TabCur &c, bool rec, uint64_t (&key)[TAB_RPL]) {
-    const int lane = threadIdx.x & 63;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t k = a.k;
+    // the next 16 lines of this wave (lane i < 16: line c.m + stride * i)
     SeqLine d;
     d.start = 0;
     d.len = 0;
-    {
-        const uint64_t mi = c.m + (uint64_t)c.stride * (uint32_t)(lane & 15);
-        if (lane < 16 && mi < c.end) d = a.lines[mi];
-    }
-    const uint32_t k = a.k;
+    const uint64_t mi = c.m + (uint64_t)c.stride * (lane & 15);
+    if (lane < 16 && mi < c.end) d = a.lines[mi];
+    const uint64_t W = d.len >= k ? d.len - k + 1 : 0;            // windows of the line
+    const uint64_t rem = lane == 0 ? (W > c.seg ? W - c.seg : 0) : W;
+    const uint32_t need = lane < 16 ? (uint32_t)((rem + NS - 1) / NS) : 0u;   // (<= 2^32 lanes: pieces are short)
+    const uint32_t cum = tab_incl_sum(need);                      // inclusive over lanes 0..15
+    const uint32_t tot = readlane32(cum, 15);
+    // this lane's line: the first i with cum_i > lane
     uint32_t li = 0;
-    uint64_t seg = c.seg;
-    uint32_t b0[NS], b1[NS], sli[NS];
-    uint64_t sseg[NS];
-    uint32_t have = 0;
 #pragma unroll
-    for (int j = 0; j < NS; ++j) {
-        // next line (from li on) that still has a segment at `seg`
-        uint64_t L = 0;
-        while (li < 16) {
-            if (c.m + (uint64_t)c.stride * li >= c.end) {
-                li = 16;
-                break;
-            }
-            L = readlane64(d.len, li);
-            if (L >= k && seg < L - k + 1) break;
-            ++li;
-            seg = 0;
-        }
-        b0[j] = b1[j] = 'A';
-        sli[j] = li;
-        sseg[j] = seg;
-        if (li < 16) {
-            const uint64_t st = readlane64(d.start, li);
-            have |= 1u << j;
-            const uint64_t i0 = seg + (uint32_t)lane, i1 = i0 + 64;
-            if (i0 < L) b0[j] = a.data[st + i0];
-            if (i1 < L) b1[j] = a.data[st + i1];
-            seg += 64;
-        }
-    }
-    if (li >= 16) {
+    for (uint32_t i = 0; i < 16; ++i) li += readlane32(cum, i) <= lane ? 1u : 0u;
+    const bool act = lane < tot && li < 16;
+    const uint32_t lsrc = li < 16 ? li : 15u;
+    const uint32_t before = (uint32_t)__shfl((int)(cum - need), (int)lsrc);
+    const uint64_t st = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)d.start, (int)lsrc)) |
+                        ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(d.start >> 32), (int)lsrc) << 32);
+    const uint64_t Wl = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)W, (int)lsrc)) |
+                        ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(W >> 32), (int)lsrc) << 32);
+    const uint64_t w0 = (li == 0 ? c.seg : 0) + (uint64_t)(lane - before) * NS;
+    // advance the cursor past what this round takes
+    if (tot <= 64) {
         c.m += (uint64_t)c.stride * 16;
         c.seg = 0;
     } else {
-        c.m += (uint64_t)c.stride * li;
-        c.seg = seg;
+        // line i* holds lane 63; it is done iff its last lane is lane 63
+        const uint32_t is = readlane32(li, 63);
+        const uint32_t ci = readlane32(cum, is), bi = ci - readlane32(need, is);
+        if (ci == 64) {
+            c.m += (uint64_t)c.stride * (is + 1);
+            c.seg = 0;
+        } else {
+            c.seg = (is == 0 ? c.seg : 0) + (uint64_t)(64 - bi) * NS;
+            c.m += (uint64_t)c.stride * is;
+        }
     }
+    // planes of the bytes [st + w0, st + w0 + NS + k - 1), from aligned dwords
+    uint64_t LO = 0, HI = 0, EX = 0;
+    const uint8_t *p = a.data + st + w0;
+    const uint32_t off = (uint32_t)((uintptr_t)p & 3u);
+    const uint32_t *pw = (const uint32_t *)(p - off);
+    const uint8_t *end = a.data + a.len;
+    constexpr int NDW = (NS + 31 + 3 + 3) / 4;
+#pragma unroll
+    for (int i = 0; i < NDW; ++i) {
+        uint32_t x = 0x41414141u;                                  // ('A': outside the line, never counted)
+        if (act && (const uint8_t *)(pw + i) < end && (uint32_t)(4 * i) < off + NS + k - 1) x = pw[i];
+        const uint32_t lo4 = __builtin_amdgcn_udot4((x ^ (x >> 1)) & 0x02020202u, 0x08040201u, 0u, false) >> 1;
+        const uint32_t hi4 = __builtin_amdgcn_udot4(x & 0x04040404u, 0x08040201u, 0u, false) >> 2;
+        const uint32_t cc = ((x >> 1) ^ (x >> 2)) & 0x03030303u;
+        const uint32_t ne = __builtin_amdgcn_perm(0u, 0x54474341u, cc) ^ x;      // 0 where the byte is A/C/G/T
+        const uint32_t nz = (((ne & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | ne) & 0x80808080u;
+        const uint32_t ex4 = __builtin_amdgcn_udot4(nz >> 7, 0x08040201u, 0u, false);
+        LO |= (uint64_t)lo4 << (4 * i);
+        HI |= (uint64_t)hi4 << (4 * i);
+        EX |= (uint64_t)ex4 << (4 * i);
+    }
+    LO >>= off;
+    HI >>= off;
+    EX >>= off;
     const uint32_t kmask = k >= 32 ? ~0u : ((1u << k) - 1u);
     const uint32_t sh = 32 - k;
     uint32_t valid = 0;
 #pragma unroll
-    for (int j = 0; j < NS; ++j) {
-        if (!(have & (1u << j))) continue;      // (wave-uniform)
-        const uint32_t x0 = b0[j], x1 = b1[j];
-        const uint64_t l0 = __ballot(((x0 >> 1) ^ (x0 >> 2)) & 1u), l1 = __ballot(((x1 >> 1) ^ (x1 >> 2)) & 1u);
-        const uint64_t h0 = __ballot((x0 >> 2) & 1u), h1 = __ballot((x1 >> 2) & 1u);
-        const uint64_t e0 = __ballot(!is_acgt(x0)), e1 = __ballot(!is_acgt(x1));
-        const uint64_t s = sseg[j] + (uint32_t)lane;
-        if (s >= readlane64(d.len, sli[j]) - k + 1) continue;   // past the line's last window
-        const uint32_t flo = funnel(l0, l1, lane) & kmask, fhi = funnel(h0, h1, lane) & kmask;
-        const uint32_t fx = funnel(e0, e1, lane) & kmask;
+    for (int m = 0; m < NS; ++m) {
+        if (!act || w0 + m >= Wl) continue;
+        const uint32_t flo = (uint32_t)(LO >> m) & kmask, fhi = (uint32_t)(HI >> m) & kmask;
+        const uint32_t fx = (uint32_t)(EX >> m) & kmask;
         const uint32_t rlo = __brev(~flo & kmask) >> sh, rhi = __brev(~fhi & kmask) >> sh, rx = __brev(fx) >> sh;
         const bool fm = (((flo ^ a.plo) | (fhi ^ a.phi) | fx) & a.pmask) == 0;   // w starts with P
         const bool rm = (((rlo ^ a.plo) | (rhi ^ a.phi) | rx) & a.pmask) == 0;   // rc(w) starts with P
         if (fx == 0) {
             if (fm || rm) {
                 const uint64_t cf = ((uint64_t)fhi << k) | flo, cr = ((uint64_t)rhi << k) | rlo;
-                key[OFF + j] = tab_mix(cf < cr ? cf : cr);
-                valid |= 1u << j;
+                key[OFF + m] = tab_mix(cf < cr ? cf : cr);
+                valid |= 1u << m;
             }
         } else if (rec) {
-            const uint64_t pos = readlane64(d.start, sli[j]) + s;
+            const uint64_t pos = st + w0 + m;
             if (a.canonical) {
-                tab_record(a, pos, 0);           // every forward window: classed on the host
+                tab_record(a, pos, 0);
             } else {
                 if (fm) tab_record(a, pos, 0);
                 if (rm) tab_record(a, pos, 1);
@@ -237,8 +245,7 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter1_kernel(TabArgs a) {
         uint64_t key[TAB_RPL];
         uint32_t rank[TAB_RPL];
         uint32_t v = 0;
-        if (c.m < c.end) v = tab_round<TAB_RPL / 2, 0>(a, c, true, key);
-        if (c.m < c.end) v |= tab_round<TAB_RPL / 2, TAB_RPL / 2>(a, c, true, key);
+        if (c.m < c.end) v = tab_round<TAB_RPL, 0>(a, c, true, key);
 #pragma unroll
         for (int j = 0; j < TAB_RPL; ++j)
             rank[j] = (v & (1u << j)) ? atomicAdd(&bcnt[key[j] >> (64 - TAB_L1)], 1u) : 0u;
