@@ -226,6 +226,14 @@ kmer_status kmer_table_stats(kmer_ctx *ctx, uint64_t *canonical, uint64_t *keys,
  * big = n_big {uint64 h, uint64 count} pairs.  Valid until the next reset. */
 kmer_status kmer_table_device(kmer_ctx *ctx, const void **d_entries, const void **d_bucket_start,
                               const void **d_bucket_len, const void **d_big, uint64_t *n_big);
+/* Linear digest of the table (after a finish): sum over its canonical entries
+ * of count x mix(h) mod 2^64, mix = the splitmix64 finalizer
+ * (z ^= z >> 30; z *= 0xBF58476D1CE4E5B9; z ^= z >> 27; z *= 0x94D049BB133111EB;
+ * z ^= z >> 31).  Linear in the counts: the digest of a count over input
+ * A + B is the sum of the digests over A and over B, and the ranks' digests
+ * of an exchanged table add up -- a size-independent check of a table that is
+ * too large to compare entry by entry.  Record keys are not included. */
+kmer_status kmer_table_digest(kmer_ctx *ctx, uint64_t *digest);
 /* Table mode across ranks (replaces the one Map.set stream of lib/kmers.js:95
  * when the count is sharded over GPUs; reads are independent, :151-155).
  * Rank o (of `world` <= 1024) owns the pass-1 partitions [o*1024/world,

@@ -54,6 +54,10 @@ kmer_status kmer_db_open(int32_t device, uint32_t k, const char *keys, uint64_t 
 /* distinct = distinct k-mers, entries = (k-mer, template) pairs after dedup. */
 kmer_status kmer_db_info(const kmer_db *db, uint32_t *k, uint32_t *n_templates, uint64_t *distinct,
                          uint64_t *entries);
+/* Matches of the DB that are still open keep it alive: its device data is then
+ * freed by the last kmer_match_close.  Do not pass `db` to any call afterwards
+ * (offsets passed to kmer_match_open must start at 0 and not decrease:
+ * KMER_E_BAD_PARAM otherwise). */
 kmer_status kmer_db_close(kmer_db *db);
 
 /* Round 1 (findKmersMatchesRedis): a query Map in iteration order — key i =

@@ -32,7 +32,7 @@ EXPORTS = ["kmer_open", "kmer_close", "kmer_count_file", "kmer_count_buffer", "k
            "kmer_lines", "kmer_result_size", "kmer_result_lines", "kmer_result_get",
            "kmer_result_arrays", "kmer_result_firsts", "kmer_result_write", "kmer_result_free",
            "kmer_synth_fastq_device",
-           "kmer_last_timing", "kmer_phase_times", "kmer_table_stats", "kmer_table_device",
+           "kmer_last_timing", "kmer_phase_times", "kmer_table_stats", "kmer_table_digest", "kmer_table_device",
            "kmer_table_exchange_prepare", "kmer_table_finish_exchanged",
            "kmer_status_string", "kmer_last_error", "kmer_version"]
 # include/kmer_match.h (the template matcher, same library)
@@ -113,6 +113,7 @@ def _load():
         "kmer_phase_times": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_char_p),
                                             ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32)]),
         "kmer_table_stats": (ctypes.c_int, [vp, pu64, pu64, pu64]),
+        "kmer_table_digest": (ctypes.c_int, [vp, pu64]),
         "kmer_table_device": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp),
                                              ctypes.POINTER(vp), pu64]),
         "kmer_table_exchange_prepare": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.POINTER(vp), pu64, pu64]),
@@ -355,6 +356,12 @@ class Counter:
         a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
         self._check(LIB.kmer_table_stats(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "table_stats")
         return a.value, b.value, c.value
+
+    def table_digest(self):
+        """kmer_table_digest: linear digest of the table (sum of count x mix(h))."""
+        d = ctypes.c_uint64()
+        self._check(LIB.kmer_table_digest(self.h, ctypes.byref(d)), "table_digest")
+        return d.value
 
     def table_device(self):
         """Table mode: (d_entries, d_bucket_start, d_bucket_len, d_big, n_big) in device memory."""

@@ -198,7 +198,7 @@ struct kmer_ctx {
     DBuf<uint32_t> tpc;            // pieces per sequence line (long lines)
     DBuf<uint64_t> tpb;            // ... their scan
     DBuf<SeqLine> tpieces;         // long lines cut into pieces of <= TAB_PIECE windows
-    DBuf<unsigned long long> tstats;   // [0..2] final statistics, [3] big-list count
+    DBuf<unsigned long long> tstats;   // [0..2] final statistics, [3] big-list count, [4] digest
     uint64_t t_keys = 0;           // pass-1 keys of the session
     std::vector<uint64_t> t_cbase; // per chunk: first key in tb1
     std::vector<std::vector<uint64_t>> t_coff;   // per chunk: TAB_NB + 1 partition starts (chunk-relative)
@@ -1074,7 +1074,7 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1 = nullptr, uint32_t qlo
     HIPCHK(c, c->tstart.ensure(TAB_NQ + 1, s));
     HIPCHK(c, c->tnd.ensure(TAB_NQ, s));
     HIPCHK(c, c->tbig.ensure(1 << 16, s));
-    HIPCHK(c, c->tstats.ensure(4, s));
+    HIPCHK(c, c->tstats.ensure(5, s));
     HIPCHK(c, hipEventRecord(c->tev[4], s));
     HIPCHK(c, launch_tab_hist2(B1, c->tunits.p, (uint32_t)n_units, c->tH.p, s));
     ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tH.p, c->tHs.p, (uint64_t)0, (size_t)nh,
@@ -2551,6 +2551,28 @@ kmer_status kmer_table_device(kmer_ctx *c, const void **d_entries, const void **
     if (d_bucket_len) *d_bucket_len = any ? c->tnd.p : nullptr;
     if (d_big) *d_big = any ? c->tbig.p : nullptr;
     if (n_big) *n_big = c->t_nbig;
+    return KMER_OK;
+}
+
+kmer_status kmer_table_digest(kmer_ctx *c, uint64_t *digest) {
+    if (!c || !digest) return KMER_E_BAD_PARAM;
+    SETTLE(c);
+    if (c->mode != MODE_TABLE) return fail(c, KMER_E_STATE, "not a table-mode context (KMER_FLAG_UNORDERED)");
+    if (!c->t_done) return fail(c, KMER_E_STATE, "no table finish yet");
+    *digest = 0;
+    if (!c->t_keys) return KMER_OK;
+    hipStream_t s = c->stream;
+    unsigned long long *d = c->tstats.p + 4;
+    HIPCHK(c, hipMemsetAsync(d, 0, 8, s));
+    HIPCHK(c, launch_tab_digest(c->t_ent, c->tstart.p, c->tnd.p, d, s));
+    uint64_t acc = 0;
+    std::vector<TabBig> big(c->t_nbig);
+    HIPCHK(c, hipMemcpyAsync(&acc, d, 8, hipMemcpyDeviceToHost, s));
+    if (!big.empty())
+        HIPCHK(c, hipMemcpyAsync(big.data(), c->tbig.p, big.size() * sizeof(TabBig), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    for (const TabBig &b : big) acc += (b.count - TAB_CMAX) * tab_digest_mix(b.h);   // entries hold TAB_CMAX
+    *digest = acc;
     return KMER_OK;
 }
 

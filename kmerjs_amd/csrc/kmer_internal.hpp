@@ -367,6 +367,14 @@ constexpr uint32_t TAB_CAP = 7000;                     // distinct keys per rang
 // top bits -- partition and bucket -- depend on every bit of the code
 constexpr uint64_t TAB_MUL = 0x9E3779B97F4A7C15ull;
 __host__ __device__ inline uint64_t tab_mix(uint64_t x) { return x * TAB_MUL; }
+// Table digest weight of a key h: the splitmix64 finalizer (kmer_table_digest)
+__host__ __device__ inline uint64_t tab_digest_mix(uint64_t h) {
+    h ^= h >> 30;
+    h *= 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 27;
+    h *= 0x94D049BB133111EBull;
+    return h ^ (h >> 31);
+}
 
 struct TabArgs {
     const uint8_t *data;
@@ -432,6 +440,8 @@ hipError_t launch_tab_scatter2(const uint64_t *B1, const TabUnit *units, uint32_
 hipError_t launch_tab_starts(const uint64_t *H2s, const TabUnit *pfirst, uint64_t total, uint64_t *start,
                              hipStream_t s);
 hipError_t launch_tab_final(const TabFinal &a, uint32_t grid, hipStream_t s);
+hipError_t launch_tab_digest(const uint64_t *ent, const uint64_t *start, const uint32_t *nd, unsigned long long *out,
+                             hipStream_t s);
 // multi-GPU table exchange: copy n segments {src offset, dst offset, length}
 // of u64 keys (one workgroup per segment, grid-strided)
 struct TabSeg {

@@ -396,6 +396,8 @@ struct kmer_db {
     Temp tmp;
     MatchBufs spare;                           // buffers of the last closed match
     bool has_spare = false;
+    uint32_t live = 0;                         // open matches
+    bool closing = false;                      // kmer_db_close called while matches were open
 };
 
 struct kmer_match {
@@ -587,12 +589,14 @@ kmer_status match_build(kmer_match *m, const uint8_t *dkeys, const uint64_t *dof
 
 kmer_status match_open_common(kmer_db *db, uint64_t n, kmer_match **out, kmer_match **mm) {
     if (!db || !out) return set_err(KMER_E_BAD_PARAM, "kmer_match_open: NULL argument");
+    if (db->closing) return set_err(KMER_E_STATE, "kmer_match_open: the DB is closed");
     if (n >= NONE) return set_err(KMER_E_BAD_PARAM, "kmer_match_open: more than 2^32 - 2 query keys");
     *out = nullptr;
     MCHK(hipSetDevice(db->device));
     kmer_match *m = new kmer_match();
     m->db = db;
     m->n = n;
+    ++db->live;
     if (db->has_spare) {                        // the last closed match's buffers
         m->b = db->spare;
         db->spare = MatchBufs();
@@ -655,6 +659,10 @@ kmer_status kmer_db_info(const kmer_db *db, uint32_t *k, uint32_t *n_templates, 
 }
 
 kmer_status kmer_db_close(kmer_db *db) {
+    if (db && db->live) {   // a match reads the DB's CSR and hands its buffers back at close:
+        db->closing = true;  // the last kmer_match_close frees the DB
+        return KMER_OK;
+    }
     free_db(db);
     return KMER_OK;
 }
@@ -662,6 +670,10 @@ kmer_status kmer_db_close(kmer_db *db) {
 kmer_status kmer_match_open(kmer_db *db, const char *keys, const uint64_t *offsets, const uint64_t *counts,
                             uint64_t n, kmer_match **out) {
     if (n && (!keys || !offsets || !counts)) return set_err(KMER_E_BAD_PARAM, "kmer_match_open: NULL argument");
+    if (n && offsets[0] != 0) return set_err(KMER_E_BAD_PARAM, "kmer_match_open: offsets[0] must be 0");
+    for (uint64_t i = 0; i < n; ++i)    // q_lookup_kernel packs keys + offsets[i] .. offsets[i + 1]
+        if (offsets[i + 1] < offsets[i])
+            return set_err(KMER_E_BAD_PARAM, "kmer_match_open: offsets must not decrease");
     kmer_match *m = nullptr;
     kmer_status st = match_open_common(db, n, out, &m);
     if (st != KMER_OK) return st;
@@ -678,6 +690,7 @@ kmer_status kmer_match_open(kmer_db *db, const char *keys, const uint64_t *offse
     (void)hipStreamSynchronize(db->s);
     if (st != KMER_OK) {
         m->release();
+        --m->db->live;
         delete m;
         return st;
     }
@@ -704,6 +717,7 @@ kmer_status kmer_match_open_device(kmer_db *db, const void *d_keys, uint32_t kle
     if (ev) (void)hipEventDestroy(ev);
     if (st != KMER_OK) {
         m->release();
+        --m->db->live;
         delete m;
         return st;
     }
@@ -829,8 +843,10 @@ kmer_status kmer_match_close(kmer_match *m) {
     if (!m) return KMER_OK;
     (void)hipSetDevice(m->db->device);
     (void)hipStreamSynchronize(m->db->s);
+    kmer_db *db = m->db;
     m->release();
     delete m;
+    if (--db->live == 0 && db->closing) free_db(db);
     return KMER_OK;
 }
 

@@ -914,6 +914,32 @@ hipError_t launch_tab_segcopy(const uint64_t *src, const TabSeg *segs, uint32_t 
     return hipGetLastError();
 }
 
+// Linear digest of a table: sum over entries of count x tab_digest_mix(h)
+// (mod 2^64; counts >= TAB_CMAX are corrected on the host from the big list).
+// One wave per bucket; one atomic per wave.
+__global__ __launch_bounds__(256) void tab_digest_kernel(const uint64_t *ent, const uint64_t *start,
+                                                         const uint32_t *nd, unsigned long long *out) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
+    uint64_t acc = 0;
+    for (uint32_t q = wv; q < TAB_NQ; q += nw) {
+        const uint64_t s0 = start[q];
+        const uint32_t n = nd[q];
+        for (uint32_t i = lane; i < n; i += 64) {
+            const uint64_t w = ent[s0 + i];
+            acc += (w & TAB_CMAX) * tab_digest_mix(((uint64_t)q << TAB_RBITS) | (w >> 20));
+        }
+    }
+    for (int d = 32; d >= 1; d >>= 1) acc += (uint64_t)__shfl_xor((long long)acc, d);
+    if (lane == 0 && acc) atomicAdd(out, (unsigned long long)acc);
+}
+
+hipError_t launch_tab_digest(const uint64_t *ent, const uint64_t *start, const uint32_t *nd, unsigned long long *out,
+                             hipStream_t s) {
+    hipLaunchKernelGGL(tab_digest_kernel, dim3(4096), dim3(256), 0, s, ent, start, nd, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_tab_final(const TabFinal &a, uint32_t grid, hipStream_t s) {
     hipLaunchKernelGGL(tab_final_kernel, dim3(grid), dim3(TAB_FWG), 0, s, a);
     return hipGetLastError();

@@ -7,9 +7,11 @@ standardScoring (:857-874) over findMatchesMongoAggregation (:452-522),
 matchSummary (:625-676); lib/stats.js zScore (:19-45) and fastp (:52-115).
 The joins and re-scoring run on the GPU; the statistics of a winner are
 scalar decimal arithmetic done here with bignumber.js 2.x semantics
-(package.json:61): dividedBy and sqrt round to 20 decimal places half up,
-plus / minus / times are exact, round(dp, 6) is half-even, toNumber parses the
-decimal string.
+(package.json:61) under the reference's BN.config({ROUNDING_MODE: 2})
+(lib/kmerFinderServer.js:7, the constructor lib/stats.js shares): dividedBy
+and sqrt round to 20 decimal places with ROUND_CEIL, a bare round(dp) is a
+ceiling, plus / minus / times are exact, round(dp, 6) is half-even, toNumber
+parses the decimal string.
 
 A template is a dict {'sequence', 'lengths', 'ulength', 'species', 'kmers'}
 (the ETL's Mongo document, src/kmerPyToMongo.py:36-42, with `reads` as
@@ -75,32 +77,36 @@ class Dec:
         return (a > b) - (a < b)
 
     def div(self, o, dp=DP):
-        """dividedBy: rounded to dp places, half away from zero."""
+        """dividedBy: rounded to dp places, ROUND_CEIL (towards +infinity)."""
         o = Dec.of(o)
         num, den = self.n * 10 ** (dp + o.s), o.n * 10 ** self.s
         neg = (num < 0) != (den < 0)
         q, r = divmod(abs(num), abs(den))
-        if 2 * r >= abs(den):
+        if r and not neg:
             q += 1
         return Dec(-q if neg else q, dp)
 
     def sqrt(self, dp=DP):
-        """sqrt rounded to dp places, half up (self >= 0)."""
+        """sqrt rounded to dp places, ROUND_CEIL (self >= 0)."""
         # y = self * 10^(2 dp) = n * 10^(2dp - s); t = floor(sqrt(y))
         e = 2 * dp - self.s
         num, den = (self.n * 10 ** e, 1) if e >= 0 else (self.n, 10 ** -e)
         t = math.isqrt(num // den)
-        if 4 * num >= (2 * t + 1) ** 2 * den:       # sqrt(y) >= t + 1/2
+        if t * t * den != num:                       # sqrt(y) is not t exactly
             t += 1
         return Dec(t, dp)
 
     def round(self, dp, half_even=False):
+        """round(dp, 6) with half_even, else round(dp): ROUND_CEIL."""
         if self.s <= dp:
             return self
         d = 10 ** (self.s - dp)
         neg = self.n < 0
         q, r = divmod(abs(self.n), d)
-        if 2 * r > d or (2 * r == d and (not half_even or q % 2 == 1)):
+        if half_even:
+            if 2 * r > d or (2 * r == d and q % 2 == 1):
+                q += 1
+        elif r and not neg:
             q += 1
         return Dec(-q if neg else q, dp)
 
@@ -204,8 +210,10 @@ class TemplateDB:
         return {"k": k.value, "templates": nt.value, "distinct": d.value, "entries": e.value}
 
     def close(self):
+        """Matches of the DB that are still open keep its device data until
+        they close (kmer_db_close defers the free to the last one)."""
         if getattr(self, "handle", None):
-            LIB.kmer_db_close(self.handle)
+            _check(LIB.kmer_db_close(self.handle), "kmer_db_close")
             self.handle = None
 
     def __del__(self):

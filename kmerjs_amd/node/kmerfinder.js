@@ -13,8 +13,10 @@
  *     rejected ones (undefined) last.
  * The joins and re-scoring run on the GPU; the statistics (lib/stats.js zScore,
  * fastp) are bignumber.js 2.x decimal arithmetic (package.json:61), restated
- * exactly with BigInt below: dividedBy / sqrt round to 20 places half up,
- * plus / minus / times are exact, round(dp, 6) is half-even.
+ * exactly with BigInt below.  lib/kmerFinderServer.js:7 sets BN.config({
+ * ROUNDING_MODE: 2 }) on the one bignumber.js constructor lib/stats.js shares,
+ * so dividedBy / sqrt round to 20 places with ROUND_CEIL and a bare round(dp)
+ * is a ceiling; plus / minus / times are exact, round(dp, 6) is half-even.
  *
  * The template DB: the reference reads Redis (kmer -> [template JSON]) or
  * MongoDB (the ETL's documents, src/kmerPyToMongo.py:36-42), neither of which
@@ -67,7 +69,7 @@ class Dec {
 
     cmp(o) { const [a, b] = this._al(o); return a > b ? 1 : a < b ? -1 : 0; }
 
-    // dividedBy: DP places, half away from zero
+    // dividedBy: DP places, ROUND_CEIL (towards +Infinity)
     div(o) {
         o = Dec.of(o);
         const num = this.n * pow10(DP + o.s);
@@ -76,29 +78,34 @@ class Dec {
         const an = babs(num);
         const ad = babs(den);
         let q = an / ad;
-        if (BigInt(2) * (an % ad) >= ad) q += BigInt(1);
+        if (!neg && an % ad !== BigInt(0)) q += BigInt(1);
         return new Dec(neg ? -q : q, DP);
     }
 
-    // sqrt: DP places, half up (this >= 0)
+    // sqrt: DP places, ROUND_CEIL (this >= 0)
     sqrt() {
         const e = 2 * DP - this.s;
         const num = e >= 0 ? this.n * pow10(e) : this.n;
         const den = e >= 0 ? BigInt(1) : pow10(-e);
         let t = isqrt(num / den);
-        const two = BigInt(2);
-        if (BigInt(4) * num >= (two * t + BigInt(1)) ** two * den) t += BigInt(1);
+        if (t * t * den !== num) t += BigInt(1);
         return new Dec(t, DP);
     }
 
-    round(dp, mode) {                 // mode 6: half-even; otherwise half-up (ROUNDING_MODE 4)
+    // mode 6: half-even; omitted: the configured ROUNDING_MODE, ROUND_CEIL
+    round(dp, mode) {
         if (this.s <= dp) return this;
         const d = pow10(this.s - dp);
         const neg = this.n < BigInt(0);
         const a = babs(this.n);
         let q = a / d;
-        const r2 = BigInt(2) * (a % d);
-        if (r2 > d || (r2 === d && (mode !== 6 || q % BigInt(2) === BigInt(1)))) q += BigInt(1);
+        const r = a % d;
+        if (mode === 6) {
+            const r2 = BigInt(2) * r;
+            if (r2 > d || (r2 === d && q % BigInt(2) === BigInt(1))) q += BigInt(1);
+        } else if (!neg && r !== BigInt(0)) {
+            q += BigInt(1);
+        }
         return new Dec(neg ? -q : q, dp);
     }
 

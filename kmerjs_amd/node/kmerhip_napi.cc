@@ -309,7 +309,8 @@ struct MatchHandle {
 
 void finalize_db(napi_env, void *data, void *) {
     DbHandle *h = static_cast<DbHandle *>(data);
-    if (h->db) kmer_db_close(h->db);
+    // open matches keep the DB alive: kmer_db_close defers to the last match
+    if (h->db) (void)kmer_db_close(h->db);
     delete h;
 }
 
@@ -427,8 +428,8 @@ napi_value DbClose(napi_env env, napi_callback_info info) {
     NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
     DbHandle *h = get_ext<DbHandle>(env, argv[0], "invalid db handle");
     if (!h) return nullptr;
-    // matches hold a reference to the db's JS object, not to kmer_db: the
-    // caller closes its matches first (kmerfinder.js does)
+    // with matches of the DB still open, kmer_db_close defers the free to the
+    // last kmer_match_close (matchOpen on this handle then throws 'db closed')
     if (h->db) kmer_db_close(h->db);
     h->db = nullptr;
     napi_value u;

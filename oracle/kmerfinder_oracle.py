@@ -14,9 +14,11 @@ What it restates (file:line in the reference tree):
 * 'standard' scoring (Mongo aggregation, :452-522, :857-874): every template
   with hits, in DB order, summarised and sorted by score;
 * lib/stats.js zScore (:19-45) and fastp (:52-115) on bignumber.js 2.x
-  (package.json:61 "^2.3.0"; absent from this image): dividedBy and sqrt round
-  to DECIMAL_PLACES = 20 with ROUNDING_MODE 4 (half up = half away from zero),
-  plus / minus / times are exact, round(dp, 6) is half-even, round(dp) half-up,
+  (package.json:61 "^2.3.0"; absent from this image) as the reference
+  configures it: lib/kmerFinderServer.js:7 runs BN.config({ROUNDING_MODE: 2})
+  on the constructor lib/stats.js shares, so dividedBy and sqrt round to
+  DECIMAL_PLACES = 20 with ROUND_CEIL (towards +infinity) and a bare round(dp)
+  is a ceiling; plus / minus / times are exact, round(dp, 6) is half-even,
   toNumber parses the decimal string.  Restated here with exact Fractions.
 
 Choices the reference leaves open (documented in DESIGN.md): the template list
@@ -54,13 +56,16 @@ class NoHits(Exception):
 
 # -- bignumber.js 2.x arithmetic ---------------------------------------------
 def bn_round(x, dp, half_even=False):
+    """round(dp, 6) when half_even, else ROUND_CEIL (the configured mode)."""
     s = 10 ** dp
-    v = x * s
+    v = Fraction(x) * s
+    if not half_even:
+        return Fraction(math.ceil(v), s)
     neg = v < 0
     a = -v if neg else v
     fl = a.numerator // a.denominator
     rem = a - fl
-    if rem > HALF or (rem == HALF and (not half_even or fl % 2 == 1)):
+    if rem > HALF or (rem == HALF and fl % 2 == 1):
         fl += 1
     return Fraction(-fl if neg else fl, s)
 
@@ -70,10 +75,10 @@ def bn_div(a, b):
 
 
 def bn_sqrt(x):
-    """sqrt rounded to 20 dp, half up (x >= 0)."""
+    """sqrt rounded to 20 dp, ROUND_CEIL (x >= 0)."""
     y = Fraction(x) * 10 ** (2 * DP)
     t = math.isqrt(y.numerator // y.denominator)         # floor(sqrt(y))
-    if y >= t * t + t + Fraction(1, 4):                    # sqrt(y) >= t + 1/2
+    if t * t != y:                                         # not exact: round up
         t += 1
     return Fraction(t, 10 ** DP)
 

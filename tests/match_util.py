@@ -74,3 +74,61 @@ def make_query(seed, templates, present, frac=0.6, noise=200, k=16, prefix="ATGA
     items = list(q.items())
     rng.shuffle(items)
     return dict(items)
+
+
+# -- the reference's matchSummary KAT (test/kmerFinderServer.js:57-82) ---------
+# Its inputs are fixtures the reference holds: the query test_data/kmers_long.json
+# (6,191 keys), the first-round state test_data/db_long_results.json (per template
+# uScore `templateentries`, tScore `templateentriestot`, `hits`) and
+# test_data/summary.json.  The template DB itself (Redis) is not in the tree, so
+# kat_db() builds one whose first round against the query reproduces that state
+# exactly: template T gets uScore(T) distinct query k-mers whose counts sum to
+# tScore(T).  Only the winner's ulength (4,881) is pinned by the KAT; `lengths`
+# is not in any fixture (any value in 9,852..10,128 gives the KAT's depth 0.36).
+KAT = {"template": "NC_017625", "score": 2295, "expected": 108, "z": 211.00, "probability": 5.03e-23,
+       "frac-q": 74.14, "frac-d": 47.02, "depth": 0.36, "total-frac-q": 74.14, "total-frac-d": 47.02,
+       "total-temp-cover": 0.36, "kmers-template": 4881, "species": "Escherichia coli DH1"}
+KAT_LENGTHS = 10000
+
+
+def kat_fixtures(golden_dir):
+    import json
+    import os
+    with open(os.path.join(golden_dir, "kmers_long.json")) as f:
+        query = json.load(f)
+    with open(os.path.join(golden_dir, "db_long_results.json")) as f:
+        res = json.load(f)
+    with open(os.path.join(golden_dir, "summary.json")) as f:
+        summary = json.load(f)
+    return query, res, summary
+
+
+def kat_db(query, res, seed=17):
+    """Templates (in db_long_results order) reproducing its first round."""
+    rng = np.random.default_rng(seed)
+    keys = list(query)
+    by_extra = {}
+    for km in keys:
+        by_extra.setdefault(query[km] - 1, []).append(km)
+    extras = sorted(e for e in by_extra if e > 0)
+    out = []
+    for name, u in res["templateentries"].items():
+        e_left = res["templateentriestot"][name] - u
+        picks = []
+        # k-mers with count > 1 carry the extra, largest first while they fit
+        for e in reversed(extras):
+            pool = by_extra[e]
+            order = rng.permutation(len(pool))
+            for i in order:
+                if e > e_left or len(picks) >= u:
+                    break
+                picks.append(pool[i])
+                e_left -= e
+        assert e_left == 0 and len(picks) <= u, name
+        ones = by_extra[0]
+        picks += [ones[i] for i in rng.choice(len(ones), size=u - len(picks), replace=False)]
+        ul = 4881 if name == KAT["template"] else u + int(rng.integers(0, 3 * u + 10))
+        out.append({"sequence": name, "lengths": KAT_LENGTHS if name == KAT["template"] else 2 * ul + 7,
+                    "ulength": ul, "species": KAT["species"] if name == KAT["template"] else "sp " + name,
+                    "kmers": picks})
+    return out

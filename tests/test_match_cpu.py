@@ -37,8 +37,8 @@ def test_round_ties():
     from kmerjs_amd.kmerfinder import Dec
     assert Dec(125, 3).round(2, True).to_number() == 0.12         # half-even
     assert Dec(135, 3).round(2, True).to_number() == 0.14
-    assert Dec(125, 3).round(2).to_number() == 0.13               # half-up
-    assert Dec(-125, 3).round(2).to_number() == -0.13             # away from zero
+    assert Dec(121, 3).round(2).to_number() == 0.13               # ROUND_CEIL (lib/kmerFinderServer.js:7)
+    assert Dec(-129, 3).round(2).to_number() == -0.12             # towards +infinity
     assert Dec(2, 0).div(3).n == 66666666666666666667
 
 
