@@ -167,7 +167,7 @@ struct kmer_ctx {
     uint64_t abs_offset = 0;
     bool open_stream = false;      // reset called, not finished
     std::unordered_map<std::string, Ent> exotic;
-    uint64_t *h_small = nullptr;   // pinned: [0..7] copy of d_scal, [8..11] pos
+    uint64_t *h_small = nullptr;   // pinned (24 words): [0..7] copy of d_scal, [8..11] pos, [12..16] table feed
     uint64_t *h_tail = nullptr;    // pinned, mapped, coherent: d_scal[0..7] written by the chunk tail kernel
     uint64_t *d_tail = nullptr;    // ... its device address
     unsigned int *d_hticket = nullptr;   // chunk tail last-block ticket (d_scal[8])
@@ -196,6 +196,7 @@ struct kmer_ctx {
     DBuf<TabUnit> tunits;          // pass-2 units, then TAB_NB partition heads
     DBuf<TabBig> tbig;             // entries with counts >= TAB_CMAX
     DBuf<uint32_t> tpc;            // pieces per sequence line (long lines)
+    DBuf<uint32_t> tleft;          // [0] count, then [q, qe) pairs: units the sort final kernel left
     DBuf<uint64_t> tpb;            // ... their scan
     DBuf<SeqLine> tpieces;         // long lines cut into pieces of <= TAB_PIECE windows
     DBuf<unsigned long long> tstats;   // [0..2] final statistics, [3] big-list count, [4] digest
@@ -913,18 +914,21 @@ kmer_status table_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_t
     const SeqLine *plines = c->lines.p;
     uint64_t n_items = n_seq;
     if (n_seq) {
-        HIPCHK(c, c->tpc.ensure(n_seq, s));
+        HIPCHK(c, c->tpc.ensure(n_seq + 1, s));
         HIPCHK(c, c->tpb.ensure(n_seq, s));
-        HIPCHK(c, launch_tab_piece_count(c->wcount.p, n_seq, c->tpc.p, s));
+        uint32_t *split = c->tpc.p + n_seq;             // set when a line is not exactly one piece
+        HIPCHK(c, hipMemsetAsync(split, 0, 4, s));
+        HIPCHK(c, launch_tab_piece_count(c->wcount.p, n_seq, c->tpc.p, split, s));
         ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tpc.p, c->tpb.p, (uint64_t)0, (size_t)n_seq,
                                                rocprim::plus<uint64_t>(), s));
         HIPCHK(c, hipMemcpyAsync(c->h_small + 12, c->tpb.p + n_seq - 1, 8, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipMemcpyAsync(c->h_small + 13, c->tpc.p + n_seq - 1, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 16, split, 4, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
         const uint64_t n_pieces = c->h_small[12] + (uint32_t)c->h_small[13];
         if (n_pieces == 0) {
             n_items = 0;                          // no line holds a window
-        } else if (n_pieces != n_seq) {           // long lines (or empty ones, dropped on the way)
+        } else if ((uint32_t)c->h_small[16]) {    // long lines (or empty ones, dropped on the way)
             HIPCHK(c, c->tpieces.ensure(std::max<uint64_t>(n_pieces, 1), s));
             HIPCHK(c, launch_tab_piece_write(c->lines.p, c->wcount.p, c->tpb.p, n_seq, c->p.k, c->tpieces.p, s));
             plines = c->tpieces.p;
@@ -1125,7 +1129,21 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1 = nullptr, uint32_t qlo
         HIPCHK(c, hipMemsetAsync(f.prof, 0, fgrid * 64ull, s));
         hprof.resize(fgrid * 8ull);
     }
+    // the sort kernel (two workgroups per CU) takes every unit it can; the
+    // general kernel (hash path, range splits) takes the ones it leaves
+    // (crowded buckets, many copies of a key).  KMERHIP_TAB_FINAL=general: the
+    // general kernel alone (A/B experiments).
+    const char *fk = getenv("KMERHIP_TAB_FINAL");
+    const bool sort_first = !(fk && strcmp(fk, "general") == 0) && !f.prof &&
+                            !(c->p.flags & KMER_FLAG_TABLE_SPLIT_TEST);
     HIPCHK(c, hipEventRecord(c->tev[2], s));
+    if (sort_first) {
+        HIPCHK(c, c->tleft.ensure(2ull * TAB_NQ + 1, s));
+        f.left = c->tleft.p + 1;
+        f.left_n = c->tleft.p;
+        HIPCHK(c, hipMemsetAsync(c->tleft.p, 0, 4, s));
+        HIPCHK(c, launch_tab_sort_final(f, 2 * fgrid, s));
+    }
     HIPCHK(c, launch_tab_final(f, fgrid, s));
     HIPCHK(c, hipEventRecord(c->tev[7], s));
     if (f.prof) {
@@ -1892,7 +1910,7 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
     }
     ok &= dalloc(&c->d_pos, 1) == hipSuccess;
     ok &= dalloc(&c->d_pos_saved, 1) == hipSuccess;
-    ok &= hipHostMalloc((void **)&c->h_small, 16 * sizeof(uint64_t), hipHostMallocDefault) == hipSuccess;
+    ok &= hipHostMalloc((void **)&c->h_small, 24 * sizeof(uint64_t), hipHostMallocDefault) == hipSuccess;
     ok &= hipHostMalloc((void **)&c->h_tail, 16 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent) ==
           hipSuccess;
     ok &= c->h_tail && hipHostGetDevicePointer((void **)&c->d_tail, c->h_tail, 0) == hipSuccess;
@@ -1964,6 +1982,7 @@ kmer_status kmer_close(kmer_ctx *c) {
     c->tunits.release();
     c->tbig.release();
     c->tstats.release();
+    c->tleft.release();
     dfree(c->d_ticket); dfree(c->d_scal); dfree(c->d_pos); dfree(c->d_pos_saved);
     dfree(c->d_P); dfree(c->d_PR);
     if (c->h_small) (void)hipHostFree(c->h_small);

@@ -425,10 +425,15 @@ struct TabFinal {
     unsigned long long *stats;     // [0] canonical entries [1] Map keys [2] sum of Map counts
     uint64_t *prof;                // experiments only (KMERHIP_TAB_PROF): per-workgroup phase clocks, 8 each
     uint32_t qlo, qhi;             // buckets [qlo, qhi) of this table (multi-GPU: the rank's partitions)
+    // units the sort kernel (tab_sort_final) leaves to the general kernel: pairs
+    // [q, qe) of buckets; the general kernel walks this list instead of
+    // [qlo, qhi) when `left` is set
+    uint32_t *left;
+    unsigned int *left_n;
 };
 
 constexpr uint64_t TAB_PIECE = 4096;                   // windows per piece of a long line (pass 1)
-hipError_t launch_tab_piece_count(const uint64_t *wcount, uint64_t n, uint32_t *pc, hipStream_t s);
+hipError_t launch_tab_piece_count(const uint64_t *wcount, uint64_t n, uint32_t *pc, uint32_t *split, hipStream_t s);
 hipError_t launch_tab_piece_write(const SeqLine *lines, const uint64_t *wcount, const uint64_t *pbase, uint64_t n,
                                   uint32_t k, SeqLine *out, hipStream_t s);
 hipError_t launch_tab_hist1(const TabArgs &a, hipStream_t s);
@@ -440,6 +445,8 @@ hipError_t launch_tab_scatter2(const uint64_t *B1, const TabUnit *units, uint32_
 hipError_t launch_tab_starts(const uint64_t *H2s, const TabUnit *pfirst, uint64_t total, uint64_t *start,
                              hipStream_t s);
 hipError_t launch_tab_final(const TabFinal &a, uint32_t grid, hipStream_t s);
+hipError_t launch_tab_sort_final(const TabFinal &a, uint32_t grid, hipStream_t s);
+constexpr uint32_t TAB_SWG = 512;                      // sort-final workgroup (8 waves, two per CU)
 hipError_t launch_tab_digest(const uint64_t *ent, const uint64_t *start, const uint32_t *nd, unsigned long long *out,
                              hipStream_t s);
 // multi-GPU table exchange: copy n segments {src offset, dst offset, length}

@@ -27,6 +27,8 @@
 //           atomic count) with ranges split and redone when they do not fit.
 //           Entries (remainder, count) are written back to the bucket's range;
 //           Map statistics on the fly.
+#include <type_traits>
+
 #include "kmer_internal.hpp"
 
 namespace kmerhip {
@@ -156,7 +158,15 @@ __device__ __forceinline__ uint32_t tab_round(const TabArgs &a, TabCur &c, bool 
 #pragma unroll
     for (int i = 0; i < NDW; ++i) {
         uint32_t x = 0x41414141u;                                  // ('A': outside the line, never counted)
-        if (act && (const uint8_t *)(pw + i) < end && (uint32_t)(4 * i) < off + NS + k - 1) x = pw[i];
+        const uint8_t *q = (const uint8_t *)(pw + i);
+        if (act && q < end && (uint32_t)(4 * i) < off + NS + k - 1) {
+            if (q + 4 <= end) {
+                x = pw[i];
+            } else {                                               // the input's last dword: no read past its end
+                for (int j = 0; j < 4; ++j)
+                    if (q + j < end) x = (x & ~(0xFFu << (8 * j))) | ((uint32_t)q[j] << (8 * j));
+            }
+        }
         const uint32_t lo4 = __builtin_amdgcn_udot4((x ^ (x >> 1)) & 0x02020202u, 0x08040201u, 0u, false) >> 1;
         const uint32_t hi4 = __builtin_amdgcn_udot4(x & 0x04040404u, 0x08040201u, 0u, false) >> 2;
         const uint32_t cc = ((x >> 1) ^ (x >> 2)) & 0x03030303u;
@@ -274,11 +284,17 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter1_kernel(TabArgs a) {
 // pass 1's per-workgroup shares of lines carry similar work: table mode has no
 // order, so a piece is just a shorter line (its k-1 byte overlap with the next
 // piece holds no window start of its own).  wcount = 2 W per line.
-__global__ __launch_bounds__(256) void tab_piece_count_kernel(const uint64_t *wcount, uint64_t n, uint32_t *pc) {
+// *split is set when a line does not map to exactly one piece (long or empty)
+__global__ __launch_bounds__(256) void tab_piece_count_kernel(const uint64_t *wcount, uint64_t n, uint32_t *pc,
+                                                              uint32_t *split) {
+    bool any = false;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t w = wcount[i] / 2;
-        pc[i] = (uint32_t)((w + TAB_PIECE - 1) / TAB_PIECE);
+        const uint32_t np = (uint32_t)((w + TAB_PIECE - 1) / TAB_PIECE);
+        pc[i] = np;
+        any |= np != 1u;
     }
+    if (__any(any) && (threadIdx.x & 63) == 0) atomicOr(split, 1u);
 }
 
 __global__ __launch_bounds__(256) void tab_piece_write_kernel(const SeqLine *lines, const uint64_t *wcount,
@@ -475,8 +491,9 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
     const uint32_t t = threadIdx.x, lane = t & 63;
     const uint32_t k = a.k;
     const uint32_t kmask = k >= 32 ? ~0u : ((1u << k) - 1u), sh = 32 - k;
-    const uint32_t per = (a.qhi - a.qlo + gridDim.x - 1) / gridDim.x;
-    const uint32_t q0 = min(a.qlo + blockIdx.x * per, a.qhi), q1 = q0 + per < a.qhi ? q0 + per : a.qhi;
+    // [q0, q1): this workgroup's share of [qlo, qhi), or (list mode) an entry
+    // of the sort kernel's leftover list
+    uint32_t q0 = 0, q1 = 0;
     const uint64_t rk = a.range_keys;
     uint64_t st_canon = 0, st_keys = 0, st_sum = 0;
     uint64_t kn[TAB_KPT];
@@ -536,7 +553,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
             st_sum += (fs ? (pal ? 2 * cnt : cnt) : 0) + (rs ? cnt : 0);
         }
     };
-    uint32_t cbase = q0;
+    uint32_t cbase = 0;
     // the unit starting at bucket u: its end (uniform over the workgroup; the
     // start cache must hold u's start, i.e. u <= cbase + TAB_SC)
     // (groups for the sort path fill the registers; the hash path's ranges
@@ -558,8 +575,19 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
         tkey[i] = TAB_EMPTY;
         tcnt[i] = 0;
     }
-    refill(cbase);
     bool dirty = false;
+    const uint32_t n_items = a.left ? *a.left_n : 1u;
+    for (uint32_t item = a.left ? blockIdx.x : 0u; item < n_items; item += a.left ? gridDim.x : 1u) {
+    if (a.left) {
+        q0 = a.left[2 * item];
+        q1 = a.left[2 * item + 1];
+    } else {
+        const uint32_t per = (a.qhi - a.qlo + gridDim.x - 1) / gridDim.x;
+        q0 = min(a.qlo + blockIdx.x * per, a.qhi);
+        q1 = q0 + per < a.qhi ? q0 + per : a.qhi;
+    }
+    cbase = q0;
+    refill(cbase);
     uint32_t q = q0, qe = q0 < q1 ? unit_end(q0) : q0;
     if (q0 < q1) load_keys(sc[0], sc[qe - cbase] - sc[0]);
     while (q < q1) {
@@ -837,9 +865,267 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
         q = qn;
         qe = qne;
     }
+    __syncthreads();                                 // (the next item refills the start cache)
+    }
     if (prof)
         for (int i = 0; i < 6; ++i) a.prof[blockIdx.x * 8 + i] = pt[i];
     // workgroup totals -> one atomic per wave
+    for (int d = 32; d >= 1; d >>= 1) {
+        st_canon += __shfl_xor(st_canon, d);
+        st_keys += __shfl_xor(st_keys, d);
+        st_sum += __shfl_xor(st_sum, d);
+    }
+    if (lane == 0 && st_canon) {
+        atomicAdd(&a.stats[0], (unsigned long long)st_canon);
+        atomicAdd(&a.stats[1], (unsigned long long)st_keys);
+        atomicAdd(&a.stats[2], (unsigned long long)st_sum);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Sort final: the common case of the final merge, two 512-thread workgroups
+// per CU (their phases overlap each other's barriers and key loads).  A unit
+// -- one bucket of up to 12,288 keys (C3: ~11.4 K), or a group of consecutive
+// small buckets of up to 6,144 keys together (C5) -- is held in registers
+// (24 keys per thread), counting-sorted into 4,096 LDS bins by the top 12 bits
+// of (bucket offset << 44 | remainder), and every held key then scans its own
+// bin (~3 keys at C3): the first copy of a key emits it with the number of
+// copies.  One bucket's bin fixes the remainder's top 12 bits, so its LDS
+// entries keep only the low 32 (48 KiB for 12,288 keys); a group's keep all
+// 64 bits (6,144 keys, the same 48 KiB).  Units that do not fit -- larger
+// buckets, or a bin with more than TS_BINMAX keys (many copies of a key) --
+// go to the leftover list for the general kernel (hash path, range splits).
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int TS_KPT = 24;                            // keys held per thread
+constexpr uint32_t TS_CAP1 = TS_KPT * TAB_SWG;        // one bucket: 12,288 keys, 32-bit LDS entries
+constexpr uint32_t TS_CAPG = TS_CAP1 / 2;             // a group: 6,144 keys, 64-bit LDS entries
+constexpr uint32_t TS_NB = 4096;                      // bins
+constexpr uint32_t TS_BINMAX = 64;                    // fuller bins: leftover (general kernel)
+constexpr uint32_t TS_GMAX = 64;                      // buckets per group
+constexpr uint32_t TS_SC = 512;                       // bucket starts cached per refill
+
+// exclusive scan of one value per thread over a 512-thread workgroup (ws: 8 words)
+__device__ __forceinline__ uint32_t block_excl_512(uint32_t v, uint32_t *ws, uint32_t *total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t inc = tab_incl_sum(v);
+    if (lane == 63) ws[wid] = inc;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        const uint32_t x = ws[w];
+        before += w < wid ? x : 0u;
+        all += x;
+    }
+    *total = all;
+    return before + inc - v;
+}
+}  // namespace
+
+__global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) {
+    __shared__ uint32_t lkey[TS_CAP1];                // sorted unit: u32 (one bucket) or u64 (a group)
+    __shared__ uint32_t bst[TS_NB];                   // bin counts, then starts, then (after the scatter) ends
+    __shared__ uint64_t sc[TS_SC + 2];                // start[cbase .. cbase + TS_SC + 1]
+    __shared__ uint32_t nout[TS_GMAX];
+    __shared__ uint32_t ws[8], smax;
+    uint64_t *const lkey64 = (uint64_t *)lkey;
+    const uint32_t t = threadIdx.x, lane = t & 63;
+    const uint32_t k = a.k;
+    const uint32_t kmask = k >= 32 ? ~0u : ((1u << k) - 1u), sh = 32 - k;
+    const uint32_t per = (a.qhi - a.qlo + gridDim.x - 1) / gridDim.x;
+    const uint32_t q0 = min(a.qlo + blockIdx.x * per, a.qhi), q1 = q0 + per < a.qhi ? q0 + per : a.qhi;
+    uint64_t st_canon = 0, st_keys = 0, st_sum = 0;
+    // Map statistics of one canonical entry h (App. A.6; as in tab_final_kernel)
+    auto account = [&](uint64_t h, uint64_t cnt) {
+        const uint64_t code = h * a.inv;
+        const uint32_t lo = (uint32_t)code & kmask, hi = (uint32_t)(code >> k) & kmask;
+        const uint32_t rlo2 = __brev(~lo & kmask) >> sh, rhi2 = __brev(~hi & kmask) >> sh;
+        const bool pal = lo == rlo2 && hi == rhi2;
+        st_canon += 1;
+        if (a.canonical) {
+            const uint32_t dif = (lo ^ rlo2) | (hi ^ rhi2);
+            const uint32_t j = dif ? __ffs(dif) - 1 : 0;
+            const uint32_t bw = (((hi >> j) & 1u) << 1) | ((lo >> j) & 1u);
+            const uint32_t br = (((rhi2 >> j) & 1u) << 1) | ((rlo2 >> j) & 1u);
+            const bool wmin = dif == 0 || bw < br;
+            const uint32_t clo = wmin ? lo : rlo2, chi = wmin ? hi : rhi2;
+            const bool cs = (((clo ^ a.plo) | (chi ^ a.phi)) & a.pmask) == 0;
+            st_keys += cs ? 1u : 0u;
+            st_sum += cs ? cnt : 0;
+        } else {
+            const bool fs = (((lo ^ a.plo) | (hi ^ a.phi)) & a.pmask) == 0;
+            const bool rs = !pal && (((rlo2 ^ a.plo) | (rhi2 ^ a.phi)) & a.pmask) == 0;
+            st_keys += (fs ? 1u : 0u) + (rs ? 1u : 0u);
+            st_sum += (fs ? (pal ? 2 * cnt : cnt) : 0) + (rs ? cnt : 0);
+        }
+    };
+    uint32_t cbase = q0;
+    auto refill = [&](uint32_t cb) {
+        __syncthreads();
+        for (uint32_t i = t; i < TS_SC + 2; i += TAB_SWG) sc[i] = a.start[cb + i < TAB_NQ ? cb + i : TAB_NQ];
+        __syncthreads();
+    };
+    auto leftover = [&](uint32_t qa, uint32_t qb) {
+        if (t == 0) {
+            const unsigned int i = atomicAdd(a.left_n, 1u);
+            a.left[2 * i] = qa;
+            a.left[2 * i + 1] = qb;
+        }
+    };
+    refill(cbase);
+    uint32_t q = q0;
+    while (q < q1) {
+        if (q - cbase >= TS_SC) {
+            cbase = q;
+            refill(cbase);
+        }
+        // the unit at q (uniform: every thread reads the same cached starts)
+        uint32_t qe = q + 1;
+        uint64_t n = sc[q + 1 - cbase] - sc[q - cbase];
+        if (n <= TS_CAPG) {
+            while (qe < q1 && qe - cbase < TS_SC && qe - q < TS_GMAX) {
+                const uint64_t ne = sc[qe + 1 - cbase] - sc[qe - cbase];
+                if (n + ne > TS_CAPG) break;
+                n += ne;
+                ++qe;
+            }
+        }
+        const uint32_t g = qe - q;
+        const uint64_t s0 = sc[q - cbase];
+        if (n == 0) {
+            for (uint32_t i = t; i < g; i += TAB_SWG) a.nd[q + i] = 0;
+            q = qe;
+            continue;
+        }
+        if (n > TS_CAP1) {                             // (g == 1) a crowded bucket
+            leftover(q, qe);
+            q = qe;
+            continue;
+        }
+        const uint64_t qbase = (uint64_t)q << TAB_RBITS;
+        const int left = (int)n - (int)t;
+        // One bucket (ONE) or a group: separate instantiations, so that each
+        // keeps only its own registers live.  Held keys: lo = low 32 bits,
+        // hi = the rest (a group's; one bucket's are its bin), pk = bin, later
+        // bin << 14 | sorted position.  Returns false when a bin is crowded.
+        auto sort_unit = [&](auto one_tag) -> bool {
+            constexpr bool ONE = decltype(one_tag)::value;
+            constexpr int KPT = ONE ? TS_KPT : TS_KPT / 2;
+            const uint32_t bsh = TAB_RBITS + (ONE ? 0 : 32 - __clz(g - 1)) - 12;
+            uint32_t lo[KPT], hi[ONE ? 1 : KPT], pk[KPT];
+            {
+                const uint64_t *src = a.B2 + s0;
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) {
+                    const uint64_t x = src[left > j * (int)TAB_SWG ? j * TAB_SWG + t : 0u] - qbase;
+                    lo[j] = (uint32_t)x;
+                    if (!ONE) hi[ONE ? 0 : j] = (uint32_t)(x >> 32);
+                    pk[j] = (uint32_t)(x >> bsh) & (TS_NB - 1);
+                }
+            }
+            __syncthreads();                           // the previous unit is done with the LDS state
+            for (uint32_t i = t; i < TS_NB; i += TAB_SWG) bst[i] = 0;
+            if (t == 0) smax = 0;
+            for (uint32_t i = t; i < g; i += TAB_SWG) nout[i] = 0;
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < KPT; ++j)
+                if (left > j * (int)TAB_SWG)
+                    __hip_atomic_fetch_add(&bst[pk[j]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __syncthreads();
+            {
+                // bin starts: thread t scans bins 8t .. 8t + 7
+                uint32_t c8[8], sum = 0, mx = 0;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    c8[i] = bst[8 * t + i];
+                    sum += c8[i];
+                    mx = max(mx, c8[i]);
+                }
+                uint32_t tot;
+                uint32_t run = block_excl_512(sum, ws, &tot);
+                for (int d = 32; d >= 1; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d));
+                if (lane == 0) atomicMax(&smax, mx);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    bst[8 * t + i] = run;
+                    run += c8[i];
+                }
+            }
+            __syncthreads();
+            if (smax > TS_BINMAX) return false;        // (uniform) many copies of a key
+            // counting-sort scatter: bst[b] runs from the start to the end of bin b
+#pragma unroll
+            for (int j = 0; j < KPT; ++j)
+                if (left > j * (int)TAB_SWG) {
+                    const uint32_t pos = atomicAdd(&bst[pk[j]], 1u);
+                    if (ONE)
+                        lkey[pos] = lo[j];
+                    else
+                        lkey64[pos] = (uint64_t)hi[ONE ? 0 : j] << 32 | lo[j];
+                    pk[j] = pk[j] << 14 | pos;
+                }
+            __syncthreads();
+            // every held key scans its bin [end of bin b - 1, end of bin b):
+            // the first copy emits (key, copies)
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                if (!__any(left > j * (int)TAB_SWG)) break;
+                const uint32_t b = pk[j] >> 14, p = pk[j] & 0x3FFFu;
+                const uint64_t xj = ((uint64_t)(ONE ? b : hi[ONE ? 0 : j]) << 32) | lo[j];
+                bool first = false;
+                uint32_t cnt = 0;
+                if (left > j * (int)TAB_SWG) {
+                    const uint32_t b0 = b ? bst[b - 1] : 0u, b1 = bst[b];
+                    first = true;
+                    for (uint32_t m = b0; m < b1; ++m) {
+                        const bool eq = ONE ? lkey[m] == lo[j] : lkey64[m] == xj;
+                        first &= !(eq && m < p);
+                        cnt += eq ? 1u : 0u;
+                    }
+                }
+                // output slots: one LDS counter bump per wave and bucket present
+                unsigned long long fm = __ballot(first);
+                uint32_t pos = 0, ql = 0;
+                if (ONE) {
+                    if (fm) {
+                        const int ld = __ffsll((long long)fm) - 1;
+                        uint32_t base = 0;
+                        if (lane == (uint32_t)ld) base = atomicAdd(&nout[0], (uint32_t)__popcll(fm));
+                        base = (uint32_t)__shfl((int)base, ld);
+                        pos = base + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
+                    }
+                } else {
+                    ql = (uint32_t)(xj >> TAB_RBITS);
+                    while (fm) {
+                        const int ld = __ffsll((long long)fm) - 1;
+                        const uint32_t qx = (uint32_t)__shfl((int)ql, ld);
+                        const unsigned long long mq = __ballot(first && ql == qx);
+                        uint32_t base = 0;
+                        if (lane == (uint32_t)ld) base = atomicAdd(&nout[qx], (uint32_t)__popcll(mq));
+                        base = (uint32_t)__shfl((int)base, ld);
+                        if (first && ql == qx) pos = base + (uint32_t)__popcll(mq & ((1ull << lane) - 1ull));
+                        fm &= ~mq;
+                    }
+                }
+                if (first) {
+                    a.out[(ONE ? s0 : sc[q + ql - cbase]) + pos] = ((xj & TAB_RMASK) << 20) | cnt;
+                    account(qbase + xj, cnt);
+                }
+            }
+            return true;
+        };
+        const bool ok = g == 1 ? sort_unit(std::true_type{}) : sort_unit(std::false_type{});
+        if (!ok) {
+            leftover(q, qe);
+            q = qe;
+            continue;
+        }
+        __syncthreads();
+        for (uint32_t i = t; i < g; i += TAB_SWG) a.nd[q + i] = nout[i];
+        q = qe;
+    }
     for (int d = 32; d >= 1; d >>= 1) {
         st_canon += __shfl_xor(st_canon, d);
         st_keys += __shfl_xor(st_keys, d);
@@ -870,10 +1156,10 @@ hipError_t launch_tab_p1_offsets(const uint64_t *H1s, uint32_t nwg, uint64_t *ou
     return hipGetLastError();
 }
 
-hipError_t launch_tab_piece_count(const uint64_t *wcount, uint64_t n, uint32_t *pc, hipStream_t s) {
+hipError_t launch_tab_piece_count(const uint64_t *wcount, uint64_t n, uint32_t *pc, uint32_t *split, hipStream_t s) {
     uint64_t blocks = (n + 255) / 256;
     blocks = blocks < 1 ? 1 : blocks > 16384 ? 16384 : blocks;
-    hipLaunchKernelGGL(tab_piece_count_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, wcount, n, pc);
+    hipLaunchKernelGGL(tab_piece_count_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, wcount, n, pc, split);
     return hipGetLastError();
 }
 
@@ -937,6 +1223,11 @@ __global__ __launch_bounds__(256) void tab_digest_kernel(const uint64_t *ent, co
 hipError_t launch_tab_digest(const uint64_t *ent, const uint64_t *start, const uint32_t *nd, unsigned long long *out,
                              hipStream_t s) {
     hipLaunchKernelGGL(tab_digest_kernel, dim3(4096), dim3(256), 0, s, ent, start, nd, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_tab_sort_final(const TabFinal &a, uint32_t grid, hipStream_t s) {
+    hipLaunchKernelGGL(tab_sort_final_kernel, dim3(grid), dim3(TAB_SWG), 0, s, a);
     return hipGetLastError();
 }
 

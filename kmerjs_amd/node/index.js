@@ -70,8 +70,8 @@ function countPath(kmerObj, fastq) {
                 reject(e);
                 return;
             }
-            kmerObj.uKmers = map.size;
-            kmerObj.lines = res.lines;
+            // (readLinesBrowser, lib/index.js:250-306, sets neither uKmers nor
+            // a line count on the object: only the unused readLineNode does, :389)
             resolve(map);
         });
     });

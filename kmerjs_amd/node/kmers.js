@@ -36,7 +36,9 @@ let addon = null;
 function native() {
     if (!addon) {
         // fails loudly if the HIP library / addon is not built: no CPU fallback
-        addon = require(path.join(__dirname, 'kmerhip.node'));
+        // (KMERHIP_ADDON: another build of the same addon, e.g. the sanitizer
+        // build of tests/test_sanitizers.py)
+        addon = require(process.env.KMERHIP_ADDON || path.join(__dirname, 'kmerhip.node'));
     }
     return addon;
 }

@@ -77,6 +77,26 @@ def count_buffer(data: bytes, prefix: bytes = b"ATGAC", k: int = 16, step: int =
         lib().oracle_free(ctypes.byref(r))
 
 
+def count_arrays(data: bytes, prefix: bytes = b"ATGAC", k: int = 16):
+    """count_buffer (step 1) as numpy arrays, for large cases: keys (n, k)
+    uint8 in Map order, counts uint64 (n,)."""
+    import numpy as np
+    r = _Res()
+    st = lib().oracle_count_buffer(data, len(data), prefix, len(prefix), k, 1, ctypes.byref(r))
+    try:
+        if st:
+            raise OracleError("oracle status %d" % st)
+        n = int(r.n)
+        if n == 0:
+            return np.zeros((0, k), np.uint8), np.zeros(0, np.uint64)
+        off = np.ctypeslib.as_array(r.key_off, shape=(n,))
+        assert int(off[-1]) == (n - 1) * k, "step-1 keys are k bytes, back to back"
+        keys = np.ctypeslib.as_array(r.keys, shape=(n * k,)).reshape(n, k).copy()
+        return keys, np.ctypeslib.as_array(r.counts, shape=(n,)).copy()
+    finally:
+        lib().oracle_free(ctypes.byref(r))
+
+
 def kmers_in_line(line: bytes, prefix: bytes = b"ATGAC", k: int = 16, step: int = 1):
     r = _Res()
     st = lib().oracle_kmers_in_line(line, len(line), prefix, len(prefix), k, step, ctypes.byref(r))

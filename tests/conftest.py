@@ -13,6 +13,13 @@ GOLDEN_DIR = os.path.join(REPO, "tests", "golden")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs under gpurun)")
     config.addinivalue_line("markers", "slow: long-running full-size check")
+    config.addinivalue_line("markers", "fullsize: BASELINE-size property test (runs after every parity test)")
+
+
+def pytest_collection_modifyitems(config, items):
+    # parity first: the full-size property tests run last, so that a stop (-x)
+    # in one of them hides no parity row (stable sort keeps the file order)
+    items.sort(key=lambda it: 1 if it.get_closest_marker("fullsize") else 0)
 
 
 @pytest.fixture(scope="session")

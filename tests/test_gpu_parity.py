@@ -37,6 +37,19 @@ def _run_cases(native, golden, inputs, flags=0, batch_bytes=0, select=None):
     return bad
 
 
+def test_c1_count_file_pins_reference_digest(native):
+    """BASELINE configs[0] through the C-ABI (kmer_count_file): test_short.fastq,
+    'ATGAC', k = 16 -> the reference's ordered Map (SURVEY.md App. C digest
+    14056308710d569d; first-key KAT of test/kmers.js:12-19), 40 lines."""
+    import os
+    from tests.conftest import GOLDEN_DIR
+    ctr = native.Counter(k=16, prefix=b"ATGAC")
+    r = ctr.count_file(os.path.join(GOLDEN_DIR, "inputs", "test_short.fastq"))
+    ctr.close()
+    assert digest(r.entries()).startswith("14056308710d569d") and r.lines == 40
+    assert r.entries() == [(b"ATGACGCAATACTCCT", 1), (b"ATGACCTGAGAGCCTT", 1)]
+
+
 def test_every_golden_case(native, golden, inputs):
     bad = _run_cases(native, golden, inputs)
     assert not bad, bad[:5]
@@ -335,56 +348,6 @@ def test_sharded_merge_matches_oracle(native, world):
         assert first_diff(r.entries(), want) is None, (world, k, p)
 
 
-def test_full_size_properties(native):
-    # BASELINE configs[1] size (10 M reads, 3.17 GB): properties that need no oracle
-    import torch
-    from kmerjs_amd import synth_fastq_device
-    n = 10_000_000
-    k, prefix = 16, b"ATGAC"
-    buf = torch.empty(n * 317, dtype=torch.uint8, device="cuda")
-    synth_fastq_device(buf.data_ptr(), 1, 0, n)
-    torch.cuda.synchronize()
-    ctr = native.Counter(k=k, prefix=prefix)
-    ctr.reset()
-    ctr.feed_device(buf.data_ptr(), buf.numel())
-    res = ctr.finish()
-    assert res.lines == 4 * n
-    # accepted windows counted independently: forward windows start with P, reverse-strand
-    # windows end (in forward coordinates) with rc(P) at q >= k - |P|
-    seq = buf.view(n, 317)[:, 13:163]
-    fwd = torch.ones((n, 150 - 5 + 1), dtype=torch.bool, device="cuda")
-    rev = torch.ones_like(fwd)
-    for i in range(5):
-        fwd &= seq[:, i:146 + i] == prefix[i]
-        rev &= seq[:, i:146 + i] == b"GTCAT"[i]
-    accepted = int(fwd[:, :150 - k + 1].sum()) + int(rev[:, k - 5:].sum())
-    del fwd, rev
-    assert int(res.counts.sum()) == accepted
-    assert len(set(res.keys())) == len(res)
-    assert all(key.startswith(prefix) for key in res.keys()[:100000])
-    f = res.firsts.astype(np.uint64)
-    assert bool(np.all(f[1:] > f[:-1]))
-    # sharded (4 ranks' worth) + merged finish reproduces the whole result
-    from kmerjs_amd.multi import device_u64, invalid_key
-    per = n // 4
-    keys, vals = [], []
-    for r in range(4):
-        ctr.reset()
-        ctr.set_position(4 * per * r, 317 * per * r)
-        ctr.feed_device(buf.data_ptr() + 317 * per * r, 317 * per)
-        d_k, d_v, m = ctr.partial_device()
-        keys.append(device_u64(d_k, m, torch.device("cuda")).clone())
-        vals.append(device_u64(d_v, 2 * m, torch.device("cuda")).view(m, 2).clone())
-    del buf
-    gk, gv = torch.cat(keys), torch.cat(vals)
-    merged = ctr.finish_merged(gk.data_ptr(), gv.data_ptr(), gk.numel(), 4 * n)
-    ctr.close()
-    assert merged.lines == res.lines
-    assert np.array_equal(merged.counts, res.counts)
-    assert np.array_equal(merged.firsts, res.firsts)
-    assert merged.keybuf == res.keybuf
-
-
 def test_long_lines_and_dense_hits(native):
     # lines spanning many tiles (every hit on the cross path, > one-workgroup sort)
     # and hit-dense prefixes (tiles overflowing their hit slots)
@@ -486,75 +449,3 @@ def test_device_group_through_the_c_abi(native, golden, inputs, devs, tmp_path):
     with pytest.raises(native.KmerError):          # device-resident calls are single-device only
         ctr.reset()
     ctr.close()
-
-
-def test_c4_shard_full_size_properties(native):
-    # BASELINE configs[3] per-GPU shard: 125 M reads (39.6 GB, seed 4) -- the
-    # 1 B-read job's share of one of 8 GPUs -- properties that need no oracle,
-    # checked on the device; then the shard as 2 ranks' worth, hit exchange +
-    # device-side ordered collect (kmer_merge_ordered) == the one-pass result
-    import torch
-    from kmerjs_amd import synth_fastq_device
-    from kmerjs_amd.multi import _CudaArray, device_u64
-    n, k, prefix = 125_000_000, 16, b"ATGAC"
-    dev = torch.device("cuda")
-    buf = torch.empty(n * 317, dtype=torch.uint8, device=dev)
-    synth_fastq_device(buf.data_ptr(), 4, 0, n)
-    torch.cuda.synchronize()
-    ctr = native.Counter(k=k, prefix=prefix)
-    ctr.reset()
-    ctr.set_position(0, 0)
-    ctr.feed_device(buf.data_ptr(), buf.numel())
-    ctr.finish(want_result=False)
-    assert ctr.lines() == 4 * n
-    dk, dc, df, m = ctr.result_device()
-    keys = torch.as_tensor(_CudaArray(dk, m * k, "|u1"), device=dev).view(m, k).clone()
-    cnt = device_u64(dc, m, dev).clone()
-    fst = device_u64(df, m, dev).clone()
-    # accepted windows counted independently, 10 M reads at a time
-    accepted = 0
-    for lo in range(0, n, 10_000_000):
-        seq = buf.view(n, 317)[lo:lo + 10_000_000, 13:163]
-        fwd = torch.ones((seq.shape[0], 146), dtype=torch.bool, device=dev)
-        rev = torch.ones_like(fwd)
-        for i in range(5):
-            fwd &= seq[:, i:146 + i] == prefix[i]
-            rev &= seq[:, i:146 + i] == b"GTCAT"[i]
-        accepted += int(fwd[:, :150 - k + 1].sum()) + int(rev[:, k - 5:].sum())
-        del fwd, rev, seq
-    assert int(cnt.sum()) == accepted
-    assert m <= 4 ** 11 and bool((keys[:, :5] == torch.tensor(list(prefix), dtype=torch.uint8, device=dev)).all())
-    assert bool((fst[1:] > fst[:-1]).all())
-    # 2 ranks' worth on the same device: exchange by key range, per-owner finish,
-    # then the owners' ordered lists merged by first occurrence on "rank 0"
-    half = n // 2
-    ctrs = [native.Counter(k=k, prefix=prefix) for _ in range(2)]
-    runs = []
-    for r, c in enumerate(ctrs):
-        c.reset()
-        c.set_position(4 * half * r, 317 * half * r)
-        c.feed_device(buf.data_ptr() + 317 * half * r, 317 * half)
-        d_x, counts = c.exchange_prepare(2)
-        x = device_u64(d_x, 2 * sum(counts), dev).clone()
-        runs.append((x[:2 * counts[0]], x[2 * counts[0]:]))
-    del buf
-    parts = []
-    for o, c in enumerate(ctrs):
-        recv = torch.cat([runs[0][o], runs[1][o]])
-        c.finish_exchanged(recv.data_ptr(), recv.numel() // 2, 4 * n,
-                           stream=torch.cuda.current_stream().cuda_stream)   # (after the cat)
-        ok, oc, of, om = c.result_device()
-        parts.append((torch.as_tensor(_CudaArray(ok, om * k, "|u1"), device=dev).clone(),
-                      device_u64(oc, om, dev).clone(), device_u64(of, om, dev).clone()))
-    del runs
-    gk = torch.cat([p[0] for p in parts])
-    gc = torch.cat([p[1] for p in parts])
-    gf = torch.cat([p[2] for p in parts])
-    torch.cuda.synchronize()
-    ctrs[0].merge_ordered(gk.data_ptr(), gc.data_ptr(), gf.data_ptr(), gc.numel(), 4 * n)
-    mk, mc, mf, mm = ctrs[0].result_device()
-    assert mm == m
-    assert torch.equal(device_u64(mc, mm, dev), cnt) and torch.equal(device_u64(mf, mm, dev), fst)
-    assert torch.equal(torch.as_tensor(_CudaArray(mk, mm * k, "|u1"), device=dev).view(mm, k), keys)
-    for c in ctrs + [ctr]:
-        c.close()

@@ -27,6 +27,21 @@ def test_node_dropin_cpu():
 
 
 @pytest.mark.gpu
+def test_c1_readfile_pins_reference_digest():
+    """BASELINE configs[0] through the reference's entry point: readFile() of
+    test_data/test_short.fastq with preffix 'ATGAC', k = 16 (test/kmers.js:28-35)
+    resolves to the reference's Map: 2 keys, the ordered digest of SURVEY.md
+    App. C (sha256 of JSON.stringify([...map]) = 14056308710d569d...), lines 40."""
+    path = os.path.join(REPO, "tests", "golden", "inputs", "test_short.fastq")
+    p = subprocess.run([NODE, os.path.join(REPO, "tests", "node", "run_readfile.js"), path, "ATGAC", "16"],
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r.get("error") is None, r
+    assert r["digest"].startswith("14056308710d569d") and r["size"] == 2 and r["lines"] == 40
+
+
+@pytest.mark.gpu
 def test_node_dropin_gpu_parity(golden):
     res = _run("gpu", 600)
     assert len(res) > 20

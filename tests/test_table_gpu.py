@@ -199,6 +199,61 @@ def test_canonical_mode_vs_oracle(native, golden, inputs, k, prefix):
         native.Counter(k=16, prefix=b"N", flags=native.FLAG_CANONICAL)
 
 
+@pytest.mark.parametrize("k,flags_name", [(31, "FLAG_UNORDERED"), (16, "FLAG_UNORDERED"), (21, "FLAG_CANONICAL")])
+def test_table_digest_matches_oracle(native, k, flags_name):
+    """kmer_table_digest (the linear checksum the full-size tests rely on)
+    equals the digest of the oracle's Map at a size the oracle covers; reads
+    with N (record keys are outside the digest) and even k (palindromes)."""
+    from oracle import oracle
+    from tests.util import canonical_summary
+    rng = np.random.default_rng(k)
+    arr = np.frombuffer(bytearray(oracle.synth_fastq(8, 0, 30000)), dtype=np.uint8).reshape(-1, 317).copy()
+    seq = arr[:, 13:163]
+    seq[rng.random(seq.shape) < 0.001] = ord("N")
+    arr[:, 13:163] = seq
+    data = arr.tobytes()
+    keys, cnt = oracle.count_arrays(data, b"", k)
+    acgt = ~(keys == ord("N")).any(axis=1)
+    classes, fwd, dig = canonical_summary(keys[acgt], cnt[acgt], k)
+    ctr = native.Counter(k=k, prefix=b"", flags=getattr(native, flags_name))
+    ctr.count_buffer(data)
+    assert ctr.table_digest() == dig
+    assert ctr.table_stats()[0] == classes
+    ctr.close()
+
+
+def test_c5_contigs_canonical_vs_oracle(native):
+    """BASELINE configs[4]'s shape at a size the oracle covers: single-line
+    FASTA contigs of 10 kb - 1 Mb (bench.make_contigs, seed 5; only lines with
+    index % 4 == 1 count, lib/kmers.js:151), k = 21, canonical k-mers on a
+    device-resident feed: classes, Σ counts and the table digest equal those
+    derived from the oracle's Map, and a sample of entries matches."""
+    import torch
+    from bench import make_contigs
+    from oracle import oracle
+    from tests.util import canonical_summary
+    k = 21
+    data, lens = make_contigs(5, 3_000_000, k)
+    assert max(lens) > 100_000
+    keys, cnt = oracle.count_arrays(data, b"", k)
+    classes, fwd, dig = canonical_summary(keys, cnt, k)
+    assert fwd == sum(L - k + 1 for i, L in enumerate(lens) if i % 4 == 1 and L >= k)
+    buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    ctr = native.Counter(k=k, prefix=b"", flags=native.FLAG_CANONICAL)
+    ctr.reset()
+    ctr.feed_device(buf.data_ptr(), buf.numel())
+    res = ctr.finish()
+    assert ctr.table_stats() == (classes, classes, fwd)
+    assert ctr.table_digest() == dig and len(res) == classes
+    got = dict(res.entries())
+    for i in range(0, len(cnt), 1009):
+        kk = keys[i].tobytes()
+        rc = oracle.complement(kk)
+        c = min(kk, rc)
+        assert got[c] == (int(cnt[i]) // 2 if kk == rc else int(cnt[i]))
+    ctr.close()
+
+
 def _table_dump(native, ctr):
     """The device table as sorted (h, count) arrays (kmer_table_device layout)."""
     import torch

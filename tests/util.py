@@ -51,6 +51,21 @@ def planar_codes(keys, k):
     return (fhi << np.uint64(k)) | flo, (rhi << np.uint64(k)) | rlo
 
 
+def canonical_summary(keys, cnt, k):
+    """From an oracle Map counted with an empty prefix, as arrays (keys (n, k)
+    A/C/G/T uint8, counts): (classes, forward windows, kmer_table_digest) of
+    the table -- each class {c, rc c} counted once per forward window: Map(c),
+    or Map(c) / 2 for a palindrome."""
+    import numpy as np
+    cf, cr = planar_codes(keys, k)
+    rep = cf <= cr
+    w = np.where(cf == cr, cnt // np.uint64(2), cnt)[rep]
+    with np.errstate(over="ignore"):
+        h = cf[rep] * np.uint64(_MUL)
+        dig = int((w * _digest_mix(h)).sum(dtype=np.uint64))
+    return int(rep.sum()), int(w.sum()), dig
+
+
 def table_digest_from_map(entries, k):
     """kmer_table_digest of the table that holds a Map counted with an empty
     prefix (entries: (key bytes, count), A/C/G/T keys only): the table counts
