@@ -88,18 +88,33 @@ typedef struct {
     int32_t device;           /* HIP device ordinal */
     uint32_t flags;           /* KMER_FLAG_* */
     uint64_t max_keys;        /* 0 = unlimited; 16777216 reproduces the reference Map cap */
-    uint64_t batch_bytes;     /* host->device batch size for file/buffer input; 0 = default (1 GiB) */
+    uint64_t batch_bytes;     /* host->device batch size for file/buffer input; 0 = default (files:
+                               * 256 MiB, read ahead on a reader thread; buffers: 1 GiB) */
     /* Multi-GPU (SURVEY.md §8b `ndev`): ndev > 1 makes a group context over
      * `devices` (ndev HIP ordinals; NULL = 0..ndev-1; an ordinal may repeat).
      * kmer_count_file / kmer_count_buffer then split the input into ndev
      * line-aligned shards counted concurrently, one per device, and merge the
      * per-device partials (copied to devices[0] over xGMI) into one result in
-     * Map order -- bit-exact with a single-device count.  Configurations
-     * without packed keys (non-ACGT prefix, step > 1, k > 32, table mode) run
-     * on devices[0] alone.  The device-resident entry points are single-device
-     * only (KMER_E_STATE on a group).  0 or 1 = single device `device`. */
+     * Map order -- bit-exact with a single-device count.  The input is read
+     * as a stream of batches cut at '\n' (batch_bytes; default for files
+     * 256 MiB, for buffers one share per device) dealt round robin to the
+     * devices, so a file never has to fit in host memory.  Table and
+     * canonical mode: every device's pass-1 keys go to the device that owns
+     * their slice of the hash space, which builds that slice of the table;
+     * kmer_table_stats / kmer_table_digest of a group add up its devices'.
+     * Configurations without packed keys or a table (non-ACGT prefix, step >
+     * 1, k > 32) run on devices[0] alone.  The other device-resident entry
+     * points are single-device only (KMER_E_STATE on a group).  0 or 1 =
+     * single device `device`. */
     uint32_t ndev;
     const int32_t *devices;
+    /* Progress of kmer_count_file / kmer_count_buffer (replaces the
+     * progress-stream of readFile(), lib/kmers.js:108-110): called on the
+     * counting thread after each input batch with the input bytes consumed so
+     * far and the input's size (for gzip: compressed bytes read and the
+     * compressed size).  NULL = none. */
+    void (*progress)(void *user, uint64_t done, uint64_t total);
+    void *progress_user;
 } kmer_params;
 
 typedef struct kmer_ctx kmer_ctx;

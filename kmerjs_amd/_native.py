@@ -55,7 +55,12 @@ class Params(ctypes.Structure):
                 ("prefix", ctypes.c_char_p), ("prefix_len", ctypes.c_uint32),
                 ("device", ctypes.c_int32), ("flags", ctypes.c_uint32),
                 ("max_keys", ctypes.c_uint64), ("batch_bytes", ctypes.c_uint64),
-                ("ndev", ctypes.c_uint32), ("devices", ctypes.POINTER(ctypes.c_int32))]
+                ("ndev", ctypes.c_uint32), ("devices", ctypes.POINTER(ctypes.c_int32)),
+                ("progress", ctypes.c_void_p), ("progress_user", ctypes.c_void_p)]
+
+
+# kmer_params.progress: void (*)(void *user, uint64_t done, uint64_t total)
+PROGRESS_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64)
 
 
 class KmerError(RuntimeError):
@@ -202,15 +207,20 @@ class Result:
 class Counter:
     """One kmer_ctx (device, configuration)."""
 
-    def __init__(self, k=16, prefix=b"ATGAC", step=1, device=0, flags=0, max_keys=0, batch_bytes=0, devices=None):
+    def __init__(self, k=16, prefix=b"ATGAC", step=1, device=0, flags=0, max_keys=0, batch_bytes=0, devices=None,
+                 progress=None):
         """devices: a list of HIP ordinals (ordinals may repeat) -> a multi-GPU
         group context: count_buffer / count_file shard the input over them and
-        merge into one result (kmer_params.ndev)."""
+        merge into one result (kmer_params.ndev).  progress(done, total): called
+        after each input batch of count_file / count_buffer."""
         if isinstance(prefix, str):
             prefix = prefix.encode("latin-1")
         self._prefix = prefix
         p = Params(k=k, step=step, prefix=prefix, prefix_len=len(prefix), device=device, flags=flags,
                    max_keys=max_keys, batch_bytes=batch_bytes)
+        if progress is not None:
+            self._progress = PROGRESS_FN(lambda _u, done, total: progress(done, total))
+            p.progress = ctypes.cast(self._progress, ctypes.c_void_p)
         if devices is not None and len(devices) > 1:
             self._devs = (ctypes.c_int32 * len(devices))(*devices)
             p.ndev = len(devices)

@@ -23,7 +23,10 @@
 #include <rocprim/iterator/transform_iterator.hpp>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdio>
+#include <deque>
+#include <mutex>
 #include <functional>
 #include <cstdlib>
 #include <cstring>
@@ -36,6 +39,7 @@
 #include "../../include/kmer_api.h"
 #include "kmer_internal.hpp"
 
+#include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
 #include <zlib.h>
@@ -207,6 +211,7 @@ struct kmer_ctx {
     bool t_done = false;           // a table finish holds results
     uint64_t *t_ent = nullptr;     // the table's entries (tb1, or the received keys' buffer after an exchange)
     DBuf<uint64_t> tsend;          // table exchange: send runs (sessions of several chunks)
+    DBuf<uint64_t> trecv;          // group table mode: the keys this child owns, received from every child
     DBuf<TabSeg> tseg;             // ... and their segment table
     hipEvent_t tev[8] = {};        // table phase events
     // multi-device group (kmer_params.ndev > 1): one child context per device;
@@ -226,6 +231,7 @@ struct kmer_ctx {
 namespace {
 
 const uint64_t DEFAULT_BATCH = 1ull << 30;
+const uint64_t FILE_BATCH = 256ull << 20;     // kmer_count_file read-ahead batch
 
 #define HIPCHK(ctx, x)                                                                      \
     do {                                                                                    \
@@ -1575,7 +1581,7 @@ kmer_status finish(kmer_ctx *c, kmer_result **out) {
 }
 
 // Feed host bytes through the device in batches cut at '\n' boundaries.
-kmer_status feed_host(kmer_ctx *c, const uint8_t *bytes, uint64_t len) {
+kmer_status feed_host(kmer_ctx *c, const uint8_t *bytes, uint64_t len, bool report = false) {
     const uint64_t batch = c->p.batch_bytes ? c->p.batch_bytes : DEFAULT_BATCH;
     uint64_t pos = 0;
     while (pos < len) {
@@ -1600,6 +1606,7 @@ kmer_status feed_host(kmer_ctx *c, const uint8_t *bytes, uint64_t len) {
         kmer_status st = feed(c, c->batch.p, n, c->stream);
         if (st) return st;
         pos = end;
+        if (report && c->p.progress) c->p.progress(c->p.progress_user, pos, len);
     }
     return KMER_OK;
 }
@@ -1607,98 +1614,325 @@ kmer_status feed_host(kmer_ctx *c, const uint8_t *bytes, uint64_t len) {
 // ---------------------------------------------------------------------------
 // multi-device group (kmer_params.ndev > 1)
 // ---------------------------------------------------------------------------
-// Count `bytes` on every child in line-aligned shards and merge on child 0:
-// shard i starts after a '\n' near i/ndev of the input; its first line index
-// (newlines before it) comes from a threaded host count; each child resets,
-// takes its position, feeds its shard and reduces it to unique packed keys
-// {first, count} (kmer_partial_device); the partials are copied in shard
-// order to devices[0] (peer copies over xGMI) and finished there
-// (kmer_finish_merged: min first, sum counts, Map order).  Record keys
-// (non-ACGT windows) move from every child to child 0 on the host.
-kmer_status group_count_buffer(kmer_ctx *g, const uint8_t *bytes, uint64_t len, kmer_result **out) {
-    const size_t N = g->group.size();
+// The input is read as a stream of batches cut at '\n' (lib/kmers.js:114-139
+// reads the file in chunks too; here a batch is up to batch_bytes, default
+// 256 MiB for files) and the batches are dealt round robin to the children,
+// one host thread per child: each sets its position (lines and bytes before
+// the batch, from a running newline count on the reading thread) and feeds the
+// batch, while the next batches are read.  Memory: a pool of batch buffers,
+// not the whole file.  Then, by configuration:
+//  * ordered (packed keys): each child reduces its session to unique packed
+//    keys {first, count} (kmer_partial_device); the partials are copied to
+//    devices[0] (peer copies over xGMI) and finished there (min first, sum
+//    counts, Map order);
+//  * table / canonical mode: each child's pass-1 keys go to the child that
+//    owns their slice of the hash space (kmer_table_exchange_prepare, peer
+//    copies), and every child runs pass 2 + final over its own buckets, all
+//    at once; statistics and digests add up over the children;
+//  * anything else (records only): every batch on devices[0].
+// Record keys (non-ACGT windows) move from every child to child 0 on the host.
+struct GroupSrc {
+    virtual ~GroupSrc() {}
+    virtual void progress(uint64_t *done, uint64_t *total) = 0;
+    // the next batch (valid until release()); false at the end of the input
+    virtual bool next(const uint8_t **p, uint64_t *n, kmer_status *st, std::string *err) = 0;
+    virtual void release(const uint8_t *) {}
+};
+
+// batches of a caller's buffer
+struct MemSrc : GroupSrc {
+    const uint8_t *b;
+    uint64_t len, batch, pos = 0;
+    MemSrc(const uint8_t *b_, uint64_t len_, uint64_t batch_) : b(b_), len(len_), batch(std::max<uint64_t>(batch_, 1)) {}
+    void progress(uint64_t *d, uint64_t *t) override {
+        *d = pos;
+        *t = len;
+    }
+    bool next(const uint8_t **p, uint64_t *n, kmer_status *, std::string *) override {
+        if (pos >= len) return false;
+        uint64_t end = std::min(len, pos + batch);
+        if (end < len) {
+            uint64_t cut = end - pos;
+            while (cut > 0 && b[pos + cut - 1] != '\n') --cut;
+            if (cut == 0) {                          // a line longer than the batch extends it
+                const void *nl = memchr(b + end, '\n', len - end);
+                end = nl ? (uint64_t)((const uint8_t *)nl - b) + 1 : len;
+            } else {
+                end = pos + cut;
+            }
+        }
+        *p = b + pos;
+        *n = end - pos;
+        pos = end;
+        return true;
+    }
+};
+
+// Batches of a file cut at '\n', read ahead: a reader thread fills a ring of
+// host buffers with the next raw ranges of the file (plain files: several
+// preads in parallel per range; gzip: zlib) while the caller counts the
+// batches it already has, so the file read overlaps the device work
+// (lib/kmers.js:108-139 streams the file in chunks too).  A batch is the
+// carry of the previous range (the bytes after its last '\n', copied into the
+// headroom in front of the next range) plus this range up to its last '\n'.
+// Several batches may be outstanding (group counts); each is released when
+// its bytes have been consumed.
+struct FileBatches : GroupSrc {
+    static constexpr uint64_t HEAD = 1ull << 20;     // headroom for the carry
+    struct Slot {
+        std::unique_ptr<uint8_t[]> buf;
+        uint64_t cap = 0, len = 0;
+        int state = 0;                               // 0 free, 1 filled, 2 in use
+        bool last = false;
+    };
+    int fd = -1;
+    gzFile gz = nullptr;
+    uint64_t batch = 0, size = 0, rd_off = 0;
+    int threads = 1;
+    std::vector<Slot> ring;
+    std::mutex m;
+    std::condition_variable cv;
+    std::thread reader;
+    bool stop = false, rd_eof = false;
+    kmer_status rd_st = KMER_OK;
+    std::string rd_err;
+    uint64_t next_fill = 0, next_take = 0, consumed = 0;
+    std::vector<uint8_t> carry;
+    std::unordered_map<const uint8_t *, std::unique_ptr<uint8_t[]>> big;   // batches of lines longer than HEAD
+    std::unordered_map<const uint8_t *, size_t> slot_of;
+    bool done = false;
+
+    ~FileBatches() override {
+        {
+            std::lock_guard<std::mutex> lk(m);
+            stop = true;
+        }
+        cv.notify_all();
+        if (reader.joinable()) reader.join();
+        if (gz) gzclose(gz);
+        if (fd >= 0) close(fd);
+    }
+
+    kmer_status open(const char *path, uint64_t batch_, size_t nslots, std::string *err) {
+        fd = ::open(path, O_RDONLY);
+        if (fd < 0) {
+            *err = std::string("cannot open ") + path;
+            return KMER_E_IO;
+        }
+        struct stat sb;
+        if (fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode)) size = (uint64_t)sb.st_size;
+        unsigned char magic[2] = {0, 0};
+        const bool gzip = pread(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b;
+        batch = std::max<uint64_t>(batch_, 1);
+        if (gzip) {
+            gz = gzdopen(dup(fd), "rb");
+            if (!gz) {
+                *err = std::string("cannot read gzip stream ") + path;
+                return KMER_E_IO;
+            }
+            gzbuffer(gz, 1 << 20);
+        } else if (size) {
+            batch = std::min<uint64_t>(batch, size);  // a small file takes one small buffer
+        }
+        const unsigned hc = std::thread::hardware_concurrency();
+        threads = gzip ? 1 : (int)std::max(1u, std::min(8u, hc ? hc / 2 : 1u));
+        ring.resize(std::max<size_t>(nslots, 2));
+        reader = std::thread([this] { read_loop(); });
+        return KMER_OK;
+    }
+
+    // raw range r into slot r % R (plain: `threads` preads in parallel)
+    void read_loop() {
+        while (true) {
+            size_t si;
+            {
+                std::unique_lock<std::mutex> lk(m);
+                si = (size_t)(next_fill % ring.size());
+                cv.wait(lk, [&] { return stop || ring[si].state == 0; });
+                if (stop) return;
+            }
+            Slot &S = ring[si];
+            if (S.cap < HEAD + batch) {
+                S.buf.reset(new (std::nothrow) uint8_t[HEAD + batch]);
+                S.cap = S.buf ? HEAD + batch : 0;
+            }
+            kmer_status st = S.buf ? KMER_OK : KMER_E_OOM;
+            uint64_t got = 0;
+            bool eof = false;
+            if (!st && gz) {
+                while (got < batch) {
+                    const unsigned want = (unsigned)std::min<uint64_t>(batch - got, 1u << 30);
+                    const int r = gzread(gz, S.buf.get() + HEAD + got, want);
+                    if (r < 0) {
+                        st = KMER_E_IO;
+                        break;
+                    }
+                    got += (uint64_t)r;
+                    if ((unsigned)r < want) break;
+                }
+                int zerr = 0;
+                gzerror(gz, &zerr);
+                if (zerr != Z_OK && zerr != Z_BUF_ERROR) st = KMER_E_IO;
+                eof = got < batch;
+            } else if (!st) {
+                // parallel preads of [rd_off, rd_off + batch); a short read (end of
+                // file, or a file that is not regular) ends the input
+                const int T = threads;
+                const uint64_t piece = (batch + T - 1) / T;
+                std::vector<uint64_t> gotv(T, 0);
+                std::vector<int> errv(T, 0);
+                auto job = [&](int t) {
+                    const uint64_t a = (uint64_t)t * piece, b = std::min<uint64_t>(batch, a + piece);
+                    uint64_t o = a;
+                    while (o < b) {
+                        const ssize_t r = pread(fd, S.buf.get() + HEAD + o, (size_t)(b - o), (off_t)(rd_off + o));
+                        if (r < 0) {
+                            errv[t] = 1;
+                            break;
+                        }
+                        if (r == 0) break;
+                        o += (uint64_t)r;
+                    }
+                    gotv[t] = o - a;
+                };
+                std::vector<std::thread> th;
+                for (int t = 1; t < T; ++t) th.emplace_back(job, t);
+                job(0);
+                for (auto &x : th) x.join();
+                for (int t = 0; t < T; ++t) {
+                    if (errv[t]) st = KMER_E_IO;
+                    const uint64_t a = (uint64_t)t * piece, b = std::min<uint64_t>(batch, a + piece);
+                    got += gotv[t];
+                    if (gotv[t] < b - a) {               // the file ends inside this piece
+                        eof = true;
+                        break;
+                    }
+                }
+                rd_off += got;
+            }
+            std::lock_guard<std::mutex> lk(m);
+            S.len = got;
+            S.last = eof || st;
+            S.state = 1;
+            if (st) {
+                rd_st = st;
+                rd_err = "read error";
+            }
+            ++next_fill;
+            cv.notify_all();
+            if (S.last) return;
+        }
+    }
+
+    bool next(const uint8_t **p, uint64_t *n, kmer_status *st, std::string *err) override {
+        while (!done) {
+            size_t si;
+            {
+                std::unique_lock<std::mutex> lk(m);
+                si = (size_t)(next_take % ring.size());
+                cv.wait(lk, [&] { return ring[si].state == 1; });
+                ring[si].state = 2;
+                ++next_take;
+                if (rd_st) {
+                    *st = rd_st;
+                    *err = rd_err;
+                    done = true;
+                    return false;
+                }
+            }
+            Slot &S = ring[si];
+            consumed += S.len;
+            const bool last = S.last;
+            uint8_t *start;
+            uint64_t have;
+            std::unique_ptr<uint8_t[]> own;
+            if (carry.size() <= HEAD) {
+                start = S.buf.get() + HEAD - carry.size();
+                memcpy(start, carry.data(), carry.size());
+                have = carry.size() + S.len;
+            } else {                                      // a line longer than the headroom
+                own.reset(new (std::nothrow) uint8_t[carry.size() + S.len]);
+                if (!own) {
+                    *st = KMER_E_OOM;
+                    *err = "host batch buffer";
+                    done = true;
+                    return false;
+                }
+                memcpy(own.get(), carry.data(), carry.size());
+                memcpy(own.get() + carry.size(), S.buf.get() + HEAD, S.len);
+                start = own.get();
+                have = carry.size() + S.len;
+            }
+            uint64_t cut = have;
+            if (!last) {
+                while (cut > 0 && start[cut - 1] != '\n') --cut;
+            }
+            carry.assign(start + cut, start + have);
+            if (last) done = true;
+            if (cut == 0) {                               // (no '\n' yet: all of it is carry)
+                release_slot(si);
+                if (last) return false;
+                continue;
+            }
+            *p = start;
+            *n = cut;
+            std::lock_guard<std::mutex> lk(m);
+            if (own) {
+                release_slot_locked(si);
+                big[start] = std::move(own);
+            } else {
+                slot_of[start] = si;
+            }
+            return true;
+        }
+        return false;
+    }
+
+    void release_slot_locked(size_t si) {
+        ring[si].state = 0;
+        cv.notify_all();
+    }
+    void release_slot(size_t si) {
+        std::lock_guard<std::mutex> lk(m);
+        release_slot_locked(si);
+    }
+    void release(const uint8_t *q) override {
+        std::lock_guard<std::mutex> lk(m);
+        auto b = big.find(q);
+        if (b != big.end()) {
+            big.erase(b);
+            return;
+        }
+        auto it = slot_of.find(q);
+        if (it != slot_of.end()) {
+            release_slot_locked(it->second);
+            slot_of.erase(it);
+        }
+    }
+    // progress: (bytes read, file size) -- for gzip the compressed offset and size
+    void progress(uint64_t *d, uint64_t *t) override {
+        *d = gz ? (uint64_t)std::max<z_off_t>(gzoffset(gz), 0) : consumed;
+        *t = size;
+        if (*d > *t && *t) *d = *t;
+    }
+};
+
+uint64_t count_newlines(const uint8_t *p, uint64_t n) {
+    uint64_t c = 0;
+    const uint8_t *e = p + n;
+    while (p < e) {
+        const void *q = memchr(p, '\n', (size_t)(e - p));
+        if (!q) break;
+        ++c;
+        p = (const uint8_t *)q + 1;
+    }
+    return c;
+}
+
+// records (non-ACGT windows) of children 1.. -> child 0
+kmer_status group_gather_records(kmer_ctx *g) {
     kmer_ctx *c0 = g->group[0];
-    if (c0->mode != MODE_PACKED && c0->mode != MODE_WINDOWS) {
-        // no packed partials to merge: the whole input on devices[0]
-        kmer_status st = kmer_count_buffer(c0, bytes, len, out);
-        if (st) g->err = c0->err;
-        return st;
-    }
-    std::vector<uint64_t> cut(N + 1, len);
-    cut[0] = 0;
-    for (size_t i = 1; i < N; ++i) {
-        uint64_t p = std::max<uint64_t>(cut[i - 1], len / N * i);
-        if (p > 0 && p < len) {
-            const void *nl = memchr(bytes + p - 1, '\n', len - (p - 1));
-            p = nl ? (uint64_t)((const uint8_t *)nl - bytes) + 1 : len;
-        }
-        cut[i] = std::min<uint64_t>(p, len);
-    }
-    std::vector<uint64_t> nls(N, 0);
-    {
-        std::vector<std::thread> th;
-        for (size_t i = 0; i < N; ++i)
-            th.emplace_back([&, i]() {
-                uint64_t n = 0;
-                const uint8_t *p = bytes + cut[i], *e = bytes + cut[i + 1];
-                while (p < e) {
-                    const void *q = memchr(p, '\n', (size_t)(e - p));
-                    if (!q) break;
-                    ++n;
-                    p = (const uint8_t *)q + 1;
-                }
-                nls[i] = n;
-            });
-        for (auto &t : th) t.join();
-    }
-    std::vector<uint64_t> before(N, 0);
-    for (size_t i = 1; i < N; ++i) before[i] = before[i - 1] + nls[i - 1];
-    const uint64_t total_lines = before[N - 1] + nls[N - 1] + ((len > 0 && bytes[len - 1] != '\n') ? 1 : 0);
-    std::vector<kmer_status> sts(N, KMER_OK);
-    std::vector<const void *> pk(N, nullptr), pv(N, nullptr);
-    std::vector<uint64_t> pn(N, 0);
-    {
-        std::vector<std::thread> th;
-        for (size_t i = 0; i < N; ++i)
-            th.emplace_back([&, i]() {
-                kmer_ctx *c = g->group[i];
-                if (hipSetDevice(c->device) != hipSuccess) {
-                    sts[i] = KMER_E_DEVICE;
-                    return;
-                }
-                kmer_status st = reset(c);
-                if (!st) st = kmer_set_position(c, before[i], cut[i]);
-                if (!st) st = feed_host(c, bytes + cut[i], cut[i + 1] - cut[i]);
-                if (!st) st = kmer_partial_device(c, &pk[i], &pv[i], &pn[i]);
-                if (st) c->open_stream = false;
-                sts[i] = st;
-            });
-        for (auto &t : th) t.join();
-    }
-    for (size_t i = 0; i < N; ++i)
-        if (sts[i]) return fail(g, sts[i], "device " + std::to_string(g->group[i]->device) + ": " + g->group[i]->err);
-    // partials -> devices[0], in shard order
-    uint64_t n = 0;
-    for (size_t i = 0; i < N; ++i) n += pn[i];
-    if (hipSetDevice(c0->device) != hipSuccess) return fail(g, KMER_E_DEVICE, "hipSetDevice");
-    hipStream_t s = c0->stream;
-    HIPCHK(g, g->gkeys.ensure(n, s));
-    HIPCHK(g, g->gvals.ensure(n, s));
-    uint64_t o = 0;
-    for (size_t i = 0; i < N; ++i) {
-        if (!pn[i]) continue;
-        kmer_ctx *c = g->group[i];
-        if (c->device == c0->device) {
-            HIPCHK(g, hipMemcpyAsync(g->gkeys.p + o, pk[i], pn[i] * 8, hipMemcpyDeviceToDevice, s));
-            HIPCHK(g, hipMemcpyAsync(g->gvals.p + o, pv[i], pn[i] * sizeof(Agg), hipMemcpyDeviceToDevice, s));
-        } else {
-            HIPCHK(g, hipMemcpyPeerAsync(g->gkeys.p + o, c0->device, pk[i], c->device, pn[i] * 8, s));
-            HIPCHK(g, hipMemcpyPeerAsync(g->gvals.p + o, c0->device, pv[i], c->device, pn[i] * sizeof(Agg), s));
-        }
-        o += pn[i];
-    }
-    HIPCHK(g, hipStreamSynchronize(s));
-    for (size_t i = 1; i < N; ++i) {
+    for (size_t i = 1; i < g->group.size(); ++i) {
         kmer_result *r = nullptr;
         kmer_status st = kmer_records_export(g->group[i], &r);
         if (st) return fail(g, st, "records export");
@@ -1709,54 +1943,257 @@ kmer_status group_count_buffer(kmer_ctx *g, const uint8_t *bytes, uint64_t len, 
             kmer_result_arrays(r, &kb, &off, &cnt);
             kmer_result_firsts(r, &fst);
             st = kmer_records_import(c0, kb, off, cnt, fst, m);
+            if (!st) st = kmer_records_clear(g->group[i]);
         }
         kmer_result_free(r);
         if (st) return fail(g, st, "records import");
     }
-    kmer_status st = kmer_finish_merged(c0, g->gkeys.p, g->gvals.p, n, total_lines, out);
-    if (st) return fail(g, st, c0->err);
     return KMER_OK;
 }
 
-// A whole file into host memory (mmap when plain, zlib when gzip), then the group count.
-kmer_status group_count_file(kmer_ctx *g, const char *path, kmer_result **out) {
-    gzFile gz = gzopen(path, "rb");
-    if (!gz) return fail(g, KMER_E_IO, std::string("cannot open ") + path);
-    gzbuffer(gz, 1 << 20);
-    std::vector<uint8_t> data;
-    size_t cap = 1 << 24, len = 0;
-    {
-        struct stat sb;
-        if (stat(path, &sb) == 0 && S_ISREG(sb.st_mode)) cap = std::max<size_t>(cap, (size_t)sb.st_size + 1);
-    }
-    std::unique_ptr<uint8_t[]> buf(new (std::nothrow) uint8_t[cap]);
-    if (!buf) {
-        gzclose(gz);
-        return fail(g, KMER_E_OOM, "host buffer");
-    }
-    while (true) {                             // (gzread passes plain files through)
-        if (len == cap) {
-            const size_t nc = cap * 2;
-            std::unique_ptr<uint8_t[]> nb(new (std::nothrow) uint8_t[nc]);
-            if (!nb) {
-                gzclose(gz);
-                return fail(g, KMER_E_OOM, "host buffer");
+// run f(i) for every child i on its own thread (device selected); first error wins
+kmer_status group_each(kmer_ctx *g, size_t n, const std::function<kmer_status(size_t)> &f) {
+    std::vector<kmer_status> sts(n, KMER_OK);
+    std::vector<std::thread> th;
+    for (size_t i = 0; i < n; ++i)
+        th.emplace_back([&, i]() {
+            if (hipSetDevice(g->group[i]->device) != hipSuccess) {
+                sts[i] = KMER_E_DEVICE;
+                return;
             }
-            memcpy(nb.get(), buf.get(), len);
-            buf = std::move(nb);
-            cap = nc;
+            sts[i] = f(i);
+        });
+    for (auto &t : th) t.join();
+    for (size_t i = 0; i < n; ++i)
+        if (sts[i]) return fail(g, sts[i], "device " + std::to_string(g->group[i]->device) + ": " + g->group[i]->err);
+    return KMER_OK;
+}
+
+kmer_status group_count(kmer_ctx *g, GroupSrc &src, kmer_result **out) {
+    const size_t N = g->group.size();
+    kmer_ctx *c0 = g->group[0];
+    const int mode = c0->mode;
+    const bool ordered = mode == MODE_PACKED || mode == MODE_WINDOWS;
+    const size_t W = (ordered || mode == MODE_TABLE) ? N : 1;    // children that take batches
+    g->t_done = false;
+    // -- the batch stream, dealt round robin over W worker threads
+    struct Job {
+        const uint8_t *p;
+        uint64_t n, lines, off;
+    };
+    struct Worker {
+        std::deque<Job> q;
+        std::mutex m;
+        std::condition_variable cv;
+        bool end = false;
+        kmer_status st = KMER_OK;
+    };
+    std::vector<std::unique_ptr<Worker>> wk;
+    for (size_t i = 0; i < W; ++i) wk.emplace_back(new Worker());
+    std::vector<std::thread> th;
+    for (size_t i = 0; i < W; ++i)
+        th.emplace_back([&, i]() {
+            Worker &w = *wk[i];
+            kmer_ctx *c = g->group[i];
+            kmer_status st = hipSetDevice(c->device) == hipSuccess ? reset(c) : KMER_E_DEVICE;
+            while (true) {
+                Job j;
+                {
+                    std::unique_lock<std::mutex> lk(w.m);
+                    w.cv.wait(lk, [&] { return !w.q.empty() || w.end; });
+                    if (w.q.empty()) break;
+                    j = w.q.front();
+                    w.q.pop_front();
+                }
+                if (!st) st = kmer_set_position(c, j.lines, j.off);
+                if (!st) st = feed_host(c, j.p, j.n);
+                if (!st) st = settle(c);
+                if (!st && hipStreamSynchronize(c->stream) != hipSuccess) st = KMER_E_DEVICE;   // bytes consumed
+                src.release(j.p);
+                if (st) {
+                    c->open_stream = false;
+                    std::lock_guard<std::mutex> lk(w.m);
+                    w.st = st;
+                }
+            }
+            std::lock_guard<std::mutex> lk(w.m);
+            if (st) w.st = st;
+        });
+    uint64_t lines = 0, off = 0, nb = 0;
+    uint8_t last = '\n';
+    kmer_status rst = KMER_OK;
+    std::string rerr;
+    const uint8_t *p = nullptr;
+    uint64_t n = 0;
+    while (src.next(&p, &n, &rst, &rerr)) {
+        bool failed = false;
+        for (auto &w : wk) {
+            std::lock_guard<std::mutex> lk(w->m);
+            failed |= w->st != KMER_OK;
         }
-        const unsigned want = (unsigned)std::min<size_t>(cap - len, 1u << 30);
-        const int r = gzread(gz, buf.get() + len, want);
-        if (r < 0) {
-            gzclose(gz);
-            return fail(g, KMER_E_IO, std::string("read error on ") + path);
+        if (failed) {
+            src.release(p);
+            break;
         }
-        len += (size_t)r;
-        if (r == 0) break;
+        const uint64_t nl = count_newlines(p, n);
+        last = p[n - 1];
+        Worker &w = *wk[nb % W];
+        {
+            std::lock_guard<std::mutex> lk(w.m);
+            w.q.push_back(Job{p, n, lines, off});
+        }
+        w.cv.notify_one();
+        lines += nl;
+        off += n;
+        ++nb;
+        if (g->p.progress) {                          // (batches handed to the devices)
+            uint64_t d = 0, t = 0;
+            src.progress(&d, &t);
+            g->p.progress(g->p.progress_user, d, t);
+        }
     }
-    gzclose(gz);
-    return group_count_buffer(g, buf.get(), len, out);
+    for (auto &w : wk) {
+        {
+            std::lock_guard<std::mutex> lk(w->m);
+            w->end = true;
+        }
+        w->cv.notify_one();
+    }
+    for (auto &t : th) t.join();
+    if (rst) return fail(g, rst, rerr);
+    for (size_t i = 0; i < W; ++i)
+        if (wk[i]->st) return fail(g, wk[i]->st, "device " + std::to_string(g->group[i]->device) + ": " + g->group[i]->err);
+    const uint64_t total_lines = lines + (off > 0 && last != '\n' ? 1 : 0);
+    if (hipSetDevice(c0->device) != hipSuccess) return fail(g, KMER_E_DEVICE, "hipSetDevice");
+    if (!ordered && mode != MODE_TABLE) {            // every batch went to devices[0]
+        kmer_status st = finish(c0, out);
+        if (st) return fail(g, st, c0->err);
+        return KMER_OK;
+    }
+    if (ordered) {
+        std::vector<const void *> pk(N, nullptr), pv(N, nullptr);
+        std::vector<uint64_t> pn(N, 0);
+        kmer_status st = group_each(g, N, [&](size_t i) { return kmer_partial_device(g->group[i], &pk[i], &pv[i], &pn[i]); });
+        if (st) return st;
+        uint64_t tot = 0;
+        for (size_t i = 0; i < N; ++i) tot += pn[i];
+        if (hipSetDevice(c0->device) != hipSuccess) return fail(g, KMER_E_DEVICE, "hipSetDevice");
+        hipStream_t s = c0->stream;
+        HIPCHK(g, g->gkeys.ensure(tot, s));
+        HIPCHK(g, g->gvals.ensure(tot, s));
+        uint64_t o = 0;
+        for (size_t i = 0; i < N; ++i) {                 // partials -> devices[0], in child order
+            if (!pn[i]) continue;
+            kmer_ctx *c = g->group[i];
+            if (c->device == c0->device) {
+                HIPCHK(g, hipMemcpyAsync(g->gkeys.p + o, pk[i], pn[i] * 8, hipMemcpyDeviceToDevice, s));
+                HIPCHK(g, hipMemcpyAsync(g->gvals.p + o, pv[i], pn[i] * sizeof(Agg), hipMemcpyDeviceToDevice, s));
+            } else {
+                HIPCHK(g, hipMemcpyPeerAsync(g->gkeys.p + o, c0->device, pk[i], c->device, pn[i] * 8, s));
+                HIPCHK(g, hipMemcpyPeerAsync(g->gvals.p + o, c0->device, pv[i], c->device, pn[i] * sizeof(Agg), s));
+            }
+            o += pn[i];
+        }
+        HIPCHK(g, hipStreamSynchronize(s));
+        st = group_gather_records(g);
+        if (st) return st;
+        st = kmer_finish_merged(c0, g->gkeys.p, g->gvals.p, tot, total_lines, out);
+        if (st) return fail(g, st, c0->err);
+        return KMER_OK;
+    }
+    // table mode: pass-1 keys to their owners, then pass 2 + final on every child
+    std::vector<const void *> snd(N, nullptr);
+    std::vector<std::vector<uint64_t>> cnt(N, std::vector<uint64_t>(N, 0));
+    std::vector<uint64_t> parts((uint64_t)N * TAB_NB, 0);
+    kmer_status st = group_each(g, N, [&](size_t i) {
+        return kmer_table_exchange_prepare(g->group[i], (uint32_t)N, &snd[i], cnt[i].data(), parts.data() + i * TAB_NB);
+    });
+    if (st) return st;
+    std::vector<uint64_t> recv_n(N, 0);
+    st = group_each(g, N, [&](size_t o) -> kmer_status {
+        kmer_ctx *c = g->group[o];
+        hipStream_t s = c->stream;
+        uint64_t tot = 0;
+        for (size_t i = 0; i < N; ++i) tot += cnt[i][o];
+        recv_n[o] = tot;
+        if (c->trecv.ensure(std::max<uint64_t>(tot, 1), s) != hipSuccess) return fail(c, KMER_E_OOM, "receive buffer");
+        uint64_t at = 0;
+        for (size_t i = 0; i < N; ++i) {                 // runs in source order
+            uint64_t before = 0;
+            for (size_t x = 0; x < o; ++x) before += cnt[i][x];
+            if (cnt[i][o]) {
+                const uint64_t *from = (const uint64_t *)snd[i] + before;
+                const int sd = g->group[i]->device;
+                const hipError_t e = sd == c->device
+                                         ? hipMemcpyAsync(c->trecv.p + at, from, cnt[i][o] * 8, hipMemcpyDeviceToDevice, s)
+                                         : hipMemcpyPeerAsync(c->trecv.p + at, c->device, from, sd, cnt[i][o] * 8, s);
+                if (e != hipSuccess) return fail(c, KMER_E_DEVICE, std::string("HIP error: ") + hipGetErrorString(e));
+            }
+            at += cnt[i][o];
+        }
+        return hipStreamSynchronize(s) == hipSuccess ? KMER_OK : fail(c, KMER_E_DEVICE, "exchange copy");
+    });
+    if (st) return st;
+    st = group_gather_records(g);
+    if (st) return st;
+    st = group_each(g, N, [&](size_t o) {
+        kmer_ctx *c = g->group[o];
+        return kmer_table_finish_exchanged(c, c->trecv.p, recv_n[o], parts.data(), (uint32_t)N, (uint32_t)o, c->stream);
+    });
+    if (st) return st;
+    g->t_done = true;
+    uint64_t keys = 0;
+    for (size_t o = 0; o < N; ++o) {
+        uint64_t kk = 0;
+        st = kmer_table_stats(g->group[o], nullptr, &kk, nullptr);
+        if (st) return fail(g, st, g->group[o]->err);
+        keys += kk;
+    }
+    if (c0->p.max_keys && keys > c0->p.max_keys)
+        return fail(g, KMER_E_TOO_MANY_KEYS, "more distinct keys than max_keys (reference Map limit)");
+    if (!out) return KMER_OK;
+    // one host result: the children's entries (disjoint canonical classes), sorted by key bytes
+    std::vector<std::pair<std::string, uint64_t>> ents;
+    for (size_t o = 0; o < N; ++o) {
+        kmer_result *r = nullptr;
+        if (hipSetDevice(g->group[o]->device) != hipSuccess) return fail(g, KMER_E_DEVICE, "hipSetDevice");
+        st = build_table_result(g->group[o], total_lines, &r);
+        if (st) return fail(g, st, g->group[o]->err);
+        for (uint64_t i = 0; i + 1 < r->offsets.size(); ++i)
+            ents.emplace_back(std::string(r->keys.data() + r->offsets[i], r->offsets[i + 1] - r->offsets[i]), r->counts[i]);
+        kmer_result_free(r);
+    }
+    std::sort(ents.begin(), ents.end());
+    kmer_result *r = new (std::nothrow) kmer_result();
+    if (!r) return fail(g, KMER_E_OOM, "host allocation failed");
+    r->lines = total_lines;
+    for (auto &e : ents) {
+        r->keys.insert(r->keys.end(), e.first.begin(), e.first.end());
+        r->offsets.push_back(r->keys.size());
+        r->counts.push_back(e.second);
+        r->firsts.push_back(0);
+    }
+    *out = r;
+    return KMER_OK;
+}
+
+constexpr uint64_t GROUP_FILE_BATCH = 256ull << 20;
+
+kmer_status group_count_buffer(kmer_ctx *g, const uint8_t *bytes, uint64_t len, kmer_result **out) {
+    const size_t N = g->group.size();
+    // default: one batch per child (a buffer is already in host memory)
+    const uint64_t batch = g->p.batch_bytes ? g->p.batch_bytes : std::max<uint64_t>(1, (len + N - 1) / N);
+    MemSrc src(bytes, len, batch);
+    return group_count(g, src, out);
+}
+
+kmer_status group_count_file(kmer_ctx *g, const char *path, kmer_result **out) {
+    const size_t N = g->group.size();
+    FileBatches src;
+    std::string err;
+    const kmer_status st = src.open(path, g->p.batch_bytes ? g->p.batch_bytes : GROUP_FILE_BATCH, N + 2, &err);
+    if (st) return fail(g, st, err);
+    return group_count(g, src, out);
 }
 
 }  // namespace
@@ -1983,6 +2420,7 @@ kmer_status kmer_close(kmer_ctx *c) {
     c->tbig.release();
     c->tstats.release();
     c->tleft.release();
+    c->trecv.release();
     dfree(c->d_ticket); dfree(c->d_scal); dfree(c->d_pos); dfree(c->d_pos_saved);
     dfree(c->d_P); dfree(c->d_PR);
     if (c->h_small) (void)hipHostFree(c->h_small);
@@ -2055,7 +2493,7 @@ kmer_status with_long_line_retry(kmer_ctx *c, const std::function<kmer_status()>
 kmer_status count_buffer_once(kmer_ctx *c, const uint8_t *bytes, size_t len, kmer_result **out) {
     kmer_status st = reset(c);
     if (st) return st;
-    st = feed_host(c, bytes, len);
+    st = feed_host(c, bytes, len, true);
     if (st) {
         c->open_stream = false;
         return st;
@@ -2085,100 +2523,31 @@ kmer_status kmer_count_file(kmer_ctx *c, const char *path, kmer_result **out) {
 namespace {
 
 kmer_status count_file_once(kmer_ctx *c, const char *path, kmer_result **out) {
-    FILE *f = fopen(path, "rb");
-    if (!f) return fail(c, KMER_E_IO, std::string("cannot open ") + path);
-    if (hipSetDevice(c->device) != hipSuccess) {
-        fclose(f);
-        return KMER_E_DEVICE;
-    }
-    kmer_status st = reset(c);
-    // staging: one batch, but no larger than the file (a small FASTQ does not
-    // commit a 1 GiB buffer); not zero-filled; grown only for a line longer
-    // than the batch
-    uint64_t batch = c->p.batch_bytes ? c->p.batch_bytes : DEFAULT_BATCH;
-    struct stat sb;
-    if (fstat(fileno(f), &sb) == 0 && S_ISREG(sb.st_mode)) batch = std::min<uint64_t>(batch, (uint64_t)sb.st_size + 1);
-    batch = std::max<uint64_t>(batch, 1);
-    // gzip input (magic 1f 8b): read through zlib; the count is that of the
-    // decompressed FASTQ (the reference reads raw bytes only)
-    gzFile gz = nullptr;
-    {
-        unsigned char magic[2] = {0, 0};
-        const size_t m = fread(magic, 1, 2, f);
-        rewind(f);
-        if (m == 2 && magic[0] == 0x1f && magic[1] == 0x8b) {
-            gz = gzdopen(dup(fileno(f)), "rb");
-            if (!gz) {
-                fclose(f);
-                return fail(c, KMER_E_IO, std::string("cannot read gzip stream ") + path);
-            }
-            gzbuffer(gz, 1 << 20);
-            batch = std::max<uint64_t>(batch, 64ull << 20);   // (file size is the compressed size)
-            batch = std::min<uint64_t>(batch, c->p.batch_bytes ? c->p.batch_bytes : DEFAULT_BATCH);
+    if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
+    // the file is read ahead (FileBatches: a reader thread, parallel preads)
+    // in batches of batch_bytes (default 256 MiB; no larger than the file),
+    // while the device counts the batch before; gzip input (magic 1f 8b) is
+    // read through zlib, the count being that of the decompressed FASTQ
+    FileBatches src;
+    std::string err;
+    kmer_status st = src.open(path, c->p.batch_bytes ? c->p.batch_bytes : FILE_BATCH, 3, &err);
+    if (st) return fail(c, st, err);
+    st = reset(c);
+    const uint8_t *p = nullptr;
+    uint64_t n = 0;
+    kmer_status rst = KMER_OK;
+    while (!st && src.next(&p, &n, &rst, &err)) {
+        st = feed_host(c, p, n);
+        if (!st) st = settle(c);
+        if (!st && hipStreamSynchronize(c->stream) != hipSuccess) st = fail(c, KMER_E_DEVICE, "stream sync");
+        src.release(p);                           // (the batch's bytes are on the device)
+        if (!st && c->p.progress) {
+            uint64_t d = 0, t = 0;
+            src.progress(&d, &t);
+            c->p.progress(c->p.progress_user, d, t);
         }
     }
-    uint64_t cap = batch;
-    std::unique_ptr<uint8_t[]> buf(new (std::nothrow) uint8_t[cap]);
-    if (!buf) {
-        if (gz) gzclose(gz);
-        fclose(f);
-        return fail(c, KMER_E_OOM, "host staging buffer");
-    }
-    uint64_t carry = 0;
-    bool eof = false;
-    while (!st && !eof) {
-        if (carry + batch > cap) {                // (a line longer than the batch)
-            const uint64_t nc = std::max(carry + batch, cap * 2);
-            std::unique_ptr<uint8_t[]> nb(new (std::nothrow) uint8_t[nc]);
-            if (!nb) {
-                st = fail(c, KMER_E_OOM, "host staging buffer");
-                break;
-            }
-            memcpy(nb.get(), buf.get(), carry);
-            buf = std::move(nb);
-            cap = nc;
-        }
-        size_t got = 0;
-        if (gz) {
-            while (got < batch) {                 // (gzread takes an unsigned int count)
-                const unsigned want = (unsigned)std::min<uint64_t>(batch - got, 1u << 30);
-                const int r = gzread(gz, buf.get() + carry + got, want);
-                if (r < 0) break;
-                got += (size_t)r;
-                if ((unsigned)r < want) break;
-            }
-            int zerr = 0;
-            gzerror(gz, &zerr);
-            if (zerr != Z_OK && zerr != Z_BUF_ERROR) {
-                st = fail(c, KMER_E_IO, std::string("gzip read error on ") + path);
-                break;
-            }
-            if (got < batch) eof = true;
-        } else {
-            got = fread(buf.get() + carry, 1, batch, f);
-            if (got < batch) {
-                if (ferror(f)) {
-                    st = fail(c, KMER_E_IO, std::string("read error on ") + path);
-                    break;
-                }
-                eof = true;
-            }
-        }
-        const uint64_t have = carry + got;
-        uint64_t cut = have;
-        if (!eof) {
-            while (cut > 0 && buf[cut - 1] != '\n') --cut;
-            if (cut == 0) {   // one line longer than the batch: keep reading
-                carry = have;
-                continue;
-            }
-        }
-        st = feed_host(c, buf.get(), cut);
-        carry = have - cut;
-        if (carry) memmove(buf.get(), buf.get() + cut, carry);
-    }
-    if (gz) gzclose(gz);
-    fclose(f);
+    if (!st && rst) st = fail(c, rst, err + " on " + path);
     if (st) {
         c->open_stream = false;
         return st;
@@ -2536,6 +2905,21 @@ kmer_status kmer_result_device(kmer_ctx *c, const void **d_keys, const void **d_
 
 kmer_status kmer_table_stats(kmer_ctx *c, uint64_t *canonical, uint64_t *keys, uint64_t *total) {
     if (!c) return KMER_E_BAD_PARAM;
+    if (!c->group.empty()) {                         // a group: its children's shares add up
+        if (c->mode != MODE_TABLE || !c->t_done) return fail(c, KMER_E_STATE, "no table finish on this group yet");
+        uint64_t a[3] = {0, 0, 0};
+        for (kmer_ctx *x : c->group) {
+            uint64_t b[3] = {0, 0, 0};
+            if (hipSetDevice(x->device) != hipSuccess) return KMER_E_DEVICE;
+            const kmer_status st = kmer_table_stats(x, &b[0], &b[1], &b[2]);
+            if (st) return fail(c, st, x->err);
+            for (int i = 0; i < 3; ++i) a[i] += b[i];
+        }
+        if (canonical) *canonical = a[0];
+        if (keys) *keys = a[1];
+        if (total) *total = a[2];
+        return KMER_OK;
+    }
     SETTLE(c);
     if (c->mode != MODE_TABLE) return fail(c, KMER_E_STATE, "not a table-mode context (KMER_FLAG_UNORDERED)");
     if (!c->t_done) return fail(c, KMER_E_STATE, "no table finish yet");
@@ -2575,6 +2959,19 @@ kmer_status kmer_table_device(kmer_ctx *c, const void **d_entries, const void **
 
 kmer_status kmer_table_digest(kmer_ctx *c, uint64_t *digest) {
     if (!c || !digest) return KMER_E_BAD_PARAM;
+    if (!c->group.empty()) {                         // a group: its children's digests add up
+        if (c->mode != MODE_TABLE || !c->t_done) return fail(c, KMER_E_STATE, "no table finish on this group yet");
+        uint64_t a = 0;
+        for (kmer_ctx *x : c->group) {
+            uint64_t d = 0;
+            if (hipSetDevice(x->device) != hipSuccess) return KMER_E_DEVICE;
+            const kmer_status st = kmer_table_digest(x, &d);
+            if (st) return fail(c, st, x->err);
+            a += d;
+        }
+        *digest = a;
+        return KMER_OK;
+    }
     SETTLE(c);
     if (c->mode != MODE_TABLE) return fail(c, KMER_E_STATE, "not a table-mode context (KMER_FLAG_UNORDERED)");
     if (!c->t_done) return fail(c, KMER_E_STATE, "no table finish yet");

@@ -6,8 +6,9 @@
 // JS surface (used by kmers.js only):
 //   open(k, prefixBuffer, step, device, flags, maxKeys, batchBytes, devices[]) -> handle
 //     (devices: >= 2 HIP ordinals -> a multi-GPU group context, kmer_params.ndev)
-//   countFile(handle, path, cb(err, {keys, offsets, counts, lines}))
-//   countBuffer(handle, buffer, cb(err, {...}))
+//   countFile(handle, path, cb(err, {keys, offsets, counts, lines}), progress(done, total)?)
+//   countBuffer(handle, buffer, cb(err, {...}), progress(done, total)?)
+//     (progress: called on the JS thread after each input batch, kmer_params.progress)
 //   close(handle)
 //   version() -> string
 // Template matching (include/kmer_match.h; used by kmerfinder.js), synchronous:
@@ -43,7 +44,30 @@ struct Handle {
     kmer_ctx *ctx = nullptr;
     bool busy = false;
     bool close_pending = false;   // close() while a call was in flight: closed when it completes
+    napi_threadsafe_function tsfn = nullptr;   // the in-flight call's progress callback (or none)
 };
+
+// kmer_params.progress of every context: runs on the counting thread (libuv
+// pool), hands (done, total) to the JS thread through the call's
+// thread-safe function
+void progress_trampoline(void *user, uint64_t done, uint64_t total) {
+    Handle *h = static_cast<Handle *>(user);
+    if (!h->tsfn) return;
+    double *d = new double[2]{(double)done, (double)total};
+    if (napi_call_threadsafe_function(h->tsfn, d, napi_tsfn_nonblocking) != napi_ok) delete[] d;
+}
+
+void progress_call_js(napi_env env, napi_value js_cb, void *, void *data) {
+    double *d = static_cast<double *>(data);
+    if (env && js_cb) {
+        napi_value undef, args[2];
+        napi_get_undefined(env, &undef);
+        napi_create_double(env, d[0], &args[0]);
+        napi_create_double(env, d[1], &args[1]);
+        napi_call_function(env, undef, js_cb, 2, args, nullptr);
+    }
+    delete[] d;
+}
 
 struct Work {
     napi_async_work work = nullptr;
@@ -136,6 +160,8 @@ napi_value Open(napi_env env, napi_callback_info info) {
         p.devices = devs.data();
     }
     Handle *h = new Handle();
+    p.progress = progress_trampoline;
+    p.progress_user = h;
     kmer_status st = kmer_open(&p, &h->ctx);
     if (st != KMER_OK) {
         delete h;
@@ -175,6 +201,10 @@ napi_value make_f64_array(napi_env env, const uint64_t *src, size_t n) {
 void Complete(napi_env env, napi_status, void *data) {
     Work *w = static_cast<Work *>(data);
     w->h->busy = false;
+    if (w->h->tsfn) {                 // (progress calls already queued are still delivered)
+        napi_release_threadsafe_function(w->h->tsfn, napi_tsfn_release);
+        w->h->tsfn = nullptr;
+    }
     if (w->h->close_pending && w->h->ctx) {
         kmer_close(w->h->ctx);
         w->h->ctx = nullptr;
@@ -215,9 +245,16 @@ void Complete(napi_env env, napi_status, void *data) {
     delete w;
 }
 
-napi_value queue(napi_env env, Work *w, napi_value handle, napi_value cb) {
+napi_value queue(napi_env env, Work *w, napi_value handle, napi_value cb, napi_value progress) {
     napi_value name;
     napi_create_string_utf8(env, "kmerhip.count", NAPI_AUTO_LENGTH, &name);
+    if (progress) {
+        napi_valuetype t;
+        napi_typeof(env, progress, &t);
+        if (t == napi_function)
+            NAPI_CALL(env, napi_create_threadsafe_function(env, progress, nullptr, name, 0, 1, nullptr, nullptr, nullptr,
+                                                           progress_call_js, &w->h->tsfn));
+    }
     NAPI_CALL(env, napi_create_reference(env, cb, 1, &w->cb));
     NAPI_CALL(env, napi_create_reference(env, handle, 1, &w->href));
     NAPI_CALL(env, napi_create_async_work(env, nullptr, name, Execute, Complete, w, &w->work));
@@ -229,8 +266,8 @@ napi_value queue(napi_env env, Work *w, napi_value handle, napi_value cb) {
 }
 
 napi_value CountFile(napi_env env, napi_callback_info info) {
-    size_t argc = 3;
-    napi_value argv[3];
+    size_t argc = 4;
+    napi_value argv[4];
     NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
     Handle *h = get_handle(env, argv[0]);
     if (!h) return nullptr;
@@ -247,12 +284,12 @@ napi_value CountFile(napi_env env, napi_callback_info info) {
     w->path.resize(n);
     w->h = h;
     w->is_file = true;
-    return queue(env, w, argv[0], argv[2]);
+    return queue(env, w, argv[0], argv[2], argc > 3 ? argv[3] : nullptr);
 }
 
 napi_value CountBuffer(napi_env env, napi_callback_info info) {
-    size_t argc = 3;
-    napi_value argv[3];
+    size_t argc = 4;
+    napi_value argv[4];
     NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
     Handle *h = get_handle(env, argv[0]);
     if (!h) return nullptr;
@@ -269,7 +306,7 @@ napi_value CountBuffer(napi_env env, napi_callback_info info) {
     w->bytes = (const uint8_t *)data;
     w->len = len;
     NAPI_CALL(env, napi_create_reference(env, argv[1], 1, &w->keep));
-    return queue(env, w, argv[0], argv[2]);
+    return queue(env, w, argv[0], argv[2], argc > 3 ? argv[3] : nullptr);
 }
 
 napi_value Close(napi_env env, napi_callback_info info) {

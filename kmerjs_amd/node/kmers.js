@@ -122,6 +122,15 @@ function devices(kmerObj) {
     return env ? env.split(',').map(Number) : [];
 }
 
+const KMER_FLAG_UNORDERED = 16;
+const KMER_FLAG_CANONICAL = 64;
+function modeFlags(mode) {
+    if (mode === undefined || mode === 'ordered') return 0;
+    if (mode === 'unordered') return KMER_FLAG_UNORDERED;
+    if (mode === 'canonical') return KMER_FLAG_CANONICAL;
+    throw new Error(`kmerjs_amd: unknown mode '${mode}' (ordered, unordered, canonical)`);
+}
+
 function tooManyKeys(msg) {
     const e = new RangeError(msg);
     e.status = KMER_E_TOO_MANY_KEYS;
@@ -142,6 +151,12 @@ class KmerJS {
         this.kmerMapSize = 0;
         this.env = env;
         this.maxKeys = MAP_MAX_KEYS;     // the reference Map's limit (lib/kmers.js:95)
+        // extension: 'ordered' (the reference's Map, insertion order) or the
+        // table modes for inputs whose Map is too large to build (BASELINE C3 /
+        // C5): 'unordered' (the same keys and counts, sorted by key) and
+        // 'canonical' (one key per {x, rc x} class; kmer_api.h KMER_FLAG_*)
+        this.mode = 'ordered';
+        this.batchBytes = 0;             // extension: input batch size (0 = the library's default)
         if (env === 'browser') this.fileDataRead = 0;
     }
 
@@ -173,11 +188,32 @@ class KmerJS {
                 // (the native result alone may not exceed the limit; a pre-filled
                 // Map is checked again after the fold)
                 handle = native().open(kmerObj.kmerLength, Buffer.from(String(kmerObj.preffix), 'latin1'),
-                    kmerObj.step, Number(process.env.KMERHIP_DEVICE || 0), 0, kmerObj.maxKeys, 0, devices(kmerObj));
+                    kmerObj.step, Number(process.env.KMERHIP_DEVICE || 0), modeFlags(kmerObj.mode), kmerObj.maxKeys,
+                    kmerObj.batchBytes || 0, devices(kmerObj));
             } catch (e) {
                 reject(e);
                 return;
             }
+            // the progress-stream of lib/kmers.js:108-110: one 'progress' event
+            // per input batch read (progress-stream's fields; bytesRead follows)
+            const t0 = Date.now();
+            let lastDone = 0;
+            const onProgress = (done, total) => {
+                const runtime = (Date.now() - t0) / 1000;
+                const speed = runtime > 0 ? done / runtime : 0;
+                kmerObj.bytesRead = done;
+                event.emit('progress', {
+                    percentage: total ? (100 * done) / total : 0,
+                    transferred: done,
+                    length: total,
+                    remaining: total > done ? total - done : 0,
+                    eta: speed > 0 && total > done ? Math.round((total - done) / speed) : 0,
+                    runtime: Math.round(runtime),
+                    delta: done - lastDone,
+                    speed,
+                });
+                lastDone = done;
+            };
             native().countFile(handle, String(kmerObj.fastq), (err, res) => {
                 native().close(handle);
                 if (err) {
@@ -196,14 +232,13 @@ class KmerJS {
                     return;
                 }
                 kmerObj.lines = res.lines;
-                event.emit('progress', { percentage: 100, transferred: 0, length: 0 });
                 if (kmerObj.progress) {
                     process.stdout.write(`Lines: ${res.lines} / Kmers: ${kmerObj.kmerMap.size}\r`);
                     process.stdout.write('\n                               \n');
                 }
                 kmerObj.kmerMapSize = kmerObj.kmerMap.size;
                 resolve(kmerObj.kmerMap);
-            });
+            }, onProgress);
         });
         return { promise, event };
     }

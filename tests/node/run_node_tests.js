@@ -232,6 +232,61 @@ async function gpuTests() {
             results.push({ name: `readFile on devices [0,0] ${c.input}`, ok: false, err: String(e) });
         }
     }
+    // readFile() progress (lib/kmers.js:108-110): one 'progress' event per input
+    // batch, with real byte counts; bytesRead follows; same Map as one batch
+    {
+        const file = path.join(repo, 'tests', 'golden', 'inputs', 'test_long.kmer.fastq');
+        const size = fs.statSync(file).size;
+        const c = golden.cases.find((x) => x.input === 'test_long.kmer.fastq' && x.prefix === 'ATGAC' && x.k === 16
+            && x.step === 1);
+        for (const devs of [[], [0, 0, 0]]) {
+            const kj = new KmerJS(file, 'ATGAC', 16, 1, 1, false);
+            kj.batchBytes = 1 << 16;
+            kj.devices = devs;
+            const ev = [];
+            const rf = kj.readFile();
+            rf.event.on('progress', (p) => ev.push(p));
+            try {
+                const m = await rf.promise;
+                await new Promise((r) => setImmediate(r));      // (events queued before the result)
+                const last = ev[ev.length - 1] || {};
+                const mono = ev.every((p, i) => i === 0 || p.transferred >= ev[i - 1].transferred);
+                const ok = sha(JSON.stringify([...m])) === c.digest && ev.length >= 2 && mono
+                    && last.transferred === size && last.length === size && last.percentage === 100
+                    && kj.bytesRead === size;
+                results.push({ name: `readFile progress events [${devs}] (${ev.length})`, ok });
+            } catch (e) {
+                results.push({ name: `readFile progress events [${devs}]`, ok: false, err: String(e) });
+            }
+        }
+    }
+    // table modes through readFile() (BASELINE C3 / C5 from the reference's entry
+    // point): the same keys and counts as the ordered Map, sorted by key; and
+    // canonical classes; on one device and on a device group
+    {
+        const file = path.join(repo, 'tests', 'golden', 'inputs', 'test_long.kmer.fastq');
+        const kj = new KmerJS(file, '', 21, 1, 1, false);
+        const ordered = await kj.readFile().promise;
+        const want = [...ordered].sort((a, b) => (a[0] < b[0] ? -1 : a[0] > b[0] ? 1 : 0));
+        for (const devs of [[], [0, 0]]) {
+            const ku = new KmerJS(file, '', 21, 1, 1, false);
+            ku.mode = 'unordered';
+            ku.devices = devs;
+            const kc = new KmerJS(file, '', 21, 1, 1, false);
+            kc.mode = 'canonical';
+            kc.devices = devs;
+            try {
+                const mu = await ku.readFile().promise;
+                const mc = await kc.readFile().promise;
+                const okU = JSON.stringify([...mu]) === JSON.stringify(want);
+                const okC = mc.size > 0 && [...mc].every(([k, v]) => k <= complement(k)
+                    && ordered.get(k) === (k === complement(k) ? 2 * v : v));
+                results.push({ name: `readFile table modes [${devs}]`, ok: okU && okC, detail: { okU, okC } });
+            } catch (e) {
+                results.push({ name: `readFile table modes [${devs}]`, ok: false, err: String(e) });
+            }
+        }
+    }
     // close() while a count is in flight: closed when it completes (no use after free)
     {
         const nat = lib.native();

@@ -124,6 +124,34 @@ def test_count_file_and_missing_file(native, tmp_path, inputs):
     ctr.close()
 
 
+def test_count_file_reads_ahead_with_progress(native, tmp_path, inputs, golden):
+    """kmer_count_file reads the file ahead in batches (FileBatches) and calls
+    kmer_params.progress after each (lib/kmers.js:108-110's progress-stream):
+    monotone byte counts ending at the file size; results equal the one-batch
+    count, for plain and gzip files and a line longer than a batch."""
+    import gzip
+    from oracle import oracle
+    data = inputs["test_long.kmer.fastq"] + b"@long\n" + b"ACGT" * 50_000 + b"\n+\n" + b"I" * 200_000 + b"\n"
+    want = oracle.count_buffer(data, b"AC", 16, 1)
+    f = tmp_path / "a.fastq"
+    f.write_bytes(data)
+    fz = tmp_path / "a.fastq.gz"
+    fz.write_bytes(gzip.compress(data))
+    for path, size in ((f, len(data)), (fz, fz.stat().st_size)):
+        seen = []
+        ctr = native.Counter(k=16, prefix=b"AC", batch_bytes=1 << 16, progress=lambda d, t: seen.append((d, t)))
+        r = ctr.count_file(str(path))
+        ctr.close()
+        assert r.entries() == want
+        assert len(seen) >= 3 and seen[-1] == (size, size), (str(path), seen[-3:])
+        assert all(b[0] >= a[0] for a, b in zip(seen, seen[1:]))
+    seen = []
+    ctr = native.Counter(k=16, prefix=b"AC", batch_bytes=1 << 16, progress=lambda d, t: seen.append((d, t)))
+    assert ctr.count_buffer(data).entries() == want
+    ctr.close()
+    assert len(seen) >= 3 and seen[-1] == (len(data), len(data))
+
+
 def test_non_ascii_rejected(native):
     ctr = native.Counter()
     with pytest.raises(native.KmerError) as ei:

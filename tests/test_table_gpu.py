@@ -73,21 +73,27 @@ def _device_input(n, seed=3):
 
 @pytest.mark.parametrize("k,prefix", [(31, b""), (16, b""), (21, b"A"), (16, b"ATGAC"), (32, b"GT")])
 def test_table_synthetic_vs_oracle(native, k, prefix):
+    # every entry (keys compared as sorted 2-bit codes: byte order) vs the oracle
     from oracle import oracle
-    buf = _device_input(100_000)
+    from tests.util import packed_sorted, result_packed_sorted, same_packed
+    buf = _device_input(30_000)
     host = buf.cpu().numpy().tobytes()
-    want = sorted(oracle.count_buffer(host, prefix, k, 1))
+    keys_o, cnt_o = oracle.count_arrays(host, prefix, k)
+    want = packed_sorted(keys_o, cnt_o)
     ctr = native.Counter(k=k, prefix=prefix, flags=native.FLAG_UNORDERED)
     ctr.reset()
     ctr.feed_device(buf.data_ptr(), len(host))
-    got = ctr.finish().entries()
+    res = ctr.finish()
     canon, keys, total = ctr.table_stats()
     with pytest.raises(native.KmerError):          # no ordered device result in table mode
         ctr.result_device()
     ctr.close()
-    assert len(got) == len(want)
-    assert first_diff(got, want) is None
-    assert keys == len(want) and total == sum(v for _, v in want)
+    assert len(res) == len(cnt_o)
+    assert same_packed(result_packed_sorted(res, k), want)
+    assert keys == len(cnt_o) and total == int(cnt_o.sum())
+    if len(res):                                   # the host result is in key byte order
+        kb = np.frombuffer(res.keybuf, dtype=np.uint8).reshape(-1, k)
+        assert bytes(kb[0]) <= bytes(kb[len(kb) // 2]) <= bytes(kb[-1])
 
 
 def test_table_chunked_feeds_match_one_feed(native):
@@ -95,15 +101,17 @@ def test_table_chunked_feeds_match_one_feed(native):
     buf = _device_input(60_000, seed=9)
     n = buf.numel()
     ctr = native.Counter(k=31, prefix=b"", flags=native.FLAG_UNORDERED)
-    one = ctr.count_buffer(buf.cpu().numpy().tobytes()).entries()
+    one = ctr.count_buffer(buf.cpu().numpy().tobytes())
+    d1 = ctr.table_digest()
     ctr.reset()
     cuts = [0, 317 * 7, 317 * 20_000, 317 * 20_001, 317 * 45_000, n]
     for lo, hi in zip(cuts, cuts[1:]):
         ctr.feed_device(buf.data_ptr() + lo, hi - lo)
     torch.cuda.synchronize()
-    many = ctr.finish().entries()
+    many = ctr.finish()
+    assert ctr.table_digest() == d1
     ctr.close()
-    assert many == one
+    assert many.keybuf == one.keybuf and np.array_equal(many.counts, one.counts)
 
 
 def test_table_realistic_reads_with_n(native):
@@ -115,12 +123,14 @@ def test_table_realistic_reads_with_n(native):
     seq[rng.random(len(seq)) < 0.8, 0] = ord("N")
     arr[:, 13:163] = seq
     data = arr.tobytes()
+    from tests.util import packed_sorted, result_packed_sorted, same_packed
     for k, p in ((16, b""), (31, b""), (21, b"GT")):
-        want = sorted(oracle.count_buffer(data, p, k, 1))
+        want = packed_sorted(*oracle.count_arrays(data, p, k))
+        assert len(want[2]) > 100                   # record keys (windows with N)
         ctr = native.Counter(k=k, prefix=p, flags=native.FLAG_UNORDERED)
-        got = ctr.count_buffer(data).entries()
+        got = result_packed_sorted(ctr.count_buffer(data), k)
         ctr.close()
-        assert first_diff(got, want) is None, (k, p)
+        assert same_packed(got, want), (k, p)
 
 
 def test_table_big_counts(native):
@@ -207,7 +217,7 @@ def test_table_digest_matches_oracle(native, k, flags_name):
     from oracle import oracle
     from tests.util import canonical_summary
     rng = np.random.default_rng(k)
-    arr = np.frombuffer(bytearray(oracle.synth_fastq(8, 0, 30000)), dtype=np.uint8).reshape(-1, 317).copy()
+    arr = np.frombuffer(bytearray(oracle.synth_fastq(8, 0, 12000)), dtype=np.uint8).reshape(-1, 317).copy()
     seq = arr[:, 13:163]
     seq[rng.random(seq.shape) < 0.001] = ord("N")
     arr[:, 13:163] = seq
@@ -252,6 +262,64 @@ def test_c5_contigs_canonical_vs_oracle(native):
         c = min(kk, rc)
         assert got[c] == (int(cnt[i]) // 2 if kk == rc else int(cnt[i]))
     ctr.close()
+
+
+@pytest.mark.parametrize("devs", [[0, 0], [0, 0, 0]])
+def test_table_group_through_the_c_abi(native, inputs, devs, tmp_path):
+    """kmer_params.ndev in table and canonical mode (BASELINE C3 / C5 on several
+    GPUs through the reference's entry point, lib/kmers.js:106): the input
+    streams in batches dealt round robin over the group (an ordinal repeated on
+    a one-GPU box), pass-1 keys go to the child owning their hash-space slice,
+    every child builds its slice -- the host result, the statistics and the
+    table digest equal the one-context table's; through kmer_count_buffer and
+    through kmer_count_file in small batches, plain and gzip."""
+    import gzip
+    from oracle import oracle
+    rng = np.random.default_rng(len(devs))
+    arr = np.frombuffer(bytearray(oracle.synth_fastq(12, 0, 20000)), dtype=np.uint8).reshape(-1, 317).copy()
+    seq = arr[:, 13:163]
+    seq[rng.random(seq.shape) < 0.001] = ord("N")
+    arr[:, 13:163] = seq
+    datas = [arr.tobytes(), inputs["test_long.kmer.fastq"], inputs["edge_contigs.fsa"], inputs["edge_blank.fastq"]]
+    for flags, k, p in ((native.FLAG_UNORDERED, 31, b""), (native.FLAG_CANONICAL, 21, b""),
+                        (native.FLAG_UNORDERED, 16, b"AC")):
+        one = native.Counter(k=k, prefix=p, flags=flags)
+        grp = native.Counter(k=k, prefix=p, flags=flags, devices=devs)
+        small = native.Counter(k=k, prefix=p, flags=flags, devices=devs, batch_bytes=1 << 16)
+        for di, data in enumerate(datas):
+            want = one.count_buffer(data)
+            ws, wd = one.table_stats(), one.table_digest()
+            got = grp.count_buffer(data)
+            assert got.entries() == want.entries() and got.lines == want.lines, (flags, k, di)
+            assert grp.table_stats() == ws and grp.table_digest() == wd
+            f = tmp_path / ("in%d.fastq" % di)
+            f.write_bytes(data)
+            fz = tmp_path / ("in%d.fastq.gz" % di)
+            fz.write_bytes(gzip.compress(data))
+            for path in (f, fz):
+                got = small.count_file(str(path))
+                assert got.entries() == want.entries() and got.lines == want.lines, (flags, k, di, str(path))
+                assert small.table_stats() == ws and small.table_digest() == wd
+        for c in (one, grp, small):
+            c.close()
+
+
+def test_ordered_group_streams_small_batches(native, inputs, tmp_path):
+    """An ordered group count of a file in 64 KiB batches dealt round robin
+    over 3 children (positions from a running newline count) equals the
+    oracle's Map, order included; a trailing line without '\n' too."""
+    from oracle import oracle
+    data = oracle.synth_fastq(13, 0, 8000) + inputs["test_kmers.fastq"] + b"@x\nACGTACGTACGTACGTACGTAAA"
+    f = tmp_path / "s.fastq"
+    f.write_bytes(data)
+    for k, p in ((16, b"ATGAC"), (21, b"")):
+        want = oracle.count_buffer(data, p, k, 1)
+        ctr = native.Counter(k=k, prefix=p, devices=[0, 0, 0], batch_bytes=1 << 16)
+        r = ctr.count_file(str(f))
+        assert first_diff(r.entries(), want) is None and r.lines == data.count(b"\n") + 1
+        r = ctr.count_buffer(data)
+        assert first_diff(r.entries(), want) is None
+        ctr.close()
 
 
 def _table_dump(native, ctr):

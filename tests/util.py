@@ -41,13 +41,19 @@ def planar_codes(keys, k):
     """(n, k) uint8 A/C/G/T keys -> (code, rc code): code = hi_plane << k | lo_plane,
     base i at bit i of each plane, A/C/G/T = (hi, lo) 00/01/10/11 (kmer_api.h)."""
     import numpy as np
-    b = keys.astype(np.uint64)
-    lo = ((b >> np.uint64(1)) ^ (b >> np.uint64(2))) & np.uint64(1)
-    hi = (b >> np.uint64(2)) & np.uint64(1)
-    w = np.uint64(1) << np.arange(k, dtype=np.uint64)
-    wr = w[::-1]
-    flo, fhi = (lo * w).sum(1), (hi * w).sum(1)
-    rlo, rhi = ((np.uint64(1) - lo) * wr).sum(1), ((np.uint64(1) - hi) * wr).sum(1)
+    n = keys.shape[0]
+    flo = np.zeros(n, np.uint64)
+    fhi = np.zeros(n, np.uint64)
+    rlo = np.zeros(n, np.uint64)
+    rhi = np.zeros(n, np.uint64)
+    for i in range(k):
+        b = keys[:, i]
+        lo = (((b >> 1) ^ (b >> 2)) & 1).astype(np.uint64)
+        hi = ((b >> 2) & 1).astype(np.uint64)
+        flo |= lo << np.uint64(i)
+        fhi |= hi << np.uint64(i)
+        rlo |= (lo ^ np.uint64(1)) << np.uint64(k - 1 - i)      # rc: reversed, complemented
+        rhi |= (hi ^ np.uint64(1)) << np.uint64(k - 1 - i)
     return (fhi << np.uint64(k)) | flo, (rhi << np.uint64(k)) | rlo
 
 
@@ -82,3 +88,33 @@ def table_digest_from_map(entries, k):
     with np.errstate(over="ignore"):
         h = cf[rep] * np.uint64(_MUL)
         return int((w * _digest_mix(h)).sum(dtype=np.uint64))
+
+
+def packed_sorted(keys, cnt):
+    """Rows of (n, k) uint8 keys (k <= 32) with counts -> (A/C/G/T rows as
+    2-bit codes, first base most significant -- byte order -- sorted, their
+    counts, {other row bytes: count}).  For comparing large table results."""
+    import numpy as np
+    n, k = keys.shape
+    lut = np.full(256, 255, np.uint8)
+    lut[list(b"ACGT")] = np.arange(4, dtype=np.uint8)
+    v = lut[keys]
+    ok = (v != 255).all(axis=1)
+    code = np.zeros(n, np.uint64)
+    for i in range(k):
+        code = (code << np.uint64(2)) | (v[:, i] & 3).astype(np.uint64)
+    o = np.argsort(code[ok], kind="stable")
+    other = {keys[i].tobytes(): int(cnt[i]) for i in np.nonzero(~ok)[0]}
+    return code[ok][o], cnt[ok][o], other
+
+
+def result_packed_sorted(res, k):
+    """packed_sorted of a kmer result whose keys all have length k."""
+    import numpy as np
+    keys = np.frombuffer(res.keybuf, dtype=np.uint8).reshape(-1, k) if len(res) else np.zeros((0, k), np.uint8)
+    return packed_sorted(keys, res.counts)
+
+
+def same_packed(a, b):
+    import numpy as np
+    return np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]
