@@ -218,8 +218,8 @@ struct kmer_ctx {
     // the group itself owns no device state beyond the merge buffers on
     // devices[0] (allocated through child 0)
     std::vector<kmer_ctx *> group;
-    DBuf<uint64_t> gkeys;
-    DBuf<Agg> gvals;
+    DBuf<uint64_t> gkeys, gkeys2;
+    DBuf<Agg> gvals, gvals2;
     double t_ms[6] = {};           // table phase times since the reset: lines, hist1, scatter1, hist2, scatter2, final
     int n_cu = 0;
     // timing (HIP events on the context stream)
@@ -1917,6 +1917,27 @@ struct FileBatches : GroupSrc {
     }
 };
 
+// group partials, concatenated by child: each child's partial is in
+// first-occurrence order but the children's batches interleave, so the
+// concatenation is re-ordered by first occurrence (radix sort of first ->
+// index, then a gather) before kmer_finish_merged, which takes index = rank
+__global__ __launch_bounds__(256) void partial_firsts_kernel(const Agg *vals, uint64_t n, uint64_t *firsts,
+                                                             uint32_t *idx) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        firsts[i] = vals[i].first;
+        idx[i] = (uint32_t)i;
+    }
+}
+
+__global__ __launch_bounds__(256) void partial_gather_kernel(const uint64_t *keys, const Agg *vals, const uint32_t *idx,
+                                                             uint64_t n, uint64_t *okeys, Agg *ovals) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t j = idx[i];
+        okeys[i] = keys[j];
+        ovals[i] = vals[j];
+    }
+}
+
 uint64_t count_newlines(const uint8_t *p, uint64_t n) {
     uint64_t c = 0;
     const uint8_t *e = p + n;
@@ -2093,6 +2114,28 @@ kmer_status group_count(kmer_ctx *g, GroupSrc &src, kmer_result **out) {
                 HIPCHK(g, hipMemcpyPeerAsync(g->gvals.p + o, c0->device, pv[i], c->device, pn[i] * sizeof(Agg), s));
             }
             o += pn[i];
+        }
+        if (nb > N && tot > 1) {                     // (batches interleaved over the children)
+            if (tot >= (1ull << 32)) return fail(g, KMER_E_TOO_MANY_KEYS, "more than 2^32 partial entries");
+            HIPCHK(g, c0->xord.ensure(tot, s));
+            HIPCHK(g, c0->xord2.ensure(tot, s));
+            HIPCHK(g, c0->ridx.ensure(tot, s));
+            HIPCHK(g, c0->ridx2.ensure(tot, s));
+            const uint32_t grid = (uint32_t)std::min<uint64_t>((tot + 255) / 256, 16384);
+            hipLaunchKernelGGL(partial_firsts_kernel, dim3(grid), dim3(256), 0, s, g->gvals.p, tot, c0->xord.p,
+                               c0->ridx.p);
+            HIPCHK(g, hipGetLastError());
+            rocprim::double_buffer<uint64_t> kb(c0->xord.p, c0->xord2.p);
+            rocprim::double_buffer<uint32_t> vb(c0->ridx.p, c0->ridx2.p);
+            kmer_ctx *c = c0;                         // (ROCPRIM_RUN's scratch)
+            ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, kb, vb, (size_t)tot, 0, 64, s));
+            HIPCHK(g, g->gkeys2.ensure(tot, s));
+            HIPCHK(g, g->gvals2.ensure(tot, s));
+            hipLaunchKernelGGL(partial_gather_kernel, dim3(grid), dim3(256), 0, s, g->gkeys.p, g->gvals.p,
+                               vb.current(), tot, g->gkeys2.p, g->gvals2.p);
+            HIPCHK(g, hipGetLastError());
+            std::swap(g->gkeys, g->gkeys2);
+            std::swap(g->gvals, g->gvals2);
         }
         HIPCHK(g, hipStreamSynchronize(s));
         st = group_gather_records(g);
@@ -2374,6 +2417,8 @@ kmer_status kmer_close(kmer_ctx *c) {
         if (hipSetDevice(c->group[0]->device) == hipSuccess) {
             c->gkeys.release();
             c->gvals.release();
+            c->gkeys2.release();
+            c->gvals2.release();
         }
         for (kmer_ctx *x : c->group) kmer_close(x);
         delete c;

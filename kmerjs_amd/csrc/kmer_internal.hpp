@@ -414,7 +414,8 @@ struct TabFinal {
     uint32_t sub_bits;             // (unused: ranges are sized per unit from range_keys)
     uint32_t range_keys;           // target keys per LDS range (small buckets are grouped up to it)
     uint32_t cap;                  // claims per range before it is split (<= TAB_CAP)
-    uint32_t ablate;               // experiments only (results WRONG): 1 no insert, 2 no emit
+    uint32_t ablate;               // experiments only (results WRONG): 1 no insert, 2 no emit; sort kernel:
+                                   // 8 no bin scan, 16 no statistics, 32 no entry stores
     TabBig *big;
     unsigned long long *big_count;
     uint64_t big_cap;

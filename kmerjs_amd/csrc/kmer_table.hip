@@ -347,14 +347,16 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2_kernel(const uint64_t *B
     cur[t] = H2s[un.hbase + (uint64_t)t * un.nunits + un.u];
     bcnt[t] = 0;
     __syncthreads();
-    for (uint32_t r0 = 0; r0 < un.len; r0 += TAB_ROUND) {
-        uint64_t key[TAB_RPL];
-        uint32_t rank[TAB_RPL];
+    // the next round's keys are loaded as soon as this round's sit in LDS, in
+    // flight while the round is written out
+    uint64_t key[TAB_RPL];
 #pragma unroll
-        for (int j = 0; j < TAB_RPL; ++j) {
-            const uint32_t i = r0 + j * TAB_WG1 + t;
-            key[j] = i < un.len ? src[i] : 0;
-        }
+    for (int j = 0; j < TAB_RPL; ++j) {
+        const uint32_t i = j * TAB_WG1 + t;
+        key[j] = i < un.len ? src[i] : 0;
+    }
+    for (uint32_t r0 = 0; r0 < un.len; r0 += TAB_ROUND) {
+        uint32_t rank[TAB_RPL];
 #pragma unroll
         for (int j = 0; j < TAB_RPL; ++j) {
             const uint32_t i = r0 + j * TAB_WG1 + t;
@@ -371,6 +373,11 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2_kernel(const uint64_t *B
             if (i < un.len) srt[bst[(uint32_t)(key[j] >> TAB_RBITS) & (TAB_NB - 1)] + rank[j]] = key[j];
         }
         __syncthreads();
+#pragma unroll
+        for (int j = 0; j < TAB_RPL; ++j) {
+            const uint32_t i = r0 + TAB_ROUND + j * TAB_WG1 + t;
+            key[j] = i < un.len ? src[i] : 0;
+        }
         for (uint32_t i = t; i < total; i += TAB_WG1) {
             const uint64_t h = srt[i];
             const uint32_t b = (uint32_t)(h >> TAB_RBITS) & (TAB_NB - 1);
@@ -936,8 +943,17 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
     const uint32_t per = (a.qhi - a.qlo + gridDim.x - 1) / gridDim.x;
     const uint32_t q0 = min(a.qlo + blockIdx.x * per, a.qhi), q1 = q0 + per < a.qhi ? q0 + per : a.qhi;
     uint64_t st_canon = 0, st_keys = 0, st_sum = 0;
+    // no prefix, odd k, Map view (C3): every entry is two Map keys, never a
+    // palindrome -- no decoding needed
+    const bool plain_odd = a.pmask == 0 && !a.canonical && (k & 1u);
     // Map statistics of one canonical entry h (App. A.6; as in tab_final_kernel)
     auto account = [&](uint64_t h, uint64_t cnt) {
+        if (plain_odd) {
+            st_canon += 1;
+            st_keys += 2;
+            st_sum += 2 * cnt;
+            return;
+        }
         const uint64_t code = h * a.inv;
         const uint32_t lo = (uint32_t)code & kmask, hi = (uint32_t)(code >> k) & kmask;
         const uint32_t rlo2 = __brev(~lo & kmask) >> sh, rhi2 = __brev(~hi & kmask) >> sh;
@@ -1067,51 +1083,81 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                     pk[j] = pk[j] << 14 | pos;
                 }
             __syncthreads();
-            // every held key scans its bin [end of bin b - 1, end of bin b):
-            // the first copy emits (key, copies)
+            // every held key scans its bin [end of bin b - 1, end of bin b) for
+            // copies of itself; the first copy emits (key, copies).  Keys go in
+            // groups of G, element m of all G bins read together (G LDS reads
+            // in flight per step, steps = the largest bin of the group: ~3 keys
+            // per bin at C3) instead of one key's bin after another.
+            constexpr int G = ONE ? 8 : 4;
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                if (!__any(left > j * (int)TAB_SWG)) break;
-                const uint32_t b = pk[j] >> 14, p = pk[j] & 0x3FFFu;
-                const uint64_t xj = ((uint64_t)(ONE ? b : hi[ONE ? 0 : j]) << 32) | lo[j];
-                bool first = false;
-                uint32_t cnt = 0;
-                if (left > j * (int)TAB_SWG) {
-                    const uint32_t b0 = b ? bst[b - 1] : 0u, b1 = bst[b];
-                    first = true;
-                    for (uint32_t m = b0; m < b1; ++m) {
-                        const bool eq = ONE ? lkey[m] == lo[j] : lkey64[m] == xj;
-                        first &= !(eq && m < p);
-                        cnt += eq ? 1u : 0u;
+            for (int g0 = 0; g0 < KPT; g0 += G) {
+                if (!__any(left > g0 * (int)TAB_SWG)) break;
+                uint32_t bb[G], cf[G], cmax = 0;          // bb: b0 | c << 14; cf: copies | first << 8
+#pragma unroll
+                for (int u = 0; u < G; ++u) {
+                    const int j = g0 + u;
+                    const bool valid = left > j * (int)TAB_SWG;
+                    const uint32_t b = pk[j] >> 14;
+                    const uint32_t b0 = b ? bst[b - 1] : 0u, b1 = (a.ablate & 8) ? b0 : bst[b];
+                    const uint32_t c = valid ? b1 - b0 : 0u;
+                    bb[u] = b0 | c << 14;
+                    cf[u] = valid ? ((a.ablate & 8) ? 0x101u : 0x100u) : 0u;   // (experiments: no bin scan)
+                    cmax = max(cmax, c);
+                }
+                for (uint32_t m = 0; m < cmax; ++m) {
+#pragma unroll
+                    for (int u = 0; u < G; ++u) {
+                        const int j = g0 + u;
+                        const uint32_t b0 = bb[u] & 0x3FFFu, c = bb[u] >> 14;
+                        const bool in = m < c;
+                        const uint32_t mm = in ? b0 + m : b0;
+                        bool eq;
+                        if (ONE) {
+                            eq = in && lkey[mm] == lo[j];
+                        } else {
+                            const uint64_t xk = ((uint64_t)hi[ONE ? 0 : j] << 32) | lo[j];
+                            eq = in && lkey64[mm] == xk;
+                        }
+                        cf[u] += eq ? 1u : 0u;
+                        if (eq && b0 + m < (pk[j] & 0x3FFFu)) cf[u] &= 0xFFu;    // an earlier copy
                     }
                 }
-                // output slots: one LDS counter bump per wave and bucket present
-                unsigned long long fm = __ballot(first);
-                uint32_t pos = 0, ql = 0;
-                if (ONE) {
-                    if (fm) {
-                        const int ld = __ffsll((long long)fm) - 1;
-                        uint32_t base = 0;
-                        if (lane == (uint32_t)ld) base = atomicAdd(&nout[0], (uint32_t)__popcll(fm));
-                        base = (uint32_t)__shfl((int)base, ld);
-                        pos = base + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
+#pragma unroll
+                for (int u = 0; u < G; ++u) {
+                    const int j = g0 + u;
+                    const uint32_t b = pk[j] >> 14;
+                    const uint64_t xj = ((uint64_t)(ONE ? b : hi[ONE ? 0 : j]) << 32) | lo[j];
+                    const bool first = (cf[u] >> 8) != 0u;
+                    const uint32_t cnt = cf[u] & 0xFFu;
+                    // output slots: one LDS counter bump per wave and bucket present
+                    unsigned long long fm = __ballot(first);
+                    uint32_t pos = 0, ql = 0;
+                    if (ONE) {
+                        if (fm) {
+                            const int ld = __ffsll((long long)fm) - 1;
+                            uint32_t base = 0;
+                            if (lane == (uint32_t)ld) base = atomicAdd(&nout[0], (uint32_t)__popcll(fm));
+                            base = (uint32_t)__shfl((int)base, ld);
+                            pos = base + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
+                        }
+                    } else {
+                        ql = (uint32_t)(xj >> TAB_RBITS);
+                        while (fm) {
+                            const int ld = __ffsll((long long)fm) - 1;
+                            const uint32_t qx = (uint32_t)__shfl((int)ql, ld);
+                            const unsigned long long mq = __ballot(first && ql == qx);
+                            uint32_t base = 0;
+                            if (lane == (uint32_t)ld) base = atomicAdd(&nout[qx], (uint32_t)__popcll(mq));
+                            base = (uint32_t)__shfl((int)base, ld);
+                            if (first && ql == qx) pos = base + (uint32_t)__popcll(mq & ((1ull << lane) - 1ull));
+                            fm &= ~mq;
+                        }
                     }
-                } else {
-                    ql = (uint32_t)(xj >> TAB_RBITS);
-                    while (fm) {
-                        const int ld = __ffsll((long long)fm) - 1;
-                        const uint32_t qx = (uint32_t)__shfl((int)ql, ld);
-                        const unsigned long long mq = __ballot(first && ql == qx);
-                        uint32_t base = 0;
-                        if (lane == (uint32_t)ld) base = atomicAdd(&nout[qx], (uint32_t)__popcll(mq));
-                        base = (uint32_t)__shfl((int)base, ld);
-                        if (first && ql == qx) pos = base + (uint32_t)__popcll(mq & ((1ull << lane) - 1ull));
-                        fm &= ~mq;
+                    if (first) {
+                        if (!(a.ablate & 32))
+                            a.out[(ONE ? s0 : sc[q + ql - cbase]) + pos] = ((xj & TAB_RMASK) << 20) | cnt;
+                        if (!(a.ablate & 16)) account(qbase + xj, cnt);
                     }
-                }
-                if (first) {
-                    a.out[(ONE ? s0 : sc[q + ql - cbase]) + pos] = ((xj & TAB_RMASK) << 20) | cnt;
-                    account(qbase + xj, cnt);
                 }
             }
             return true;

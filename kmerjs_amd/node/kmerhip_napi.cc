@@ -22,6 +22,10 @@
 //   matchClose(match)
 #include <node_api.h>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -634,7 +638,22 @@ napi_value MatchClose(napi_env env, napi_callback_info info) {
     return u;
 }
 
+// KMERHIP_SEGV_TRACE=1 (diagnostics): a backtrace on stderr for a fatal signal
+void segv_trace(int sig) {
+    void *fr[64];
+    const int n = backtrace(fr, 64);
+    const char msg[] = "kmerhip: fatal signal, backtrace:\n";
+    (void)!write(2, msg, sizeof(msg) - 1);
+    backtrace_symbols_fd(fr, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
 napi_value Init(napi_env env, napi_value exports) {
+    if (getenv("KMERHIP_SEGV_TRACE")) {
+        signal(SIGSEGV, segv_trace);
+        signal(SIGABRT, segv_trace);
+    }
     napi_property_descriptor props[] = {
         {"open", nullptr, Open, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"countFile", nullptr, CountFile, nullptr, nullptr, nullptr, napi_enumerable, nullptr},

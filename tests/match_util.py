@@ -106,7 +106,7 @@ def kat_fixtures(golden_dir):
 def kat_db(query, res, seed=17):
     """Templates (in db_long_results order) reproducing its first round."""
     rng = np.random.default_rng(seed)
-    keys = list(query)
+    keys = [km for km in query if set(km) <= set("ACGT")]     # (template k-mers come from genomes)
     by_extra = {}
     for km in keys:
         by_extra.setdefault(query[km] - 1, []).append(km)

@@ -14,8 +14,10 @@ pytestmark = pytest.mark.skipif(NODE is None, reason="node not installed")
 
 
 def _run(mode, timeout):
-    p = subprocess.run([NODE, RUNNER, mode], capture_output=True, text=True, timeout=timeout)
-    assert p.returncode == 0, p.stderr
+    # (KMERHIP_SEGV_TRACE: the addon prints a backtrace on a fatal signal)
+    p = subprocess.run([NODE, RUNNER, mode], capture_output=True, text=True, timeout=timeout,
+                       env=dict(os.environ, KMERHIP_SEGV_TRACE="1"))
+    assert p.returncode == 0, (p.returncode, p.stderr[-4000:])
     res = json.loads(p.stdout.strip().splitlines()[-1])
     bad = [r for r in res if not r["ok"]]
     assert res and not bad, bad[:5]
