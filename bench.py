@@ -483,7 +483,7 @@ def main():
             kern_name = {"lines": "nl_count_kernel + nl_write_kernel + seq_lines_kernel",
                          "hist1": "tab_hist1_kernel (+ scan)", "scatter1": "tab_scatter1_kernel",
                          "hist2": "tab_hist2_kernel (+ scan)", "scatter2": "tab_scatter2_kernel",
-                         "final": "tab_final_kernel"}[kern_name]
+                         "final": "tab_sort_final_kernel (+ tab_final_kernel on its leftover units)"}[kern_name]
         elif args.k > 64 or (args.flags & 2 and args.k > 32):
             # general path (k > 64): line arrays + one thread per window, every
             # hit a record merged on the host -- the feed kernels together

@@ -1608,6 +1608,7 @@ kmer_status feed_host(kmer_ctx *c, const uint8_t *bytes, uint64_t len, bool repo
         pos = end;
         if (report && c->p.progress) c->p.progress(c->p.progress_user, pos, len);
     }
+    if (report && len == 0 && c->p.progress) c->p.progress(c->p.progress_user, 0, 0);
     return KMER_OK;
 }
 
@@ -2072,6 +2073,11 @@ kmer_status group_count(kmer_ctx *g, GroupSrc &src, kmer_result **out) {
             src.progress(&d, &t);
             g->p.progress(g->p.progress_user, d, t);
         }
+    }
+    if (nb == 0 && g->p.progress) {                   // (an empty input: one event)
+        uint64_t d = 0, t = 0;
+        src.progress(&d, &t);
+        g->p.progress(g->p.progress_user, d, t);
     }
     for (auto &w : wk) {
         {
@@ -2596,6 +2602,11 @@ kmer_status count_file_once(kmer_ctx *c, const char *path, kmer_result **out) {
     if (st) {
         c->open_stream = false;
         return st;
+    }
+    if (c->p.progress && src.consumed == 0) {        // (an empty file: one event, as progress-stream's end)
+        uint64_t d = 0, t = 0;
+        src.progress(&d, &t);
+        c->p.progress(c->p.progress_user, d, t);
     }
     return finish(c, out);
 }

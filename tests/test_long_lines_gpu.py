@@ -28,17 +28,22 @@ def data():
 @pytest.mark.parametrize("k,prefix,step", [(21, b"ATGAC", 1), (21, b"AT", 1), (21, b"", 1), (21, b"ANG", 1),
                                            (21, b"ACG", 2)])
 def test_long_contig_matches_oracle(data, k, prefix, step, tmp_path):
+    import numpy as np
     from kmerjs_amd import _native
     from oracle import oracle
-    want = oracle.count_buffer(data, prefix, k, step)
     c = _native.Counter(k=k, prefix=prefix, step=step)
-    got = c.count_buffer(data).entries()                 # retried in long-line mode
-    assert len(got) == len(want)
-    assert first_diff(got, want) is None
     p = tmp_path / "contig.fastq"
     p.write_bytes(data)
-    got2 = c.count_file(str(p)).entries()
-    assert first_diff(got2, want) is None
+    if step == 1:                                        # ordered keys + counts as arrays (Map order)
+        keys, cnt = oracle.count_arrays(data, prefix, k)
+        for r in (c.count_buffer(data), c.count_file(str(p))):   # (retried in long-line mode)
+            assert r.keybuf == keys.tobytes() and np.array_equal(r.counts, cnt)
+    else:
+        want = oracle.count_buffer(data, prefix, k, step)
+        got = c.count_buffer(data).entries()
+        assert len(got) == len(want)
+        assert first_diff(got, want) is None
+        assert first_diff(c.count_file(str(p)).entries(), want) is None
     c.close()
 
 

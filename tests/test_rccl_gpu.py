@@ -47,14 +47,18 @@ def test_rccl_world1_exchange_collect_and_table():
         assert got == want
         # table mode: key exchange by hash-space slice + stats all-reduce
         one = _native.Counter(k=31, prefix=b"", flags=_native.FLAG_UNORDERED)
-        one.count_buffer(host)
+        one.reset()
+        one.feed_device(buf.data_ptr(), buf.numel())
+        one.finish(want_result=False)
         want_stats = one.table_stats()
+        want_digest = one.table_digest()
         one.close()
         tab = _native.Counter(k=31, prefix=b"", flags=_native.FLAG_UNORDERED)
         tab.reset()
         tab.feed_device(buf.data_ptr(), buf.numel())
         multi.finish_table_exchange(tab)
         assert multi.table_stats_all(tab) == want_stats
+        assert tab.table_digest() == want_digest
         tab.close()
     finally:
         dist.destroy_process_group()

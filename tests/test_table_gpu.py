@@ -101,15 +101,24 @@ def test_table_chunked_feeds_match_one_feed(native):
     buf = _device_input(60_000, seed=9)
     n = buf.numel()
     ctr = native.Counter(k=31, prefix=b"", flags=native.FLAG_UNORDERED)
-    one = ctr.count_buffer(buf.cpu().numpy().tobytes())
-    d1 = ctr.table_digest()
+    ctr.reset()
+    ctr.feed_device(buf.data_ptr(), n)
+    ctr.finish(want_result=False)
+    d1, s1 = ctr.table_digest(), ctr.table_stats()
     ctr.reset()
     cuts = [0, 317 * 7, 317 * 20_000, 317 * 20_001, 317 * 45_000, n]
     for lo, hi in zip(cuts, cuts[1:]):
         ctr.feed_device(buf.data_ptr() + lo, hi - lo)
     torch.cuda.synchronize()
+    ctr.finish(want_result=False)
+    assert ctr.table_digest() == d1 and ctr.table_stats() == s1
+    # (entry by entry at a smaller size)
+    small = buf[:317 * 8000].cpu().numpy().tobytes()
+    one = ctr.count_buffer(small)
+    ctr.reset()
+    for lo, hi in ((0, 317 * 3), (317 * 3, 317 * 5000), (317 * 5000, len(small))):
+        ctr.feed_device(buf.data_ptr() + lo, hi - lo)
     many = ctr.finish()
-    assert ctr.table_digest() == d1
     ctr.close()
     assert many.keybuf == one.keybuf and np.array_equal(many.counts, one.counts)
 
@@ -192,7 +201,7 @@ def test_canonical_mode_vs_oracle(native, golden, inputs, k, prefix):
     # {x, rc x} class, counted once per forward window
     from oracle import oracle
     rng = np.random.default_rng(k)
-    arr = np.frombuffer(bytearray(oracle.synth_fastq(6, 0, 20000)), dtype=np.uint8).reshape(-1, 317).copy()
+    arr = np.frombuffer(bytearray(oracle.synth_fastq(6, 0, 6000)), dtype=np.uint8).reshape(-1, 317).copy()
     seq = arr[:, 13:163]
     seq[rng.random(seq.shape) < 0.002] = ord("N")
     arr[:, 13:163] = seq
@@ -276,7 +285,7 @@ def test_table_group_through_the_c_abi(native, inputs, devs, tmp_path):
     import gzip
     from oracle import oracle
     rng = np.random.default_rng(len(devs))
-    arr = np.frombuffer(bytearray(oracle.synth_fastq(12, 0, 20000)), dtype=np.uint8).reshape(-1, 317).copy()
+    arr = np.frombuffer(bytearray(oracle.synth_fastq(12, 0, 6000)), dtype=np.uint8).reshape(-1, 317).copy()
     seq = arr[:, 13:163]
     seq[rng.random(seq.shape) < 0.001] = ord("N")
     arr[:, 13:163] = seq

@@ -1,0 +1,43 @@
+"""Per-kernel duration statistics of the TIMED steps of a bench.py run under
+`rocprofv3 --kernel-trace` (profiles/ evidence).
+
+bench.py runs W warmup steps, then K timed steps; with its side legs switched
+off (--no-pcie --no-e2e --no-pipelined --no-match --no-cpu-baseline) every
+kernel is dispatched the same number of times per step, so the timed steps are
+the last K x (dispatches / (W + K)) dispatches of each kernel.  Kernels whose
+dispatch count is not a multiple of W + K are reported over all dispatches and
+flagged.
+
+usage: python tools/kernel_stats.py TRACE_DIR WARMUP STEPS [out.csv]
+"""
+import csv
+import glob
+import re
+import statistics
+import sys
+from collections import defaultdict
+
+root, W, K = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+out = sys.argv[4] if len(sys.argv) > 4 else None
+rows = []
+for path in glob.glob(root + "/**/*kernel_trace.csv", recursive=True):
+    rows += list(csv.DictReader(open(path)))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+by = defaultdict(list)
+for r in rows:
+    m = re.findall(r"kmerhip::(\w+)", r["Kernel_Name"])
+    name = m[0] if m else r["Kernel_Name"].split("(")[0][:60]
+    by[name].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)   # us
+res = []
+for name, d in by.items():
+    n = len(d)
+    exact = n % (W + K) == 0
+    take = d[-(n // (W + K)) * K:] if exact and n >= W + K else d
+    res.append({"kernel": name, "dispatches_total": n, "dispatches_timed": len(take),
+                "timed_window_exact": exact, "avg_us": statistics.mean(take), "min_us": min(take),
+                "max_us": max(take), "stdev_us": statistics.pstdev(take), "sum_us": sum(take)})
+res.sort(key=lambda x: -x["sum_us"])
+w = csv.DictWriter(open(out, "w") if out else sys.stdout, fieldnames=list(res[0].keys()))
+w.writeheader()
+for x in res:
+    w.writerow({k: (round(v, 2) if isinstance(v, float) else v) for k, v in x.items()})
