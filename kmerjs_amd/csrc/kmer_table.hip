@@ -262,19 +262,26 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter1_kernel(TabArgs a) {
         __syncthreads();
         uint32_t total;
         const uint32_t cnt = bcnt[t];
-        bst[t] = block_excl_1024(cnt, ws, &total);
+        const uint32_t my_st = block_excl_1024(cnt, ws, &total);
+        bst[t] = my_st;
+        cur[t] -= my_st;                          // (write-out: B1[cur[p] + i], one LDS read per key)
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < TAB_RPL; ++j)
             if (v & (1u << j)) srt[bst[key[j] >> (64 - TAB_L1)] + rank[j]] = key[j];
         __syncthreads();
+#ifndef TAB_EXP_S1_NOSTORE                         // (experiment builds only)
         for (uint32_t i = t; i < total; i += TAB_WG1) {
             const uint64_t h = srt[i];
-            const uint32_t p = (uint32_t)(h >> (64 - TAB_L1));
-            a.B1[cur[p] + (i - bst[p])] = h;
+#ifdef TAB_EXP_NT
+            __builtin_nontemporal_store(h, &a.B1[cur[(uint32_t)(h >> (64 - TAB_L1))] + i]);
+#else
+            a.B1[cur[(uint32_t)(h >> (64 - TAB_L1))] + i] = h;
+#endif
         }
+#endif
         __syncthreads();
-        cur[t] += cnt;
+        cur[t] += my_st + cnt;
         bcnt[t] = 0;
         if (!__syncthreads_or(c.m < c.end)) break;
     }
@@ -344,6 +351,10 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2_kernel(const uint64_t *B
     const uint32_t t = threadIdx.x;
     const TabUnit un = units[blockIdx.x];
     const uint64_t *src = B1 + un.start;
+#ifdef TAB_EXP_S2_COPY                            // (experiment builds only: a plain streaming copy)
+    for (uint32_t i = t; i < un.len; i += TAB_WG1) B2[un.start + i] = src[i];
+    return;
+#endif
     cur[t] = H2s[un.hbase + (uint64_t)t * un.nunits + un.u];
     bcnt[t] = 0;
     __syncthreads();
@@ -365,7 +376,9 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2_kernel(const uint64_t *B
         __syncthreads();
         uint32_t total;
         const uint32_t cnt = bcnt[t];
-        bst[t] = block_excl_1024(cnt, ws, &total);
+        const uint32_t my_st = block_excl_1024(cnt, ws, &total);
+        bst[t] = my_st;
+        cur[t] -= my_st;                          // (write-out: B2[cur[b] + i], one LDS read per key)
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < TAB_RPL; ++j) {
@@ -378,13 +391,18 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2_kernel(const uint64_t *B
             const uint32_t i = r0 + TAB_ROUND + j * TAB_WG1 + t;
             key[j] = i < un.len ? src[i] : 0;
         }
+#ifndef TAB_EXP_S2_NOSTORE                         // (experiment builds only: -DTAB_EXP_S2_NOSTORE)
         for (uint32_t i = t; i < total; i += TAB_WG1) {
             const uint64_t h = srt[i];
-            const uint32_t b = (uint32_t)(h >> TAB_RBITS) & (TAB_NB - 1);
-            B2[cur[b] + (i - bst[b])] = h;
+#ifdef TAB_EXP_NT
+            __builtin_nontemporal_store(h, &B2[cur[(uint32_t)(h >> TAB_RBITS) & (TAB_NB - 1)] + i]);
+#else
+            B2[cur[(uint32_t)(h >> TAB_RBITS) & (TAB_NB - 1)] + i] = h;
+#endif
         }
+#endif
         __syncthreads();
-        cur[t] += cnt;
+        cur[t] += my_st + cnt;
         bcnt[t] = 0;
         __syncthreads();
     }
@@ -1122,6 +1140,18 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                         if (eq && b0 + m < (pk[j] & 0x3FFFu)) cf[u] &= 0xFFu;    // an earlier copy
                     }
                 }
+                // one bucket: the group's output slots from ONE counter bump per wave
+                uint32_t gbase = 0;
+                if (ONE) {
+                    uint32_t tot = 0;
+#pragma unroll
+                    for (int u = 0; u < G; ++u) tot += (uint32_t)__popcll(__ballot((cf[u] >> 8) != 0u));
+                    if (tot) {
+                        if (lane == 0) gbase = atomicAdd(&nout[0], tot);
+                        gbase = (uint32_t)__builtin_amdgcn_readlane((int)gbase, 0);
+                    }
+                }
+                const unsigned long long below = (1ull << lane) - 1ull;
 #pragma unroll
                 for (int u = 0; u < G; ++u) {
                     const int j = g0 + u;
@@ -1133,13 +1163,8 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                     unsigned long long fm = __ballot(first);
                     uint32_t pos = 0, ql = 0;
                     if (ONE) {
-                        if (fm) {
-                            const int ld = __ffsll((long long)fm) - 1;
-                            uint32_t base = 0;
-                            if (lane == (uint32_t)ld) base = atomicAdd(&nout[0], (uint32_t)__popcll(fm));
-                            base = (uint32_t)__shfl((int)base, ld);
-                            pos = base + (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
-                        }
+                        pos = gbase + (uint32_t)__popcll(fm & below);
+                        gbase += (uint32_t)__popcll(fm);
                     } else {
                         ql = (uint32_t)(xj >> TAB_RBITS);
                         while (fm) {

@@ -31,8 +31,11 @@ for r in rows:
 res = []
 for name, d in by.items():
     n = len(d)
+    # (bench.py may dispatch a kernel once more before its warmup: e.g. a
+    # verification count; the timed steps are still the LAST ones)
+    per = n // (W + K)
     exact = n % (W + K) == 0
-    take = d[-(n // (W + K)) * K:] if exact and n >= W + K else d
+    take = d[-per * K:] if per else d
     res.append({"kernel": name, "dispatches_total": n, "dispatches_timed": len(take),
                 "timed_window_exact": exact, "avg_us": statistics.mean(take), "min_us": min(take),
                 "max_us": max(take), "stdev_us": statistics.pstdev(take), "sum_us": sum(take)})
