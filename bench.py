@@ -230,9 +230,12 @@ def main():
     ap.add_argument("--collect", action="store_true",
                     help="N > 1: the timed step also gathers every rank's ordered key range to rank 0 and merges "
                          "them on the device into ONE result in Map order (kmer_merge_ordered)")
-    ap.add_argument("--merge", default="hits", choices=("hits", "alltoall", "gather"),
+    ap.add_argument("--merge", default=None, choices=("hits", "alltoall", "gather", "dense"),
                     help="N > 1: hits: key-range all-to-all of the hits + per-rank finish (result distributed by "
-                         "key range); alltoall: the same with per-rank partials; gather: all partials to rank 0")
+                         "key range); alltoall: the same with per-rank partials; dense: per-rank partials as dense "
+                         "count / first-occurrence arrays, one reduce-scatter each (SURVEY §8e; short keys); "
+                         "gather: all partials to rank 0.  Default: dense for c4 (bytes independent of the input "
+                         "size), hits otherwise")
     args = ap.parse_args()
     # per-config defaults (explicit flags still win)
     argv = " ".join(sys.argv)
@@ -268,6 +271,8 @@ def main():
             args.flags |= FLAG_CANONICAL
     if args.config != "c2":
         args.no_pcie = True
+    if args.merge is None:
+        args.merge = "dense" if args.config == "c4" and 2 * (args.k - len(args.prefix)) <= 26 else "hits"
     from kmerjs_amd._native import FLAG_CANONICAL as _FC
     table = bool(args.flags & (FLAG_UNORDERED | _FC))
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
@@ -282,8 +287,8 @@ def main():
     import torch
     import torch.distributed as dist
     from kmerjs_amd import Counter
-    from kmerjs_amd.multi import (collect_ordered_device, device_u64, finish_distributed, finish_exchange,
-                                  finish_table_exchange, merge_to)
+    from kmerjs_amd.multi import (collect_ordered_device, device_u64, finish_dense, finish_distributed,
+                                  finish_exchange, finish_table_exchange, merge_to)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -365,6 +370,8 @@ def main():
             finish_exchange(c, args.k, len(prefix), total_lines)
         elif args.merge == "alltoall":
             finish_distributed(c, args.k, len(prefix), total_lines)
+        elif args.merge == "dense":
+            finish_dense(c, args.k, len(prefix), total_lines)
         else:
             merge_to(c, args.k, len(prefix), total_lines, dst=0, want_result=False)
         if collect and args.merge != "gather":
@@ -534,7 +541,8 @@ def main():
                        "parallelism": "dp%d (reads sharded; %s%s)" % (
                            world, "RCCL all-to-all of pass-1 keys by hash-space slice, per-rank table finish"
                            if table else {"hits": "RCCL all-to-all of hits by key range, per-rank finish",
-                        "alltoall": "RCCL all-to-all of partials by key range, per-rank finish"}.get(
+                        "alltoall": "RCCL all-to-all of partials by key range, per-rank finish",
+                        "dense": "RCCL reduce-scatter of dense count / first-occurrence arrays, per-rank finish"}.get(
                             args.merge, "RCCL gather of partials, finish on rank 0"),
                            "; + alltoallv gather of the ordered ranges to rank 0 and device merge into one "
                            "Map-order result" if args.collect and world > 1 else "")},

@@ -22,6 +22,10 @@ first-occurrence order).  Two ways to finish:
   (unique keys + {first, count}, kmer_partial_device) merged with
   kmer_finish_merged -- fewer bytes on the wire when keys repeat a lot within
   a shard (high coverage), one more reduce per rank.
+* finish_dense (short keys, 2(k - |P|) <= 26 bits): SURVEY §8(e)'s dense
+  merge -- per-rank partials scattered into dense count / first-occurrence
+  arrays over the key space, one reduce-scatter each (sum, min): constant
+  bytes on the wire whatever the input size (C4).
 * merge_to: gather every partial to one rank and finish there (one ordered
   result on one GPU; the gather and the merge grow with the rank count).
 
@@ -305,6 +309,65 @@ def finish_distributed(ctr, k, plen, total_lines, group=None, want_result=False,
     # the merged finish runs on the context's own stream and may still read the
     # received buffers after returning: keep them alive until the next finish
     ctr._keepalive = (rk, rv)
+    return ctr.finish_merged(rk.data_ptr(), rv.data_ptr(), rk.numel(), total_lines, want_result=want_result)
+
+
+INT64_MAX = (1 << 63) - 1
+
+
+def dense_reduce(keys, vals, kbits, group=None):
+    """SURVEY.md §8(e)'s dense merge, for short packed keys (2(k - |P|) <= 26
+    bits: C2 / C4 have 22): this rank's partial entries (unique packed keys,
+    {first, count}) are scattered into dense arrays over the whole key space
+    -- counts and first-occurrence keys -- and ONE reduce-scatter each (sum,
+    min) leaves every rank its equal slice of the key space, summed over the
+    ranks.  Bytes on the wire are 16 B x 2^kbits whatever the input size
+    (C4: 67 MB per rank against 16 B per hit = 527 MB for the hit exchange).
+    Returns this rank's entries (keys int64[m], vals int64[m, 2] {first,
+    count}) in first-occurrence order."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = keys.device
+    n_slots = 1 << kbits
+    per = -(-n_slots // world)
+    cnt = torch.zeros(per * world, dtype=torch.int64, device=dev)
+    fst = torch.full((per * world,), INT64_MAX, dtype=torch.int64, device=dev)
+    ok = keys < n_slots                                  # (the reduce's invalid-key sentinel)
+    kk = keys[ok]
+    cnt[kk] = vals[ok, 1]
+    fst[kk] = vals[ok, 0]
+    if dist.get_backend(group) == "gloo":                # (CPU tests: gloo has no reduce_scatter)
+        cnt, fst = cnt.cpu(), fst.cpu()
+        dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
+        dist.all_reduce(fst, op=dist.ReduceOp.MIN, group=group)
+        out_c = cnt[rank * per:(rank + 1) * per].to(dev)
+        out_f = fst[rank * per:(rank + 1) * per].to(dev)
+    else:
+        out_c = torch.empty(per, dtype=torch.int64, device=dev)
+        out_f = torch.empty(per, dtype=torch.int64, device=dev)
+        dist.reduce_scatter_tensor(out_c, cnt, op=dist.ReduceOp.SUM, group=group)
+        dist.reduce_scatter_tensor(out_f, fst, op=dist.ReduceOp.MIN, group=group)
+    idx = torch.nonzero(out_c > 0).flatten()
+    f = out_f[idx]
+    o = torch.argsort(f)
+    return idx[o] + rank * per, torch.stack([f[o], out_c[idx][o]], dim=1).contiguous()
+
+
+def finish_dense(ctr, k, plen, total_lines, group=None, want_result=False, records=True, dst=0):
+    """Finish a sharded count with the dense reduce (dense_reduce): afterwards
+    every rank holds its key range of the result, ordered by first occurrence
+    (device, kmer_result_device), as after finish_exchange.  Record keys are
+    merged on rank `dst`."""
+    d_k, d_v, n = ctr.partial_device()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    keys = device_u64(d_k, n, dev) if n else torch.empty(0, dtype=torch.int64, device=dev)
+    vals = device_u64(d_v, 2 * n, dev).view(n, 2) if n else torch.empty((0, 2), dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()                     # (the partial is on the context's stream)
+    rk, rv = dense_reduce(keys, vals, 2 * (k - plen), group=group)
+    if records:
+        gather_records(ctr, dst=dst, group=group)
+    torch.cuda.synchronize()
+    ctr._keepalive = (rk, rv)                    # (see finish_distributed)
     return ctr.finish_merged(rk.data_ptr(), rv.data_ptr(), rk.numel(), total_lines, want_result=want_result)
 
 

@@ -160,6 +160,61 @@ def test_shuffle_partials_by_key_range_gloo(world):
     assert sorted(got) == sent                                 # nothing lost, nothing duplicated
 
 
+def _dense_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        kbits = 12
+        g = torch.Generator().manual_seed(10 + rank)
+        n = 700 + 91 * rank
+        keys = torch.unique(torch.randint(0, 1 << kbits, (n,), generator=g, dtype=torch.int64))
+        keys = keys[torch.randperm(keys.numel(), generator=g)]
+        keys = torch.cat([keys, torch.tensor([1 << kbits])])            # + the reduce's invalid sentinel
+        first = torch.arange(keys.numel(), dtype=torch.int64) + (rank << 40)
+        vals = torch.stack([first, torch.randint(1, 9, (keys.numel(),), generator=g)], dim=1)
+        rk, rv = multi.dense_reduce(keys, vals, kbits)
+        q.put(("ok", rank, keys.tolist(), vals.tolist(), rk.tolist(), rv.tolist()))
+    except Exception as e:  # pragma: no cover
+        q.put(("err", rank, repr(e), None, None, None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dense_reduce_gloo(world):
+    """finish_dense's collective (SURVEY §8e dense merge): per key, counts add
+    and the first occurrence is the minimum over the ranks; every key lands on
+    exactly one rank (its slice of the key space), in first-occurrence order."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dense_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[0] == "ok" for r in res), res
+    want = {}
+    for r in res:
+        for key, (f, c) in zip(r[2], r[3]):
+            if key < 1 << 12:
+                pf, pc = want.get(key, (None, 0))
+                want[key] = (f if pf is None else min(pf, f), pc + c)
+    got = {}
+    per = -(-(1 << 12) // world)
+    for r in sorted(res, key=lambda x: x[1]):
+        rank, rk, rv = r[1], r[4], r[5]
+        assert all(rank * per <= key < (rank + 1) * per for key in rk)
+        assert [v[0] for v in rv] == sorted(v[0] for v in rv)
+        for key, (f, c) in zip(rk, rv):
+            assert key not in got
+            got[key] = (f, c)
+    assert got == want
+
+
 def test_key_owner_balanced_and_monotone():
     keys = torch.arange(0, 1 << 22, 97, dtype=torch.int64)
     for world in (1, 2, 3, 8):

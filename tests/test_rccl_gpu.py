@@ -45,6 +45,15 @@ def test_rccl_world1_exchange_collect_and_table():
         got = multi.collect_ordered(ctr, 16, 4 * n)
         ctr.close()
         assert got == want
+        # ordered: dense reduce-scatter merge + device collect
+        ctr = _native.Counter(k=16, prefix=b"ATGAC")
+        ctr.reset()
+        ctr.set_position(0, 0)
+        ctr.feed_device(buf.data_ptr(), buf.numel())
+        multi.finish_dense(ctr, 16, 5, 4 * n)
+        got = multi.collect_ordered(ctr, 16, 4 * n)
+        ctr.close()
+        assert got == want
         # table mode: key exchange by hash-space slice + stats all-reduce
         one = _native.Counter(k=31, prefix=b"", flags=_native.FLAG_UNORDERED)
         one.reset()
