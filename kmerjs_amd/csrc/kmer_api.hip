@@ -1849,7 +1849,7 @@ struct FileBatches : GroupSrc {
             std::unique_ptr<uint8_t[]> own;
             if (carry.size() <= HEAD) {
                 start = S.buf.get() + HEAD - carry.size();
-                memcpy(start, carry.data(), carry.size());
+                if (!carry.empty()) memcpy(start, carry.data(), carry.size());
                 have = carry.size() + S.len;
             } else {                                      // a line longer than the headroom
                 own.reset(new (std::nothrow) uint8_t[carry.size() + S.len]);
