@@ -176,9 +176,10 @@ def make_workload(args, rank, world, dev):
     raise SystemExit("unknown config " + args.config)
 
 
-def load_traffic(args, kernel):
-    """HBM bytes per launch of `kernel` in this config, from the committed PMC
-    passes (profiles/pmc_traffic.json, keyed by config name and kernel)."""
+def load_traffic(args, kern_name):
+    """HBM bytes per launch of the kernel(s) `kern_name` names ("a + b (note)":
+    the sum over a and b) in this config, from the committed PMC passes
+    (profiles/pmc_traffic.json, keyed by config name and kernel)."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
@@ -186,10 +187,17 @@ def load_traffic(args, kernel):
         with open(path) as f:
             d = json.load(f)
         e = d.get(args.config, {})
-        if e.get("reads") not in (None, args.reads) or e.get("k") not in (None, args.k) or \
+        reads = args.reads if args.config in ("c2", "c3", "c4") else 0   # (c1/c5 inputs are not read-based)
+        if e.get("reads") not in (None, reads) or e.get("k") not in (None, args.k) or \
                 e.get("prefix") not in (None, args.prefix):
             return None
-        return e.get("kernels", {}).get(kernel, {}).get("hbm_bytes_per_launch")
+        total = 0.0
+        for kernel in kern_name.split(" (")[0].split(" + "):
+            v = e.get("kernels", {}).get(kernel.strip(), {}).get("hbm_bytes_per_launch")
+            if v is None:
+                return None
+            total += v
+        return total
     except Exception:
         return None
 
@@ -513,7 +521,7 @@ def main():
             kern_name = "scan_planes_kernel"
             algo_bytes = nbytes + 24 * (accepted / world)
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
-        traffic = load_traffic(args, kern_name.split(" ")[0])
+        traffic = load_traffic(args, kern_name)
         out = {
             "metric": "k-mers/sec + distinct-kmers/sec, k=%d 150bp synthetic FASTQ, 1/2/4/8 GPU" % args.k,
             "value": value,
