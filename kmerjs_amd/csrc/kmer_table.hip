@@ -80,7 +80,20 @@ struct TabCur {
     uint64_t m, end;               // next sequence ordinal of this wave, end of the workgroup's share
     uint64_t seg;                  // first window of the next segment in line m
     uint32_t stride;               // waves per workgroup
+    uint64_t dstart, dlen;         // lane i < 16: line m + stride * i (prefetched a round ahead)
 };
+
+// the descriptors of the wave's next 16 lines (lane i < 16: line c.m + stride * i)
+__device__ __forceinline__ void tab_fetch(const TabArgs &a, TabCur &c) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t mi = c.m + (uint64_t)c.stride * (lane & 15);
+    c.dstart = 0;
+    c.dlen = 0;
+    if (lane < 16 && mi < c.end) {
+        c.dstart = a.lines[mi].start;
+        c.dlen = a.lines[mi].len;
+    }
+}
 
 __device__ __forceinline__ void tab_record(const TabArgs &a, uint64_t pos, uint32_t strand) {
     const unsigned long long i = atomicAdd(a.rec_count, 1ull);
@@ -105,17 +118,16 @@ __device__ __forceinline__ void tab_record(const TabArgs &a, uint64_t pos, uint3
 // scatter1 84.4 -> 64.2 ms at C3).  key[OFF + m] = h of the lane's window m,
 // bit m of the result set iff it is counted; non-ACGT windows become records
 // (rec).
-template <int NS, int OFF>
+__device__ __forceinline__ uint64_t tab_brev64(uint64_t x) {
+    return ((uint64_t)__brev((uint32_t)x) << 32) | __brev((uint32_t)(x >> 32));
+}
+
+template <int NS, int OFF, bool PFX>
 __device__ __forceinline__ uint32_t tab_round(const TabArgs &a, TabCur &c, bool rec, uint64_t (&key)[TAB_RPL]) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t k = a.k;
-    // the next 16 lines of this wave (lane i < 16: line c.m + stride * i)
-    SeqLine d;
-    d.start = 0;
-    d.len = 0;
-    const uint64_t mi = c.m + (uint64_t)c.stride * (lane & 15);
-    if (lane < 16 && mi < c.end) d = a.lines[mi];
-    const uint64_t W = d.len >= k ? d.len - k + 1 : 0;            // windows of the line
+    // the next 16 lines of this wave (fetched by the previous round)
+    const uint64_t W = c.dlen >= k ? c.dlen - k + 1 : 0;          // windows of the line
     const uint64_t rem = lane == 0 ? (W > c.seg ? W - c.seg : 0) : W;
     const uint32_t need = lane < 16 ? (uint32_t)((rem + NS - 1) / NS) : 0u;   // (<= 2^32 lanes: pieces are short)
     const uint32_t cum = tab_incl_sum(need);                      // inclusive over lanes 0..15
@@ -127,8 +139,8 @@ __device__ __forceinline__ uint32_t tab_round(const TabArgs &a, TabCur &c, bool 
     const bool act = lane < tot && li < 16;
     const uint32_t lsrc = li < 16 ? li : 15u;
     const uint32_t before = (uint32_t)__shfl((int)(cum - need), (int)lsrc);
-    const uint64_t st = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)d.start, (int)lsrc)) |
-                        ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(d.start >> 32), (int)lsrc) << 32);
+    const uint64_t st = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)c.dstart, (int)lsrc)) |
+                        ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(c.dstart >> 32), (int)lsrc) << 32);
     const uint64_t Wl = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)W, (int)lsrc)) |
                         ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(W >> 32), (int)lsrc) << 32);
     const uint64_t w0 = (li == 0 ? c.seg : 0) + (uint64_t)(lane - before) * NS;
@@ -148,6 +160,8 @@ __device__ __forceinline__ uint32_t tab_round(const TabArgs &a, TabCur &c, bool 
             c.m += (uint64_t)c.stride * is;
         }
     }
+    // the next round's descriptors load while this round's bytes do
+    tab_fetch(a, c);
     // planes of the bytes [st + w0, st + w0 + NS + k - 1), from aligned dwords
     uint64_t LO = 0, HI = 0, EX = 0;
     const uint8_t *p = a.data + st + w0;
@@ -181,6 +195,25 @@ __device__ __forceinline__ uint32_t tab_round(const TabArgs &a, TabCur &c, bool 
     HI >>= off;
     EX >>= off;
     const uint32_t kmask = k >= 32 ? ~0u : ((1u << k) - 1u);
+    if (!PFX) {
+        // no prefix, and every byte the lane's windows span is A/C/G/T (the
+        // common case): every window counts, no per-window tests; rc(w) from
+        // the complemented planes reversed once per round
+        const uint32_t nv = act ? (uint32_t)(Wl - w0 < (uint64_t)NS ? Wl - w0 : (uint64_t)NS) : 0u;
+        const uint32_t nb = nv + k - 1;                            // bytes spanned (<= 47)
+        if (nv > 0 && (EX & ((1ull << nb) - 1)) == 0) {
+            const uint64_t RLO = tab_brev64(~LO), RHI = tab_brev64(~HI);
+#pragma unroll
+            for (int m = 0; m < NS; ++m) {
+                const uint32_t flo = (uint32_t)(LO >> m) & kmask, fhi = (uint32_t)(HI >> m) & kmask;
+                const uint32_t rlo = (uint32_t)(RLO >> (64 - m - k)) & kmask;
+                const uint32_t rhi = (uint32_t)(RHI >> (64 - m - k)) & kmask;
+                const uint64_t cf = ((uint64_t)fhi << k) | flo, cr = ((uint64_t)rhi << k) | rlo;
+                key[OFF + m] = tab_mix(cf < cr ? cf : cr);
+            }
+            return ((nv >= 32 ? ~0u : (1u << nv) - 1u)) << OFF;
+        }
+    }
     const uint32_t sh = 32 - k;
     uint32_t valid = 0;
 #pragma unroll
@@ -217,12 +250,14 @@ __device__ __forceinline__ TabCur tab_cursor(const TabArgs &a, uint32_t waves) {
     c.m = m0 + (threadIdx.x >> 6);
     c.seg = 0;
     c.stride = waves;
+    tab_fetch(a, c);
     return c;
 }
 
 }  // namespace
 
 // pass 1, histogram: keys per (workgroup, partition)
+template <bool PFX>
 __global__ __launch_bounds__(256) void tab_hist1_kernel(TabArgs a) {
     __shared__ uint32_t hist[TAB_NB];
     for (uint32_t i = threadIdx.x; i < TAB_NB; i += 256) hist[i] = 0;
@@ -230,7 +265,7 @@ __global__ __launch_bounds__(256) void tab_hist1_kernel(TabArgs a) {
     TabCur c = tab_cursor(a, 4);
     while (c.m < c.end) {
         uint64_t key[TAB_RPL];
-        uint32_t v = tab_round<TAB_RPL, 0>(a, c, false, key);
+        uint32_t v = tab_round<TAB_RPL, 0, PFX>(a, c, false, key);
 #pragma unroll
         for (int j = 0; j < TAB_RPL; ++j)
             if (v & (1u << j)) atomicAdd(&hist[key[j] >> (64 - TAB_L1)], 1u);
@@ -241,6 +276,7 @@ __global__ __launch_bounds__(256) void tab_hist1_kernel(TabArgs a) {
 
 // pass 1, scatter: the same keys, LDS-sorted by partition in rounds of 16 K,
 // written as one contiguous run per partition and round
+template <bool PFX>
 __global__ __launch_bounds__(TAB_WG1) void tab_scatter1_kernel(TabArgs a) {
     __shared__ uint64_t srt[TAB_ROUND];
     __shared__ uint64_t cur[TAB_NB];
@@ -255,7 +291,7 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter1_kernel(TabArgs a) {
         uint64_t key[TAB_RPL];
         uint32_t rank[TAB_RPL];
         uint32_t v = 0;
-        if (c.m < c.end) v = tab_round<TAB_RPL, 0>(a, c, true, key);
+        if (c.m < c.end) v = tab_round<TAB_RPL, 0, PFX>(a, c, true, key);
 #pragma unroll
         for (int j = 0; j < TAB_RPL; ++j)
             rank[j] = (v & (1u << j)) ? atomicAdd(&bcnt[key[j] >> (64 - TAB_L1)], 1u) : 0u;
@@ -1213,12 +1249,19 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
 // launchers
 // ---------------------------------------------------------------------------
 hipError_t launch_tab_hist1(const TabArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(tab_hist1_kernel, dim3(a.nwg), dim3(256), 0, s, a);
+    // (no prefix: the windows' fast path, kmer_table.hip tab_round)
+    if (a.pmask == 0)
+        hipLaunchKernelGGL(tab_hist1_kernel<false>, dim3(a.nwg), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(tab_hist1_kernel<true>, dim3(a.nwg), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_tab_scatter1(const TabArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(tab_scatter1_kernel, dim3(a.nwg), dim3(TAB_WG1), 0, s, a);
+    if (a.pmask == 0)
+        hipLaunchKernelGGL(tab_scatter1_kernel<false>, dim3(a.nwg), dim3(TAB_WG1), 0, s, a);
+    else
+        hipLaunchKernelGGL(tab_scatter1_kernel<true>, dim3(a.nwg), dim3(TAB_WG1), 0, s, a);
     return hipGetLastError();
 }
 
