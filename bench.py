@@ -499,18 +499,22 @@ def main():
                          "hist1": "tab_hist1_kernel (+ scan)", "scatter1": "tab_scatter1_kernel",
                          "hist2": "tab_hist2_kernel (+ scan)", "scatter2": "tab_scatter2_kernel",
                          "final": "tab_sort_final_kernel (+ tab_final_kernel on its leftover units)"}[kern_name]
-        elif args.k > 64 or (args.flags & 2 and args.k > 32):
+        elif args.k > 64 or (not args.prefix and args.k > 31):
             # general path (k > 64): line arrays + one thread per window, every
             # hit a record merged on the host -- the feed kernels together
             kern_name = "lines + windows_kernel (general path; host record merge dominates the step)"
             kern_ms = sum(feed_ms_l) / len(feed_ms_l)
             algo_bytes = nbytes + 40 * (accepted / world)
-        elif args.k > 32 or args.flags & 2:
-            # tile path with records (k in 33..64, or records forced): the plane scan
-            # for A/C/G/T prefixes (else the byte-SWAR scan), hits become records
-            kern_name = ("scan_planes_kernel" if args.prefix and set(args.prefix) <= set("ACGT") else
+        elif args.flags & 2 or not set(args.prefix) <= set("ACGT"):
+            # tile path with records (records forced, or a non-ACGT prefix): the
+            # plane scan for A/C/G/T prefixes (else the byte-SWAR scan)
+            kern_name = ("scan_planes_kernel" if set(args.prefix) <= set("ACGT") else
                          "scan_tile_kernel") + " (tile records path; host record merge dominates the step)"
             algo_bytes = nbytes + 24 * (accepted / world)
+        elif args.k > 32:
+            # packed path with 128-bit window codes (k in 33..64, ACGT prefix)
+            kern_name = "scan_planes_kernel (k > 32: 128-bit window codes)"
+            algo_bytes = nbytes + 32 * (accepted / world)
         elif (args.prefix and len(args.prefix) <= 3) or not args.prefix:
             # dense-hit path: the timed kernels are the two streaming newline passes
             kern_name = "nl_count_kernel + nl_write_kernel (dense-hit path)"

@@ -102,8 +102,9 @@ typedef struct {
      * canonical mode: every device's pass-1 keys go to the device that owns
      * their slice of the hash space, which builds that slice of the table;
      * kmer_table_stats / kmer_table_digest of a group add up its devices'.
-     * Configurations without packed keys or a table (non-ACGT prefix, step >
-     * 1, k > 32) run on devices[0] alone.  The other device-resident entry
+     * Configurations without packed partials or a table (non-ACGT prefix,
+     * step > 1, k > 64, keys of 64 bits or more: k - |P| >= 32) run on
+     * devices[0] alone.  The other device-resident entry
      * points are single-device only (KMER_E_STATE on a group).  0 or 1 =
      * single device `device`. */
     uint32_t ndev;
@@ -153,7 +154,9 @@ kmer_status kmer_sync(kmer_ctx *ctx);
 /* Multi-GPU merge.  kmer_partial_device reduces this context's session to its
  * unique packed keys: keys = uint64[n] 2-bit suffix codes (the k-|P| bases
  * after the prefix, first base most significant), vals = n x {uint64 first,
- * uint64 count} (first-occurrence order, count).  Device pointers, valid until
+ * uint64 count} (first-occurrence order, count).  Keys of 64 bits or more
+ * (k - |P| >= 32, counted on the packed path as two words) have no partial:
+ * KMER_E_STATE here and in the hit exchange below.  Device pointers, valid until
  * the next call on the context.  Concatenate the partials of every rank on one
  * device (e.g. RCCL gather over xGMI) and hand them to kmer_finish_merged,
  * which reduces again (min first, sum count), orders by first occurrence and

@@ -112,6 +112,7 @@ struct kmer_ctx {
     hipEvent_t evq = nullptr;      // orders sstream after stream
     std::string err;
     uint32_t kbits = 0;            // packed key bits = 2*(k - |P|)
+    bool wide = false;             // packed keys of >= 64 bits (k <= 64): two words, the high one in rkeyh
 
     // per tile
     uint64_t tile_cap = 0;
@@ -121,11 +122,14 @@ struct kmer_ctx {
     DBuf<uint64_t> tbase, nlpos;   // ... exclusive scan, chunk-relative '\n' positions
     uint64_t host_lines = 0;       // StreamPos.lines as last seen by the host (dense-hit path)
     DBuf<HitRec> hits, ovf;
+    DBuf<uint64_t> hits_hi, ovf_hi;   // k > 32: the first k - 32 bases of each hit record's window
     DBuf<unsigned long long> lb_cnt, lb_lnl;   // general path look-back
     DBuf<uint64_t> tp_cnt, tp_lnl;             // general path, two-pass debug mode
     // session packed hits, by rank (first-occurrence order of all hits)
     uint64_t n_hits = 0, n_cross = 0;
     DBuf<uint64_t> rkey, rkey2, rord, rcnt;
+    DBuf<uint64_t> rkeyh, whA, whB;    // wide keys: high words by rank; sort scratch
+    DBuf<uint32_t> ridx3;
     DBuf<uint32_t> rkey32, rkey32b;   // narrow keys: 2(k-|P|) + 1 <= 32 bits
     bool narrow = false;
     bool planes = false;           // ACGT prefix: bit-plane scan kernel
@@ -144,6 +148,7 @@ struct kmer_ctx {
     bool out_pending = false;      // unique count of the last finish not yet read back (h_tail[8])
     bool timing_pending = false;   // finish events not yet read
     DBuf<uint64_t> xord, xord2, xkey, xkey2;   // cross list
+    DBuf<uint64_t> xkeyl, xkeyh;               // ... wide keys (xkey then holds the entry's index)
     DBuf<uint32_t> xslot;
     // finish outputs
     DBuf<uint64_t> ukey, first, cnt_out, roff;
@@ -305,8 +310,16 @@ kmer_status ensure_tiles(kmer_ctx *c, uint64_t n_tiles) {
         HIPCHK(c, c->bsum.ensure(cap / TSCAN_BLOCK + 2, s));
         HIPCHK(c, c->bscan.ensure(cap / TSCAN_BLOCK + 2, s));
         HIPCHK(c, c->hits.ensure(cap * HMAX, s));
+        if (c->p.k > 32) HIPCHK(c, c->hits_hi.ensure(cap * HMAX, s));
     }
     c->tile_cap = cap;
+    return KMER_OK;
+}
+
+// the overflow hit list (and, k > 32, its high code words)
+kmer_status ensure_ovf(kmer_ctx *c, uint64_t n, hipStream_t s) {
+    HIPCHK(c, c->ovf.ensure(n, s));
+    if (c->p.k > 32) HIPCHK(c, c->ovf_hi.ensure(c->ovf.cap, s));
     return KMER_OK;
 }
 
@@ -419,6 +432,7 @@ kmer_status ensure_rank_arrays(kmer_ctx *c, uint64_t need, uint64_t keep, hipStr
     if (need >= (1ull << 32)) return fail(c, KMER_E_TOO_MANY_KEYS, "more than 2^32 prefix hits in one session");
     if (c->narrow) HIPCHK(c, c->rkey32.ensure(need, s, true, keep));
     else HIPCHK(c, c->rkey.ensure(need, s, true, keep));
+    if (c->wide) HIPCHK(c, c->rkeyh.ensure(need, s, true, keep));
     HIPCHK(c, c->rord.ensure(need, s, true, keep));
     HIPCHK(c, c->ridx.ensure(need, s, true, keep));
     return KMER_OK;
@@ -428,6 +442,10 @@ kmer_status ensure_cross(kmer_ctx *c, uint64_t need, hipStream_t s) {
     HIPCHK(c, c->xord.ensure(need, s, true, c->n_cross));
     HIPCHK(c, c->xkey.ensure(need, s, true, c->n_cross));
     HIPCHK(c, c->xslot.ensure(need, s, true, c->n_cross));
+    if (c->wide) {
+        HIPCHK(c, c->xkeyl.ensure(need, s, true, c->n_cross));
+        HIPCHK(c, c->xkeyh.ensure(need, s, true, c->n_cross));
+    }
     return KMER_OK;
 }
 
@@ -440,6 +458,9 @@ void bind_hits(kmer_ctx *c, HitArgs &h) {
     h.xord = c->xord.p;
     h.xkey = c->xkey.p;
     h.xslot = c->xslot.p;
+    h.rkeyh = c->rkeyh.p;
+    h.xkeyl = c->xkeyl.p;
+    h.xkeyh = c->xkeyh.p;
     h.xbase = c->n_cross;
     h.xcap = c->xord.cap;
 }
@@ -504,6 +525,8 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
     a.ovf_cap = c->ovf.cap;
     a.err = c->d_err;
     a.ablate = (c->p.flags >> 8) & 0xFFu;   // KMER_FLAG_ABLATE_* (experiments only)
+    a.hits_hi = c->hits_hi.p;
+    a.ovf_hi = c->ovf_hi.p;
 
     HitArgs &h = p.h;
     memset(&h, 0, sizeof(h));
@@ -522,6 +545,13 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
     h.pbits = c->pbits;
     h.smask = (c->kbits >= 64) ? ~0ull : ((1ull << c->kbits) - 1ull);
     h.invalid_key = c->kbits >= 63 ? ~0ull : (1ull << c->kbits);
+    h.hits_hi = c->hits_hi.p;
+    h.ovf_hi = c->ovf_hi.p;
+    h.wide = c->wide ? 1u : 0u;
+    if (c->wide) {                               // (high word: kbits - 64 < 64 bits, then the invalid bit)
+        h.smask_hi = (1ull << (c->kbits - 64)) - 1ull;
+        h.invalid_key = 1ull << (c->kbits - 64);
+    }
     h.out_base = c->n_hits;
     h.recs = c->recs.p;
     h.rec_count = c->d_rec_count;
@@ -583,9 +613,12 @@ kmer_status settle(kmer_ctx *c) {
         HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
         HIPCHK(c, hipMemcpyAsync(c->d_pos, c->d_pos_saved, sizeof(StreamPos), hipMemcpyDeviceToDevice, s));
         if (e & ERR_OVF_OVERFLOW) {
-            HIPCHK(c, c->ovf.ensure(c->h_small[1] + 1024, s));
+            st = ensure_ovf(c, c->h_small[1] + 1024, s);
+            if (st) return st;
             p.a.ovf = c->ovf.p;
             p.h.ovf = c->ovf.p;
+            p.a.ovf_hi = c->ovf_hi.p;
+            p.h.ovf_hi = c->ovf_hi.p;
             p.a.ovf_cap = p.h.ovf_cap = c->ovf.cap;
             if (packed) {
                 st = ensure_rank_arrays(c, c->n_hits + (uint64_t)p.n_tiles * HMAX + c->ovf.cap, c->n_hits, s);
@@ -1344,6 +1377,7 @@ kmer_status apply_cross(kmer_ctx *c) {
         ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, ob, kb, (size_t)n, 0, obits, s));
         HIPCHK(c, launch_cross_scatter(c->xslot.p, ob.current(), kb.current(), n, c->rkey.p, k32, c->rord.p, s));
     }
+    if (c->wide) HIPCHK(c, launch_cross_wide_fix(c->xslot.p, n, c->xkeyl.p, c->xkeyh.p, c->rkey.p, c->rkeyh.p, s));
     c->n_cross = 0;
     return KMER_OK;
 }
@@ -1375,6 +1409,25 @@ kmer_status sort_and_heads(kmer_ctx *c, K *keys, K *keys2, uint64_t n, bool with
         HIPCHK(c, launch_heads32((const uint32_t *)kb.current(), vb.current(), n, (uint32_t)invalid, rcnt, c->hrec.p, c->hcnt.p, s));
     else
         HIPCHK(c, launch_heads((const uint64_t *)kb.current(), vb.current(), n, invalid, rcnt, c->hrec.p, c->hcnt.p, s));
+    return KMER_OK;
+}
+
+// wide keys (two words): stable (lo, rank) sort, then a stable sort of the
+// high words by that order -> ranks ordered by (hi, lo), ascending within a
+// key; heads over the pairs (hcnt prefilled with 1, as the sparse heads)
+kmer_status sort_and_heads_wide(kmer_ctx *c, uint64_t n) {
+    hipStream_t s = c->stream;
+    HIPCHK(c, c->whA.ensure(n, s));
+    HIPCHK(c, c->whB.ensure(n, s));
+    HIPCHK(c, c->ridx3.ensure(n, s));
+    rocprim::counting_iterator<uint32_t> iota(0u);
+    ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, c->rkey.p, c->rkey2.p, iota, c->ridx2.p, (size_t)n, 0, 64, s));
+    HIPCHK(c, launch_gather_u64(c->rkeyh.p, c->ridx2.p, n, c->whA.p, s));
+    const int hbits = (int)c->kbits - 64 + 1;    // + the invalid bit
+    ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, c->whA.p, c->whB.p, c->ridx2.p, c->ridx3.p, (size_t)n, 0, hbits, s));
+    HIPCHK(c, launch_gather_u64(c->rkey.p, c->ridx3.p, n, c->rkey2.p, s));
+    HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)c->hcnt.p, 1, n, s));
+    HIPCHK(c, launch_heads_wide(c->whB.p, c->rkey2.p, c->ridx3.p, n, 1ull << (c->kbits - 64), c->hcnt.p, s));
     return KMER_OK;
 }
 
@@ -1445,7 +1498,9 @@ kmer_status rank_finish(kmer_ctx *c, uint64_t n, bool partial, bool with_counts,
     kmer_status st;
     // (merged partials carry counts: the sort finish sums them in 64 bits)
     const bool bucket = c->narrow && c->kbits <= BKT_LOW + 11 && !with_counts && !(c->p.flags & KMER_FLAG_SORT_FINISH);
-    if (bucket)
+    if (c->wide)
+        st = sort_and_heads_wide(c, n);          // (no partials / merged counts: refused for wide keys)
+    else if (bucket)
         st = bucket_heads(c, n);
     else if (c->narrow)
         st = sort_and_heads<uint32_t>(c, c->rkey32.p, c->rkey32b.p, n, with_counts);
@@ -1460,6 +1515,7 @@ kmer_status rank_finish(kmer_ctx *c, uint64_t n, bool partial, bool with_counts,
     e.hrec = with_counts ? c->hrec.p : nullptr;
     e.rkey32 = c->narrow ? c->rkey32.p : nullptr;
     e.rkey64 = c->narrow ? nullptr : c->rkey.p;
+    e.rkeyh = c->wide ? c->rkeyh.p : nullptr;
     e.opos = c->opos.p;
     e.rord = c->rord.p;
     e.n = n;
@@ -1995,7 +2051,8 @@ kmer_status group_count(kmer_ctx *g, GroupSrc &src, kmer_result **out) {
     const size_t N = g->group.size();
     kmer_ctx *c0 = g->group[0];
     const int mode = c0->mode;
-    const bool ordered = mode == MODE_PACKED || mode == MODE_WINDOWS;
+    // (keys of >= 64 bits have no packed partials: devices[0] counts alone)
+    const bool ordered = (mode == MODE_PACKED && !c0->wide) || mode == MODE_WINDOWS;
     const size_t W = (ordered || mode == MODE_TABLE) ? N : 1;    // children that take batches
     g->t_done = false;
     // -- the batch stream, dealt round robin over W worker threads
@@ -2345,8 +2402,8 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
         c->mode = MODE_TABLE;
     else if (dense_ok && (plen == 0 ? k <= 31 : (acgt && plen <= 3 && k <= (uint32_t)KMAX_DENSE)))
         c->mode = MODE_WINDOWS;
-    else if (dense_ok && acgt && k <= (uint32_t)KMAX_DENSE)
-        c->mode = MODE_PACKED;
+    else if (dense_ok && acgt && k <= (uint32_t)KMAX_TILE)
+        c->mode = MODE_PACKED;                  // (k > 32: 128-bit window codes)
     else if (pp->step == 1 && plen > 0 && k <= (uint32_t)KMAX_TILE)
         c->mode = MODE_TILE_REC;
     else
@@ -2354,6 +2411,7 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
     const bool packed_keys = c->mode == MODE_PACKED || c->mode == MODE_WINDOWS;
     c->kbits = packed_keys ? 2 * (k - plen) : 0;
     c->narrow = packed_keys && c->kbits <= 31;
+    c->wide = packed_keys && c->kbits >= 64;
     c->planes = (c->mode == MODE_PACKED || c->mode == MODE_TILE_REC) && acgt && !(pp->flags & KMER_FLAG_BYTE_SCAN);
     if (c->planes) {
         // plane bits of a base: bit 1 (plane L) and bit 2 (plane H) of its ASCII byte
@@ -2408,7 +2466,7 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
           hipEventCreateWithFlags(&c->evw, hipEventDisableTiming) == hipSuccess;
     if (!ok) return cleanup(KMER_E_OOM);
     if (ensure_records(c, 1 << 16) || ensure_tiles(c, 1 << 12)) return cleanup(KMER_E_OOM);
-    if (c->ovf.ensure(1 << 16, c->stream) != hipSuccess) return cleanup(KMER_E_OOM);
+    if (ensure_ovf(c, 1 << 16, c->stream) != KMER_OK) return cleanup(KMER_E_OOM);
     if (hipMemset(c->d_err, 0, 4) != hipSuccess) return cleanup(KMER_E_DEVICE);
     if (reset(c) != KMER_OK) return cleanup(KMER_E_DEVICE);
     c->open_stream = false;
@@ -2618,6 +2676,7 @@ kmer_status kmer_partial_device(kmer_ctx *c, const void **d_keys, const void **d
     SETTLE(c);
     if (c->mode != MODE_PACKED && c->mode != MODE_WINDOWS)
         return fail(c, KMER_E_STATE, "configuration has no packed keys");
+    if (c->wide) return fail(c, KMER_E_STATE, "keys of 64 bits or more (k - |P| >= 32) have no packed partials");
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
     kmer_status st = apply_cross(c);
     if (st) return st;
@@ -2637,6 +2696,7 @@ kmer_status kmer_finish_merged(kmer_ctx *c, const void *d_keys, const void *d_va
     SETTLE(c);
     if (c->mode != MODE_PACKED && c->mode != MODE_WINDOWS)
         return fail(c, KMER_E_STATE, "configuration has no packed keys");
+    if (c->wide) return fail(c, KMER_E_STATE, "keys of 64 bits or more (k - |P| >= 32) have no packed partials");
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
     if (out) *out = nullptr;
     hipStream_t s = c->stream;
@@ -2719,6 +2779,7 @@ kmer_status kmer_exchange_prepare(kmer_ctx *c, uint32_t world, const void **d_se
     SETTLE(c);
     if (c->mode != MODE_PACKED && c->mode != MODE_WINDOWS)
         return fail(c, KMER_E_STATE, "configuration has no packed keys");
+    if (c->wide) return fail(c, KMER_E_STATE, "keys of 64 bits or more (k - |P| >= 32) have no packed partials");
     if (!c->open_stream) return fail(c, KMER_E_STATE, "exchange without reset/feed");
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
     hipStream_t s = c->stream;
@@ -2758,6 +2819,7 @@ kmer_status kmer_finish_exchanged(kmer_ctx *c, const void *d_recv, uint64_t n, u
     SETTLE(c);
     if (c->mode != MODE_PACKED && c->mode != MODE_WINDOWS)
         return fail(c, KMER_E_STATE, "configuration has no packed keys");
+    if (c->wide) return fail(c, KMER_E_STATE, "keys of 64 bits or more (k - |P| >= 32) have no packed partials");
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
     if (out) *out = nullptr;
     hipStream_t s = c->stream;

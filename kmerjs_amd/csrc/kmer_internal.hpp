@@ -75,7 +75,8 @@ struct SeqLine {
 
 // A verified prefix hit from the tile scan with its tile-local line context.
 struct HitRec {
-    uint64_t code;         // 2-bit codes of the k-byte forward window (k <= 32)
+    uint64_t code;         // 2-bit codes of the k-byte forward window (its last 32 bases when k > 32;
+                           // the first k - 32 are in ScanArgs::hits_hi / ovf_hi at the same index)
     uint32_t tile;
     uint32_t qm;           // [13:0] pattern position q, [14] strand, [15] exotic, [16] line start in tile,
                            // [31:17] ordinal of the hit in its tile
@@ -119,6 +120,7 @@ struct ScanArgs {
     uint64_t ovf_cap;
     unsigned int *err;
     uint32_t ablate;               // experiments only: bit0 = drop all candidates
+    uint64_t *hits_hi, *ovf_hi;    // k > 32: code of the window's first k - 32 bases, per hit slot
 };
 
 // Bit-plane prefix test (ACGT prefixes): per prefix base i, xor masks that
@@ -150,10 +152,18 @@ struct HitArgs {
     uint32_t n_tiles, k, plen;
     uint64_t abs_offset;
     const StreamPos *pos;
-    uint32_t packed;               // ACGT windows (k <= 32) are ranked packed keys
+    uint32_t packed;               // ACGT windows are ranked packed keys
     uint32_t pbits;                // order-key position bits (PBITS_*)
-    uint64_t smask;                // suffix mask: 2*(k - |P|) bits
-    uint64_t invalid_key;          // 2^(2*(k-|P|)): sorts after every real key
+    uint64_t smask;                // suffix mask: 2*(k - |P|) bits (its low 64 when wide)
+    uint64_t invalid_key;          // 2^(2*(k-|P|)): sorts after every real key (wide: in rkeyh)
+    // k > 32: 128-bit window codes (hits_hi / ovf_hi); wide (2(k - |P|) >= 64):
+    // keys of two words, the high one in rkeyh (cross list: xkeyh, and xkey
+    // holds the entry's own index until apply_cross has moved it)
+    const uint64_t *hits_hi, *ovf_hi;
+    uint32_t wide;
+    uint64_t smask_hi;             // wide: mask of the high word (2(k - |P|) - 64 bits)
+    uint64_t *rkeyh;
+    uint64_t *xkeyh, *xkeyl;
     uint64_t out_base;             // session hits before this chunk
     uint64_t *rkey;                // by rank: suffix code (invalid_key: filtered / record)
     uint32_t *rkey32;              // ... as u32 when 2(k-|P|) + 1 <= 32 (then rkey is unused)
@@ -189,7 +199,8 @@ struct EmitArgs {
     const uint32_t *hcnt;          // by rank: the key's count at its first occurrence, else 0
     const HeadRec *hrec;           // merged finish (summed counts): by rank, key and u64 count of heads; else null
     const uint32_t *rkey32;        // hrec == null: key by rank (narrow keys) ...
-    const uint64_t *rkey64;        // ... or (wide keys)
+    const uint64_t *rkey64;        // ... or (wider keys)
+    const uint64_t *rkeyh;         // ... with, for keys of >= 64 bits, their high words
     const uint32_t *opos;          // exclusive scan of (hcnt != 0): output position
     const uint64_t *rord;          // by rank: order key
     uint64_t n;
@@ -307,6 +318,14 @@ hipError_t launch_heads_sparse(const uint64_t *skey64, const uint32_t *skey32, c
 hipError_t launch_heads32(const uint32_t *skey, const uint32_t *srank, uint64_t n, uint32_t invalid_key,
                           const uint64_t *rcnt, HeadRec *hrec, uint32_t *hcnt, hipStream_t s);
 hipError_t launch_emit(const EmitArgs &a, hipStream_t s);
+// wide keys (2(k - |P|) >= 64 bits, k <= 64): dst[i] = src[idx[i]]; the cross
+// entries' keys after apply_cross; heads over (hi, lo) sorted ranks (hcnt
+// prefilled with 1, as launch_heads_sparse)
+hipError_t launch_gather_u64(const uint64_t *src, const uint32_t *idx, uint64_t n, uint64_t *dst, hipStream_t s);
+hipError_t launch_cross_wide_fix(const uint32_t *xslot, uint64_t n, const uint64_t *xkeyl, const uint64_t *xkeyh,
+                                 uint64_t *rkey, uint64_t *rkeyh, hipStream_t s);
+hipError_t launch_heads_wide(const uint64_t *shi, const uint64_t *slo, const uint32_t *srank, uint64_t n,
+                             uint64_t invalid_hi, uint32_t *hcnt, hipStream_t s);
 // bucket finish (u32 keys of <= BKT_LOW + 11 bits)
 constexpr uint32_t BKT_LOW = 14;             // keys per bucket table: 2^14 (128 KiB of LDS: min rank, count)
 constexpr uint32_t BKT_MAX = 2048;           // buckets (keys of <= BKT_LOW + 11 bits)

@@ -195,6 +195,14 @@ __device__ __forceinline__ uint64_t revcomp_code(uint64_t x, uint32_t k) {
     return k >= 32 ? x : (x >> (64 - 2 * k));
 }
 
+// the same for a 128-bit code of 32 < k <= 64 bases (hi: the first k - 32)
+__device__ __forceinline__ void revcomp_code128(uint64_t hi, uint64_t lo, uint32_t k, uint64_t *rhi, uint64_t *rlo) {
+    const uint64_t h = revcomp_code(lo, 32), l = revcomp_code(hi, 32);   // the 128 bits reversed
+    const uint32_t s = 128 - 2 * k;                                     // garbage bits at the bottom (< 64)
+    *rlo = s ? (l >> s) | (h << (64 - s)) : l;
+    *rhi = s ? h >> s : h;
+}
+
 // Shared tile prologue: stage tile + halos in LDS, per-thread words, '\n'
 // count, block exclusive scan (sh.tpre), tile's last '\n' (sh.lastpos).
 // Returns the tile's '\n' count (bytes < len only).
@@ -408,7 +416,8 @@ __device__ __forceinline__ int last_newline_in_chunk(const uint8_t *buf, int c, 
 // THREAD_MAP: sh.nlmap holds one bit per 64-byte thread region (plane
 // kernel; chunks inside a region are resolved through cpre), else one bit per
 // 16-byte chunk (byte kernel).
-template <bool THREAD_MAP>
+// WIDE: k > 32 (the window's first k - 32 bases go to hits_hi / ovf_hi)
+template <bool THREAD_MAP, bool WIDE>
 __device__ __forceinline__ void emit_hit(const ScanArgs &a, const uint8_t *buf, ScanShared &sh, uint32_t tile,
                                       uint32_t e) {
     const uint32_t k = a.k, plen = a.plen;
@@ -430,6 +439,18 @@ __device__ __forceinline__ void emit_hit(const ScanArgs &a, const uint8_t *buf, 
         const uint32_t pk = ((c & 3u) << 6) | (((c >> 8) & 3u) << 4) | (((c >> 16) & 3u) << 2) |
                             ((c >> 24) & 3u);                // first byte most significant
         code = (code << (2 * nb)) | (pk >> (2 * (4 - nb)));
+    }
+    // k > 32: code keeps the last 32 bases; the first k - 32 (the window's
+    // bytes are ACGT-checked above)
+    uint64_t chi = 0;
+    if (WIDE) {
+        for (uint32_t b = 0; b < k - 32; b += 4) {
+            const uint32_t x = lds_word(buf, s0 + (int)b);
+            const uint32_t nb = k - 32 - b >= 4 ? 4u : k - 32 - b;
+            const uint32_t c = ((x >> 1) ^ (x >> 2)) & 0x03030303u;
+            const uint32_t pk = ((c & 3u) << 6) | (((c >> 8) & 3u) << 4) | (((c >> 16) & 3u) << 2) | ((c >> 24) & 3u);
+            chi = (chi << (2 * nb)) | (pk >> (2 * (4 - nb)));
+        }
     }
     // crosses a line end (or the end of input); k == 1: line.length > 1
     const bool valid = !hasnl && !(k == 1 && buf[FH + s0 - 1] == '\n' && buf[FH + s0 + 1] == '\n');
@@ -521,16 +542,22 @@ __device__ __forceinline__ void emit_hit(const ScanArgs &a, const uint8_t *buf, 
     r.lstart = lstart >= 0 ? (uint32_t)lstart : 0u;
     if (slot < HMAX) {
         a.hits[(uint64_t)tile * HMAX + slot] = r;
+        if (WIDE) a.hits_hi[(uint64_t)tile * HMAX + slot] = chi;
     } else {
         const unsigned long long o = atomicAdd(a.ovf_count, 1ull);
-        if (o < a.ovf_cap) a.ovf[o] = r;
-        else atomicOr(a.err, ERR_OVF_OVERFLOW);
+        if (o < a.ovf_cap) {
+            a.ovf[o] = r;
+            if (WIDE) a.ovf_hi[o] = chi;
+        } else {
+            atomicOr(a.err, ERR_OVF_OVERFLOW);
+        }
     }
 }
 
 // One candidate word (4 window starts at tile position q0 with a 4-byte
 // match on some strand): exact prefix test of its 8 (position, strand)
 // windows, then one hit record per verified window.
+template <bool WIDE>
 __device__ __forceinline__ void scan_word(const ScanArgs &a, const uint8_t *buf, ScanShared &sh, uint32_t tile,
                                           const uint32_t *pw, uint32_t q0) {
     const uint32_t plen = a.plen, P4 = a.p4, R4 = a.r4, PM = a.pmask;
@@ -555,7 +582,7 @@ __device__ __forceinline__ void scan_word(const ScanArgs &a, const uint8_t *buf,
             const uint32_t mk = n >= 4 ? 0xFFFFFFFFu : ((1u << (8 * n)) - 1u);
             ok = ((lds_word(buf, q + (int)b) ^ pw[(strand ? KMAX_TILE / 4 : 0) + b / 4]) & mk) == 0;
         }
-        if (ok) emit_hit<false>(a, buf, sh, tile, ((uint32_t)q << 1) | strand);
+        if (ok) emit_hit<false, WIDE>(a, buf, sh, tile, ((uint32_t)q << 1) | strand);
     }
 }
 
@@ -567,7 +594,7 @@ __device__ __forceinline__ void scan_word(const ScanArgs &a, const uint8_t *buf,
 // window at each of its 16 positions compared to P[0:4] and rc(P)[0:4] with
 // v_cmp (the compiler ORs the lane masks on the scalar unit).  A packed
 // 4 x 16-bit block scan gives the exclusive '\n' count of every chunk.
-template <bool FULL4>
+template <bool FULL4, bool WIDE>
 __global__ __launch_bounds__(TPB) void scan_tile_kernel(ScanArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t buf[BUFSZ];
     __shared__ ScanShared sh;
@@ -733,13 +760,13 @@ __global__ __launch_bounds__(TPB) void scan_tile_kernel(ScanArgs a) {
             cand &= cand - 1;
             const uint32_t q0 = 16u * (uint32_t)(tid + TPB * (bitc >> 2)) + 4u * (uint32_t)(bitc & 3);
             if (pos < QCAP) sh.q[pos] = q0;
-            else scan_word(a, buf, sh, tile, pw, q0);   // queue full (short prefixes): process in place
+            else scan_word<WIDE>(a, buf, sh, tile, pw, q0);   // queue full (short prefixes): process in place
             ++pos;
         }
     }
     __syncthreads();
     const uint32_t nq = min(sh.qn, (uint32_t)QCAP);
-    for (uint32_t h = tid; h < nq; h += TPB) scan_word(a, buf, sh, tile, pw, sh.q[h]);
+    for (uint32_t h = tid; h < nq; h += TPB) scan_word<WIDE>(a, buf, sh, tile, pw, sh.q[h]);
     if (nq > 64 || sh.qn > QCAP) {
         __syncthreads();         // uniform: every wave may have written records
         if (tid == 0) {
@@ -757,6 +784,7 @@ __global__ __launch_bounds__(TPB) void scan_tile_kernel(ScanArgs a) {
 
 // Plane-kernel candidate (q << 1) | strand: byte-exact prefix check (the
 // planes alias non-ACGT bytes), then the hit record.
+template <bool WIDE>
 __device__ __forceinline__ void verify_emit(const ScanArgs &a, const uint8_t *buf, ScanShared &sh, uint32_t tile,
                                             const uint32_t *pw, uint32_t e) {
     const uint32_t strand = e & 1u, plen = a.plen;
@@ -772,7 +800,7 @@ __device__ __forceinline__ void verify_emit(const ScanArgs &a, const uint8_t *bu
         if (ok) atomicAdd(&sh.nx, 0u);
         return;
     }
-    if (ok) emit_hit<true>(a, buf, sh, tile, e);
+    if (ok) emit_hit<true, WIDE>(a, buf, sh, tile, e);
 }
 
 // ---------------------------------------------------------------------------
@@ -797,7 +825,7 @@ __device__ __forceinline__ uint32_t plane_match(uint32_t L0, uint32_t H0, uint32
     return acc;
 }
 
-template <bool FULL5>
+template <bool FULL5, bool WIDE>
 __global__ __launch_bounds__(TPB) void scan_planes_kernel(ScanArgs a, PlaneArgs pa) {
     __shared__ __attribute__((aligned(16))) uint8_t buf[BUFSZ];
     __shared__ ScanShared sh;
@@ -990,7 +1018,7 @@ __global__ __launch_bounds__(TPB) void scan_planes_kernel(ScanArgs a, PlaneArgs 
                             while (m) {
                                 const uint32_t bit = __ffs(m) - 1;
                                 m &= m - 1;
-                                verify_emit(a, buf, sh, tile, pw, e0 + (bit << 1));
+                                verify_emit<WIDE>(a, buf, sh, tile, pw, e0 + (bit << 1));
                             }
                         }
                     }
@@ -1007,7 +1035,7 @@ __global__ __launch_bounds__(TPB) void scan_planes_kernel(ScanArgs a, PlaneArgs 
         while (m) {
             const uint32_t bit = __ffs(m) - 1;
             m &= m - 1;
-            verify_emit(a, buf, sh, tile, pw, en.x + (bit << 1));
+            verify_emit<WIDE>(a, buf, sh, tile, pw, en.x + (bit << 1));
         }
     }
     if (nq > 64 || sh.qn > QE) {
@@ -1030,8 +1058,9 @@ __global__ __launch_bounds__(TPB) void scan_planes_kernel(ScanArgs a, PlaneArgs 
 // Returns the packed key (invalid_key when the hit does not count as a packed
 // key: non-sequence line, or a record) and writes records for exotic windows
 // / record mode.  *lk = order of the hit among its tile's hits (local).
-__device__ __forceinline__ uint64_t resolve_hit(const HitArgs &a, const HitRec &r, const TileSum &tb,
-                                                uint64_t *order_out, uint32_t *lk, bool *lvalid_out) {
+__device__ __forceinline__ uint64_t resolve_hit(const HitArgs &a, const HitRec &r, uint64_t code_hi,
+                                                const TileSum &tb, uint64_t *order_out, uint32_t *lk,
+                                                bool *lvalid_out, uint64_t *key_hi) {
     const uint32_t t = r.tile;
     const uint32_t strand = (r.qm >> 14) & 1u;
     const bool exotic = (r.qm >> 15) & 1u;
@@ -1056,9 +1085,18 @@ __device__ __forceinline__ uint64_t resolve_hit(const HitArgs &a, const HitRec &
     *lk = (r.c_local << 17) | (strand << 16) | (strand ? 0xFFFFu - sp : sp);
     *lvalid_out = lvalid;
     uint64_t key = a.invalid_key;
+    *key_hi = a.wide ? a.invalid_key : 0;        // (wide: the invalid marker is in the high word)
+    if (a.wide) key = 0;
     if (seq) {
         if (a.packed && !exotic) {
-            key = (strand ? revcomp_code(r.code, a.k) : r.code) & a.smask;
+            if (a.k > 32) {
+                uint64_t h = code_hi, l = r.code;
+                if (strand) revcomp_code128(code_hi, r.code, a.k, &h, &l);
+                key = l & a.smask;
+                *key_hi = h & a.smask_hi;
+            } else {
+                key = (strand ? revcomp_code(r.code, a.k) : r.code) & a.smask;
+            }
         } else {
             const unsigned long long n = atomicAdd(a.rec_count, 1ull);
             if (n < a.rec_cap) {
@@ -1078,16 +1116,23 @@ __device__ __forceinline__ uint64_t resolve_hit(const HitArgs &a, const HitRec &
 
 // Write one resolved packed hit at its rank slot, or to the cross list.
 __device__ __forceinline__ void place_hit(const HitArgs &a, uint64_t slot, bool cross, uint64_t xi, uint64_t key,
-                                          uint64_t order) {
+                                          uint64_t key_hi, uint64_t order) {
     a.ridx[slot] = (uint32_t)slot;
     if (!cross) {
         if (a.rkey32) a.rkey32[slot] = (uint32_t)key;
         else a.rkey[slot] = key;
+        if (a.wide) a.rkeyh[slot] = key_hi;
         a.rord[slot] = order;
     } else if (xi < a.xcap) {
         a.xord[xi] = order;
-        a.xkey[xi] = key;
         a.xslot[xi] = (uint32_t)slot;
+        if (a.wide) {                            // (the cross kernels move the index; cross_wide_fix the key)
+            a.xkey[xi] = xi;
+            a.xkeyl[xi] = key;
+            a.xkeyh[xi] = key_hi;
+        } else {
+            a.xkey[xi] = key;
+        }
     } else {
         atomicOr(a.err, ERR_CROSS_OVERFLOW);
     }
@@ -1101,11 +1146,13 @@ __device__ __forceinline__ void place_hit(const HitArgs &a, uint64_t slot, bool 
 // rank, or on the cross list (line crosses a tile edge / tile overflowed).
 constexpr uint32_t HTPW = 4;
 constexpr uint32_t HENT = HTPW * HMAX;       // staged hits per wave
+template <bool WIDE>
 __global__ __launch_bounds__(256) void hit_kernel(HitArgs a) {
     __shared__ uint32_t s_lk[4][HENT];
     __shared__ uint8_t s_x[4][HENT];
     __shared__ uint64_t s_key[4][HENT];
     __shared__ uint64_t s_ord[4][HENT];
+    __shared__ uint64_t s_keyh[WIDE ? 4 : 1][WIDE ? HENT : 1];
     const uint32_t wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t t0 = __builtin_amdgcn_readfirstlane((blockIdx.x * 4 + wid) * HTPW);
     if (t0 >= a.n_tiles || *a.ovf_count > a.ovf_cap) return;   // overflowed scan: the host redoes the chunk
@@ -1135,14 +1182,16 @@ __global__ __launch_bounds__(256) void hit_kernel(HitArgs a) {
                     tsu = ts[v];
                     tbu = tb[v];
                 }
-            const HitRec r = a.hits[(uint64_t)(t0 + u) * HMAX + i];
-            uint64_t order;
+            const uint64_t hslot = (uint64_t)(t0 + u) * HMAX + i;
+            const HitRec r = a.hits[hslot];
+            uint64_t order, kh;
             uint32_t lk;
             bool lvalid;
-            const uint64_t key = resolve_hit(a, r, tbu, &order, &lk, &lvalid);
+            const uint64_t key = resolve_hit(a, r, a.k > 32 ? a.hits_hi[hslot] : 0, tbu, &order, &lk, &lvalid, &kh);
             s_lk[wid][e] = lk;
             s_x[wid][e] = (tsu.nh > (uint32_t)HMAX || !lvalid || r.c_local == (uint32_t)tsu.cnt) ? 1 : 0;
             s_key[wid][e] = key;
+            if (WIDE) s_keyh[WIDE ? wid : 0][WIDE ? e : 0] = kh;
             s_ord[wid][e] = order;
         }
     }
@@ -1180,7 +1229,8 @@ __global__ __launch_bounds__(256) void hit_kernel(HitArgs a) {
                 xr += less & (uint32_t)s_x[wid][j];
             }
         }
-        place_hit(a, a.out_base + hb + rank, cross, a.xbase + xb + xr, s_key[wid][e], s_ord[wid][e]);
+        place_hit(a, a.out_base + hb + rank, cross, a.xbase + xb + xr, s_key[wid][e],
+                  WIDE ? s_keyh[WIDE ? wid : 0][WIDE ? e : 0] : 0, s_ord[wid][e]);
     }
 }
 
@@ -1190,13 +1240,13 @@ __global__ __launch_bounds__(256) void hit_overflow_kernel(HitArgs a) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const HitRec r = a.ovf[i];
         const TileSum tb = a.tscan[r.tile];
-        uint64_t order;
+        uint64_t order, kh;
         uint32_t lk;
         bool lvalid;
-        const uint64_t key = resolve_hit(a, r, tb, &order, &lk, &lvalid);
+        const uint64_t key = resolve_hit(a, r, a.k > 32 ? a.ovf_hi[i] : 0, tb, &order, &lk, &lvalid, &kh);
         if (!a.packed) continue;
         const uint32_t ord = r.qm >> 17;
-        place_hit(a, a.out_base + tb.nh + ord, true, a.xbase + tb.nx + ord, key, order);
+        place_hit(a, a.out_base + tb.nh + ord, true, a.xbase + tb.nx + ord, key, kh, order);
     }
     // chunk tail, by the last block to finish (every hit of the chunk has read
     // pos by then): advance the stream position past the chunk, publish the
@@ -1800,6 +1850,49 @@ __global__ __launch_bounds__(256) void heads_sparse_kernel(const K *skey, const 
 }
 
 // ---------------------------------------------------------------------------
+// Wide keys (2(k - |P|) >= 64 bits, k <= 64): two words per key, hi in a
+// parallel array.  The rank finish sorts (lo, rank) and then, stably,
+// (hi, rank) -- LSD order: by (hi, lo), ranks ascending within a key.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void gather_u64_kernel(const uint64_t *src, const uint32_t *idx, uint64_t n,
+                                                         uint64_t *dst) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        dst[i] = src[idx[i]];
+}
+
+// after apply_cross the cross slots hold their entry's index: put the key there
+__global__ __launch_bounds__(256) void cross_wide_fix_kernel(const uint32_t *xslot, uint64_t n, const uint64_t *xkeyl,
+                                                             const uint64_t *xkeyh, uint64_t *rkey, uint64_t *rkeyh) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t sl = xslot[i];
+        const uint64_t x = rkey[sl];
+        rkey[sl] = xkeyl[x];
+        rkeyh[sl] = xkeyh[x];
+    }
+}
+
+// heads_sparse_kernel over (hi, lo) pairs: hcnt prefilled with 1; members of
+// groups of >= 2 and invalid keys (hi == invalid_hi) are written
+__global__ __launch_bounds__(256) void heads_wide_kernel(const uint64_t *shi, const uint64_t *slo,
+                                                         const uint32_t *srank, uint64_t n, uint64_t invalid_hi,
+                                                         uint32_t *hcnt) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t h = shi[i], l = slo[i];
+        const bool dp = i > 0 && shi[i - 1] == h && slo[i - 1] == l;
+        const bool dn = i + 1 < n && shi[i + 1] == h && slo[i + 1] == l;
+        const bool inv = h == invalid_hi;
+        if (!inv && !dp && !dn) continue;
+        uint32_t v = 0;
+        if (!inv && !dp) {
+            uint64_t e = i + 1;                  // (groups are short: hits of one k-mer)
+            while (e < n && shi[e] == h && slo[e] == l) ++e;
+            v = (uint32_t)(e - i);
+        }
+        hcnt[srank[i]] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Bucket finish (u32 keys of <= 24 bits): instead of sorting, partition the
 // ranked hits by key >> BKT_LOW into <= 2048 buckets (LDS-privatised
 // histogram, scan, scatter), then one workgroup per bucket keeps an LDS table
@@ -1925,7 +2018,7 @@ __global__ __launch_bounds__(1024) void bucket_heads_kernel(const uint16_t *pkey
 __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
     // decoded keys of this block's heads, staged so that the block's output
     // range [o0 * k, o_end * k) is written with coalesced dword stores
-    __shared__ __attribute__((aligned(16))) uint8_t kbuf[256 * KMAX_PACKED];
+    __shared__ __attribute__((aligned(16))) uint8_t kbuf[256 * KMAX_TILE];
     __shared__ uint32_t s_o0, s_oend;
     const uint64_t n = a.n;
     const uint32_t k = a.k, plen = a.plen;
@@ -1953,13 +2046,14 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
         }
         const uint32_t o0 = s_o0, oend = s_oend;
         if (f) {
-            uint64_t key, cnt;
+            uint64_t key, cnt, keyh = 0;
             if (a.hrec) {
                 const HeadRec v = a.hrec[r];
                 key = v.key;
                 cnt = v.count;
             } else {
                 key = a.rkey32 ? (uint64_t)a.rkey32[r] : a.rkey64[r];
+                if (a.rkeyh) keyh = a.rkeyh[r];
                 cnt = hc;
             }
             const uint64_t first = a.rord[r];
@@ -1973,27 +2067,37 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
                 a.cnt_out[o] = cnt;
                 a.first_out[o] = first;
                 uint8_t *out = staged ? kbuf + (o - o0) * k : a.keys_out + (uint64_t)o * k;
-                uint32_t words[8];
-#pragma unroll
-                for (int w = 0; w < 8; ++w) {
+                // word w = bases 4w .. 4w + 3, stored as soon as it is formed
+                // (static indices only: no private-memory array)
+                const uint32_t nw = (k + 3) / 4;
+                uint32_t w0 = 0, w1 = 0, w2 = 0;
+                for (int w = 0; w < KMAX_TILE / 4; ++w) {
+                    if ((uint32_t)w >= nw) break;
                     uint32_t v = 0;
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const uint32_t pos = 4 * w + j;
                         uint32_t ch = 0;
-                        if (pos < plen) ch = a.P[pos];
-                        else if (pos < k)
-                            ch = (0x54474341u >> (8 * ((uint32_t)(key >> (2 * (k - 1 - pos))) & 3u))) & 0xFFu;
+                        if (pos < plen) {
+                            ch = a.P[pos];
+                        } else if (pos < k) {
+                            const uint32_t sh = 2 * (k - 1 - pos);      // (< 128)
+                            const uint32_t b = (uint32_t)(sh < 64 ? key >> sh : keyh >> (sh - 64)) & 3u;
+                            ch = (0x54474341u >> (8 * b)) & 0xFFu;
+                        }
                         v |= ch << (8 * j);
                     }
-                    words[w] = v;
-                }
-                if (k == 16) {
-                    *(uint4 *)out = make_uint4(words[0], words[1], words[2], words[3]);
-                } else if ((k & 3) == 0) {
-                    for (uint32_t w = 0; w < k / 4; ++w) *(uint32_t *)(out + 4 * w) = words[w];
-                } else {
-                    for (uint32_t b = 0; b < k; ++b) out[b] = (uint8_t)(words[b >> 2] >> (8 * (b & 3)));
+                    if (k == 16) {                     // one 16-byte store
+                        if (w == 0) w0 = v;
+                        else if (w == 1) w1 = v;
+                        else if (w == 2) w2 = v;
+                        else *(uint4 *)out = make_uint4(w0, w1, w2, v);
+                    } else if ((k & 3) == 0) {
+                        *(uint32_t *)(out + 4 * w) = v;
+                    } else {
+                        for (uint32_t b = 4 * w; b < k && b < 4 * (uint32_t)w + 4; ++b)
+                            out[b] = (uint8_t)(v >> (8 * (b & 3)));
+                    }
                 }
             }
         }
@@ -2250,18 +2354,32 @@ hipError_t launch_lines(const TileArgs &a, bool lookback, hipStream_t s) {
 }
 
 hipError_t launch_scan_planes(const ScanArgs &a, const PlaneArgs &pa, hipStream_t s) {
-    if (pa.pb >= 5) hipLaunchKernelGGL((scan_planes_kernel<true>), dim3(a.n_tiles), dim3(TPB), 0, s, a, pa);
-    else hipLaunchKernelGGL((scan_planes_kernel<false>), dim3(a.n_tiles), dim3(TPB), 0, s, a, pa);
+    const dim3 g(a.n_tiles);
+    if (a.k > 32) {
+        if (pa.pb >= 5) hipLaunchKernelGGL((scan_planes_kernel<true, true>), g, dim3(TPB), 0, s, a, pa);
+        else hipLaunchKernelGGL((scan_planes_kernel<false, true>), g, dim3(TPB), 0, s, a, pa);
+    } else {
+        if (pa.pb >= 5) hipLaunchKernelGGL((scan_planes_kernel<true, false>), g, dim3(TPB), 0, s, a, pa);
+        else hipLaunchKernelGGL((scan_planes_kernel<false, false>), g, dim3(TPB), 0, s, a, pa);
+    }
     return hipGetLastError();
 }
 hipError_t launch_scan_tiles(const ScanArgs &a, hipStream_t s) {
-    if (a.plen >= 4) hipLaunchKernelGGL((scan_tile_kernel<true>), dim3(a.n_tiles), dim3(TPB), 0, s, a);
-    else hipLaunchKernelGGL((scan_tile_kernel<false>), dim3(a.n_tiles), dim3(TPB), 0, s, a);
+    const dim3 g(a.n_tiles);
+    if (a.k > 32) {
+        if (a.plen >= 4) hipLaunchKernelGGL((scan_tile_kernel<true, true>), g, dim3(TPB), 0, s, a);
+        else hipLaunchKernelGGL((scan_tile_kernel<false, true>), g, dim3(TPB), 0, s, a);
+    } else {
+        if (a.plen >= 4) hipLaunchKernelGGL((scan_tile_kernel<true, false>), g, dim3(TPB), 0, s, a);
+        else hipLaunchKernelGGL((scan_tile_kernel<false, false>), g, dim3(TPB), 0, s, a);
+    }
     return hipGetLastError();
 }
 
 hipError_t launch_hits(const HitArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL(hit_kernel, dim3((a.n_tiles + 4 * HTPW - 1) / (4 * HTPW)), dim3(256), 0, s, a);
+    const dim3 grid((a.n_tiles + 4 * HTPW - 1) / (4 * HTPW));
+    if (a.wide) hipLaunchKernelGGL(hit_kernel<true>, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(hit_kernel<false>, grid, dim3(256), 0, s, a);
     hipLaunchKernelGGL(hit_overflow_kernel, dim3(64), dim3(256), 0, s, a);
     return hipGetLastError();
 }
@@ -2315,6 +2433,22 @@ hipError_t launch_cross_segsort(uint64_t *ord, uint64_t *key, const uint32_t *sl
                                 uint32_t *rkey32, uint64_t *rord, uint32_t pbits, hipStream_t s) {
     if (n) hipLaunchKernelGGL(cross_segsort_kernel, dim3(grid_for(n)), dim3(256), 0, s, ord, key, slot, n, rkey, rkey32,
                               rord, pbits + 1);
+    return hipGetLastError();
+}
+hipError_t launch_gather_u64(const uint64_t *src, const uint32_t *idx, uint64_t n, uint64_t *dst, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(gather_u64_kernel, dim3(grid_for(n)), dim3(256), 0, s, src, idx, n, dst);
+    return hipGetLastError();
+}
+hipError_t launch_cross_wide_fix(const uint32_t *xslot, uint64_t n, const uint64_t *xkeyl, const uint64_t *xkeyh,
+                                 uint64_t *rkey, uint64_t *rkeyh, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(cross_wide_fix_kernel, dim3(grid_for(n)), dim3(256), 0, s, xslot, n, xkeyl, xkeyh, rkey,
+                              rkeyh);
+    return hipGetLastError();
+}
+hipError_t launch_heads_wide(const uint64_t *shi, const uint64_t *slo, const uint32_t *srank, uint64_t n,
+                             uint64_t invalid_hi, uint32_t *hcnt, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(heads_wide_kernel, dim3(grid_for(n)), dim3(256), 0, s, shi, slo, srank, n, invalid_hi,
+                              hcnt);
     return hipGetLastError();
 }
 hipError_t launch_heads(const uint64_t *skey, const uint32_t *srank, uint64_t n, uint64_t invalid_key,

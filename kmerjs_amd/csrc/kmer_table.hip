@@ -986,7 +986,7 @@ __device__ __forceinline__ uint32_t block_excl_512(uint32_t v, uint32_t *ws, uin
 
 __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) {
     __shared__ uint32_t lkey[TS_CAP1];                // sorted unit: u32 (one bucket) or u64 (a group)
-    __shared__ uint32_t bst[TS_NB];                   // bin counts, then starts, then (after the scatter) ends
+    __shared__ uint32_t bst[TS_NB];                   // bin counts, then starts
     __shared__ uint64_t sc[TS_SC + 2];                // start[cbase .. cbase + TS_SC + 1]
     __shared__ uint32_t nout[TS_GMAX];
     __shared__ uint32_t ws[8], smax;
@@ -1099,10 +1099,12 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
             if (t == 0) smax = 0;
             for (uint32_t i = t; i < g; i += TAB_SWG) nout[i] = 0;
             __syncthreads();
+            // bin counts; the returned value is the key's rank in its bin (< 2^14)
 #pragma unroll
             for (int j = 0; j < KPT; ++j)
                 if (left > j * (int)TAB_SWG)
-                    __hip_atomic_fetch_add(&bst[pk[j]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    pk[j] = pk[j] << 14 |
+                            __hip_atomic_fetch_add(&bst[pk[j]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __syncthreads();
             {
                 // bin starts: thread t scans bins 8t .. 8t + 7
@@ -1125,16 +1127,17 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
             }
             __syncthreads();
             if (smax > TS_BINMAX) return false;        // (uniform) many copies of a key
-            // counting-sort scatter: bst[b] runs from the start to the end of bin b
+            // counting-sort scatter: bin start + rank in the bin (bst[b] stays the start of bin b)
 #pragma unroll
             for (int j = 0; j < KPT; ++j)
                 if (left > j * (int)TAB_SWG) {
-                    const uint32_t pos = atomicAdd(&bst[pk[j]], 1u);
+                    const uint32_t b = pk[j] >> 14;
+                    const uint32_t pos = bst[b] + (pk[j] & 0x3FFFu);
                     if (ONE)
                         lkey[pos] = lo[j];
                     else
                         lkey64[pos] = (uint64_t)hi[ONE ? 0 : j] << 32 | lo[j];
-                    pk[j] = pk[j] << 14 | pos;
+                    pk[j] = b << 14 | pos;
                 }
             __syncthreads();
             // every held key scans its bin [end of bin b - 1, end of bin b) for
@@ -1152,7 +1155,7 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                     const int j = g0 + u;
                     const bool valid = left > j * (int)TAB_SWG;
                     const uint32_t b = pk[j] >> 14;
-                    const uint32_t b0 = b ? bst[b - 1] : 0u, b1 = (a.ablate & 8) ? b0 : bst[b];
+                    const uint32_t b0 = bst[b], b1 = (a.ablate & 8) ? b0 : b + 1 < TS_NB ? bst[b + 1] : (uint32_t)n;
                     const uint32_t c = valid ? b1 - b0 : 0u;
                     bb[u] = b0 | c << 14;
                     cf[u] = valid ? ((a.ablate & 8) ? 0x101u : 0x100u) : 0u;   // (experiments: no bin scan)
