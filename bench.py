@@ -41,16 +41,20 @@ def cpu_baseline(k, prefix, seconds_target=8.0):
     n = 20000
     data = oracle.synth_fastq(1, 0, n)
     t0 = time.perf_counter()
-    oracle.count_buffer(data, prefix, k, 1)
+    r0 = oracle.count_buffer(data, prefix, k, 1)
     dt = time.perf_counter() - t0
-    n = int(max(20000, min(5_000_000, n * seconds_target / max(dt, 1e-6))))
+    n_cap = int(20_000_000 / max(1e-9, len(r0) / n))       # (host result lists of <= ~20 M entries)
+    n = int(max(20000, min(5_000_000, n_cap, n * seconds_target / max(dt, 1e-6))))
     data = oracle.synth_fastq(1, 0, n)
     t0 = time.perf_counter()
-    oracle.count_buffer(data, prefix, k, 1)
+    r1 = oracle.count_buffer(data, prefix, k, 1)
     dt1 = time.perf_counter() - t0
-    # one thread per core (the box's CPU share is 16; ctypes calls release the GIL)
+    # one thread per core (the box's CPU share is 16; ctypes calls release the GIL);
+    # the Python merge of the shards' Maps is bounded to ~20 M entries (dense
+    # prefixes: nearly every hit a distinct key)
     cores = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
-    nt = n * cores
+    per_read = max(1e-9, len(r1) / n)
+    nt = max(cores, min(n * cores, int(20_000_000 / per_read)))
     data = oracle.synth_fastq(1, 0, nt)
     per = (nt + cores - 1) // cores
     shards = [data[i * per * RECORD:min(nt, (i + 1) * per) * RECORD] for i in range(cores)]

@@ -65,7 +65,7 @@ function countPath(kmerObj, fastq) {
             }
             let map;
             try {
-                map = KmerMap.fromNative(res);
+                map = KmerMap.fromNative(res, drop.native().indexKeys);
             } catch (e) {
                 reject(e);
                 return;

@@ -25,10 +25,13 @@
 
 class KmerMap extends Map {
     // keys: a Latin-1 string of all keys back to back; off: n + 1 offsets;
-    // cnt: n values (array-like)
-    constructor(keys, off, cnt) {
+    // cnt: n values (array-like); buf, indexer: the same keys as a Buffer and
+    // the addon's indexKeys (builds _index's table natively), or absent
+    constructor(keys, off, cnt, buf = null, indexer = null) {
         super();
         this._all = keys;
+        this._buf = buf;
+        this._indexer = indexer;
         this._off = off;
         this._cnt = cnt;
         this._n = cnt.length;
@@ -39,10 +42,10 @@ class KmerMap extends Map {
         this._ndel = 0;
     }
 
-    static fromNative(res) {
+    static fromNative(res, indexer = null) {
         const n = res.counts.length;
         const all = n ? res.keys.latin1Slice(0, res.offsets[n]) : '';
-        return new KmerMap(all, res.offsets, res.counts);
+        return new KmerMap(all, res.offsets, res.counts, res.keys, indexer);
     }
 
     _key(i) { return this._all.substring(this._off[i], this._off[i + 1]); }
@@ -70,13 +73,19 @@ class KmerMap extends Map {
             const off = this._off;
             let cap = 16;
             while (cap < 2 * n) cap *= 2;
-            const tab = new Int32Array(cap).fill(-1);
             const mask = cap - 1;
-            for (let i = 0; i < n; i += 1) {
-                let h = this._hashAt(off[i], off[i + 1]) & mask;
-                while (tab[h] !== -1) h = (h + 1) & mask;
-                tab[h] = i;
+            let tab;
+            if (this._indexer !== null && this._buf !== null && off instanceof Float64Array) {
+                tab = this._indexer(this._buf, off, n, cap);     // (the same table, built natively)
+            } else {
+                tab = new Int32Array(cap).fill(-1);
+                for (let i = 0; i < n; i += 1) {
+                    let h = this._hashAt(off[i], off[i + 1]) & mask;
+                    while (tab[h] !== -1) h = (h + 1) & mask;
+                    tab[h] = i;
+                }
             }
+            this._buf = null;            // (the string holds the keys from here on)
             this._tab = tab;
             this._mask = mask;
         }
@@ -144,6 +153,7 @@ class KmerMap extends Map {
 
     clear() {
         this._n = 0;
+        this._buf = null;
         this._ndel = 0;
         this._all = '';
         this._tab = null;

@@ -7,6 +7,7 @@
 //   open(k, prefixBuffer, step, device, flags, maxKeys, batchBytes, devices[]) -> handle
 //     (devices: >= 2 HIP ordinals -> a multi-GPU group context, kmer_params.ndev)
 //   countFile(handle, path, cb(err, {keys, offsets, counts, lines}), progress(done, total)?)
+//   indexKeys(keysBuffer, offsetsFloat64Array, n, cap) -> Int32Array (KmerMap index)
 //   countBuffer(handle, buffer, cb(err, {...}), progress(done, total)?)
 //     (progress: called on the JS thread after each input batch, kmer_params.progress)
 //   close(handle)
@@ -638,6 +639,65 @@ napi_value MatchClose(napi_env env, napi_callback_info info) {
     return u;
 }
 
+// indexKeys(keys Buffer, offsets Float64Array, n, cap) -> Int32Array(cap): the
+// KmerMap's key -> packed index table (kmer_map.js _index): open addressing,
+// FNV-1a over the key bytes (the Latin-1 character codes), linear probing,
+// -1 = empty.  The same table the JS loop builds, without a per-character
+// charCodeAt (C2: 1.96 M keys).
+napi_value IndexKeys(napi_env env, napi_callback_info info) {
+    size_t argc = 4;
+    napi_value argv[4];
+    NAPI_CALL(env, napi_get_cb_info(env, info, &argc, argv, nullptr, nullptr));
+    bool isbuf = false;
+    if (argc >= 4) napi_is_buffer(env, argv[0], &isbuf);
+    napi_typedarray_type tt = napi_int8_array;
+    size_t olen = 0;
+    void *od = nullptr;
+    if (!isbuf || napi_get_typedarray_info(env, argv[1], &tt, &olen, &od, nullptr, nullptr) != napi_ok ||
+        tt != napi_float64_array) {
+        napi_throw_type_error(env, nullptr, "indexKeys(keys Buffer, offsets Float64Array, n, cap)");
+        return nullptr;
+    }
+    void *kd = nullptr;
+    size_t klen = 0;
+    NAPI_CALL(env, napi_get_buffer_info(env, argv[0], &kd, &klen));
+    double n = 0, cap = 0;
+    napi_get_value_double(env, argv[2], &n);
+    napi_get_value_double(env, argv[3], &cap);
+    const double *off = static_cast<const double *>(od);
+    const uint64_t cn = (uint64_t)cap;
+    if (n < 0 || (size_t)n + 1 > olen || cn == 0 || (cn & (cn - 1)) || cn < (uint64_t)n + 1 ||
+        cn > 0x7FFFFFFFull || (n > 0 && off[(size_t)n] > (double)klen)) {
+        napi_throw_range_error(env, nullptr, "indexKeys: bad sizes");
+        return nullptr;
+    }
+    napi_value ab, ta;
+    void *data = nullptr;
+    NAPI_CALL(env, napi_create_arraybuffer(env, cn * 4, &data, &ab));
+    int32_t *tab = static_cast<int32_t *>(data);
+    memset(tab, 0xFF, cn * 4);
+    const uint8_t *keys = static_cast<const uint8_t *>(kd);
+    const uint32_t mask = (uint32_t)(cn - 1);
+    // hashes first (a sequential pass), then the inserts with the home slots
+    // prefetched a few keys ahead (the table is far larger than the caches)
+    const size_t nn = (size_t)n;
+    std::vector<uint32_t> hv(nn);
+    for (size_t i = 0; i < nn; ++i) {
+        uint32_t h = 0x811c9dc5u;
+        for (uint64_t j = (uint64_t)off[i]; j < (uint64_t)off[i + 1]; ++j) h = (h ^ keys[j]) * 16777619u;
+        hv[i] = h & mask;
+    }
+    constexpr size_t AHEAD = 16;
+    for (size_t i = 0; i < nn; ++i) {
+        if (i + AHEAD < nn) __builtin_prefetch(tab + hv[i + AHEAD], 1);
+        uint32_t h = hv[i];
+        while (tab[h] != -1) h = (h + 1) & mask;
+        tab[h] = (int32_t)i;
+    }
+    NAPI_CALL(env, napi_create_typedarray(env, napi_int32_array, cn, ab, 0, &ta));
+    return ta;
+}
+
 // KMERHIP_SEGV_TRACE=1 (diagnostics): a backtrace on stderr for a fatal signal
 void segv_trace(int sig) {
     void *fr[64];
@@ -670,6 +730,7 @@ napi_value Init(napi_env env, napi_value exports) {
         {"matchRemove", nullptr, MatchRemove, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"matchRemoved", nullptr, MatchRemoved, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
         {"matchClose", nullptr, MatchClose, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
+        {"indexKeys", nullptr, IndexKeys, nullptr, nullptr, nullptr, napi_enumerable, nullptr},
     };
     napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
     return exports;

@@ -222,7 +222,7 @@ class KmerJS {
                 }
                 try {
                     if (kmerObj.kmerMap.size === 0 && !(kmerObj.kmerMap instanceof KmerMap)) {
-                        kmerObj.kmerMap = KmerMap.fromNative(res);      // built lazily (kmer_map.js)
+                        kmerObj.kmerMap = KmerMap.fromNative(res, native().indexKeys);   // built lazily (kmer_map.js)
                     } else {
                         foldResult(kmerObj.kmerMap, res);
                         if (kmerObj.kmerMap.size > kmerObj.maxKeys) throw tooManyKeys('Map maximum size exceeded');

@@ -119,6 +119,26 @@ function cpuTests() {
         assert.ok(!km._packedOnly());
         assert.strictEqual([...km.keys()][7], uniq[8]);
     });
+    check('native KmerMap index (indexKeys) = the JS table; same Map semantics', () => {
+        const n = 20000;
+        const keys = [];
+        for (let i = 0; i < n; i += 1) keys.push('AC' + ((i * 40503 + 7) >>> 0).toString(4).padStart(9, 'G') + '\xe9\r'.slice(0, i % 3));
+        const uniq = [...new Set(keys)];
+        const buf = Buffer.from(uniq.join(''), 'latin1');
+        const off = new Float64Array(uniq.length + 1);
+        for (let i = 0; i < uniq.length; i += 1) off[i + 1] = off[i] + uniq[i].length;
+        const cnt = new Float64Array(uniq.length).map((_, i) => i + 1);
+        const res = { keys: buf, offsets: off, counts: cnt };
+        const js = lib.KmerMap.fromNative(res);
+        const nat = lib.KmerMap.fromNative(res, lib.native().indexKeys);
+        assert.deepStrictEqual(nat._index(), js._index());
+        for (let i = 0; i < uniq.length; i += 37) assert.strictEqual(nat.get(uniq[i]), i + 1);
+        assert.strictEqual(nat.get('ACZ'), undefined);
+        nat.set(uniq[3], 0); nat.delete(uniq[4]); nat.set('new', 1);
+        assert.deepStrictEqual([...nat].slice(2, 5), [[uniq[2], 3], [uniq[3], 0], [uniq[5], 6]]);
+        assert.deepStrictEqual([...nat].pop(), ['new', 1]);
+        assert.throws(() => lib.native().indexKeys(buf, off, uniq.length, 3), RangeError);
+    });
     check('legacy npm main (lib/index.js) exports and fields', () => {
         const legacy = require(path.join(repo, 'kmerjs_amd', 'node', 'index.js'));
         for (const name of ['kmers', 'complement', 'KmerJSClient', 'KmerJSServer']) assert.ok(name in legacy, name);
