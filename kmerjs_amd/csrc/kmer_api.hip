@@ -2402,8 +2402,8 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
         c->mode = MODE_TABLE;
     else if (dense_ok && (plen == 0 ? k <= 31 : (acgt && plen <= 3 && k <= (uint32_t)KMAX_DENSE)))
         c->mode = MODE_WINDOWS;
-    else if (dense_ok && acgt && k <= (uint32_t)KMAX_TILE)
-        c->mode = MODE_PACKED;                  // (k > 32: 128-bit window codes)
+    else if (dense_ok && plen > 0 && k <= (uint32_t)KMAX_TILE)
+        c->mode = MODE_PACKED;                  // (k > 32: 128-bit window codes; any prefix bytes: key = P + suffix code)
     else if (pp->step == 1 && plen > 0 && k <= (uint32_t)KMAX_TILE)
         c->mode = MODE_TILE_REC;
     else

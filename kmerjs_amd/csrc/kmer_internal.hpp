@@ -208,7 +208,7 @@ struct EmitArgs {
     uint64_t *nuniq;
     uint64_t *nuniq_host;          // mapped host copy of *nuniq (or null)
     uint32_t k, plen, partial;
-    uint8_t P[32];
+    uint8_t P[KMAX_TILE];          // the prefix (|P| <= k <= 64 on the packed paths)
     uint8_t *keys_out;             // decode: n * k bytes
     uint64_t *cnt_out, *first_out;
     uint64_t *ukey;                // partial: suffix codes

@@ -416,7 +416,18 @@ __device__ __forceinline__ int last_newline_in_chunk(const uint8_t *buf, int c, 
 // THREAD_MAP: sh.nlmap holds one bit per 64-byte thread region (plane
 // kernel; chunks inside a region are resolved through cpre), else one bit per
 // 16-byte chunk (byte kernel).
-// WIDE: k > 32 (the window's first k - 32 bases go to hits_hi / ovf_hi)
+// bytes [from, to) of a 32-bit word (clamped to 0..4)
+__device__ __forceinline__ uint32_t byte_range_mask(int from, int to) {
+    from = from < 0 ? 0 : from > 4 ? 4 : from;
+    to = to < 0 ? 0 : to > 4 ? 4 : to;
+    const uint32_t a = to >= 4 ? ~0u : (1u << (8 * to)) - 1u, b = from >= 4 ? ~0u : (1u << (8 * from)) - 1u;
+    return a & ~b;
+}
+
+// WIDE: k > 32 (the window's first k - 32 bases go to hits_hi / ovf_hi).
+// !THREAD_MAP (the byte kernel, which also serves non-ACGT prefixes): only the
+// suffix bytes decide `exotic` -- the key is P + the suffix's 2-bit code, so a
+// prefix may hold any bytes
 template <bool THREAD_MAP, bool WIDE>
 __device__ __forceinline__ void emit_hit(const ScanArgs &a, const uint8_t *buf, ScanShared &sh, uint32_t tile,
                                       uint32_t e) {
@@ -427,6 +438,7 @@ __device__ __forceinline__ void emit_hit(const ScanArgs &a, const uint8_t *buf, 
     // window bytes: ACGT check (v_perm against "ACGT"), '\n' check, 2-bit codes
     bool exotic = false, hasnl = false;
     uint64_t code = 0;
+    const int sfx0 = strand ? 0 : (int)plen, sfx1 = strand ? (int)(k - plen) : (int)k;   // suffix bytes
 #pragma unroll 4
     for (uint32_t b = 0; b < k; b += 4) {
         const uint32_t x = lds_word(buf, s0 + (int)b);
@@ -434,7 +446,8 @@ __device__ __forceinline__ void emit_hit(const ScanArgs &a, const uint8_t *buf, 
         const uint32_t mk = nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
         const uint32_t c = ((x >> 1) ^ (x >> 2)) & 0x03030303u;
         const uint32_t expect = __builtin_amdgcn_perm(0u, 0x54474341u, c);   // "ACGT"[c] per byte
-        exotic |= ((expect ^ x) & mk) != 0;
+        const uint32_t mx = THREAD_MAP ? mk : mk & byte_range_mask(sfx0 - (int)b, sfx1 - (int)b);
+        exotic |= ((expect ^ x) & mx) != 0;
         hasnl |= (nl_flags(x) & mk) != 0;
         const uint32_t pk = ((c & 3u) << 6) | (((c >> 8) & 3u) << 4) | (((c >> 16) & 3u) << 2) |
                             ((c >> 24) & 3u);                // first byte most significant

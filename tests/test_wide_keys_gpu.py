@@ -65,6 +65,39 @@ def test_wide_with_n_batches_and_records_path(native):
             assert first_diff(got, want) is None, (k, p, flags, batch)
 
 
+def test_long_prefix_present_in_the_data(native, synth):
+    # a 34-byte prefix cut from the input (so that it occurs): the emitted keys
+    # carry all of it (|P| > 32)
+    from oracle import oracle
+    buf, host = synth
+    line = host.split(b"\n")[1]
+    for k, p in ((40, line[10:44]), (64, line[20:60]), (36, line[5:37])):
+        want = oracle.count_buffer(host, p, k, 1)
+        ctr = native.Counter(k=k, prefix=p)
+        got = ctr.count_buffer(host).entries()
+        ctr.close()
+        assert len(want) > 0 and first_diff(got, want) is None, (k, p)
+
+
+def test_non_acgt_prefixes_on_the_packed_path(native):
+    # the key is P + the suffix's 2-bit code, so a prefix of any bytes stays on
+    # the device (non-ACGT suffixes are records); reads with N at p = 0.02
+    from oracle import oracle
+    rng = np.random.default_rng(21)
+    arr = np.frombuffer(bytearray(oracle.synth_fastq(4, 0, 20000)), dtype=np.uint8).reshape(-1, 317).copy()
+    seq = arr[:, 13:163]
+    seq[rng.random(seq.shape) < 0.02] = ord("N")
+    arr[:, 13:163] = seq
+    data = arr.tobytes()
+    for k, p in ((16, b"N"), (16, b"NA"), (21, b"AN"), (40, b"NAC"), (12, b"GNT"), (16, b"X"), (8, b"NNNN"),
+                 (33, b"N"), (16, b"@s")):
+        want = oracle.count_buffer(data, p, k, 1)
+        ctr = native.Counter(k=k, prefix=p)
+        got = ctr.count_buffer(data).entries()
+        ctr.close()
+        assert first_diff(got, want) is None, (k, p, len(got), len(want))
+
+
 def test_wide_group_and_partials(native):
     from oracle import oracle
     data = oracle.synth_fastq(8, 0, 30000)
