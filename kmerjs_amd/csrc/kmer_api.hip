@@ -454,7 +454,6 @@ void bind_hits(kmer_ctx *c, HitArgs &h) {
     h.rkey = c->rkey.p;
     h.rkey32 = c->narrow ? c->rkey32.p : nullptr;
     h.rord = c->rord.p;
-    h.ridx = c->ridx.p;
     h.xord = c->xord.p;
     h.xkey = c->xkey.p;
     h.xslot = c->xslot.p;
@@ -834,7 +833,7 @@ kmer_status chunk_lines(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_
     if (n_seq) {
         HIPCHK(c, c->lines.ensure(n_seq, s));
         HIPCHK(c, c->wcount.ensure(n_seq, s));
-        HIPCHK(c, launch_seq_lines(c->nlpos.p, n_nl, len, li0, n_seq, c->p.k, c->lines.p, c->wcount.p,
+        HIPCHK(c, launch_seq_lines(c->nlpos.p, n_nl, len, li0, n_seq, c->p.k, c->p.step, c->lines.p, c->wcount.p,
                                    check_len ? c->d_err : nullptr, (1ull << c->pbits) - 1ull, s));
     }
     *n_nl_out = n_nl;
@@ -886,22 +885,27 @@ kmer_status windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n
     auto code = [](char ch) -> uint64_t { return ch == 'A' ? 0u : ch == 'C' ? 1u : ch == 'G' ? 2u : 3u; };
     for (char ch : c->prefix) w.pcode = (w.pcode << 2) | code(ch);
     for (char ch : c->rprefix) w.rcode = (w.rcode << 2) | code(ch);
+    w.step = c->p.step;
     w.smask = (c->kbits >= 64) ? ~0ull : ((1ull << c->kbits) - 1ull);
     w.invalid_key = c->kbits >= 63 ? ~0ull : (1ull << c->kbits);
     w.out_base = c->n_hits;
     w.rkey = c->rkey.p;
     w.rkey32 = c->narrow ? c->rkey32.p : nullptr;
     w.rord = c->rord.p;
-    w.ridx = c->ridx.p;
     w.err = c->d_err;
+    w.empty = (unsigned long long *)(c->d_scal + 10);
+    w.P = c->d_P;
     for (int attempt = 0; attempt < 8; ++attempt) {
         w.recs = c->recs.p;
         w.rec_count = c->d_rec_count;
         w.rec_cap = c->recs.cap;
         HIPCHK(c, hipMemsetAsync(c->d_rec_count, 0, 8, s));
+        HIPCHK(c, hipMemsetAsync(c->d_scal + 10, 0, 8, s));
+        HIPCHK(c, hipMemsetAsync(c->d_scal + 11, 0xFF, 8, s));
         HIPCHK(c, launch_windows_packed(w, s));
         HIPCHK(c, hipEventRecord(c->ev1, s));
         HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 18, c->d_scal + 10, 2 * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
         const uint32_t e = (uint32_t)c->h_small[5];
         st = check_err(c, e);
@@ -919,6 +923,15 @@ kmer_status windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n
     }
     c->n_hits += total;
     c->chunk_open = c->h_small[7] != 0;
+    if (c->h_small[18]) {                        // step > 1, no prefix: the empty substrings' key ""
+        auto it = c->exotic.find(std::string());
+        if (it == c->exotic.end()) {
+            c->exotic.emplace(std::string(), Ent{c->h_small[18], c->h_small[19]});
+        } else {
+            it->second.count += c->h_small[18];
+            it->second.first = std::min(it->second.first, c->h_small[19]);
+        }
+    }
     const uint64_t nrec = c->h_small[0];
     if (nrec) {
         st = drain_records(c, d, nrec, s);
@@ -2392,6 +2405,8 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
     bool acgt = plen > 0;
     for (char ch : c->prefix) acgt &= ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T';
     const bool dense_ok = !(pp->flags & KMER_FLAG_NO_DENSE) && pp->step == 1 && plen <= k;
+    const bool win_step = !(pp->flags & KMER_FLAG_NO_DENSE) && pp->step > 1 && plen <= k &&
+                          (plen == 0 ? k <= 31 : (acgt && k <= (uint32_t)KMAX_DENSE));
     if ((pp->flags & KMER_FLAG_CANONICAL) &&
         !(pp->step == 1 && plen <= k && k <= (uint32_t)KMAX_PACKED && (plen == 0 || acgt))) {
         delete c;                               // (canonical counts exist in table mode only)
@@ -2402,6 +2417,8 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
         c->mode = MODE_TABLE;
     else if (dense_ok && (plen == 0 ? k <= 31 : (acgt && plen <= 3 && k <= (uint32_t)KMAX_DENSE)))
         c->mode = MODE_WINDOWS;
+    else if (win_step)
+        c->mode = MODE_WINDOWS;                 // step > 1: every stepped window ranked (the tile scan has no line ends)
     else if (dense_ok && plen > 0 && k <= (uint32_t)KMAX_TILE)
         c->mode = MODE_PACKED;                  // (k > 32: 128-bit window codes; any prefix bytes: key = P + suffix code)
     else if (pp->step == 1 && plen > 0 && k <= (uint32_t)KMAX_TILE)

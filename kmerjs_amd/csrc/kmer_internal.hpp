@@ -168,7 +168,6 @@ struct HitArgs {
     uint64_t *rkey;                // by rank: suffix code (invalid_key: filtered / record)
     uint32_t *rkey32;              // ... as u32 when 2(k-|P|) + 1 <= 32 (then rkey is unused)
     uint64_t *rord;                // by rank: first-occurrence order key
-    uint32_t *ridx;                // by rank: the rank itself (sort payload)
     uint64_t *xord, *xkey;         // cross list in natural-slot order (order, key, natural slot)
     uint32_t *xslot;
     uint64_t xbase, xcap;          // session cross entries before this chunk, capacity
@@ -274,13 +273,15 @@ struct WinArgs {
     const uint64_t *wbase;         // by sequence ordinal: rank of the line's first window (chunk-relative)
     uint32_t k, plen;
     uint32_t pbits;                // order-key position bits (PBITS_*)
+    uint32_t step;                 // windows at 0, step, 2 step, ... of the line and of its complement
+    unsigned long long *empty;     // step > 1, no prefix: [0] empty keys "" counted, [1] min order key of one
+    const uint8_t *P;              // device copy of the prefix (cut-short windows of step > 1)
     uint64_t pcode, rcode;         // P and rc(P) as 2-bit codes (first base most significant)
     uint64_t smask, invalid_key;
     uint64_t out_base;
     uint64_t *rkey;
     uint32_t *rkey32;
     uint64_t *rord;
-    uint32_t *ridx;
     Record *recs;
     unsigned long long *rec_count;
     uint64_t rec_cap;
@@ -358,8 +359,10 @@ hipError_t launch_nl_count(const uint8_t *data, uint64_t len, uint32_t n_tiles, 
                            hipStream_t s);
 hipError_t launch_nl_write(const uint8_t *data, uint64_t len, uint32_t n_tiles, const uint64_t *tbase, uint64_t *nl,
                            hipStream_t s);
+// wcount = windows of both strands per sequence line: 2 ceil(W / step)
 hipError_t launch_seq_lines(const uint64_t *nl, uint64_t n_nl, uint64_t len, uint64_t li0, uint64_t n_seq, uint32_t k,
-                            SeqLine *lines, uint64_t *wcount, unsigned int *err, uint64_t maxrel, hipStream_t s);
+                            uint32_t step, SeqLine *lines, uint64_t *wcount, unsigned int *err, uint64_t maxrel,
+                            hipStream_t s);
 hipError_t launch_pos_after(StreamPos *pos, uint64_t lines, const uint8_t *data, uint64_t len,
                             unsigned long long *ends_open, hipStream_t s);
 hipError_t launch_windows_packed(const WinArgs &a, hipStream_t s);

@@ -1130,7 +1130,7 @@ __device__ __forceinline__ uint64_t resolve_hit(const HitArgs &a, const HitRec &
 // Write one resolved packed hit at its rank slot, or to the cross list.
 __device__ __forceinline__ void place_hit(const HitArgs &a, uint64_t slot, bool cross, uint64_t xi, uint64_t key,
                                           uint64_t key_hi, uint64_t order) {
-    a.ridx[slot] = (uint32_t)slot;
+    // (no rank payload: the finish sorts (key, iota))
     if (!cross) {
         if (a.rkey32) a.rkey32[slot] = (uint32_t)key;
         else a.rkey[slot] = key;
@@ -1525,13 +1525,14 @@ __device__ __forceinline__ uint64_t window_code(const uint8_t *p, uint32_t k, bo
     return code;
 }
 
-__device__ __forceinline__ void win_record(const WinArgs &a, uint64_t order, uint64_t pos, uint32_t strand) {
+__device__ __forceinline__ void win_record(const WinArgs &a, uint64_t order, uint64_t pos, uint32_t strand,
+                                           uint32_t len) {
     const unsigned long long n = atomicAdd(a.rec_count, 1ull);
     if (n < a.rec_cap) {
         Record rec;
         rec.order = order;
         rec.pos = pos;
-        rec.len = a.k;
+        rec.len = len;
         rec.strand = strand;
         a.recs[n] = rec;
     } else {
@@ -1543,7 +1544,6 @@ __device__ __forceinline__ void win_place(const WinArgs &a, uint64_t rank, uint6
     if (a.rkey32) a.rkey32[rank] = (uint32_t)key;
     else a.rkey[rank] = key;
     a.rord[rank] = order;
-    a.ridx[rank] = (uint32_t)rank;
 }
 
 // ---- sequence lines of a chunk without look-back (dense-hit path) ----
@@ -1621,7 +1621,8 @@ __global__ __launch_bounds__(256) void nl_write_kernel(const uint8_t *data, uint
 
 // sequence ordinal m -> SeqLine (len 0: no windows) and its window count 2W
 __global__ __launch_bounds__(256) void seq_lines_kernel(const uint64_t *nl, uint64_t n_nl, uint64_t len,
-                                                        uint64_t li0, uint64_t n_seq, uint32_t k, SeqLine *lines,
+                                                        uint64_t li0, uint64_t n_seq, uint32_t k, uint32_t step,
+                                                        SeqLine *lines,
                                                         uint64_t *wcount, unsigned int *err, uint64_t maxrel) {
     const uint32_t lsh = 64 - __popcll(maxrel);            // line index bits: 63 - pbits
     const uint64_t first = (1u - (uint32_t)li0) & 3u;      // first sequence line, relative to li0
@@ -1642,7 +1643,7 @@ __global__ __launch_bounds__(256) void seq_lines_kernel(const uint64_t *nl, uint
                 const uint64_t W = L - k + 1;
                 // (err null: no order key, no limit)
                 if (err && (W - 1 > maxrel || (sl.line_index >> (lsh - 1)))) atomicOr(err, ERR_LINE_TOO_LONG);
-                w2 = 2 * W;
+                w2 = 2 * ((W + step - 1) / step);
             }
         }
         lines[m] = sl;
@@ -1659,7 +1660,14 @@ __global__ void pos_after_kernel(StreamPos *pos, uint64_t lines, const uint8_t *
     }
 }
 
-// one workgroup per sequence line (grid-stride), one thread per window
+// one workgroup per sequence line (grid-stride), one thread per forward
+// position s: the forward window at s when s % step == 0 and the reverse
+// strand's window at p = W - 1 - s when p % step == 0.  lib/kmers.js:88-100
+// steps through the line and through its complement from their own starts,
+// W times (index j, ini = j * step): past L - k the substring is cut short,
+// past L it is "" -- the short keys become records, the empty ones a count.
+// Order keys: step 1, line | strand | (strand ? maxrel - s : s) as on the
+// tile path; step > 1, line | strand | j (the loop index) on both strands.
 __global__ __launch_bounds__(256) void windows_packed_kernel(WinArgs a) {
     const uint32_t k = a.k, plen = a.plen;
     const uint32_t tailbits = 2 * (k - plen);
@@ -1671,12 +1679,17 @@ __global__ __launch_bounds__(256) void windows_packed_kernel(WinArgs a) {
         if (W - 1 > maxrel) continue;            // reported by seq_lines_kernel
         const uint64_t base = a.out_base + a.wbase[li];
         const uint64_t lo = sl.line_index << (a.pbits + 1);
+        const uint32_t step = a.step;
+        const uint64_t Ws = (W + step - 1) / step;   // windows per strand
         for (uint64_t s = threadIdx.x; s < W; s += blockDim.x) {
+            const bool fw = step == 1 || s % step == 0, rv = step == 1 || (W - 1 - s) % step == 0;
+            if (!fw && !rv) continue;
             const uint64_t pos = sl.start + s;
             bool exotic;
             const uint64_t code = window_code(a.data + pos, k, pos + k + 4 <= a.len, &exotic);
             const uint64_t rc = revcomp_code(code, k);
-            const uint64_t of = lo | s, orr = lo | (1ull << a.pbits) | (maxrel - s);
+            const uint64_t of = lo | (step == 1 ? s : s / step);
+            const uint64_t orr = lo | (1ull << a.pbits) | (step == 1 ? maxrel - s : (W - 1 - s) / step);
             // prefix tests on the codes: a non-ACGT byte in the prefix bases never
             // matches (its code aliases, so exotic windows re-check the bytes)
             bool mf = plen == 0 || (code >> tailbits) == a.pcode;
@@ -1691,12 +1704,37 @@ __global__ __launch_bounds__(256) void windows_packed_kernel(WinArgs a) {
                     mr = mr && xr == (uint8_t)((0x54474341u >> (8 * cr)) & 0xFFu);
                 }
             }
-            const uint64_t rf = base + s, rr = base + W + (W - 1 - s);
-            win_place(a, rf, (mf && !exotic) ? (code & a.smask) : a.invalid_key, of);
-            win_place(a, rr, (mr && !exotic) ? (rc & a.smask) : a.invalid_key, orr);
+            const uint64_t rf = base + s / step, rr = base + Ws + (W - 1 - s) / step;
+            if (fw) win_place(a, rf, (mf && !exotic) ? (code & a.smask) : a.invalid_key, of);
+            if (rv) win_place(a, rr, (mr && !exotic) ? (rc & a.smask) : a.invalid_key, orr);
             if (exotic) {
-                if (mf) win_record(a, of, pos, 0);
-                if (mr) win_record(a, orr, pos, 1);
+                if (mf && fw) win_record(a, of, pos, 0, k);
+                if (mr && rv) win_record(a, orr, pos, 1, k);
+            }
+        }
+        if (step == 1 || Ws >= W) continue;
+        // indices j in [Ws, W) of each strand: p = j * step > L - k
+        const uint64_t L = sl.len, ntail = W - Ws;
+        for (uint64_t t = threadIdx.x; t < 2 * ntail; t += blockDim.x) {
+            const uint32_t strand = t >= ntail ? 1u : 0u;
+            const uint64_t j = Ws + (strand ? t - ntail : t), p = j * step;
+            if (p >= L) continue;                    // "": counted below
+            const uint64_t len = L - p;              // (< k)
+            if (len < plen) continue;
+            bool ok = true;
+            for (uint32_t b = 0; b < plen && ok; ++b) {
+                const uint8_t c = strand ? comp_byte(a.data[sl.start + L - 1 - p - b]) : a.data[sl.start + p + b];
+                ok = c == a.P[b];
+            }
+            // the reverse strand's S[p, L) is rc of the line's first L - p bytes
+            if (ok) win_record(a, lo | ((uint64_t)strand << a.pbits) | j, sl.start + (strand ? 0 : p), strand,
+                               (uint32_t)len);
+        }
+        if (plen == 0 && threadIdx.x == 0) {
+            const uint64_t j0 = (L + step - 1) / step;   // first index whose substring is ""
+            if (j0 < W) {
+                atomicAdd(&a.empty[0], (unsigned long long)(2 * (W - j0)));
+                atomicMin(&a.empty[1], (unsigned long long)(lo | j0));
             }
         }
     }
@@ -2556,10 +2594,11 @@ hipError_t launch_nl_write(const uint8_t *data, uint64_t len, uint32_t n_tiles, 
     return hipGetLastError();
 }
 hipError_t launch_seq_lines(const uint64_t *nl, uint64_t n_nl, uint64_t len, uint64_t li0, uint64_t n_seq, uint32_t k,
-                            SeqLine *lines, uint64_t *wcount, unsigned int *err, uint64_t maxrel, hipStream_t s) {
+                            uint32_t step, SeqLine *lines, uint64_t *wcount, unsigned int *err, uint64_t maxrel,
+                            hipStream_t s) {
     if (n_seq)
-        hipLaunchKernelGGL(seq_lines_kernel, dim3(grid_for(n_seq)), dim3(256), 0, s, nl, n_nl, len, li0, n_seq, k, lines,
-                           wcount, err, maxrel);
+        hipLaunchKernelGGL(seq_lines_kernel, dim3(grid_for(n_seq)), dim3(256), 0, s, nl, n_nl, len, li0, n_seq, k, step,
+                           lines, wcount, err, maxrel);
     return hipGetLastError();
 }
 hipError_t launch_pos_after(StreamPos *pos, uint64_t lines, const uint8_t *data, uint64_t len,
