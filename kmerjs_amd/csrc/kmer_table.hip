@@ -18,8 +18,11 @@
 //           input (1.3 B/window, cheaper than a key buffer), ranks each key in
 //           its partition with an LDS atomic, sorts a round of 16 K keys in LDS
 //           and writes each partition's run contiguously.
-//   pass 2  per run of a partition: the next 10 bits, same LDS sort -> B2 in
-//           2^20 buckets, contiguous per bucket.
+//   pass 2  per run of a partition: the next 10 bits, LDS sort in rounds of
+//           8 K keys -> B2 in 2^20 buckets, contiguous per bucket; each round
+//           writes a bucket's keys only up to its last 64-B boundary and
+//           carries the rest into the next round (whole blocks, no partial
+//           lines left behind).
 //   final   one persistent workgroup per CU, unit by unit (a bucket, or a
 //           group of small buckets): a counting sort of the unit's keys into
 //           4,096 LDS bins and a per-thread dedupe of adjacent bins; crowded
@@ -27,6 +30,8 @@
 //           atomic count) with ranges split and redone when they do not fit.
 //           Entries (remainder, count) are written back to the bucket's range;
 //           Map statistics on the fly.
+#include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "kmer_internal.hpp"
@@ -439,6 +444,91 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2_kernel(const uint64_t *B
 #endif
         __syncthreads();
         cur[t] += my_st + cnt;
+        bcnt[t] = 0;
+        __syncthreads();
+    }
+}
+
+// pass 2, scatter with aligned write-out: rounds of 8 K keys; each bucket's
+// keys of a round go out only up to the last 64-B boundary of its B2 range
+// (8 keys), the rest (<= 7 keys) is carried in the bucket owner's registers
+// into the next round's LDS sort.  A round then writes whole 64-B blocks
+// (besides the first, partial block of each (unit, bucket) range) instead of
+// ~16-key runs that straddle lines, which left partial L2 lines to be evicted
+// before the next round completed them.  Thread t owns bucket t; bucket
+// order inside a range is free (table mode has no order).
+constexpr int TS2_RPL = 8;
+constexpr int TS2_ROUND = TS2_RPL * TAB_WG1;           // new keys per round
+constexpr int TS2_CARRY = 7;                           // carried keys per bucket (< one 64-B block)
+__global__ __launch_bounds__(TAB_WG1) void tab_scatter2c_kernel(const uint64_t *B1, const TabUnit *units,
+                                                                const uint64_t *H2s, uint64_t *B2) {
+    __shared__ uint64_t srt[TS2_ROUND + TS2_CARRY * TAB_WG1];
+    __shared__ uint64_t cur[TAB_NB];
+    __shared__ uint32_t bcnt[TAB_NB], bst[TAB_NB];
+    __shared__ uint32_t ws[16];
+    const uint32_t t = threadIdx.x;
+    const TabUnit un = units[blockIdx.x];
+    const uint64_t *src = B1 + un.start;
+    uint64_t dest = H2s[un.hbase + (uint64_t)t * un.nunits + un.u];   // next B2 slot of bucket t
+    cur[t] = dest;
+    bcnt[t] = 0;
+    uint32_t cc = 0;                               // carried keys of bucket t
+    uint64_t ck[TS2_CARRY];
+#pragma unroll
+    for (int i = 0; i < TS2_CARRY; ++i) ck[i] = 0;
+    __syncthreads();
+    uint64_t key[TS2_RPL];
+#pragma unroll
+    for (int j = 0; j < TS2_RPL; ++j) {
+        const uint32_t i = j * TAB_WG1 + t;
+        key[j] = i < un.len ? src[i] : 0;
+    }
+    for (uint32_t r0 = 0; r0 < un.len; r0 += TS2_ROUND) {
+        const bool last = r0 + TS2_ROUND >= un.len;
+        uint32_t rank[TS2_RPL];
+#pragma unroll
+        for (int j = 0; j < TS2_RPL; ++j) {
+            const uint32_t i = r0 + j * TAB_WG1 + t;
+            rank[j] = i < un.len ? atomicAdd(&bcnt[(uint32_t)(key[j] >> TAB_RBITS) & (TAB_NB - 1)], 1u) : 0u;
+        }
+        __syncthreads();
+        const uint32_t n_new = bcnt[t], tot = n_new + cc;
+        uint32_t total;
+        const uint32_t my_st = block_excl_1024(tot, ws, &total);
+        // keys of bucket t written this round: up to the last 64-B boundary
+        const uint64_t aend = last ? dest + tot : ((dest + tot) & ~7ull);
+        const uint32_t full = aend > dest ? (uint32_t)(aend - dest) : 0u;
+        bst[t] = my_st;
+        cur[t] = dest - my_st;                    // (write-out: B2[cur[b] + i] for i < bst[b] + full)
+        __syncthreads();
+        // this round's keys first, then the carried ones
+#pragma unroll
+        for (int j = 0; j < TS2_RPL; ++j) {
+            const uint32_t i = r0 + j * TAB_WG1 + t;
+            if (i < un.len) srt[bst[(uint32_t)(key[j] >> TAB_RBITS) & (TAB_NB - 1)] + rank[j]] = key[j];
+        }
+#pragma unroll
+        for (int i = 0; i < TS2_CARRY; ++i)
+            if ((uint32_t)i < cc) srt[my_st + n_new + i] = ck[i];
+        bcnt[t] = my_st + full;                   // (write-out limit of bucket t)
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < TS2_RPL; ++j) {
+            const uint32_t i = r0 + TS2_ROUND + j * TAB_WG1 + t;
+            key[j] = i < un.len ? src[i] : 0;
+        }
+        for (uint32_t i = t; i < total; i += TAB_WG1) {
+            const uint64_t h = srt[i];
+            const uint32_t b = (uint32_t)(h >> TAB_RBITS) & (TAB_NB - 1);
+            if (i < bcnt[b]) B2[cur[b] + i] = h;
+        }
+        // the rest of bucket t is carried
+        cc = tot - full;
+#pragma unroll
+        for (int i = 0; i < TS2_CARRY; ++i)
+            if ((uint32_t)i < cc) ck[i] = srt[my_st + full + i];
+        dest += full;
+        __syncthreads();
         bcnt[t] = 0;
         __syncthreads();
     }
@@ -1296,7 +1386,15 @@ hipError_t launch_tab_hist2(const uint64_t *B1, const TabUnit *units, uint32_t n
 
 hipError_t launch_tab_scatter2(const uint64_t *B1, const TabUnit *units, uint32_t n_units, const uint64_t *H2s,
                                uint64_t *B2, hipStream_t s) {
-    hipLaunchKernelGGL(tab_scatter2_kernel, dim3(n_units), dim3(TAB_WG1), 0, s, B1, units, H2s, B2);
+    // KMERHIP_TAB_S2=plain: the 16 K-round kernel without aligned write-out (A/B experiments)
+    static const bool plain = [] {
+        const char *e = getenv("KMERHIP_TAB_S2");
+        return e && strcmp(e, "plain") == 0;
+    }();
+    if (plain)
+        hipLaunchKernelGGL(tab_scatter2_kernel, dim3(n_units), dim3(TAB_WG1), 0, s, B1, units, H2s, B2);
+    else
+        hipLaunchKernelGGL(tab_scatter2c_kernel, dim3(n_units), dim3(TAB_WG1), 0, s, B1, units, H2s, B2);
     return hipGetLastError();
 }
 
