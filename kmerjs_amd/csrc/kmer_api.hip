@@ -119,7 +119,8 @@ struct kmer_ctx {
     DBuf<TileSum> tsum, tscan, bsum, bscan;
     DBuf<uint64_t> wcount, wbase;  // dense-hit path: windows / first rank per sequence line
     DBuf<uint32_t> tcount;         // dense-hit path: '\n' per tile
-    DBuf<uint64_t> tbase, nlpos;   // ... exclusive scan, chunk-relative '\n' positions
+    DBuf<uint64_t> tbase, nlpos;   // ... exclusive scan, chunk-relative '\n' positions (or sequence-line bounds)
+    DBuf<uint16_t> nlslots;        // tile-relative '\n' positions, NL_SLOTS per tile
     uint64_t host_lines = 0;       // StreamPos.lines as last seen by the host (dense-hit path)
     DBuf<HitRec> hits, ovf;
     DBuf<uint64_t> hits_hi, ovf_hi;   // k > 32: the first k - 32 bases of each hit record's window
@@ -814,27 +815,52 @@ kmer_status general_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n
 kmer_status chunk_lines(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s, bool check_len,
                         uint64_t *n_nl_out, uint64_t *n_seq_out) {
     const uint64_t li0 = c->host_lines;
+    // one pass over the input: per-tile counts + positions in per-tile slots
+    // (KMERHIP_NL=two: the count pass + a second, writing pass; A/B experiments)
+    static const bool two = [] {
+        const char *e = getenv("KMERHIP_NL");
+        return e && strcmp(e, "two") == 0;
+    }();
     HIPCHK(c, c->tcount.ensure(n_tiles, s));
     HIPCHK(c, c->tbase.ensure(n_tiles, s));
-    HIPCHK(c, launch_nl_count(d, len, n_tiles, c->tcount.p, c->d_err, s));
+    if (two) {
+        HIPCHK(c, launch_nl_count(d, len, n_tiles, c->tcount.p, c->d_err, s));
+    } else {
+        HIPCHK(c, c->nlslots.ensure((uint64_t)n_tiles * NL_SLOTS, s));
+        HIPCHK(c, launch_nl_slots(d, len, n_tiles, NL_SLOTS, c->nlslots.p, c->tcount.p, c->d_err, s));
+    }
     ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tcount.p, c->tbase.p, (uint64_t)0, (size_t)n_tiles,
                                            rocprim::plus<uint64_t>(), s));
     HIPCHK(c, hipMemcpyAsync(c->h_small + 14, c->tbase.p + n_tiles - 1, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipMemcpyAsync(c->h_small + 15, c->tcount.p + n_tiles - 1, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
-    kmer_status st = check_err(c, (uint32_t)c->h_small[5]);
+    const uint32_t e = (uint32_t)c->h_small[5];
+    kmer_status st = check_err(c, e);
     if (st) return st;
+    const bool slots = !two && !(e & ERR_LINE_OVERFLOW);
+    if (e & ERR_LINE_OVERFLOW) HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));   // (short lines: two passes)
     const uint64_t n_nl = c->h_small[14] + (uint32_t)c->h_small[15];
-    HIPCHK(c, c->nlpos.ensure(n_nl + 1, s));
-    HIPCHK(c, launch_nl_write(d, len, n_tiles, c->tbase.p, c->nlpos.p, s));
+    if (!slots) {
+        HIPCHK(c, c->nlpos.ensure(n_nl + 1, s));
+        HIPCHK(c, launch_nl_write(d, len, n_tiles, c->tbase.p, c->nlpos.p, s));
+    }
     const uint64_t first = (1u - (uint32_t)li0) & 3u;
     const uint64_t n_seq = n_nl >= first ? (n_nl - first) / 4 + 1 : 0;
     if (n_seq) {
         HIPCHK(c, c->lines.ensure(n_seq, s));
         HIPCHK(c, c->wcount.ensure(n_seq, s));
-        HIPCHK(c, launch_seq_lines(c->nlpos.p, n_nl, len, li0, n_seq, c->p.k, c->p.step, c->lines.p, c->wcount.p,
-                                   check_len ? c->d_err : nullptr, (1ull << c->pbits) - 1ull, s));
+        unsigned int *lerr = check_len ? c->d_err : nullptr;
+        const uint64_t maxrel = (1ull << c->pbits) - 1ull;
+        if (slots) {
+            HIPCHK(c, c->nlpos.ensure(2 * n_seq, s));
+            HIPCHK(c, launch_seq_lines_slots(c->nlslots.p, c->tcount.p, c->tbase.p, n_tiles, NL_SLOTS, len, li0, first,
+                                             n_nl, n_seq, c->p.k, c->p.step, c->nlpos.p, c->lines.p, c->wcount.p,
+                                             lerr, maxrel, s));
+        } else {
+            HIPCHK(c, launch_seq_lines(c->nlpos.p, n_nl, len, li0, n_seq, c->p.k, c->p.step, c->lines.p,
+                                       c->wcount.p, lerr, maxrel, s));
+        }
     }
     *n_nl_out = n_nl;
     *n_seq_out = n_seq;
@@ -2509,6 +2535,7 @@ kmer_status kmer_close(kmer_ctx *c) {
     (void)settle(c);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->tcount.release();
+    c->nlslots.release();
     for (auto *b : {&c->tbase, &c->nlpos, &c->wcount, &c->wbase, &c->tp_cnt, &c->tp_lnl, &c->rkey, &c->rkey2, &c->rord, &c->rcnt, &c->xord, &c->xord2,
                     &c->xkey, &c->xkey2, &c->ukey, &c->first, &c->cnt_out, &c->roff})
         b->release();

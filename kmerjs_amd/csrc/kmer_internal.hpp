@@ -24,6 +24,9 @@ constexpr uint32_t MAXREL = (1u << 23) - 1;  // longest sequence line (bytes - 1
 // (lines up to 1 TiB, 2^23 lines) -- KMER_FLAG_LONG_LINES, or the automatic
 // retry of kmer_count_file / kmer_count_buffer.
 constexpr uint32_t PBITS_DEFAULT = 23, PBITS_LONG = 40;
+// newline positions kept per 16 KiB tile by the one-pass line split (lines of
+// >= 16 bytes on average; denser tiles take the two-pass route)
+constexpr uint32_t NL_SLOTS = 1024;
 
 // error bits (device-side, OR-ed into ctx->d_err)
 enum : uint32_t {
@@ -359,6 +362,16 @@ hipError_t launch_nl_count(const uint8_t *data, uint64_t len, uint32_t n_tiles, 
                            hipStream_t s);
 hipError_t launch_nl_write(const uint8_t *data, uint64_t len, uint32_t n_tiles, const uint64_t *tbase, uint64_t *nl,
                            hipStream_t s);
+// one pass: per-tile '\n' counts + tile-relative positions in `cap` u16 slots per
+// tile (ERR_LINE_OVERFLOW: a tile had more; fall back to nl_write)
+hipError_t launch_nl_slots(const uint8_t *data, uint64_t len, uint32_t n_tiles, uint32_t cap, uint16_t *slots,
+                          uint32_t *tcount, unsigned int *err, hipStream_t s);
+// sequence lines from the slots (tbase: exclusive scan of tcount); lse: 2 n_seq scratch words
+hipError_t launch_seq_lines_slots(const uint16_t *slots, const uint32_t *tcount, const uint64_t *tbase,
+                                  uint32_t n_tiles, uint32_t cap, uint64_t len, uint64_t li0, uint64_t first,
+                                  uint64_t n_nl, uint64_t n_seq, uint32_t k, uint32_t step, uint64_t *lse,
+                                  SeqLine *lines, uint64_t *wcount, unsigned int *err, uint64_t maxrel,
+                                  hipStream_t s);
 // wcount = windows of both strands per sequence line: 2 ceil(W / step)
 hipError_t launch_seq_lines(const uint64_t *nl, uint64_t n_nl, uint64_t len, uint64_t li0, uint64_t n_seq, uint32_t k,
                             uint32_t step, SeqLine *lines, uint64_t *wcount, unsigned int *err, uint64_t maxrel,

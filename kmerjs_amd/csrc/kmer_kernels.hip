@@ -1619,6 +1619,97 @@ __global__ __launch_bounds__(256) void nl_write_kernel(const uint8_t *data, uint
     }
 }
 
+// '\n' count per tile AND its tile-relative positions (u16) in the tile's
+// fixed slot array of `cap` entries, in one pass: the sequence lines are then
+// found from the slots after a scan of the counts, without a second pass over
+// the input.  A tile with more than `cap` newlines (lines shorter than
+// TILE / cap bytes on average) sets ERR_LINE_OVERFLOW: the host then writes
+// the global position array the two-pass way (nl_write_kernel).
+__global__ __launch_bounds__(256) void nl_slots_kernel(const uint8_t *data, uint64_t len, uint32_t cap,
+                                                       uint16_t *slots, uint32_t *tcount, unsigned int *err) {
+    __shared__ uint32_t ws[4];
+    uint32_t z[16], o = 0;
+    const int64_t g = (int64_t)blockIdx.x * TILE + 64 * threadIdx.x;
+    const uint32_t cnt = (uint64_t)g < len ? thread_nl_flags(data, len, g, z, &o) : 0u;
+    if (o & 0x80808080u) atomicOr(err, ERR_NONASCII);
+    const uint32_t incl = wave_incl_sum(cnt);
+    const int wid = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 63) ws[wid] = incl;
+    __syncthreads();
+    const uint32_t total = ws[0] + ws[1] + ws[2] + ws[3];
+    if (threadIdx.x == 0) {
+        tcount[blockIdx.x] = total;
+        if (total > cap) atomicOr(err, ERR_LINE_OVERFLOW);
+    }
+    if (!cnt || total > cap) return;
+    uint32_t o2 = incl - cnt;
+    for (int w = 0; w < wid; ++w) o2 += ws[w];
+    uint16_t *dst = slots + (uint64_t)blockIdx.x * cap;
+    const uint32_t t0 = 64 * threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        uint32_t m = z[j];
+        while (m) {
+            const int b = __ffs(m) - 1;          // bit 7 of a byte
+            m &= m - 1;
+            dst[o2++] = (uint16_t)(t0 + 4 * j + (b >> 3));
+        }
+    }
+}
+
+// Sequence-line bounds from the tile slots: newline r (chunk-relative, r =
+// tbase[tile] + i) ends line r and starts line r + 1; line r is sequence
+// ordinal (r - first) / 4 when r - first is a multiple of 4.  One workgroup
+// per tile.  The chunk's first line starts at 0 and a trailing open segment
+// ends at len (thread 0 of tile 0).
+__global__ __launch_bounds__(256) void seq_mark_kernel(const uint16_t *slots, const uint32_t *tcount,
+                                                       const uint64_t *tbase, uint32_t cap, uint64_t len,
+                                                       uint64_t first, uint64_t n_nl, uint64_t n_seq,
+                                                       uint64_t *lstart, uint64_t *lend) {
+    const uint32_t tile = blockIdx.x;
+    const uint32_t n = tcount[tile];
+    const uint64_t rb = tbase[tile];
+    const uint16_t *src = slots + (uint64_t)tile * cap;
+    for (uint32_t i = threadIdx.x; i < n; i += 256) {
+        const uint64_t r = rb + i;
+        const uint64_t pos = (uint64_t)tile * TILE + src[i];
+        if (r >= first && ((r - first) & 3) == 0) lend[(r - first) >> 2] = pos;
+        const uint64_t r1 = r + 1;
+        if (r1 >= first && ((r1 - first) & 3) == 0 && ((r1 - first) >> 2) < n_seq) lstart[(r1 - first) >> 2] = pos + 1;
+    }
+    if (tile == 0 && threadIdx.x == 0 && n_seq) {
+        if (first == 0) lstart[0] = 0;
+        const uint64_t rl = first + 4 * (n_seq - 1);
+        if (rl == n_nl) lend[n_seq - 1] = len;   // (the open trailing segment)
+    }
+}
+
+// sequence ordinal m -> SeqLine and its window count from the marked bounds
+__global__ __launch_bounds__(256) void seq_lines_se_kernel(const uint64_t *lstart, const uint64_t *lend, uint64_t li0,
+                                                           uint64_t first, uint64_t n_seq, uint32_t k, uint32_t step,
+                                                           SeqLine *lines, uint64_t *wcount, unsigned int *err,
+                                                           uint64_t maxrel) {
+    const uint32_t lsh = 64 - __popcll(maxrel);
+    for (uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; m < n_seq; m += (uint64_t)gridDim.x * blockDim.x) {
+        SeqLine sl;
+        sl.line_index = li0 + first + 4 * m;
+        sl.start = 0;
+        sl.len = 0;
+        uint64_t w2 = 0;
+        const uint64_t st = lstart[m], en = lend[m];
+        const uint64_t L = en > st ? en - st : 0;
+        if (L > 1 && L >= k) {
+            sl.start = st;
+            sl.len = L;
+            const uint64_t W = L - k + 1;
+            if (err && (W - 1 > maxrel || (sl.line_index >> (lsh - 1)))) atomicOr(err, ERR_LINE_TOO_LONG);
+            w2 = 2 * ((W + step - 1) / step);
+        }
+        lines[m] = sl;
+        wcount[m] = w2;
+    }
+}
+
 // sequence ordinal m -> SeqLine (len 0: no windows) and its window count 2W
 __global__ __launch_bounds__(256) void seq_lines_kernel(const uint64_t *nl, uint64_t n_nl, uint64_t len,
                                                         uint64_t li0, uint64_t n_seq, uint32_t k, uint32_t step,
@@ -2591,6 +2682,23 @@ hipError_t launch_nl_count(const uint8_t *data, uint64_t len, uint32_t n_tiles, 
 hipError_t launch_nl_write(const uint8_t *data, uint64_t len, uint32_t n_tiles, const uint64_t *tbase, uint64_t *nl,
                            hipStream_t s) {
     hipLaunchKernelGGL(nl_write_kernel, dim3(n_tiles), dim3(256), 0, s, data, len, tbase, nl);
+    return hipGetLastError();
+}
+hipError_t launch_nl_slots(const uint8_t *data, uint64_t len, uint32_t n_tiles, uint32_t cap, uint16_t *slots,
+                          uint32_t *tcount, unsigned int *err, hipStream_t s) {
+    hipLaunchKernelGGL(nl_slots_kernel, dim3(n_tiles), dim3(256), 0, s, data, len, cap, slots, tcount, err);
+    return hipGetLastError();
+}
+hipError_t launch_seq_lines_slots(const uint16_t *slots, const uint32_t *tcount, const uint64_t *tbase,
+                                  uint32_t n_tiles, uint32_t cap, uint64_t len, uint64_t li0, uint64_t first,
+                                  uint64_t n_nl, uint64_t n_seq, uint32_t k, uint32_t step, uint64_t *lse,
+                                  SeqLine *lines, uint64_t *wcount, unsigned int *err, uint64_t maxrel,
+                                  hipStream_t s) {
+    if (!n_seq) return hipSuccess;
+    hipLaunchKernelGGL(seq_mark_kernel, dim3(n_tiles), dim3(256), 0, s, slots, tcount, tbase, cap, len, first, n_nl,
+                       n_seq, lse, lse + n_seq);
+    hipLaunchKernelGGL(seq_lines_se_kernel, dim3(grid_for(n_seq)), dim3(256), 0, s, lse, lse + n_seq, li0, first,
+                       n_seq, k, step, lines, wcount, err, maxrel);
     return hipGetLastError();
 }
 hipError_t launch_seq_lines(const uint64_t *nl, uint64_t n_nl, uint64_t len, uint64_t li0, uint64_t n_seq, uint32_t k,

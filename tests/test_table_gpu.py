@@ -96,6 +96,33 @@ def test_table_synthetic_vs_oracle(native, k, prefix):
         assert bytes(kb[0]) <= bytes(kb[len(kb) // 2]) <= bytes(kb[-1])
 
 
+@pytest.mark.parametrize("read_len", [3, 9, 30, 150])
+def test_line_split_short_and_long_lines(native, read_len):
+    # the one-pass line split keeps 1,024 newline positions per 16 KiB tile:
+    # reads of 3 and 9 bases (lines of ~4-7 bytes) overflow it and take the
+    # two-pass route, 30 and 150 do not; every route must give the oracle's
+    # Map (ordered dense-hit path and table mode), mixed lengths included
+    from oracle import oracle
+    rng = np.random.default_rng(read_len)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    recs = []
+    for i in range(12000):
+        L = read_len if i % 5 else 150
+        s = acgt[rng.integers(0, 4, L)].tobytes()
+        recs.append(b"@r%d\n%s\n+\n%s\n" % (i, s, b"I" * L))
+    data = b"".join(recs)
+    for k, prefix in ((3, b""), (16, b""), (12, b"A")):
+        want = oracle.count_buffer(data, prefix, k, 1)
+        ctr = native.Counter(k=k, prefix=prefix)
+        got = ctr.count_buffer(data).entries()
+        ctr.close()
+        assert got == want, (k, prefix)
+        ctr = native.Counter(k=k, prefix=prefix, flags=native.FLAG_UNORDERED)
+        e = ctr.count_buffer(data).entries()
+        ctr.close()
+        assert e == sorted(want), (k, prefix, "table")
+
+
 def test_table_chunked_feeds_match_one_feed(native):
     import torch
     buf = _device_input(60_000, seed=9)
