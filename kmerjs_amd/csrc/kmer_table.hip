@@ -376,8 +376,33 @@ __global__ __launch_bounds__(256) void tab_hist2_kernel(const uint64_t *B1, cons
     __syncthreads();
     const TabUnit un = units[blockIdx.x];
     const uint64_t *src = B1 + un.start;
-    for (uint32_t i = threadIdx.x; i < un.len; i += 256)
-        atomicAdd(&hist[(uint32_t)(src[i] >> TAB_RBITS) & (TAB_NB - 1)], 1u);
+    uint32_t len = un.len;
+    // 16-B loads, 4 in flight per thread (the unit's first key alone when it
+    // is not 16-B aligned, and its last when an odd count remains)
+    if (((uintptr_t)src & 8u) && len) {
+        if (threadIdx.x == 0) atomicAdd(&hist[(uint32_t)(src[0] >> TAB_RBITS) & (TAB_NB - 1)], 1u);
+        ++src;
+        --len;
+    }
+    const ulonglong2 *s2 = (const ulonglong2 *)src;
+    const uint32_t np = len / 2;
+    uint32_t i = threadIdx.x;
+    for (; i + 3 * 256 < np; i += 4 * 256) {
+        ulonglong2 x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = s2[i + u * 256];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            atomicAdd(&hist[(uint32_t)(x[u].x >> TAB_RBITS) & (TAB_NB - 1)], 1u);
+            atomicAdd(&hist[(uint32_t)(x[u].y >> TAB_RBITS) & (TAB_NB - 1)], 1u);
+        }
+    }
+    for (; i < np; i += 256) {
+        const ulonglong2 x = s2[i];
+        atomicAdd(&hist[(uint32_t)(x.x >> TAB_RBITS) & (TAB_NB - 1)], 1u);
+        atomicAdd(&hist[(uint32_t)(x.y >> TAB_RBITS) & (TAB_NB - 1)], 1u);
+    }
+    if ((len & 1u) && threadIdx.x == 0) atomicAdd(&hist[(uint32_t)(src[len - 1] >> TAB_RBITS) & (TAB_NB - 1)], 1u);
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < TAB_NB; b += 256) H2[un.hbase + (uint64_t)b * un.nunits + un.u] = hist[b];
 }
