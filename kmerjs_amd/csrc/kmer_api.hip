@@ -853,10 +853,9 @@ kmer_status chunk_lines(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_
         unsigned int *lerr = check_len ? c->d_err : nullptr;
         const uint64_t maxrel = (1ull << c->pbits) - 1ull;
         if (slots) {
-            HIPCHK(c, c->nlpos.ensure(2 * n_seq, s));
             HIPCHK(c, launch_seq_lines_slots(c->nlslots.p, c->tcount.p, c->tbase.p, n_tiles, NL_SLOTS, len, li0, first,
-                                             n_nl, n_seq, c->p.k, c->p.step, c->nlpos.p, c->lines.p, c->wcount.p,
-                                             lerr, maxrel, s));
+                                             n_nl, n_seq, c->p.k, c->p.step, c->lines.p, c->wcount.p, lerr, maxrel,
+                                             s));
         } else {
             HIPCHK(c, launch_seq_lines(c->nlpos.p, n_nl, len, li0, n_seq, c->p.k, c->p.step, c->lines.p,
                                        c->wcount.p, lerr, maxrel, s));
@@ -997,13 +996,17 @@ kmer_status table_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_t
         uint32_t *split = c->tpc.p + n_seq;             // set when a line is not exactly one piece
         HIPCHK(c, hipMemsetAsync(split, 0, 4, s));
         HIPCHK(c, launch_tab_piece_count(c->wcount.p, n_seq, c->tpc.p, split, s));
-        ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tpc.p, c->tpb.p, (uint64_t)0, (size_t)n_seq,
-                                               rocprim::plus<uint64_t>(), s));
-        HIPCHK(c, hipMemcpyAsync(c->h_small + 12, c->tpb.p + n_seq - 1, 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipMemcpyAsync(c->h_small + 13, c->tpc.p + n_seq - 1, 4, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipMemcpyAsync(c->h_small + 16, split, 4, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
-        const uint64_t n_pieces = c->h_small[12] + (uint32_t)c->h_small[13];
+        uint64_t n_pieces = n_seq;                // (no split: one piece per line)
+        if ((uint32_t)c->h_small[16]) {
+            ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tpc.p, c->tpb.p, (uint64_t)0, (size_t)n_seq,
+                                                   rocprim::plus<uint64_t>(), s));
+            HIPCHK(c, hipMemcpyAsync(c->h_small + 12, c->tpb.p + n_seq - 1, 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipMemcpyAsync(c->h_small + 13, c->tpc.p + n_seq - 1, 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            n_pieces = c->h_small[12] + (uint32_t)c->h_small[13];
+        }
         if (n_pieces == 0) {
             n_items = 0;                          // no line holds a window
         } else if ((uint32_t)c->h_small[16]) {    // long lines (or empty ones, dropped on the way)

@@ -366,12 +366,11 @@ hipError_t launch_nl_write(const uint8_t *data, uint64_t len, uint32_t n_tiles, 
 // tile (ERR_LINE_OVERFLOW: a tile had more; fall back to nl_write)
 hipError_t launch_nl_slots(const uint8_t *data, uint64_t len, uint32_t n_tiles, uint32_t cap, uint16_t *slots,
                           uint32_t *tcount, unsigned int *err, hipStream_t s);
-// sequence lines from the slots (tbase: exclusive scan of tcount); lse: 2 n_seq scratch words
+// sequence lines from the slots (tbase: exclusive scan of tcount)
 hipError_t launch_seq_lines_slots(const uint16_t *slots, const uint32_t *tcount, const uint64_t *tbase,
                                   uint32_t n_tiles, uint32_t cap, uint64_t len, uint64_t li0, uint64_t first,
-                                  uint64_t n_nl, uint64_t n_seq, uint32_t k, uint32_t step, uint64_t *lse,
-                                  SeqLine *lines, uint64_t *wcount, unsigned int *err, uint64_t maxrel,
-                                  hipStream_t s);
+                                  uint64_t n_nl, uint64_t n_seq, uint32_t k, uint32_t step, SeqLine *lines,
+                                  uint64_t *wcount, unsigned int *err, uint64_t maxrel, hipStream_t s);
 // wcount = windows of both strands per sequence line: 2 ceil(W / step)
 hipError_t launch_seq_lines(const uint64_t *nl, uint64_t n_nl, uint64_t len, uint64_t li0, uint64_t n_seq, uint32_t k,
                             uint32_t step, SeqLine *lines, uint64_t *wcount, unsigned int *err, uint64_t maxrel,

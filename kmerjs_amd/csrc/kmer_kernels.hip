@@ -1657,56 +1657,67 @@ __global__ __launch_bounds__(256) void nl_slots_kernel(const uint8_t *data, uint
     }
 }
 
-// Sequence-line bounds from the tile slots: newline r (chunk-relative, r =
-// tbase[tile] + i) ends line r and starts line r + 1; line r is sequence
-// ordinal (r - first) / 4 when r - first is a multiple of 4.  One workgroup
-// per tile.  The chunk's first line starts at 0 and a trailing open segment
-// ends at len (thread 0 of tile 0).
-__global__ __launch_bounds__(256) void seq_mark_kernel(const uint16_t *slots, const uint32_t *tcount,
-                                                       const uint64_t *tbase, uint32_t cap, uint64_t len,
-                                                       uint64_t first, uint64_t n_nl, uint64_t n_seq,
-                                                       uint64_t *lstart, uint64_t *lend) {
-    const uint32_t tile = blockIdx.x;
+// Sequence lines from the tile slots, one wave per tile: newline r
+// (chunk-relative, r = tbase[tile] + i) ends line r, which is sequence
+// ordinal (r - first) / 4 when r - first is a multiple of 4; its start is the
+// previous newline + 1 -- slot i - 1, or the last newline of the nearest
+// earlier tile that has one (0: the chunk's first line).  The open trailing
+// segment (line n_nl, no newline after it) ends at len.
+__device__ __forceinline__ uint64_t nl_before_tile(const uint16_t *slots, const uint32_t *tcount, uint32_t cap,
+                                                   int64_t tile) {
+    for (int64_t u = tile - 1; u >= 0; --u) {
+        const uint32_t n = tcount[u];
+        if (n) return (uint64_t)u * TILE + slots[(uint64_t)u * cap + n - 1] + 1;
+    }
+    return 0;
+}
+
+__device__ __forceinline__ void put_seq_line(uint64_t st, uint64_t en, uint64_t li, uint32_t k, uint32_t step,
+                                             uint32_t lsh, uint64_t maxrel, SeqLine *line, uint64_t *wc,
+                                             unsigned int *err) {
+    SeqLine sl;
+    sl.line_index = li;
+    sl.start = 0;
+    sl.len = 0;
+    uint64_t w2 = 0;
+    const uint64_t L = en > st ? en - st : 0;
+    if (L > 1 && L >= k) {
+        sl.start = st;
+        sl.len = L;
+        const uint64_t W = L - k + 1;
+        // (err null: no order key, no limit)
+        if (err && (W - 1 > maxrel || (li >> (lsh - 1)))) atomicOr(err, ERR_LINE_TOO_LONG);
+        w2 = 2 * ((W + step - 1) / step);
+    }
+    *line = sl;
+    *wc = w2;
+}
+
+__global__ __launch_bounds__(256) void seq_lines_slots_kernel(const uint16_t *slots, const uint32_t *tcount,
+                                                              const uint64_t *tbase, uint32_t n_tiles, uint32_t cap,
+                                                              uint64_t len, uint64_t li0, uint64_t first,
+                                                              uint64_t n_nl, uint64_t n_seq, uint32_t k,
+                                                              uint32_t step, SeqLine *lines, uint64_t *wcount,
+                                                              unsigned int *err, uint64_t maxrel) {
+    const uint32_t lsh = 64 - __popcll(maxrel);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile >= n_tiles) return;
     const uint32_t n = tcount[tile];
     const uint64_t rb = tbase[tile];
     const uint16_t *src = slots + (uint64_t)tile * cap;
-    for (uint32_t i = threadIdx.x; i < n; i += 256) {
+    const uint64_t t0 = (uint64_t)tile * TILE;
+    for (uint32_t i = lane; i < n; i += 64) {
         const uint64_t r = rb + i;
-        const uint64_t pos = (uint64_t)tile * TILE + src[i];
-        if (r >= first && ((r - first) & 3) == 0) lend[(r - first) >> 2] = pos;
-        const uint64_t r1 = r + 1;
-        if (r1 >= first && ((r1 - first) & 3) == 0 && ((r1 - first) >> 2) < n_seq) lstart[(r1 - first) >> 2] = pos + 1;
+        if (r < first || ((r - first) & 3) != 0) continue;
+        const uint64_t en = t0 + src[i];
+        const uint64_t st = i ? t0 + src[i - 1] + 1 : nl_before_tile(slots, tcount, cap, tile);
+        const uint64_t m = (r - first) >> 2;
+        put_seq_line(st, en, li0 + r, k, step, lsh, maxrel, lines + m, wcount + m, err);
     }
-    if (tile == 0 && threadIdx.x == 0 && n_seq) {
-        if (first == 0) lstart[0] = 0;
-        const uint64_t rl = first + 4 * (n_seq - 1);
-        if (rl == n_nl) lend[n_seq - 1] = len;   // (the open trailing segment)
-    }
-}
-
-// sequence ordinal m -> SeqLine and its window count from the marked bounds
-__global__ __launch_bounds__(256) void seq_lines_se_kernel(const uint64_t *lstart, const uint64_t *lend, uint64_t li0,
-                                                           uint64_t first, uint64_t n_seq, uint32_t k, uint32_t step,
-                                                           SeqLine *lines, uint64_t *wcount, unsigned int *err,
-                                                           uint64_t maxrel) {
-    const uint32_t lsh = 64 - __popcll(maxrel);
-    for (uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; m < n_seq; m += (uint64_t)gridDim.x * blockDim.x) {
-        SeqLine sl;
-        sl.line_index = li0 + first + 4 * m;
-        sl.start = 0;
-        sl.len = 0;
-        uint64_t w2 = 0;
-        const uint64_t st = lstart[m], en = lend[m];
-        const uint64_t L = en > st ? en - st : 0;
-        if (L > 1 && L >= k) {
-            sl.start = st;
-            sl.len = L;
-            const uint64_t W = L - k + 1;
-            if (err && (W - 1 > maxrel || (sl.line_index >> (lsh - 1)))) atomicOr(err, ERR_LINE_TOO_LONG);
-            w2 = 2 * ((W + step - 1) / step);
-        }
-        lines[m] = sl;
-        wcount[m] = w2;
+    if (tile == n_tiles - 1 && lane == 0 && n_seq && first + 4 * (n_seq - 1) == n_nl) {
+        const uint64_t st = n ? t0 + src[n - 1] + 1 : nl_before_tile(slots, tcount, cap, tile);
+        put_seq_line(st, len, li0 + n_nl, k, step, lsh, maxrel, lines + n_seq - 1, wcount + n_seq - 1, err);
     }
 }
 
@@ -2691,14 +2702,11 @@ hipError_t launch_nl_slots(const uint8_t *data, uint64_t len, uint32_t n_tiles, 
 }
 hipError_t launch_seq_lines_slots(const uint16_t *slots, const uint32_t *tcount, const uint64_t *tbase,
                                   uint32_t n_tiles, uint32_t cap, uint64_t len, uint64_t li0, uint64_t first,
-                                  uint64_t n_nl, uint64_t n_seq, uint32_t k, uint32_t step, uint64_t *lse,
-                                  SeqLine *lines, uint64_t *wcount, unsigned int *err, uint64_t maxrel,
-                                  hipStream_t s) {
+                                  uint64_t n_nl, uint64_t n_seq, uint32_t k, uint32_t step, SeqLine *lines,
+                                  uint64_t *wcount, unsigned int *err, uint64_t maxrel, hipStream_t s) {
     if (!n_seq) return hipSuccess;
-    hipLaunchKernelGGL(seq_mark_kernel, dim3(n_tiles), dim3(256), 0, s, slots, tcount, tbase, cap, len, first, n_nl,
-                       n_seq, lse, lse + n_seq);
-    hipLaunchKernelGGL(seq_lines_se_kernel, dim3(grid_for(n_seq)), dim3(256), 0, s, lse, lse + n_seq, li0, first,
-                       n_seq, k, step, lines, wcount, err, maxrel);
+    hipLaunchKernelGGL(seq_lines_slots_kernel, dim3((n_tiles + 3) / 4), dim3(256), 0, s, slots, tcount, tbase,
+                       n_tiles, cap, len, li0, first, n_nl, n_seq, k, step, lines, wcount, err, maxrel);
     return hipGetLastError();
 }
 hipError_t launch_seq_lines(const uint64_t *nl, uint64_t n_nl, uint64_t len, uint64_t li0, uint64_t n_seq, uint32_t k,
