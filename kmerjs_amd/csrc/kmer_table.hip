@@ -16,8 +16,9 @@
 //           a shift of them, canonical code, h = tab_mix(code).  hist1 counts keys per
 //           (workgroup, top-10-bit partition) in LDS; scatter1 re-reads the
 //           input (1.3 B/window, cheaper than a key buffer), ranks each key in
-//           its partition with an LDS atomic, sorts a round of 16 K keys in LDS
-//           and writes each partition's run contiguously.
+//           its partition with an LDS atomic, sorts a round of 8 K keys in LDS
+//           and writes each partition's run contiguously (two 512-thread
+//           workgroups per CU: one's stores overlap the other's formation).
 //   pass 2  per run of a partition: the next 10 bits, LDS sort in rounds of
 //           8 K keys -> B2 in 2^20 buckets, contiguous per bucket; each round
 //           writes a bucket's keys only up to its last 64-B boundary and
@@ -74,6 +75,22 @@ __device__ __forceinline__ uint32_t block_excl_1024(uint32_t v, uint32_t *ws, ui
     return before + inc - v;
 }
 
+// exclusive scan of one value per thread over a 512-thread workgroup (ws: 8 words)
+__device__ __forceinline__ uint32_t block_excl_512(uint32_t v, uint32_t *ws, uint32_t *total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t inc = tab_incl_sum(v);
+    if (lane == 63) ws[wid] = inc;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        const uint32_t x = ws[w];
+        before += w < wid ? x : 0u;
+        all += x;
+    }
+    *total = all;
+    return before + inc - v;
+}
 __device__ __forceinline__ uint32_t readlane32(uint32_t v, uint32_t i) {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)i);
 }
@@ -277,6 +294,60 @@ __global__ __launch_bounds__(256) void tab_hist1_kernel(TabArgs a) {
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < TAB_NB; i += 256) a.H1[(uint64_t)i * a.nwg + blockIdx.x] = hist[i];
+}
+
+// pass 1, scatter in half-size workgroups: 512 threads, rounds of 8 K keys,
+// 80 KB of LDS -- two workgroups per CU, so that one's write-out overlaps the
+// other's window formation (one 1,024-thread workgroup per CU runs its
+// formation, LDS sort and stores strictly one after another).  Thread t keeps
+// bins 2t and 2t + 1.
+constexpr int TAB_WGH = 512;
+template <bool PFX>
+__global__ __launch_bounds__(TAB_WGH) void tab_scatter1h_kernel(TabArgs a) {
+    __shared__ uint64_t srt[TAB_RPL * TAB_WGH];
+    __shared__ uint64_t cur[TAB_NB];
+    __shared__ uint32_t bcnt[TAB_NB];
+    __shared__ uint16_t bst[TAB_NB];                 // (round starts < 8 K)
+    uint32_t *const ws = (uint32_t *)srt;            // (scan scratch: srt is free between rounds)
+    const uint32_t t = threadIdx.x, b0 = 2 * t, b1 = 2 * t + 1;
+    cur[b0] = a.base + a.H1s[(uint64_t)b0 * a.nwg + blockIdx.x];
+    cur[b1] = a.base + a.H1s[(uint64_t)b1 * a.nwg + blockIdx.x];
+    bcnt[b0] = 0;
+    bcnt[b1] = 0;
+    __syncthreads();
+    TabCur c = tab_cursor(a, TAB_WGH / 64);
+    while (true) {
+        uint64_t key[TAB_RPL];
+        uint32_t rank[TAB_RPL];
+        uint32_t v = 0;
+        if (c.m < c.end) v = tab_round<TAB_RPL, 0, PFX>(a, c, true, key);
+#pragma unroll
+        for (int j = 0; j < TAB_RPL; ++j)
+            rank[j] = (v & (1u << j)) ? atomicAdd(&bcnt[key[j] >> (64 - TAB_L1)], 1u) : 0u;
+        __syncthreads();
+        uint32_t total;
+        const uint32_t c0 = bcnt[b0], c1 = bcnt[b1];
+        const uint32_t st0 = block_excl_512(c0 + c1, ws, &total), st1 = st0 + c0;
+        bst[b0] = (uint16_t)st0;
+        bst[b1] = (uint16_t)st1;
+        cur[b0] -= st0;                           // (write-out: B1[cur[p] + i], one LDS read per key)
+        cur[b1] -= st1;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < TAB_RPL; ++j)
+            if (v & (1u << j)) srt[bst[key[j] >> (64 - TAB_L1)] + rank[j]] = key[j];
+        __syncthreads();
+        for (uint32_t i = t; i < total; i += TAB_WGH) {
+            const uint64_t h = srt[i];
+            a.B1[cur[(uint32_t)(h >> (64 - TAB_L1))] + i] = h;
+        }
+        __syncthreads();
+        cur[b0] += st0 + c0;
+        cur[b1] += st1 + c1;
+        bcnt[b0] = 0;
+        bcnt[b1] = 0;
+        if (!__syncthreads_or(c.m < c.end)) break;
+    }
 }
 
 // pass 1, scatter: the same keys, LDS-sorted by partition in rounds of 16 K,
@@ -1081,22 +1152,6 @@ constexpr uint32_t TS_BINMAX = 64;                    // fuller bins: leftover (
 constexpr uint32_t TS_GMAX = 64;                      // buckets per group
 constexpr uint32_t TS_SC = 512;                       // bucket starts cached per refill
 
-// exclusive scan of one value per thread over a 512-thread workgroup (ws: 8 words)
-__device__ __forceinline__ uint32_t block_excl_512(uint32_t v, uint32_t *ws, uint32_t *total) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint32_t inc = tab_incl_sum(v);
-    if (lane == 63) ws[wid] = inc;
-    __syncthreads();
-    uint32_t before = 0, all = 0;
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-        const uint32_t x = ws[w];
-        before += w < wid ? x : 0u;
-        all += x;
-    }
-    *total = all;
-    return before + inc - v;
-}
 }  // namespace
 
 __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) {
@@ -1376,6 +1431,18 @@ hipError_t launch_tab_hist1(const TabArgs &a, hipStream_t s) {
 }
 
 hipError_t launch_tab_scatter1(const TabArgs &a, hipStream_t s) {
+    // KMERHIP_TAB_S1=full: one 1,024-thread workgroup per CU (A/B experiments)
+    static const bool half = [] {
+        const char *e = getenv("KMERHIP_TAB_S1");
+        return !(e && strcmp(e, "full") == 0);
+    }();
+    if (half) {
+        if (a.pmask == 0)
+            hipLaunchKernelGGL(tab_scatter1h_kernel<false>, dim3(a.nwg), dim3(TAB_WGH), 0, s, a);
+        else
+            hipLaunchKernelGGL(tab_scatter1h_kernel<true>, dim3(a.nwg), dim3(TAB_WGH), 0, s, a);
+        return hipGetLastError();
+    }
     if (a.pmask == 0)
         hipLaunchKernelGGL(tab_scatter1_kernel<false>, dim3(a.nwg), dim3(TAB_WG1), 0, s, a);
     else
