@@ -211,7 +211,7 @@ def load_traffic(args, kern_name):
 # (a bucket is held in registers across its LDS ranges) + one 8-B entry written
 # per distinct canonical k-mer.
 def table_phase_bytes(nbytes, n_keys, canonical):
-    return {"lines": 2 * nbytes, "hist1": nbytes, "scatter1": nbytes + 8 * n_keys, "hist2": 8 * n_keys,
+    return {"lines": nbytes, "hist1": nbytes, "scatter1": nbytes + 8 * n_keys, "hist2": 8 * n_keys,
             "scatter2": 16 * n_keys, "final": 8 * n_keys + 8 * canonical}
 
 
@@ -499,9 +499,9 @@ def main():
             kern_name = max(phases, key=lambda x: phases[x])
             kern_ms = phases[kern_name]
             algo_bytes = pbytes[kern_name]
-            kern_name = {"lines": "nl_count_kernel + nl_write_kernel + seq_lines_kernel",
-                         "hist1": "tab_hist1_kernel (+ scan)", "scatter1": "tab_scatter1_kernel",
-                         "hist2": "tab_hist2_kernel (+ scan)", "scatter2": "tab_scatter2_kernel",
+            kern_name = {"lines": "nl_slots_kernel + seq_lines_slots_kernel",
+                         "hist1": "tab_hist1_kernel (+ scan)", "scatter1": "tab_scatter1h_kernel",
+                         "hist2": "tab_hist2_kernel (+ scan)", "scatter2": "tab_scatter2c_kernel",
                          "final": "tab_sort_final_kernel (+ tab_final_kernel on its leftover units)"}[kern_name]
         elif args.k > 64 or (not args.prefix and args.k > 31):
             # general path (k > 64): line arrays + one thread per window, every
@@ -520,9 +520,10 @@ def main():
             kern_name = "scan_planes_kernel (k > 32: 128-bit window codes)"
             algo_bytes = nbytes + 32 * (accepted / world)
         elif (args.prefix and len(args.prefix) <= 3) or not args.prefix:
-            # dense-hit path: the timed kernels are the two streaming newline passes
-            kern_name = "nl_count_kernel + nl_write_kernel (dense-hit path)"
-            algo_bytes = 2 * nbytes
+            # dense-hit path: the timed phase is the line split -- one streaming
+            # pass over the input (nl_slots_kernel) + the sequence-line descriptors
+            kern_name = "nl_slots_kernel + seq_lines_slots_kernel (dense-hit path line split)"
+            algo_bytes = nbytes
         else:
             # algorithmic bytes per scan launch: the whole FASTQ batch is
             # read once (B_in) + one 24-B hit record written per accepted window
