@@ -548,6 +548,7 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
     h.hits_hi = c->hits_hi.p;
     h.ovf_hi = c->ovf_hi.p;
     h.wide = c->wide ? 1u : 0u;
+    h.ablate = a.ablate;
     if (c->wide) {                               // (high word: kbits - 64 < 64 bits, then the invalid bit)
         h.smask_hi = (1ull << (c->kbits - 64)) - 1ull;
         h.invalid_key = 1ull << (c->kbits - 64);

@@ -164,6 +164,7 @@ struct HitArgs {
     // holds the entry's own index until apply_cross has moved it)
     const uint64_t *hits_hi, *ovf_hi;
     uint32_t wide;
+    uint32_t ablate;               // experiments (KMER_FLAG_ABLATE_*): no line-length errors on unwritten records
     uint64_t smask_hi;             // wide: mask of the high word (2(k - |P|) - 64 bits)
     uint64_t *rkeyh;
     uint64_t *xkeyh, *xkeyl;

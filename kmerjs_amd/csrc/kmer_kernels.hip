@@ -553,6 +553,14 @@ __device__ __forceinline__ void emit_hit(const ScanArgs &a, const uint8_t *buf, 
     r.qm = (uint32_t)q | (strand << 14) | ((exotic ? 1u : 0u) << 15) | ((lstart >= 0 ? 1u : 0u) << 16) | (slot << 17);
     r.c_local = c_local;
     r.lstart = lstart >= 0 ? (uint32_t)lstart : 0u;
+    if (a.ablate & 8u) {                         // experiments: the record computed, not stored
+        if (r.code == 0x0123456789ABCDEFull && r.qm == 7u && r.lstart == 3u) atomicOr(a.err, 0u);
+        return;
+    }
+    if (a.ablate & 16u) {                        // experiments: every record to the same 64 slots
+        a.hits[threadIdx.x & 63u] = r;
+        return;
+    }
     if (slot < HMAX) {
         a.hits[(uint64_t)tile * HMAX + slot] = r;
         if (WIDE) a.hits_hi[(uint64_t)tile * HMAX + slot] = chi;
@@ -1088,10 +1096,10 @@ __device__ __forceinline__ uint64_t resolve_hit(const HitArgs &a, const HitRec &
     const bool seq = (li & 3) == 1;
     const uint64_t maxrel = (1ull << a.pbits) - 1ull;
     if (rel > maxrel) {
-        if (seq) atomicOr(a.err, ERR_LINE_TOO_LONG);
+        if (seq && !a.ablate) atomicOr(a.err, ERR_LINE_TOO_LONG);
         rel = maxrel;                            // (non-sequence lines only need a consistent order)
     }
-    if (li >> (63 - a.pbits)) atomicOr(a.err, ERR_LINE_TOO_LONG);   // (line field full: long-line mode)
+    if ((li >> (63 - a.pbits)) && !a.ablate) atomicOr(a.err, ERR_LINE_TOO_LONG);   // (line field full: long-line mode)
     const uint64_t order = (li << (a.pbits + 1)) | ((uint64_t)strand << a.pbits) | (strand ? maxrel - rel : rel);
     *order_out = order;
     const uint32_t sp = (uint32_t)(s0 + 64);     // < 2^15
