@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_select.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 #include <rocprim/iterator/transform_iterator.hpp>
 
@@ -128,7 +129,7 @@ struct kmer_ctx {
     DBuf<uint64_t> tp_cnt, tp_lnl;             // general path, two-pass debug mode
     // session packed hits, by rank (first-occurrence order of all hits)
     uint64_t n_hits = 0, n_cross = 0;
-    DBuf<uint64_t> rkey, rkey2, rord, rcnt;
+    DBuf<uint64_t> rkey, rkey2, rord, rord2, rcnt, csel;
     DBuf<uint64_t> rkeyh, whA, whB;    // wide keys: high words by rank; sort scratch
     DBuf<uint32_t> ridx3;
     DBuf<uint32_t> rkey32, rkey32b;   // narrow keys: 2(k-|P|) + 1 <= 32 bits
@@ -1494,6 +1495,56 @@ kmer_status bucket_heads(kmer_ctx *c, uint64_t n) {
     return KMER_OK;
 }
 
+struct KeyValid32 {
+    uint32_t inv;
+    __host__ __device__ bool operator()(uint32_t k) const { return k != inv; }
+};
+struct KeyValid64 {
+    uint64_t inv;
+    __host__ __device__ bool operator()(uint64_t k) const { return k != inv; }
+};
+
+// Dense-hit path with a prefix: every window of a sequence line holds a rank
+// slot and the windows that do not start with the prefix (or its reverse
+// complement) carry the invalid key.  The matching ones are compacted, in
+// rank order, before the finish sorts them -- a 1-3-base prefix rejects most
+// windows (C2 input, prefix ACG: 37.5 M of 2.7 G).
+kmer_status compact_windows(kmer_ctx *c) {
+    hipStream_t s = c->stream;
+    const uint64_t n = c->n_hits;
+    if (n == 0) return KMER_OK;
+    const uint64_t invalid = c->kbits >= 63 ? ~0ull : (1ull << c->kbits);
+    HIPCHK(c, c->ridx2.ensure(n, s));
+    HIPCHK(c, c->csel.ensure(1, s));
+    rocprim::counting_iterator<uint32_t> iota(0u);
+    if (c->narrow) {
+        auto fl = rocprim::make_transform_iterator(c->rkey32.p, KeyValid32{(uint32_t)invalid});
+        ROCPRIM_RUN(c, rocprim::select(t, b, iota, fl, c->ridx2.p, c->csel.p, (size_t)n, s));
+    } else {
+        auto fl = rocprim::make_transform_iterator(c->rkey.p, KeyValid64{invalid});
+        ROCPRIM_RUN(c, rocprim::select(t, b, iota, fl, c->ridx2.p, c->csel.p, (size_t)n, s));
+    }
+    HIPCHK(c, hipMemcpyAsync(c->h_small + 20, c->csel.p, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    const uint64_t n2 = c->h_small[20];
+    if (n2 >= n) return KMER_OK;
+    // gathered into the second buffers, copied back (the session buffers keep their size)
+    if (c->narrow) {
+        HIPCHK(c, c->rkey32b.ensure(n2 + 1, s));
+        HIPCHK(c, launch_gather_u32(c->rkey32.p, c->ridx2.p, n2, c->rkey32b.p, s));
+        HIPCHK(c, hipMemcpyAsync(c->rkey32.p, c->rkey32b.p, n2 * 4, hipMemcpyDeviceToDevice, s));
+    } else {
+        HIPCHK(c, c->rkey2.ensure(n2 + 1, s));
+        HIPCHK(c, launch_gather_u64(c->rkey.p, c->ridx2.p, n2, c->rkey2.p, s));
+        HIPCHK(c, hipMemcpyAsync(c->rkey.p, c->rkey2.p, n2 * 8, hipMemcpyDeviceToDevice, s));
+    }
+    HIPCHK(c, c->rord2.ensure(n2 + 1, s));
+    HIPCHK(c, launch_gather_u64(c->rord.p, c->ridx2.p, n2, c->rord2.p, s));
+    HIPCHK(c, hipMemcpyAsync(c->rord.p, c->rord2.p, n2 * 8, hipMemcpyDeviceToDevice, s));
+    c->n_hits = n2;
+    return KMER_OK;
+}
+
 // resolve a deferred unique count (finish without a host result)
 kmer_status resolve_out(kmer_ctx *c) {
     kmer_status st = resolve_feed_timing(c);
@@ -1655,6 +1706,10 @@ kmer_status finish(kmer_ctx *c, kmer_result **out) {
     if (c->mode == MODE_PACKED || c->mode == MODE_WINDOWS) {
         st = apply_cross(c);
         if (st) return st;
+        if (c->mode == MODE_WINDOWS && !c->prefix.empty()) {
+            st = compact_windows(c);
+            if (st) return st;
+        }
         st = rank_finish(c, c->n_hits, false, false, &nu, sync);
         if (st) return st;
         c->n_out = nu;
@@ -2540,7 +2595,7 @@ kmer_status kmer_close(kmer_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->tcount.release();
     c->nlslots.release();
-    for (auto *b : {&c->tbase, &c->nlpos, &c->wcount, &c->wbase, &c->tp_cnt, &c->tp_lnl, &c->rkey, &c->rkey2, &c->rord, &c->rcnt, &c->xord, &c->xord2,
+    for (auto *b : {&c->tbase, &c->nlpos, &c->wcount, &c->wbase, &c->tp_cnt, &c->tp_lnl, &c->rkey, &c->rkey2, &c->rord, &c->rord2, &c->csel, &c->rcnt, &c->xord, &c->xord2,
                     &c->xkey, &c->xkey2, &c->ukey, &c->first, &c->cnt_out, &c->roff})
         b->release();
     for (auto *b : {&c->ridx, &c->ridx2, &c->opos, &c->xslot, &c->rkey32, &c->rkey32b, &c->bH, &c->bHs}) b->release();

@@ -327,6 +327,7 @@ hipError_t launch_emit(const EmitArgs &a, hipStream_t s);
 // entries' keys after apply_cross; heads over (hi, lo) sorted ranks (hcnt
 // prefilled with 1, as launch_heads_sparse)
 hipError_t launch_gather_u64(const uint64_t *src, const uint32_t *idx, uint64_t n, uint64_t *dst, hipStream_t s);
+hipError_t launch_gather_u32(const uint32_t *src, const uint32_t *idx, uint64_t n, uint32_t *dst, hipStream_t s);
 hipError_t launch_cross_wide_fix(const uint32_t *xslot, uint64_t n, const uint64_t *xkeyl, const uint64_t *xkeyh,
                                  uint64_t *rkey, uint64_t *rkeyh, hipStream_t s);
 hipError_t launch_heads_wide(const uint64_t *shi, const uint64_t *slo, const uint32_t *srank, uint64_t n,

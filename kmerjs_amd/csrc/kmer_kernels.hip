@@ -2021,6 +2021,12 @@ __global__ __launch_bounds__(256) void gather_u64_kernel(const uint64_t *src, co
         dst[i] = src[idx[i]];
 }
 
+__global__ __launch_bounds__(256) void gather_u32_kernel(const uint32_t *src, const uint32_t *idx, uint64_t n,
+                                                         uint32_t *dst) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        dst[i] = src[idx[i]];
+}
+
 // after apply_cross the cross slots hold their entry's index: put the key there
 __global__ __launch_bounds__(256) void cross_wide_fix_kernel(const uint32_t *xslot, uint64_t n, const uint64_t *xkeyl,
                                                              const uint64_t *xkeyh, uint64_t *rkey, uint64_t *rkeyh) {
@@ -2594,6 +2600,10 @@ hipError_t launch_cross_segsort(uint64_t *ord, uint64_t *key, const uint32_t *sl
                                 uint32_t *rkey32, uint64_t *rord, uint32_t pbits, hipStream_t s) {
     if (n) hipLaunchKernelGGL(cross_segsort_kernel, dim3(grid_for(n)), dim3(256), 0, s, ord, key, slot, n, rkey, rkey32,
                               rord, pbits + 1);
+    return hipGetLastError();
+}
+hipError_t launch_gather_u32(const uint32_t *src, const uint32_t *idx, uint64_t n, uint32_t *dst, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(gather_u32_kernel, dim3(grid_for(n)), dim3(256), 0, s, src, idx, n, dst);
     return hipGetLastError();
 }
 hipError_t launch_gather_u64(const uint64_t *src, const uint32_t *idx, uint64_t n, uint64_t *dst, hipStream_t s) {

@@ -24,6 +24,7 @@
  */
 'use strict';
 const EventEmitter = require('events');
+const fs = require('fs');
 const path = require('path');
 const { KmerMap } = require('./kmer_map.js');
 
@@ -197,8 +198,9 @@ class KmerJS {
             // the progress-stream of lib/kmers.js:108-110: one 'progress' event
             // per input batch read (progress-stream's fields; bytesRead follows)
             const t0 = Date.now();
-            let lastDone = 0;
-            const onProgress = (done, total) => {
+            let lastDone = 0, lastTotal = -1, finished = false;
+            const emitProgress = (done, total) => {
+                lastTotal = total;
                 const runtime = (Date.now() - t0) / 1000;
                 const speed = runtime > 0 ? done / runtime : 0;
                 kmerObj.bytesRead = done;
@@ -214,8 +216,16 @@ class KmerJS {
                 });
                 lastDone = done;
             };
+            // (batch events come from the reader thread; the completion may be
+            // delivered before the last of them -- it then emits the final one
+            // itself, and later arrivals are dropped, so events stay monotone and
+            // end at the whole file before the promise resolves)
+            const onProgress = (done, total) => {
+                if (!finished) emitProgress(done, total);
+            };
             native().countFile(handle, String(kmerObj.fastq), (err, res) => {
                 native().close(handle);
+                finished = true;
                 if (err) {
                     reject(err.status === KMER_E_TOO_MANY_KEYS ? tooManyKeys(err.message) : err);
                     return;
@@ -230,6 +240,13 @@ class KmerJS {
                 } catch (e) {
                     reject(e);        // (never an exception escaping the completion callback)
                     return;
+                }
+                if (lastTotal < 0 || lastDone < lastTotal) {
+                    let size = lastTotal;
+                    if (size < 0) {
+                        try { size = fs.statSync(String(kmerObj.fastq)).size; } catch (e) { size = lastDone; }
+                    }
+                    emitProgress(size, size);
                 }
                 kmerObj.lines = res.lines;
                 if (kmerObj.progress) {
