@@ -841,7 +841,8 @@ kmer_status chunk_lines(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_
     kmer_status st = check_err(c, e);
     if (st) return st;
     const bool slots = !two && !(e & ERR_LINE_OVERFLOW);
-    if (e & ERR_LINE_OVERFLOW) HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));   // (short lines: two passes)
+    if (e & ERR_LINE_OVERFLOW)                   // (short lines: two passes; other bits kept)
+        HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)c->d_err, (int)(e & ~ERR_LINE_OVERFLOW), 1, s));
     const uint64_t n_nl = c->h_small[14] + (uint32_t)c->h_small[15];
     if (!slots) {
         HIPCHK(c, c->nlpos.ensure(n_nl + 1, s));
