@@ -577,9 +577,17 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
     p.d = d;
     p.len = len;
     // the chunk runs on the low-priority stream, after everything queued so far
-    p.s = c->sstream;
-    HIPCHK(c, hipEventRecord(c->evq, s));
-    HIPCHK(c, hipStreamWaitEvent(p.s, c->evq, 0));
+    // (KMERHIP_ONE_STREAM=1: on the caller's stream itself, no cross-stream
+    // waits -- A/B experiments)
+    static const bool one_stream = [] {
+        const char *e = getenv("KMERHIP_ONE_STREAM");
+        return e && strcmp(e, "1") == 0;
+    }();
+    p.s = one_stream ? s : c->sstream;
+    if (p.s != s) {
+        HIPCHK(c, hipEventRecord(c->evq, s));
+        HIPCHK(c, hipStreamWaitEvent(p.s, c->evq, 0));
+    }
     // prologue: pending reset / position, position snapshot, zeroed chunk counters
     st = resolve_feed_timing(c);
     if (st) return st;
