@@ -576,12 +576,15 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
     p.n_blocks = (n_tiles + TSCAN_BLOCK - 1) / TSCAN_BLOCK;
     p.d = d;
     p.len = len;
-    // the chunk runs on the low-priority stream, after everything queued so far
-    // (KMERHIP_ONE_STREAM=1: on the caller's stream itself, no cross-stream
-    // waits -- A/B experiments)
+    // the chunk runs on the caller's stream (the context's own for the C-ABI
+    // feeds), after everything queued so far: no cross-stream event waits
+    // between the previous finish, the chunk and its finish (C2: 1.009 ->
+    // 0.981 ms per step; two sessions in rotation still overlap, one's finish
+    // with the other's chunk).  KMERHIP_ONE_STREAM=0: the chunk on a separate
+    // low-priority stream (A/B experiments)
     static const bool one_stream = [] {
         const char *e = getenv("KMERHIP_ONE_STREAM");
-        return e && strcmp(e, "1") == 0;
+        return !(e && strcmp(e, "0") == 0);
     }();
     p.s = one_stream ? s : c->sstream;
     if (p.s != s) {
