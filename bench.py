@@ -215,9 +215,71 @@ def table_phase_bytes(nbytes, n_keys, canonical):
             "scatter2": 16 * n_keys, "final": 8 * n_keys + 8 * canonical}
 
 
+def rank_envs(n, port, base=None):
+    """Environment of each of the n worker processes `--gpus n` starts when no
+    launcher set WORLD_SIZE: one process per GPU, rank r on device r."""
+    base = dict(os.environ if base is None else base)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                  "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+        e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")     # (RCCL across processes: dmabuf IPC only)
+        envs.append(e)
+    return envs
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, dry_run=False, script=None):
+    """`python bench.py --gpus N` without a launcher: start N child processes
+    of this script, one per GPU (ranks 0..N-1, rendezvous on 127.0.0.1), and
+    return the exit status of the job (the first failing rank's, else 0).
+    Runs before anything touches the GPU, and never execs: the children are
+    fresh processes whose stdout is this process's (rank 0 prints the line)."""
+    import subprocess
+    envs = rank_envs(n, free_port())
+    cmd = [sys.executable, script or os.path.abspath(__file__)] + [a for a in argv if a != "--dry-run-launch"]
+    if dry_run:
+        keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
+        for e in envs:
+            print(json.dumps({"cmd": cmd, "env": {k: e[k] for k in keys}}))
+        return 0
+    procs = [subprocess.Popen(cmd, env=e) for e in envs]
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                r = p.poll()
+                if r is None:
+                    continue
+                live.remove(p)
+                if r != 0 and rc == 0:
+                    rc = r
+                    for q in live:            # one rank failed: the others would wait forever in a collective
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc if rc >= 0 else 128 - rc
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs (ranks).  Under torch.distributed.run WORLD_SIZE must equal it; without a launcher "
+                         "bench.py starts the N rank processes itself")
+    ap.add_argument("--dry-run-launch", action="store_true",
+                    help="print the rank environments --gpus N would start and exit (no GPU)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--reads", type=int, default=10_000_000, help="reads per GPU")
@@ -249,6 +311,10 @@ def main():
                          "gather: all partials to rank 0.  Default: dense for c4 (bytes independent of the input "
                          "size), hits otherwise")
     args = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.dry_run_launch):
+        sys.exit(launch_ranks(max(1, args.gpus), sys.argv[1:], dry_run=args.dry_run_launch))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        sys.exit("bench.py: WORLD_SIZE=%s but --gpus %d" % (os.environ["WORLD_SIZE"], args.gpus))
     # per-config defaults (explicit flags still win)
     argv = " ".join(sys.argv)
     from kmerjs_amd._native import FLAG_UNORDERED
@@ -309,6 +375,8 @@ def main():
     if os.environ.get("KMERHIP_ONE_DEVICE") == "1":
         local = 0
     backend = os.environ.get("KMERHIP_DIST_BACKEND", "nccl")
+    one_device = os.environ.get("KMERHIP_ONE_DEVICE") == "1"
+    rccl_ranks = 0
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
@@ -316,6 +384,10 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        world = dist.get_world_size()
+        rank = dist.get_rank()
+        if dist.get_backend() == "nccl":
+            rccl_ranks = world
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -473,6 +545,38 @@ def main():
             want = oracle.count_buffer(oracle.synth_fastq(args.seed, 0, world * args.reads), prefix, args.k, 1)
             assert got == want, "distributed result differs from the oracle"
             print("verify: %d entries equal the oracle" % len(want), file=sys.stderr)
+    verified_table = None
+    if os.environ.get("KMERHIP_BENCH_VERIFY") == "1" and table and world > 1 and args.config in ("c3", "c4", "c2"):
+        # rehearsal check of the table exchange: the ranks' table digests (linear in
+        # the counts, kmer_table_digest) add up to the digest of ONE context's table
+        # over the whole job's input, and so do the table statistics
+        d = ctr.table_digest()
+        dig = torch.tensor([d - (1 << 64) if d >= (1 << 63) else d], dtype=torch.int64)   # (sum wraps mod 2^64)
+        st = torch.tensor(list(ctr.table_stats()), dtype=torch.int64)
+        cdev = "cpu" if dist.get_backend() == "gloo" else dev
+        dig, st = dig.to(cdev), st.to(cdev)
+        dist.all_reduce(dig)
+        dist.all_reduce(st)
+        if rank == 0:
+            whole = torch.empty(world * args.reads * RECORD, dtype=torch.uint8, device=dev)
+            from kmerjs_amd import synth_fastq_device
+            synth_fastq_device(whole.data_ptr(), args.seed, 0, world * args.reads)
+            torch.cuda.synchronize()
+            one = Counter(k=args.k, prefix=prefix, device=local, flags=args.flags)
+            one.reset()
+            one.feed_device(whole.data_ptr(), whole.numel())
+            one.finish(want_result=False)
+            want_d, want_s = one.table_digest(), one.table_stats()
+            one.close()
+            del whole
+            got_d = int(dig.item()) & ((1 << 64) - 1)
+            got_s = tuple(int(x) for x in st.tolist())
+            # (record keys were moved to rank 0, so their share of stats counts once)
+            assert got_d == want_d, "table digest of the ranks %x != one context's %x" % (got_d, want_d)
+            assert got_s == tuple(want_s), "table stats of the ranks %s != one context's %s" % (got_s, want_s)
+            verified_table = {"digest": "%016x" % want_d, "stats": list(want_s)}
+            print("verify: table digest %016x and stats %s of the %d ranks equal one context's table"
+                  % (want_d, list(want_s), world), file=sys.stderr)
 
     if rank == 0:
         windows_step = wl["windows_total"]
@@ -531,6 +635,7 @@ def main():
             algo_bytes = nbytes + 24 * (accepted / world)
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
         traffic = load_traffic(args, kern_name)
+        coll = "RCCL" if rccl_ranks else (dist.get_backend().upper() if world > 1 else "")
         out = {
             "metric": "k-mers/sec + distinct-kmers/sec, k=%d 150bp synthetic FASTQ, 1/2/4/8 GPU" % args.k,
             "value": value,
@@ -555,14 +660,18 @@ def main():
                        "bytes_per_gpu": nbytes,
                        "pipeline": ("%d sessions in rotation: finishes overlap later scans" % nctx if nctx > 1
                                     else "off (steps in sequence)"),
-                       "parallelism": "dp%d (reads sharded; %s%s)" % (
-                           world, "RCCL all-to-all of pass-1 keys by hash-space slice, per-rank table finish"
-                           if table else {"hits": "RCCL all-to-all of hits by key range, per-rank finish",
-                        "alltoall": "RCCL all-to-all of partials by key range, per-rank finish",
-                        "dense": "RCCL reduce-scatter of dense count / first-occurrence arrays, per-rank finish"}.get(
-                            args.merge, "RCCL gather of partials, finish on rank 0"),
+                       "parallelism": "dp1 (one GPU; no collective)" if world == 1 else
+                       "dp%d (reads sharded; %s%s%s)" % (
+                           world, coll + " all-to-all of pass-1 keys by hash-space slice, per-rank table finish"
+                           if table else {"hits": coll + " all-to-all of hits by key range, per-rank finish",
+                        "alltoall": coll + " all-to-all of partials by key range, per-rank finish",
+                        "dense": coll + " reduce-scatter of dense count / first-occurrence arrays, per-rank finish"}.get(
+                            args.merge, coll + " gather of partials, finish on rank 0"),
                            "; + alltoallv gather of the ordered ranges to rank 0 and device merge into one "
-                           "Map-order result" if args.collect and world > 1 else "")},
+                           "Map-order result" if args.collect else "",
+                           "; REHEARSAL: every rank on device 0" if one_device else ""),
+                       "backend": "none" if world == 1 else ("rccl" if rccl_ranks else dist.get_backend())},
+            "rccl_ranks": rccl_ranks,
             "distinct_kmers_per_s": distinct * args.steps / elapsed,
             "distinct_kmers": distinct,
             "accepted_windows": accepted,
@@ -573,6 +682,8 @@ def main():
                          "algorithmic_bytes_per_launch": algo_bytes, "kernel_ms": kern_ms,
                          "step_frac": step_frac, "step_bytes_per_window": b_in + b_table},
         }
+        if verified_table is not None:
+            out["verified_table"] = verified_table
         if phases is not None:
             out["table_phase_ms"] = phases
             out["canonical_kmers"] = canonical

@@ -74,10 +74,8 @@ enum {
      * kmer_count_file / kmer_count_buffer switch to it by themselves when a
      * longer line turns up (the count is redone once); the device-resident
      * calls and multi-GPU group contexts need the flag. */
-    KMER_FLAG_LONG_LINES = 1u << 7,
-    /* experiments only (results are WRONG with these set): ablate parts of the tile scan */
-    KMER_FLAG_ABLATE_HITS = 1u << 8,   /* drop every prefix candidate */
-    KMER_FLAG_ABLATE_SWAR = 1u << 9    /* skip the SWAR prefix scan entirely */
+    KMER_FLAG_LONG_LINES = 1u << 7
+    /* bits 8..15 are reserved (kmer_open rejects them) */
 };
 
 typedef struct {

@@ -47,6 +47,9 @@
 
 using namespace kmerhip;
 
+// every KMER_FLAG_* of include/kmer_api.h
+constexpr uint32_t KMER_FLAGS_PUBLIC = 0xFFu;
+
 namespace {
 
 // PACKED: tile scan, packed keys; TILE_REC: tile scan, records (host merge);
@@ -525,7 +528,7 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
     a.ovf_count = c->d_ovf_count;
     a.ovf_cap = c->ovf.cap;
     a.err = c->d_err;
-    a.ablate = (c->p.flags >> 8) & 0xFFu;   // KMER_FLAG_ABLATE_* (experiments only)
+    a.ablate = KH_EXPERIMENTS ? (c->p.flags & KMERHIP_XFLAG_MASK) >> 8 : 0u;   // (experiments only)
     a.hits_hi = c->hits_hi.p;
     a.ovf_hi = c->ovf_hi.p;
 
@@ -583,7 +586,7 @@ kmer_status scan_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_ti
     // with the other's chunk).  KMERHIP_ONE_STREAM=0: the chunk on a separate
     // low-priority stream (A/B experiments)
     static const bool one_stream = [] {
-        const char *e = getenv("KMERHIP_ONE_STREAM");
+        const char *e = exp_env("KMERHIP_ONE_STREAM");
         return !(e && strcmp(e, "0") == 0);
     }();
     p.s = one_stream ? s : c->sstream;
@@ -831,7 +834,7 @@ kmer_status chunk_lines(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_
     // one pass over the input: per-tile counts + positions in per-tile slots
     // (KMERHIP_NL=two: the count pass + a second, writing pass; A/B experiments)
     static const bool two = [] {
-        const char *e = getenv("KMERHIP_NL");
+        const char *e = exp_env("KMERHIP_NL");
         return e && strcmp(e, "two") == 0;
     }();
     HIPCHK(c, c->tcount.ensure(n_tiles, s));
@@ -1191,11 +1194,11 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1 = nullptr, uint32_t qlo
     f.nd = c->tnd.p;
     const uint64_t mean = n / TAB_NQ;
     uint64_t range_keys = 3000;               // mean keys per LDS range (load ~0.37: short probes; measured best at C3)
-    if (const char *rk = getenv("KMERHIP_TAB_RANGE")) range_keys = std::max<uint64_t>(64, strtoull(rk, nullptr, 10));
+    if (const char *rk = exp_env("KMERHIP_TAB_RANGE")) range_keys = std::max<uint64_t>(64, strtoull(rk, nullptr, 10));
     while (f.sub_bits < 16 && (mean >> f.sub_bits) > range_keys) ++f.sub_bits;
     f.range_keys = (uint32_t)std::min<uint64_t>(range_keys, TAB_CAP);
     f.cap = (c->p.flags & KMER_FLAG_TABLE_SPLIT_TEST) ? 64 : TAB_CAP;
-    if (const char *ab = getenv("KMERHIP_TAB_ABLATE")) f.ablate = (uint32_t)atoi(ab);   // experiments only
+    if (const char *ab = exp_env("KMERHIP_TAB_ABLATE")) f.ablate = (uint32_t)atoi(ab);   // experiments only
     f.big = c->tbig.p;
     f.big_count = c->tstats.p + 3;
     f.big_cap = c->tbig.cap;
@@ -1216,7 +1219,7 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1 = nullptr, uint32_t qlo
     const uint32_t fgrid = (uint32_t)std::max(c->n_cu, 1);
     std::vector<uint64_t> hprof;
 #ifdef TAB_PROF
-    if (getenv("KMERHIP_TAB_PROF")) {         // experiments (-DTAB_PROF build): per-phase clocks of the final kernel
+    if (exp_env("KMERHIP_TAB_PROF")) {         // experiments (-DTAB_PROF build): per-phase clocks of the final kernel
 #else
     if (false) {
 #endif
@@ -1228,7 +1231,7 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1 = nullptr, uint32_t qlo
     // general kernel (hash path, range splits) takes the ones it leaves
     // (crowded buckets, many copies of a key).  KMERHIP_TAB_FINAL=general: the
     // general kernel alone (A/B experiments).
-    const char *fk = getenv("KMERHIP_TAB_FINAL");
+    const char *fk = exp_env("KMERHIP_TAB_FINAL");
     const bool sort_first = !(fk && strcmp(fk, "general") == 0) && !f.prof &&
                             !(c->p.flags & KMER_FLAG_TABLE_SPLIT_TEST);
     HIPCHK(c, hipEventRecord(c->tev[2], s));
@@ -2438,6 +2441,8 @@ const char *kmer_last_error(const kmer_ctx *ctx) { return ctx ? ctx->err.c_str()
 kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
     if (!pp || !out) return KMER_E_BAD_PARAM;
     if (pp->k == 0 || pp->step == 0 || (pp->prefix_len && !pp->prefix)) return KMER_E_BAD_PARAM;
+    // reserved / experiment-only flag bits (KMERHIP_XFLAG_*, a -DKMERHIP_EXPERIMENTS build)
+    if (!KH_EXPERIMENTS && (pp->flags & ~KMER_FLAGS_PUBLIC)) return KMER_E_BAD_PARAM;
     *out = nullptr;
     if (pp->ndev > 1) {
         if (pp->ndev > 64) return KMER_E_BAD_PARAM;

@@ -3,8 +3,30 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace kmerhip {
+
+// ---- experiment switches ----------------------------------------------------
+// A/B switches (KMERHIP_* environment variables) and ablations (the
+// KMERHIP_XFLAG_ABLATE_* bits of kmer_params.flags; results are WRONG with
+// them) exist only in a -DKMERHIP_EXPERIMENTS build of the library, made by
+// tools/ for timing studies.  The shipping libkmerhip.so reads no environment
+// variable, and kmer_open rejects the ablation bits (KMER_E_BAD_PARAM).
+#ifdef KMERHIP_EXPERIMENTS
+inline const char *exp_env(const char *name) { return getenv(name); }
+#define KH_ABLATE(a) ((a).ablate)
+constexpr bool KH_EXPERIMENTS = true;
+#else
+inline const char *exp_env(const char *) { return nullptr; }
+#define KH_ABLATE(a) 0u
+constexpr bool KH_EXPERIMENTS = false;
+#endif
+enum : uint32_t {
+    KMERHIP_XFLAG_ABLATE_HITS = 1u << 8,   // drop every prefix candidate
+    KMERHIP_XFLAG_ABLATE_SWAR = 1u << 9,   // skip the SWAR prefix scan
+    KMERHIP_XFLAG_MASK = 0xFFu << 8,       // bits 8..15: tile-scan ablations (ScanArgs::ablate)
+};
 
 // ---- tile geometry (tile kernel) -------------------------------------------
 // One workgroup owns one 16 KiB tile of the input.  The tile plus a front halo

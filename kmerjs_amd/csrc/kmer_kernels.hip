@@ -553,11 +553,11 @@ __device__ __forceinline__ void emit_hit(const ScanArgs &a, const uint8_t *buf, 
     r.qm = (uint32_t)q | (strand << 14) | ((exotic ? 1u : 0u) << 15) | ((lstart >= 0 ? 1u : 0u) << 16) | (slot << 17);
     r.c_local = c_local;
     r.lstart = lstart >= 0 ? (uint32_t)lstart : 0u;
-    if (a.ablate & 8u) {                         // experiments: the record computed, not stored
+    if (KH_ABLATE(a) & 8u) {                         // experiments: the record computed, not stored
         if (r.code == 0x0123456789ABCDEFull && r.qm == 7u && r.lstart == 3u) atomicOr(a.err, 0u);
         return;
     }
-    if (a.ablate & 16u) {                        // experiments: every record to the same 64 slots
+    if (KH_ABLATE(a) & 16u) {                        // experiments: every record to the same 64 slots
         a.hits[threadIdx.x & 63u] = r;
         return;
     }
@@ -666,7 +666,7 @@ __global__ __launch_bounds__(TPB) void scan_tile_kernel(ScanArgs a) {
     uint64_t packed = 0;         // 16-bit '\n' count of chunk i in bits [16i, 16i+16)
     // only the last tile has bytes past len (sentinels): keep the masking out of the hot loop
     const bool tail_tile = (uint64_t)(g0 + TILE) > len;
-    const bool do_swar = !(a.ablate & 2u);
+    const bool do_swar = !(KH_ABLATE(a) & 2u);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int c = tid + TPB * i;
@@ -759,7 +759,7 @@ __global__ __launch_bounds__(TPB) void scan_tile_kernel(ScanArgs a) {
         a.tsum[tile].lnl = lp >= 0 ? a.abs_offset + (uint64_t)(g0 + lp + 1) : 0;
     }
     const uint32_t k = a.k, plen = a.plen;
-    if (plen > k || (a.ablate & 1u)) cand = 0;
+    if (plen > k || (KH_ABLATE(a) & 1u)) cand = 0;
     const uint32_t *pw = (const uint32_t *)s_pr;             // P words, then rc(P) words
 
     // ---- candidate words -> LDS queue (one LDS atomic per wave) -> verified
@@ -817,7 +817,7 @@ __device__ __forceinline__ void verify_emit(const ScanArgs &a, const uint8_t *bu
         const uint32_t mk = n >= 4 ? 0xFFFFFFFFu : ((1u << (8 * n)) - 1u);
         ok = ((lds_word(buf, q + (int)b) ^ pw[(strand ? KMAX_TILE / 4 : 0) + b / 4]) & mk) == 0;
     }
-    if (a.ablate & 4u) {                         // experiments: verified, no record
+    if (KH_ABLATE(a) & 4u) {                         // experiments: verified, no record
         if (ok) atomicAdd(&sh.nx, 0u);
         return;
     }
@@ -970,7 +970,7 @@ __global__ __launch_bounds__(TPB) void scan_planes_kernel(ScanArgs a, PlaneArgs 
         mf[h] = plane_match(L[h], H[h], L[h + 1], H[h + 1], pa.kl, pa.kh, pb, SL, SH);
         mr[h] = plane_match(L[h], H[h], L[h + 1], H[h + 1], pa.rl, pa.rh, pb, SL, SH);
     }
-    if (a.k < a.plen || (a.ablate & 1u)) mf[0] = mf[1] = mr[0] = mr[1] = 0;
+    if (a.k < a.plen || (KH_ABLATE(a) & 1u)) mf[0] = mf[1] = mr[0] = mr[1] = 0;
 
     // ---- block scan of the per-thread '\\n' counts -> cpre per chunk ----
     __syncthreads();
@@ -1096,10 +1096,10 @@ __device__ __forceinline__ uint64_t resolve_hit(const HitArgs &a, const HitRec &
     const bool seq = (li & 3) == 1;
     const uint64_t maxrel = (1ull << a.pbits) - 1ull;
     if (rel > maxrel) {
-        if (seq && !a.ablate) atomicOr(a.err, ERR_LINE_TOO_LONG);
+        if (seq && !KH_ABLATE(a)) atomicOr(a.err, ERR_LINE_TOO_LONG);
         rel = maxrel;                            // (non-sequence lines only need a consistent order)
     }
-    if ((li >> (63 - a.pbits)) && !a.ablate) atomicOr(a.err, ERR_LINE_TOO_LONG);   // (line field full: long-line mode)
+    if ((li >> (63 - a.pbits)) && !KH_ABLATE(a)) atomicOr(a.err, ERR_LINE_TOO_LONG);   // (line field full: long-line mode)
     const uint64_t order = (li << (a.pbits + 1)) | ((uint64_t)strand << a.pbits) | (strand ? maxrel - rel : rel);
     *order_out = order;
     const uint32_t sp = (uint32_t)(s0 + 64);     // < 2^15

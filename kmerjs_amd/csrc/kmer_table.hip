@@ -805,7 +805,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
     // start cache must hold u's start, i.e. u <= cbase + TAB_SC)
     // (groups for the sort path fill the registers; the hash path's ranges
     // split a group whose distinct keys overflow the table)
-    const uint64_t gk = !(a.ablate & 4) ? (uint64_t)TAB_REG_MAX : rk;
+    const uint64_t gk = !(KH_ABLATE(a) & 4) ? (uint64_t)TAB_REG_MAX : rk;
     auto unit_end = [&](uint32_t u) -> uint32_t {
         uint32_t e = u + 1;
         uint64_t tot = sc[u + 1 - cbase] - sc[u - cbase];
@@ -887,7 +887,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
         // LDS atomic per key and plain LDS stores, instead of a CAS + a count
         // add per key (plus probes) and a slot scan per range.  A unit with a
         // crowded run of bins (many copies of one key) takes the hash path below.
-        if (inreg && !(a.ablate & 4)) {
+        if (inreg && !(KH_ABLATE(a) & 4)) {
             // bins: the top 12 bits of (bucket offset << 44 | remainder), so a
             // group's buckets occupy consecutive bin ranges
             const uint32_t bsh = TAB_RBITS + (g > 1 ? 32 - __clz(g - 1) : 0) - 12;
@@ -1010,7 +1010,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
                 const int left = (int)n - (int)t;
 #pragma unroll
                 for (int j = 0; j < TAB_KPT; ++j)
-                    if (left > j * (int)TAB_FWG && kn[j] >= rlo && kn[j] < rhi && !(a.ablate & 1)) pend |= 1u << j;
+                    if (left > j * (int)TAB_FWG && kn[j] >= rlo && kn[j] < rhi && !(KH_ABLATE(a) & 1)) pend |= 1u << j;
                 // (groups of four keys: enough CAS round trips in flight
                 // without spilling the held keys)
                 uint32_t cl = 0;
@@ -1058,7 +1058,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
             // emit (and clear) the occupied slots: per wave, one LDS counter
             // bump per bucket present among the wave's entries
 #pragma unroll 1
-            for (uint32_t i = t; i < TAB_SLOTS && !(a.ablate & 2); i += TAB_FWG) {
+            for (uint32_t i = t; i < TAB_SLOTS && !(KH_ABLATE(a) & 2); i += TAB_FWG) {
                 const uint64_t key = tkey[i];
                 const bool v = key != TAB_EMPTY;
                 uint64_t m = __ballot(v);
@@ -1325,10 +1325,10 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                     const int j = g0 + u;
                     const bool valid = left > j * (int)TAB_SWG;
                     const uint32_t b = pk[j] >> 14;
-                    const uint32_t b0 = bst[b], b1 = (a.ablate & 8) ? b0 : b + 1 < TS_NB ? bst[b + 1] : (uint32_t)n;
+                    const uint32_t b0 = bst[b], b1 = (KH_ABLATE(a) & 8) ? b0 : b + 1 < TS_NB ? bst[b + 1] : (uint32_t)n;
                     const uint32_t c = valid ? b1 - b0 : 0u;
                     bb[u] = b0 | c << 14;
-                    cf[u] = valid ? ((a.ablate & 8) ? 0x101u : 0x100u) : 0u;   // (experiments: no bin scan)
+                    cf[u] = valid ? ((KH_ABLATE(a) & 8) ? 0x101u : 0x100u) : 0u;   // (experiments: no bin scan)
                     cmax = max(cmax, c);
                 }
                 for (uint32_t m = 0; m < cmax; ++m) {
@@ -1388,9 +1388,9 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                         }
                     }
                     if (first) {
-                        if (!(a.ablate & 32))
+                        if (!(KH_ABLATE(a) & 32))
                             a.out[(ONE ? s0 : sc[q + ql - cbase]) + pos] = ((xj & TAB_RMASK) << 20) | cnt;
-                        if (!(a.ablate & 16)) account(qbase + xj, cnt);
+                        if (!(KH_ABLATE(a) & 16)) account(qbase + xj, cnt);
                     }
                 }
             }
@@ -1433,7 +1433,7 @@ hipError_t launch_tab_hist1(const TabArgs &a, hipStream_t s) {
 hipError_t launch_tab_scatter1(const TabArgs &a, hipStream_t s) {
     // KMERHIP_TAB_S1=full: one 1,024-thread workgroup per CU (A/B experiments)
     static const bool half = [] {
-        const char *e = getenv("KMERHIP_TAB_S1");
+        const char *e = exp_env("KMERHIP_TAB_S1");
         return !(e && strcmp(e, "full") == 0);
     }();
     if (half) {
@@ -1480,7 +1480,7 @@ hipError_t launch_tab_scatter2(const uint64_t *B1, const TabUnit *units, uint32_
                                uint64_t *B2, hipStream_t s) {
     // KMERHIP_TAB_S2=plain: the 16 K-round kernel without aligned write-out (A/B experiments)
     static const bool plain = [] {
-        const char *e = getenv("KMERHIP_TAB_S2");
+        const char *e = exp_env("KMERHIP_TAB_S2");
         return e && strcmp(e, "plain") == 0;
     }();
     if (plain)

@@ -54,3 +54,34 @@ def test_product_does_not_reference_oracle():
                 with open(os.path.join(root, fn), encoding="utf-8") as f:
                     src = f.read()
                 assert "oracle" not in src.replace("oracle/kmer_oracle.c", ""), fn
+
+
+EXPERIMENT_ENV = ("KMERHIP_TAB_ABLATE", "KMERHIP_TAB_RANGE", "KMERHIP_TAB_FINAL", "KMERHIP_NL", "KMERHIP_TAB_S1",
+                  "KMERHIP_TAB_S2", "KMERHIP_ONE_STREAM", "KMERHIP_TAB_PROF")
+
+
+def test_shipping_library_has_no_experiment_switches():
+    """the A/B switches exist only in a -DKMERHIP_EXPERIMENTS
+    build (tools/); the default library cannot read them, so a stray variable
+    in a user's environment changes nothing."""
+    with open(os.path.join(REPO, "kmerjs_amd", "libkmerhip.so"), "rb") as f:
+        blob = f.read()
+    present = [n for n in EXPERIMENT_ENV if n.encode() in blob]
+    assert not present, present
+
+
+def test_header_has_no_result_corrupting_flag():
+    with open(os.path.join(REPO, "include", "kmer_api.h")) as f:
+        text = f.read()
+    assert "ABLATE" not in text and "WRONG" not in text
+
+
+def test_open_rejects_reserved_flag_bits_without_gpu():
+    from kmerjs_amd import _native
+    for bit in range(8, 16):
+        try:
+            _native.Counter(flags=1 << bit)
+        except _native.KmerError as e:
+            assert e.status == 2
+        else:
+            raise AssertionError("accepted flag bit %d" % bit)
