@@ -100,9 +100,13 @@ typedef struct {
      * canonical mode: every device's pass-1 keys go to the device that owns
      * their slice of the hash space, which builds that slice of the table;
      * kmer_table_stats / kmer_table_digest of a group add up its devices'.
-     * Configurations without packed partials or a table (non-ACGT prefix,
-     * step > 1, k > 64, keys of 64 bits or more: k - |P| >= 32) run on
-     * devices[0] alone.  The other device-resident entry
+     * Every ordered configuration with packed keys is sharded too (any prefix
+     * bytes, step > 1).  Only the configurations without packed partials run
+     * on devices[0] alone: k > 64 and unprefixed k > 31 (the general path),
+     * keys of 64 bits or more (k - |P| >= 32), and KMER_FLAG_NO_DENSE.  A
+     * group count that meets a line longer than 2^23 bytes is redone in
+     * long-line mode on every device, as a single-device count is.  The other
+     * device-resident entry
      * points are single-device only (KMER_E_STATE on a group).  0 or 1 =
      * single device `device`. */
     uint32_t ndev;

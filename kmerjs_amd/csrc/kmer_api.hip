@@ -236,6 +236,9 @@ struct kmer_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr;
     hipEvent_t evw = nullptr;      // cross-stream wait (no timing)
     double scan_ms = 0.0, feed_ms = 0.0, finish_ms = 0.0;
+    // progress of the current whole-input call (report_progress: monotone across a retry)
+    bool progress_any = false;
+    uint64_t progress_hw = 0;
 };
 
 namespace {
@@ -263,6 +266,17 @@ const uint64_t FILE_BATCH = 256ull << 20;     // kmer_count_file read-ahead batc
         t = (ctx)->tmp.p;                                                               \
         HIPCHK(ctx, CALL);                                                              \
     } while (0)
+
+// Progress callback of kmer_count_file / kmer_count_buffer: monotone over the
+// whole call, so a long-line retry (which reads the input again from the
+// start) reports nothing until it passes what was already reported.
+void report_progress(kmer_ctx *c, uint64_t done, uint64_t total) {
+    if (!c->p.progress) return;
+    if (c->progress_any && done <= c->progress_hw) return;
+    c->progress_any = true;
+    c->progress_hw = done;
+    c->p.progress(c->p.progress_user, done, total);
+}
 
 kmer_status fail(kmer_ctx *c, kmer_status s, const std::string &msg) {
     c->err = msg;
@@ -1775,9 +1789,9 @@ kmer_status feed_host(kmer_ctx *c, const uint8_t *bytes, uint64_t len, bool repo
         kmer_status st = feed(c, c->batch.p, n, c->stream);
         if (st) return st;
         pos = end;
-        if (report && c->p.progress) c->p.progress(c->p.progress_user, pos, len);
+        if (report) report_progress(c, pos, len);
     }
-    if (report && len == 0 && c->p.progress) c->p.progress(c->p.progress_user, 0, 0);
+    if (report && len == 0) report_progress(c, 0, 0);
     return KMER_OK;
 }
 
@@ -1852,6 +1866,7 @@ struct FileBatches : GroupSrc {
     struct Slot {
         std::unique_ptr<uint8_t[]> buf;
         uint64_t cap = 0, len = 0;
+        uint64_t zoff = 0;                           // gzip: compressed bytes read when the slot was filled
         int state = 0;                               // 0 free, 1 filled, 2 in use
         bool last = false;
     };
@@ -1867,6 +1882,7 @@ struct FileBatches : GroupSrc {
     kmer_status rd_st = KMER_OK;
     std::string rd_err;
     uint64_t next_fill = 0, next_take = 0, consumed = 0;
+    uint64_t consumed_z = 0;                         // gzip: compressed offset of the last batch taken
     std::vector<uint8_t> carry;
     std::unordered_map<const uint8_t *, std::unique_ptr<uint8_t[]>> big;   // batches of lines longer than HEAD
     std::unordered_map<const uint8_t *, size_t> slot_of;
@@ -1890,9 +1906,13 @@ struct FileBatches : GroupSrc {
             return KMER_E_IO;
         }
         struct stat sb;
-        if (fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode)) size = (uint64_t)sb.st_size;
+        const bool regular = fstat(fd, &sb) == 0 && S_ISREG(sb.st_mode);
+        if (regular) size = (uint64_t)sb.st_size;
         unsigned char magic[2] = {0, 0};
-        const bool gzip = pread(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b;
+        // a pipe, FIFO, socket or terminal (fs.createReadStream reads those too)
+        // cannot be pread: zlib reads it sequentially on the reader thread, and
+        // passes it through unchanged when it is not gzip (transparent mode)
+        const bool gzip = !regular || (pread(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b);
         batch = std::max<uint64_t>(batch_, 1);
         if (gzip) {
             gz = gzdopen(dup(fd), "rb");
@@ -1944,6 +1964,7 @@ struct FileBatches : GroupSrc {
                 gzerror(gz, &zerr);
                 if (zerr != Z_OK && zerr != Z_BUF_ERROR) st = KMER_E_IO;
                 eof = got < batch;
+                S.zoff = (uint64_t)std::max<z_off_t>(gzoffset(gz), 0);   // (gz is this thread's alone)
             } else if (!st) {
                 // parallel preads of [rd_off, rd_off + batch); a short read (end of
                 // file, or a file that is not regular) ends the input
@@ -2012,6 +2033,7 @@ struct FileBatches : GroupSrc {
             }
             Slot &S = ring[si];
             consumed += S.len;
+            consumed_z = S.zoff;
             const bool last = S.last;
             uint8_t *start;
             uint64_t have;
@@ -2079,9 +2101,11 @@ struct FileBatches : GroupSrc {
             slot_of.erase(it);
         }
     }
-    // progress: (bytes read, file size) -- for gzip the compressed offset and size
+    // progress: (bytes taken, file size) -- for gzip the compressed offset of the
+    // batches taken and the compressed size.  Called on the consuming thread
+    // only (never touches the gzFile, which the reader thread owns)
     void progress(uint64_t *d, uint64_t *t) override {
-        *d = gz ? (uint64_t)std::max<z_off_t>(gzoffset(gz), 0) : consumed;
+        *d = gz ? consumed_z : consumed;
         *t = size;
         if (*d > *t && *t) *d = *t;
     }
@@ -2241,13 +2265,13 @@ kmer_status group_count(kmer_ctx *g, GroupSrc &src, kmer_result **out) {
         if (g->p.progress) {                          // (batches handed to the devices)
             uint64_t d = 0, t = 0;
             src.progress(&d, &t);
-            g->p.progress(g->p.progress_user, d, t);
+            report_progress(g, d, t);
         }
     }
     if (nb == 0 && g->p.progress) {                   // (an empty input: one event)
         uint64_t d = 0, t = 0;
         src.progress(&d, &t);
-        g->p.progress(g->p.progress_user, d, t);
+        report_progress(g, d, t);
     }
     for (auto &w : wk) {
         {
@@ -2709,12 +2733,20 @@ namespace {
 // A whole-input count that met a sequence line longer than the default
 // order key's position field (2^23 bytes: a FASTA contig or chromosome) is
 // redone once in long-line mode (2^40-byte lines, up to 2^23 lines).
+// A group context redoes it on every device.
+void set_pbits(kmer_ctx *c, uint32_t pbits) {
+    c->pbits = pbits;
+    for (kmer_ctx *x : c->group) x->pbits = pbits;
+}
+
 kmer_status with_long_line_retry(kmer_ctx *c, const std::function<kmer_status()> &count) {
+    c->progress_any = false;
+    c->progress_hw = 0;
     kmer_status st = count();
     if (st == KMER_E_LINE_TOO_LONG && c->pbits == PBITS_DEFAULT && c->mode != MODE_TABLE) {
-        c->pbits = PBITS_LONG;
+        set_pbits(c, PBITS_LONG);
         st = count();
-        c->pbits = PBITS_DEFAULT;
+        set_pbits(c, PBITS_DEFAULT);
     }
     return st;
 }
@@ -2737,7 +2769,7 @@ kmer_status count_file_once(kmer_ctx *c, const char *path, kmer_result **out);
 kmer_status kmer_count_buffer(kmer_ctx *c, const uint8_t *bytes, size_t len, kmer_result **out) {
     if (!c || !out || (!bytes && len)) return KMER_E_BAD_PARAM;
     *out = nullptr;
-    if (!c->group.empty()) return group_count_buffer(c, bytes, len, out);
+    if (!c->group.empty()) return with_long_line_retry(c, [&] { return group_count_buffer(c, bytes, len, out); });
     if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
     return with_long_line_retry(c, [&] { return count_buffer_once(c, bytes, len, out); });
 }
@@ -2745,7 +2777,7 @@ kmer_status kmer_count_buffer(kmer_ctx *c, const uint8_t *bytes, size_t len, kme
 kmer_status kmer_count_file(kmer_ctx *c, const char *path, kmer_result **out) {
     if (!c || !path || !out) return KMER_E_BAD_PARAM;
     *out = nullptr;
-    if (!c->group.empty()) return group_count_file(c, path, out);
+    if (!c->group.empty()) return with_long_line_retry(c, [&] { return group_count_file(c, path, out); });
     return with_long_line_retry(c, [&] { return count_file_once(c, path, out); });
 }
 
@@ -2773,7 +2805,7 @@ kmer_status count_file_once(kmer_ctx *c, const char *path, kmer_result **out) {
         if (!st && c->p.progress) {
             uint64_t d = 0, t = 0;
             src.progress(&d, &t);
-            c->p.progress(c->p.progress_user, d, t);
+            report_progress(c, d, t);
         }
     }
     if (!st && rst) st = fail(c, rst, err + " on " + path);
@@ -2784,7 +2816,7 @@ kmer_status count_file_once(kmer_ctx *c, const char *path, kmer_result **out) {
     if (c->p.progress && src.consumed == 0) {        // (an empty file: one event, as progress-stream's end)
         uint64_t d = 0, t = 0;
         src.progress(&d, &t);
-        c->p.progress(c->p.progress_user, d, t);
+        report_progress(c, d, t);
     }
     return finish(c, out);
 }

@@ -43,9 +43,28 @@ class KmerMap extends Map {
     }
 
     static fromNative(res, indexer = null) {
+        return new KmerMap('', [0], []).adopt(res, indexer);
+    }
+
+    // Become the packed native result `res` (replacing any content): how
+    // readFile() fills the very Map object the constructor created, so that a
+    // holder of this.kmerMap sees the counts (lib/kmers.js:76, :178 resolve the
+    // constructor's Map).
+    adopt(res, indexer = null) {
+        super.clear();
         const n = res.counts.length;
-        const all = n ? res.keys.latin1Slice(0, res.offsets[n]) : '';
-        return new KmerMap(all, res.offsets, res.counts, res.keys, indexer);
+        this._all = n ? res.keys.latin1Slice(0, res.offsets[n]) : '';
+        this._buf = res.keys;
+        this._indexer = indexer;
+        this._off = res.offsets;
+        this._cnt = res.counts;
+        this._n = n;
+        this._tab = null;
+        this._mask = 0;
+        this._mod = null;
+        this._del = null;
+        this._ndel = 0;
+        return this;
     }
 
     _key(i) { return this._all.substring(this._off[i], this._off[i + 1]); }

@@ -17,14 +17,21 @@
  * promise with a RangeError, as Map.set throws in the reference.  kmersInLine() stays a synchronous CPU
  * loop over one line, as in the reference (lib/kmers.js:88-100).
  *
+ * this.kmerMap is created by the constructor (an empty KmerMap) and readFile()
+ * fills that same object, as the reference resolves the constructor's Map
+ * (lib/kmers.js:76, :178).  `event` is a Readable stream, as the reference's
+ * progress-stream is (lib/kmers.js:108, :183): 'progress' events, a
+ * progress() method returning the last one, and the stream ends after the
+ * count (no bytes flow through it: the file is read natively).
+ *
  * Documented divergences (error/diagnostic paths only): a missing file
  * rejects the promise (the reference throws from an unhandled stream error,
  * lib/kmers.js:139); progress is printed once per file instead of once per
  * line (lib/kmers.js:166-169); env 'browser' is not served by the GPU addon.
  */
 'use strict';
-const EventEmitter = require('events');
 const fs = require('fs');
+const stream = require('stream');
 const path = require('path');
 const { KmerMap } = require('./kmer_map.js');
 
@@ -148,7 +155,7 @@ class KmerJS {
         this.progress = progress;
         this.coverage = coverage;
         this.evalue = new BN(0.05);
-        this.kmerMap = new Map();
+        this.kmerMap = new KmerMap('', [0], []);   // a Map (instanceof Map), filled in place by readFile()
         this.kmerMapSize = 0;
         this.env = env;
         this.maxKeys = MAP_MAX_KEYS;     // the reference Map's limit (lib/kmers.js:95)
@@ -175,12 +182,17 @@ class KmerJS {
 
     readFile() {
         const kmerObj = this;
-        const event = new EventEmitter();
+        // progress-stream is a Transform the file is piped through (lib/kmers.js:108-110, :139);
+        // here the bytes never reach JS, so the stream carries only the events and ends
+        const event = new stream.PassThrough();
+        let lastProgress = null;
+        event.progress = () => lastProgress;
         kmerObj.lines = 0;
         kmerObj.bytesRead = 0;
         kmerObj.linesPerChunk = 0;
         const promise = new Promise((resolve, reject) => {
             if (kmerObj.env !== 'node') {
+                event.end();
                 reject(new Error("kmerjs_amd: env '" + kmerObj.env + "' is not served by the GPU addon"));
                 return;
             }
@@ -192,6 +204,7 @@ class KmerJS {
                     kmerObj.step, Number(process.env.KMERHIP_DEVICE || 0), modeFlags(kmerObj.mode), kmerObj.maxKeys,
                     kmerObj.batchBytes || 0, devices(kmerObj));
             } catch (e) {
+                event.end();
                 reject(e);
                 return;
             }
@@ -204,7 +217,7 @@ class KmerJS {
                 const runtime = (Date.now() - t0) / 1000;
                 const speed = runtime > 0 ? done / runtime : 0;
                 kmerObj.bytesRead = done;
-                event.emit('progress', {
+                lastProgress = {
                     percentage: total ? (100 * done) / total : 0,
                     transferred: done,
                     length: total,
@@ -213,7 +226,8 @@ class KmerJS {
                     runtime: Math.round(runtime),
                     delta: done - lastDone,
                     speed,
-                });
+                };
+                event.emit('progress', lastProgress);
                 lastDone = done;
             };
             // (batch events come from the reader thread; the completion may be
@@ -227,17 +241,22 @@ class KmerJS {
                 native().close(handle);
                 finished = true;
                 if (err) {
+                    event.end();
                     reject(err.status === KMER_E_TOO_MANY_KEYS ? tooManyKeys(err.message) : err);
                     return;
                 }
                 try {
-                    if (kmerObj.kmerMap.size === 0 && !(kmerObj.kmerMap instanceof KmerMap)) {
-                        kmerObj.kmerMap = KmerMap.fromNative(res, native().indexKeys);   // built lazily (kmer_map.js)
+                    if (kmerObj.kmerMap.size === 0 && kmerObj.kmerMap instanceof KmerMap) {
+                        kmerObj.kmerMap.adopt(res, native().indexKeys);   // the same object, filled lazily (kmer_map.js)
+                    } else if (kmerObj.kmerMap.size === 0 && kmerObj.kmerMap.constructor === Map) {
+                        // (a caller replaced it with a plain empty Map: fill that object too)
+                        foldResult(kmerObj.kmerMap, res);
                     } else {
                         foldResult(kmerObj.kmerMap, res);
                         if (kmerObj.kmerMap.size > kmerObj.maxKeys) throw tooManyKeys('Map maximum size exceeded');
                     }
                 } catch (e) {
+                    event.end();
                     reject(e);        // (never an exception escaping the completion callback)
                     return;
                 }
@@ -254,6 +273,7 @@ class KmerJS {
                     process.stdout.write('\n                               \n');
                 }
                 kmerObj.kmerMapSize = kmerObj.kmerMap.size;
+                event.end();
                 resolve(kmerObj.kmerMap);
             }, onProgress);
         });

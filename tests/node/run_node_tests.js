@@ -6,6 +6,7 @@ const assert = require('assert');
 const crypto = require('crypto');
 const fs = require('fs');
 const path = require('path');
+const stream = require('stream');
 
 const mode = process.argv[2] || 'cpu';
 const repo = path.resolve(__dirname, '..', '..');
@@ -48,6 +49,14 @@ function cpuTests() {
         assert.strictEqual(k.step, 1);
         assert.strictEqual(k.evalue.cmp(0.05), 0);
         assert.ok(k.kmerMap instanceof Map);
+    });
+    check('constructor Map is the Map readFile() fills; event is a Readable', () => {
+        const k = new KmerJS('f.fastq', 'ATGAC', 16, 1, 1, false, 'browser');
+        assert.ok(k.kmerMap instanceof Map && k.kmerMap instanceof lib.KmerMap && k.kmerMap.size === 0);
+        const rf = k.readFile();                     // (browser env: rejects without touching the GPU)
+        assert.ok(rf.event instanceof stream.Readable && typeof rf.event.pipe === 'function');
+        assert.strictEqual(rf.event.progress(), null);
+        rf.promise.catch(() => {});
     });
     check('legacy kmers()', () => {
         const m = new Map();
@@ -178,6 +187,24 @@ async function gpuTests() {
         } catch (e) {
             results.push({ name: `readFile ${c.input} '${c.prefix}' k=${c.k}`, ok: false, err: String(e) });
         }
+    }
+    // the resolved Map is the constructor's Map object (lib/kmers.js:76, :178), and
+    // event is a Readable that ends after the count, like progress-stream (:108, :183)
+    {
+        const file = path.join(repo, 'tests', 'golden', 'inputs', 'test_long.kmer.fastq');
+        const kj = new KmerJS(file, 'ATGAC', 16, 1, 1, false);
+        const before = kj.kmerMap;
+        const { promise, event } = kj.readFile();
+        let ended = false;
+        event.on('end', () => { ended = true; });
+        event.resume();
+        const m = await promise;
+        await new Promise((r) => setImmediate(r));
+        const last = event.progress();
+        const ok = m === before && kj.kmerMap === before && m.size === 401 && event instanceof stream.Readable
+            && ended && last !== null && last.transferred === fs.statSync(file).size;
+        results.push({ name: 'readFile fills the constructor Map; event is a Readable that ends', ok,
+            err: ok ? undefined : `same ${m === before} size ${m.size} ended ${ended} last ${JSON.stringify(last)}` });
     }
     // reference test/kmers.js:28-35 and :45-52 (via .promise: the reference tests call .then on the handle)
     const short = await new KmerJS(path.join(repo, 'tests', 'golden', 'inputs', 'test_short.fastq'), 'ATGAC', 16, 1, 1, false).readFile().promise;

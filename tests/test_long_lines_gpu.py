@@ -65,3 +65,40 @@ def test_device_feed_needs_the_flag(data):
     got = c.finish().entries()
     c.close()
     assert first_diff(got, oracle.count_buffer(data, b"ATGAC", 21, 1)) is None
+
+
+@pytest.mark.parametrize("prefix", [b"ATGAC", b"", b"NNA"])
+def test_group_context_retries_long_lines(data, prefix, tmp_path):
+    """A device group meets a > 2^23-byte line: the count is redone in long-line
+    mode on every device, as a single-device count is (group_count
+    had no retry).  The W == 1 path (k > 64 would be the general path; NNA is
+    the byte-SWAR packed path) and the sharded ordered paths."""
+    from kmerjs_amd import _native
+    from oracle import oracle
+    want = oracle.count_buffer(data, prefix, 21, 1)
+    p = tmp_path / "contig.fastq"
+    p.write_bytes(data)
+    c = _native.Counter(k=21, prefix=prefix, devices=[0, 0], batch_bytes=4 << 20)
+    assert first_diff(c.count_buffer(data).entries(), want) is None
+    assert first_diff(c.count_file(str(p)).entries(), want) is None
+    c.close()
+
+
+def test_progress_stays_monotone_across_the_long_line_retry(data, tmp_path):
+    """The retry re-reads the input from the start; the progress callback must
+    not go backwards (readFile()'s 'progress' events)."""
+    from kmerjs_amd import _native
+    p = tmp_path / "contig.fastq"
+    p.write_bytes(data)
+    for devices in (None, [0, 0]):
+        seen = []
+        c = _native.Counter(k=21, prefix=b"ATGAC", batch_bytes=1 << 20, devices=devices,
+                            progress=lambda d, t: seen.append((d, t)))
+        c.count_buffer(data)
+        assert seen and all(b[0] > a[0] for a, b in zip(seen, seen[1:])), seen[:8]
+        assert seen[-1][0] == len(data)
+        seen.clear()
+        c.count_file(str(p))
+        assert seen and all(b[0] > a[0] for a, b in zip(seen, seen[1:])), seen[:8]
+        assert seen[-1] == (len(data), len(data))
+        c.close()

@@ -64,8 +64,28 @@ function runBatch() {
     next();
 }
 
+// --time <fastq> <prefix> <k> <progress 0|1>: wall time of the unmodified
+// readFile() (promise resolved), the Map's size and ordered digest (sha256 of
+// JSON.stringify([...map]), first 16 hex), as one JSON line on stderr (with
+// progress=1 the reference writes a line to stdout per input line).
+function runTime() {
+    const [file, prefix, k, prog] = process.argv.slice(3);
+    const ref = loadReference();
+    const kj = new ref.KmerJS(file, prefix, parseInt(k, 10), 1, 1, prog === '1', 'node');
+    const t0 = process.hrtime.bigint();
+    kj.readFile().promise.then((map) => {
+        const t1 = process.hrtime.bigint();
+        const digest = require('crypto').createHash('sha256').update(JSON.stringify([...map]), 'utf8')
+            .digest('hex').slice(0, 16);
+        process.stderr.write(JSON.stringify({ seconds: Number(t1 - t0) / 1e9, size: map.size, lines: kj.lines,
+            sum: [...map.values()].reduce((a, b) => a + b, 0), digest, progress: prog === '1' }) + '\n');
+    });
+}
+
 if (require.main === module && process.argv[2] === '--batch') {
     runBatch();
+} else if (require.main === module && process.argv[2] === '--time') {
+    runTime();
 } else if (require.main === module) {
     const [file, prefix, k, step, out] = process.argv.slice(2);
     const ref = loadReference();
