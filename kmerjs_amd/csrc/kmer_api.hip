@@ -489,7 +489,7 @@ kmer_status launch_chunk(kmer_ctx *c) {
     auto &p = c->pend;
     const hipStream_t s = p.s;
     HIPCHK(c, hipEventRecord(c->ev0, s));
-    if (c->planes) HIPCHK(c, launch_scan_planes(p.a, c->pargs, s));
+    if (c->planes) HIPCHK(c, launch_scan_planes(p.a, c->pargs, c->n_cu, s));
     else HIPCHK(c, launch_scan_tiles(p.a, s));
     HIPCHK(c, hipEventRecord(c->ev1, s));
     HIPCHK(c, launch_tile_reduce(c->tsum.p, p.n_tiles, c->bsum.p, s));

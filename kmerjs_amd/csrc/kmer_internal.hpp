@@ -317,7 +317,7 @@ struct WinArgs {
 // ---- launchers (kmer_kernels.hip) ------------------------------------------
 hipError_t launch_lines(const TileArgs &a, bool lookback, hipStream_t s);
 hipError_t launch_scan_tiles(const ScanArgs &a, hipStream_t s);
-hipError_t launch_scan_planes(const ScanArgs &a, const PlaneArgs &pa, hipStream_t s);
+hipError_t launch_scan_planes(const ScanArgs &a, const PlaneArgs &pa, int n_cu, hipStream_t s);
 hipError_t launch_hits(const HitArgs &a, hipStream_t s);
 // exclusive scan of the per-tile sums (init folded in); bsum / bscan: n_blocks scratch
 hipError_t launch_tile_reduce(const TileSum *in, uint32_t n, TileSum *bsum, hipStream_t s);
