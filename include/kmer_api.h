@@ -74,8 +74,21 @@ enum {
      * kmer_count_file / kmer_count_buffer switch to it by themselves when a
      * longer line turns up (the count is redone once); the device-resident
      * calls and multi-GPU group contexts need the flag. */
-    KMER_FLAG_LONG_LINES = 1u << 7
+    KMER_FLAG_LONG_LINES = 1u << 7,
     /* bits 8..15 are reserved (kmer_open rejects them) */
+    /* FASTA input (an extension; the reference has no FASTA parser:
+     * test/kmers.js:53-61, test/kmerFinderServer.js:158, so its readFile()
+     * counts only lines with index % 4 == 1 of a .fsa file, lib/kmers.js:151).
+     * A line starting with '>' opens a record (the header is not counted);
+     * lines before the first header form a headerless record; a record's
+     * sequence is its other lines joined (one trailing '\r' per line dropped),
+     * so windows span line breaks; each sequence is counted as the reference
+     * counts a sequence line (length > 1; windows of it and of its complement;
+     * first-occurrence order by record).  Every mode (ordered, UNORDERED,
+     * CANONICAL, any k / step / prefix; records longer than 2^23 bytes through
+     * the long-line retry).  kmer_result_lines = input lines.  Device feeds
+     * must cut chunks before a header line (offset 0, or a '>' after '\n'). */
+    KMER_FLAG_FASTA = 1u << 16
 };
 
 typedef struct {

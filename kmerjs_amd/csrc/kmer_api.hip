@@ -48,7 +48,7 @@
 using namespace kmerhip;
 
 // every KMER_FLAG_* of include/kmer_api.h
-constexpr uint32_t KMER_FLAGS_PUBLIC = 0xFFu;
+constexpr uint32_t KMER_FLAGS_PUBLIC = 0xFFu | KMER_FLAG_FASTA;
 
 namespace {
 
@@ -236,6 +236,13 @@ struct kmer_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr;
     hipEvent_t evw = nullptr;      // cross-stream wait (no timing)
     double scan_ms = 0.0, feed_ms = 0.0, finish_ms = 0.0;
+    // FASTA input (KMER_FLAG_FASTA, kmer_fasta.hip): each chunk is rewritten
+    // into FASTQ-shaped lines before it is counted
+    bool fasta = false;
+    DBuf<FaTile> fa_t, fa_x;       // per-tile functions, their exclusive scan (n_tiles + 1)
+    DBuf<uint8_t> fa_out[2];       // rewritten chunks (alternating: the previous one may still be read)
+    uint32_t fa_flip = 0;
+    uint64_t fa_lines = 0;         // input lines of the session (kmerObj.lines)
     // progress of the current whole-input call (report_progress: monotone across a retry)
     bool progress_any = false;
     uint64_t progress_hw = 0;
@@ -267,12 +274,12 @@ const uint64_t FILE_BATCH = 256ull << 20;     // kmer_count_file read-ahead batc
         HIPCHK(ctx, CALL);                                                              \
     } while (0)
 
-// Progress callback of kmer_count_file / kmer_count_buffer: monotone over the
-// whole call, so a long-line retry (which reads the input again from the
-// start) reports nothing until it passes what was already reported.
+// Progress callback of kmer_count_file / kmer_count_buffer: non-decreasing over
+// the whole call, so a long-line retry (which reads the input again from the
+// start) reports nothing until it is back at what was already reported.
 void report_progress(kmer_ctx *c, uint64_t done, uint64_t total) {
     if (!c->p.progress) return;
-    if (c->progress_any && done <= c->progress_hw) return;
+    if (c->progress_any && done < c->progress_hw) return;
     c->progress_any = true;
     c->progress_hw = done;
     c->p.progress(c->p.progress_user, done, total);
@@ -1377,9 +1384,47 @@ kmer_status build_table_result(kmer_ctx *c, uint64_t lines, kmer_result **out) {
     return KMER_OK;
 }
 
+struct FaTileOp {
+    __host__ __device__ FaTile operator()(const FaTile &a, const FaTile &b) const { return fa_tile_compose(a, b); }
+};
+
+// FASTA: rewrite the chunk [d, d + len) into FASTQ-shaped lines on the device
+// (kmer_fasta.hip) -> *od, *olen; counts the chunk's input lines.  One host
+// wait (the rewritten size).
+kmer_status fasta_rewrite(kmer_ctx *c, const uint8_t *d, uint64_t len, hipStream_t s, const uint8_t **od,
+                          uint64_t *olen) {
+    const uint64_t nt64 = (len + TILE - 1) / TILE;
+    if (nt64 > 0x7FFFFFFFull) return fail(c, KMER_E_BAD_PARAM, "chunk too large");
+    const uint32_t n_tiles = (uint32_t)nt64;
+    HIPCHK(c, c->fa_t.ensure(n_tiles + 1ull, s));
+    HIPCHK(c, c->fa_x.ensure(n_tiles + 1ull, s));
+    HIPCHK(c, hipMemsetAsync(c->fa_t.p + n_tiles, 0, sizeof(FaTile), s));   // (the identity: the scan's total lands there)
+    HIPCHK(c, launch_fa_tiles(d, len, n_tiles, c->fa_t.p, s));
+    FaTile id;
+    memset(&id, 0, sizeof(id));
+    ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->fa_t.p, c->fa_x.p, id, (size_t)n_tiles + 1, FaTileOp(), s));
+    FaTile tot;
+    uint8_t last = 0;
+    HIPCHK(c, hipMemcpyAsync(&tot, c->fa_x.p + n_tiles, sizeof(FaTile), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(&last, d + len - 1, 1, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    c->fa_flip ^= 1u;
+    DBuf<uint8_t> &ob = c->fa_out[c->fa_flip];
+    HIPCHK(c, ob.ensure(tot.c0 + 16, s));
+    HIPCHK(c, launch_fa_write(d, len, n_tiles, c->fa_x.p, ob.p, s));
+    c->fa_lines += tot.nl + (last != '\n' ? 1 : 0);
+    *od = ob.p;
+    *olen = tot.c0;
+    return KMER_OK;
+}
+
 kmer_status feed(kmer_ctx *c, const uint8_t *d, uint64_t len, hipStream_t s) {
     kmer_status st0 = settle(c);
     if (st0) return st0;
+    if (c->fasta && len) {
+        st0 = fasta_rewrite(c, d, len, s, &d, &len);
+        if (st0) return st0;
+    }
     if (c->mode != MODE_PACKED && c->mode != MODE_TILE_REC) {
         kmer_status st = flush_prep(c, s, 0);
         if (st) return st;
@@ -1408,6 +1453,7 @@ kmer_status reset(kmer_ctx *c) {
     c->n_hits = 0;
     c->n_cross = 0;
     c->host_lines = 0;
+    c->fa_lines = 0;
     c->long_seg = false;
     c->chunk_open = false;
     c->out_pending = false;
@@ -1759,8 +1805,40 @@ kmer_status finish(kmer_ctx *c, kmer_result **out) {
     StreamPos pos;
     st = read_pos(c, &pos);
     if (st) return st;
-    if (c->mode == MODE_TABLE) return build_table_result(c, pos.lines + pos.ends_open, out);
-    return build_result(c, pos.lines + pos.ends_open, out);
+    const uint64_t lines = c->fasta ? c->fa_lines : pos.lines + pos.ends_open;
+    if (c->mode == MODE_TABLE) return build_table_result(c, lines, out);
+    return build_result(c, lines, out);
+}
+
+// Where a batch of input may end (chunks are cut at line ends; FASTA chunks
+// before a header line, so that no record spans two chunks).
+// batch_cut: the last cut inside [p, p + n), 0 = none;
+// batch_extend: the first cut at or after b + from, else len.
+uint64_t batch_cut(const uint8_t *p, uint64_t n, bool fasta) {
+    if (!fasta) {
+        const void *q = n ? memrchr(p, '\n', n) : nullptr;
+        return q ? (uint64_t)((const uint8_t *)q - p) + 1 : 0;
+    }
+    uint64_t e = n ? n - 1 : 0;                  // a '\n' at j < n - 1 with p[j + 1] == '>'
+    while (e > 0) {
+        const void *q = memrchr(p, '\n', e);
+        if (!q) return 0;
+        const uint64_t j = (uint64_t)((const uint8_t *)q - p);
+        if (p[j + 1] == '>') return j + 1;
+        e = j;
+    }
+    return 0;
+}
+
+uint64_t batch_extend(const uint8_t *b, uint64_t from, uint64_t len, bool fasta) {
+    uint64_t i = from;
+    while (i < len) {
+        const void *q = memchr(b + i, '\n', len - i);
+        if (!q) return len;
+        i = (uint64_t)((const uint8_t *)q - b) + 1;
+        if (!fasta || (i < len && b[i] == '>')) return i;
+    }
+    return len;
 }
 
 // Feed host bytes through the device in batches cut at '\n' boundaries.
@@ -1770,16 +1848,10 @@ kmer_status feed_host(kmer_ctx *c, const uint8_t *bytes, uint64_t len, bool repo
     while (pos < len) {
         uint64_t end = std::min(len, pos + batch);
         if (end < len) {
-            // cut after the last '\n' in [pos, end); a line longer than the batch extends it
-            const uint8_t *p = bytes + pos;
-            uint64_t cut = end - pos;
-            while (cut > 0 && p[cut - 1] != '\n') --cut;
-            if (cut == 0) {
-                const void *nl = memchr(bytes + end, '\n', len - end);
-                end = nl ? (uint64_t)((const uint8_t *)nl - bytes) + 1 : len;
-            } else {
-                end = pos + cut;
-            }
+            // cut after the last '\n' in [pos, end) (FASTA: before the last header
+            // line); a line (record) longer than the batch extends it
+            const uint64_t cut = batch_cut(bytes + pos, end - pos, c->fasta);
+            end = cut ? pos + cut : batch_extend(bytes, end, len, c->fasta);
         }
         const uint64_t n = end - pos;
         kmer_status st0 = settle(c);            // the previous batch is done with the staging buffer
@@ -1827,7 +1899,9 @@ struct GroupSrc {
 struct MemSrc : GroupSrc {
     const uint8_t *b;
     uint64_t len, batch, pos = 0;
-    MemSrc(const uint8_t *b_, uint64_t len_, uint64_t batch_) : b(b_), len(len_), batch(std::max<uint64_t>(batch_, 1)) {}
+    bool fasta;
+    MemSrc(const uint8_t *b_, uint64_t len_, uint64_t batch_, bool fasta_)
+        : b(b_), len(len_), batch(std::max<uint64_t>(batch_, 1)), fasta(fasta_) {}
     void progress(uint64_t *d, uint64_t *t) override {
         *d = pos;
         *t = len;
@@ -1835,15 +1909,9 @@ struct MemSrc : GroupSrc {
     bool next(const uint8_t **p, uint64_t *n, kmer_status *, std::string *) override {
         if (pos >= len) return false;
         uint64_t end = std::min(len, pos + batch);
-        if (end < len) {
-            uint64_t cut = end - pos;
-            while (cut > 0 && b[pos + cut - 1] != '\n') --cut;
-            if (cut == 0) {                          // a line longer than the batch extends it
-                const void *nl = memchr(b + end, '\n', len - end);
-                end = nl ? (uint64_t)((const uint8_t *)nl - b) + 1 : len;
-            } else {
-                end = pos + cut;
-            }
+        if (end < len) {                             // (a line / record longer than the batch extends it)
+            const uint64_t cut = batch_cut(b + pos, end - pos, fasta);
+            end = cut ? pos + cut : batch_extend(b, end, len, fasta);
         }
         *p = b + pos;
         *n = end - pos;
@@ -1887,6 +1955,7 @@ struct FileBatches : GroupSrc {
     std::unordered_map<const uint8_t *, std::unique_ptr<uint8_t[]>> big;   // batches of lines longer than HEAD
     std::unordered_map<const uint8_t *, size_t> slot_of;
     bool done = false;
+    bool fasta = false;                              // batches cut before header lines
 
     ~FileBatches() override {
         {
@@ -2055,10 +2124,7 @@ struct FileBatches : GroupSrc {
                 start = own.get();
                 have = carry.size() + S.len;
             }
-            uint64_t cut = have;
-            if (!last) {
-                while (cut > 0 && start[cut - 1] != '\n') --cut;
-            }
+            const uint64_t cut = last ? have : batch_cut(start, have, fasta);
             carry.assign(start + cut, start + have);
             if (last) done = true;
             if (cut == 0) {                               // (no '\n' yet: all of it is carry)
@@ -2130,6 +2196,21 @@ __global__ __launch_bounds__(256) void partial_gather_kernel(const uint64_t *key
         okeys[i] = keys[j];
         ovals[i] = vals[j];
     }
+}
+
+// records a FASTA batch holds (kmer_fasta.hip's rewrite: one per header line,
+// plus a headerless one when the batch does not start with a header)
+uint64_t fasta_records(const uint8_t *p, uint64_t n) {
+    if (!n) return 0;
+    uint64_t r = p[0] != '>' ? 1 : 0;
+    const uint8_t *e = p + n;
+    for (const uint8_t *q = p; q < e;) {
+        if (*q == '>' && (q == p || q[-1] == '\n')) ++r;
+        const void *nl = memchr(q, '\n', (size_t)(e - q));
+        if (!nl) break;
+        q = (const uint8_t *)nl + 1;
+    }
+    return r;
 }
 
 uint64_t count_newlines(const uint8_t *p, uint64_t n) {
@@ -2235,8 +2316,9 @@ kmer_status group_count(kmer_ctx *g, GroupSrc &src, kmer_result **out) {
             std::lock_guard<std::mutex> lk(w.m);
             if (st) w.st = st;
         });
-    uint64_t lines = 0, off = 0, nb = 0;
+    uint64_t lines = 0, off = 0, nb = 0, in_lines = 0;
     uint8_t last = '\n';
+    const bool fasta = (g->p.flags & KMER_FLAG_FASTA) != 0;
     kmer_status rst = KMER_OK;
     std::string rerr;
     const uint8_t *p = nullptr;
@@ -2251,7 +2333,11 @@ kmer_status group_count(kmer_ctx *g, GroupSrc &src, kmer_result **out) {
             src.release(p);
             break;
         }
-        const uint64_t nl = count_newlines(p, n);
+        // positions are counted in the lines the devices see: FASTA batches are
+        // rewritten into four lines per record (kmer_fasta.hip)
+        const uint64_t in_nl = count_newlines(p, n);
+        const uint64_t nl = fasta ? 4 * fasta_records(p, n) : in_nl;
+        in_lines += in_nl;
         last = p[n - 1];
         Worker &w = *wk[nb % W];
         {
@@ -2284,7 +2370,7 @@ kmer_status group_count(kmer_ctx *g, GroupSrc &src, kmer_result **out) {
     if (rst) return fail(g, rst, rerr);
     for (size_t i = 0; i < W; ++i)
         if (wk[i]->st) return fail(g, wk[i]->st, "device " + std::to_string(g->group[i]->device) + ": " + g->group[i]->err);
-    const uint64_t total_lines = lines + (off > 0 && last != '\n' ? 1 : 0);
+    const uint64_t total_lines = in_lines + (off > 0 && last != '\n' ? 1 : 0);
     if (hipSetDevice(c0->device) != hipSuccess) return fail(g, KMER_E_DEVICE, "hipSetDevice");
     if (!ordered && mode != MODE_TABLE) {            // every batch went to devices[0]
         kmer_status st = finish(c0, out);
@@ -2426,13 +2512,14 @@ kmer_status group_count_buffer(kmer_ctx *g, const uint8_t *bytes, uint64_t len, 
     const size_t N = g->group.size();
     // default: one batch per child (a buffer is already in host memory)
     const uint64_t batch = g->p.batch_bytes ? g->p.batch_bytes : std::max<uint64_t>(1, (len + N - 1) / N);
-    MemSrc src(bytes, len, batch);
+    MemSrc src(bytes, len, batch, (g->p.flags & KMER_FLAG_FASTA) != 0);
     return group_count(g, src, out);
 }
 
 kmer_status group_count_file(kmer_ctx *g, const char *path, kmer_result **out) {
     const size_t N = g->group.size();
     FileBatches src;
+    src.fasta = (g->p.flags & KMER_FLAG_FASTA) != 0;
     std::string err;
     const kmer_status st = src.open(path, g->p.batch_bytes ? g->p.batch_bytes : GROUP_FILE_BATCH, N + 2, &err);
     if (st) return fail(g, st, err);
@@ -2497,6 +2584,7 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
     kmer_ctx *c = new (std::nothrow) kmer_ctx();
     if (!c) return KMER_E_OOM;
     c->p = *pp;
+    c->fasta = (pp->flags & KMER_FLAG_FASTA) != 0;
     c->prefix.assign((const char *)pp->prefix, pp->prefix_len);
     c->rprefix.resize(c->prefix.size());
     for (size_t i = 0; i < c->prefix.size(); ++i)
@@ -2636,6 +2724,10 @@ kmer_status kmer_close(kmer_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     c->tcount.release();
     c->nlslots.release();
+    c->fa_t.release();
+    c->fa_x.release();
+    c->fa_out[0].release();
+    c->fa_out[1].release();
     for (auto *b : {&c->tbase, &c->nlpos, &c->wcount, &c->wbase, &c->tp_cnt, &c->tp_lnl, &c->rkey, &c->rkey2, &c->rord, &c->rord2, &c->csel, &c->rcnt, &c->xord, &c->xord2,
                     &c->xkey, &c->xkey2, &c->ukey, &c->first, &c->cnt_out, &c->roff})
         b->release();
@@ -2790,6 +2882,7 @@ kmer_status count_file_once(kmer_ctx *c, const char *path, kmer_result **out) {
     // while the device counts the batch before; gzip input (magic 1f 8b) is
     // read through zlib, the count being that of the decompressed FASTQ
     FileBatches src;
+    src.fasta = c->fasta;
     std::string err;
     kmer_status st = src.open(path, c->p.batch_bytes ? c->p.batch_bytes : FILE_BATCH, 3, &err);
     if (st) return fail(c, st, err);
@@ -3155,7 +3248,7 @@ kmer_status kmer_lines(kmer_ctx *c, uint64_t *lines) {
     StreamPos pos;
     kmer_status st = read_pos(c, &pos);
     if (st) return st;
-    *lines = pos.lines + pos.ends_open;
+    *lines = c->fasta ? c->fa_lines : pos.lines + pos.ends_open;
     return KMER_OK;
 }
 

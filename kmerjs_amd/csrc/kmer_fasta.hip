@@ -1,0 +1,240 @@
+// kmer_fasta.hip — FASTA input (KMER_FLAG_FASTA; SURVEY §8(f) row 4, an
+// extension: the reference has no FASTA parser -- test/kmers.js:53-61 "TODO:
+// FASTA tests missing!", test/kmerFinderServer.js:158 "TODO: FIX FASTA
+// parser" -- and applied to a .fsa file its readFile() counts only the lines
+// with index % 4 == 1, lib/kmers.js:151).
+//
+// FASTA semantics (restated in oracle/kmer_oracle.c, oracle_count_fasta): a
+// line starting with '>' opens a record (the header, not counted); the lines
+// before the first header form a headerless record; a record's sequence is its
+// other lines joined (one trailing '\r' of each line dropped, empty lines add
+// nothing), so windows run across line breaks; each record's sequence s is
+// counted as the reference counts a sequence line (length > 1, windows of s
+// then of complement(s), prefix test, first-occurrence order by record).
+//
+// On the device a chunk of FASTA is rewritten, in one streaming pass plus a
+// scan, into the FASTQ shape every counting path already reads: per record
+// the four lines  header, joined sequence, "", ""  -- so the record's sequence
+// is line 4r + 1 -- and the chunk is then counted like FASTQ (ordered, table,
+// canonical; long records through long-line mode).  Chunks must be cut before
+// a header line (kmer_count_buffer / kmer_count_file do; device feeds must).
+//
+// Byte rule (chunk byte i, c = B[i], h = the current line is a header):
+//   at a line start:  h = (c == '>');  '>' at i > 0 -> "\n\n\n" first (closes
+//                     the previous record: sequence line, line 3, line 4);
+//                     i == 0 and c != '>' -> "\n" first (the headerless
+//                     record's empty header line)
+//   c == '\n'         -> "\n" in a header line, nothing in a sequence line
+//   c == '\r' before '\n' or at the chunk end -> nothing; any other byte -> c
+//   after the last byte: "\n\n\n" (+ "\n" when it ends an unterminated header)
+// Whether a line is a header depends on its first byte, which may lie in an
+// earlier tile: each tile (and each thread inside a tile) is a function of
+// the incoming state h (FaFn), composed by an exclusive scan.
+#include "kmer_internal.hpp"
+
+namespace kmerhip {
+
+namespace {
+
+constexpr int FA_BPT = 64;                       // bytes per thread
+constexpr int FA_TILE = TPB * FA_BPT;            // 16 KiB
+constexpr int FA_OUT_MAX = FA_TILE * 5 / 2 + 8;  // ">\n" lines: 2 input bytes -> 5 output bytes
+
+// thread function packed in 64 bits: [47:24] c1, [23:0] c0, [49:48] kind
+__device__ __forceinline__ uint64_t fa_pack(uint32_t kind, uint32_t c0, uint32_t c1) {
+    return (uint64_t)c0 | ((uint64_t)c1 << 24) | ((uint64_t)kind << 48);
+}
+__device__ __forceinline__ uint32_t fa_kind(uint64_t f) { return (uint32_t)(f >> 48) & 3u; }
+__device__ __forceinline__ uint32_t fa_c(uint64_t f, uint32_t s) { return (uint32_t)(f >> (s ? 24 : 0)) & 0xFFFFFFu; }
+// a then b
+__device__ __forceinline__ uint64_t fa_compose(uint64_t a, uint64_t b) {
+    const uint32_t ka = fa_kind(a), kb = fa_kind(b);
+    const uint32_t s0 = ka ? ka - 1 : 0u, s1 = ka ? ka - 1 : 1u;
+    return fa_pack(kb ? kb : ka, fa_c(a, 0) + fa_c(b, s0), fa_c(a, 1) + fa_c(b, s1));
+}
+
+// One thread's walk over bytes [64 t, 64 t + 64) of the tile staged at buf
+// (buf[-1] and buf[FA_TILE] are the neighbours; out of the chunk: '\n').
+// WRITE: with the incoming state h, append the output bytes at out[o].
+template <bool WRITE>
+__device__ __forceinline__ uint64_t fa_walk(const uint8_t *buf, int64_t g, uint64_t len, uint32_t h_in, uint8_t *out,
+                                            uint32_t o, uint32_t *nl_out) {
+    const int t0 = (int)threadIdx.x * FA_BPT;
+    uint32_t common = 0, dep = 0, nl = 0, h = h_in;
+    bool saw = false;
+    uint8_t prev = buf[t0 - 1];
+    const int n = (int64_t)len - g <= 0 ? 0 : (int64_t)len - g >= FA_BPT ? FA_BPT : (int)((int64_t)len - g);
+    for (int j = 0; j < n; ++j) {
+        const uint8_t c = buf[t0 + j];
+        const int64_t gi = g + j;
+        if (prev == '\n') {                       // line start (the chunk start reads '\n' behind it)
+            saw = true;
+            h = c == '>';
+            if (c == '>' && gi > 0) {
+                common += 3;
+                if (WRITE) { out[o++] = '\n'; out[o++] = '\n'; out[o++] = '\n'; }
+            }
+            if (gi == 0 && c != '>') {
+                common += 1;
+                if (WRITE) out[o++] = '\n';
+            }
+        }
+        const uint8_t nx = buf[t0 + j + 1];
+        if (c == '\n') {
+            ++nl;
+            if (saw) common += h; else dep += 1;
+            if (WRITE && h) out[o++] = '\n';
+        } else if (!(c == '\r' && ((uint64_t)gi + 1 == len || nx == '\n'))) {
+            common += 1;
+            if (WRITE) out[o++] = c;
+        }
+        if ((uint64_t)gi + 1 == len) {             // after the chunk's last byte
+            common += 3;
+            if (WRITE) { out[o++] = '\n'; out[o++] = '\n'; out[o++] = '\n'; }
+            if (c != '\n') {
+                if (saw) common += h; else dep += 1;
+                if (WRITE && h) out[o++] = '\n';
+            }
+        }
+        prev = c;
+    }
+    *nl_out = nl;
+    return fa_pack(saw ? 1u + h : 0u, common, common + dep);
+}
+
+// inclusive scan of thread functions over the workgroup; returns this
+// thread's EXCLUSIVE prefix, *total = the whole tile's function
+__device__ __forceinline__ uint64_t fa_block_scan(uint64_t f, uint64_t *wtot, uint64_t *total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint64_t incl = f;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(incl, d);
+        if (lane >= d) incl = fa_compose(y, incl);
+    }
+    uint64_t excl = __shfl_up(incl, 1);
+    if (lane == 0) excl = fa_pack(0, 0, 0);
+    if (lane == 63) wtot[wid] = incl;
+    __syncthreads();
+    uint64_t before = fa_pack(0, 0, 0), all = fa_pack(0, 0, 0);
+#pragma unroll
+    for (int w = 0; w < TPB / 64; ++w) {
+        if (w < wid) before = fa_compose(before, wtot[w]);
+        all = fa_compose(all, wtot[w]);
+    }
+    *total = all;
+    return fa_compose(before, excl);
+}
+
+// tile bytes + one byte on each side into LDS (out of the chunk: '\n')
+__device__ __forceinline__ void fa_stage(const uint8_t *data, uint64_t len, int64_t g0, uint8_t *buf) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int64_t g = g0 + 16 * (tid + TPB * i);
+        uint4 v;
+        if (g + 16 <= (int64_t)len) {
+            v = *(const uint4 *)(data + g);
+        } else {
+            uint32_t w[4];
+            for (int q = 0; q < 4; ++q) {
+                uint32_t x = 0;
+                for (int b = 0; b < 4; ++b) {
+                    const int64_t p = g + 4 * q + b;
+                    x |= (uint32_t)((uint64_t)p < len ? data[p] : (uint8_t)'\n') << (8 * b);
+                }
+                w[q] = x;
+            }
+            v = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        *(uint4 *)(buf + 16 * (tid + TPB * i)) = v;
+    }
+    if (tid == 0) buf[-1] = g0 > 0 ? data[g0 - 1] : (uint8_t)'\n';
+    if (tid == 1) buf[FA_TILE] = (uint64_t)(g0 + FA_TILE) < len ? data[g0 + FA_TILE] : (uint8_t)'\n';
+}
+
+struct FaShared {
+    uint64_t wtot[TPB / 64];
+    uint32_t nl[TPB / 64];
+};
+
+__global__ __launch_bounds__(TPB) void fa_tiles_kernel(const uint8_t *data, uint64_t len, FaTile *tiles) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[FA_TILE + 32];
+    __shared__ FaShared sh;
+    uint8_t *buf = stage + 16;
+    const int64_t g0 = (int64_t)blockIdx.x * FA_TILE;
+    fa_stage(data, len, g0, buf);
+    __syncthreads();
+    uint32_t nl = 0;
+    const uint64_t f = fa_walk<false>(buf, g0 + FA_BPT * threadIdx.x, len, 0, nullptr, 0, &nl);
+    uint64_t total;
+    uint32_t s = nl;
+    for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
+    if ((threadIdx.x & 63) == 0) sh.nl[threadIdx.x >> 6] = s;
+    (void)fa_block_scan(f, sh.wtot, &total);
+    if (threadIdx.x == 0) {
+        FaTile t;
+        t.kind = fa_kind(total);
+        t.pad = 0;
+        t.c0 = fa_c(total, 0);
+        t.c1 = fa_c(total, 1);
+        t.nl = (uint64_t)sh.nl[0] + sh.nl[1] + sh.nl[2] + sh.nl[3];
+        tiles[blockIdx.x] = t;
+    }
+}
+
+// tiles_x: exclusive scan of the tile functions (FaTileOp); the output of
+// tile T starts at tiles_x[T] applied to state 0
+__global__ __launch_bounds__(TPB) void fa_write_kernel(const uint8_t *data, uint64_t len, const FaTile *tiles_x,
+                                                      uint8_t *out) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[FA_TILE + 32];
+    __shared__ __attribute__((aligned(16))) uint8_t ob[FA_OUT_MAX + 16];
+    __shared__ FaShared sh;
+    uint8_t *buf = stage + 16;
+    const int64_t g0 = (int64_t)blockIdx.x * FA_TILE;
+    fa_stage(data, len, g0, buf);
+    const FaTile px = tiles_x[blockIdx.x];
+    const uint32_t h_tile = px.kind ? px.kind - 1 : 0u;  // (state at the chunk start: no line yet)
+    const uint64_t off = px.c0;
+    __syncthreads();
+    uint32_t nl = 0;
+    const int64_t g = g0 + FA_BPT * threadIdx.x;
+    const uint64_t f = fa_walk<false>(buf, g, len, 0, nullptr, 0, &nl);
+    uint64_t total;
+    const uint64_t ex = fa_block_scan(f, sh.wtot, &total);
+    // this thread's incoming state and output offset inside the tile
+    const uint32_t kx = fa_kind(ex);
+    const uint32_t h = kx ? kx - 1 : h_tile;
+    const uint32_t o = fa_c(ex, h_tile);
+    (void)fa_walk<true>(buf, g, len, h, ob, o, &nl);
+    const uint32_t n_out = fa_c(total, h_tile);
+    __syncthreads();
+    // the tile's output, [off, off + n_out): bytes up to a 4-byte boundary,
+    // whole words, the rest as bytes
+    const uint64_t a0 = (off + 3) & ~3ull;
+    const uint32_t head = a0 - off < (uint64_t)n_out ? (uint32_t)(a0 - off) : n_out;
+    const uint32_t words = (n_out - head) / 4;
+    for (uint32_t i = threadIdx.x; i < head; i += TPB) out[off + i] = ob[i];
+    for (uint32_t i = threadIdx.x; i < words; i += TPB) {
+        const uint32_t p = head + 4 * i;
+        const uint32_t w = (uint32_t)ob[p] | ((uint32_t)ob[p + 1] << 8) | ((uint32_t)ob[p + 2] << 16) |
+                           ((uint32_t)ob[p + 3] << 24);
+        *(uint32_t *)(out + a0 + 4 * i) = w;
+    }
+    for (uint32_t i = head + 4 * words + threadIdx.x; i < n_out; i += TPB) out[off + i] = ob[i];
+}
+
+}  // namespace
+
+hipError_t launch_fa_tiles(const uint8_t *data, uint64_t len, uint32_t n_tiles, FaTile *tiles, hipStream_t s) {
+    hipLaunchKernelGGL(fa_tiles_kernel, dim3(n_tiles), dim3(TPB), 0, s, data, len, tiles);
+    return hipGetLastError();
+}
+
+hipError_t launch_fa_write(const uint8_t *data, uint64_t len, uint32_t n_tiles, const FaTile *tiles_x, uint8_t *out,
+                           hipStream_t s) {
+    hipLaunchKernelGGL(fa_write_kernel, dim3(n_tiles), dim3(TPB), 0, s, data, len, tiles_x, out);
+    return hipGetLastError();
+}
+
+}  // namespace kmerhip

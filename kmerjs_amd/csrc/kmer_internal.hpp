@@ -514,6 +514,28 @@ struct TabSeg {
     uint64_t src, dst, len;
 };
 hipError_t launch_tab_segcopy(const uint64_t *src, const TabSeg *segs, uint32_t n, uint64_t *dst, hipStream_t s);
+// FASTA input (kmer_fasta.hip, KMER_FLAG_FASTA): a chunk of FASTA rewritten
+// as FASTQ-shaped lines (header, joined sequence, "", "" per record).  A tile
+// of 16 KiB is a function of the header state it inherits: kind 0 passes the
+// state through, 1 / 2 leave it 0 / 1; c0 / c1 = output bytes for an incoming
+// state 0 / 1; nl = input '\n' bytes.  Composed by an exclusive scan.
+struct FaTile {
+    uint32_t kind, pad;
+    uint64_t c0, c1, nl;
+};
+__host__ __device__ inline FaTile fa_tile_compose(const FaTile &a, const FaTile &b) {
+    FaTile r;
+    const uint32_t s0 = a.kind ? a.kind - 1 : 0u, s1 = a.kind ? a.kind - 1 : 1u;
+    r.kind = b.kind ? b.kind : a.kind;
+    r.pad = 0;
+    r.c0 = a.c0 + (s0 ? b.c1 : b.c0);
+    r.c1 = a.c1 + (s1 ? b.c1 : b.c0);
+    r.nl = a.nl + b.nl;
+    return r;
+}
+hipError_t launch_fa_tiles(const uint8_t *data, uint64_t len, uint32_t n_tiles, FaTile *tiles, hipStream_t s);
+hipError_t launch_fa_write(const uint8_t *data, uint64_t len, uint32_t n_tiles, const FaTile *tiles_x, uint8_t *out,
+                           hipStream_t s);
 hipError_t launch_synth_fastq(uint8_t *out, uint64_t seed, uint64_t first_read, uint64_t n_reads,
                               hipStream_t s);
 hipError_t launch_permute_rows(const uint8_t *keys, const uint64_t *cnt, const uint64_t *first, const uint32_t *idx,

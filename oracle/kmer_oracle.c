@@ -239,6 +239,69 @@ int oracle_count_buffer(const uint8_t *buf, size_t len, const uint8_t *prefix, s
     return st;
 }
 
+/* FASTA mode (KMER_FLAG_FASTA) — an EXTENSION, parity unpinned by the
+ * reference: it has no FASTA parser (test/kmers.js:53-61 "TODO: FASTA tests
+ * missing!", test/kmerFinderServer.js:158 "TODO: FIX FASTA parser").  Records
+ * start at lines beginning with '>' (the header is not counted); lines before
+ * the first header form a headerless record; a record's sequence is its other
+ * lines, each without one trailing '\r', concatenated; each sequence is then
+ * counted exactly as readFile() counts a sequence line (lib/kmers.js:151-155:
+ * length > 1, kmersInLine of the sequence and of its complement).  `lines`
+ * counts input lines as lib/kmers.js:114-136 splits them. */
+static int fasta_flush(oracle_result *r, const uint8_t *seq, size_t L, uint8_t **rc, size_t *rc_cap,
+                       const uint8_t *prefix, size_t plen, uint32_t k, uint32_t step) {
+    if (L <= 1) return ORACLE_OK;
+    r->seq_lines++;
+    int st = kmers_in_line(r, seq, L, prefix, plen, k, step);
+    if (st) return st;
+    if (L > *rc_cap) {
+        free(*rc);
+        *rc_cap = L * 2;
+        *rc = malloc(*rc_cap);
+        if (!*rc) return ORACLE_E_OOM;
+    }
+    oracle_complement(seq, L, *rc);
+    return kmers_in_line(r, *rc, L, prefix, plen, k, step);
+}
+
+int oracle_count_fasta(const uint8_t *buf, size_t len, const uint8_t *prefix, size_t plen,
+                       uint32_t k, uint32_t step, oracle_result *out) {
+    int st = res_init(out);
+    if (st) return st;
+    for (size_t i = 0; i < len; ++i)
+        if (buf[i] >= 0x80) return ORACLE_E_NONASCII;
+    uint8_t *seq = NULL, *rc = NULL;
+    size_t seq_len = 0, seq_cap = 0, rc_cap = 0;
+    size_t pos = 0;
+    while (pos < len && !st) {
+        const uint8_t *nl = memchr(buf + pos, '\n', len - pos);
+        size_t end = nl ? (size_t)(nl - buf) : len;
+        size_t L = end - pos;
+        if (!nl && L == 0) break;
+        const uint8_t *line = buf + pos;
+        out->lines++;
+        pos = nl ? end + 1 : len;
+        if (L > 0 && line[L - 1] == '\r') --L;
+        if (L > 0 && line[0] == '>') {                 /* a header: the record before it ends */
+            st = fasta_flush(out, seq, seq_len, &rc, &rc_cap, prefix, plen, k, step);
+            seq_len = 0;
+            continue;
+        }
+        if (seq_len + L > seq_cap) {
+            seq_cap = (seq_len + L) * 2 + 64;
+            uint8_t *q = realloc(seq, seq_cap);
+            if (!q) { st = ORACLE_E_OOM; break; }
+            seq = q;
+        }
+        if (L) memcpy(seq + seq_len, line, L);
+        seq_len += L;
+    }
+    if (!st) st = fasta_flush(out, seq, seq_len, &rc, &rc_cap, prefix, plen, k, step);
+    free(seq);
+    free(rc);
+    return st;
+}
+
 /* ---- synthetic FASTQ, identical to the device generator ----
  * Record i: "@r%010llu\n" + 150 bases + "\n+\n" + 150 x 'I' + "\n" = 317 B.
  * Base b of read i = "ACGT"[(mix(seed*G + i*8 + b/32) >> 2*(b%32)) & 3]. */

@@ -37,7 +37,7 @@ def lib():
         if not os.path.exists(path):
             build()
         L = ctypes.CDLL(path)
-        for fn in ("oracle_count_buffer", "oracle_kmers_in_line"):
+        for fn in ("oracle_count_buffer", "oracle_kmers_in_line", "oracle_count_fasta"):
             f = getattr(L, fn)
             f.restype = ctypes.c_int
             f.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
@@ -62,10 +62,13 @@ def _collect(r):
     return out
 
 
-def count_buffer(data: bytes, prefix: bytes = b"ATGAC", k: int = 16, step: int = 1, stats=False):
-    """Ordered [(key_bytes, count)] exactly as the reference's Map iteration."""
+def count_buffer(data: bytes, prefix: bytes = b"ATGAC", k: int = 16, step: int = 1, stats=False, fasta=False):
+    """Ordered [(key_bytes, count)] exactly as the reference's Map iteration.
+    fasta: the FASTA-mode extension (oracle_count_fasta: records by '>'
+    header, sequence lines joined; parity unpinned by the reference)."""
     r = _Res()
-    st = lib().oracle_count_buffer(data, len(data), prefix, len(prefix), k, step, ctypes.byref(r))
+    fn = lib().oracle_count_fasta if fasta else lib().oracle_count_buffer
+    st = fn(data, len(data), prefix, len(prefix), k, step, ctypes.byref(r))
     try:
         if st:
             raise OracleError("oracle status %d" % st)

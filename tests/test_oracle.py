@@ -81,3 +81,27 @@ def test_kmers_long_json_subset(inputs):
 
 def test_js_stringify_format():
     assert js_stringify([(b"A\rC", 2)]) == '[["A\\rC",2]]'
+
+
+def test_fasta_oracle_matches_python_restatement():
+    """oracle_count_fasta (the FASTA-mode checker; parity unpinned by the
+    reference, which has no FASTA parser) against an independent Python
+    restatement, on edge-rich inputs: CRLF, blank lines, wrapped and 1-base
+    lines, empty records, headerless first record, exotic bytes, no trailing
+    newline; and against hand-computed cases."""
+    from oracle import oracle
+    from tests.fasta_util import fasta_reference_py, make_fasta
+    cases = [make_fasta(1, 20, 400), make_fasta(2, 20, 300, crlf=True, blank=0.2),
+             make_fasta(3, 15, 200, headerless=True, exotic=0.05), make_fasta(4, 10, 100, width=1),
+             make_fasta(5, 12, 150, tail_newline=False), b"", b">only header", b"ACGTACGT", b">a\n>b\n\n>c\nAC\nGT\n"]
+    for data in cases:
+        for prefix, k, step in ((b"", 4, 1), (b"A", 5, 1), (b"AC", 3, 2), (b"", 1, 1)):
+            want, lines = fasta_reference_py(data, prefix, k, step)
+            got, st = oracle.count_buffer(data, prefix, k, step, stats=True, fasta=True)
+            assert got == want, (data[:40], prefix, k, step)
+            assert st["lines"] == lines
+    # hand-computed: windows cross the line break of one record
+    got = oracle.count_buffer(b">r\nAC\nGT\n", b"", 4, 1, fasta=True)
+    assert got == [(b"ACGT", 2)]
+    # ... and do not cross records
+    assert oracle.count_buffer(b">r\nAC\n>s\nGT\n", b"", 4, 1, fasta=True) == []
