@@ -74,6 +74,29 @@ def cpu_baseline(k, prefix, seconds_target=8.0):
                                   "Maps; %.1f s" % (nt, cores, dtn)}}
 
 
+def reference_js_c2(args):
+    """The reference's own Node.js path (lib/kmers.js readFile(), unmodified) on
+    this exact C2 workload, timed ONCE in the build container by
+    tools/time_ref_c2.py (the reference never travels to the GPU box, SURVEY
+    §8c): profiles/ref_js_c2.json.  Reported beside the C port's timing."""
+    if args.reads != 10_000_000 or args.k != 16 or args.prefix != "ATGAC" or args.seed != 1:
+        return None
+    path = os.path.join(REPO, "profiles", "ref_js_c2.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    runs = {r["progress"]: r for r in d["runs"]}
+    r0 = runs[False]
+    return {"value": r0["kmers_per_s"], "unit": "k-mers/s", "cores": 1, "kind": "reference",
+            "seconds": r0["seconds"], "progress_true": {"value": runs[True]["kmers_per_s"],
+                                                       "seconds": runs[True]["seconds"]},
+            "digest_equals_oracle": r0["digest_equals_oracle"],
+            "sample": "the whole C2 workload (10 M reads, 3.17 GB), node %s, progress=false (default progress=true "
+                      "beside it)" % d["host"]["node"],
+            "where": d["where"] + " (%s, %d vCPU)" % (d["host"]["cpu"], d["host"]["vcpus"])}
+
+
 def end_to_end(buf, args):
     """readFile() -> Map through the Node drop-in on the same input written to
     a file: a child `node` process, timed inside it."""
@@ -705,6 +728,9 @@ def main():
             out["end_to_end"] = end_to_end(buf, args)
         if not args.no_cpu_baseline and world == 1 and args.config == "c2":
             out["cpu_baseline"] = cpu_baseline(args.k, prefix)
+            ref = reference_js_c2(args)
+            if ref is not None:
+                out["cpu_baseline"]["reference_js"] = ref
         if (not args.no_match and world == 1 and args.config == "c2" and args.pipeline == 1 and args.k == 16
                 and args.prefix == "ATGAC"):
             # §8(f3): the count just measured, still in HBM, joined against a
