@@ -4,7 +4,7 @@
 // parser" -- and applied to a .fsa file its readFile() counts only the lines
 // with index % 4 == 1, lib/kmers.js:151).
 //
-// FASTA semantics (restated in oracle/kmer_oracle.c, oracle_count_fasta): a
+// FASTA semantics (restated for the tests in oracle/kmer_oracle.c): a
 // line starting with '>' opens a record (the header, not counted); the lines
 // before the first header form a headerless record; a record's sequence is its
 // other lines joined (one trailing '\r' of each line dropped, empty lines add

@@ -1,0 +1,348 @@
+// kmer_finish.hip — the ordered finish: cross-list placement, key sort / bucket heads,
+// emit in first-occurrence (Map) order, host results.
+#include "kmer_host.hpp"
+
+namespace kmerhip {
+
+// ---------------------------------------------------------------------------
+// finish
+// ---------------------------------------------------------------------------
+// Place the cross entries: sorted by order key they take the natural slots
+// sorted ascending (the slots that tile-local ranking left to them).
+kmer_status apply_cross(kmer_ctx *c) {
+    hipStream_t s = c->stream;
+    const uint64_t n = c->n_cross;
+    if (n == 0) return KMER_OK;
+    uint32_t *k32 = c->narrow ? c->rkey32.p : nullptr;
+    if (!c->long_seg) {
+        HIPCHK(c, launch_cross_segsort(c->xord.p, c->xkey.p, c->xslot.p, n, c->rkey.p, k32, c->rord.p, c->pbits, s));
+    } else if (n <= XSMALL_MAX) {
+        HIPCHK(c, launch_cross_sort_small(c->xslot.p, c->xord.p, c->xkey.p, n, c->rkey.p, k32, c->rord.p, s));
+    } else {
+        StreamPos pos;
+        kmer_status st = read_pos(c, &pos);
+        if (st) return st;
+        HIPCHK(c, c->xord2.ensure(n, s));
+        HIPCHK(c, c->xkey2.ensure(n, s));
+        rocprim::double_buffer<uint64_t> ob(c->xord.p, c->xord2.p);
+        rocprim::double_buffer<uint64_t> kb(c->xkey.p, c->xkey2.p);
+        const int obits = std::min(64, bit_width(((pos.lines + 1) << (c->pbits + 1)) | ((2ull << c->pbits) - 1ull)));
+        ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, ob, kb, (size_t)n, 0, obits, s));
+        HIPCHK(c, launch_cross_scatter(c->xslot.p, ob.current(), kb.current(), n, c->rkey.p, k32, c->rord.p, s));
+    }
+    if (c->wide) HIPCHK(c, launch_cross_wide_fix(c->xslot.p, n, c->xkeyl.p, c->xkeyh.p, c->rkey.p, c->rkeyh.p, s));
+    c->n_cross = 0;
+    return KMER_OK;
+}
+
+// stable radix sort of (key, rank), then the heads.  Without per-entry
+// counts the by-rank keys are kept (the sort writes a copy), hcnt is
+// prefilled with 1 and only repeated / invalid keys are scattered
+// (heads_sparse); merged partials (with_counts) sum u64 counts into HeadRecs.
+template <typename K>
+kmer_status sort_and_heads(kmer_ctx *c, K *keys, K *keys2, uint64_t n, bool with_counts) {
+    hipStream_t s = c->stream;
+    const uint64_t invalid = c->kbits >= 63 ? ~0ull : (1ull << c->kbits);
+    const int end_bit = std::min<int>(8 * (int)sizeof(K), (int)c->kbits + 1);   // + the invalid-key bit
+    if (!with_counts) {
+        rocprim::counting_iterator<uint32_t> iota(0u);
+        ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, keys, keys2, iota, c->ridx2.p, (size_t)n, 0, end_bit, s));
+        HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)c->hcnt.p, 1, n, s));
+        if (sizeof(K) == 4)
+            HIPCHK(c, launch_heads_sparse(nullptr, (const uint32_t *)keys2, c->ridx2.p, n, invalid, c->hcnt.p, s));
+        else
+            HIPCHK(c, launch_heads_sparse((const uint64_t *)keys2, nullptr, c->ridx2.p, n, invalid, c->hcnt.p, s));
+        return KMER_OK;
+    }
+    rocprim::double_buffer<K> kb(keys, keys2);
+    rocprim::double_buffer<uint32_t> vb(c->ridx.p, c->ridx2.p);
+    ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, kb, vb, (size_t)n, 0, end_bit, s));
+    const uint64_t *rcnt = c->rcnt.p;
+    if (sizeof(K) == 4)
+        HIPCHK(c, launch_heads32((const uint32_t *)kb.current(), vb.current(), n, (uint32_t)invalid, rcnt, c->hrec.p, c->hcnt.p, s));
+    else
+        HIPCHK(c, launch_heads((const uint64_t *)kb.current(), vb.current(), n, invalid, rcnt, c->hrec.p, c->hcnt.p, s));
+    return KMER_OK;
+}
+
+// wide keys (two words): stable (lo, rank) sort, then a stable sort of the
+// high words by that order -> ranks ordered by (hi, lo), ascending within a
+// key; heads over the pairs (hcnt prefilled with 1, as the sparse heads)
+kmer_status sort_and_heads_wide(kmer_ctx *c, uint64_t n) {
+    hipStream_t s = c->stream;
+    HIPCHK(c, c->whA.ensure(n, s));
+    HIPCHK(c, c->whB.ensure(n, s));
+    HIPCHK(c, c->ridx3.ensure(n, s));
+    rocprim::counting_iterator<uint32_t> iota(0u);
+    ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, c->rkey.p, c->rkey2.p, iota, c->ridx2.p, (size_t)n, 0, 64, s));
+    HIPCHK(c, launch_gather_u64(c->rkeyh.p, c->ridx2.p, n, c->whA.p, s));
+    const int hbits = (int)c->kbits - 64 + 1;    // + the invalid bit
+    ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, c->whA.p, c->whB.p, c->ridx2.p, c->ridx3.p, (size_t)n, 0, hbits, s));
+    HIPCHK(c, launch_gather_u64(c->rkey.p, c->ridx3.p, n, c->rkey2.p, s));
+    HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)c->hcnt.p, 1, n, s));
+    HIPCHK(c, launch_heads_wide(c->whB.p, c->rkey2.p, c->ridx3.p, n, 1ull << (c->kbits - 64), c->hcnt.p, s));
+    return KMER_OK;
+}
+
+// bucket partition + per-bucket LDS tables (keys of <= 24 bits)
+kmer_status bucket_heads(kmer_ctx *c, uint64_t n) {
+    hipStream_t s = c->stream;
+    const uint32_t shift = std::min<uint32_t>(c->kbits, BKT_LOW);
+    const uint32_t nb = 1u << (c->kbits - shift);
+    const uint64_t nblk64 = (n + BKT_EPB_HOST - 1) / BKT_EPB_HOST;
+    if (nblk64 > 0x7FFFFFFFull) return fail(c, KMER_E_BAD_PARAM, "too many hits");
+    const uint32_t nblk = (uint32_t)nblk64;
+    const uint32_t invalid = 1u << c->kbits;
+    HIPCHK(c, c->bH.ensure((uint64_t)nb * nblk, s));
+    HIPCHK(c, c->bHs.ensure((uint64_t)nb * nblk, s));
+    HIPCHK(c, c->pkey16.ensure(n, s));
+    HIPCHK(c, c->ridx2.ensure(n, s));
+    HIPCHK(c, launch_bucket_hist(c->rkey32.p, n, invalid, shift, nb, nblk, c->bH.p, c->hcnt.p, s));
+    ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->bH.p, c->bHs.p, 0u, (size_t)nb * nblk, rocprim::plus<uint32_t>(), s));
+    HIPCHK(c, launch_bucket_scatter(c->rkey32.p, n, invalid, shift, nb, nblk, c->bHs.p, c->pkey16.p, c->ridx2.p, s));
+    HIPCHK(c, launch_bucket_heads(c->pkey16.p, c->ridx2.p, c->bHs.p, c->bH.p, nb, nblk, shift, c->hcnt.p, s));
+    return KMER_OK;
+}
+
+struct KeyValid32 {
+    uint32_t inv;
+    __host__ __device__ bool operator()(uint32_t k) const { return k != inv; }
+};
+struct KeyValid64 {
+    uint64_t inv;
+    __host__ __device__ bool operator()(uint64_t k) const { return k != inv; }
+};
+
+// Dense-hit path with a prefix: every window of a sequence line holds a rank
+// slot and the windows that do not start with the prefix (or its reverse
+// complement) carry the invalid key.  The matching ones are compacted, in
+// rank order, before the finish sorts them -- a 1-3-base prefix rejects most
+// windows (C2 input, prefix ACG: 37.5 M of 2.7 G).
+kmer_status compact_windows(kmer_ctx *c) {
+    hipStream_t s = c->stream;
+    const uint64_t n = c->n_hits;
+    if (n == 0) return KMER_OK;
+    const uint64_t invalid = c->kbits >= 63 ? ~0ull : (1ull << c->kbits);
+    HIPCHK(c, c->ridx2.ensure(n, s));
+    HIPCHK(c, c->csel.ensure(1, s));
+    rocprim::counting_iterator<uint32_t> iota(0u);
+    if (c->narrow) {
+        auto fl = rocprim::make_transform_iterator(c->rkey32.p, KeyValid32{(uint32_t)invalid});
+        ROCPRIM_RUN(c, rocprim::select(t, b, iota, fl, c->ridx2.p, c->csel.p, (size_t)n, s));
+    } else {
+        auto fl = rocprim::make_transform_iterator(c->rkey.p, KeyValid64{invalid});
+        ROCPRIM_RUN(c, rocprim::select(t, b, iota, fl, c->ridx2.p, c->csel.p, (size_t)n, s));
+    }
+    HIPCHK(c, hipMemcpyAsync(c->h_small + 20, c->csel.p, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    const uint64_t n2 = c->h_small[20];
+    if (n2 >= n) return KMER_OK;
+    // gathered into the second buffers, copied back (the session buffers keep their size)
+    if (c->narrow) {
+        HIPCHK(c, c->rkey32b.ensure(n2 + 1, s));
+        HIPCHK(c, launch_gather_u32(c->rkey32.p, c->ridx2.p, n2, c->rkey32b.p, s));
+        HIPCHK(c, hipMemcpyAsync(c->rkey32.p, c->rkey32b.p, n2 * 4, hipMemcpyDeviceToDevice, s));
+    } else {
+        HIPCHK(c, c->rkey2.ensure(n2 + 1, s));
+        HIPCHK(c, launch_gather_u64(c->rkey.p, c->ridx2.p, n2, c->rkey2.p, s));
+        HIPCHK(c, hipMemcpyAsync(c->rkey.p, c->rkey2.p, n2 * 8, hipMemcpyDeviceToDevice, s));
+    }
+    HIPCHK(c, c->rord2.ensure(n2 + 1, s));
+    HIPCHK(c, launch_gather_u64(c->rord.p, c->ridx2.p, n2, c->rord2.p, s));
+    HIPCHK(c, hipMemcpyAsync(c->rord.p, c->rord2.p, n2 * 8, hipMemcpyDeviceToDevice, s));
+    c->n_hits = n2;
+    return KMER_OK;
+}
+
+// resolve a deferred unique count (finish without a host result)
+kmer_status resolve_out(kmer_ctx *c) {
+    kmer_status st = resolve_feed_timing(c);
+    if (st) return st;
+    if (c->out_pending) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        c->n_out = c->h_tail[8];
+        c->out_pending = false;
+    }
+    if (c->timing_pending) {
+        float ms = 0.f;
+        HIPCHK(c, hipEventSynchronize(c->ev3));
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev2, c->ev3));
+        c->finish_ms = ms;
+        c->timing_pending = false;
+    }
+    return KMER_OK;
+}
+
+// Rank arrays (rkey / rord / ridx [/ rcnt]) of n hits -> unique keys in
+// first-occurrence order: stable radix sort of (key, rank); group heads flag
+// their rank; a scan of the flags gives each unique key its output position.
+// partial: (code, {first, count}) into ukey/uval; else decoded keys, counts
+// and firsts into keys_out / cnt_out / first.  Returns the unique count.
+// sync = false: the unique count is copied back asynchronously (resolve_out).
+kmer_status rank_finish(kmer_ctx *c, uint64_t n, bool partial, bool with_counts, uint64_t *nu_out, bool sync) {
+    hipStream_t s = c->stream;
+    *nu_out = 0;
+    if (n == 0) return KMER_OK;
+    if (c->narrow) HIPCHK(c, c->rkey32b.ensure(n, s));
+    else HIPCHK(c, c->rkey2.ensure(n, s));
+    HIPCHK(c, c->ridx2.ensure(n, s));
+    if (with_counts) HIPCHK(c, c->hrec.ensure(n, s));
+    HIPCHK(c, c->hcnt.ensure(n + 4, s));
+    HIPCHK(c, c->opos.ensure(n, s));
+    if (partial) {
+        HIPCHK(c, c->ukey.ensure(n, s));
+        HIPCHK(c, c->uval.ensure(n, s));
+    } else {
+        HIPCHK(c, c->keys_out.ensure(n * c->p.k, s));
+        HIPCHK(c, c->cnt_out.ensure(n, s));
+        HIPCHK(c, c->first.ensure(n, s));
+    }
+    const uint64_t invalid = c->kbits >= 63 ? ~0ull : (1ull << c->kbits);
+    kmer_status st;
+    // (merged partials carry counts: the sort finish sums them in 64 bits)
+    const bool bucket = c->narrow && c->kbits <= BKT_LOW + 11 && !with_counts && !(c->p.flags & KMER_FLAG_SORT_FINISH);
+    if (c->wide)
+        st = sort_and_heads_wide(c, n);          // (no partials / merged counts: refused for wide keys)
+    else if (bucket)
+        st = bucket_heads(c, n);
+    else if (c->narrow)
+        st = sort_and_heads<uint32_t>(c, c->rkey32.p, c->rkey32b.p, n, with_counts);
+    else
+        st = sort_and_heads<uint64_t>(c, c->rkey.p, c->rkey2.p, n, with_counts);
+    if (st) return st;
+    auto is_head = rocprim::make_transform_iterator(c->hcnt.p, IsHead());
+    ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, is_head, c->opos.p, 0u, (size_t)n, rocprim::plus<uint32_t>(), s));
+    EmitArgs e;
+    memset(&e, 0, sizeof(e));
+    e.hcnt = c->hcnt.p;
+    e.hrec = with_counts ? c->hrec.p : nullptr;
+    e.rkey32 = c->narrow ? c->rkey32.p : nullptr;
+    e.rkey64 = c->narrow ? nullptr : c->rkey.p;
+    e.rkeyh = c->wide ? c->rkeyh.p : nullptr;
+    e.opos = c->opos.p;
+    e.rord = c->rord.p;
+    e.n = n;
+    e.invalid_key = invalid;
+    e.nuniq = c->d_nuniq;
+    e.nuniq_host = c->d_tail + 8;
+    e.k = c->p.k;
+    e.plen = (uint32_t)c->prefix.size();
+    e.partial = partial ? 1u : 0u;
+    memcpy(e.P, c->prefix.data(), std::min<size_t>(c->prefix.size(), sizeof(e.P)));
+    e.keys_out = c->keys_out.p;
+    e.cnt_out = c->cnt_out.p;
+    e.first_out = c->first.p;
+    e.ukey = c->ukey.p;
+    e.uval = c->uval.p;
+    HIPCHK(c, launch_emit(e, s));
+    if (!sync) {
+        c->out_pending = true;
+        return KMER_OK;
+    }
+    HIPCHK(c, hipStreamSynchronize(s));
+    *nu_out = c->h_tail[8];
+    return KMER_OK;
+}
+
+// ordered device entries + host records -> host result
+kmer_status build_result(kmer_ctx *c, uint64_t lines, kmer_result **out) {
+    kmer_result *r = new (std::nothrow) kmer_result();
+    if (!r) return fail(c, KMER_E_OOM, "host allocation failed");
+    r->lines = lines;
+    const uint64_t n = c->n_out, k = c->p.k;
+    std::vector<uint64_t> order(n), cnt(n);
+    std::vector<char> dkeys(n * k);
+    if (n) {
+        hipStream_t s = c->stream;
+        if (hipMemcpyAsync(order.data(), c->first.p, n * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(cnt.data(), c->cnt_out.p, n * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(dkeys.data(), c->keys_out.p, n * k, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+            delete r;
+            return fail(c, KMER_E_DEVICE, "result copy failed");
+        }
+    }
+    std::vector<std::pair<uint64_t, const std::pair<const std::string, Ent> *>> ex;
+    ex.reserve(c->exotic.size());
+    for (auto &kv : c->exotic) ex.emplace_back(kv.second.first, &kv);
+    std::sort(ex.begin(), ex.end(), [](const auto &x, const auto &y) { return x.first < y.first; });
+    const uint64_t total = n + ex.size();
+    r->keys.reserve(n * k + ex.size() * k);
+    r->offsets.reserve(total + 1);
+    r->counts.reserve(total);
+    r->firsts.reserve(total);
+    uint64_t i = 0, j = 0;
+    while (i < n || j < ex.size()) {
+        if (j >= ex.size() || (i < n && order[i] < ex[j].first)) {
+            r->keys.insert(r->keys.end(), dkeys.begin() + i * k, dkeys.begin() + (i + 1) * k);
+            r->counts.push_back(cnt[i]);
+            r->firsts.push_back(order[i]);
+            ++i;
+        } else {
+            const std::string &key = ex[j].second->first;
+            r->keys.insert(r->keys.end(), key.begin(), key.end());
+            r->counts.push_back(ex[j].second->second.count);
+            r->firsts.push_back(ex[j].first);
+            ++j;
+        }
+        r->offsets.push_back(r->keys.size());
+    }
+    *out = r;
+    return KMER_OK;
+}
+
+kmer_status read_pos(kmer_ctx *c, StreamPos *pos) {
+    kmer_status st = settle(c);
+    if (st) return st;
+    st = flush_prep(c, c->stream, 0);
+    if (st) return st;
+    HIPCHK(c, hipMemcpyAsync(c->h_small + 8, c->d_pos, sizeof(StreamPos), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    memcpy(pos, c->h_small + 8, sizeof(StreamPos));
+    return KMER_OK;
+}
+
+// Without a host result (`out` NULL) and without max_keys, nothing here waits
+// for the device: the unique count and the timing are read back lazily.
+kmer_status finish(kmer_ctx *c, kmer_result **out) {
+    if (!c->open_stream) return fail(c, KMER_E_STATE, "finish without reset/feed");
+    kmer_status st = settle(c);
+    if (st) return st;
+    HIPCHK(c, hipEventRecord(c->ev2, c->stream));
+    uint64_t nu = 0;
+    c->n_out = 0;
+    const bool sync = out || c->p.max_keys;
+    if (c->mode == MODE_PACKED || c->mode == MODE_WINDOWS) {
+        st = apply_cross(c);
+        if (st) return st;
+        if (c->mode == MODE_WINDOWS && !c->prefix.empty()) {
+            st = compact_windows(c);
+            if (st) return st;
+        }
+        st = rank_finish(c, c->n_hits, false, false, &nu, sync);
+        if (st) return st;
+        c->n_out = nu;
+    } else if (c->mode == MODE_TABLE) {
+        st = table_finish(c);
+        if (st) return st;
+    }
+    HIPCHK(c, hipEventRecord(c->ev3, c->stream));
+    c->timing_pending = true;
+    c->open_stream = false;
+    if (!sync) return KMER_OK;
+    st = resolve_out(c);
+    if (st) return st;
+    const uint64_t total = c->n_out + c->exotic.size();
+    if (c->p.max_keys && total > c->p.max_keys)
+        return fail(c, KMER_E_TOO_MANY_KEYS, "more distinct keys than max_keys (reference Map limit)");
+    if (!out) return KMER_OK;
+    StreamPos pos;
+    st = read_pos(c, &pos);
+    if (st) return st;
+    const uint64_t lines = c->fasta ? c->fa_lines : pos.lines + pos.ends_open;
+    if (c->mode == MODE_TABLE) return build_table_result(c, lines, out);
+    return build_result(c, lines, out);
+}
+
+
+}  // namespace kmerhip

@@ -1144,9 +1144,36 @@ __device__ __forceinline__ void tile_fill_regs(const uint8_t *data, int64_t g0, 
     }
 }
 
-template <bool FULL5, bool WIDE>
-__global__ __launch_bounds__(TPB) void scan_planes_pkernel(ScanArgs a, PlaneArgs pa) {
-    __shared__ __attribute__((aligned(16))) uint8_t bufs[2 * PBUF];
+// Tile staged through registers (interior tiles: four 16-B loads per lane,
+// no bounds tests)
+__device__ __forceinline__ void tile_load_regs(const uint8_t *data, int64_t g0, uint64_t len, uint8_t *buf) {
+    if (!tile_interior(g0, len)) {
+        tile_fill_regs(data, g0, len, buf);
+        return;
+    }
+    const int tid = threadIdx.x;
+    const uint8_t *src = data + g0 + 16 * tid;
+    uint4 v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = *(const uint4 *)(src + 16 * TPB * i);
+    uint4 vh = make_uint4(0, 0, 0, 0);
+    const bool halo = tid < NCH_FRONT + NCH_BACK;
+    const int hc = tid < NCH_FRONT ? tid : NCH_FRONT + NCH_MAIN + (tid - NCH_FRONT);
+    if (halo) vh = *(const uint4 *)(data + g0 - FH + 16 * hc);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *(uint4 *)(buf + FH + (tid + TPB * i) * 16) = v[i];
+    if (halo) *(uint4 *)(buf + hc * 16) = vh;
+}
+
+// DMA: two tile buffers, the next tile copied by LDS-DMA during the current
+// one (PSCAN_WG_PER_CU workgroups per CU).  !DMA: one buffer, each tile loaded
+// through registers at the top of its iteration -- the persistent loop alone
+// (8 workgroups per CU, as many as the per-tile kernel holds), which saves the
+// per-workgroup dispatch of scan_planes_kernel.
+template <bool FULL5, bool WIDE, bool DMA>
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(DMA ? 4 : 7, 8)))
+void scan_planes_pkernel(ScanArgs a, PlaneArgs pa) {
+    __shared__ __attribute__((aligned(16))) uint8_t bufs[(DMA ? 2 : 1) * PBUF];
     __shared__ ScanShared sh;
     __shared__ __attribute__((aligned(16))) uint8_t s_pr[2 * KMAX_TILE];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1160,25 +1187,29 @@ __global__ __launch_bounds__(TPB) void scan_planes_pkernel(ScanArgs a, PlaneArgs
         sh.nx = 0;
         sh.qn = 0;
     }
-    {
+    if (DMA) {
         const int64_t g0 = (int64_t)tile * TILE;
         if (tile_interior(g0, len)) tile_dma(a.data, g0, bufs);
         else tile_fill_regs(a.data, g0, len, bufs);
+        KH_DMA_BARRIER();
     }
-    KH_DMA_BARRIER();
     const uint32_t *pw = (const uint32_t *)s_pr;
     uint2 *qe = (uint2 *)sh.q;
     constexpr uint32_t QE = QCAP / 2;
     uint32_t b = 0;
     while (true) {
-        uint8_t *buf = bufs + b * PBUF;
+        uint8_t *buf = bufs + (DMA ? b * PBUF : 0);
         const int64_t g0 = (int64_t)tile * TILE;
         const uint32_t nxt = tile + gridDim.x;
         const bool have_next = nxt < a.n_tiles;
         const int64_t g1 = (int64_t)nxt * TILE;
-        const bool next_dma = have_next && tile_interior(g1, len);
+        const bool next_dma = DMA && have_next && tile_interior(g1, len);
         // the other buffer was last read before the previous tile's final barrier
         if (next_dma) tile_dma(a.data, g1, bufs + (b ^ 1u) * PBUF);
+        if (!DMA) {
+            tile_load_regs(a.data, g0, len, buf);
+            KH_LDS_BARRIER();
+        }
 
         // ---- this thread's 64 bytes (4 chunks) + 4 look-ahead bytes ----
         uint32_t w[17];
@@ -1368,8 +1399,9 @@ __global__ __launch_bounds__(TPB) void scan_planes_pkernel(ScanArgs a, PlaneArgs
             sh.nx = 0;
             sh.qn = 0;
         }
-        if (have_next && !next_dma) tile_fill_regs(a.data, g1, len, bufs + (b ^ 1u) * PBUF);
-        KH_DMA_BARRIER();            // next tile landed; this tile's LDS no longer read
+        if (DMA && have_next && !next_dma) tile_fill_regs(a.data, g1, len, bufs + (b ^ 1u) * PBUF);
+        if (DMA) KH_DMA_BARRIER();   // next tile landed; this tile's LDS no longer read
+        else KH_LDS_BARRIER();       // this tile's LDS no longer read
         if (!have_next) break;
         tile = nxt;
         b ^= 1u;
@@ -2824,22 +2856,31 @@ hipError_t launch_lines(const TileArgs &a, bool lookback, hipStream_t s) {
 }
 
 hipError_t launch_scan_planes(const ScanArgs &a, const PlaneArgs &pa, int n_cu, hipStream_t s) {
-    // the persistent LDS-DMA kernel (PSCAN_WG_PER_CU workgroups per CU walk the
-    // tiles); KMERHIP_SCAN=tile: one workgroup per tile (A/B experiments)
-    static const bool per_tile = [] {
+    // KMERHIP_SCAN (A/B experiments): "tile" one workgroup per tile; "dma" the
+    // persistent LDS-DMA kernel (PSCAN_WG_PER_CU workgroups per CU; measured
+    // slower: 1.12 vs 0.775 ms at C2); "loop" (default) the
+    // persistent register-staged loop, 8 workgroups per CU
+    static const int mode = [] {
         const char *e = exp_env("KMERHIP_SCAN");
-        return e && strcmp(e, "tile") == 0;
+        return !e ? 2 : strcmp(e, "tile") == 0 ? 0 : strcmp(e, "dma") == 0 ? 1 : 2;
     }();
-    if (!per_tile) {
-        const uint32_t grid = (uint32_t)std::min<uint64_t>(a.n_tiles, (uint64_t)std::max(n_cu, 1) * PSCAN_WG_PER_CU);
+    if (mode != 0) {
+        const uint64_t per_cu = mode == 1 ? PSCAN_WG_PER_CU : 8;
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(a.n_tiles, (uint64_t)std::max(n_cu, 1) * per_cu);
         const dim3 g(std::max<uint32_t>(grid, 1));
+#define KH_LAUNCH_P(F5, W)                                                                  \
+    do {                                                                                    \
+        if (mode == 1) hipLaunchKernelGGL((scan_planes_pkernel<F5, W, true>), g, dim3(TPB), 0, s, a, pa); \
+        else hipLaunchKernelGGL((scan_planes_pkernel<F5, W, false>), g, dim3(TPB), 0, s, a, pa);          \
+    } while (0)
         if (a.k > 32) {
-            if (pa.pb >= 5) hipLaunchKernelGGL((scan_planes_pkernel<true, true>), g, dim3(TPB), 0, s, a, pa);
-            else hipLaunchKernelGGL((scan_planes_pkernel<false, true>), g, dim3(TPB), 0, s, a, pa);
+            if (pa.pb >= 5) KH_LAUNCH_P(true, true);
+            else KH_LAUNCH_P(false, true);
         } else {
-            if (pa.pb >= 5) hipLaunchKernelGGL((scan_planes_pkernel<true, false>), g, dim3(TPB), 0, s, a, pa);
-            else hipLaunchKernelGGL((scan_planes_pkernel<false, false>), g, dim3(TPB), 0, s, a, pa);
+            if (pa.pb >= 5) KH_LAUNCH_P(true, false);
+            else KH_LAUNCH_P(false, false);
         }
+#undef KH_LAUNCH_P
         return hipGetLastError();
     }
     const dim3 g(a.n_tiles);

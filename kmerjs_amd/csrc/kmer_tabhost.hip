@@ -1,0 +1,388 @@
+// kmer_tabhost.hip — table mode orchestration (kernels: kmer_table.hip): pass 1 per chunk,
+// pass 2 + final at finish, host results of a table.
+#include "kmer_host.hpp"
+
+namespace kmerhip {
+
+// ---------------------------------------------------------------------------
+// table mode feed (kernels: kmer_table.hip)
+// ---------------------------------------------------------------------------
+// Pass 1 of one chunk: its sequence lines, then per workgroup share of lines
+// a histogram of keys by partition, a scan, and the scatter into tb1 after
+// the session's earlier keys.  Non-ACGT windows go to the host map.
+float ev_ms(kmer_ctx *c, hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) ms = 0.f;
+    return ms;
+}
+
+kmer_status table_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s) {
+    const uint64_t li0 = c->host_lines;
+    HIPCHK(c, hipEventRecord(c->ev0, s));
+    HIPCHK(c, hipEventRecord(c->tev[0], s));
+    uint64_t n_nl = 0, n_seq = 0;
+    kmer_status st = chunk_lines(c, d, len, n_tiles, s, false, &n_nl, &n_seq);
+    if (st) return st;
+    HIPCHK(c, launch_pos_after(c->d_pos, li0 + n_nl, d, len, c->d_ends_open, s));
+    c->host_lines = li0 + n_nl;
+    // long lines -> pieces of <= TAB_PIECE windows (balance pass 1's shares)
+    const SeqLine *plines = c->lines.p;
+    uint64_t n_items = n_seq;
+    if (n_seq) {
+        HIPCHK(c, c->tpc.ensure(n_seq + 1, s));
+        HIPCHK(c, c->tpb.ensure(n_seq, s));
+        uint32_t *split = c->tpc.p + n_seq;             // set when a line is not exactly one piece
+        HIPCHK(c, hipMemsetAsync(split, 0, 4, s));
+        HIPCHK(c, launch_tab_piece_count(c->wcount.p, n_seq, c->tpc.p, split, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 16, split, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        uint64_t n_pieces = n_seq;                // (no split: one piece per line)
+        if ((uint32_t)c->h_small[16]) {
+            ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tpc.p, c->tpb.p, (uint64_t)0, (size_t)n_seq,
+                                                   rocprim::plus<uint64_t>(), s));
+            HIPCHK(c, hipMemcpyAsync(c->h_small + 12, c->tpb.p + n_seq - 1, 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipMemcpyAsync(c->h_small + 13, c->tpc.p + n_seq - 1, 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            n_pieces = c->h_small[12] + (uint32_t)c->h_small[13];
+        }
+        if (n_pieces == 0) {
+            n_items = 0;                          // no line holds a window
+        } else if ((uint32_t)c->h_small[16]) {    // long lines (or empty ones, dropped on the way)
+            HIPCHK(c, c->tpieces.ensure(std::max<uint64_t>(n_pieces, 1), s));
+            HIPCHK(c, launch_tab_piece_write(c->lines.p, c->wcount.p, c->tpb.p, n_seq, c->p.k, c->tpieces.p, s));
+            plines = c->tpieces.p;
+            n_items = n_pieces;
+        }
+    }
+    HIPCHK(c, hipEventRecord(c->tev[1], s));
+    if (n_items) {
+        TabArgs a;
+        memset(&a, 0, sizeof(a));
+        a.data = d;
+        a.len = len;
+        a.lines = plines;
+        a.n_lines = n_items;
+        const uint64_t nwg0 = std::min<uint64_t>(8192, (n_items + 63) / 64);
+        a.lpw = (n_items + nwg0 - 1) / nwg0;
+        a.nwg = (uint32_t)((n_items + a.lpw - 1) / a.lpw);
+        a.k = c->p.k;
+        for (size_t i = 0; i < c->prefix.size(); ++i) {
+            const uint8_t ch = (uint8_t)c->prefix[i];
+            a.plo |= ((((uint32_t)ch >> 1) ^ ((uint32_t)ch >> 2)) & 1u) << i;
+            a.phi |= (((uint32_t)ch >> 2) & 1u) << i;
+        }
+        a.pmask = c->prefix.size() >= 32 ? ~0u : ((1u << c->prefix.size()) - 1u);
+        a.canonical = (c->p.flags & KMER_FLAG_CANONICAL) ? 1u : 0u;
+        a.err = c->d_err;
+        const uint64_t nh = (uint64_t)TAB_NB * a.nwg;
+        HIPCHK(c, c->tH.ensure(nh, s));
+        HIPCHK(c, c->tHs.ensure(nh, s));
+        HIPCHK(c, c->tp1.ensure(TAB_NB, s));
+        a.H1 = c->tH.p;
+        HIPCHK(c, launch_tab_hist1(a, s));
+        ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tH.p, c->tHs.p, (uint64_t)0, (size_t)nh,
+                                               rocprim::plus<uint64_t>(), s));
+        HIPCHK(c, launch_tab_p1_offsets(c->tHs.p, a.nwg, c->tp1.p, s));
+        std::vector<uint64_t> off(TAB_NB + 1);
+        HIPCHK(c, hipMemcpyAsync(off.data(), c->tp1.p, TAB_NB * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 14, c->tHs.p + nh - 1, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 15, c->tH.p + nh - 1, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipEventRecord(c->tev[2], s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        c->t_ms[0] += ev_ms(c, c->tev[0], c->tev[1]);
+        c->t_ms[1] += ev_ms(c, c->tev[1], c->tev[2]);
+        const uint64_t n_c = c->h_small[14] + (uint32_t)c->h_small[15];
+        off[TAB_NB] = n_c;
+        HIPCHK(c, c->tb1.ensure(c->t_keys + n_c, s, true, c->t_keys));
+        a.H1s = c->tHs.p;
+        a.base = c->t_keys;
+        a.B1 = c->tb1.p;
+        for (int attempt = 0;; ++attempt) {
+            a.recs = c->recs.p;
+            a.rec_count = c->d_rec_count;
+            a.rec_cap = c->recs.cap;
+            HIPCHK(c, hipMemsetAsync(c->d_rec_count, 0, 8, s));
+            HIPCHK(c, hipEventRecord(c->tev[2], s));
+            HIPCHK(c, launch_tab_scatter1(a, s));
+            HIPCHK(c, hipEventRecord(c->tev[3], s));
+            HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            const float ms_s1 = ev_ms(c, c->tev[2], c->tev[3]);
+            const uint32_t e = (uint32_t)c->h_small[5];
+            st = check_err(c, e);
+            if (st) return st;
+            if (!(e & ERR_REC_OVERFLOW)) {         // (a redo rewrites the same key ranges)
+                c->t_ms[2] += ms_s1;
+                break;
+            }
+            if (attempt == 7) return fail(c, KMER_E_OOM, "record list kept overflowing");
+            HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
+            st = ensure_records(c, c->h_small[0] + 1024);
+            if (st) return st;
+        }
+        const uint64_t nrec = c->h_small[0];
+        if (nrec) {
+            st = drain_records(c, d, nrec, s);
+            if (st) return st;
+        }
+        c->t_cbase.push_back(c->t_keys);
+        c->t_coff.push_back(std::move(off));
+        c->t_keys += n_c;
+    }
+    HIPCHK(c, hipEventRecord(c->ev1, s));
+    HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    c->scan_ms += ms;
+    c->feed_ms += ms;
+    c->chunk_open = c->h_small[7] != 0;
+    c->abs_offset += len;
+    return KMER_OK;
+}
+
+uint64_t inv_odd(uint64_t a) {   // inverse of an odd number mod 2^64 (Newton)
+    uint64_t x = a;
+    for (int i = 0; i < 5; ++i) x *= 2 - a * x;
+    return x;
+}
+
+// Pass 2 + final of the session: pass-1 partitions (one run per chunk) are
+// cut into units; each unit's keys go to their 2^20 buckets in tb2; the
+// final kernel merges each bucket in LDS and writes its entries into tb1.
+// B1: the pass-1 keys (default: this session's, tb1); [qlo, qhi): the buckets
+// present (multi-GPU: this rank's partitions; the others are left empty).
+kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t qhi) {
+    hipStream_t s = c->stream;
+    c->t_canon = c->t_nkeys = c->t_sum = c->t_nbig = 0;
+    c->t_done = true;
+    const uint64_t n = c->t_keys;
+    if (n == 0) return KMER_OK;
+    // the table is written over the pass-1 keys (dead after pass 2)
+    if (!B1) B1 = c->tb1.p;
+    c->t_ent = const_cast<uint64_t *>(B1);
+    std::vector<TabUnit> units;
+    std::vector<TabUnit> heads(TAB_NB);
+    uint64_t ubase = 0;
+    for (uint32_t p = 0; p < TAB_NB; ++p) {
+        const size_t first = units.size();
+        for (size_t ch = 0; ch < c->t_cbase.size(); ++ch) {
+            const uint64_t a0 = c->t_coff[ch][p], a1 = c->t_coff[ch][p + 1];
+            for (uint64_t o = a0; o < a1; o += TAB_UNIT) {
+                TabUnit u{};
+                u.start = c->t_cbase[ch] + o;
+                u.len = (uint32_t)std::min<uint64_t>(TAB_UNIT, a1 - o);
+                units.push_back(u);
+            }
+        }
+        if (units.size() == first) units.push_back(TabUnit{});   // empty partition: zero histogram row
+        const uint32_t nun = (uint32_t)(units.size() - first);
+        for (size_t i = first; i < units.size(); ++i) {
+            units[i].u = (uint32_t)(i - first);
+            units[i].nunits = nun;
+            units[i].hbase = ubase * TAB_NB;
+        }
+        heads[p] = units[first];
+        ubase += nun;
+    }
+    const uint64_t n_units = units.size();
+    if (n_units >= (1ull << 31)) return fail(c, KMER_E_BAD_PARAM, "too many table units");
+    units.insert(units.end(), heads.begin(), heads.end());
+    HIPCHK(c, c->tunits.ensure(units.size(), s));
+    HIPCHK(c, hipMemcpyAsync(c->tunits.p, units.data(), units.size() * sizeof(TabUnit), hipMemcpyHostToDevice, s));
+    const uint64_t nh = n_units * TAB_NB;
+    HIPCHK(c, c->tH.ensure(nh, s));
+    HIPCHK(c, c->tHs.ensure(nh, s));
+    HIPCHK(c, c->tb2.ensure(n, s));
+    HIPCHK(c, c->tstart.ensure(TAB_NQ + 1, s));
+    HIPCHK(c, c->tnd.ensure(TAB_NQ, s));
+    HIPCHK(c, c->tbig.ensure(1 << 16, s));
+    HIPCHK(c, c->tstats.ensure(5, s));
+    HIPCHK(c, hipEventRecord(c->tev[4], s));
+    HIPCHK(c, launch_tab_hist2(B1, c->tunits.p, (uint32_t)n_units, c->tH.p, s));
+    ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tH.p, c->tHs.p, (uint64_t)0, (size_t)nh,
+                                           rocprim::plus<uint64_t>(), s));
+    HIPCHK(c, hipEventRecord(c->tev[5], s));
+    HIPCHK(c, launch_tab_scatter2(B1, c->tunits.p, (uint32_t)n_units, c->tHs.p, c->tb2.p, s));
+    HIPCHK(c, hipEventRecord(c->tev[6], s));
+    HIPCHK(c, launch_tab_starts(c->tHs.p, c->tunits.p + n_units, n, c->tstart.p, s));
+    HIPCHK(c, hipMemsetAsync(c->tstats.p, 0, 4 * sizeof(unsigned long long), s));
+    TabFinal f;
+    memset(&f, 0, sizeof(f));
+    f.B2 = c->tb2.p;
+    f.start = c->tstart.p;
+    f.out = c->t_ent;
+    f.nd = c->tnd.p;
+    const uint64_t mean = n / TAB_NQ;
+    uint64_t range_keys = 3000;               // mean keys per LDS range (load ~0.37: short probes; measured best at C3)
+    if (const char *rk = exp_env("KMERHIP_TAB_RANGE")) range_keys = std::max<uint64_t>(64, strtoull(rk, nullptr, 10));
+    while (f.sub_bits < 16 && (mean >> f.sub_bits) > range_keys) ++f.sub_bits;
+    f.range_keys = (uint32_t)std::min<uint64_t>(range_keys, TAB_CAP);
+    f.cap = (c->p.flags & KMER_FLAG_TABLE_SPLIT_TEST) ? 64 : TAB_CAP;
+    if (const char *ab = exp_env("KMERHIP_TAB_ABLATE")) f.ablate = (uint32_t)atoi(ab);   // experiments only
+    f.big = c->tbig.p;
+    f.big_count = c->tstats.p + 3;
+    f.big_cap = c->tbig.cap;
+    f.err = c->d_err;
+    f.k = c->p.k;
+    for (size_t i = 0; i < c->prefix.size(); ++i) {
+        const uint8_t ch = (uint8_t)c->prefix[i];
+        f.plo |= ((((uint32_t)ch >> 1) ^ ((uint32_t)ch >> 2)) & 1u) << i;
+        f.phi |= (((uint32_t)ch >> 2) & 1u) << i;
+    }
+    f.pmask = c->prefix.size() >= 32 ? ~0u : ((1u << c->prefix.size()) - 1u);
+    f.inv = inv_odd(TAB_MUL);
+    f.canonical = (c->p.flags & KMER_FLAG_CANONICAL) ? 1u : 0u;
+    f.stats = c->tstats.p;
+    f.qlo = qlo;
+    f.qhi = qhi;
+    if (qlo != 0 || qhi != TAB_NQ) HIPCHK(c, hipMemsetAsync(c->tnd.p, 0, TAB_NQ * sizeof(uint32_t), s));
+    const uint32_t fgrid = (uint32_t)std::max(c->n_cu, 1);
+    std::vector<uint64_t> hprof;
+#ifdef TAB_PROF
+    if (exp_env("KMERHIP_TAB_PROF")) {         // experiments (-DTAB_PROF build): per-phase clocks of the final kernel
+#else
+    if (false) {
+#endif
+        HIPCHK(c, hipMalloc((void **)&f.prof, fgrid * 64ull));
+        HIPCHK(c, hipMemsetAsync(f.prof, 0, fgrid * 64ull, s));
+        hprof.resize(fgrid * 8ull);
+    }
+    // the sort kernel (two workgroups per CU) takes every unit it can; the
+    // general kernel (hash path, range splits) takes the ones it leaves
+    // (crowded buckets, many copies of a key).  KMERHIP_TAB_FINAL=general: the
+    // general kernel alone (A/B experiments).
+    const char *fk = exp_env("KMERHIP_TAB_FINAL");
+    const bool sort_first = !(fk && strcmp(fk, "general") == 0) && !f.prof &&
+                            !(c->p.flags & KMER_FLAG_TABLE_SPLIT_TEST);
+    HIPCHK(c, hipEventRecord(c->tev[2], s));
+    if (sort_first) {
+        HIPCHK(c, c->tleft.ensure(2ull * TAB_NQ + 1, s));
+        f.left = c->tleft.p + 1;
+        f.left_n = c->tleft.p;
+        HIPCHK(c, hipMemsetAsync(c->tleft.p, 0, 4, s));
+        HIPCHK(c, launch_tab_sort_final(f, 2 * fgrid, s));
+    }
+    HIPCHK(c, launch_tab_final(f, fgrid, s));
+    HIPCHK(c, hipEventRecord(c->tev[7], s));
+    if (f.prof) {
+        HIPCHK(c, hipMemcpyAsync(hprof.data(), f.prof, fgrid * 64ull, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        (void)hipFree(f.prof);
+        double ph[6] = {0, 0, 0, 0, 0, 0};
+        uint64_t ranges = 0, buckets = 0;
+        for (uint32_t g = 0; g < fgrid; ++g) {
+            for (int i = 0; i < 6; ++i) ph[i] += i == 4 ? 0 : (double)hprof[g * 8 + i] * 0.01 / fgrid;   // us
+            ranges += hprof[g * 8 + 4] >> 32;
+            buckets += hprof[g * 8 + 4] & 0xFFFFFFFFull;
+        }
+        fprintf(stderr, "tab_final prof (us per workgroup): load+setup %.0f range-syncs %.0f insert %.0f emit %.0f "
+                        "empty %.0f | buckets %llu ranges %llu sub_bits %u\n", ph[0], ph[1], ph[2], ph[3], ph[5],
+                (unsigned long long)buckets, (unsigned long long)ranges, f.sub_bits);
+    }
+    HIPCHK(c, hipMemcpyAsync(c->h_small + 8, c->tstats.p, 4 * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    c->t_ms[3] += ev_ms(c, c->tev[4], c->tev[5]);
+    c->t_ms[4] += ev_ms(c, c->tev[5], c->tev[6]);
+    c->t_ms[5] += ev_ms(c, c->tev[2], c->tev[7]);
+    const uint32_t e = (uint32_t)c->h_small[5];
+    if (e & ERR_COUNT_OVERFLOW) return fail(c, KMER_E_TOO_MANY_KEYS, "a k-mer count exceeds 2^32 - 1");
+    if (e & ERR_BIG_OVERFLOW) return fail(c, KMER_E_OOM, "too many k-mers with counts >= 2^20");
+    if (e & ERR_TAB_SPLIT) return fail(c, KMER_E_DEVICE, "table bucket could not be split");
+    c->t_canon = c->h_small[8];
+    c->t_nkeys = c->h_small[9];
+    c->t_sum = c->h_small[10];
+    c->t_nbig = c->h_small[11];
+    c->n_out = c->t_nkeys;
+    return KMER_OK;
+}
+
+// Canonical classes of the record keys (KMER_FLAG_CANONICAL: forward windows)
+std::unordered_map<std::string, uint64_t> canonical_records(const kmer_ctx *c) {
+    std::unordered_map<std::string, uint64_t> cls;
+    for (auto &kv : c->exotic) {
+        std::string r(kv.first.rbegin(), kv.first.rend());
+        for (char &ch : r) ch = (char)comp((uint8_t)ch);
+        cls[std::min(kv.first, r)] += kv.second.count;
+    }
+    return cls;
+}
+
+// Host result of a table finish: every canonical entry expanded into its Map
+// keys (c and rc c, prefix-filtered; palindromes counted twice), plus the
+// record keys; entries sorted by key bytes (the table has no order).
+kmer_status build_table_result(kmer_ctx *c, uint64_t lines, kmer_result **out) {
+    kmer_result *r = new (std::nothrow) kmer_result();
+    if (!r) return fail(c, KMER_E_OOM, "host allocation failed");
+    r->lines = lines;
+    std::vector<std::pair<std::string, uint64_t>> ents;
+    const uint32_t k = c->p.k;
+    if (c->t_keys) {
+        hipStream_t s = c->stream;
+        std::vector<uint64_t> start(TAB_NQ + 1), ent(c->t_keys);
+        std::vector<uint32_t> nd(TAB_NQ);
+        std::vector<TabBig> big(c->t_nbig);
+        bool ok = hipMemcpyAsync(start.data(), c->tstart.p, start.size() * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
+                  hipMemcpyAsync(nd.data(), c->tnd.p, nd.size() * 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
+                  hipMemcpyAsync(ent.data(), c->t_ent, ent.size() * 8, hipMemcpyDeviceToHost, s) == hipSuccess;
+        if (ok && !big.empty())
+            ok = hipMemcpyAsync(big.data(), c->tbig.p, big.size() * sizeof(TabBig), hipMemcpyDeviceToHost, s) == hipSuccess;
+        if (!ok || hipStreamSynchronize(s) != hipSuccess) {
+            delete r;
+            return fail(c, KMER_E_DEVICE, "result copy failed");
+        }
+        std::unordered_map<uint64_t, uint64_t> bigc;
+        for (auto &b : big) bigc[b.h] = b.count;
+        const uint64_t inv = inv_odd(TAB_MUL);
+        const bool canon = (c->p.flags & KMER_FLAG_CANONICAL) != 0;
+        const uint64_t kmask = k >= 32 ? 0xFFFFFFFFull : ((1ull << k) - 1);
+        std::string key(k, 'A'), rkey(k, 'A');
+        for (uint32_t q = 0; q < TAB_NQ; ++q) {
+            for (uint32_t i = 0; i < nd[q]; ++i) {
+                const uint64_t w = ent[start[q] + i];
+                const uint64_t h = ((uint64_t)q << TAB_RBITS) | (w >> 20);
+                uint64_t cnt = w & TAB_CMAX;
+                if (cnt == TAB_CMAX) cnt = bigc[h];
+                const uint64_t x = h * inv;          // tab_mix^-1
+                const uint64_t lo = x & kmask, hi = (x >> k) & kmask;
+                for (uint32_t j = 0; j < k; ++j) {
+                    const uint32_t v = (uint32_t)(((hi >> j) & 1u) << 1 | ((lo >> j) & 1u));
+                    key[j] = "ACGT"[v];
+                    rkey[k - 1 - j] = "TGCA"[v];
+                }
+                const bool pal = key == rkey;
+                if (canon) {                          // one key per class, counted once per window
+                    const std::string &ck = key < rkey ? key : rkey;
+                    if (ck.compare(0, c->prefix.size(), c->prefix) == 0) ents.emplace_back(ck, cnt);
+                    continue;
+                }
+                if (key.compare(0, c->prefix.size(), c->prefix) == 0) ents.emplace_back(key, pal ? 2 * cnt : cnt);
+                if (!pal && rkey.compare(0, c->prefix.size(), c->prefix) == 0) ents.emplace_back(rkey, cnt);
+            }
+        }
+    }
+    if (c->p.flags & KMER_FLAG_CANONICAL) {
+        // record keys (non-ACGT windows; forward windows only, unfiltered):
+        // classed under min(x, rc x), then the prefix is tested on that key
+        for (auto &kv : canonical_records(c))
+            if (kv.first.compare(0, c->prefix.size(), c->prefix) == 0) ents.emplace_back(kv.first, kv.second);
+    } else {
+        for (auto &kv : c->exotic) ents.emplace_back(kv.first, kv.second.count);
+    }
+    std::sort(ents.begin(), ents.end());
+    r->keys.reserve(ents.size() * k);
+    r->offsets.reserve(ents.size() + 1);
+    r->counts.reserve(ents.size());
+    for (auto &e : ents) {
+        r->keys.insert(r->keys.end(), e.first.begin(), e.first.end());
+        r->offsets.push_back(r->keys.size());
+        r->counts.push_back(e.second);
+        r->firsts.push_back(0);
+    }
+    *out = r;
+    return KMER_OK;
+}
+
+
+}  // namespace kmerhip

@@ -90,7 +90,7 @@ def split_at_records(buf: bytes, world):
 
 
 def invalid_key(k, plen):
-    """Packed-key sentinel of the device reduce: 1 << 2(k-|P|) (kmer_api.hip)."""
+    """Packed-key sentinel of the device reduce: 1 << 2(k-|P|) (kmer_finish.hip)."""
     return 1 << (2 * (k - plen))
 
 
@@ -243,7 +243,7 @@ def finish_exchange(ctr, k, plen, total_lines, group=None, want_result=False, re
 
 
 def table_part_range(o, world, parts=1024):
-    """Pass-1 partitions [lo, hi) owned by rank o (tab_part_lo, kmer_api.hip)."""
+    """Pass-1 partitions [lo, hi) owned by rank o (tab_part_lo, kmer_api.hip / kmer_tabhost.hip)."""
     return o * parts // world, (o + 1) * parts // world
 
 
