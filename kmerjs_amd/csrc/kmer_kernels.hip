@@ -2856,13 +2856,13 @@ hipError_t launch_lines(const TileArgs &a, bool lookback, hipStream_t s) {
 }
 
 hipError_t launch_scan_planes(const ScanArgs &a, const PlaneArgs &pa, int n_cu, hipStream_t s) {
-    // KMERHIP_SCAN (A/B experiments): "tile" one workgroup per tile; "dma" the
+    // one workgroup per tile.  KMERHIP_SCAN (A/B experiments): "dma" the
     // persistent LDS-DMA kernel (PSCAN_WG_PER_CU workgroups per CU; measured
-    // slower: 1.12 vs 0.775 ms at C2); "loop" (default) the
-    // persistent register-staged loop, 8 workgroups per CU
+    // slower: 1.12 vs 0.775 ms at C2); "loop" the persistent
+    // register-staged loop, 8 workgroups per CU
     static const int mode = [] {
         const char *e = exp_env("KMERHIP_SCAN");
-        return !e ? 2 : strcmp(e, "tile") == 0 ? 0 : strcmp(e, "dma") == 0 ? 1 : 2;
+        return !e ? 0 : strcmp(e, "dma") == 0 ? 1 : strcmp(e, "loop") == 0 ? 2 : 0;
     }();
     if (mode != 0) {
         const uint64_t per_cu = mode == 1 ? PSCAN_WG_PER_CU : 8;
