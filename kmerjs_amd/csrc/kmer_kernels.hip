@@ -56,6 +56,13 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
     return x;
 }
 
+// '\n' bytes among four ASCII bytes (< 0x80): bit 7 of (x ^ "\n\n\n\n") +
+// 0x7F per byte is set iff the byte is NOT '\n' (no carries: every byte < 0x80),
+// so the count is 4 - popcount.  One v_xad_u32 + and + bcnt per word.
+__device__ __forceinline__ uint32_t not_nl_bits(uint32_t x) {
+    return ((x ^ 0x0A0A0A0Au) + 0x7F7F7F7Fu) & 0x80808080u;
+}
+
 // per-byte 0x80 flag for bytes equal to '\n'; exact for ASCII bytes (< 0x80)
 __device__ __forceinline__ uint32_t nl_flags(uint32_t x) {
     uint32_t t = x ^ 0x0A0A0A0Au;
@@ -439,7 +446,7 @@ __device__ __forceinline__ void emit_hit(const ScanArgs &a, const uint8_t *buf, 
     const int q = (int)(e >> 1);
     const int s0 = strand ? q + (int)plen - (int)k : q;   // window start, tile-relative
     // window bytes: ACGT check (v_perm against "ACGT"), '\n' check, 2-bit codes
-    bool exotic = false, hasnl = false;
+    uint32_t exo_bits = 0, nl_bits = 0;          // (OR-accumulated; tested once)
     uint64_t code = 0;
     const int sfx0 = strand ? 0 : (int)plen, sfx1 = strand ? (int)(k - plen) : (int)k;   // suffix bytes
 #pragma unroll 4
@@ -450,12 +457,13 @@ __device__ __forceinline__ void emit_hit(const ScanArgs &a, const uint8_t *buf, 
         const uint32_t c = ((x >> 1) ^ (x >> 2)) & 0x03030303u;
         const uint32_t expect = __builtin_amdgcn_perm(0u, 0x54474341u, c);   // "ACGT"[c] per byte
         const uint32_t mx = THREAD_MAP ? mk : mk & byte_range_mask(sfx0 - (int)b, sfx1 - (int)b);
-        exotic |= ((expect ^ x) & mx) != 0;
-        hasnl |= (nl_flags(x) & mk) != 0;
-        const uint32_t pk = ((c & 3u) << 6) | (((c >> 8) & 3u) << 4) | (((c >> 16) & 3u) << 2) |
-                            ((c >> 24) & 3u);                // first byte most significant
+        exo_bits |= (expect ^ x) & mx;
+        nl_bits |= nl_flags(x) & mk;
+        // the four 2-bit codes, first byte most significant: c0 * 64 + c1 * 16 + c2 * 4 + c3
+        const uint32_t pk = __builtin_amdgcn_udot4(c, 0x01041040u, 0u, false);
         code = (code << (2 * nb)) | (pk >> (2 * (4 - nb)));
     }
+    const bool exotic = exo_bits != 0, hasnl = nl_bits != 0;
     // k > 32: code keeps the last 32 bases; the first k - 32 (the window's
     // bytes are ACGT-checked above)
     uint64_t chi = 0;
@@ -464,7 +472,7 @@ __device__ __forceinline__ void emit_hit(const ScanArgs &a, const uint8_t *buf, 
             const uint32_t x = lds_word(buf, s0 + (int)b);
             const uint32_t nb = k - 32 - b >= 4 ? 4u : k - 32 - b;
             const uint32_t c = ((x >> 1) ^ (x >> 2)) & 0x03030303u;
-            const uint32_t pk = ((c & 3u) << 6) | (((c >> 8) & 3u) << 4) | (((c >> 16) & 3u) << 2) | ((c >> 24) & 3u);
+            const uint32_t pk = __builtin_amdgcn_udot4(c, 0x01041040u, 0u, false);
             chi = (chi << (2 * nb)) | (pk >> (2 * (4 - nb)));
         }
     }
@@ -912,7 +920,8 @@ __global__ __launch_bounds__(TPB) void scan_planes_kernel(ScanArgs a, PlaneArgs 
         uint32_t cnt = 0;
         if (!tail_tile) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) cnt += __popc(nl_flags(w[4 * j + i]));
+            for (int i = 0; i < 4; ++i) cnt += __popc(not_nl_bits(w[4 * j + i]));
+            cnt = 16u - cnt;
         } else {
             const int64_t gc = g0 + 64 * tid + 16 * j;
 #pragma unroll
@@ -1240,7 +1249,8 @@ void scan_planes_pkernel(ScanArgs a, PlaneArgs pa) {
             uint32_t cnt = 0;
             if (!tail_tile) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) cnt += __popc(nl_flags(w[4 * j + i]));
+                for (int i = 0; i < 4; ++i) cnt += __popc(not_nl_bits(w[4 * j + i]));
+            cnt = 16u - cnt;
             } else {
                 const int64_t gc = g0 + 64 * tid + 16 * j;
 #pragma unroll
