@@ -489,7 +489,6 @@ struct TabFinal {
     // [qlo, qhi) when `left` is set
     uint32_t *left;
     unsigned int *left_n;
-    uint32_t pf;                   // sort final: warm the caches with the next unit's keys while one is sorted
 };
 
 constexpr uint64_t TAB_PIECE = 4096;                   // windows per piece of a long line (pass 1)

@@ -220,9 +220,6 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
     f.range_keys = (uint32_t)std::min<uint64_t>(range_keys, TAB_CAP);
     f.cap = (c->p.flags & KMER_FLAG_TABLE_SPLIT_TEST) ? 64 : TAB_CAP;
     if (const char *ab = exp_env("KMERHIP_TAB_ABLATE")) f.ablate = (uint32_t)atoi(ab);   // experiments only
-    // KMERHIP_TAB_PF=1 (A/B experiments): the sort final kernel warms the
-    // caches with the next unit's keys
-    if (const char *pf = exp_env("KMERHIP_TAB_PF")) f.pf = (uint32_t)atoi(pf);
     f.big = c->tbig.p;
     f.big_count = c->tstats.p + 3;
     f.big_cap = c->tbig.cap;

@@ -1154,7 +1154,6 @@ constexpr uint32_t TS_SC = 512;                       // bucket starts cached pe
 
 }  // namespace
 
-template <bool PF>
 __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) {
     __shared__ uint32_t lkey[TS_CAP1];                // sorted unit: u32 (one bucket) or u64 (a group)
     __shared__ uint32_t bst[TS_NB];                   // bin counts, then starts
@@ -1168,8 +1167,6 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
     const uint32_t per = (a.qhi - a.qlo + gridDim.x - 1) / gridDim.x;
     const uint32_t q0 = min(a.qlo + blockIdx.x * per, a.qhi), q1 = q0 + per < a.qhi ? q0 + per : a.qhi;
     uint64_t st_canon = 0, st_keys = 0, st_sum = 0;
-    __shared__ uint32_t pfs[64 * (TAB_SWG / 64)];      // cache-warming LDS-DMA target (never read)
-    const uint64_t ne = PF ? a.start[a.qhi] : 0;       // (end of this table's keys)
     // no prefix, odd k, Map view (C3): every entry is two Map keys, never a
     // palindrome -- no decoding needed
     const bool plain_odd = a.pmask == 0 && !a.canonical && (k & 1u);
@@ -1265,26 +1262,6 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                     lo[j] = (uint32_t)x;
                     if (!ONE) hi[ONE ? 0 : j] = (uint32_t)(x >> 32);
                     pk[j] = (uint32_t)(x >> bsh) & (TS_NB - 1);
-                }
-            }
-            // the next unit's keys (up to one bucket's worth after this unit):
-            // one 4-B LDS-DMA load per 128-B line into a scratch LDS area that is
-            // never read -- no VGPR, and no wait of the compiler's drains it --
-            // so the lines are on their way into L2 / the Infinity Cache while
-            // this unit is sorted
-            if (PF && qe - cbase < TS_SC + 1) {
-                const uint64_t nx = sc[qe - cbase];
-                const uint32_t dst = (uint32_t)(uintptr_t)(pfs + 64 * (t >> 6));
-#pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    uint64_t o = nx + 16ull * (t + i * TAB_SWG);
-                    o = o < ne && o < nx + TS_CAP1 ? o : nx;
-                    const uint32_t *g = (const uint32_t *)(a.B2 + o);
-                    uint32_t keep;
-                    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                                 : "=&s"(keep)
-                                 : "v"(g), "s"(__builtin_amdgcn_readfirstlane(dst))
-                                 : "memory");
                 }
             }
             __syncthreads();                           // the previous unit is done with the LDS state
@@ -1434,7 +1411,6 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
         st_keys += __shfl_xor(st_keys, d);
         st_sum += __shfl_xor(st_sum, d);
     }
-    if (PF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the warming copies have landed)
     if (lane == 0 && st_canon) {
         atomicAdd(&a.stats[0], (unsigned long long)st_canon);
         atomicAdd(&a.stats[1], (unsigned long long)st_keys);
@@ -1558,8 +1534,7 @@ hipError_t launch_tab_digest(const uint64_t *ent, const uint64_t *start, const u
 }
 
 hipError_t launch_tab_sort_final(const TabFinal &a, uint32_t grid, hipStream_t s) {
-    if (a.pf) hipLaunchKernelGGL(tab_sort_final_kernel<true>, dim3(grid), dim3(TAB_SWG), 0, s, a);
-    else hipLaunchKernelGGL(tab_sort_final_kernel<false>, dim3(grid), dim3(TAB_SWG), 0, s, a);
+    hipLaunchKernelGGL(tab_sort_final_kernel, dim3(grid), dim3(TAB_SWG), 0, s, a);
     return hipGetLastError();
 }
 
