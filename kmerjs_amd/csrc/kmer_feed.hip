@@ -169,6 +169,10 @@ void bind_hits(kmer_ctx *c, HitArgs &h) {
     h.xkeyh = c->xkeyh.p;
     h.xbase = c->n_cross;
     h.xcap = c->xord.cap;
+    uint64_t rcap = c->narrow ? c->rkey32.cap : c->rkey.cap;
+    rcap = std::min<uint64_t>(rcap, c->rord.cap);
+    if (c->wide) rcap = std::min<uint64_t>(rcap, c->rkeyh.cap);
+    h.rcap = rcap;
 }
 
 // One attempt at the pending chunk: scan, tile scan, hit resolution and the
@@ -177,7 +181,7 @@ kmer_status launch_chunk(kmer_ctx *c) {
     auto &p = c->pend;
     const hipStream_t s = p.s;
     HIPCHK(c, hipEventRecord(c->ev0, s));
-    if (c->planes) HIPCHK(c, launch_scan_planes(p.a, c->pargs, c->n_cu, s));
+    if (c->planes) HIPCHK(c, launch_scan_planes(p.a, c->pargs, s));
     else HIPCHK(c, launch_scan_tiles(p.a, s));
     HIPCHK(c, hipEventRecord(c->ev1, s));
     HIPCHK(c, launch_tile_reduce(c->tsum.p, p.n_tiles, c->bsum.p, s));

@@ -191,6 +191,7 @@ struct HitArgs {
     uint64_t *rkeyh;
     uint64_t *xkeyh, *xkeyl;
     uint64_t out_base;             // session hits before this chunk
+    uint64_t rcap;                 // capacity of the rank arrays (a slot past it: the chunk overflowed and is redone)
     uint64_t *rkey;                // by rank: suffix code (invalid_key: filtered / record)
     uint32_t *rkey32;              // ... as u32 when 2(k-|P|) + 1 <= 32 (then rkey is unused)
     uint64_t *rord;                // by rank: first-occurrence order key
@@ -317,7 +318,7 @@ struct WinArgs {
 // ---- launchers (kmer_kernels.hip) ------------------------------------------
 hipError_t launch_lines(const TileArgs &a, bool lookback, hipStream_t s);
 hipError_t launch_scan_tiles(const ScanArgs &a, hipStream_t s);
-hipError_t launch_scan_planes(const ScanArgs &a, const PlaneArgs &pa, int n_cu, hipStream_t s);
+hipError_t launch_scan_planes(const ScanArgs &a, const PlaneArgs &pa, hipStream_t s);
 hipError_t launch_hits(const HitArgs &a, hipStream_t s);
 // exclusive scan of the per-tile sums (init folded in); bsum / bscan: n_blocks scratch
 hipError_t launch_tile_reduce(const TileSum *in, uint32_t n, TileSum *bsum, hipStream_t s);

@@ -1085,339 +1085,6 @@ __global__ __launch_bounds__(TPB) void scan_planes_kernel(ScanArgs a, PlaneArgs 
     }
 }
 
-// ---------------------------------------------------------------------------
-// Persistent plane kernel: the same per-tile work as scan_planes_kernel, but
-// each workgroup walks tiles blockIdx.x, + gridDim.x, ... and the NEXT tile is
-// copied HBM -> LDS by LDS-DMA (global_load_lds_dwordx4: no VGPR staging)
-// into the second of two tile buffers while the current one is processed.
-// In scan_planes_kernel a workgroup's load and its compute run strictly one
-// after the other, so the bytes in flight per CU drop whenever its workgroups
-// compute (the no-candidate ablation ran at 0.64 of HBM peak); here every
-// workgroup keeps a 16 KiB tile in flight through its whole compute phase.
-// The DMA stays in flight across the tile's barriers: they wait for LDS
-// operations only (lgkmcnt), and the copy is waited for (vmcnt(0)) once, at
-// the tile's last barrier.  Tiles at the ends of the chunk (whose halos reach
-// outside [0, len)) are staged through registers with '\n' padding instead.
-// ---------------------------------------------------------------------------
-constexpr int PBUF = (BUFSZ + 15) & ~15;     // one tile buffer (tile + halos), 16-B aligned
-constexpr uint32_t PSCAN_WG_PER_CU = 4;      // 2 x 16.5 KiB buffers + ScanShared per workgroup
-
-// barrier over LDS traffic only: an LDS-DMA in flight is not waited for
-#define KH_LDS_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
-// ... and over the workgroup's LDS-DMA copies (and every other vector memory op)
-#define KH_DMA_BARRIER() asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory")
-
-__device__ __forceinline__ uint32_t lds_addr(const void *p) {
-    return (uint32_t)(uintptr_t)p;       // LDS aperture address: the low 32 bits are the LDS byte offset
-}
-
-// one wave-instruction: lane l copies 16 bytes from gsrc (its own address) to
-// LDS byte lds_base + 16 l (lds_base wave-uniform)
-__device__ __forceinline__ void dma16(const uint8_t *gsrc, uint32_t lds_base) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(gsrc), "s"(lds_base)
-                 : "memory");
-}
-
-__device__ __forceinline__ bool tile_interior(int64_t g0, uint64_t len) {
-    return g0 - FH >= 0 && (uint64_t)(g0 + TILE + BH) <= len;
-}
-
-// Tile + halos of an interior tile into `buf` by LDS-DMA: 16 wave-instructions
-// of 1 KiB for the tile (4 per wave), one for each halo.
-__device__ __forceinline__ void tile_dma(const uint8_t *data, int64_t g0, uint8_t *buf) {
-    const int lane = threadIdx.x & 63;
-    const int wid = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const uint32_t base = lds_addr(buf);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int blk = 4 * wid + i;                         // 1 KiB block of the tile
-        dma16(data + g0 + 1024 * blk + 16 * lane, base + FH + 1024 * blk);
-    }
-    if (wid == 0 && lane < NCH_FRONT) dma16(data + g0 - FH + 16 * lane, base);
-    if (wid == 1 && lane < NCH_BACK) dma16(data + g0 + TILE + 16 * lane, base + FH + TILE);
-}
-
-// Tile + halos of an edge tile into `buf` through registers (bytes outside
-// [0, len) read as '\n')
-__device__ __forceinline__ void tile_fill_regs(const uint8_t *data, int64_t g0, uint64_t len, uint8_t *buf) {
-    const int tid = threadIdx.x;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-        *(uint4 *)(buf + FH + (tid + TPB * i) * 16) = load_chunk(data, g0 + (int64_t)(tid + TPB * i) * 16, len);
-    if (tid < NCH_FRONT + NCH_BACK) {
-        const int hc = tid < NCH_FRONT ? tid : NCH_FRONT + NCH_MAIN + (tid - NCH_FRONT);
-        *(uint4 *)(buf + hc * 16) = load_chunk(data, g0 - FH + (int64_t)hc * 16, len);
-    }
-}
-
-// Tile staged through registers (interior tiles: four 16-B loads per lane,
-// no bounds tests)
-__device__ __forceinline__ void tile_load_regs(const uint8_t *data, int64_t g0, uint64_t len, uint8_t *buf) {
-    if (!tile_interior(g0, len)) {
-        tile_fill_regs(data, g0, len, buf);
-        return;
-    }
-    const int tid = threadIdx.x;
-    const uint8_t *src = data + g0 + 16 * tid;
-    uint4 v[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = *(const uint4 *)(src + 16 * TPB * i);
-    uint4 vh = make_uint4(0, 0, 0, 0);
-    const bool halo = tid < NCH_FRONT + NCH_BACK;
-    const int hc = tid < NCH_FRONT ? tid : NCH_FRONT + NCH_MAIN + (tid - NCH_FRONT);
-    if (halo) vh = *(const uint4 *)(data + g0 - FH + 16 * hc);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) *(uint4 *)(buf + FH + (tid + TPB * i) * 16) = v[i];
-    if (halo) *(uint4 *)(buf + hc * 16) = vh;
-}
-
-// DMA: two tile buffers, the next tile copied by LDS-DMA during the current
-// one (PSCAN_WG_PER_CU workgroups per CU).  !DMA: one buffer, each tile loaded
-// through registers at the top of its iteration -- the persistent loop alone
-// (8 workgroups per CU, as many as the per-tile kernel holds), which saves the
-// per-workgroup dispatch of scan_planes_kernel.
-template <bool FULL5, bool WIDE, bool DMA>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(DMA ? 4 : 7, 8)))
-void scan_planes_pkernel(ScanArgs a, PlaneArgs pa) {
-    __shared__ __attribute__((aligned(16))) uint8_t bufs[(DMA ? 2 : 1) * PBUF];
-    __shared__ ScanShared sh;
-    __shared__ __attribute__((aligned(16))) uint8_t s_pr[2 * KMAX_TILE];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint64_t len = a.len;
-    uint32_t tile = blockIdx.x;
-    if (tile >= a.n_tiles) return;                 // (uniform: the whole workgroup leaves)
-    if (tid < 2 * KMAX_TILE) s_pr[tid] = a.PR[tid];
-    if (tid == 0) {
-        sh.last_chunk = -1;
-        sh.nh = 0;
-        sh.nx = 0;
-        sh.qn = 0;
-    }
-    if (DMA) {
-        const int64_t g0 = (int64_t)tile * TILE;
-        if (tile_interior(g0, len)) tile_dma(a.data, g0, bufs);
-        else tile_fill_regs(a.data, g0, len, bufs);
-        KH_DMA_BARRIER();
-    }
-    const uint32_t *pw = (const uint32_t *)s_pr;
-    uint2 *qe = (uint2 *)sh.q;
-    constexpr uint32_t QE = QCAP / 2;
-    uint32_t b = 0;
-    while (true) {
-        uint8_t *buf = bufs + (DMA ? b * PBUF : 0);
-        const int64_t g0 = (int64_t)tile * TILE;
-        const uint32_t nxt = tile + gridDim.x;
-        const bool have_next = nxt < a.n_tiles;
-        const int64_t g1 = (int64_t)nxt * TILE;
-        const bool next_dma = DMA && have_next && tile_interior(g1, len);
-        // the other buffer was last read before the previous tile's final barrier
-        if (next_dma) tile_dma(a.data, g1, bufs + (b ^ 1u) * PBUF);
-        if (!DMA) {
-            tile_load_regs(a.data, g0, len, buf);
-            KH_LDS_BARRIER();
-        }
-
-        // ---- this thread's 64 bytes (4 chunks) + 4 look-ahead bytes ----
-        uint32_t w[17];
-        {
-            const uint4 *src = (const uint4 *)(buf + FH + 64 * tid);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint4 x = src[j];
-                w[4 * j] = x.x;
-                w[4 * j + 1] = x.y;
-                w[4 * j + 2] = x.z;
-                w[4 * j + 3] = x.w;
-            }
-            w[16] = *(const uint32_t *)(buf + FH + 64 * tid + 64);
-        }
-        {
-            // non-ASCII bytes (every tile byte is some thread's; halos are their
-            // neighbours' tile bytes, or '\n' padding)
-            uint32_t orall = 0;
-#pragma unroll
-            for (int j = 0; j < 16; ++j) orall |= w[j];
-            if (orall & 0x80808080u) atomicOr(a.err, ERR_NONASCII);
-        }
-        const bool tail_tile = (uint64_t)(g0 + TILE) > len;
-        uint32_t ccnt[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            uint32_t cnt = 0;
-            if (!tail_tile) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) cnt += __popc(not_nl_bits(w[4 * j + i]));
-            cnt = 16u - cnt;
-            } else {
-                const int64_t gc = g0 + 64 * tid + 16 * j;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int64_t n = (int64_t)len - (gc + 4 * i);
-                    uint32_t z = nl_flags(w[4 * j + i]);
-                    z = n <= 0 ? 0u : n < 4 ? (z & ((1u << (8 * n)) - 1u)) : z;
-                    cnt += __popc(z);
-                }
-            }
-            ccnt[j] = cnt;
-        }
-        const uint32_t ttot = ccnt[0] + ccnt[1] + ccnt[2] + ccnt[3];
-        {
-            const unsigned long long m = __ballot(ttot != 0);
-            if (lane == 0) {
-                sh.nlmap[2 * wid] = (uint32_t)m;
-                sh.nlmap[2 * wid + 1] = (uint32_t)(m >> 32);
-                if (m) atomicMax(&sh.last_chunk, 64 * wid + 63 - (int)__clzll((long long)m));
-            }
-        }
-        const uint32_t incl = wave_incl_sum(ttot);
-        if (lane == 63) sh.wsum[wid][0] = incl;
-
-        // ---- bit-planes and the prefix test (scan_planes_kernel) ----
-        const uint32_t W0 = 0x08040201u, W1 = 0x80402010u;
-        uint32_t L[3], H[3];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            uint32_t gl[4], gh[4];
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                const uint32_t x0 = w[8 * h + 2 * p], x1 = w[8 * h + 2 * p + 1];
-                gl[p] = __builtin_amdgcn_udot4(x0 & 0x02020202u, W0,
-                                               __builtin_amdgcn_udot4(x1 & 0x02020202u, W1, 0u, false), false);
-                gh[p] = __builtin_amdgcn_udot4(x0 & 0x04040404u, W0,
-                                               __builtin_amdgcn_udot4(x1 & 0x04040404u, W1, 0u, false), false);
-            }
-            L[h] = (gl[0] >> 1) | (gl[1] << 7) | (gl[2] << 15) | (gl[3] << 23);
-            H[h] = (gh[0] >> 2) | (gh[1] << 6) | (gh[2] << 14) | (gh[3] << 22);
-        }
-        {
-            const uint32_t x = w[16];
-            L[2] = __builtin_amdgcn_udot4(x & 0x02020202u, W0, 0u, false) >> 1;
-            H[2] = __builtin_amdgcn_udot4(x & 0x04040404u, W0, 0u, false) >> 2;
-        }
-        uint32_t mf[2], mr[2];
-        const uint32_t pb = FULL5 ? 5u : pa.pb;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            uint32_t SL[5], SH[5];
-            SL[0] = L[h];
-            SH[0] = H[h];
-#pragma unroll
-            for (uint32_t i = 1; i < 5; ++i) {
-                SL[i] = __builtin_amdgcn_alignbit(L[h + 1], L[h], i);
-                SH[i] = __builtin_amdgcn_alignbit(H[h + 1], H[h], i);
-            }
-            mf[h] = plane_match(L[h], H[h], L[h + 1], H[h + 1], pa.kl, pa.kh, pb, SL, SH);
-            mr[h] = plane_match(L[h], H[h], L[h + 1], H[h + 1], pa.rl, pa.rh, pb, SL, SH);
-        }
-        if (a.k < a.plen || (KH_ABLATE(a) & 1u)) mf[0] = mf[1] = mr[0] = mr[1] = 0;
-
-        // ---- block scan of the per-thread '\n' counts -> cpre per chunk ----
-        KH_LDS_BARRIER();
-        {
-            uint32_t pre = incl - ttot, tot = 0;
-#pragma unroll
-            for (int ww = 0; ww < TPB / 64; ++ww) {
-                pre += ww < wid ? sh.wsum[ww][0] : 0u;
-                tot += sh.wsum[ww][0];
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                sh.cpre[4 * tid + j] = (uint16_t)pre;
-                pre += ccnt[j];
-            }
-            if (tid == 0) {
-                a.tsum[tile].cnt = tot;
-                sh.tcnt = tot;
-            }
-        }
-        KH_LDS_BARRIER();            // cpre visible
-        if (tid == 0) {
-            const int lt = sh.last_chunk;
-            int lp = -1;
-            if (lt >= 0) {
-                int c = 4 * lt + 3;
-                while ((c == NCH_MAIN - 1 ? sh.tcnt : (uint32_t)sh.cpre[c + 1]) == sh.cpre[c]) --c;
-                const int64_t lim = (int64_t)len - g0;
-                lp = last_newline_in_chunk(buf, c, lim < TILE ? (int)lim : TILE);
-            }
-            sh.lastpos = lp;
-            a.tsum[tile].lnl = lp >= 0 ? a.abs_offset + (uint64_t)(g0 + lp + 1) : 0;
-        }
-
-        // ---- candidates -> LDS queue, verification (scan_planes_kernel) ----
-        {
-            const uint32_t mm[4] = {mf[0], mf[1], mr[0], mr[1]};
-            unsigned long long bl[4];
-            uint32_t tot = 0;
-#pragma unroll
-            for (int hs = 0; hs < 4; ++hs) {
-                bl[hs] = __ballot(mm[hs] != 0);
-                tot += (uint32_t)__popcll(bl[hs]);
-            }
-            if (tot) {
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(&sh.qn, tot);
-                base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-#pragma unroll
-                for (int hs = 0; hs < 4; ++hs) {
-                    if (bl[hs]) {
-                        if (mm[hs]) {
-                            const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi(
-                                                            (uint32_t)(bl[hs] >> 32),
-                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bl[hs], 0u));
-                            const uint32_t e0 =
-                                ((64u * (uint32_t)tid + 32u * (uint32_t)(hs & 1)) << 1) | (uint32_t)(hs >> 1);
-                            if (pos < QE) {
-                                qe[pos] = make_uint2(e0, mm[hs]);
-                            } else {
-                                uint32_t m = mm[hs];
-                                while (m) {
-                                    const uint32_t bit = __ffs(m) - 1;
-                                    m &= m - 1;
-                                    verify_emit<WIDE>(a, buf, sh, tile, pw, e0 + (bit << 1));
-                                }
-                            }
-                        }
-                        base += (uint32_t)__popcll(bl[hs]);
-                    }
-                }
-            }
-        }
-        KH_LDS_BARRIER();
-        const uint32_t qn = sh.qn;
-        const uint32_t nq = min(qn, QE);
-        for (uint32_t h = tid; h < nq; h += TPB) {
-            const uint2 en = qe[h];
-            uint32_t m = en.y;
-            while (m) {
-                const uint32_t bit = __ffs(m) - 1;
-                m &= m - 1;
-                verify_emit<WIDE>(a, buf, sh, tile, pw, en.x + (bit << 1));
-            }
-        }
-        // (nq <= 64: wave 0 alone verified, and tid 0 is in it)
-        if (nq > 64 || qn > QE) KH_LDS_BARRIER();
-        if (tid == 0) {
-            a.tsum[tile].nh = sh.nh;
-            a.tsum[tile].nx = sh.nh > (uint32_t)HMAX ? sh.nh : sh.nx;
-            if (sh.nh > (uint32_t)HMAX || (sh.nh && sh.tcnt == 0)) set_info(a.err, INFO_LONGSEG);
-            sh.last_chunk = -1;          // (for the next tile: published by the barrier below)
-            sh.nh = 0;
-            sh.nx = 0;
-            sh.qn = 0;
-        }
-        if (DMA && have_next && !next_dma) tile_fill_regs(a.data, g1, len, bufs + (b ^ 1u) * PBUF);
-        if (DMA) KH_DMA_BARRIER();   // next tile landed; this tile's LDS no longer read
-        else KH_LDS_BARRIER();       // this tile's LDS no longer read
-        if (!have_next) break;
-        tile = nxt;
-        b ^= 1u;
-    }
-}
-
 // Resolve one hit: global line index / line start from the tile scans, the
 // reference's sequence-line rule (lib/kmers.js:151-155), first-occurrence
 // order key (line << (pbits + 1) | strand << pbits | strand ? maxrel - rel : rel).
@@ -1485,6 +1152,10 @@ __device__ __forceinline__ void place_hit(const HitArgs &a, uint64_t slot, bool 
                                           uint64_t key_hi, uint64_t order) {
     // (no rank payload: the finish sorts (key, iota))
     if (!cross) {
+        if (slot >= a.rcap) {                    // only when hits overflowed the lists: redone
+            atomicOr(a.err, ERR_OVF_OVERFLOW);
+            return;
+        }
         if (a.rkey32) a.rkey32[slot] = (uint32_t)key;
         else a.rkey[slot] = key;
         if (a.wide) a.rkeyh[slot] = key_hi;
@@ -2865,34 +2536,7 @@ hipError_t launch_lines(const TileArgs &a, bool lookback, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_scan_planes(const ScanArgs &a, const PlaneArgs &pa, int n_cu, hipStream_t s) {
-    // one workgroup per tile.  KMERHIP_SCAN (A/B experiments): "dma" the
-    // persistent LDS-DMA kernel (PSCAN_WG_PER_CU workgroups per CU; measured
-    // slower: 1.12 vs 0.775 ms at C2); "loop" the persistent
-    // register-staged loop, 8 workgroups per CU
-    static const int mode = [] {
-        const char *e = exp_env("KMERHIP_SCAN");
-        return !e ? 0 : strcmp(e, "dma") == 0 ? 1 : strcmp(e, "loop") == 0 ? 2 : 0;
-    }();
-    if (mode != 0) {
-        const uint64_t per_cu = mode == 1 ? PSCAN_WG_PER_CU : 8;
-        const uint32_t grid = (uint32_t)std::min<uint64_t>(a.n_tiles, (uint64_t)std::max(n_cu, 1) * per_cu);
-        const dim3 g(std::max<uint32_t>(grid, 1));
-#define KH_LAUNCH_P(F5, W)                                                                  \
-    do {                                                                                    \
-        if (mode == 1) hipLaunchKernelGGL((scan_planes_pkernel<F5, W, true>), g, dim3(TPB), 0, s, a, pa); \
-        else hipLaunchKernelGGL((scan_planes_pkernel<F5, W, false>), g, dim3(TPB), 0, s, a, pa);          \
-    } while (0)
-        if (a.k > 32) {
-            if (pa.pb >= 5) KH_LAUNCH_P(true, true);
-            else KH_LAUNCH_P(false, true);
-        } else {
-            if (pa.pb >= 5) KH_LAUNCH_P(true, false);
-            else KH_LAUNCH_P(false, false);
-        }
-#undef KH_LAUNCH_P
-        return hipGetLastError();
-    }
+hipError_t launch_scan_planes(const ScanArgs &a, const PlaneArgs &pa, hipStream_t s) {
     const dim3 g(a.n_tiles);
     if (a.k > 32) {
         if (pa.pb >= 5) hipLaunchKernelGGL((scan_planes_kernel<true, true>), g, dim3(TPB), 0, s, a, pa);

@@ -1,7 +1,6 @@
 #!/bin/bash
-# One GPU call: the GPU test suite, then an A/B of the C2 bench (shipping
-# library vs the experiments build with KMERHIP_SCAN=tile, the per-tile scan
-# kernel), then the two-rank rehearsal.  Stops at the first failing step.
+# One GPU call: the GPU test suite, then the C2 bench twice, then the
+# two-rank rehearsal.  Stops at the first failing step.
 # Output under gpurun_out/chk/.
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -11,12 +10,10 @@ timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
     > gpurun_out/chk/pytest.txt 2>&1 || { tail -30 gpurun_out/chk/pytest.txt; exit 1; }
 tail -2 gpurun_out/chk/pytest.txt
 timeout -k 10 120 $B > gpurun_out/chk/c2_new.json 2> gpurun_out/chk/c2_new.err || { tail gpurun_out/chk/c2_new.err; exit 1; }
-KMERHIP_LIB_EXPERIMENT=kmerjs_amd/libkmerhip_exp.so KMERHIP_SCAN=tile timeout -k 10 120 $B \
-    > gpurun_out/chk/c2_tile.json 2> gpurun_out/chk/c2_tile.err || { tail gpurun_out/chk/c2_tile.err; exit 1; }
 timeout -k 10 120 $B > gpurun_out/chk/c2_new2.json 2> gpurun_out/chk/c2_new2.err || { tail gpurun_out/chk/c2_new2.err; exit 1; }
 python - <<'PY'
 import json
-for n in ("c2_new", "c2_tile", "c2_new2"):
+for n in ("c2_new", "c2_new2"):
     d = json.load(open("gpurun_out/chk/%s.json" % n))
     print(n, "ms/step %.4f scan %.4f frac %.3f distinct %d" % (d["ms_per_step"], d["scan_kernel_ms"], d["roofline"]["frac"], d["distinct_kmers"]))
 PY
