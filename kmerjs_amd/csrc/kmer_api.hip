@@ -147,6 +147,8 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
         if (ok) ok &= hipMemcpy(c->d_PR, pr.data(), pr.size(), hipMemcpyHostToDevice) == hipSuccess;
     }
     ok &= dalloc(&c->d_ticket, 4) == hipSuccess;
+    ok &= dalloc(&c->d_bticket, 1) == hipSuccess;
+    if (ok) ok &= hipMemset(c->d_bticket, 0, sizeof(unsigned int)) == hipSuccess;
     ok &= dalloc(&c->d_scal, 16) == hipSuccess;
     if (ok) {
         ok &= hipMemset(c->d_scal, 0, 128) == hipSuccess;
@@ -208,7 +210,7 @@ kmer_status kmer_close(kmer_ctx *c) {
     for (auto *b : {&c->tbase, &c->nlpos, &c->wcount, &c->wbase, &c->tp_cnt, &c->tp_lnl, &c->rkey, &c->rkey2, &c->rord, &c->rord2, &c->csel, &c->rcnt, &c->xord, &c->xord2,
                     &c->xkey, &c->xkey2, &c->ukey, &c->first, &c->cnt_out, &c->roff})
         b->release();
-    for (auto *b : {&c->ridx, &c->ridx2, &c->opos, &c->xslot, &c->rkey32, &c->rkey32b, &c->bH, &c->bHs}) b->release();
+    for (auto *b : {&c->ridx, &c->ridx2, &c->ecnt, &c->bbase, &c->xslot, &c->rkey32, &c->rkey32b, &c->bH, &c->bHs}) b->release();
     c->pkey16.release();
     c->xsend.release();
     c->xH.release();
@@ -238,12 +240,13 @@ kmer_status kmer_close(kmer_ctx *c) {
     c->tpieces.release();
     c->tH.release();
     c->tnd.release();
+    c->epre.release();
     c->tunits.release();
     c->tbig.release();
     c->tstats.release();
     c->tleft.release();
     c->trecv.release();
-    dfree(c->d_ticket); dfree(c->d_scal); dfree(c->d_pos); dfree(c->d_pos_saved);
+    dfree(c->d_ticket); dfree(c->d_bticket); dfree(c->d_scal); dfree(c->d_pos); dfree(c->d_pos_saved);
     dfree(c->d_P); dfree(c->d_PR);
     if (c->h_small) (void)hipHostFree(c->h_small);
     if (c->h_tail) (void)hipHostFree(c->h_tail);

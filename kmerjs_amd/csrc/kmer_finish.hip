@@ -84,7 +84,8 @@ kmer_status sort_and_heads_wide(kmer_ctx *c, uint64_t n) {
     return KMER_OK;
 }
 
-// bucket partition + per-bucket LDS tables (keys of <= 24 bits)
+// bucket partition + per-bucket LDS tables (keys of <= BKT_LOW + 11 bits):
+// histogram per (bucket, block), offsets (one kernel), scatter, tables
 kmer_status bucket_heads(kmer_ctx *c, uint64_t n) {
     hipStream_t s = c->stream;
     const uint32_t shift = std::min<uint32_t>(c->kbits, BKT_LOW);
@@ -97,10 +98,12 @@ kmer_status bucket_heads(kmer_ctx *c, uint64_t n) {
     HIPCHK(c, c->bHs.ensure((uint64_t)nb * nblk, s));
     HIPCHK(c, c->pkey16.ensure(n, s));
     HIPCHK(c, c->ridx2.ensure(n, s));
+    HIPCHK(c, c->bbase.ensure(2 * BKT_MAX + 2, s));   // bucket totals [0, nb), starts [BKT_MAX, BKT_MAX + nb]
+    uint32_t *btot = c->bbase.p, *bstart = c->bbase.p + BKT_MAX;
     HIPCHK(c, launch_bucket_hist(c->rkey32.p, n, invalid, shift, nb, nblk, c->bH.p, c->hcnt.p, s));
-    ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->bH.p, c->bHs.p, 0u, (size_t)nb * nblk, rocprim::plus<uint32_t>(), s));
-    HIPCHK(c, launch_bucket_scatter(c->rkey32.p, n, invalid, shift, nb, nblk, c->bHs.p, c->pkey16.p, c->ridx2.p, s));
-    HIPCHK(c, launch_bucket_heads(c->pkey16.p, c->ridx2.p, c->bHs.p, c->bH.p, nb, nblk, shift, c->hcnt.p, s));
+    HIPCHK(c, launch_bucket_offsets(c->bH.p, nb, nblk, c->bHs.p, btot, bstart, c->d_bticket, s));
+    HIPCHK(c, launch_bucket_scatter(c->rkey32.p, n, invalid, shift, nb, nblk, c->bHs.p, bstart, c->pkey16.p, c->ridx2.p, s));
+    HIPCHK(c, launch_bucket_heads(c->pkey16.p, c->ridx2.p, bstart, nb, shift, c->hcnt.p, s));
     return KMER_OK;
 }
 
@@ -174,8 +177,9 @@ kmer_status resolve_out(kmer_ctx *c) {
 }
 
 // Rank arrays (rkey / rord / ridx [/ rcnt]) of n hits -> unique keys in
-// first-occurrence order: stable radix sort of (key, rank); group heads flag
-// their rank; a scan of the flags gives each unique key its output position.
+// first-occurrence order: the keys grouped (bucket tables or a radix sort of
+// (key, rank)); group heads flag their rank with the count; the emit kernel
+// gives each flagged rank its output position (heads before it).
 // partial: (code, {first, count}) into ukey/uval; else decoded keys, counts
 // and firsts into keys_out / cnt_out / first.  Returns the unique count.
 // sync = false: the unique count is copied back asynchronously (resolve_out).
@@ -188,7 +192,6 @@ kmer_status rank_finish(kmer_ctx *c, uint64_t n, bool partial, bool with_counts,
     HIPCHK(c, c->ridx2.ensure(n, s));
     if (with_counts) HIPCHK(c, c->hrec.ensure(n, s));
     HIPCHK(c, c->hcnt.ensure(n + 4, s));
-    HIPCHK(c, c->opos.ensure(n, s));
     if (partial) {
         HIPCHK(c, c->ukey.ensure(n, s));
         HIPCHK(c, c->uval.ensure(n, s));
@@ -210,16 +213,25 @@ kmer_status rank_finish(kmer_ctx *c, uint64_t n, bool partial, bool with_counts,
     else
         st = sort_and_heads<uint64_t>(c, c->rkey.p, c->rkey2.p, n, with_counts);
     if (st) return st;
-    auto is_head = rocprim::make_transform_iterator(c->hcnt.p, IsHead());
-    ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, is_head, c->opos.p, 0u, (size_t)n, rocprim::plus<uint32_t>(), s));
+    // heads per emit workgroup; their prefixes (summed in the emit kernel, or
+    // scanned here when there are many workgroups)
+    const uint64_t nbe = emit_blocks(n);
+    HIPCHK(c, c->ecnt.ensure(nbe, s));
+    HIPCHK(c, launch_head_count(c->hcnt.p, n, c->ecnt.p, s));
     EmitArgs e;
     memset(&e, 0, sizeof(e));
+    e.ecnt = c->ecnt.p;
+    if (nbe > EMIT_DIRECT_MAX) {
+        HIPCHK(c, c->epre.ensure(nbe, s));
+        ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->ecnt.p, c->epre.p, (uint64_t)0, (size_t)nbe,
+                                               rocprim::plus<uint64_t>(), s));
+        e.epre = c->epre.p;
+    }
     e.hcnt = c->hcnt.p;
     e.hrec = with_counts ? c->hrec.p : nullptr;
     e.rkey32 = c->narrow ? c->rkey32.p : nullptr;
     e.rkey64 = c->narrow ? nullptr : c->rkey.p;
     e.rkeyh = c->wide ? c->rkeyh.p : nullptr;
-    e.opos = c->opos.p;
     e.rord = c->rord.p;
     e.n = n;
     e.invalid_key = invalid;

@@ -148,7 +148,8 @@ struct kmer_ctx {
     bool narrow = false;
     bool planes = false;           // ACGT prefix: bit-plane scan kernel
     PlaneArgs pargs{};
-    DBuf<uint32_t> ridx, ridx2, opos;
+    DBuf<uint32_t> ridx, ridx2, ecnt, bbase;
+    DBuf<uint64_t> epre;
     DBuf<HeadRec> hrec;
     DBuf<uint32_t> hcnt;           // by rank: != 0 iff first occurrence of its key (bucket finish: count)
     DBuf<uint32_t> bH, bHs;        // bucket finish: per (bucket, block) counts, their scan
@@ -180,6 +181,7 @@ struct kmer_ctx {
     // [5] err (u32) [6] line count [7] chunk ends open
     uint64_t *d_scal = nullptr;
     unsigned int *d_ticket = nullptr, *d_err = nullptr;
+    unsigned int *d_bticket = nullptr;   // bucket_offsets_kernel last-block ticket (returned to 0 by it)
     unsigned long long *d_rec_count = nullptr, *d_line_count = nullptr, *d_ovf_count = nullptr;
     unsigned long long *d_xcount = nullptr, *d_chunk_hits = nullptr, *d_ends_open = nullptr;
     uint64_t *d_nuniq = nullptr;
@@ -343,11 +345,6 @@ struct GroupSrc {
     // the next batch (valid until release()); false at the end of the input
     virtual bool next(const uint8_t **p, uint64_t *n, kmer_status *st, std::string *err) = 0;
     virtual void release(const uint8_t *) {}
-};
-
-// (hcnt != 0) -> 1: the first occurrences, scanned for output positions
-struct IsHead {
-    __host__ __device__ uint32_t operator()(uint32_t c) const { return c ? 1u : 0u; }
 };
 
 // ---- functions shared between the host translation units ----

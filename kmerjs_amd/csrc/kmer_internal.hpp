@@ -227,7 +227,8 @@ struct EmitArgs {
     const uint32_t *rkey32;        // hrec == null: key by rank (narrow keys) ...
     const uint64_t *rkey64;        // ... or (wider keys)
     const uint64_t *rkeyh;         // ... with, for keys of >= 64 bits, their high words
-    const uint32_t *opos;          // exclusive scan of (hcnt != 0): output position
+    const uint32_t *ecnt;          // heads per EMIT_RPB ranks (head_count_kernel)
+    const uint64_t *epre;          // ... their exclusive scan, or null: each workgroup sums the earlier counts
     const uint64_t *rord;          // by rank: order key
     uint64_t n;
     uint64_t invalid_key;
@@ -346,6 +347,9 @@ hipError_t launch_heads_sparse(const uint64_t *skey64, const uint32_t *skey32, c
 hipError_t launch_heads32(const uint32_t *skey, const uint32_t *srank, uint64_t n, uint32_t invalid_key,
                           const uint64_t *rcnt, HeadRec *hrec, uint32_t *hcnt, hipStream_t s);
 hipError_t launch_emit(const EmitArgs &a, hipStream_t s);
+hipError_t launch_head_count(const uint32_t *hcnt, uint64_t n, uint32_t *ecnt, hipStream_t s);
+uint64_t emit_blocks(uint64_t n);
+constexpr uint64_t EMIT_DIRECT_MAX = 8192;   // emit workgroups that sum the earlier counts themselves
 // wide keys (2(k - |P|) >= 64 bits, k <= 64): dst[i] = src[idx[i]]; the cross
 // entries' keys after apply_cross; heads over (hi, lo) sorted ranks (hcnt
 // prefilled with 1, as launch_heads_sparse)
@@ -361,10 +365,13 @@ constexpr uint32_t BKT_MAX = 2048;           // buckets (keys of <= BKT_LOW + 11
 constexpr uint32_t BKT_EPB_HOST = 4096;      // elements per partition block (= BKT_EPB)
 hipError_t launch_bucket_hist(const uint32_t *key, uint64_t n, uint32_t invalid, uint32_t shift, uint32_t nb,
                               uint32_t nblk, uint32_t *H, uint32_t *hcnt, hipStream_t s);
+hipError_t launch_bucket_offsets(const uint32_t *H, uint32_t nb, uint32_t nblk, uint32_t *Hs, uint32_t *btot,
+                                 uint32_t *bbase, unsigned int *ticket, hipStream_t s);
 hipError_t launch_bucket_scatter(const uint32_t *key, uint64_t n, uint32_t invalid, uint32_t shift, uint32_t nb,
-                                 uint32_t nblk, const uint32_t *Hs, uint16_t *pkey, uint32_t *prank, hipStream_t s);
-hipError_t launch_bucket_heads(const uint16_t *pkey, const uint32_t *prank, const uint32_t *Hs, const uint32_t *H,
-                               uint32_t nb, uint32_t nblk, uint32_t shift, uint32_t *hcnt, hipStream_t s);
+                                 uint32_t nblk, const uint32_t *Hs, const uint32_t *bbase, uint16_t *pkey,
+                                 uint32_t *prank, hipStream_t s);
+hipError_t launch_bucket_heads(const uint16_t *pkey, const uint32_t *prank, const uint32_t *bbase, uint32_t nb,
+                               uint32_t shift, uint32_t *hcnt, hipStream_t s);
 // multi-GPU hit exchange (kmer_exchange_prepare / kmer_finish_exchanged)
 struct XHit {
     uint64_t ord;                  // first-occurrence order key

@@ -2109,11 +2109,70 @@ __global__ __launch_bounds__(256) void bucket_hist_kernel(const uint32_t *key, u
     for (uint32_t b = threadIdx.x; b < nb; b += 256) H[(uint64_t)b * nblk + blockIdx.x] = hist[b];
 }
 
+// Offsets of the partition (one launch, no library scan): workgroup b scans
+// bucket b's row of block counts (H[b * nblk + blk] -> Hs, bucket-relative)
+// and publishes the bucket's total; the last workgroup to finish turns the
+// totals into the buckets' starts (bbase[nb] = all keys).  The totals are
+// stored and read at agent scope (sc1: past the XCDs' private L2s), drained
+// before the ticket add that announces them.
+__global__ __launch_bounds__(256) void bucket_offsets_kernel(const uint32_t *H, uint32_t nb, uint32_t nblk,
+                                                             uint32_t *Hs, uint32_t *btot, uint32_t *bbase,
+                                                             unsigned int *ticket) {
+    __shared__ uint32_t ws[4];
+    __shared__ bool last;
+    const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t per = (nblk + 255) / 256, j0 = tid * per, j1 = min(j0 + per, nblk);
+    const uint32_t *row = H + (uint64_t)b * nblk;
+    uint32_t sum = 0;
+    for (uint32_t j = j0; j < j1; ++j) sum += row[j];
+    const uint32_t incl = wave_incl_sum(sum);
+    if (lane == 63) ws[wid] = incl;
+    __syncthreads();
+    uint32_t pre = incl - sum;
+    for (uint32_t w = 0; w < wid; ++w) pre += ws[w];
+    uint32_t *out = Hs + (uint64_t)b * nblk;
+    for (uint32_t j = j0; j < j1; ++j) {
+        const uint32_t v = row[j];
+        out[j] = pre;
+        pre += v;
+    }
+    if (tid == 0) {
+        __hip_atomic_store(btot + b, ws[0] + ws[1] + ws[2] + ws[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last = atomicAdd(ticket, 1u) == nb - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    // bucket starts: nb <= BKT_MAX totals, 8 per thread
+    uint32_t v[BKT_MAX / 256], s = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < BKT_MAX / 256; ++u) {
+        const uint32_t q = tid * (BKT_MAX / 256) + u;
+        v[u] = q < nb ? __hip_atomic_load(btot + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        s += v[u];
+    }
+    const uint32_t inc2 = wave_incl_sum(s);
+    __syncthreads();
+    if (lane == 63) ws[wid] = inc2;
+    __syncthreads();
+    uint32_t p = inc2 - s;
+    for (uint32_t w = 0; w < wid; ++w) p += ws[w];
+#pragma unroll
+    for (uint32_t u = 0; u < BKT_MAX / 256; ++u) {
+        const uint32_t q = tid * (BKT_MAX / 256) + u;
+        if (q < nb) bbase[q] = p;
+        p += v[u];
+    }
+    if (tid == 255) bbase[nb] = p;
+    if (tid == 0) *ticket = 0;
+}
+
 // Scatter with the block's elements first grouped by bucket in LDS, so that
 // each bucket's run goes out as one contiguous (coalesced) piece.
 __global__ __launch_bounds__(256) void bucket_scatter_kernel(const uint32_t *key, uint64_t n, uint32_t invalid,
                                                              uint32_t shift, uint32_t nb, uint32_t nblk,
-                                                             const uint32_t *Hs, uint16_t *pkey, uint32_t *prank) {
+                                                             const uint32_t *Hs, const uint32_t *bbase, uint16_t *pkey,
+                                                             uint32_t *prank) {
     __shared__ uint32_t cnt[BKT_MAX];          // per bucket: count, then local start
     __shared__ uint32_t skey[BKT_EPB];
     __shared__ uint32_t srank[BKT_EPB];
@@ -2142,9 +2201,11 @@ __global__ __launch_bounds__(256) void bucket_scatter_kernel(const uint32_t *key
     __syncthreads();
     uint32_t pre = incl - sum;
     for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) pre += wtot[w];
+    uint32_t lst[BKT_MAX / 256];
 #pragma unroll
     for (uint32_t u = 0; u < BKT_MAX / 256; ++u) {
         const uint32_t b = threadIdx.x * (BKT_MAX / 256) + u;
+        lst[u] = pre;                            // local start of bucket b in skey / srank
         if (b < nb) cnt[b] = pre;
         pre += loc[u];
     }
@@ -2158,19 +2219,25 @@ __global__ __launch_bounds__(256) void bucket_scatter_kernel(const uint32_t *key
             srank[p] = (uint32_t)(base + u * 256 + threadIdx.x);
         }
     }
+    // cnt[b] := global position of local element 0 of bucket b (mod 2^32:
+    // element e of bucket b goes to cnt[b] + e)
+#pragma unroll
+    for (uint32_t u = 0; u < BKT_MAX / 256; ++u) {
+        const uint32_t b = threadIdx.x * (BKT_MAX / 256) + u;
+        if (b < nb && loc[u]) cnt[b] = bbase[b] + Hs[(uint64_t)b * nblk + blockIdx.x] - lst[u];
+    }
     __syncthreads();
     const uint32_t lo_mask = (1u << shift) - 1u;
     for (uint32_t e = threadIdx.x; e < valid; e += 256) {
         const uint32_t k = skey[e], b = k >> shift;
-        const uint32_t pos = Hs[(uint64_t)b * nblk + blockIdx.x] + (e - cnt[b]);
+        const uint32_t pos = cnt[b] + e;
         pkey[pos] = (uint16_t)(k & lo_mask);
         prank[pos] = srank[e];
     }
 }
 
 __global__ __launch_bounds__(1024) void bucket_heads_kernel(const uint16_t *pkey, const uint32_t *prank,
-                                                            const uint32_t *Hs, const uint32_t *H, uint32_t nb,
-                                                            uint32_t nblk, uint32_t shift, uint32_t *hcnt) {
+                                                            const uint32_t *bbase, uint32_t shift, uint32_t *hcnt) {
     __shared__ uint32_t minr[1u << BKT_LOW];
     __shared__ uint32_t cnt[1u << BKT_LOW];
     const uint32_t b = blockIdx.x, nk = 1u << shift;
@@ -2179,9 +2246,7 @@ __global__ __launch_bounds__(1024) void bucket_heads_kernel(const uint16_t *pkey
         cnt[j] = 0;
     }
     __syncthreads();
-    const uint64_t last = (uint64_t)nb * nblk - 1;
-    const uint32_t lo = Hs[(uint64_t)b * nblk];
-    const uint32_t hi = b + 1 < nb ? Hs[(uint64_t)(b + 1) * nblk] : Hs[last] + H[last];
+    const uint32_t lo = bbase[b], hi = bbase[b + 1];
     for (uint32_t e = lo + threadIdx.x; e < hi; e += blockDim.x) {
         const uint32_t j = pkey[e], r = prank[e];
         atomicMin(&minr[j], r);
@@ -2194,40 +2259,89 @@ __global__ __launch_bounds__(1024) void bucket_heads_kernel(const uint16_t *pkey
     }
 }
 
-// One thread per rank; flagged ranks emit output entry opos[rank]: decoded key
-// (P + suffix, 'ACGT' from the 2-bit code, first base most significant),
-// count, first-occurrence order -- or the packed (code, {first, count}) pair
-// for a partial result.
+// Heads (hcnt != 0) per EMIT_RPB ranks: the emit workgroups' prefixes.
+constexpr uint32_t EMIT_RPB = 1024;
+__global__ __launch_bounds__(256) void head_count_kernel(const uint32_t *hcnt, uint64_t n, uint32_t *ecnt) {
+    __shared__ uint32_t ws[4];
+    const uint64_t r0 = (uint64_t)blockIdx.x * EMIT_RPB + 4 * threadIdx.x;
+    uint32_t c = 0;
+    if (r0 + 4 <= n) {
+        const uint4 v = *(const uint4 *)(hcnt + r0);
+        c = (v.x != 0) + (v.y != 0) + (v.z != 0) + (v.w != 0);
+    } else {
+        for (uint64_t r = r0; r < n; ++r) c += hcnt[r] != 0;
+    }
+    c = wave_incl_sum(c);
+    if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) ecnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// Ordered output, EMIT_RPB ranks per workgroup in rounds of 256 (thread t:
+// rank base + 256 i + t).  A flagged rank (its key's first occurrence) emits
+// output entry o = heads before it: the workgroup's prefix (the sum of the
+// earlier workgroups' head counts, or their scan when there are many), then
+// ballot / mbcnt inside the workgroup.  Entry: decoded key (P + suffix,
+// 'ACGT' from the 2-bit code, first base most significant), count,
+// first-occurrence order -- or the packed (code, {first, count}) pair for a
+// partial result.
 __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
-    // decoded keys of this block's heads, staged so that the block's output
-    // range [o0 * k, o_end * k) is written with coalesced dword stores
+    // decoded keys of a round's heads, staged so that the round's output
+    // range [o0 * k, oend * k) is written with coalesced dword stores
     __shared__ __attribute__((aligned(16))) uint8_t kbuf[256 * KMAX_TILE];
-    __shared__ uint32_t s_o0, s_oend;
+    __shared__ uint32_t s_w[EMIT_RPB / 256][4];  // heads per (round, wave)
+    __shared__ uint64_t s_pre;
+    __shared__ uint32_t s_wp[4];
     const uint64_t n = a.n;
     const uint32_t k = a.k, plen = a.plen;
     const bool staged = !a.partial && (k & 3);     // else: aligned direct stores
-    for (uint64_t base = (uint64_t)blockIdx.x * 256; base < n; base += (uint64_t)gridDim.x * 256) {
-        const uint64_t r = base + threadIdx.x;
-        const uint64_t last = (base + 256 < n ? base + 256 : n) - 1;
-        uint32_t hc = 0, o = 0;
-        if (r < n) {
-            hc = a.hcnt[r];
-            o = a.opos[r];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint64_t rb = (uint64_t)blockIdx.x * EMIT_RPB;
+    constexpr int NR = EMIT_RPB / 256;
+    uint32_t hcr[NR];
+    unsigned long long hm[NR];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+        const uint64_t r = rb + 256 * i + tid;
+        hcr[i] = r < n ? a.hcnt[r] : 0u;
+        hm[i] = __ballot(hcr[i] != 0);
+        if (lane == 0) s_w[i][wid] = (uint32_t)__popcll(hm[i]);
+    }
+    if (a.epre) {                                // scanned workgroup prefixes
+        if (tid == 0) s_pre = a.epre[blockIdx.x];
+    } else {                                     // few workgroups: sum the earlier ones' counts
+        uint32_t p = 0;                          // (<= EMIT_DIRECT_MAX workgroups: fits 32 bits)
+        for (uint32_t j = tid; j < blockIdx.x; j += 256) p += a.ecnt[j];
+        p = wave_incl_sum(p);
+        if (lane == 63) s_wp[wid] = p;
+    }
+    __syncthreads();
+    if (!a.epre && tid == 0) s_pre = (uint64_t)s_wp[0] + s_wp[1] + s_wp[2] + s_wp[3];
+    __syncthreads();
+    uint64_t o0 = s_pre;                         // first output entry of the round
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+        const uint64_t r = rb + 256 * i + tid;
+        if (rb + 256 * i >= n) break;            // (uniform)
+        uint32_t before = 0, rt = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            before += w < wid ? s_w[i][w] : 0u;
+            rt += s_w[i][w];
         }
+        const uint32_t hc = hcr[i];
         const uint32_t f = hc ? 1u : 0u;
+        const uint64_t o64 = o0 + before +
+                             __builtin_amdgcn_mbcnt_hi((uint32_t)(hm[i] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm[i], 0u));
+        const uint64_t oend = o0 + rt;
         if (r == n - 1) {
-            *a.nuniq = (uint64_t)o + f;
+            *a.nuniq = o64 + f;
             if (a.nuniq_host) {
-                *a.nuniq_host = (uint64_t)o + f;
+                *a.nuniq_host = o64 + f;
                 __threadfence_system();
             }
         }
-        if (staged) {
-            if (threadIdx.x == 0) s_o0 = o;
-            if (r == last) s_oend = o + f;
-            __syncthreads();
-        }
-        const uint32_t o0 = s_o0, oend = s_oend;
+        const uint64_t o = o64;
         if (f) {
             uint64_t key, cnt, keyh = 0;
             if (a.hrec) {
@@ -2249,7 +2363,7 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
             } else {
                 a.cnt_out[o] = cnt;
                 a.first_out[o] = first;
-                uint8_t *out = staged ? kbuf + (o - o0) * k : a.keys_out + (uint64_t)o * k;
+                uint8_t *out = staged ? kbuf + (o - o0) * k : a.keys_out + o * k;
                 // word w = bases 4w .. 4w + 3, stored as soon as it is formed
                 // (static indices only: no private-memory array)
                 const uint32_t nw = (k + 3) / 4;
@@ -2284,25 +2398,27 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
                 }
             }
         }
-        if (!staged) continue;        // (uniform: no barrier skipped by part of the block)
-        __syncthreads();
-        const uint64_t g0 = (uint64_t)o0 * k, g1 = (uint64_t)oend * k;
-        const uint64_t a0 = (g0 + 3) & ~3ull, a1 = g1 & ~3ull;
-        if (a0 >= a1) {
-            for (uint64_t g = g0 + threadIdx.x; g < g1; g += 256) a.keys_out[g] = kbuf[g - g0];
-        } else {
-            if (threadIdx.x < a0 - g0) a.keys_out[g0 + threadIdx.x] = kbuf[threadIdx.x];
-            if (threadIdx.x < g1 - a1) a.keys_out[a1 + threadIdx.x] = kbuf[a1 - g0 + threadIdx.x];
-            const uint32_t sh = (uint32_t)(a0 - g0);
-            for (uint64_t g = a0 + 4 * threadIdx.x; g < a1; g += 4 * 256) {
-                const uint32_t l = (uint32_t)(g - g0);
-                const uint32_t v = sh == 0 ? *(const uint32_t *)(kbuf + l)
-                                           : (uint32_t)kbuf[l] | ((uint32_t)kbuf[l + 1] << 8) |
-                                                 ((uint32_t)kbuf[l + 2] << 16) | ((uint32_t)kbuf[l + 3] << 24);
-                *(uint32_t *)(a.keys_out + g) = v;
+        if (staged) {                            // (uniform: no barrier skipped by part of the block)
+            __syncthreads();
+            const uint64_t g0 = (uint64_t)o0 * k, g1 = (uint64_t)oend * k;
+            const uint64_t a0 = (g0 + 3) & ~3ull, a1 = g1 & ~3ull;
+            if (a0 >= a1) {
+                for (uint64_t g = g0 + threadIdx.x; g < g1; g += 256) a.keys_out[g] = kbuf[g - g0];
+            } else {
+                if (threadIdx.x < a0 - g0) a.keys_out[g0 + threadIdx.x] = kbuf[threadIdx.x];
+                if (threadIdx.x < g1 - a1) a.keys_out[a1 + threadIdx.x] = kbuf[a1 - g0 + threadIdx.x];
+                const uint32_t sh = (uint32_t)(a0 - g0);
+                for (uint64_t g = a0 + 4 * threadIdx.x; g < a1; g += 4 * 256) {
+                    const uint32_t l = (uint32_t)(g - g0);
+                    const uint32_t v = sh == 0 ? *(const uint32_t *)(kbuf + l)
+                                               : (uint32_t)kbuf[l] | ((uint32_t)kbuf[l + 1] << 8) |
+                                                     ((uint32_t)kbuf[l + 2] << 16) | ((uint32_t)kbuf[l + 3] << 24);
+                    *(uint32_t *)(a.keys_out + g) = v;
+                }
             }
+            __syncthreads();                     // kbuf is reused by the next round
         }
-        __syncthreads();              // kbuf / s_o0 are reused by the next range
+        o0 = oend;
     }
 }
 
@@ -2668,19 +2784,30 @@ hipError_t launch_bucket_hist(const uint32_t *key, uint64_t n, uint32_t invalid,
     hipLaunchKernelGGL(bucket_hist_kernel, dim3(nblk), dim3(256), 0, s, key, n, invalid, shift, nb, nblk, H, hcnt);
     return hipGetLastError();
 }
-hipError_t launch_bucket_scatter(const uint32_t *key, uint64_t n, uint32_t invalid, uint32_t shift, uint32_t nb,
-                                 uint32_t nblk, const uint32_t *Hs, uint16_t *pkey, uint32_t *prank, hipStream_t s) {
-    hipLaunchKernelGGL(bucket_scatter_kernel, dim3(nblk), dim3(256), 0, s, key, n, invalid, shift, nb, nblk, Hs, pkey,
-                       prank);
+hipError_t launch_bucket_offsets(const uint32_t *H, uint32_t nb, uint32_t nblk, uint32_t *Hs, uint32_t *btot,
+                                 uint32_t *bbase, unsigned int *ticket, hipStream_t s) {
+    hipLaunchKernelGGL(bucket_offsets_kernel, dim3(nb), dim3(256), 0, s, H, nb, nblk, Hs, btot, bbase, ticket);
     return hipGetLastError();
 }
-hipError_t launch_bucket_heads(const uint16_t *pkey, const uint32_t *prank, const uint32_t *Hs, const uint32_t *H,
-                               uint32_t nb, uint32_t nblk, uint32_t shift, uint32_t *hcnt, hipStream_t s) {
-    hipLaunchKernelGGL(bucket_heads_kernel, dim3(nb), dim3(1024), 0, s, pkey, prank, Hs, H, nb, nblk, shift, hcnt);
+hipError_t launch_bucket_scatter(const uint32_t *key, uint64_t n, uint32_t invalid, uint32_t shift, uint32_t nb,
+                                 uint32_t nblk, const uint32_t *Hs, const uint32_t *bbase, uint16_t *pkey,
+                                 uint32_t *prank, hipStream_t s) {
+    hipLaunchKernelGGL(bucket_scatter_kernel, dim3(nblk), dim3(256), 0, s, key, n, invalid, shift, nb, nblk, Hs, bbase,
+                       pkey, prank);
+    return hipGetLastError();
+}
+hipError_t launch_bucket_heads(const uint16_t *pkey, const uint32_t *prank, const uint32_t *bbase, uint32_t nb,
+                               uint32_t shift, uint32_t *hcnt, hipStream_t s) {
+    hipLaunchKernelGGL(bucket_heads_kernel, dim3(nb), dim3(1024), 0, s, pkey, prank, bbase, shift, hcnt);
+    return hipGetLastError();
+}
+uint64_t emit_blocks(uint64_t n) { return (n + EMIT_RPB - 1) / EMIT_RPB; }
+hipError_t launch_head_count(const uint32_t *hcnt, uint64_t n, uint32_t *ecnt, hipStream_t s) {
+    if (n) hipLaunchKernelGGL(head_count_kernel, dim3((uint32_t)emit_blocks(n)), dim3(256), 0, s, hcnt, n, ecnt);
     return hipGetLastError();
 }
 hipError_t launch_emit(const EmitArgs &a, hipStream_t s) {
-    if (a.n) hipLaunchKernelGGL(emit_kernel, dim3(grid_for(a.n)), dim3(256), 0, s, a);
+    if (a.n) hipLaunchKernelGGL(emit_kernel, dim3((uint32_t)emit_blocks(a.n)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 hipError_t launch_merge_prep(const uint64_t *keys, const Agg *vals, uint64_t n, uint64_t *rkey, uint32_t *rkey32,
