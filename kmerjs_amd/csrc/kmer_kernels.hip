@@ -63,6 +63,15 @@ __device__ __forceinline__ uint32_t not_nl_bits(uint32_t x) {
     return ((x ^ 0x0A0A0A0Au) + 0x7F7F7F7Fu) & 0x80808080u;
 }
 
+// The same with the xor and the add in one v_xad_u32 (the compiler emits a
+// v_xor / v_add pair for the expression above): 3 VALU per word with the and
+// and the accumulating bcnt, not 4.  k0a / k7f hold 0x0A0A0A0A / 0x7F7F7F7F.
+__device__ __forceinline__ uint32_t not_nl_bits_xad(uint32_t x, uint32_t k0a, uint32_t k7f) {
+    uint32_t r;
+    asm("v_xad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(k0a), "s"(k7f));
+    return r & 0x80808080u;
+}
+
 // per-byte 0x80 flag for bytes equal to '\n'; exact for ASCII bytes (< 0x80)
 __device__ __forceinline__ uint32_t nl_flags(uint32_t x) {
     uint32_t t = x ^ 0x0A0A0A0Au;
@@ -914,13 +923,14 @@ __global__ __launch_bounds__(TPB) void scan_planes_kernel(ScanArgs a, PlaneArgs 
         w[16] = *(const uint32_t *)(buf + FH + 64 * tid + 64);
     }
     const bool tail_tile = (uint64_t)(g0 + TILE) > len;
+    const uint32_t k0a = 0x0A0A0A0Au, k7f = 0x7F7F7F7Fu;
     uint32_t ccnt[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         uint32_t cnt = 0;
         if (!tail_tile) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) cnt += __popc(not_nl_bits(w[4 * j + i]));
+            for (int i = 0; i < 4; ++i) cnt += __popc(not_nl_bits_xad(w[4 * j + i], k0a, k7f));
             cnt = 16u - cnt;
         } else {
             const int64_t gc = g0 + 64 * tid + 16 * j;
@@ -947,7 +957,10 @@ __global__ __launch_bounds__(TPB) void scan_planes_kernel(ScanArgs a, PlaneArgs 
     if (lane == 63) sh.wsum[wid][0] = incl;
 
     // ---- bit-planes of the 68 bytes: gL/gH groups of 8 bases (2 words) ----
-    const uint32_t W0 = 0x08040201u, W1 = 0x80402010u;
+    // y = low nibbles of x0, x1's low nibbles above them (v_bfi): byte i holds
+    // base i's bits 1 / 2 at bits 1 / 2 (x0) and 5 / 6 (x1), so ONE v_dot4
+    // with weights 2^i per plane puts the 8 bases at consecutive bits
+    const uint32_t W0 = 0x08040201u;
     uint32_t L[3], H[3];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -955,8 +968,10 @@ __global__ __launch_bounds__(TPB) void scan_planes_kernel(ScanArgs a, PlaneArgs 
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             const uint32_t x0 = w[8 * h + 2 * p], x1 = w[8 * h + 2 * p + 1];
-            gl[p] = __builtin_amdgcn_udot4(x0 & 0x02020202u, W0, __builtin_amdgcn_udot4(x1 & 0x02020202u, W1, 0u, false), false);
-            gh[p] = __builtin_amdgcn_udot4(x0 & 0x04040404u, W0, __builtin_amdgcn_udot4(x1 & 0x04040404u, W1, 0u, false), false);
+            uint32_t y;                          // (inline: the compiler splits it into two ands and a bitop3)
+            asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(y) : "s"(0x0F0F0F0Fu), "v"(x0), "v"(x1 << 4));
+            gl[p] = __builtin_amdgcn_udot4(y & 0x22222222u, W0, 0u, false);
+            gh[p] = __builtin_amdgcn_udot4(y & 0x44444444u, W0, 0u, false);
         }
         // gl: bits 1..8, gh: bits 2..9 for 8 bases
         L[h] = (gl[0] >> 1) | (gl[1] << 7) | (gl[2] << 15) | (gl[3] << 23);
