@@ -349,7 +349,7 @@ hipError_t launch_heads32(const uint32_t *skey, const uint32_t *srank, uint64_t 
 hipError_t launch_emit(const EmitArgs &a, hipStream_t s);
 hipError_t launch_head_count(const uint32_t *hcnt, uint64_t n, uint32_t *ecnt, hipStream_t s);
 uint64_t emit_blocks(uint64_t n);
-constexpr uint64_t EMIT_DIRECT_MAX = 8192;   // emit workgroups that sum the earlier counts themselves
+constexpr uint64_t EMIT_DIRECT_MAX = 4096;   // emit workgroups that sum the earlier counts themselves (O(n^2) reads)
 // wide keys (2(k - |P|) >= 64 bits, k <= 64): dst[i] = src[idx[i]]; the cross
 // entries' keys after apply_cross; heads over (hi, lo) sorted ranks (hcnt
 // prefilled with 1, as launch_heads_sparse)

@@ -2128,8 +2128,8 @@ __global__ __launch_bounds__(256) void bucket_hist_kernel(const uint32_t *key, u
 // bucket b's row of block counts (H[b * nblk + blk] -> Hs, bucket-relative)
 // and publishes the bucket's total; the last workgroup to finish turns the
 // totals into the buckets' starts (bbase[nb] = all keys).  The totals are
-// stored and read at agent scope (sc1: past the XCDs' private L2s), drained
-// before the ticket add that announces them.
+// stored write-through (sc1), drained before the ticket add that announces
+// them, and read back by atomics.
 __global__ __launch_bounds__(256) void bucket_offsets_kernel(const uint32_t *H, uint32_t nb, uint32_t nblk,
                                                              uint32_t *Hs, uint32_t *btot, uint32_t *bbase,
                                                              unsigned int *ticket) {
@@ -2163,7 +2163,9 @@ __global__ __launch_bounds__(256) void bucket_offsets_kernel(const uint32_t *H, 
 #pragma unroll
     for (uint32_t u = 0; u < BKT_MAX / 256; ++u) {
         const uint32_t q = tid * (BKT_MAX / 256) + u;
-        v[u] = q < nb ? __hip_atomic_load(btot + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        // (read by an atomic, at the memory side: an agent-scope load may be
+        // served by this XCD's L2, which can hold the line from an earlier call)
+        v[u] = q < nb ? __hip_atomic_fetch_add(btot + q, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
         s += v[u];
     }
     const uint32_t inc2 = wave_incl_sum(s);
