@@ -82,6 +82,10 @@ struct DBuf {
         T *q = nullptr;
         hipError_t e = hipMalloc((void **)&q, nc * sizeof(T));
         if (e != hipSuccess) return e;
+        if (exp_env("KMERHIP_POISON")) {           // (experiments build: every new buffer starts as 0xA5 bytes)
+            e = hipMemsetAsync(q, 0xA5, nc * sizeof(T), s);
+            if (e != hipSuccess) return e;
+        }
         if (p) {
             if (keep && used) {
                 e = hipMemcpyAsync(q, p, used * sizeof(T), hipMemcpyDeviceToDevice, s);
@@ -218,6 +222,8 @@ struct kmer_ctx {
     DBuf<uint32_t> tH, tnd;        // pass-1 / pass-2 histograms; distinct entries per bucket
     DBuf<uint64_t> tHs, tstart;    // their scans; bucket starts (TAB_NQ + 1)
     DBuf<uint64_t> tp1;            // pass-1 partition starts of the last chunk (TAB_NB)
+    DBuf<uint64_t> tspill;         // pass-1 keys past their fixed run (tab_scatter1f)
+    DBuf<unsigned long long> tspc; // [0] spill count, [1, 1 + TAB_NB) its histogram, then TAB_NB cursors
     DBuf<TabUnit> tunits;          // pass-2 units, then TAB_NB partition heads
     DBuf<TabBig> tbig;             // entries with counts >= TAB_CMAX
     DBuf<uint32_t> tpc;            // pieces per sequence line (long lines)

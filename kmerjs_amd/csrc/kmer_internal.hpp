@@ -460,7 +460,19 @@ struct TabArgs {
     unsigned long long *rec_count;
     uint64_t rec_cap;
     unsigned int *err;
+    // pass 1 without the counting pass (tab_scatter1f): workgroup w's run of
+    // partition p starts at base + p * R + pcw[w] and holds pcw[w + 1] - pcw[w]
+    // keys; keys past it go to spill[0 .. spill_cap) (count: *spill_n)
+    const uint64_t *pcw;
+    uint64_t R;
+    uint64_t *spill;
+    unsigned long long *spill_n;
+    uint64_t spill_cap;
 };
+
+// Pass-1 filler of a run's unused tail (tab_scatter1f), skipped by pass 2:
+// tab_mix(2^64 - 1), whose code is no k-mer of k <= 31 (codes < 2^62).
+constexpr uint64_t TAB_SENT = 0ull - TAB_MUL;
 
 struct TabUnit {                   // pass 2: a run of one pass-1 partition's keys
     uint64_t start;                // first key in B1
@@ -509,8 +521,16 @@ hipError_t launch_tab_p1_offsets(const uint64_t *H1s, uint32_t nwg, uint64_t *ou
 hipError_t launch_tab_hist2(const uint64_t *B1, const TabUnit *units, uint32_t n_units, uint32_t *H2, hipStream_t s);
 hipError_t launch_tab_scatter2(const uint64_t *B1, const TabUnit *units, uint32_t n_units, const uint64_t *H2s,
                                uint64_t *B2, hipStream_t s);
-hipError_t launch_tab_starts(const uint64_t *H2s, const TabUnit *pfirst, uint64_t total, uint64_t *start,
-                             hipStream_t s);
+hipError_t launch_tab_starts(const uint64_t *H2s, const uint32_t *H2, uint64_t nh, const TabUnit *pfirst,
+                             uint64_t *start, hipStream_t s);
+hipError_t launch_tab_scatter1f(const TabArgs &a, hipStream_t s);
+hipError_t launch_tab_wg_windows(const SeqLine *lines, uint64_t n, uint64_t lpw, uint32_t k, uint32_t nwg,
+                                 uint64_t *W, hipStream_t s);
+// pass-1 spill (tab_scatter1f): keys by partition (hist: TAB_NB counters), then
+// placed at cur[partition]++ (cur: absolute B1 offsets)
+hipError_t launch_tab_spill_hist(const uint64_t *keys, uint64_t n, unsigned long long *hist, hipStream_t s);
+hipError_t launch_tab_spill_place(const uint64_t *keys, uint64_t n, unsigned long long *cur, uint64_t *B1,
+                                  hipStream_t s);
 hipError_t launch_tab_final(const TabFinal &a, uint32_t grid, hipStream_t s);
 hipError_t launch_tab_sort_final(const TabFinal &a, uint32_t grid, hipStream_t s);
 constexpr uint32_t TAB_SWG = 512;                      // sort-final workgroup (8 waves, two per CU)

@@ -16,6 +16,145 @@ float ev_ms(kmer_ctx *c, hipEvent_t a, hipEvent_t b) {
     return ms;
 }
 
+// The pass-1 scatter of a chunk (records of non-ACGT windows: the attempt is
+// redone with a larger record list until it fits), then its records drained.
+kmer_status table_scatter1(kmer_ctx *c, TabArgs &a, hipStream_t s, hipError_t (*launch)(const TabArgs &, hipStream_t)) {
+    for (int attempt = 0;; ++attempt) {
+        a.recs = c->recs.p;
+        a.rec_count = c->d_rec_count;
+        a.rec_cap = c->recs.cap;
+        HIPCHK(c, hipMemsetAsync(c->d_rec_count, 0, 8, s));
+        if (attempt && a.spill_n) HIPCHK(c, hipMemsetAsync(a.spill_n, 0, 8, s));
+        HIPCHK(c, hipEventRecord(c->tev[2], s));
+        HIPCHK(c, launch(a, s));
+        HIPCHK(c, hipEventRecord(c->tev[3], s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        const float ms_s1 = ev_ms(c, c->tev[2], c->tev[3]);
+        const uint32_t e = (uint32_t)c->h_small[5];
+        kmer_status st = check_err(c, e);
+        if (st) return st;
+        if (!(e & ERR_REC_OVERFLOW)) {         // (a redo rewrites the same key ranges)
+            c->t_ms[2] += ms_s1;
+            break;
+        }
+        if (attempt == 7) return fail(c, KMER_E_OOM, "record list kept overflowing");
+        HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
+        st = ensure_records(c, c->h_small[0] + 1024);
+        if (st) return st;
+    }
+    return KMER_OK;
+}
+
+kmer_status table_pass1_counted(kmer_ctx *c, TabArgs &a, hipStream_t s) {
+    const uint64_t nh = (uint64_t)TAB_NB * a.nwg;
+    a.H1 = c->tH.p;
+    HIPCHK(c, launch_tab_hist1(a, s));
+    ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tH.p, c->tHs.p, (uint64_t)0, (size_t)nh,
+                                           rocprim::plus<uint64_t>(), s));
+    HIPCHK(c, launch_tab_p1_offsets(c->tHs.p, a.nwg, c->tp1.p, s));
+    std::vector<uint64_t> off(TAB_NB + 1);
+    HIPCHK(c, hipMemcpyAsync(off.data(), c->tp1.p, TAB_NB * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(c->h_small + 14, c->tHs.p + nh - 1, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(c->h_small + 15, c->tH.p + nh - 1, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipEventRecord(c->tev[2], s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    c->t_ms[0] += ev_ms(c, c->tev[0], c->tev[1]);
+    c->t_ms[1] += ev_ms(c, c->tev[1], c->tev[2]);
+    const uint64_t n_c = c->h_small[14] + (uint32_t)c->h_small[15];
+    off[TAB_NB] = n_c;
+    HIPCHK(c, c->tb1.ensure(c->t_keys + n_c, s, true, c->t_keys));
+    a.H1s = c->tHs.p;
+    a.base = c->t_keys;
+    a.B1 = c->tb1.p;
+    kmer_status st = table_scatter1(c, a, s, launch_tab_scatter1);
+    if (st) return st;
+    c->t_cbase.push_back(c->t_keys);
+    c->t_coff.push_back(std::move(off));
+    c->t_keys += n_c;
+    return KMER_OK;
+}
+
+// Pass 1 with fixed runs (tab_scatter1f): workgroup w's run in partition p
+// holds its mean share of keys + 2 standard deviations + 4, rounded up to 8 (a hash partition's
+// count is ~Poisson; at C3 ~5 % of the slots are filler, ~2 % of the runs
+// spill a few keys), sized from the workgroups' window counts.  *done false:
+// the spill list overflowed (crowded partitions: repeated k-mers), nothing of
+// the chunk is kept and the caller runs the counted pass.
+kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done) {
+    *done = false;
+    uint64_t *W = c->tHs.p, *pcw = c->tHs.p + a.nwg;
+    HIPCHK(c, launch_tab_wg_windows(a.lines, a.n_lines, a.lpw, a.k, a.nwg, W, s));
+    std::vector<uint64_t> hw(a.nwg), hp(a.nwg + 1);
+    HIPCHK(c, hipMemcpyAsync(hw.data(), W, a.nwg * 8ull, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipEventRecord(c->tev[2], s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    const float ms0 = ev_ms(c, c->tev[0], c->tev[1]), ms1 = ev_ms(c, c->tev[1], c->tev[2]);
+    uint64_t tot = 0;
+    hp[0] = 0;
+    double sig = 2.0;                          // (KMERHIP_TAB_SIGMA: A/B experiments)
+    if (const char *e = exp_env("KMERHIP_TAB_SIGMA")) sig = atof(e);
+    for (uint32_t w = 0; w < a.nwg; ++w) {
+        const double mu = (double)hw[w] / TAB_NB;
+        hp[w + 1] = hp[w] + (hw[w] ? ((uint64_t)(mu + sig * std::sqrt(mu)) + 4 + 7) & ~7ull : 0);
+        tot += hw[w];
+    }
+    const uint64_t R = hp[a.nwg];
+    const uint64_t spill_cap = std::max<uint64_t>(1u << 20, tot / 256);
+    const uint64_t region = (uint64_t)TAB_NB * R;
+    const uint64_t cb = (c->t_keys + 7) & ~7ull;  // (runs of multiples of 8 keys start at 64-B boundaries)
+    HIPCHK(c, c->tb1.ensure(cb + region + spill_cap, s, true, c->t_keys));
+    HIPCHK(c, c->tspill.ensure(spill_cap, s));
+    HIPCHK(c, c->tspc.ensure(1 + 2 * TAB_NB, s));
+    HIPCHK(c, hipMemcpyAsync(pcw, hp.data(), hp.size() * 8, hipMemcpyHostToDevice, s));
+    a.pcw = pcw;
+    a.R = R;
+    a.base = cb;
+    a.B1 = c->tb1.p;
+    a.spill = c->tspill.p;
+    a.spill_n = c->tspc.p;
+    a.spill_cap = spill_cap;
+    HIPCHK(c, hipMemsetAsync(c->tspc.p, 0, (1 + TAB_NB) * 8, s));
+    kmer_status st = table_scatter1(c, a, s, launch_tab_scatter1f);
+    if (st) return st;
+    unsigned long long ns = 0;
+    HIPCHK(c, hipMemcpyAsync(&ns, c->tspc.p, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    if (ns > spill_cap) {                      // (records of the attempt are dropped: the counted pass redoes them)
+        if (exp_env("KMERHIP_TAB_SPILL_LOG")) fprintf(stderr, "tab pass 1: spill list overflow (%llu)\n", ns);
+        return KMER_OK;
+    }
+    std::vector<uint64_t> off(TAB_NB + 1);
+    for (uint32_t p = 0; p <= TAB_NB; ++p) off[p] = (uint64_t)p * R;
+    c->t_cbase.push_back(cb);
+    c->t_coff.push_back(std::move(off));
+    c->t_keys = cb + region;
+    if (ns) {                                  // the spill list: one more chunk, partition-major
+        std::vector<unsigned long long> hh(TAB_NB), cur(TAB_NB);
+        std::vector<uint64_t> so(TAB_NB + 1);
+        HIPCHK(c, launch_tab_spill_hist(c->tspill.p, ns, c->tspc.p + 1, s));
+        HIPCHK(c, hipMemcpyAsync(hh.data(), c->tspc.p + 1, TAB_NB * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        so[0] = 0;
+        for (uint32_t p = 0; p < TAB_NB; ++p) {
+            cur[p] = c->t_keys + so[p];
+            so[p + 1] = so[p] + hh[p];
+        }
+        HIPCHK(c, hipMemcpyAsync(c->tspc.p + 1 + TAB_NB, cur.data(), TAB_NB * 8, hipMemcpyHostToDevice, s));
+        HIPCHK(c, launch_tab_spill_place(c->tspill.p, ns, c->tspc.p + 1 + TAB_NB, c->tb1.p, s));
+        c->t_cbase.push_back(c->t_keys);
+        c->t_coff.push_back(std::move(so));
+        c->t_keys += ns;
+    }
+    if (exp_env("KMERHIP_TAB_SPILL_LOG"))
+        fprintf(stderr, "tab pass 1: %llu keys, %llu slots, %llu spilled\n", (unsigned long long)tot,
+                (unsigned long long)region, ns);
+    c->t_ms[0] += ms0;
+    c->t_ms[1] += ms1;
+    *done = true;
+    return KMER_OK;
+}
+
 kmer_status table_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s) {
     const uint64_t li0 = c->host_lines;
     HIPCHK(c, hipEventRecord(c->ev0, s));
@@ -78,46 +217,17 @@ kmer_status table_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_t
         HIPCHK(c, c->tH.ensure(nh, s));
         HIPCHK(c, c->tHs.ensure(nh, s));
         HIPCHK(c, c->tp1.ensure(TAB_NB, s));
-        a.H1 = c->tH.p;
-        HIPCHK(c, launch_tab_hist1(a, s));
-        ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tH.p, c->tHs.p, (uint64_t)0, (size_t)nh,
-                                               rocprim::plus<uint64_t>(), s));
-        HIPCHK(c, launch_tab_p1_offsets(c->tHs.p, a.nwg, c->tp1.p, s));
-        std::vector<uint64_t> off(TAB_NB + 1);
-        HIPCHK(c, hipMemcpyAsync(off.data(), c->tp1.p, TAB_NB * 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipMemcpyAsync(c->h_small + 14, c->tHs.p + nh - 1, 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipMemcpyAsync(c->h_small + 15, c->tH.p + nh - 1, 4, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipEventRecord(c->tev[2], s));
-        HIPCHK(c, hipStreamSynchronize(s));
-        c->t_ms[0] += ev_ms(c, c->tev[0], c->tev[1]);
-        c->t_ms[1] += ev_ms(c, c->tev[1], c->tev[2]);
-        const uint64_t n_c = c->h_small[14] + (uint32_t)c->h_small[15];
-        off[TAB_NB] = n_c;
-        HIPCHK(c, c->tb1.ensure(c->t_keys + n_c, s, true, c->t_keys));
-        a.H1s = c->tHs.p;
-        a.base = c->t_keys;
-        a.B1 = c->tb1.p;
-        for (int attempt = 0;; ++attempt) {
-            a.recs = c->recs.p;
-            a.rec_count = c->d_rec_count;
-            a.rec_cap = c->recs.cap;
-            HIPCHK(c, hipMemsetAsync(c->d_rec_count, 0, 8, s));
-            HIPCHK(c, hipEventRecord(c->tev[2], s));
-            HIPCHK(c, launch_tab_scatter1(a, s));
-            HIPCHK(c, hipEventRecord(c->tev[3], s));
-            HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
-            HIPCHK(c, hipStreamSynchronize(s));
-            const float ms_s1 = ev_ms(c, c->tev[2], c->tev[3]);
-            const uint32_t e = (uint32_t)c->h_small[5];
-            st = check_err(c, e);
+        // no prefix and k <= 31: pass 1 without the counting pass (fixed runs,
+        // tab_scatter1f); an overfull spill list falls back to the counted pass
+        // (KMERHIP_TAB_P1=count: always counted, A/B experiments)
+        const char *p1 = exp_env("KMERHIP_TAB_P1");
+        bool done = false;
+        if (a.pmask == 0 && a.k <= 31 && !(p1 && strcmp(p1, "count") == 0)) {
+            st = table_pass1_fixed(c, a, s, &done);
             if (st) return st;
-            if (!(e & ERR_REC_OVERFLOW)) {         // (a redo rewrites the same key ranges)
-                c->t_ms[2] += ms_s1;
-                break;
-            }
-            if (attempt == 7) return fail(c, KMER_E_OOM, "record list kept overflowing");
-            HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
-            st = ensure_records(c, c->h_small[0] + 1024);
+        }
+        if (!done) {
+            st = table_pass1_counted(c, a, s);
             if (st) return st;
         }
         const uint64_t nrec = c->h_small[0];
@@ -125,9 +235,6 @@ kmer_status table_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_t
             st = drain_records(c, d, nrec, s);
             if (st) return st;
         }
-        c->t_cbase.push_back(c->t_keys);
-        c->t_coff.push_back(std::move(off));
-        c->t_keys += n_c;
     }
     HIPCHK(c, hipEventRecord(c->ev1, s));
     HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
@@ -205,7 +312,7 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
     HIPCHK(c, hipEventRecord(c->tev[5], s));
     HIPCHK(c, launch_tab_scatter2(B1, c->tunits.p, (uint32_t)n_units, c->tHs.p, c->tb2.p, s));
     HIPCHK(c, hipEventRecord(c->tev[6], s));
-    HIPCHK(c, launch_tab_starts(c->tHs.p, c->tunits.p + n_units, n, c->tstart.p, s));
+    HIPCHK(c, launch_tab_starts(c->tHs.p, c->tH.p, nh, c->tunits.p + n_units, c->tstart.p, s));
     HIPCHK(c, hipMemsetAsync(c->tstats.p, 0, 4 * sizeof(unsigned long long), s));
     TabFinal f;
     memset(&f, 0, sizeof(f));

@@ -350,6 +350,123 @@ __global__ __launch_bounds__(TAB_WGH) void tab_scatter1h_kernel(TabArgs a) {
     }
 }
 
+// pass 1 without the counting pass (no prefix, k <= 31: every window of a
+// line is a key, so a workgroup's share of keys is known from its lines):
+// partition p's keys of workgroup w go to a run of fixed capacity at base +
+// p * R + pcw[w] (1.08x the workgroup's uniform share + 16: ~3.5 standard
+// deviations of a hash partition's count), in the same LDS-sorted rounds as
+// tab_scatter1h; the run's unused tail is filled with TAB_SENT, which pass 2
+// skips.  A key past its run's capacity goes to the spill list (one atomic per
+// wave and write-out step), which the host places partition-major after the
+// runs as one more chunk (tab_spill_*; an overfull list: the chunk is redone
+// with the counting pass).  Saves tab_hist1's second formation of every
+// window.
+template <bool PFX>
+__global__ __launch_bounds__(TAB_WGH) void tab_scatter1f_kernel(TabArgs a) {
+    __shared__ uint64_t srt[TAB_RPL * TAB_WGH];
+    __shared__ uint32_t fill[TAB_NB];
+    __shared__ uint32_t bcnt[TAB_NB];
+    __shared__ uint16_t bst[TAB_NB];                 // (round starts < 8 K)
+    uint32_t *const ws = (uint32_t *)srt;            // (scan scratch: srt is free between rounds)
+    const uint32_t t = threadIdx.x, b0 = 2 * t, b1 = 2 * t + 1;
+    const uint64_t r0 = a.base + a.pcw[blockIdx.x];
+    const uint32_t cap = (uint32_t)(a.pcw[blockIdx.x + 1] - a.pcw[blockIdx.x]);
+    const uint64_t R = a.R;
+    fill[b0] = 0;
+    fill[b1] = 0;
+    bcnt[b0] = 0;
+    bcnt[b1] = 0;
+    __syncthreads();
+    TabCur c = tab_cursor(a, TAB_WGH / 64);
+    while (true) {
+        uint64_t key[TAB_RPL];
+        uint32_t rank[TAB_RPL];
+        uint32_t v = 0;
+        if (c.m < c.end) v = tab_round<TAB_RPL, 0, PFX>(a, c, true, key);
+#pragma unroll
+        for (int j = 0; j < TAB_RPL; ++j)
+            rank[j] = (v & (1u << j)) ? atomicAdd(&bcnt[key[j] >> (64 - TAB_L1)], 1u) : 0u;
+        __syncthreads();
+        uint32_t total;
+        const uint32_t c0 = bcnt[b0], c1 = bcnt[b1];
+        const uint32_t st0 = block_excl_512(c0 + c1, ws, &total), st1 = st0 + c0;
+        bst[b0] = (uint16_t)st0;
+        bst[b1] = (uint16_t)st1;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < TAB_RPL; ++j)
+            if (v & (1u << j)) srt[bst[key[j] >> (64 - TAB_L1)] + rank[j]] = key[j];
+        __syncthreads();
+        for (uint32_t i = t; i < total; i += TAB_WGH) {
+            const uint64_t h = srt[i];
+            const uint32_t p = (uint32_t)(h >> (64 - TAB_L1));
+            const uint32_t j = fill[p] + (i - bst[p]);
+            const bool sp = j >= cap;
+            if (!sp) a.B1[r0 + p * R + j] = h;
+            const uint64_t m = __ballot(sp);
+            if (m) {
+                const uint32_t lane = t & 63, lead = (uint32_t)__ffsll((unsigned long long)m) - 1;
+                unsigned long long o = 0;
+                if (lane == lead) o = atomicAdd(a.spill_n, (unsigned long long)__popcll(m));
+                o = (unsigned long long)(uint32_t)__shfl((int)(uint32_t)o, (int)lead) |
+                    ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(o >> 32), (int)lead) << 32);
+                o += (unsigned long long)__popcll(m & ((1ull << lane) - 1));
+                if (sp && o < a.spill_cap) a.spill[o] = h;
+            }
+        }
+        __syncthreads();
+        fill[b0] += c0;
+        fill[b1] += c1;
+        bcnt[b0] = 0;
+        bcnt[b1] = 0;
+        if (!__syncthreads_or(c.m < c.end)) break;
+    }
+    // the runs' unused tails (a wave per partition)
+    for (uint32_t p = t >> 6; p < TAB_NB; p += TAB_WGH / 64) {
+        const uint32_t f = min(fill[p], cap);
+        for (uint32_t j = f + (t & 63); j < cap; j += 64) a.B1[r0 + p * R + j] = TAB_SENT;
+    }
+}
+
+// the spill list of tab_scatter1f, partition-major (order within a partition
+// is free: table mode has none)
+__global__ __launch_bounds__(256) void tab_spill_hist_kernel(const uint64_t *keys, uint64_t n,
+                                                             unsigned long long *hist) {
+    __shared__ uint32_t h[TAB_NB];
+    for (uint32_t i = threadIdx.x; i < TAB_NB; i += 256) h[i] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+        atomicAdd(&h[keys[i] >> (64 - TAB_L1)], 1u);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < TAB_NB; i += 256)
+        if (h[i]) atomicAdd(&hist[i], (unsigned long long)h[i]);
+}
+
+__global__ __launch_bounds__(256) void tab_spill_place_kernel(const uint64_t *keys, uint64_t n,
+                                                              unsigned long long *cur, uint64_t *B1) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint64_t h = keys[i];
+        B1[atomicAdd(&cur[h >> (64 - TAB_L1)], 1ull)] = h;
+    }
+}
+
+// keys (windows) of each pass-1 workgroup's share of lines: the fixed runs of
+// tab_scatter1f are sized from them
+__global__ __launch_bounds__(256) void tab_wg_windows_kernel(const SeqLine *lines, uint64_t n, uint64_t lpw,
+                                                             uint32_t k, uint64_t *W) {
+    __shared__ uint64_t ws[4];
+    const uint64_t m0 = (uint64_t)blockIdx.x * lpw, m1 = m0 + lpw < n ? m0 + lpw : n;
+    uint64_t x = 0;
+    for (uint64_t m = m0 + threadIdx.x; m < m1; m += 256) {
+        const uint64_t len = lines[m].len;
+        x += len >= k ? len - k + 1 : 0;
+    }
+    for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) W[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
 // pass 1, scatter: the same keys, LDS-sorted by partition in rounds of 16 K,
 // written as one contiguous run per partition and round
 template <bool PFX>
@@ -450,8 +567,9 @@ __global__ __launch_bounds__(256) void tab_hist2_kernel(const uint64_t *B1, cons
     uint32_t len = un.len;
     // 16-B loads, 4 in flight per thread (the unit's first key alone when it
     // is not 16-B aligned, and its last when an odd count remains)
+    // (TAB_SENT: an unused pass-1 slot, not a key)
     if (((uintptr_t)src & 8u) && len) {
-        if (threadIdx.x == 0) atomicAdd(&hist[(uint32_t)(src[0] >> TAB_RBITS) & (TAB_NB - 1)], 1u);
+        if (threadIdx.x == 0 && src[0] != TAB_SENT) atomicAdd(&hist[(uint32_t)(src[0] >> TAB_RBITS) & (TAB_NB - 1)], 1u);
         ++src;
         --len;
     }
@@ -464,16 +582,17 @@ __global__ __launch_bounds__(256) void tab_hist2_kernel(const uint64_t *B1, cons
         for (int u = 0; u < 4; ++u) x[u] = s2[i + u * 256];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            atomicAdd(&hist[(uint32_t)(x[u].x >> TAB_RBITS) & (TAB_NB - 1)], 1u);
-            atomicAdd(&hist[(uint32_t)(x[u].y >> TAB_RBITS) & (TAB_NB - 1)], 1u);
+            if (x[u].x != TAB_SENT) atomicAdd(&hist[(uint32_t)(x[u].x >> TAB_RBITS) & (TAB_NB - 1)], 1u);
+            if (x[u].y != TAB_SENT) atomicAdd(&hist[(uint32_t)(x[u].y >> TAB_RBITS) & (TAB_NB - 1)], 1u);
         }
     }
     for (; i < np; i += 256) {
         const ulonglong2 x = s2[i];
-        atomicAdd(&hist[(uint32_t)(x.x >> TAB_RBITS) & (TAB_NB - 1)], 1u);
-        atomicAdd(&hist[(uint32_t)(x.y >> TAB_RBITS) & (TAB_NB - 1)], 1u);
+        if (x.x != TAB_SENT) atomicAdd(&hist[(uint32_t)(x.x >> TAB_RBITS) & (TAB_NB - 1)], 1u);
+        if (x.y != TAB_SENT) atomicAdd(&hist[(uint32_t)(x.y >> TAB_RBITS) & (TAB_NB - 1)], 1u);
     }
-    if ((len & 1u) && threadIdx.x == 0) atomicAdd(&hist[(uint32_t)(src[len - 1] >> TAB_RBITS) & (TAB_NB - 1)], 1u);
+    if ((len & 1u) && threadIdx.x == 0 && src[len - 1] != TAB_SENT)
+        atomicAdd(&hist[(uint32_t)(src[len - 1] >> TAB_RBITS) & (TAB_NB - 1)], 1u);
     __syncthreads();
     for (uint32_t b = threadIdx.x; b < TAB_NB; b += 256) H2[un.hbase + (uint64_t)b * un.nunits + un.u] = hist[b];
 }
@@ -508,7 +627,8 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2_kernel(const uint64_t *B
 #pragma unroll
         for (int j = 0; j < TAB_RPL; ++j) {
             const uint32_t i = r0 + j * TAB_WG1 + t;
-            rank[j] = i < un.len ? atomicAdd(&bcnt[(uint32_t)(key[j] >> TAB_RBITS) & (TAB_NB - 1)], 1u) : 0u;
+            rank[j] = i < un.len && key[j] != TAB_SENT
+                          ? atomicAdd(&bcnt[(uint32_t)(key[j] >> TAB_RBITS) & (TAB_NB - 1)], 1u) : 0u;
         }
         __syncthreads();
         uint32_t total;
@@ -520,7 +640,7 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2_kernel(const uint64_t *B
 #pragma unroll
         for (int j = 0; j < TAB_RPL; ++j) {
             const uint32_t i = r0 + j * TAB_WG1 + t;
-            if (i < un.len) srt[bst[(uint32_t)(key[j] >> TAB_RBITS) & (TAB_NB - 1)] + rank[j]] = key[j];
+            if (i < un.len && key[j] != TAB_SENT) srt[bst[(uint32_t)(key[j] >> TAB_RBITS) & (TAB_NB - 1)] + rank[j]] = key[j];
         }
         __syncthreads();
 #pragma unroll
@@ -585,7 +705,8 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2c_kernel(const uint64_t *
 #pragma unroll
         for (int j = 0; j < TS2_RPL; ++j) {
             const uint32_t i = r0 + j * TAB_WG1 + t;
-            rank[j] = i < un.len ? atomicAdd(&bcnt[(uint32_t)(key[j] >> TAB_RBITS) & (TAB_NB - 1)], 1u) : 0u;
+            rank[j] = i < un.len && key[j] != TAB_SENT
+                          ? atomicAdd(&bcnt[(uint32_t)(key[j] >> TAB_RBITS) & (TAB_NB - 1)], 1u) : 0u;
         }
         __syncthreads();
         const uint32_t n_new = bcnt[t], tot = n_new + cc;
@@ -601,7 +722,7 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2c_kernel(const uint64_t *
 #pragma unroll
         for (int j = 0; j < TS2_RPL; ++j) {
             const uint32_t i = r0 + j * TAB_WG1 + t;
-            if (i < un.len) srt[bst[(uint32_t)(key[j] >> TAB_RBITS) & (TAB_NB - 1)] + rank[j]] = key[j];
+            if (i < un.len && key[j] != TAB_SENT) srt[bst[(uint32_t)(key[j] >> TAB_RBITS) & (TAB_NB - 1)] + rank[j]] = key[j];
         }
 #pragma unroll
         for (int i = 0; i < TS2_CARRY; ++i)
@@ -631,14 +752,15 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2c_kernel(const uint64_t *
 }
 
 // bucket q = (p, b) starts at the scanned H2 entry of (p, b, unit 0)
-__global__ __launch_bounds__(256) void tab_starts_kernel(const uint64_t *H2s, const TabUnit *pfirst, uint64_t total,
-                                                         uint64_t *start) {
+// (the end: the keys counted by pass 2 -- B1 may hold TAB_SENT slots)
+__global__ __launch_bounds__(256) void tab_starts_kernel(const uint64_t *H2s, const uint32_t *H2, uint64_t nh,
+                                                         const TabUnit *pfirst, uint64_t *start) {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q < TAB_NQ) {
         const TabUnit u = pfirst[q >> TAB_L2];
         start[q] = H2s[u.hbase + (uint64_t)(q & (TAB_NB - 1)) * u.nunits];
     }
-    if (q == 0) start[TAB_NQ] = total;
+    if (q == 0) start[TAB_NQ] = nh ? H2s[nh - 1] + H2[nh - 1] : 0;
 }
 
 namespace {
@@ -1490,9 +1612,36 @@ hipError_t launch_tab_scatter2(const uint64_t *B1, const TabUnit *units, uint32_
     return hipGetLastError();
 }
 
-hipError_t launch_tab_starts(const uint64_t *H2s, const TabUnit *pfirst, uint64_t total, uint64_t *start,
-                             hipStream_t s) {
-    hipLaunchKernelGGL(tab_starts_kernel, dim3(TAB_NQ / 256), dim3(256), 0, s, H2s, pfirst, total, start);
+hipError_t launch_tab_starts(const uint64_t *H2s, const uint32_t *H2, uint64_t nh, const TabUnit *pfirst,
+                             uint64_t *start, hipStream_t s) {
+    hipLaunchKernelGGL(tab_starts_kernel, dim3(TAB_NQ / 256), dim3(256), 0, s, H2s, H2, nh, pfirst, start);
+    return hipGetLastError();
+}
+
+hipError_t launch_tab_scatter1f(const TabArgs &a, hipStream_t s) {
+    if (a.pmask == 0)
+        hipLaunchKernelGGL(tab_scatter1f_kernel<false>, dim3(a.nwg), dim3(TAB_WGH), 0, s, a);
+    else
+        hipLaunchKernelGGL(tab_scatter1f_kernel<true>, dim3(a.nwg), dim3(TAB_WGH), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_tab_spill_hist(const uint64_t *keys, uint64_t n, unsigned long long *hist, hipStream_t s) {
+    const uint32_t g = (uint32_t)std::min<uint64_t>(1024, (n + 255) / 256);
+    hipLaunchKernelGGL(tab_spill_hist_kernel, dim3(std::max(g, 1u)), dim3(256), 0, s, keys, n, hist);
+    return hipGetLastError();
+}
+
+hipError_t launch_tab_spill_place(const uint64_t *keys, uint64_t n, unsigned long long *cur, uint64_t *B1,
+                                  hipStream_t s) {
+    const uint32_t g = (uint32_t)std::min<uint64_t>(4096, (n + 255) / 256);
+    hipLaunchKernelGGL(tab_spill_place_kernel, dim3(std::max(g, 1u)), dim3(256), 0, s, keys, n, cur, B1);
+    return hipGetLastError();
+}
+
+hipError_t launch_tab_wg_windows(const SeqLine *lines, uint64_t n, uint64_t lpw, uint32_t k, uint32_t nwg,
+                                 uint64_t *W, hipStream_t s) {
+    hipLaunchKernelGGL(tab_wg_windows_kernel, dim3(nwg), dim3(256), 0, s, lines, n, lpw, k, W);
     return hipGetLastError();
 }
 

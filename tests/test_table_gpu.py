@@ -185,6 +185,37 @@ def test_table_big_counts(native):
     assert dict(want).get(b"A" * 15) == 9000 * 136
 
 
+@pytest.mark.parametrize("k", [16, 31])
+def test_table_fixed_runs_spill(native, k):
+    # no prefix: pass 1 writes fixed per-workgroup runs (tab_scatter1f); a
+    # poly-A read every 8th record crowds one partition far past its runs, so
+    # ~390 K keys take the spill list (placed as one more chunk), and a second
+    # feed of poly-A alone overflows the list (> 2^20 keys: the chunk is redone
+    # with the counting pass) -- every route must give the oracle's Map
+    from oracle import oracle
+    from tests.util import packed_sorted, result_packed_sorted, same_packed
+    arr = np.frombuffer(bytearray(oracle.synth_fastq(21, 0, 24000)), dtype=np.uint8).reshape(-1, 317).copy()
+    arr[::8, 13:163] = ord("A")
+    mixed = arr.tobytes()
+    polya = b"".join(b"@p%010d\n%s\n+\n%s\n" % (i, b"A" * 150, b"I" * 150) for i in range(9000))
+    data = mixed + polya
+    want = packed_sorted(*oracle.count_arrays(data, b"", k))
+    ctr = native.Counter(k=k, prefix=b"", flags=native.FLAG_UNORDERED)
+    got = result_packed_sorted(ctr.count_buffer(mixed), k)
+    assert same_packed(got, packed_sorted(*oracle.count_arrays(mixed, b"", k)))
+    import torch
+    dev = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    ctr.reset()
+    ctr.feed_device(dev.data_ptr(), len(mixed))
+    ctr.feed_device(dev.data_ptr() + len(mixed), len(polya))
+    torch.cuda.synchronize()
+    got = result_packed_sorted(ctr.finish(), k)
+    canon, keys, total = ctr.table_stats()
+    ctr.close()
+    assert same_packed(got, want)
+    assert total == int(want[1].sum()) + sum(want[2].values())
+
+
 def test_table_matches_ordered_path_at_scale(native):
     # 2 M reads, k = 31, no prefix (C3's configuration): the table's Map keys
     # and counts equal the ordered dense path's result (960 windows per 2 reads)
