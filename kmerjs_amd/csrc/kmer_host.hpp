@@ -79,8 +79,16 @@ struct DBuf {
         if (n <= cap) return hipSuccess;
         uint64_t nc = std::max<uint64_t>(n, cap + cap / 2);
         nc = std::max<uint64_t>(nc, 1024);
+        hipError_t e;
+        if (p && !(keep && used)) {               // nothing to keep: the old block goes first (peak = the new size)
+            e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return e;
+            (void)hipFree(p);
+            p = nullptr;
+            cap = 0;
+        }
         T *q = nullptr;
-        hipError_t e = hipMalloc((void **)&q, nc * sizeof(T));
+        e = hipMalloc((void **)&q, nc * sizeof(T));
         if (e != hipSuccess) return e;
         if (exp_env("KMERHIP_POISON")) {           // (experiments build: every new buffer starts as 0xA5 bytes)
             e = hipMemsetAsync(q, 0xA5, nc * sizeof(T), s);

@@ -142,6 +142,7 @@ kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done
         }
         HIPCHK(c, hipMemcpyAsync(c->tspc.p + 1 + TAB_NB, cur.data(), TAB_NB * 8, hipMemcpyHostToDevice, s));
         HIPCHK(c, launch_tab_spill_place(c->tspill.p, ns, c->tspc.p + 1 + TAB_NB, c->tb1.p, s));
+        HIPCHK(c, hipStreamSynchronize(s));      // (cur is a host temporary: the copy may read it until here)
         c->t_cbase.push_back(c->t_keys);
         c->t_coff.push_back(std::move(so));
         c->t_keys += ns;
