@@ -88,7 +88,10 @@ enum {
      * CANONICAL, any k / step / prefix; records longer than 2^23 bytes through
      * the long-line retry).  kmer_result_lines = input lines.  Device feeds
      * must cut chunks before a header line (offset 0, or a '>' after '\n'). */
-    KMER_FLAG_FASTA = 1u << 16
+    KMER_FLAG_FASTA = 1u << 16,
+    /* debug: table pass 1 always with fixed per-workgroup runs (by default
+     * only when their filler slots are <= 1/12 of the keys: large inputs) */
+    KMER_FLAG_TABLE_FIXED_TEST = 1u << 17
 };
 
 typedef struct {

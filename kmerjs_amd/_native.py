@@ -21,6 +21,7 @@ FLAG_TABLE_SPLIT_TEST = 32
 FLAG_CANONICAL = 64
 FLAG_LONG_LINES = 128
 FLAG_FASTA = 1 << 16      # FASTA records (an extension; kmer_api.h)
+FLAG_TABLE_FIXED_TEST = 1 << 17   # debug: table pass 1 always with fixed runs
 TAB_PARTS = 1024    # table mode: pass-1 partitions (ownership unit across ranks)
 WRITE_JSON = 0      # JSON.stringify(mapToJSON(map)), lib/kmers.js:46-54
 WRITE_LEGACY = 1    # "{\nkey: count,...}\n", lib/index.js:381-388

@@ -54,7 +54,7 @@
 using namespace kmerhip;
 
 // every KMER_FLAG_* of include/kmer_api.h
-constexpr uint32_t KMER_FLAGS_PUBLIC = 0xFFu | KMER_FLAG_FASTA;
+constexpr uint32_t KMER_FLAGS_PUBLIC = 0xFFu | KMER_FLAG_FASTA | KMER_FLAG_TABLE_FIXED_TEST;
 
 namespace kmerhip {
 

@@ -79,8 +79,9 @@ kmer_status table_pass1_counted(kmer_ctx *c, TabArgs &a, hipStream_t s) {
 // holds its mean share of keys + 2 standard deviations + 4, rounded up to 8 (a hash partition's
 // count is ~Poisson; at C3 ~5 % of the slots are filler, ~2 % of the runs
 // spill a few keys), sized from the workgroups' window counts.  *done false:
-// the spill list overflowed (crowded partitions: repeated k-mers), nothing of
-// the chunk is kept and the caller runs the counted pass.
+// the runs would be more than 1/12 filler (small shares), or the spill list
+// overflowed (crowded partitions: repeated k-mers); nothing of the chunk is
+// kept and the caller runs the counted pass.
 kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done) {
     *done = false;
     uint64_t *W = c->tHs.p, *pcw = c->tHs.p + a.nwg;
@@ -102,6 +103,9 @@ kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done
     const uint64_t R = hp[a.nwg];
     const uint64_t spill_cap = std::max<uint64_t>(1u << 20, tot / 256);
     const uint64_t region = (uint64_t)TAB_NB * R;
+    // small shares (C5's 1 GB of contigs: ~256 keys per run, 16 % filler) move
+    // more filler through pass 2 than the counting pass costs: counted instead
+    if (region > tot + tot / 12 && !(c->p.flags & KMER_FLAG_TABLE_FIXED_TEST)) return KMER_OK;
     const uint64_t cb = (c->t_keys + 7) & ~7ull;  // (runs of multiples of 8 keys start at 64-B boundaries)
     HIPCHK(c, c->tb1.ensure(cb + region + spill_cap, s, true, c->t_keys));
     HIPCHK(c, c->tspill.ensure(spill_cap, s));

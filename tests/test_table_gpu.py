@@ -200,7 +200,8 @@ def test_table_fixed_runs_spill(native, k):
     polya = b"".join(b"@p%010d\n%s\n+\n%s\n" % (i, b"A" * 150, b"I" * 150) for i in range(9000))
     data = mixed + polya
     want = packed_sorted(*oracle.count_arrays(data, b"", k))
-    ctr = native.Counter(k=k, prefix=b"", flags=native.FLAG_UNORDERED)
+    # (small shares: the fixed runs are forced, FLAG_TABLE_FIXED_TEST)
+    ctr = native.Counter(k=k, prefix=b"", flags=native.FLAG_UNORDERED | native.FLAG_TABLE_FIXED_TEST)
     got = result_packed_sorted(ctr.count_buffer(mixed), k)
     assert same_packed(got, packed_sorted(*oracle.count_arrays(mixed, b"", k)))
     import torch
