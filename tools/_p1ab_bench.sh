@@ -2,7 +2,7 @@
 # (KMERHIP_TAB_SIGMA) vs the counted pass (KMERHIP_TAB_P1=count)
 set -o pipefail
 mkdir -p gpurun_out/p1ab && export TMPDIR=/tmp
-for v in count:2 fixed:2 fixed:3 fixed:4; do
+for v in fixed:1.5 fixed:2 fixed:2.5; do
   p=${v%%:*}; sg=${v#*:}; n=${p}_$sg
   KMERHIP_LIB_EXPERIMENT=kmerjs_amd/libkmerhip_exp.so KMERHIP_TAB_SPILL_LOG=1 KMERHIP_TAB_P1=$p KMERHIP_TAB_SIGMA=$sg \
     timeout -k 10 300 python3 bench.py --config c3 --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline > gpurun_out/p1ab/$n.json 2> gpurun_out/p1ab/$n.err || { tail gpurun_out/p1ab/$n.err; exit 1; }
