@@ -134,8 +134,11 @@ def count_windows(lines_bytes_lengths, first_line, k):
     return tot
 
 
-def make_contigs(seed, target_bytes, k):
-    """C5: single-line FASTA '>c%08d\n' + contig of 10 kb - 1 Mb, seed 5."""
+def make_contigs(seed, target_bytes, k, width=0):
+    """C5 (SURVEY.md §8d): FASTA '>c%08d\n' + contig of 10 kb - 1 Mb, seed 5;
+    single-line (width 0: the reference reads it as FASTQ, line index % 4 == 1
+    counts) or wrapped at `width` columns (KMER_FLAG_FASTA input, .fsa style).
+    Returns (bytes, line lengths) -- for width > 0 the contig lengths instead."""
     import numpy as np
     rng = np.random.default_rng(seed)
     parts, lens, n, i = [], [], 0, 0
@@ -143,10 +146,19 @@ def make_contigs(seed, target_bytes, k):
     while n < target_bytes:
         L = int(rng.integers(10_000, 1_000_001))
         head = b">c%08d\n" % i
-        seq = acgt[rng.integers(0, 4, L)].tobytes()
-        parts += [head, seq, b"\n"]
-        lens += [len(head) - 1, L]
-        n += len(head) + L + 1
+        seq = acgt[rng.integers(0, 4, L)]
+        if width:
+            full = L // width
+            body = np.full(full * (width + 1), ord("\n"), np.uint8).reshape(full, width + 1)
+            body[:, :width] = seq[:full * width].reshape(full, width)
+            tail = seq[full * width:].tobytes()
+            parts += [head, body.tobytes(), tail + (b"\n" if tail else b"")]
+            lens.append(L)
+            n += len(head) + body.size + len(tail) + (1 if tail else 0)
+        else:
+            parts += [head, seq.tobytes(), b"\n"]
+            lens += [len(head) - 1, L]
+            n += len(head) + L + 1
         i += 1
     return b"".join(parts), lens
 
@@ -168,6 +180,30 @@ def make_workload(args, rank, world, dev):
                 "total_lines": world * args.reads * 4, "windows": per, "windows_total": world * per,
                 "desc": "%s: %d synthetic 150bp reads per GPU, k=%d, prefix '%s'"
                         % (args.config.upper(), args.reads, args.k, args.prefix)}
+    if args.config == "c5" and args.fasta:
+        # .fsa-style multi-line contigs (60 columns), every record counted
+        # (KMER_FLAG_FASTA; parity unpinned by the reference, which has no FASTA
+        # parser: test/kmerFinderServer.js:158)
+        data, lens = make_contigs(5 + rank, args.contig_bytes, args.k, width=60)
+        n_lines = data.count(b"\n")
+        info = torch.tensor([len(data), n_lines], dtype=torch.int64, device=dev)
+        if world > 1:
+            allv = [torch.zeros_like(info) for _ in range(world)]
+            dist.all_gather(allv, info)
+            sizes = [(int(x[0]), int(x[1])) for x in allv]
+        else:
+            sizes = [(len(data), n_lines)]
+        per = sum(2 * (L - args.k + 1) for L in lens if L >= args.k and L > 1)
+        tot = torch.tensor([per], dtype=torch.int64, device=dev)
+        if world > 1:
+            dist.all_reduce(tot)
+        buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev)
+        return {"buf": buf, "nbytes": len(data), "lines_before": sum(n for _, n in sizes[:rank]),
+                "byte_offset": sum(b for b, _ in sizes[:rank]), "total_lines": sum(n for _, n in sizes),
+                "windows": per, "windows_total": int(tot.item()), "records": len(lens),
+                "desc": "C5 FASTA: contigs 10 kb-1 Mb in 60-column lines (seed 5+rank), %.2f GB per GPU, "
+                        "every record counted (KMER_FLAG_FASTA), k=%d, prefix '%s'" % (len(data) / 1e9, args.k,
+                                                                                    args.prefix)}
     if args.config == "c5":
         data, lens = make_contigs(5 + rank, args.contig_bytes, args.k)
         info = torch.tensor([len(data), len(lens)], dtype=torch.int64, device=dev)
@@ -324,6 +360,9 @@ def main():
                          "(table mode); c4 125 M reads per GPU (1 B on 8), k=16; c5 long contigs k=21")
     ap.add_argument("--contig-bytes", type=int, default=1_000_000_000, help="c5: bytes of contigs per GPU")
     ap.add_argument("--ordered", action="store_true", help="c5: the reference's ordered Map instead of canonical")
+    ap.add_argument("--fasta", action="store_true",
+                    help="c5: .fsa-style contigs in 60-column lines, counted by record (KMER_FLAG_FASTA, an "
+                         "extension: parity unpinned by the reference, which has no FASTA parser)")
     ap.add_argument("--collect", action="store_true",
                     help="N > 1: the timed step also gathers every rank's ordered key range to rank 0 and merges "
                          "them on the device into ONE result in Map order (kmer_merge_ordered)")
@@ -370,6 +409,9 @@ def main():
             args.prefix = ""
         if "--ordered" not in argv:
             args.flags |= FLAG_CANONICAL
+        if args.fasta:
+            from kmerjs_amd._native import FLAG_FASTA
+            args.flags |= FLAG_FASTA
     if args.config != "c2":
         args.no_pcie = True
     if args.merge is None:
@@ -623,13 +665,15 @@ def main():
             # twice that, the canonical sum once
             n_keys = (accepted if args.flags & _FC else accepted // 2) if not args.prefix else None
             pbytes = table_phase_bytes(nbytes, n_keys or 0, canonical)
+            pbytes["fasta"] = 2 * nbytes      # (the rewrite: the chunk read once, about its size written)
             kern_name = max(phases, key=lambda x: phases[x])
             kern_ms = phases[kern_name]
             algo_bytes = pbytes[kern_name]
             kern_name = {"lines": "nl_slots_kernel + seq_lines_slots_kernel",
                          "hist1": "tab_hist1_kernel (+ scan)", "scatter1": "tab_scatter1h_kernel",
                          "hist2": "tab_hist2_kernel (+ scan)", "scatter2": "tab_scatter2c_kernel",
-                         "final": "tab_sort_final_kernel (+ tab_final_kernel on its leftover units)"}[kern_name]
+                         "final": "tab_sort_final_kernel (+ tab_final_kernel on its leftover units)",
+                         "fasta": "fa_tiles_kernel + fa_write_kernel (FASTA rewrite)"}[kern_name]
         elif args.k > 64 or (not args.prefix and args.k > 31):
             # general path (k > 64): line arrays + one thread per window, every
             # hit a record merged on the host -- the feed kernels together
@@ -672,7 +716,8 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": {"c1": "test_data/test_short.fastq (reference fixture)",
-                     "c5": "synthetic contigs (numpy PCG64, seed 5 + rank)"}.get(
+                     "c5": "synthetic contigs (numpy PCG64, seed 5 + rank)%s" % (
+                         ", 60-column FASTA records" if args.fasta else "")}.get(
                          args.config, "synthetic (on-device splitmix64 FASTQ, 317 B records, seed %d)" % args.seed),
             "config": {"workload": wl["desc"], "name": args.config,
                        "reads_per_gpu": args.reads if args.config in ("c2", "c3", "c4") else None,

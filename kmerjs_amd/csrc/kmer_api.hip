@@ -53,8 +53,35 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
             }
             g->group.push_back(c);
         }
+        // peer access between every pair of distinct devices, so the group's
+        // partial / key copies (hipMemcpyPeerAsync, kmer_group.hip) go device to
+        // device over xGMI.  A pair the platform refuses (no P2P path) keeps
+        // working: the runtime stages such peer copies through host memory;
+        // g->peer_staged counts those pairs (KMERHIP_PEER_LOG prints them).
+        for (kmer_ctx *a : g->group)
+            for (kmer_ctx *b : g->group) {
+                if (a->device == b->device) continue;
+                int can = 0;
+                if (hipDeviceCanAccessPeer(&can, a->device, b->device) != hipSuccess) can = 0;
+                hipError_t e = hipErrorPeerAccessUnsupported;
+                if (can && hipSetDevice(a->device) == hipSuccess) {
+                    e = hipDeviceEnablePeerAccess(b->device, 0);
+                    if (e == hipErrorPeerAccessAlreadyEnabled) {
+                        (void)hipGetLastError();   // (enabled by an earlier group: fine)
+                        e = hipSuccess;
+                    }
+                }
+                if (e != hipSuccess) {
+                    (void)hipGetLastError();
+                    ++g->peer_staged;
+                    if (getenv("KMERHIP_PEER_LOG"))
+                        fprintf(stderr, "kmerhip: no peer access %d -> %d (%s): peer copies staged by the runtime\n",
+                                a->device, b->device, hipGetErrorString(e));
+                }
+            }
         g->device = g->group[0]->device;
         g->mode = g->group[0]->mode;
+        (void)hipSetDevice(g->device);
         *out = g;
         return KMER_OK;
     }
@@ -170,6 +197,7 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
     ok &= c->h_tail && hipHostGetDevicePointer((void **)&c->d_tail, c->h_tail, 0) == hipSuccess;
     if (c->h_tail) memset(c->h_tail, 0, 16 * sizeof(uint64_t));
     for (hipEvent_t &e : c->tev) ok &= hipEventCreate(&e) == hipSuccess;
+    for (hipEvent_t &e : c->fa_ev) ok &= hipEventCreate(&e) == hipSuccess;
     ok &= hipEventCreate(&c->ev0) == hipSuccess && hipEventCreate(&c->ev1) == hipSuccess &&
           hipEventCreate(&c->ev2) == hipSuccess && hipEventCreate(&c->ev3) == hipSuccess &&
           hipEventCreate(&c->ev4) == hipSuccess &&
@@ -208,7 +236,7 @@ kmer_status kmer_close(kmer_ctx *c) {
     c->fa_out[0].release();
     c->fa_out[1].release();
     for (auto *b : {&c->tbase, &c->nlpos, &c->wcount, &c->wbase, &c->tp_cnt, &c->tp_lnl, &c->rkey, &c->rkey2, &c->rord, &c->rord2, &c->csel, &c->rcnt, &c->xord, &c->xord2,
-                    &c->xkey, &c->xkey2, &c->ukey, &c->first, &c->cnt_out, &c->roff})
+                    &c->xkey, &c->xkey2, &c->ukey, &c->first, &c->cnt_out})
         b->release();
     for (auto *b : {&c->ridx, &c->ridx2, &c->ecnt, &c->bbase, &c->xslot, &c->rkey32, &c->rkey32b, &c->bH, &c->bHs}) b->release();
     c->pkey16.release();
@@ -251,9 +279,13 @@ kmer_status kmer_close(kmer_ctx *c) {
     dfree(c->d_P); dfree(c->d_PR);
     if (c->h_small) (void)hipHostFree(c->h_small);
     if (c->h_tail) (void)hipHostFree(c->h_tail);
+    for (hipStream_t us : c->up_streams) (void)hipStreamSynchronize(us);
+    if (c->up_p) (void)hipHostFree(c->up_p);
     for (hipEvent_t e : {c->ev0, c->ev1, c->ev2, c->ev3, c->ev4, c->evw})
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->tev)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->fa_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->sstream) (void)hipStreamSynchronize(c->sstream);
     if (c->evq) (void)hipEventDestroy(c->evq);
@@ -528,9 +560,10 @@ kmer_status kmer_table_exchange_prepare(kmer_ctx *c, uint32_t world, const void 
     if (segs.size() >= (1ull << 31)) return fail(c, KMER_E_BAD_PARAM, "too many table segments");
     HIPCHK(c, c->tsend.ensure(n, s));
     HIPCHK(c, c->tseg.ensure(segs.size(), s));
-    HIPCHK(c, hipMemcpyAsync(c->tseg.p, segs.data(), segs.size() * sizeof(TabSeg), hipMemcpyHostToDevice, s));
+    kmer_status st = upload(c, c->tseg.p, segs.data(), segs.size() * sizeof(TabSeg), s);
+    if (st) return st;
     HIPCHK(c, launch_tab_segcopy(c->tb1.p, c->tseg.p, (uint32_t)segs.size(), c->tsend.p, s));
-    HIPCHK(c, hipStreamSynchronize(s));        // (segs is a host temporary; the caller's collective follows)
+    HIPCHK(c, hipStreamSynchronize(s));        // (the caller's collective follows)
     *d_send = c->tsend.p;
     return KMER_OK;
 }
@@ -744,11 +777,11 @@ kmer_status kmer_table_digest(kmer_ctx *c, uint64_t *digest) {
 kmer_status kmer_phase_times(kmer_ctx *c, uint32_t max, const char **names, double *ms, uint32_t *n) {
     if (!c || !n || (max && (!names || !ms))) return KMER_E_BAD_PARAM;
     SETTLE(c);
-    static const char *tab_names[6] = {"lines", "hist1", "scatter1", "hist2", "scatter2", "final"};
+    static const char *tab_names[7] = {"lines", "hist1", "scatter1", "hist2", "scatter2", "final", "fasta"};
     static const char *ord_names[3] = {"scan", "feed", "finish"};
     if (c->mode == MODE_TABLE) {
-        *n = 6;
-        for (uint32_t i = 0; i < 6 && i < max; ++i) {
+        *n = c->fasta ? 7 : 6;                   // (fasta: the FASTA rewrite of the chunks)
+        for (uint32_t i = 0; i < *n && i < max; ++i) {
             names[i] = tab_names[i];
             ms[i] = c->t_ms[i];
         }

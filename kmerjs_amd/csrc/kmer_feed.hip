@@ -34,6 +34,32 @@ kmer_status ensure_ovf(kmer_ctx *c, uint64_t n, hipStream_t s) {
     return KMER_OK;
 }
 
+// Host -> device upload through the context's pinned arena (kmer_host.hpp):
+// the caller's buffer may go out of scope as soon as this returns.
+kmer_status upload(kmer_ctx *c, void *dst, const void *src, size_t n, hipStream_t s) {
+    if (n == 0) return KMER_OK;
+    const size_t need = (n + 255) & ~(size_t)255;
+    if (c->up_used + need > c->up_cap || c->up_streams.size() >= 8) {
+        for (hipStream_t us : c->up_streams) HIPCHK(c, hipStreamSynchronize(us));
+        c->up_streams.clear();
+        c->up_used = 0;
+        if (need > c->up_cap) {
+            if (c->up_p) HIPCHK(c, hipHostFree(c->up_p));
+            c->up_p = nullptr;
+            c->up_cap = 0;
+            const size_t cap = std::max<size_t>(need, 4u << 20);
+            HIPCHK(c, hipHostMalloc((void **)&c->up_p, cap, hipHostMallocDefault));
+            c->up_cap = cap;
+        }
+    }
+    uint8_t *h = c->up_p + c->up_used;
+    memcpy(h, src, n);
+    c->up_used += need;
+    if (std::find(c->up_streams.begin(), c->up_streams.end(), s) == c->up_streams.end()) c->up_streams.push_back(s);
+    HIPCHK(c, hipMemcpyAsync(dst, h, n, hipMemcpyHostToDevice, s));
+    return KMER_OK;
+}
+
 kmer_status ensure_records(kmer_ctx *c, uint64_t n) {
     HIPCHK(c, c->recs.ensure(n, c->stream));
     HIPCHK(c, c->rec_keys.ensure(c->recs.cap * (uint64_t)c->p.k, c->stream));
@@ -48,11 +74,7 @@ kmer_status drain_records(kmer_ctx *c, const uint8_t *d_data, uint64_t n, hipStr
     const uint64_t k = c->p.k;
     kmer_status st = ensure_records(c, n);
     if (st) return st;
-    HIPCHK(c, c->roff.ensure(n, s));
-    std::vector<uint64_t> off(n);
-    for (uint64_t i = 0; i < n; ++i) off[i] = i * k;
-    HIPCHK(c, hipMemcpyAsync(c->roff.p, off.data(), n * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(c, launch_gather_records(c->recs.p, c->roff.p, n, d_data, c->rec_keys.p, s));
+    HIPCHK(c, launch_gather_records(c->recs.p, k, n, d_data, c->rec_keys.p, s));
     std::vector<Record> recs(n);
     std::vector<char> keys(n * k);
     HIPCHK(c, hipMemcpyAsync(recs.data(), c->recs.p, n * sizeof(Record), hipMemcpyDeviceToHost, s));
@@ -402,10 +424,10 @@ kmer_status two_pass_prefix(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_
     HIPCHK(c, hipMemcpyAsync(&lastb, d + len - 1, 1, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     pos.ends_open = lastb != '\n';
-    HIPCHK(c, hipMemcpyAsync(c->tp_cnt.p, cnt.data(), n_tiles * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(c, hipMemcpyAsync(c->tp_lnl.p, last.data(), n_tiles * 8, hipMemcpyHostToDevice, s));
-    HIPCHK(c, hipMemcpyAsync(c->d_pos, &pos, sizeof(pos), hipMemcpyHostToDevice, s));
-    HIPCHK(c, hipStreamSynchronize(s));
+    kmer_status st = upload(c, c->tp_cnt.p, cnt.data(), n_tiles * 8, s);
+    if (!st) st = upload(c, c->tp_lnl.p, last.data(), n_tiles * 8, s);
+    if (!st) st = upload(c, c->d_pos, &pos, sizeof(pos), s);
+    if (st) return st;
     return KMER_OK;
 }
 
@@ -699,6 +721,7 @@ kmer_status fasta_rewrite(kmer_ctx *c, const uint8_t *d, uint64_t len, hipStream
     HIPCHK(c, c->fa_t.ensure(n_tiles + 1ull, s));
     HIPCHK(c, c->fa_x.ensure(n_tiles + 1ull, s));
     HIPCHK(c, hipMemsetAsync(c->fa_t.p + n_tiles, 0, sizeof(FaTile), s));   // (the identity: the scan's total lands there)
+    HIPCHK(c, hipEventRecord(c->fa_ev[0], s));
     HIPCHK(c, launch_fa_tiles(d, len, n_tiles, c->fa_t.p, s));
     FaTile id;
     memset(&id, 0, sizeof(id));
@@ -712,6 +735,11 @@ kmer_status fasta_rewrite(kmer_ctx *c, const uint8_t *d, uint64_t len, hipStream
     DBuf<uint8_t> &ob = c->fa_out[c->fa_flip];
     HIPCHK(c, ob.ensure(tot.c0 + 16, s));
     HIPCHK(c, launch_fa_write(d, len, n_tiles, c->fa_x.p, ob.p, s));
+    HIPCHK(c, hipEventRecord(c->fa_ev[1], s));
+    if (c->mode == MODE_TABLE) {             // (table_feed synchronises the stream before its own timing)
+        HIPCHK(c, hipEventSynchronize(c->fa_ev[1]));
+        c->t_ms[6] += ev_ms(c, c->fa_ev[0], c->fa_ev[1]);
+    }
     c->fa_lines += tot.nl + (last != '\n' ? 1 : 0);
     *od = ob.p;
     *olen = tot.c0;
@@ -760,6 +788,7 @@ kmer_status reset(kmer_ctx *c) {
     c->timing_pending = false;
     c->n_out = 0;
     c->t_keys = 0;
+    c->t_fill = 0;
     c->t_cbase.clear();
     c->t_coff.clear();
     c->t_done = false;

@@ -178,7 +178,7 @@ struct kmer_ctx {
     DBuf<uint64_t> xkeyl, xkeyh;               // ... wide keys (xkey then holds the entry's index)
     DBuf<uint32_t> xslot;
     // finish outputs
-    DBuf<uint64_t> ukey, first, cnt_out, roff;
+    DBuf<uint64_t> ukey, first, cnt_out;
     DBuf<Agg> uval;
     DBuf<uint8_t> keys_out;
     uint64_t n_out = 0;            // ordered entries of the last finish (device)
@@ -206,6 +206,13 @@ struct kmer_ctx {
     std::unordered_map<std::string, Ent> exotic;
     uint64_t *h_small = nullptr;   // pinned (24 words): [0..7] copy of d_scal, [8..11] pos, [12..16] table feed
     uint64_t *h_tail = nullptr;    // pinned, mapped, coherent: d_scal[0..7] written by the chunk tail kernel
+    // pinned staging of every host -> device upload (upload()): a pageable
+    // hipMemcpyAsync may read its host buffer after the call returns, so the
+    // bytes are copied here first; a region is reused only after the streams
+    // that read it have been synchronised (bump allocation, drained on wrap)
+    uint8_t *up_p = nullptr;
+    size_t up_cap = 0, up_used = 0;
+    std::vector<hipStream_t> up_streams;
     uint64_t *d_tail = nullptr;    // ... its device address
     unsigned int *d_hticket = nullptr;   // chunk tail last-block ticket (d_scal[8])
     uint64_t tail_seq = 0;         // last chunk sequence number handed to the chunk tail kernel
@@ -239,7 +246,8 @@ struct kmer_ctx {
     DBuf<uint64_t> tpb;            // ... their scan
     DBuf<SeqLine> tpieces;         // long lines cut into pieces of <= TAB_PIECE windows
     DBuf<unsigned long long> tstats;   // [0..2] final statistics, [3] big-list count, [4] digest
-    uint64_t t_keys = 0;           // pass-1 keys of the session
+    uint64_t t_keys = 0;           // pass-1 slots of the session (keys, plus filler of fixed runs)
+    uint64_t t_fill = 0;           // ... of which filler slots (an estimate: windows with non-ACGT bytes are not keys)
     std::vector<uint64_t> t_cbase; // per chunk: first key in tb1
     std::vector<std::vector<uint64_t>> t_coff;   // per chunk: TAB_NB + 1 partition starts (chunk-relative)
     uint64_t t_canon = 0, t_nkeys = 0, t_sum = 0, t_nbig = 0;   // last finish
@@ -253,9 +261,11 @@ struct kmer_ctx {
     // the group itself owns no device state beyond the merge buffers on
     // devices[0] (allocated through child 0)
     std::vector<kmer_ctx *> group;
+    uint32_t peer_staged = 0;      // device pairs of the group without peer access (copies staged by the runtime)
     DBuf<uint64_t> gkeys, gkeys2;
     DBuf<Agg> gvals, gvals2;
-    double t_ms[6] = {};           // table phase times since the reset: lines, hist1, scatter1, hist2, scatter2, final
+    double t_ms[7] = {};           // table phase times since the reset: lines, hist1, scatter1, hist2, scatter2, final, fasta
+    hipEvent_t fa_ev[2] = {nullptr, nullptr};   // around a chunk's FASTA rewrite
     int n_cu = 0;
     // timing (HIP events on the context stream)
     hipEvent_t ev0 = nullptr, ev1 = nullptr, ev2 = nullptr, ev3 = nullptr, ev4 = nullptr;
@@ -363,6 +373,7 @@ struct GroupSrc {
 
 // ---- functions shared between the host translation units ----
 kmer_status ensure_tiles(kmer_ctx *c, uint64_t n_tiles);
+kmer_status upload(kmer_ctx *c, void *dst, const void *src, size_t n, hipStream_t s);
 kmer_status ensure_ovf(kmer_ctx *c, uint64_t n, hipStream_t s);
 kmer_status ensure_records(kmer_ctx *c, uint64_t n);
 kmer_status drain_records(kmer_ctx *c, const uint8_t *d_data, uint64_t n, hipStream_t s);

@@ -388,7 +388,7 @@ hipError_t launch_xprep(const XHit *x, uint64_t n, uint64_t *rkey, uint32_t *rke
                         hipStream_t s);
 hipError_t launch_merge_prep(const uint64_t *keys, const Agg *vals, uint64_t n, uint64_t *rkey, uint32_t *rkey32,
                              uint64_t *rord, uint64_t *rcnt, uint32_t *ridx, hipStream_t s);
-hipError_t launch_gather_records(const Record *recs, const uint64_t *key_off, uint64_t n,
+hipError_t launch_gather_records(const Record *recs, uint64_t stride, uint64_t n,
                                  const uint8_t *data, uint8_t *out, hipStream_t s);
 hipError_t launch_nl_count(const uint8_t *data, uint64_t len, uint32_t n_tiles, uint32_t *tcount, unsigned int *err,
                            hipStream_t s);

@@ -53,9 +53,16 @@ kmer_status feed_host(kmer_ctx *c, const uint8_t *bytes, uint64_t len, bool repo
         kmer_status st0 = settle(c);            // the previous batch is done with the staging buffer
         if (st0) return st0;
         HIPCHK(c, c->batch.ensure(n, c->stream));
+        // (the caller's bytes, read in place -- a batch is too large to stage
+        // through the upload arena: on an error the copy is waited for before
+        // returning, so the caller may release them; on success the caller's
+        // settle / finish waits for it)
         HIPCHK(c, hipMemcpyAsync(c->batch.p, bytes + pos, n, hipMemcpyHostToDevice, c->stream));
         kmer_status st = feed(c, c->batch.p, n, c->stream);
-        if (st) return st;
+        if (st) {
+            (void)hipStreamSynchronize(c->stream);
+            return st;
+        }
         pos = end;
         if (report) report_progress(c, pos, len);
     }

@@ -2127,9 +2127,9 @@ __global__ __launch_bounds__(256) void bucket_hist_kernel(const uint32_t *key, u
 // Offsets of the partition (one launch, no library scan): workgroup b scans
 // bucket b's row of block counts (H[b * nblk + blk] -> Hs, bucket-relative)
 // and publishes the bucket's total; the last workgroup to finish turns the
-// totals into the buckets' starts (bbase[nb] = all keys).  The totals are
-// stored write-through (sc1), drained before the ticket add that announces
-// them, and read back by atomics.
+// totals into the buckets' starts (bbase[nb] = all keys).  The ticket add is
+// acquire-release at agent scope (HIP memory model); the totals are read
+// back by atomics.
 __global__ __launch_bounds__(256) void bucket_offsets_kernel(const uint32_t *H, uint32_t nb, uint32_t nblk,
                                                              uint32_t *Hs, uint32_t *btot, uint32_t *bbase,
                                                              unsigned int *ticket) {
@@ -2152,9 +2152,11 @@ __global__ __launch_bounds__(256) void bucket_offsets_kernel(const uint32_t *H, 
         pre += v;
     }
     if (tid == 0) {
+        // release (the total reaches memory before the ticket announces it) and
+        // acquire (the last workgroup sees every earlier total) at agent scope:
+        // the compiler emits the L2 writeback / invalidate the XCDs need
         __hip_atomic_store(btot + b, ws[0] + ws[1] + ws[2] + ws[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        last = atomicAdd(ticket, 1u) == nb - 1;
+        last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
     }
     __syncthreads();
     if (!last) return;
@@ -2561,12 +2563,13 @@ __global__ __launch_bounds__(256) void xprep_kernel(const XHit *x, uint64_t n, u
     }
 }
 
-__global__ __launch_bounds__(256) void gather_records_kernel(const Record *recs, const uint64_t *key_off,
+// (key i at i * stride: the host map reads them back at that fixed stride)
+__global__ __launch_bounds__(256) void gather_records_kernel(const Record *recs, uint64_t stride,
                                                              uint64_t n, const uint8_t *data, uint8_t *out) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const Record r = recs[i];
-        uint8_t *o = out + key_off[i];
+        uint8_t *o = out + i * stride;
         const uint8_t *src = data + r.pos;
         if (r.strand) {
             for (uint32_t b = 0; b < r.len; ++b) o[b] = comp_byte(src[r.len - 1 - b]);
@@ -2854,12 +2857,12 @@ hipError_t launch_xprep(const XHit *x, uint64_t n, uint64_t *rkey, uint32_t *rke
     if (n) hipLaunchKernelGGL(xprep_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, n, rkey, rkey32, rord, ridx);
     return hipGetLastError();
 }
-hipError_t launch_gather_records(const Record *recs, const uint64_t *key_off, uint64_t n, const uint8_t *data,
+hipError_t launch_gather_records(const Record *recs, uint64_t stride, uint64_t n, const uint8_t *data,
                                  uint8_t *out, hipStream_t s) {
     if (n == 0) return hipSuccess;
     uint64_t blocks = (n + 255) / 256;
     if (blocks > 8192) blocks = 8192;
-    hipLaunchKernelGGL(gather_records_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, recs, key_off, n, data, out);
+    hipLaunchKernelGGL(gather_records_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, recs, stride, n, data, out);
     return hipGetLastError();
 }
 

@@ -460,6 +460,11 @@ kmer_status build_db(kmer_db *db, const char *keys, uint64_t n, const uint64_t *
     MCHK(dalloc(&pos, n));
     MCHK(dalloc(&bad, 1));
     MCHK(hipMemsetAsync(bad, 0, 4, s));
+    // (the caller's arrays, read in place: waited for on every return path)
+    struct SyncOnExit {
+        hipStream_t s;
+        ~SyncOnExit() { (void)hipStreamSynchronize(s); }
+    } wait_uploads{s};
     MCHK(hipMemcpyAsync(dkeys, keys, n * db->k, hipMemcpyHostToDevice, s));
     MCHK(hipMemcpyAsync(dts, ts, ((uint64_t)db->nt + 1) * 8, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(db_pack_kernel, dim3(grid_for(n)), dim3(256), 0, s, dkeys, n, db->k, c, bad);

@@ -110,7 +110,8 @@ kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done
     HIPCHK(c, c->tb1.ensure(cb + region + spill_cap, s, true, c->t_keys));
     HIPCHK(c, c->tspill.ensure(spill_cap, s));
     HIPCHK(c, c->tspc.ensure(1 + 2 * TAB_NB, s));
-    HIPCHK(c, hipMemcpyAsync(pcw, hp.data(), hp.size() * 8, hipMemcpyHostToDevice, s));
+    kmer_status st = upload(c, pcw, hp.data(), hp.size() * 8, s);
+    if (st) return st;
     a.pcw = pcw;
     a.R = R;
     a.base = cb;
@@ -119,7 +120,7 @@ kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done
     a.spill_n = c->tspc.p;
     a.spill_cap = spill_cap;
     HIPCHK(c, hipMemsetAsync(c->tspc.p, 0, (1 + TAB_NB) * 8, s));
-    kmer_status st = table_scatter1(c, a, s, launch_tab_scatter1f);
+    st = table_scatter1(c, a, s, launch_tab_scatter1f);
     if (st) return st;
     unsigned long long ns = 0;
     HIPCHK(c, hipMemcpyAsync(&ns, c->tspc.p, 8, hipMemcpyDeviceToHost, s));
@@ -133,6 +134,7 @@ kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done
     c->t_cbase.push_back(cb);
     c->t_coff.push_back(std::move(off));
     c->t_keys = cb + region;
+    c->t_fill += region - std::min<uint64_t>(region, tot - std::min<uint64_t>(tot, ns));
     if (ns) {                                  // the spill list: one more chunk, partition-major
         std::vector<unsigned long long> hh(TAB_NB), cur(TAB_NB);
         std::vector<uint64_t> so(TAB_NB + 1);
@@ -144,9 +146,9 @@ kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done
             cur[p] = c->t_keys + so[p];
             so[p + 1] = so[p] + hh[p];
         }
-        HIPCHK(c, hipMemcpyAsync(c->tspc.p + 1 + TAB_NB, cur.data(), TAB_NB * 8, hipMemcpyHostToDevice, s));
+        st = upload(c, c->tspc.p + 1 + TAB_NB, cur.data(), TAB_NB * 8, s);
+        if (st) return st;
         HIPCHK(c, launch_tab_spill_place(c->tspill.p, ns, c->tspc.p + 1 + TAB_NB, c->tb1.p, s));
-        HIPCHK(c, hipStreamSynchronize(s));      // (cur is a host temporary: the copy may read it until here)
         c->t_cbase.push_back(c->t_keys);
         c->t_coff.push_back(std::move(so));
         c->t_keys += ns;
@@ -206,7 +208,16 @@ kmer_status table_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_t
         a.len = len;
         a.lines = plines;
         a.n_lines = n_items;
-        const uint64_t nwg0 = std::min<uint64_t>(8192, (n_items + 63) / 64);
+        uint64_t nwg0 = std::min<uint64_t>(8192, (n_items + 63) / 64);
+        // long lines cut into pieces (contigs, C5): every item is ~4,096 windows,
+        // so 64 items per workgroup made runs of ~256 keys per partition -- too
+        // small for fixed runs (16 % filler) and for the scatter's writes.  Fewer,
+        // larger shares instead: ~2 M windows per workgroup (>= 2 per CU), which
+        // puts the fixed runs' filler near C3's 6 %.  (KMERHIP_TAB_NWG=items:
+        // the old sizing, A/B experiments.)
+        const char *nw = exp_env("KMERHIP_TAB_NWG");
+        if (plines == c->tpieces.p && !(nw && strcmp(nw, "items") == 0))
+            nwg0 = std::min<uint64_t>(nwg0, std::max<uint64_t>(2ull * std::max(c->n_cu, 1), len >> 21));
         a.lpw = (n_items + nwg0 - 1) / nwg0;
         a.nwg = (uint32_t)((n_items + a.lpw - 1) / a.lpw);
         a.k = c->p.k;
@@ -301,7 +312,8 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
     if (n_units >= (1ull << 31)) return fail(c, KMER_E_BAD_PARAM, "too many table units");
     units.insert(units.end(), heads.begin(), heads.end());
     HIPCHK(c, c->tunits.ensure(units.size(), s));
-    HIPCHK(c, hipMemcpyAsync(c->tunits.p, units.data(), units.size() * sizeof(TabUnit), hipMemcpyHostToDevice, s));
+    kmer_status st = upload(c, c->tunits.p, units.data(), units.size() * sizeof(TabUnit), s);
+    if (st) return st;
     const uint64_t nh = n_units * TAB_NB;
     HIPCHK(c, c->tH.ensure(nh, s));
     HIPCHK(c, c->tHs.ensure(nh, s));
@@ -325,7 +337,7 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
     f.start = c->tstart.p;
     f.out = c->t_ent;
     f.nd = c->tnd.p;
-    const uint64_t mean = n / TAB_NQ;
+    const uint64_t mean = (n - std::min(n, c->t_fill)) / TAB_NQ;   // (keys, not filler slots)
     uint64_t range_keys = 3000;               // mean keys per LDS range (load ~0.37: short probes; measured best at C3)
     if (const char *rk = exp_env("KMERHIP_TAB_RANGE")) range_keys = std::max<uint64_t>(64, strtoull(rk, nullptr, 10));
     while (f.sub_bits < 16 && (mean >> f.sub_bits) > range_keys) ++f.sub_bits;
@@ -432,12 +444,18 @@ kmer_status build_table_result(kmer_ctx *c, uint64_t lines, kmer_result **out) {
     const uint32_t k = c->p.k;
     if (c->t_keys) {
         hipStream_t s = c->stream;
-        std::vector<uint64_t> start(TAB_NQ + 1), ent(c->t_keys);
+        std::vector<uint64_t> start(TAB_NQ + 1), ent;
         std::vector<uint32_t> nd(TAB_NQ);
         std::vector<TabBig> big(c->t_nbig);
+        // (the table's extent is start[TAB_NQ], the keys pass 2 counted: t_keys
+        // also holds the filler slots of a fixed-run pass 1)
         bool ok = hipMemcpyAsync(start.data(), c->tstart.p, start.size() * 8, hipMemcpyDeviceToHost, s) == hipSuccess &&
                   hipMemcpyAsync(nd.data(), c->tnd.p, nd.size() * 4, hipMemcpyDeviceToHost, s) == hipSuccess &&
-                  hipMemcpyAsync(ent.data(), c->t_ent, ent.size() * 8, hipMemcpyDeviceToHost, s) == hipSuccess;
+                  hipStreamSynchronize(s) == hipSuccess && start[TAB_NQ] <= c->t_keys;
+        if (ok) {
+            ent.resize(start[TAB_NQ]);
+            ok = hipMemcpyAsync(ent.data(), c->t_ent, ent.size() * 8, hipMemcpyDeviceToHost, s) == hipSuccess;
+        }
         if (ok && !big.empty())
             ok = hipMemcpyAsync(big.data(), c->tbig.p, big.size() * sizeof(TabBig), hipMemcpyDeviceToHost, s) == hipSuccess;
         if (!ok || hipStreamSynchronize(s) != hipSuccess) {

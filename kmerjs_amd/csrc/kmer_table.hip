@@ -353,8 +353,8 @@ __global__ __launch_bounds__(TAB_WGH) void tab_scatter1h_kernel(TabArgs a) {
 // pass 1 without the counting pass (no prefix, k <= 31: every window of a
 // line is a key, so a workgroup's share of keys is known from its lines):
 // partition p's keys of workgroup w go to a run of fixed capacity at base +
-// p * R + pcw[w] (1.08x the workgroup's uniform share + 16: ~3.5 standard
-// deviations of a hash partition's count), in the same LDS-sorted rounds as
+// p * R + pcw[w] (the workgroup's mean share mu + 2 sqrt(mu) + 4, rounded up
+// to 8 keys: table_pass1_fixed in kmer_tabhost.hip), in the same LDS-sorted rounds as
 // tab_scatter1h; the run's unused tail is filled with TAB_SENT, which pass 2
 // skips.  A key past its run's capacity goes to the spill list (one atomic per
 // wave and write-out step), which the host places partition-major after the
@@ -1290,14 +1290,22 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
     const uint32_t q0 = min(a.qlo + blockIdx.x * per, a.qhi), q1 = q0 + per < a.qhi ? q0 + per : a.qhi;
     uint64_t st_canon = 0, st_keys = 0, st_sum = 0;
     // no prefix, odd k, Map view (C3): every entry is two Map keys, never a
-    // palindrome -- no decoding needed
+    // palindrome; no prefix, canonical view (C5): every entry is one key with
+    // its count -- no decoding needed in either
     const bool plain_odd = a.pmask == 0 && !a.canonical && (k & 1u);
+    const bool plain_canon = a.pmask == 0 && a.canonical;
     // Map statistics of one canonical entry h (App. A.6; as in tab_final_kernel)
     auto account = [&](uint64_t h, uint64_t cnt) {
         if (plain_odd) {
             st_canon += 1;
             st_keys += 2;
             st_sum += 2 * cnt;
+            return;
+        }
+        if (plain_canon) {
+            st_canon += 1;
+            st_keys += 1;
+            st_sum += cnt;
             return;
         }
         const uint64_t code = h * a.inv;

@@ -248,10 +248,9 @@ class KmerJS {
                 try {
                     if (kmerObj.kmerMap.size === 0 && kmerObj.kmerMap instanceof KmerMap) {
                         kmerObj.kmerMap.adopt(res, native().indexKeys);   // the same object, filled lazily (kmer_map.js)
-                    } else if (kmerObj.kmerMap.size === 0 && kmerObj.kmerMap.constructor === Map) {
-                        // (a caller replaced it with a plain empty Map: fill that object too)
-                        foldResult(kmerObj.kmerMap, res);
                     } else {
+                        // (a caller-supplied Map, empty or not: filled in place, then
+                        // held to the reference Map's limit, lib/kmers.js:95)
                         foldResult(kmerObj.kmerMap, res);
                         if (kmerObj.kmerMap.size > kmerObj.maxKeys) throw tooManyKeys('Map maximum size exceeded');
                     }

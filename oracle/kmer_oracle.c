@@ -198,6 +198,42 @@ int oracle_kmers_in_line(const uint8_t *line, size_t n, const uint8_t *prefix, s
     return kmers_in_line(out, line, n, prefix, plen, k, step);
 }
 
+/* The line loop of readFile() (lib/kmers.js:114-171) over one piece of the
+ * stream; *li is `i` of lib/kmers.js:143, carried across pieces (pieces end at
+ * a '\n' -- a whole number of lines -- except the stream's last). */
+static int count_lines(oracle_result *out, const uint8_t *buf, size_t len, int *li, uint8_t **rc, size_t *rc_cap,
+                       const uint8_t *prefix, size_t plen, uint32_t k, uint32_t step) {
+    int st = ORACLE_OK;
+    size_t pos = 0;
+    while (pos < len) {
+        const uint8_t *nl = memchr(buf + pos, '\n', len - pos);
+        size_t end = nl ? (size_t)(nl - buf) : len;
+        size_t L = end - pos;
+        if (!nl && L == 0) break;   /* _flush: empty trailing segment dropped (:131) */
+        const uint8_t *line = buf + pos;
+        if (*li == 1 && L > 1) {    /* :151 */
+            out->seq_lines++;
+            st = kmers_in_line(out, line, L, prefix, plen, k, step);
+            if (st) break;
+            if (L > *rc_cap) {
+                free(*rc);
+                *rc_cap = L * 2;
+                *rc = malloc(*rc_cap);
+                if (!*rc) { st = ORACLE_E_OOM; break; }
+            }
+            oracle_complement(line, L, *rc);
+            st = kmers_in_line(out, *rc, L, prefix, plen, k, step);
+            if (st) break;
+        } else if (*li == 3) {
+            *li = -1;               /* :160-161 */
+        }
+        *li += 1;
+        out->lines++;
+        pos = nl ? end + 1 : len;
+    }
+    return st;
+}
+
 /* readFile() — lib/kmers.js:106-185, over an in-memory byte buffer. */
 int oracle_count_buffer(const uint8_t *buf, size_t len, const uint8_t *prefix, size_t plen,
                         uint32_t k, uint32_t step, oracle_result *out) {
@@ -207,34 +243,33 @@ int oracle_count_buffer(const uint8_t *buf, size_t len, const uint8_t *prefix, s
         if (buf[i] >= 0x80) return ORACLE_E_NONASCII;
     uint8_t *rc = NULL;
     size_t rc_cap = 0;
-    int li = 0;                 /* `i` of lib/kmers.js:143 */
-    size_t pos = 0;
-    while (pos < len) {
-        const uint8_t *nl = memchr(buf + pos, '\n', len - pos);
-        size_t end = nl ? (size_t)(nl - buf) : len;
-        size_t L = end - pos;
-        if (!nl && L == 0) break;   /* _flush: empty trailing segment dropped (:131) */
-        const uint8_t *line = buf + pos;
-        if (li == 1 && L > 1) {     /* :151 */
-            out->seq_lines++;
-            st = kmers_in_line(out, line, L, prefix, plen, k, step);
-            if (st) break;
-            if (L > rc_cap) {
-                free(rc);
-                rc_cap = L * 2;
-                rc = malloc(rc_cap);
-                if (!rc) { st = ORACLE_E_OOM; break; }
-            }
-            oracle_complement(line, L, rc);
-            st = kmers_in_line(out, rc, L, prefix, plen, k, step);
-            if (st) break;
-        } else if (li == 3) {
-            li = -1;                /* :160-161 */
-        }
-        li += 1;
-        out->lines++;
-        pos = nl ? end + 1 : len;
+    int li = 0;
+    st = count_lines(out, buf, len, &li, &rc, &rc_cap, prefix, plen, k, step);
+    free(rc);
+    return st;
+}
+
+void oracle_synth_fastq(uint64_t seed, uint64_t first_read, uint64_t n_reads, uint8_t *out);
+
+/* readFile() over the synthetic FASTQ of reads [first_read, first_read +
+ * n_reads) (oracle_synth_fastq), generated and counted in
+ * blocks of whole records, so full-size workloads (C2, the C4 shard) need no
+ * copy of their input in memory.  The same line loop as oracle_count_buffer. */
+int oracle_count_synth(uint64_t seed, uint64_t first_read, uint64_t n_reads, const uint8_t *prefix, size_t plen,
+                       uint32_t k, uint32_t step, oracle_result *out) {
+    int st = res_init(out);
+    if (st) return st;
+    const uint64_t B = 8192;
+    uint8_t *buf = malloc(B * 317), *rc = NULL;
+    if (!buf) return ORACLE_E_OOM;
+    size_t rc_cap = 0;
+    int li = 0;
+    for (uint64_t r = 0; r < n_reads && !st; r += B) {
+        const uint64_t n = n_reads - r < B ? n_reads - r : B;
+        oracle_synth_fastq(seed, first_read + r, n, buf);
+        st = count_lines(out, buf, n * 317, &li, &rc, &rc_cap, prefix, plen, k, step);
     }
+    free(buf);
     free(rc);
     return st;
 }
@@ -330,4 +365,125 @@ void oracle_synth_fastq(uint64_t seed, uint64_t first_read, uint64_t n_reads, ui
         memset(s + 153, 'I', 150);
         s[303] = '\n';
     }
+}
+
+/* ---- table digest (kmer_table_digest's definition), streaming ----
+ * Table mode stores one entry per canonical class {x, rc x} (SURVEY.md App.
+ * A.6), counted once per FORWARD window of a sequence line (lines as
+ * readFile() splits them, lib/kmers.js:114-171; windows lib/kmers.js:88-100
+ * with step 1); windows holding a byte outside A/C/G/T are records, outside
+ * the digest.  With the planar code of a k-mer (base i at bit i of two planes,
+ * A/C/G/T = (hi, lo) 00/01/10/11, code = hi << k | lo) and h = min(code(w),
+ * code(rc w)) * 0x9E3779B97F4A7C15, the digest is
+ *     sum over classes of count x mix(h) = sum over forward windows of mix(h)
+ * (mod 2^64; mix = splitmix64's finaliser): linear, so no map is needed.
+ * Codes are rolled: one new base per window on the forward planes (shift
+ * down) and on the reverse-complement planes (shift up). */
+static inline uint64_t digest_mix(uint64_t h) {
+    h ^= h >> 30;
+    h *= 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 27;
+    h *= 0x94D049BB133111EBull;
+    return h ^ (h >> 31);
+}
+
+static void digest_line(const uint8_t *t, size_t L, uint32_t k, uint64_t *dig, uint64_t *win) {
+    const uint64_t mask = k >= 64 ? ~0ull : (1ull << k) - 1;
+    uint64_t flo = 0, fhi = 0, rlo = 0, rhi = 0, acc = 0, n = 0;
+    uint32_t run = 0;                        /* A/C/G/T bytes ending here */
+    for (size_t i = 0; i < L; ++i) {
+        const uint8_t b = t[i];
+        if (b == 'A' || b == 'C' || b == 'G' || b == 'T') {
+            const uint64_t lo = ((b >> 1) ^ (b >> 2)) & 1u, hi = (b >> 2) & 1u;
+            flo = (flo >> 1) | (lo << (k - 1));
+            fhi = (fhi >> 1) | (hi << (k - 1));
+            rlo = ((rlo << 1) | (lo ^ 1u)) & mask;
+            rhi = ((rhi << 1) | (hi ^ 1u)) & mask;
+            if (run < k) ++run;
+        } else {
+            run = 0;
+        }
+        if (i + 1 >= k) {                    /* window [i + 1 - k, i] */
+            ++n;
+            if (run >= k) {
+                const uint64_t cf = fhi << k | flo, cr = rhi << k | rlo;
+                acc += digest_mix((cf < cr ? cf : cr) * 0x9E3779B97F4A7C15ull);
+            }
+        }
+    }
+    *dig += acc;
+    *win += n;
+}
+
+/* over a buffer: sequence lines as readFile() finds them (k <= 31) */
+static void digest_lines(const uint8_t *buf, size_t len, int *li, uint32_t k, uint64_t *dig, uint64_t *win) {
+    size_t pos = 0;
+    while (pos < len) {
+        const uint8_t *nl = memchr(buf + pos, '\n', len - pos);
+        size_t end = nl ? (size_t)(nl - buf) : len;
+        size_t L = end - pos;
+        if (!nl && L == 0) break;
+        if (*li == 1 && L > 1) digest_line(buf + pos, L, k, dig, win);
+        else if (*li == 3) *li = -1;
+        *li += 1;
+        pos = nl ? end + 1 : len;
+    }
+}
+
+int oracle_table_digest_buffer(const uint8_t *buf, size_t len, uint32_t k, uint64_t *digest, uint64_t *windows) {
+    if (k == 0 || k > 31) return ORACLE_E_NONASCII + 2;
+    int li = 0;
+    *digest = 0;
+    *windows = 0;
+    digest_lines(buf, len, &li, k, digest, windows);
+    return ORACLE_OK;
+}
+
+#include <pthread.h>
+
+typedef struct {
+    uint64_t seed, r0, r1, dig, win;
+    uint32_t k;
+    int st;
+} digest_job;
+
+static void *digest_worker(void *arg) {
+    digest_job *j = arg;
+    const uint64_t B = 4096;
+    uint8_t *buf = malloc(B * 317);
+    if (!buf) { j->st = ORACLE_E_OOM; return NULL; }
+    for (uint64_t r = j->r0; r < j->r1; r += B) {
+        const uint64_t n = j->r1 - r < B ? j->r1 - r : B;
+        int li = 0;                          /* blocks are whole records */
+        oracle_synth_fastq(j->seed, r, n, buf);
+        digest_lines(buf, n * 317, &li, j->k, &j->dig, &j->win);
+    }
+    free(buf);
+    return NULL;
+}
+
+/* the table digest of the synthetic FASTQ reads [first_read, first_read +
+ * n_reads) on `threads` threads (full-size C3: 100 M reads, 24 G windows) */
+int oracle_table_digest_synth(uint64_t seed, uint64_t first_read, uint64_t n_reads, uint32_t k, uint32_t threads,
+                              uint64_t *digest, uint64_t *windows) {
+    if (k == 0 || k > 31) return ORACLE_E_NONASCII + 2;
+    if (threads == 0) threads = 1;
+    if (threads > 256) threads = 256;
+    digest_job jobs[256];
+    pthread_t tid[256];
+    int st = ORACLE_OK;
+    for (uint32_t t = 0; t < threads; ++t) {
+        jobs[t] = (digest_job){seed, first_read + n_reads * t / threads, first_read + n_reads * (t + 1) / threads,
+                               0, 0, k, ORACLE_OK};
+        if (pthread_create(&tid[t], NULL, digest_worker, &jobs[t])) { threads = t; st = ORACLE_E_OOM; break; }
+    }
+    *digest = 0;
+    *windows = 0;
+    for (uint32_t t = 0; t < threads; ++t) {
+        pthread_join(tid[t], NULL);
+        *digest += jobs[t].dig;
+        *windows += jobs[t].win;
+        if (jobs[t].st) st = jobs[t].st;
+    }
+    return st;
 }

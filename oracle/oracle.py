@@ -45,6 +45,16 @@ def lib():
         L.oracle_free.argtypes = [ctypes.POINTER(_Res)]
         L.oracle_complement.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]
         L.oracle_synth_fastq.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p]
+        L.oracle_count_synth.restype = ctypes.c_int
+        L.oracle_count_synth.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_char_p,
+                                         ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(_Res)]
+        L.oracle_table_digest_buffer.restype = ctypes.c_int
+        L.oracle_table_digest_buffer.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32,
+                                                 ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        L.oracle_table_digest_synth.restype = ctypes.c_int
+        L.oracle_table_digest_synth.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                                ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64),
+                                                ctypes.POINTER(ctypes.c_uint64)]
         _LIB = L
     return _LIB
 
@@ -98,6 +108,49 @@ def count_arrays(data: bytes, prefix: bytes = b"ATGAC", k: int = 16):
         return keys, np.ctypeslib.as_array(r.counts, shape=(n,)).copy()
     finally:
         lib().oracle_free(ctypes.byref(r))
+
+
+def count_synth_arrays(seed: int, first_read: int, n_reads: int, prefix: bytes = b"ATGAC", k: int = 16):
+    """readFile() over the synthetic reads [first_read, first_read + n_reads)
+    (oracle_count_synth: generated and counted in blocks, no input copy), as
+    numpy arrays in Map order: keys (n, k) uint8, counts, first-occurrence
+    ordinals (monotone), lines."""
+    import numpy as np
+    r = _Res()
+    st = lib().oracle_count_synth(seed, first_read, n_reads, prefix, len(prefix), k, 1, ctypes.byref(r))
+    try:
+        if st:
+            raise OracleError("oracle status %d" % st)
+        n = int(r.n)
+        if n == 0:
+            return np.zeros((0, k), np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint64), int(r.lines)
+        off = np.ctypeslib.as_array(r.key_off, shape=(n,))
+        assert int(off[-1]) == (n - 1) * k, "step-1 keys are k bytes, back to back"
+        keys = np.ctypeslib.as_array(r.keys, shape=(n * k,)).reshape(n, k).copy()
+        return (keys, np.ctypeslib.as_array(r.counts, shape=(n,)).copy(),
+                np.ctypeslib.as_array(r.first, shape=(n,)).copy(), int(r.lines))
+    finally:
+        lib().oracle_free(ctypes.byref(r))
+
+
+def table_digest(data: bytes, k: int):
+    """kmer_table_digest's definition, streamed over a buffer (no map):
+    (digest, windows examined per strand)."""
+    d, w = ctypes.c_uint64(), ctypes.c_uint64()
+    st = lib().oracle_table_digest_buffer(data, len(data), k, ctypes.byref(d), ctypes.byref(w))
+    if st:
+        raise OracleError("oracle status %d" % st)
+    return d.value, w.value
+
+
+def table_digest_synth(seed: int, first_read: int, n_reads: int, k: int, threads: int = 1):
+    """table_digest of the synthetic reads [first_read, first_read + n_reads)
+    on `threads` host threads: (digest, windows per strand)."""
+    d, w = ctypes.c_uint64(), ctypes.c_uint64()
+    st = lib().oracle_table_digest_synth(seed, first_read, n_reads, k, threads, ctypes.byref(d), ctypes.byref(w))
+    if st:
+        raise OracleError("oracle status %d" % st)
+    return d.value, w.value
 
 
 def kmers_in_line(line: bytes, prefix: bytes = b"ATGAC", k: int = 16, step: int = 1):

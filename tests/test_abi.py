@@ -85,3 +85,34 @@ def test_open_rejects_reserved_flag_bits_without_gpu():
             assert e.status == 2
         else:
             raise AssertionError("accepted flag bit %d" % bit)
+
+
+def _h2d_copies():
+    """Every hipMemcpyAsync(..., hipMemcpyHostToDevice, ...) in the library's
+    sources: (file, line, source argument)."""
+    out = []
+    csrc = os.path.join(REPO, "kmerjs_amd", "csrc")
+    for fn in sorted(os.listdir(csrc)):
+        if not fn.endswith((".hip", ".hpp")):
+            continue
+        with open(os.path.join(csrc, fn), encoding="utf-8") as f:
+            src = f.read()
+        for m in re.finditer(r"hipMemcpyAsync\s*\(([^;]*?)hipMemcpyHostToDevice", src):
+            args = [a.strip() for a in m.group(1).split(",")]
+            out.append((fn, src.count("\n", 0, m.start()) + 1, args[1]))
+    return out
+
+
+def test_no_async_upload_reads_a_host_temporary():
+    # A pageable hipMemcpyAsync may read its host buffer after the call has
+    # returned (round 4: a std::vector died first and stray keys were written).
+    # Host temporaries go through the pinned upload arena (upload(),
+    # kmer_feed.hip); the copies left read the arena, the caller's buffers or
+    # long-lived members (ctx->..., db->..., m->...).
+    copies = _h2d_copies()
+    assert copies, "pattern found no upload at all"
+    bad = [(fn, ln, a) for fn, ln, a in copies
+           if ".data()" in a or (a.startswith("&") and "->" not in a) or a in ("off", "cur", "hp", "units", "segs")]
+    assert not bad, bad
+    srcs = sorted(set(a for _, _, a in copies))
+    assert srcs == sorted(set(["h", "bytes + pos", "keys", "ts", "&db->entries", "&m->hits0", "offsets", "counts"])), srcs

@@ -1,10 +1,13 @@
-"""Full-size property tests of the BASELINE configurations (C2, C3, the C4
-per-GPU shard): at these sizes no oracle finishes, so they check properties
-that hold at any size -- Σ counts against windows counted independently on
-the device, sortedness of first-occurrence keys, key uniqueness, sharded ==
-whole, and for table mode the linear table digest (kmer_table_digest: the
-digest over input A + B is the sum of the digests over A and B, pinned to the
-oracle at small sizes in tests/test_table_gpu.py).  Marked `fullsize`:
+"""Full-size tests of the BASELINE configurations (C2, C3, the C4 per-GPU
+shard).  Pinned to answers computed ahead of time at the same sizes: C2's
+ordered Map digest is the reference's own (lib/kmers.js run unmodified on the
+same bytes, profiles/ref_js_c2.json) and the oracle's; the C4 shard's Map
+digest and C3's table digest come from the oracle streamed over the same
+synthetic reads (tests/golden/fullsize.json, tests/golden/gen_fullsize.py).
+Plus properties that hold at any size -- Σ counts against windows counted
+independently on the device, sortedness of first-occurrence keys, key
+uniqueness, sharded == whole, and the linear table digest (the digest over
+input A + B is the sum of the digests over A and B).  Marked `fullsize`:
 tests/conftest.py runs them after every parity test."""
 import numpy as np
 import pytest
@@ -43,6 +46,17 @@ def test_c2_full_size_properties(native):
     accepted = int(fwd[:, :150 - k + 1].sum()) + int(rev[:, k - 5:].sum())
     del fwd, rev
     assert int(res.counts.sum()) == accepted
+    # the reference's own output on this workload: lib/kmers.js readFile()
+    # (:106-185) run unmodified on the same 3.17 GB in the build container
+    # (profiles/ref_js_c2.json), and the oracle's streamed count
+    # (tests/golden/fullsize.json, tests/golden/gen_fullsize.py)
+    from tests.util import fullsize_golden, map_digest_arrays
+    ref = {"size": 1_956_210, "sum": 2_635_074, "digest": "aadbad6b77b37001"}
+    gold = fullsize_golden()["c2"]
+    assert {x: gold[x] for x in ref} == ref
+    assert len(res) == ref["size"] and int(res.counts.sum()) == ref["sum"]
+    keys = np.frombuffer(res.keybuf, dtype=np.uint8).reshape(-1, k)
+    assert map_digest_arrays(keys, res.counts) == ref["digest"]
     assert len(set(res.keys())) == len(res)
     assert all(key.startswith(prefix) for key in res.keys()[:100000])
     f = res.firsts.astype(np.uint64)
@@ -100,6 +114,12 @@ def test_c3_full_size_properties(native):
         d = ctr.table_digest()
         assert total == 2 * 120 * n == 24_000_000_000
         assert keys == 2 * canon
+        # the oracle's table digest of the same 100 M reads (a streamed sum
+        # over forward windows, tests/golden/gen_fullsize.py)
+        from tests.util import fullsize_golden
+        gold = fullsize_golden()["c3"]
+        assert gold["forward_windows"] == total // 2
+        assert d == gold["table_digest"]
         assert 11_900_000_000 < canon <= 12_000_000_000
         assert total == parts[0][0][2] + parts[1][0][2]
         assert canon <= parts[0][0][0] + parts[1][0][0]
@@ -191,6 +211,12 @@ def test_c4_shard_full_size_properties(native):
     assert int(cnt.sum()) == accepted
     assert m <= 4 ** 11 and bool((keys[:, :5] == torch.tensor(list(prefix), dtype=torch.uint8, device=dev)).all())
     assert bool((fst[1:] > fst[:-1]).all())
+    # the oracle's Map of the same 125 M reads (streamed on 8 record-aligned
+    # shards and merged by first occurrence, tests/golden/gen_fullsize.py)
+    from tests.util import fullsize_golden, map_digest_arrays
+    gold = fullsize_golden()["c4"]
+    assert m == gold["size"] and int(cnt.sum()) == gold["sum"] and gold["lines"] == 4 * n
+    assert map_digest_arrays(keys.cpu().numpy(), cnt.cpu().numpy().view(np.uint64)) == gold["digest"]
     # 2 ranks' worth on the same device: exchange by key range, per-owner finish,
     # then the owners' ordered lists merged by first occurrence on "rank 0"
     half = n // 2

@@ -105,3 +105,55 @@ def test_fasta_oracle_matches_python_restatement():
     assert got == [(b"ACGT", 2)]
     # ... and do not cross records
     assert oracle.count_buffer(b">r\nAC\n>s\nGT\n", b"", 4, 1, fasta=True) == []
+
+
+def test_streamed_count_equals_buffer_count():
+    # oracle_count_synth (blocks of generated records, the line state carried)
+    # == oracle_count_buffer over the same bytes; its digest helper == digest()
+    import numpy as np
+    from tests.util import map_digest_arrays
+    data = oracle.synth_fastq(7, 1000, 20000)
+    keys, cnt = oracle.count_arrays(data, b"ATGAC", 16)
+    k2, c2, f2, lines = oracle.count_synth_arrays(7, 1000, 20000, b"ATGAC", 16)
+    assert np.array_equal(keys, k2) and np.array_equal(cnt, c2) and lines == 80000
+    assert bool(np.all(f2[1:] > f2[:-1]))
+    ents = oracle.count_buffer(data, b"ATGAC", 16)
+    assert map_digest_arrays(keys, cnt) == digest(ents)[:16]
+
+
+def test_streamed_table_digest_equals_map_digest():
+    # oracle_table_digest (a sum over forward windows, no map) == the table
+    # digest derived from the oracle's Map (canonical classes counted once per
+    # forward window, App. A.6), with N bytes (records, outside the digest),
+    # odd / even k (palindromes) and k = 1
+    import numpy as np
+    from tests.util import canonical_summary
+    for k in (31, 16, 21, 2, 1):
+        rng = np.random.default_rng(k)
+        arr = np.frombuffer(bytearray(oracle.synth_fastq(8, 0, 3000)), dtype=np.uint8).reshape(-1, 317).copy()
+        seq = arr[:, 13:163]
+        seq[rng.random(seq.shape) < 0.002] = ord("N")
+        arr[:, 13:163] = seq
+        data = arr.tobytes()
+        keys, cnt = oracle.count_arrays(data, b"", k)
+        acgt = ~(keys == ord("N")).any(axis=1)
+        _, fwd, dig = canonical_summary(keys[acgt], cnt[acgt], k)
+        got, win = oracle.table_digest(data, k)
+        assert got == dig and win == 3000 * (150 - k + 1), k
+    clean = oracle.synth_fastq(3, 500, 4000)
+    assert oracle.table_digest_synth(3, 500, 4000, 31, 1) == oracle.table_digest(clean, 31)
+    assert oracle.table_digest_synth(3, 500, 4000, 31, 3) == oracle.table_digest(clean, 31)
+
+
+def test_fullsize_golden_c2_is_the_reference_digest():
+    # tests/golden/fullsize.json's C2 answer (the oracle, streamed and merged
+    # over shards) equals the reference's own readFile() run on the same bytes
+    # (profiles/ref_js_c2.json)
+    import json
+    import os
+    from tests.util import fullsize_golden
+    ref = json.load(open(os.path.join(os.path.dirname(__file__), "..", "profiles", "ref_js_c2.json")))
+    run = ref["runs"][0]
+    g = fullsize_golden()
+    assert (g["c2"]["digest"], g["c2"]["size"], g["c2"]["sum"]) == (run["digest"], run["size"], run["sum"])
+    assert g["c4"]["lines"] == 4 * 125_000_000 and g["c3"]["forward_windows"] == 100_000_000 * 120

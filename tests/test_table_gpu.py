@@ -254,10 +254,12 @@ def _canonical_from_map(entries):
     return sorted(out)
 
 
-@pytest.mark.parametrize("k,prefix", [(21, b""), (16, b"A"), (31, b""), (12, b"GT")])
-def test_canonical_mode_vs_oracle(native, golden, inputs, k, prefix):
+@pytest.mark.parametrize("k,prefix,fixed", [(21, b"", False), (16, b"A", False), (31, b"", False), (12, b"GT", False),
+                                            (21, b"", True), (31, b"", True)])
+def test_canonical_mode_vs_oracle(native, golden, inputs, k, prefix, fixed):
     # KMER_FLAG_CANONICAL (BASELINE C5's "canonical k-mers"): one key per
-    # {x, rc x} class, counted once per forward window
+    # {x, rc x} class, counted once per forward window; `fixed`: pass 1 with
+    # fixed runs and filler slots forced (FLAG_TABLE_FIXED_TEST)
     from oracle import oracle
     rng = np.random.default_rng(k)
     arr = np.frombuffer(bytearray(oracle.synth_fastq(6, 0, 6000)), dtype=np.uint8).reshape(-1, 317).copy()
@@ -265,7 +267,7 @@ def test_canonical_mode_vs_oracle(native, golden, inputs, k, prefix):
     seq[rng.random(seq.shape) < 0.002] = ord("N")
     arr[:, 13:163] = seq
     datas = [arr.tobytes(), inputs["test_kmers.fastq"], inputs["test_long.kmer.fastq"], inputs["edge_contigs.fsa"]]
-    ctr = native.Counter(k=k, prefix=prefix, flags=native.FLAG_CANONICAL)
+    ctr = native.Counter(k=k, prefix=prefix, flags=native.FLAG_CANONICAL | (native.FLAG_TABLE_FIXED_TEST if fixed else 0))
     for data in datas:
         want = _canonical_from_map(oracle.count_buffer(data, prefix, k, 1))
         got = ctr.count_buffer(data).entries()
@@ -349,8 +351,10 @@ def test_table_group_through_the_c_abi(native, inputs, devs, tmp_path):
     seq[rng.random(seq.shape) < 0.001] = ord("N")
     arr[:, 13:163] = seq
     datas = [arr.tobytes(), inputs["test_long.kmer.fastq"], inputs["edge_contigs.fsa"], inputs["edge_blank.fastq"]]
+    fx = native.FLAG_TABLE_FIXED_TEST           # (fixed runs with filler slots through the group's key exchange)
     for flags, k, p in ((native.FLAG_UNORDERED, 31, b""), (native.FLAG_CANONICAL, 21, b""),
-                        (native.FLAG_UNORDERED, 16, b"AC")):
+                        (native.FLAG_UNORDERED, 16, b"AC"), (native.FLAG_UNORDERED | fx, 31, b""),
+                        (native.FLAG_CANONICAL | fx, 21, b"")):
         one = native.Counter(k=k, prefix=p, flags=flags)
         grp = native.Counter(k=k, prefix=p, flags=flags, devices=devs)
         small = native.Counter(k=k, prefix=p, flags=flags, devices=devs, batch_bytes=1 << 16)
@@ -418,14 +422,19 @@ def _table_dump(native, ctr):
     return h[o], cnt[o]
 
 
-@pytest.mark.parametrize("world,k,flags_name,with_n", [(2, 31, "FLAG_UNORDERED", False), (3, 21, "FLAG_CANONICAL", True),
-                                                       (1, 16, "FLAG_UNORDERED", True)])
-def test_table_exchange_matches_one_table(native, world, k, flags_name, with_n):
+@pytest.mark.parametrize("world,k,flags_name,with_n,fixed", [
+    (2, 31, "FLAG_UNORDERED", False, False), (3, 21, "FLAG_CANONICAL", True, False),
+    (1, 16, "FLAG_UNORDERED", True, False), (2, 31, "FLAG_UNORDERED", False, True),
+    (3, 21, "FLAG_CANONICAL", True, True), (2, 31, "FLAG_UNORDERED", "polya", True)])
+def test_table_exchange_matches_one_table(native, world, k, flags_name, with_n, fixed):
     """Multi-GPU table mode in one process: `world` contexts count record-aligned
     shards, their pass-1 keys are exchanged by owning partition range
     (kmer_table_exchange_prepare / _finish_exchanged, the all-to-all done with
     device copies), and the union of the owners' tables equals the one-context
-    table entry for entry; the ranks' statistics add up to its statistics."""
+    table entry for entry; the ranks' statistics add up to its statistics.
+    `fixed`: the ranks' pass 1 writes fixed runs (FLAG_TABLE_FIXED_TEST), so
+    filler slots, the chunks' alignment gaps and (poly-A reads crowding one
+    partition) spill chunks travel through the segment-copy exchange."""
     import torch
     from kmerjs_amd import multi
     from oracle import oracle
@@ -435,7 +444,10 @@ def test_table_exchange_matches_one_table(native, world, k, flags_name, with_n):
         rng = np.random.default_rng(k)
         arr = np.frombuffer(bytearray(oracle.synth_fastq(5, 0, n_reads)), dtype=np.uint8).reshape(-1, 317).copy()
         seq = arr[:, 13:163]
-        seq[rng.random(seq.shape) < 0.001] = ord("N")
+        if with_n == "polya":
+            seq[::16] = ord("A")          # (~560 K copies per rank: spill chunks, no list overflow)
+        else:
+            seq[rng.random(seq.shape) < 0.001] = ord("N")
         arr[:, 13:163] = seq
         buf = torch.from_numpy(arr.reshape(-1)).cuda()
     else:
@@ -448,7 +460,8 @@ def test_table_exchange_matches_one_table(native, world, k, flags_name, with_n):
     want_stats = one.table_stats()
     one.close()
     cuts = [317 * (n_reads * r // world) for r in range(world + 1)]
-    ctrs = [native.Counter(k=k, prefix=b"", flags=flags) for _ in range(world)]
+    ctrs = [native.Counter(k=k, prefix=b"", flags=flags | (native.FLAG_TABLE_FIXED_TEST if fixed else 0))
+            for _ in range(world)]
     sends = []
     for r, c in enumerate(ctrs):
         c.reset()

@@ -13,6 +13,28 @@ def digest(entries):
     return hashlib.sha256(js_stringify(entries).encode("utf-8")).hexdigest()
 
 
+def map_digest_arrays(keys, counts):
+    """digest()[:16] of a Map given as arrays in Map order -- keys (n, k) uint8
+    of JSON-plain bytes (A/C/G/T), counts (n,) -- without building the list
+    of pairs (full-size results: millions of entries)."""
+    h = hashlib.sha256()
+    h.update(b"[")
+    kb = keys.tobytes()
+    k = keys.shape[1] if keys.ndim == 2 else 0
+    for i, c in enumerate(counts.tolist()):
+        h.update(b'%s["%s",%d]' % (b"," if i else b"", kb[i * k:(i + 1) * k], c))
+    h.update(b"]")
+    return h.hexdigest()[:16]
+
+
+def fullsize_golden():
+    """tests/golden/fullsize.json: the oracle's answers at the BASELINE
+    workloads' full sizes (tests/golden/gen_fullsize.py)."""
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fullsize.json")) as f:
+        return json.load(f)
+
+
 def first_diff(a, b):
     for i, (x, y) in enumerate(zip(a, b)):
         if x != y:
