@@ -675,11 +675,13 @@ def main():
                          "final": "tab_sort_final_kernel (+ tab_final_kernel on its leftover units)",
                          "fasta": "fa_tiles_kernel + fa_write_kernel (FASTA rewrite)"}[kern_name]
         elif args.k > 64 or (not args.prefix and args.k > 31):
-            # general path (k > 64): line arrays + one thread per window, every
-            # hit a record merged on the host -- the feed kernels together
-            kern_name = "lines + windows_kernel (general path; host record merge dominates the step)"
+            # general path (k > 64, unprefixed k > 31): line arrays + one thread
+            # per window; the accepted windows are merged on the device
+            # (general_merge: hash sort + byte-checked groups) -- the feed
+            # kernels together (lines, windows, append)
+            kern_name = "lines_kernel + windows_kernel (general path, device merge at finish)"
             kern_ms = sum(feed_ms_l) / len(feed_ms_l)
-            algo_bytes = nbytes + 40 * (accepted / world)
+            algo_bytes = nbytes + (24 + args.k) * (accepted / world)
         elif args.flags & 2 or not set(args.prefix) <= set("ACGT"):
             # tile path with records (records forced, or a non-ACGT prefix): the
             # plane scan for A/C/G/T prefixes (else the byte-SWAR scan)

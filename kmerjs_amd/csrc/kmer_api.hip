@@ -143,6 +143,9 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
         c->mode = MODE_TILE_REC;
     else
         c->mode = MODE_GENERAL;
+    // general path with step 1: every record is a k-byte key, merged on the
+    // device (KMER_FLAG_NO_DENSE keeps the host record merge, for the tests)
+    c->gm_on = c->mode == MODE_GENERAL && pp->step == 1 && !(pp->flags & KMER_FLAG_NO_DENSE);
     const bool packed_keys = c->mode == MODE_PACKED || c->mode == MODE_WINDOWS;
     c->kbits = packed_keys ? 2 * (k - plen) : 0;
     c->narrow = packed_keys && c->kbits <= 31;
@@ -165,11 +168,13 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
     ok &= dalloc(&c->d_P, std::max<uint32_t>(plen, 1)) == hipSuccess;
     if (ok && plen) ok &= hipMemcpy(c->d_P, c->prefix.data(), plen, hipMemcpyHostToDevice) == hipSuccess;
     {
-        // [0,64) P and [64,128) rc(P) (tile kernel, truncated), [128, 128+|P|) full P (general kernel)
-        std::vector<uint8_t> pr(2 * KMAX_TILE + c->prefix.size(), 0);
+        // [0,64) P and [64,128) rc(P) (tile kernel, truncated), [128, 128+|P|) full P,
+        // [128+|P|, 128+2|P|) full rc(P) (general kernels)
+        std::vector<uint8_t> pr(2 * KMAX_TILE + 2 * c->prefix.size(), 0);
         memcpy(pr.data(), c->prefix.data(), std::min<size_t>(c->prefix.size(), KMAX_TILE));
         memcpy(pr.data() + KMAX_TILE, c->rprefix.data(), std::min<size_t>(c->rprefix.size(), KMAX_TILE));
         memcpy(pr.data() + 2 * KMAX_TILE, c->prefix.data(), c->prefix.size());
+        memcpy(pr.data() + 2 * KMAX_TILE + c->prefix.size(), c->rprefix.data(), c->rprefix.size());
         ok &= dalloc(&c->d_PR, pr.size()) == hipSuccess;
         if (ok) ok &= hipMemcpy(c->d_PR, pr.data(), pr.size(), hipMemcpyHostToDevice) == hipSuccess;
     }
@@ -275,6 +280,12 @@ kmer_status kmer_close(kmer_ctx *c) {
     c->tstats.release();
     c->tleft.release();
     c->trecv.release();
+    c->gm_keys.release();
+    c->gm_keys2.release();
+    for (auto *b : {&c->gm_cnt, &c->gm_cnt2, &c->gm_first, &c->gm_first2, &c->gm_h1, &c->gm_h2, &c->gm_h1b, &c->gm_h2b})
+        b->release();
+    for (auto *b : {&c->gm_idx, &c->gm_idx2, &c->gm_head, &c->gm_gid, &c->gm_start}) b->release();
+    c->gm_flag.release();
     dfree(c->d_ticket); dfree(c->d_bticket); dfree(c->d_scal); dfree(c->d_pos); dfree(c->d_pos_saved);
     dfree(c->d_P); dfree(c->d_PR);
     if (c->h_small) (void)hipHostFree(c->h_small);
@@ -611,6 +622,11 @@ kmer_status kmer_table_finish_exchanged(kmer_ctx *c, void *d_recv, uint64_t n, c
 kmer_status kmer_records_export(kmer_ctx *c, kmer_result **out) {
     if (!c || !out) return KMER_E_BAD_PARAM;
     SETTLE(c);
+    if (c->gm_on && c->gm_n) {              // (general-path entries held on the device travel as records)
+        if (hipSetDevice(c->device) != hipSuccess) return KMER_E_DEVICE;
+        kmer_status st = general_to_host(c);
+        if (st) return st;
+    }
     kmer_result *r = new (std::nothrow) kmer_result();
     if (!r) return KMER_E_OOM;
     std::vector<std::pair<uint64_t, const std::pair<const std::string, Ent> *>> ex;

@@ -495,7 +495,82 @@ kmer_status collect_lines(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t 
     return KMER_OK;
 }
 
+// General path with the device merge (step 1): the chunk's sequence lines
+// (chunk_lines, as the dense path), the windows flattened over them
+// (gen_windows_kernel), the accepted ones appended to the session's entries.
+kmer_status general_feed_dev(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s) {
+    const uint64_t li0 = c->host_lines;
+    HIPCHK(c, hipEventRecord(c->ev0, s));
+    uint64_t n_nl = 0, n_seq = 0;
+    kmer_status st = chunk_lines(c, d, len, n_tiles, s, true, &n_nl, &n_seq);
+    if (st) return st;
+    uint64_t total = 0;
+    if (n_seq) {
+        HIPCHK(c, c->wbase.ensure(n_seq, s));
+        ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->wcount.p, c->wbase.p, (uint64_t)0, (size_t)n_seq,
+                                               rocprim::plus<uint64_t>(), s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 14, c->wbase.p + n_seq - 1, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 15, c->wcount.p + n_seq - 1, 8, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(c, launch_pos_after(c->d_pos, li0 + n_nl, d, len, c->d_ends_open, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    if (n_seq) total = c->h_small[14] + c->h_small[15];
+    c->host_lines = li0 + n_nl;
+    uint64_t nrec = 0;
+    if (total) {
+        if (c->prefix.empty()) {                // (every window is a record)
+            st = ensure_records(c, total);
+            if (st) return st;
+        }
+        GenWinArgs w;
+        memset(&w, 0, sizeof(w));
+        w.data = d;
+        w.len = len;
+        w.lines = c->lines.p;
+        w.wbase = c->wbase.p;
+        w.n_lines = n_seq;
+        w.total = total;
+        w.k = c->p.k;
+        w.plen = (uint32_t)c->prefix.size();
+        w.pbits = c->pbits;
+        w.P = c->d_PR + 2 * KMAX_TILE;
+        w.RP = w.P + c->prefix.size();
+        w.err = c->d_err;
+        for (int attempt = 0;; ++attempt) {
+            w.recs = c->recs.p;
+            w.rec_count = c->d_rec_count;
+            w.rec_cap = c->recs.cap;
+            HIPCHK(c, hipMemsetAsync(c->d_rec_count, 0, 8, s));
+            HIPCHK(c, launch_gen_windows(w, s));
+            HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            const uint32_t e = (uint32_t)c->h_small[5];
+            st = check_err(c, e);
+            if (st) return st;
+            if (!(e & ERR_REC_OVERFLOW)) break;
+            if (attempt == 7) return fail(c, KMER_E_OOM, "record list kept overflowing");
+            HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
+            st = ensure_records(c, c->h_small[0] + 1024);
+            if (st) return st;
+        }
+        nrec = c->h_small[0];
+    }
+    if (nrec) {
+        st = general_append(c, d, nrec, s);
+        if (st) return st;
+    }
+    HIPCHK(c, hipEventRecord(c->ev1, s));
+    HIPCHK(c, hipEventSynchronize(c->ev1));
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    c->scan_ms += ms;
+    c->feed_ms += ms;
+    c->abs_offset += len;
+    return KMER_OK;
+}
+
 kmer_status general_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s) {
+    if (c->gm_on) return general_feed_dev(c, d, len, n_tiles, s);
     uint64_t nlines = 0;
     kmer_status st = collect_lines(c, d, len, n_tiles, s, &nlines);
     if (st) return st;
@@ -789,6 +864,8 @@ kmer_status reset(kmer_ctx *c) {
     c->n_out = 0;
     c->t_keys = 0;
     c->t_fill = 0;
+    c->gm_n = 0;
+    c->gm_merged = true;
     c->t_cbase.clear();
     c->t_coff.clear();
     c->t_done = false;

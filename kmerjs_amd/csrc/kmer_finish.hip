@@ -256,6 +256,169 @@ kmer_status rank_finish(kmer_ctx *c, uint64_t n, bool partial, bool with_counts,
     return KMER_OK;
 }
 
+// ---------------------------------------------------------------------------
+// general path, device merge (step 1): k > 64, unprefixed k > 31, any prefix
+// bytes -- no host merge of the records (lib/kmers.js:88-100 has no k limit)
+// ---------------------------------------------------------------------------
+constexpr uint64_t GM_MERGE_AT = 1ull << 25;   // entries held before an intermediate merge
+
+// a chunk's records (c->recs) -> session entries (key bytes, count 1, first)
+kmer_status general_append(kmer_ctx *c, const uint8_t *d, uint64_t nrec, hipStream_t s) {
+    const uint64_t k = c->p.k;
+    if (c->gm_n && c->gm_n + nrec > GM_MERGE_AT) {
+        kmer_status st = general_merge(c);
+        if (st) return st;
+    }
+    const uint64_t n = c->gm_n + nrec;
+    HIPCHK(c, c->gm_keys.ensure(n * k, s, true, c->gm_n * k));
+    HIPCHK(c, c->gm_cnt.ensure(n, s, true, c->gm_n));
+    HIPCHK(c, c->gm_first.ensure(n, s, true, c->gm_n));
+    HIPCHK(c, launch_gen_append(c->recs.p, nrec, d, (uint32_t)k, c->gm_keys.p + c->gm_n * k, c->gm_cnt.p + c->gm_n,
+                                c->gm_first.p + c->gm_n, s));
+    c->gm_n = n;
+    c->gm_merged = false;
+    return KMER_OK;
+}
+
+// entries -> unique entries: 128-bit hash of the key bytes, stable LSD radix
+// sort by (h1, h2), groups where the hash changes (neighbours with equal
+// hashes compared byte for byte: a collision redoes the merge with another
+// seed), one thread per group sums counts and takes the min first.  The
+// entries stay in hash order (general_finish puts them in Map order).
+kmer_status general_merge(kmer_ctx *c) {
+    if (c->gm_merged || c->gm_n == 0) {
+        c->gm_merged = true;
+        return KMER_OK;
+    }
+    hipStream_t s = c->stream;
+    const uint64_t n = c->gm_n, k = c->p.k;
+    if (n >= 0xFFFFFFFFull) return fail(c, KMER_E_TOO_MANY_KEYS, "more than 2^32 - 1 general-path entries");
+    HIPCHK(c, c->gm_h1.ensure(n, s));
+    HIPCHK(c, c->gm_h2.ensure(n, s));
+    HIPCHK(c, c->gm_h1b.ensure(n, s));
+    HIPCHK(c, c->gm_h2b.ensure(n, s));
+    HIPCHK(c, c->gm_idx.ensure(n, s));
+    HIPCHK(c, c->gm_idx2.ensure(n, s));
+    HIPCHK(c, c->gm_head.ensure(n, s));
+    HIPCHK(c, c->gm_gid.ensure(n, s));
+    HIPCHK(c, c->gm_start.ensure(n + 1, s));
+    HIPCHK(c, c->gm_flag.ensure(1, s));
+    for (uint64_t attempt = 0; attempt < 4; ++attempt) {
+        HIPCHK(c, hipMemsetAsync(c->gm_flag.p, 0, sizeof(unsigned int), s));
+        HIPCHK(c, launch_gen_hash(c->gm_keys.p, n, (uint32_t)k, 0x6A09E667F3BCC909ull + attempt, c->gm_h1.p, c->gm_h2.p,
+                                  c->gm_idx.p, s));
+        ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, c->gm_h2.p, c->gm_h2b.p, c->gm_idx.p, c->gm_idx2.p, (size_t)n,
+                                                 0, 64, s));
+        HIPCHK(c, launch_gather_u64(c->gm_h1.p, c->gm_idx2.p, n, c->gm_h1b.p, s));
+        ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, c->gm_h1b.p, c->gm_h1.p, c->gm_idx2.p, c->gm_idx.p, (size_t)n,
+                                                 0, 64, s));
+        HIPCHK(c, launch_gather_u64(c->gm_h2.p, c->gm_idx.p, n, c->gm_h2b.p, s));   // (h2 of each sorted entry)
+        HIPCHK(c, launch_gen_heads(c->gm_h1.p, c->gm_h2b.p, c->gm_idx.p, n, c->gm_keys.p, (uint32_t)k, c->gm_head.p,
+                                   c->gm_flag.p, s));
+        ROCPRIM_RUN(c, rocprim::inclusive_scan(t, b, c->gm_head.p, c->gm_gid.p, (size_t)n, rocprim::plus<uint32_t>(), s));
+        uint32_t hv[2] = {0, 0};
+        HIPCHK(c, hipMemcpyAsync(&hv[0], c->gm_flag.p, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(&hv[1], c->gm_gid.p + n - 1, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        if (hv[0]) continue;                       // a hash collision: another seed
+        const uint64_t ng = hv[1];
+        HIPCHK(c, c->gm_keys2.ensure(ng * k, s));
+        HIPCHK(c, c->gm_cnt2.ensure(ng, s));
+        HIPCHK(c, c->gm_first2.ensure(ng, s));
+        HIPCHK(c, launch_gen_starts(c->gm_head.p, c->gm_gid.p, n, c->gm_start.p, s));
+        HIPCHK(c, launch_gen_reduce(c->gm_start.p, ng, c->gm_idx.p, c->gm_keys.p, c->gm_cnt.p, c->gm_first.p,
+                                    (uint32_t)k, c->gm_keys2.p, c->gm_cnt2.p, c->gm_first2.p, s));
+        std::swap(c->gm_keys, c->gm_keys2);
+        std::swap(c->gm_cnt, c->gm_cnt2);
+        std::swap(c->gm_first, c->gm_first2);
+        c->gm_n = ng;
+        c->gm_merged = true;
+        if (c->p.max_keys && ng + c->exotic.size() > c->p.max_keys)
+            return fail(c, KMER_E_TOO_MANY_KEYS, "more distinct keys than max_keys (reference Map limit)");
+        return KMER_OK;
+    }
+    return fail(c, KMER_E_DEVICE, "general-path key hashes kept colliding");
+}
+
+// merged entries in first-occurrence (Map) order -> the context's result arrays.
+// Host records of k bytes (imported from other ranks, or folded by an earlier
+// kmer_records_export) join the entries first, so a key never appears twice.
+kmer_status general_finish(kmer_ctx *c) {
+    const uint64_t k = c->p.k;
+    if (!c->exotic.empty()) {
+        std::vector<char> hk;
+        std::vector<uint64_t> hc, hf;
+        for (auto it = c->exotic.begin(); it != c->exotic.end();) {
+            if (it->first.size() != k) {
+                ++it;
+                continue;
+            }
+            hk.insert(hk.end(), it->first.begin(), it->first.end());
+            hc.push_back(it->second.count);
+            hf.push_back(it->second.first);
+            it = c->exotic.erase(it);
+        }
+        const uint64_t m = hc.size(), n0 = c->gm_n;
+        if (m) {
+            hipStream_t s = c->stream;
+            HIPCHK(c, c->gm_keys.ensure((n0 + m) * k, s, true, n0 * k));
+            HIPCHK(c, c->gm_cnt.ensure(n0 + m, s, true, n0));
+            HIPCHK(c, c->gm_first.ensure(n0 + m, s, true, n0));
+            kmer_status st = upload(c, c->gm_keys.p + n0 * k, hk.data(), m * k, s);
+            if (!st) st = upload(c, c->gm_cnt.p + n0, hc.data(), m * 8, s);
+            if (!st) st = upload(c, c->gm_first.p + n0, hf.data(), m * 8, s);
+            if (st) return st;
+            c->gm_n = n0 + m;
+            c->gm_merged = false;
+        }
+    }
+    kmer_status st = general_merge(c);
+    if (st) return st;
+    const uint64_t n = c->gm_n;
+    c->n_out = n;
+    if (n == 0) return KMER_OK;
+    hipStream_t s = c->stream;
+    HIPCHK(c, c->xord2.ensure(n, s));
+    HIPCHK(c, c->ridx2.ensure(n, s));
+    HIPCHK(c, c->keys_out.ensure(n * k, s));
+    HIPCHK(c, c->cnt_out.ensure(n, s));
+    HIPCHK(c, c->first.ensure(n, s));
+    rocprim::counting_iterator<uint32_t> iota(0u);
+    ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, c->gm_first.p, c->xord2.p, iota, c->ridx2.p, (size_t)n, 0, 64, s));
+    HIPCHK(c, launch_permute_rows(c->gm_keys.p, c->gm_cnt.p, c->gm_first.p, c->ridx2.p, n, (uint32_t)k, c->keys_out.p,
+                                  c->cnt_out.p, c->first.p, s));
+    c->gm_n = 0;
+    return KMER_OK;
+}
+
+// the session's entries folded into the host record map (kmer_records_export
+// before a multi-rank gather: the ranks' general-path keys travel as records)
+kmer_status general_to_host(kmer_ctx *c) {
+    kmer_status st = general_merge(c);
+    if (st) return st;
+    const uint64_t n = c->gm_n, k = c->p.k;
+    if (n == 0) return KMER_OK;
+    std::vector<char> keys(n * k);
+    std::vector<uint64_t> cnt(n), fst(n);
+    hipStream_t s = c->stream;
+    HIPCHK(c, hipMemcpyAsync(keys.data(), c->gm_keys.p, n * k, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(cnt.data(), c->gm_cnt.p, n * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(fst.data(), c->gm_first.p, n * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    for (uint64_t i = 0; i < n; ++i) {
+        std::string key(keys.data() + i * k, k);
+        auto it = c->exotic.find(key);
+        if (it == c->exotic.end()) {
+            c->exotic.emplace(std::move(key), Ent{cnt[i], fst[i]});
+        } else {
+            it->second.count += cnt[i];
+            it->second.first = std::min(it->second.first, fst[i]);
+        }
+    }
+    c->gm_n = 0;
+    return KMER_OK;
+}
+
 // ordered device entries + host records -> host result
 kmer_status build_result(kmer_ctx *c, uint64_t lines, kmer_result **out) {
     kmer_result *r = new (std::nothrow) kmer_result();
@@ -336,6 +499,9 @@ kmer_status finish(kmer_ctx *c, kmer_result **out) {
         c->n_out = nu;
     } else if (c->mode == MODE_TABLE) {
         st = table_finish(c);
+        if (st) return st;
+    } else if (c->mode == MODE_GENERAL && c->gm_on) {
+        st = general_finish(c);
         if (st) return st;
     }
     HIPCHK(c, hipEventRecord(c->ev3, c->stream));

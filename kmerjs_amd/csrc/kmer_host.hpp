@@ -262,6 +262,15 @@ struct kmer_ctx {
     // devices[0] (allocated through child 0)
     std::vector<kmer_ctx *> group;
     uint32_t peer_staged = 0;      // device pairs of the group without peer access (copies staged by the runtime)
+    // general path, device merge (step 1, kmer_finish.hip general_merge):
+    // session entries -- key bytes at stride k, counts, first-occurrence keys
+    bool gm_on = false;
+    bool gm_merged = true;         // entries unique (merged since the last append)
+    uint64_t gm_n = 0;
+    DBuf<uint8_t> gm_keys, gm_keys2;
+    DBuf<uint64_t> gm_cnt, gm_cnt2, gm_first, gm_first2, gm_h1, gm_h2, gm_h1b, gm_h2b;
+    DBuf<uint32_t> gm_idx, gm_idx2, gm_head, gm_gid, gm_start;
+    DBuf<unsigned int> gm_flag;
     DBuf<uint64_t> gkeys, gkeys2;
     DBuf<Agg> gvals, gvals2;
     double t_ms[7] = {};           // table phase times since the reset: lines, hist1, scatter1, hist2, scatter2, final, fasta
@@ -374,6 +383,10 @@ struct GroupSrc {
 // ---- functions shared between the host translation units ----
 kmer_status ensure_tiles(kmer_ctx *c, uint64_t n_tiles);
 kmer_status upload(kmer_ctx *c, void *dst, const void *src, size_t n, hipStream_t s);
+kmer_status general_append(kmer_ctx *c, const uint8_t *d, uint64_t nrec, hipStream_t s);
+kmer_status general_merge(kmer_ctx *c);
+kmer_status general_finish(kmer_ctx *c);
+kmer_status general_to_host(kmer_ctx *c);
 kmer_status ensure_ovf(kmer_ctx *c, uint64_t n, hipStream_t s);
 kmer_status ensure_records(kmer_ctx *c, uint64_t n);
 kmer_status drain_records(kmer_ctx *c, const uint8_t *d_data, uint64_t n, hipStream_t s);

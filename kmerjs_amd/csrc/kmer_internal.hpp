@@ -275,6 +275,23 @@ struct TileArgs {
     unsigned int *err;
 };
 
+// General path with the device merge (step 1): sequence lines from
+// chunk_lines, their windows flattened (wbase: exclusive scan of 2W per line)
+struct GenWinArgs {
+    const uint8_t *data;
+    uint64_t len;
+    const SeqLine *lines;
+    const uint64_t *wbase;
+    uint64_t n_lines, total;       // lines, windows of both strands
+    uint32_t k, plen, pbits;
+    const uint8_t *P, *RP;         // the prefix and its reverse complement (device)
+    Record *recs;
+    unsigned long long *rec_count;
+    uint64_t rec_cap;
+    unsigned int *err;
+};
+hipError_t launch_gen_windows(const GenWinArgs &a, hipStream_t s);
+
 struct WindowArgs {
     const uint8_t *data;
     const SeqLine *lines;
@@ -566,6 +583,16 @@ hipError_t launch_fa_write(const uint8_t *data, uint64_t len, uint32_t n_tiles, 
                            hipStream_t s);
 hipError_t launch_synth_fastq(uint8_t *out, uint64_t seed, uint64_t first_read, uint64_t n_reads,
                               hipStream_t s);
+hipError_t launch_gen_append(const Record *recs, uint64_t n, const uint8_t *data, uint32_t k, uint8_t *keys,
+                             uint64_t *cnt, uint64_t *first, hipStream_t s);
+hipError_t launch_gen_hash(const uint8_t *keys, uint64_t n, uint32_t k, uint64_t seed, uint64_t *h1, uint64_t *h2,
+                           uint32_t *idx, hipStream_t s);
+hipError_t launch_gen_heads(const uint64_t *h1, const uint64_t *h2, const uint32_t *idx, uint64_t n, const uint8_t *keys,
+                            uint32_t k, uint32_t *head, unsigned int *collide, hipStream_t s);
+hipError_t launch_gen_starts(const uint32_t *head, const uint32_t *gid, uint64_t n, uint32_t *start, hipStream_t s);
+hipError_t launch_gen_reduce(const uint32_t *start, uint64_t ng, const uint32_t *idx, const uint8_t *keys,
+                             const uint64_t *cnt, const uint64_t *first, uint32_t k, uint8_t *okeys, uint64_t *ocnt,
+                             uint64_t *ofirst, hipStream_t s);
 hipError_t launch_permute_rows(const uint8_t *keys, const uint64_t *cnt, const uint64_t *first, const uint32_t *idx,
                                uint64_t n, uint32_t k, uint8_t *okeys, uint64_t *ocnt, uint64_t *ofirst,
                                hipStream_t s);

@@ -866,7 +866,26 @@ __device__ __forceinline__ uint32_t plane_match(uint32_t L0, uint32_t H0, uint32
     return acc;
 }
 
-template <bool FULL5, bool WIDE>
+// The reference's default prefix, ATGAC (lib/kmers.js:67, BASELINE C2 / C4),
+// compiled in: its plane masks are constants, so the compiler folds the XORs
+// into the AND chains (v_bitop3 with the complements absorbed) -- about 40 VALU
+// fewer per thread.  Bit 4i .. 4i+3 of the word: kl, kh, rl, rh of base i
+// (1 = the mask is ~0, i.e. the base's plane bit is 0).
+__host__ __device__ constexpr uint32_t plane_masks_const(const char *p, const char *r) {
+    uint32_t m = 0;
+    for (int i = 0; i < 5; ++i) {
+        const uint32_t cp = (((uint32_t)p[i] >> 1) & 1u) | ((((uint32_t)p[i] >> 2) & 1u) << 1);
+        const uint32_t cr = (((uint32_t)r[i] >> 1) & 1u) | ((((uint32_t)r[i] >> 2) & 1u) << 1);
+        m |= ((cp & 1u) ? 0u : 1u) << (4 * i);
+        m |= ((cp & 2u) ? 0u : 1u) << (4 * i + 1);
+        m |= ((cr & 1u) ? 0u : 1u) << (4 * i + 2);
+        m |= ((cr & 2u) ? 0u : 1u) << (4 * i + 3);
+    }
+    return m;
+}
+constexpr uint32_t PM_ATGAC = plane_masks_const("ATGAC", "GTCAT");
+
+template <bool FULL5, bool WIDE, uint32_t PM = 0>
 __global__ __launch_bounds__(TPB) void scan_planes_kernel(ScanArgs a, PlaneArgs pa) {
     __shared__ __attribute__((aligned(16))) uint8_t buf[BUFSZ];
     __shared__ ScanShared sh;
@@ -984,6 +1003,21 @@ __global__ __launch_bounds__(TPB) void scan_planes_kernel(ScanArgs a, PlaneArgs 
     }
     uint32_t mf[2], mr[2];
     const uint32_t pb = FULL5 ? 5u : pa.pb;
+    uint32_t kl[5], kh[5], rl[5], rh[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        if constexpr (PM != 0) {
+            kl[i] = ((PM >> (4 * i)) & 1u) ? ~0u : 0u;
+            kh[i] = ((PM >> (4 * i + 1)) & 1u) ? ~0u : 0u;
+            rl[i] = ((PM >> (4 * i + 2)) & 1u) ? ~0u : 0u;
+            rh[i] = ((PM >> (4 * i + 3)) & 1u) ? ~0u : 0u;
+        } else {
+            kl[i] = pa.kl[i];
+            kh[i] = pa.kh[i];
+            rl[i] = pa.rl[i];
+            rh[i] = pa.rh[i];
+        }
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         uint32_t SL[5], SH[5];
@@ -994,8 +1028,8 @@ __global__ __launch_bounds__(TPB) void scan_planes_kernel(ScanArgs a, PlaneArgs 
             SL[i] = __builtin_amdgcn_alignbit(L[h + 1], L[h], i);
             SH[i] = __builtin_amdgcn_alignbit(H[h + 1], H[h], i);
         }
-        mf[h] = plane_match(L[h], H[h], L[h + 1], H[h + 1], pa.kl, pa.kh, pb, SL, SH);
-        mr[h] = plane_match(L[h], H[h], L[h + 1], H[h + 1], pa.rl, pa.rh, pb, SL, SH);
+        mf[h] = plane_match(L[h], H[h], L[h + 1], H[h + 1], kl, kh, pb, SL, SH);
+        mr[h] = plane_match(L[h], H[h], L[h + 1], H[h + 1], rl, rh, pb, SL, SH);
     }
     if (a.k < a.plen || (KH_ABLATE(a) & 1u)) mf[0] = mf[1] = mr[0] = mr[1] = 0;
 
@@ -1523,6 +1557,208 @@ __global__ __launch_bounds__(256) void windows_kernel(WindowArgs a) {
                 }
             }
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// General path, device merge (step 1: every record is a key of exactly k
+// bytes; any k, any prefix bytes).  A chunk's records become session entries
+// (key bytes, count 1, first-occurrence key); a merge groups equal keys by a
+// 128-bit hash of their bytes (radix sorts on the device), checks the bytes of
+// every pair of neighbours with equal hashes (a collision is reported, never
+// merged), and reduces each group to (key, count sum, min first).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void gen_append_kernel(const Record *recs, uint64_t n, const uint8_t *data,
+                                                         uint32_t k, uint8_t *keys, uint64_t *cnt, uint64_t *first) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const Record r = recs[i];
+        uint8_t *o = keys + i * k;
+        const uint8_t *src = data + r.pos;
+        if (r.strand) {
+            for (uint32_t b = 0; b < k; ++b) o[b] = comp_byte(src[k - 1 - b]);
+        } else {
+            for (uint32_t b = 0; b < k; ++b) o[b] = src[b];
+        }
+        cnt[i] = 1;
+        first[i] = r.order;
+    }
+}
+
+// Windows of the general path (step 1, any k, any prefix bytes), one lane per
+// window position of the flattened window space: each wave takes an equal
+// contiguous range of positions (Σ W over the chunk's sequence lines), finds
+// its first line by a binary search of wbase, then walks 64 positions per
+// step -- lane j of a step holds the start of line li + j, and every lane finds
+// its own line among those 64 by a 6-step shuffle search (lines without
+// windows take no positions).  A lane tests its position s on both strands:
+// forward iff the line's bytes at s are P, reverse iff the bytes at s + k - |P|
+// are rc(P) (the reverse strand's window L - k - s, lib/kmers.js:88-100, 153).
+// Accepted windows are queued per wave in LDS and written as records with one
+// atomic per 128 records.
+__device__ __forceinline__ bool gen_match(const uint8_t *p, const uint8_t *P, uint32_t plen) {
+    bool ok = true;
+    for (uint32_t b = 0; b < plen && ok; ++b) ok = p[b] == P[b];
+    return ok;
+}
+
+constexpr uint32_t GW_Q = 256;                   // records queued per wave
+
+__global__ __launch_bounds__(256) void gen_windows_kernel(GenWinArgs a) {
+    __shared__ Record q[4][GW_Q];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    Record *wq = q[wv];
+    const uint64_t npos = a.total / 2;
+    const uint64_t nw = (uint64_t)gridDim.x * 4, gw = (uint64_t)blockIdx.x * 4 + wv;
+    uint64_t f = npos * gw / nw;
+    const uint64_t fend = npos * (gw + 1) / nw;
+    if (f >= fend) return;
+    const uint32_t k = a.k, plen = a.plen;
+    // first line: the last li with wbase[li] / 2 <= f
+    uint64_t lo = 0, hi = a.n_lines;                 // invariant: wbase[lo] / 2 <= f < wbase[hi] / 2 (hi: +inf)
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) / 2;
+        if (a.wbase[mid] / 2 <= f) lo = mid; else hi = mid;
+    }
+    uint64_t li = lo;
+    uint32_t cnt = 0;
+    auto flush = [&]() {
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(a.rec_count, (unsigned long long)cnt);
+        base = __shfl(base, 0);
+        for (uint32_t i = lane; i < cnt; i += 64) {
+            if (base + i < a.rec_cap) a.recs[base + i] = wq[i];
+            else atomicOr(a.err, ERR_REC_OVERFLOW);
+        }
+        cnt = 0;
+    };
+    while (f < fend) {
+        // lines li .. li + 63: starts (flat positions) and their end
+        const uint64_t lj = li + lane;
+        const bool lin = lj < a.n_lines;
+        const uint64_t B = lin ? a.wbase[lj] / 2 : ~0ull;
+        SeqLine sl = {0, 0, 0};
+        if (lin) sl = a.lines[lj];
+        const uint64_t Wl = sl.len >= k ? sl.len - k + 1 : 0;
+        const uint64_t E = __shfl(lin ? B + Wl : ~0ull, 63);   // end of line li + 63 (covered range)
+        const uint64_t g = f + lane;
+        const bool act = g < fend && g < E;
+        // lane's line: the last j with B_j <= g (6 shuffle steps)
+        uint32_t j = 0;
+#pragma unroll
+        for (uint32_t st = 32; st >= 1; st >>= 1) {
+            const uint64_t bj = __shfl(B, (int)(j + st));
+            if (j + st < 64 && bj <= g) j += st;
+        }
+        const uint64_t start = __shfl(sl.start, (int)j), L = __shfl(sl.len, (int)j), lidx = __shfl(sl.line_index, (int)j);
+        const uint64_t s = g - __shfl(B, (int)j);
+        bool fw = false, rv = false;
+        if (act) {
+            const uint8_t *line = a.data + start;
+            fw = gen_match(line + s, a.P, plen);
+            rv = gen_match(line + s + k - plen, a.RP, plen);
+        }
+        const unsigned long long mf = __ballot(fw), mr = __ballot(rv);
+        const uint32_t n = (uint32_t)(__popcll(mf) + __popcll(mr));
+        if (cnt + n > GW_Q) flush();
+        const unsigned long long below = (1ull << lane) - 1ull;
+        const uint64_t lo_key = lidx << (a.pbits + 1);
+        if (fw) {
+            Record r;
+            r.order = lo_key | s;
+            r.pos = start + s;
+            r.len = k;
+            r.strand = 0;
+            wq[cnt + __popcll(mf & below)] = r;
+        }
+        if (rv) {
+            Record r;
+            r.order = lo_key | (1ull << a.pbits) | (L - k - s);
+            r.pos = start + s;
+            r.len = k;
+            r.strand = 1;
+            wq[cnt + __popcll(mf) + __popcll(mr & below)] = r;
+        }
+        cnt += n;
+        // next step: 64 positions on, from the line of the last covered lane
+        const uint64_t adv = E - f < 64 ? E - f : 64;
+        const uint32_t jl = (uint32_t)__shfl((int)j, (int)(adv - 1));
+        f += adv;
+        li += adv < 64 ? 64 : jl;
+    }
+    if (cnt) flush();
+}
+
+__device__ __forceinline__ uint64_t gen_mix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// two independent 64-bit hashes of each k-byte key (8 bytes per step)
+__global__ __launch_bounds__(256) void gen_hash_kernel(const uint8_t *keys, uint64_t n, uint32_t k, uint64_t seed,
+                                                       uint64_t *h1, uint64_t *h2, uint32_t *idx) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t *p = keys + i * k;
+        uint64_t a = gen_mix(seed ^ ((uint64_t)k * 0x9E3779B97F4A7C15ull)), b = gen_mix(~seed + k);
+        for (uint32_t j = 0; j < k; j += 8) {
+            uint64_t w = 0;
+            const uint32_t m = k - j < 8 ? k - j : 8;
+            for (uint32_t t = 0; t < m; ++t) w |= (uint64_t)p[j + t] << (8 * t);
+            a = (a ^ w) * 0xFF51AFD7ED558CCDull;
+            a ^= a >> 32;
+            b = (b + w) * 0xC4CEB9FE1A85EC53ull;
+            b ^= b >> 29;
+        }
+        h1[i] = gen_mix(a);
+        h2[i] = gen_mix(b ^ 0x2545F4914F6CDD1Dull);
+        idx[i] = (uint32_t)i;
+    }
+}
+
+// after the sort by (h1, h2): a group starts where the hash changes; equal
+// hashes with different bytes are a collision (flagged, the caller redoes the
+// merge with another seed).  Heads record their sorted position by group.
+__global__ __launch_bounds__(256) void gen_heads_kernel(const uint64_t *h1, const uint64_t *h2, const uint32_t *idx,
+                                                        uint64_t n, const uint8_t *keys, uint32_t k, uint32_t *head,
+                                                        unsigned int *collide) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        bool same = i > 0 && h1[i] == h1[i - 1] && h2[i] == h2[i - 1];
+        if (same) {
+            const uint8_t *x = keys + (uint64_t)idx[i] * k, *y = keys + (uint64_t)idx[i - 1] * k;
+            bool eq = true;
+            for (uint32_t b = 0; b < k && eq; ++b) eq = x[b] == y[b];
+            if (!eq) atomicOr(collide, 1u);
+        }
+        head[i] = same ? 0u : 1u;
+    }
+}
+
+// groups: gid (inclusive scan of the heads, 1-based) -> start of each group
+__global__ __launch_bounds__(256) void gen_starts_kernel(const uint32_t *head, const uint32_t *gid, uint64_t n,
+                                                         uint32_t *start) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        if (head[i]) start[gid[i] - 1] = (uint32_t)i;
+        if (i == n - 1) start[gid[i]] = (uint32_t)n;
+    }
+}
+
+// one thread per group: its key (the head's bytes), count sum, min first
+__global__ __launch_bounds__(256) void gen_reduce_kernel(const uint32_t *start, uint64_t ng, const uint32_t *idx,
+                                                         const uint8_t *keys, const uint64_t *cnt, const uint64_t *first,
+                                                         uint32_t k, uint8_t *okeys, uint64_t *ocnt, uint64_t *ofirst) {
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ng; g += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t s0 = start[g], s1 = start[g + 1];
+        uint64_t c = 0, f = ~0ull;
+        for (uint32_t i = s0; i < s1; ++i) {
+            const uint32_t j = idx[i];
+            c += cnt[j];
+            f = min(f, first[j]);
+        }
+        const uint8_t *src = keys + (uint64_t)idx[s0] * k;
+        uint8_t *o = okeys + g * k;
+        for (uint32_t b = 0; b < k; ++b) o[b] = src[b];
+        ocnt[g] = c;
+        ofirst[g] = f;
     }
 }
 
@@ -2674,6 +2910,15 @@ hipError_t launch_lines(const TileArgs &a, bool lookback, hipStream_t s) {
 
 hipError_t launch_scan_planes(const ScanArgs &a, const PlaneArgs &pa, hipStream_t s) {
     const dim3 g(a.n_tiles);
+    uint32_t pm = 0;                         // the planes' masks as plane_masks_const encodes them
+    for (int i = 0; i < 5; ++i)
+        pm |= (pa.kl[i] ? 1u : 0u) << (4 * i) | (pa.kh[i] ? 1u : 0u) << (4 * i + 1) |
+              (pa.rl[i] ? 1u : 0u) << (4 * i + 2) | (pa.rh[i] ? 1u : 0u) << (4 * i + 3);
+    if (pa.pb >= 5 && pm == PM_ATGAC) {     // the default prefix, compiled in
+        if (a.k > 32) hipLaunchKernelGGL((scan_planes_kernel<true, true, PM_ATGAC>), g, dim3(TPB), 0, s, a, pa);
+        else hipLaunchKernelGGL((scan_planes_kernel<true, false, PM_ATGAC>), g, dim3(TPB), 0, s, a, pa);
+        return hipGetLastError();
+    }
     if (a.k > 32) {
         if (pa.pb >= 5) hipLaunchKernelGGL((scan_planes_kernel<true, true>), g, dim3(TPB), 0, s, a, pa);
         else hipLaunchKernelGGL((scan_planes_kernel<false, true>), g, dim3(TPB), 0, s, a, pa);
@@ -2733,6 +2978,49 @@ static uint32_t grid_for(uint64_t n) {
     uint64_t blocks = (n + 255) / 256;
     if (blocks > 16384) blocks = 16384;
     return (uint32_t)(blocks ? blocks : 1);
+}
+
+hipError_t launch_gen_windows(const GenWinArgs &a, hipStream_t s) {
+    if (a.total == 0) return hipSuccess;
+    const uint64_t waves = std::min<uint64_t>(65536, (a.total / 2 + 255) / 256);   // >= 256 positions per wave
+    hipLaunchKernelGGL(gen_windows_kernel, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_append(const Record *recs, uint64_t n, const uint8_t *data, uint32_t k, uint8_t *keys,
+                             uint64_t *cnt, uint64_t *first, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(gen_append_kernel, dim3(grid_for(n)), dim3(256), 0, s, recs, n, data, k, keys, cnt, first);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_hash(const uint8_t *keys, uint64_t n, uint32_t k, uint64_t seed, uint64_t *h1, uint64_t *h2,
+                           uint32_t *idx, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(gen_hash_kernel, dim3(grid_for(n)), dim3(256), 0, s, keys, n, k, seed, h1, h2, idx);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_heads(const uint64_t *h1, const uint64_t *h2, const uint32_t *idx, uint64_t n, const uint8_t *keys,
+                            uint32_t k, uint32_t *head, unsigned int *collide, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(gen_heads_kernel, dim3(grid_for(n)), dim3(256), 0, s, h1, h2, idx, n, keys, k, head, collide);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_starts(const uint32_t *head, const uint32_t *gid, uint64_t n, uint32_t *start, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(gen_starts_kernel, dim3(grid_for(n)), dim3(256), 0, s, head, gid, n, start);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_reduce(const uint32_t *start, uint64_t ng, const uint32_t *idx, const uint8_t *keys,
+                             const uint64_t *cnt, const uint64_t *first, uint32_t k, uint8_t *okeys, uint64_t *ocnt,
+                             uint64_t *ofirst, hipStream_t s) {
+    if (ng == 0) return hipSuccess;
+    hipLaunchKernelGGL(gen_reduce_kernel, dim3(grid_for(ng)), dim3(256), 0, s, start, ng, idx, keys, cnt, first, k,
+                       okeys, ocnt, ofirst);
+    return hipGetLastError();
 }
 
 hipError_t launch_cross_scatter(const uint32_t *slot, const uint64_t *ord, const uint64_t *key, uint64_t n,

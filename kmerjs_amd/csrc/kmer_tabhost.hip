@@ -208,16 +208,7 @@ kmer_status table_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_t
         a.len = len;
         a.lines = plines;
         a.n_lines = n_items;
-        uint64_t nwg0 = std::min<uint64_t>(8192, (n_items + 63) / 64);
-        // long lines cut into pieces (contigs, C5): every item is ~4,096 windows,
-        // so 64 items per workgroup made runs of ~256 keys per partition -- too
-        // small for fixed runs (16 % filler) and for the scatter's writes.  Fewer,
-        // larger shares instead: ~2 M windows per workgroup (>= 2 per CU), which
-        // puts the fixed runs' filler near C3's 6 %.  (KMERHIP_TAB_NWG=items:
-        // the old sizing, A/B experiments.)
-        const char *nw = exp_env("KMERHIP_TAB_NWG");
-        if (plines == c->tpieces.p && !(nw && strcmp(nw, "items") == 0))
-            nwg0 = std::min<uint64_t>(nwg0, std::max<uint64_t>(2ull * std::max(c->n_cu, 1), len >> 21));
+        const uint64_t nwg0 = std::min<uint64_t>(8192, (n_items + 63) / 64);
         a.lpw = (n_items + nwg0 - 1) / nwg0;
         a.nwg = (uint32_t)((n_items + a.lpw - 1) / a.lpw);
         a.k = c->p.k;
