@@ -1568,36 +1568,53 @@ __global__ __launch_bounds__(256) void windows_kernel(WindowArgs a) {
 // every pair of neighbours with equal hashes (a collision is reported, never
 // merged), and reduces each group to (key, count sum, min first).
 // ---------------------------------------------------------------------------
+// (one wave per record: lanes copy consecutive bytes -- the keys are >= 32
+// bytes on this path -- so loads and stores stay coalesced)
 __global__ __launch_bounds__(256) void gen_append_kernel(const Record *recs, uint64_t n, const uint8_t *data,
                                                          uint32_t k, uint8_t *keys, uint64_t *cnt, uint64_t *first) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += nw) {
         const Record r = recs[i];
         uint8_t *o = keys + i * k;
         const uint8_t *src = data + r.pos;
-        if (r.strand) {
-            for (uint32_t b = 0; b < k; ++b) o[b] = comp_byte(src[k - 1 - b]);
-        } else {
-            for (uint32_t b = 0; b < k; ++b) o[b] = src[b];
+        for (uint32_t b = lane; b < k; b += 64) o[b] = r.strand ? comp_byte(src[k - 1 - b]) : src[b];
+        if (lane == 0) {
+            cnt[i] = 1;
+            first[i] = r.order;
         }
-        cnt[i] = 1;
-        first[i] = r.order;
     }
 }
 
 // Windows of the general path (step 1, any k, any prefix bytes), one lane per
 // window position of the flattened window space: each wave takes an equal
 // contiguous range of positions (Σ W over the chunk's sequence lines), finds
-// its first line by a binary search of wbase, then walks 64 positions per
-// step -- lane j of a step holds the start of line li + j, and every lane finds
-// its own line among those 64 by a 6-step shuffle search (lines without
-// windows take no positions).  A lane tests its position s on both strands:
-// forward iff the line's bytes at s are P, reverse iff the bytes at s + k - |P|
-// are rc(P) (the reverse strand's window L - k - s, lib/kmers.js:88-100, 153).
-// Accepted windows are queued per wave in LDS and written as records with one
-// atomic per 128 records.
-__device__ __forceinline__ bool gen_match(const uint8_t *p, const uint8_t *P, uint32_t plen) {
+// its first line by a binary search of wbase, then loads the descriptors of
+// 64 lines at a time (lane j: line li + j) and walks every position those
+// lines cover, 64 per step: each lane finds its own line among the 64 by a
+// 6-step shuffle search (lines without windows take no positions).  A lane
+// tests its position s on both strands: forward iff the line's bytes at s are
+// P, reverse iff the bytes at s + k - |P| are rc(P) (the reverse strand's
+// window L - k - s, lib/kmers.js:88-100, 153).  The first 8 bytes of both
+// tests are loaded at once (no chain of dependent byte loads) and compared
+// with P / rc(P) held in registers.  Accepted windows are queued per wave in
+// LDS and written as records with one atomic per flush.
+__device__ __forceinline__ uint64_t gen_load8(const uint8_t *p, uint32_t n) {
+    uint64_t w = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < 8; ++t)
+        if (t < n) w |= (uint64_t)p[t] << (8 * t);
+    return w;
+}
+
+__device__ __forceinline__ bool gen_match(const uint8_t *p, const uint8_t *P, uint32_t plen, uint64_t P8) {
+    const uint32_t n0 = plen < 8 ? plen : 8;
+    if (gen_load8(p, n0) != P8) return false;
     bool ok = true;
-    for (uint32_t b = 0; b < plen && ok; ++b) ok = p[b] == P[b];
+    for (uint32_t b = 8; b < plen && ok; b += 8) {
+        const uint32_t n = plen - b < 8 ? plen - b : 8;
+        ok = gen_load8(p + b, n) == gen_load8(P + b, n);
+    }
     return ok;
 }
 
@@ -1613,6 +1630,7 @@ __global__ __launch_bounds__(256) void gen_windows_kernel(GenWinArgs a) {
     const uint64_t fend = npos * (gw + 1) / nw;
     if (f >= fend) return;
     const uint32_t k = a.k, plen = a.plen;
+    const uint64_t P8 = gen_load8(a.P, plen < 8 ? plen : 8), R8 = gen_load8(a.RP, plen < 8 ? plen : 8);
     // first line: the last li with wbase[li] / 2 <= f
     uint64_t lo = 0, hi = a.n_lines;                 // invariant: wbase[lo] / 2 <= f < wbase[hi] / 2 (hi: +inf)
     while (hi - lo > 1) {
@@ -1632,58 +1650,69 @@ __global__ __launch_bounds__(256) void gen_windows_kernel(GenWinArgs a) {
         cnt = 0;
     };
     while (f < fend) {
-        // lines li .. li + 63: starts (flat positions) and their end
+        // lines li .. li + 63: starts (flat positions), descriptors, covered end E
         const uint64_t lj = li + lane;
         const bool lin = lj < a.n_lines;
         const uint64_t B = lin ? a.wbase[lj] / 2 : ~0ull;
         SeqLine sl = {0, 0, 0};
         if (lin) sl = a.lines[lj];
         const uint64_t Wl = sl.len >= k ? sl.len - k + 1 : 0;
-        const uint64_t E = __shfl(lin ? B + Wl : ~0ull, 63);   // end of line li + 63 (covered range)
-        const uint64_t g = f + lane;
-        const bool act = g < fend && g < E;
-        // lane's line: the last j with B_j <= g (6 shuffle steps)
+        const uint64_t E = __shfl(lin ? B + Wl : ~0ull, 63);
+        const uint64_t fe = E < fend ? E : fend;
         uint32_t j = 0;
+        while (f < fe) {
+            const uint64_t g = f + lane;
+            const bool act = g < fe;
+            // lane's line: the last j' >= j (its line is no earlier than the
+            // previous step's) with B_j' <= g, 6 shuffle steps
+            j = 0;
 #pragma unroll
-        for (uint32_t st = 32; st >= 1; st >>= 1) {
-            const uint64_t bj = __shfl(B, (int)(j + st));
-            if (j + st < 64 && bj <= g) j += st;
+            for (uint32_t st = 32; st >= 1; st >>= 1) {
+                const uint64_t bj = __shfl(B, (int)(j + st));
+                if (j + st < 64 && bj <= g) j += st;
+            }
+            const uint64_t start = __shfl(sl.start, (int)j), L = __shfl(sl.len, (int)j),
+                           lidx = __shfl(sl.line_index, (int)j);
+            const uint64_t s = g - __shfl(B, (int)j);
+            bool fw = false, rv = false;
+            if (act) {
+                const uint8_t *line = a.data + start;
+                fw = gen_match(line + s, a.P, plen, P8);
+                rv = gen_match(line + s + k - plen, a.RP, plen, R8);
+            }
+            const unsigned long long mf = __ballot(fw), mr = __ballot(rv);
+            const uint32_t n = (uint32_t)(__popcll(mf) + __popcll(mr));
+            if (n) {
+                if (cnt + n > GW_Q) flush();
+                const unsigned long long below = (1ull << lane) - 1ull;
+                const uint64_t lo_key = lidx << (a.pbits + 1);
+                if (fw) {
+                    Record r;
+                    r.order = lo_key | s;
+                    r.pos = start + s;
+                    r.len = k;
+                    r.strand = 0;
+                    wq[cnt + __popcll(mf & below)] = r;
+                }
+                if (rv) {
+                    Record r;
+                    r.order = lo_key | (1ull << a.pbits) | (L - k - s);
+                    r.pos = start + s;
+                    r.len = k;
+                    r.strand = 1;
+                    wq[cnt + __popcll(mf) + __popcll(mr & below)] = r;
+                }
+                cnt += n;
+            }
+            f += 64;
         }
-        const uint64_t start = __shfl(sl.start, (int)j), L = __shfl(sl.len, (int)j), lidx = __shfl(sl.line_index, (int)j);
-        const uint64_t s = g - __shfl(B, (int)j);
-        bool fw = false, rv = false;
-        if (act) {
-            const uint8_t *line = a.data + start;
-            fw = gen_match(line + s, a.P, plen);
-            rv = gen_match(line + s + k - plen, a.RP, plen);
+        // next 64 lines: from the line holding position f (f >= E: line li + 64 on)
+        if (f >= E) {
+            f = E;
+            li += 64;
+        } else {
+            li += (uint32_t)__shfl((int)j, 63);    // (f >= fend: the loop ends)
         }
-        const unsigned long long mf = __ballot(fw), mr = __ballot(rv);
-        const uint32_t n = (uint32_t)(__popcll(mf) + __popcll(mr));
-        if (cnt + n > GW_Q) flush();
-        const unsigned long long below = (1ull << lane) - 1ull;
-        const uint64_t lo_key = lidx << (a.pbits + 1);
-        if (fw) {
-            Record r;
-            r.order = lo_key | s;
-            r.pos = start + s;
-            r.len = k;
-            r.strand = 0;
-            wq[cnt + __popcll(mf & below)] = r;
-        }
-        if (rv) {
-            Record r;
-            r.order = lo_key | (1ull << a.pbits) | (L - k - s);
-            r.pos = start + s;
-            r.len = k;
-            r.strand = 1;
-            wq[cnt + __popcll(mf) + __popcll(mr & below)] = r;
-        }
-        cnt += n;
-        // next step: 64 positions on, from the line of the last covered lane
-        const uint64_t adv = E - f < 64 ? E - f : 64;
-        const uint32_t jl = (uint32_t)__shfl((int)j, (int)(adv - 1));
-        f += adv;
-        li += adv < 64 ? 64 : jl;
     }
     if (cnt) flush();
 }
@@ -1694,24 +1723,34 @@ __device__ __forceinline__ uint64_t gen_mix(uint64_t z) {
     return z ^ (z >> 31);
 }
 
-// two independent 64-bit hashes of each k-byte key (8 bytes per step)
+// two independent 64-bit hashes of each k-byte key, one wave per key: lane l
+// takes the key's 8-byte words l, l + 64, ...; each word is mixed with its
+// position (so the sums over the lanes are position-sensitive), the mixed
+// words are summed over the wave, and the sums finalised
 __global__ __launch_bounds__(256) void gen_hash_kernel(const uint8_t *keys, uint64_t n, uint32_t k, uint64_t seed,
                                                        uint64_t *h1, uint64_t *h2, uint32_t *idx) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += nw) {
         const uint8_t *p = keys + i * k;
-        uint64_t a = gen_mix(seed ^ ((uint64_t)k * 0x9E3779B97F4A7C15ull)), b = gen_mix(~seed + k);
-        for (uint32_t j = 0; j < k; j += 8) {
+        uint64_t a = 0, b = 0;
+        for (uint32_t j = 8 * lane; j < k; j += 512) {
             uint64_t w = 0;
             const uint32_t m = k - j < 8 ? k - j : 8;
             for (uint32_t t = 0; t < m; ++t) w |= (uint64_t)p[j + t] << (8 * t);
-            a = (a ^ w) * 0xFF51AFD7ED558CCDull;
-            a ^= a >> 32;
-            b = (b + w) * 0xC4CEB9FE1A85EC53ull;
-            b ^= b >> 29;
+            a += gen_mix(w ^ (seed + (uint64_t)j * 0x9E3779B97F4A7C15ull));
+            b += gen_mix((w + 0x632BE59BD9B4E019ull) ^ (~seed + (uint64_t)j * 0xD6E8FEB86659FD93ull));
         }
-        h1[i] = gen_mix(a);
-        h2[i] = gen_mix(b ^ 0x2545F4914F6CDD1Dull);
-        idx[i] = (uint32_t)i;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            a += __shfl_xor(a, d);
+            b += __shfl_xor(b, d);
+        }
+        if (lane == 0) {
+            h1[i] = gen_mix(a ^ k);
+            h2[i] = gen_mix(b + k);
+            idx[i] = (uint32_t)i;
+        }
     }
 }
 
@@ -1742,23 +1781,33 @@ __global__ __launch_bounds__(256) void gen_starts_kernel(const uint32_t *head, c
     }
 }
 
-// one thread per group: its key (the head's bytes), count sum, min first
+// one wave per group: its key (the head's bytes, copied by the lanes), the
+// count sum and the min first (lanes stride over the group's members)
 __global__ __launch_bounds__(256) void gen_reduce_kernel(const uint32_t *start, uint64_t ng, const uint32_t *idx,
                                                          const uint8_t *keys, const uint64_t *cnt, const uint64_t *first,
                                                          uint32_t k, uint8_t *okeys, uint64_t *ocnt, uint64_t *ofirst) {
-    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < ng; g += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    for (uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); g < ng; g += nw) {
         const uint32_t s0 = start[g], s1 = start[g + 1];
         uint64_t c = 0, f = ~0ull;
-        for (uint32_t i = s0; i < s1; ++i) {
+        for (uint32_t i = s0 + lane; i < s1; i += 64) {
             const uint32_t j = idx[i];
             c += cnt[j];
             f = min(f, first[j]);
         }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            c += __shfl_xor(c, d);
+            f = min(f, (uint64_t)__shfl_xor(f, d));
+        }
         const uint8_t *src = keys + (uint64_t)idx[s0] * k;
         uint8_t *o = okeys + g * k;
-        for (uint32_t b = 0; b < k; ++b) o[b] = src[b];
-        ocnt[g] = c;
-        ofirst[g] = f;
+        for (uint32_t b = lane; b < k; b += 64) o[b] = src[b];
+        if (lane == 0) {
+            ocnt[g] = c;
+            ofirst[g] = f;
+        }
     }
 }
 
@@ -2990,14 +3039,14 @@ hipError_t launch_gen_windows(const GenWinArgs &a, hipStream_t s) {
 hipError_t launch_gen_append(const Record *recs, uint64_t n, const uint8_t *data, uint32_t k, uint8_t *keys,
                              uint64_t *cnt, uint64_t *first, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(gen_append_kernel, dim3(grid_for(n)), dim3(256), 0, s, recs, n, data, k, keys, cnt, first);
+    hipLaunchKernelGGL(gen_append_kernel, dim3(grid_for(64 * n)), dim3(256), 0, s, recs, n, data, k, keys, cnt, first);
     return hipGetLastError();
 }
 
 hipError_t launch_gen_hash(const uint8_t *keys, uint64_t n, uint32_t k, uint64_t seed, uint64_t *h1, uint64_t *h2,
                            uint32_t *idx, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(gen_hash_kernel, dim3(grid_for(n)), dim3(256), 0, s, keys, n, k, seed, h1, h2, idx);
+    hipLaunchKernelGGL(gen_hash_kernel, dim3(grid_for(64 * n)), dim3(256), 0, s, keys, n, k, seed, h1, h2, idx);
     return hipGetLastError();
 }
 
@@ -3018,7 +3067,7 @@ hipError_t launch_gen_reduce(const uint32_t *start, uint64_t ng, const uint32_t 
                              const uint64_t *cnt, const uint64_t *first, uint32_t k, uint8_t *okeys, uint64_t *ocnt,
                              uint64_t *ofirst, hipStream_t s) {
     if (ng == 0) return hipSuccess;
-    hipLaunchKernelGGL(gen_reduce_kernel, dim3(grid_for(ng)), dim3(256), 0, s, start, ng, idx, keys, cnt, first, k,
+    hipLaunchKernelGGL(gen_reduce_kernel, dim3(grid_for(64 * ng)), dim3(256), 0, s, start, ng, idx, keys, cnt, first, k,
                        okeys, ocnt, ofirst);
     return hipGetLastError();
 }
