@@ -177,6 +177,84 @@ __device__ __forceinline__ void fa_stage(const uint8_t *data, uint64_t len, int6
     if (tid == 1) buf[FA_TILE] = (uint64_t)(g0 + FA_TILE) < len ? data[g0 + FA_TILE] : (uint8_t)'\n';
 }
 
+// per-byte 0x80 flags of bytes equal to c (ASCII bytes < 0x80)
+__device__ __forceinline__ uint32_t fa_eq(uint32_t x, uint32_t c4) {
+    const uint32_t t = x ^ c4;
+    return ~(t + 0x7F7F7F7Fu) & 0x80808080u;
+}
+// the 0x80 flags of a word as 4 bits
+__device__ __forceinline__ uint32_t fa_bits4(uint32_t f) {
+    return ((f >> 7) & 1u) | ((f >> 14) & 2u) | ((f >> 21) & 4u) | ((f >> 28) & 8u);
+}
+
+// The common case, a block of sequence bytes: no '>' and no '\r' among the
+// thread's 64 bytes, not the chunk's first or last block.  Every line start
+// in it opens a sequence line (h = 0), so '\n' bytes are dropped, except the
+// block's first '\n' when it ends a line that began earlier in state h = 1 (a
+// header's end).  Counting: popcounts.  Writing: each input word compacted by
+// one v_perm (selector from a 16-entry LDS table, by the word's drop mask)
+// into a 64-bit accumulator; whole output words stored, the thread's first and
+// last partial words as bytes.  Returns false when the block is not common.
+__device__ __forceinline__ bool fa_fast_ok(const uint32_t (&w)[17], int64_t g, uint64_t len) {
+    if (g <= 0 || (uint64_t)g + FA_BPT >= len) return false;
+    uint32_t any = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) any |= fa_eq(w[i], 0x3E3E3E3Eu) | fa_eq(w[i], 0x0D0D0D0Du);
+    return any == 0;
+}
+
+template <bool WRITE>
+__device__ __forceinline__ uint64_t fa_fast(const uint32_t (&w)[17], uint8_t prev, uint32_t h_in, uint8_t *out,
+                                            uint64_t o, const uint32_t *sel, uint32_t *nl_out) {
+    uint32_t nlm[16], nl = 0, p0 = 64;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        nlm[i] = fa_bits4(fa_eq(w[i], 0x0A0A0A0Au));
+        nl += __popc(nlm[i]);
+        if (nlm[i] && p0 == 64) p0 = 4 * i + (__ffs(nlm[i]) - 1);
+    }
+    *nl_out = nl;
+    const bool prev_nl = prev == '\n';
+    const bool saw = prev_nl || p0 <= 62;
+    const uint32_t common = 64 - nl, dep = (!prev_nl && nl) ? 1u : 0u;
+    if (WRITE) {
+        if (h_in && dep) nlm[p0 >> 2] &= ~(1u << (p0 & 3));   // a header's closing '\n' stays
+        const uint64_t a_start = (o + 3) & ~3ull;
+        uint64_t acc = 0;
+        uint32_t accn = 0;
+        auto emit_word = [&](uint32_t v) {            // output bytes [o, o + 4) -- whole words past a_start
+            if (o >= a_start) {
+                *(uint32_t *)(out + o) = v;
+            } else {
+                for (uint32_t b = 0; b < 4; ++b) out[o + b] = (uint8_t)(v >> (8 * b));
+            }
+            o += 4;
+        };
+        // (bytes before a_start are written singly, so the accumulator starts
+        // aligned: the first (a_start - o) output bytes go out one by one)
+        uint32_t lead = (uint32_t)(a_start - o);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t v = __builtin_amdgcn_perm(0u, w[i], sel[nlm[i]]);
+            acc |= (uint64_t)v << (8 * accn);
+            accn += 4 - __popc(nlm[i]);
+            while (lead && accn) {                    // (at most 3 bytes, once per thread)
+                out[o++] = (uint8_t)acc;
+                acc >>= 8;
+                --accn;
+                --lead;
+            }
+            if (accn >= 4) {
+                emit_word((uint32_t)acc);
+                acc >>= 32;
+                accn -= 4;
+            }
+        }
+        for (uint32_t b = 0; b < accn; ++b) out[o + b] = (uint8_t)(acc >> (8 * b));
+    }
+    return fa_pack(saw ? 1u : 0u, common, common + dep);
+}
+
 // a thread's 64 bytes + the 4 after them, and the byte before
 __device__ __forceinline__ uint8_t fa_regs(const uint8_t *buf, uint32_t (&w)[17]) {
     const uint4 *src = (const uint4 *)(buf + FA_BPT * threadIdx.x);
@@ -206,7 +284,9 @@ __global__ __launch_bounds__(TPB) void fa_tiles_kernel(const uint8_t *data, uint
     __syncthreads();
     uint32_t nl = 0, w[17];
     const uint8_t prev = fa_regs(buf, w);
-    const uint64_t f = fa_walk<false>(w, prev, g0 + FA_BPT * threadIdx.x, len, 0, nullptr, 0, &nl);
+    const int64_t g = g0 + FA_BPT * threadIdx.x;
+    const uint64_t f = fa_fast_ok(w, g, len) ? fa_fast<false>(w, prev, 0, nullptr, 0, nullptr, &nl)
+                                             : fa_walk<false>(w, prev, g, len, 0, nullptr, 0, &nl);
     uint64_t total;
     uint32_t s = nl;
     for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d);
@@ -229,9 +309,19 @@ __global__ __launch_bounds__(TPB) void fa_write_kernel(const uint8_t *data, uint
                                                       uint8_t *out) {
     __shared__ __attribute__((aligned(16))) uint8_t stage[FA_TILE + 32];
     __shared__ FaShared sh;
+    __shared__ uint32_t sel[16];                 // v_perm selector keeping the bytes whose drop bit is clear
     uint8_t *buf = stage + 16;
     const int64_t g0 = (int64_t)blockIdx.x * FA_TILE;
     fa_stage(data, len, g0, buf);
+    if (threadIdx.x < 16) {
+        uint32_t v = 0x0C0C0C0Cu, n = 0;
+        for (uint32_t b = 0; b < 4; ++b)
+            if (!((threadIdx.x >> b) & 1u)) {
+                v = (v & ~(0xFFu << (8 * n))) | (b << (8 * n));
+                ++n;
+            }
+        sel[threadIdx.x] = v;
+    }
     const FaTile px = tiles_x[blockIdx.x];
     const uint32_t h_tile = px.kind ? px.kind - 1 : 0u;  // (state at the chunk start: no line yet)
     const uint64_t off = px.c0;
@@ -239,13 +329,18 @@ __global__ __launch_bounds__(TPB) void fa_write_kernel(const uint8_t *data, uint
     uint32_t nl = 0, w[17];
     const uint8_t prev = fa_regs(buf, w);
     const int64_t g = g0 + FA_BPT * threadIdx.x;
-    const uint64_t f = fa_walk<false>(w, prev, g, len, 0, nullptr, 0, &nl);
+    const bool fast = fa_fast_ok(w, g, len);
+    const uint64_t f = fast ? fa_fast<false>(w, prev, 0, nullptr, 0, sel, &nl)
+                            : fa_walk<false>(w, prev, g, len, 0, nullptr, 0, &nl);
     uint64_t total;
     const uint64_t ex = fa_block_scan(f, sh.wtot, &total);
     // this thread's incoming state and output offset
     const uint32_t kx = fa_kind(ex);
     const uint32_t h = kx ? kx - 1 : h_tile;
-    (void)fa_walk<true>(w, prev, g, len, h, out, off + fa_c(ex, h_tile), &nl);
+    if (fast)
+        (void)fa_fast<true>(w, prev, h, out, off + fa_c(ex, h_tile), sel, &nl);
+    else
+        (void)fa_walk<true>(w, prev, g, len, h, out, off + fa_c(ex, h_tile), &nl);
 }
 
 }  // namespace

@@ -1660,51 +1660,70 @@ __global__ __launch_bounds__(256) void gen_windows_kernel(GenWinArgs a) {
         const uint64_t E = __shfl(lin ? B + Wl : ~0ull, 63);
         const uint64_t fe = E < fend ? E : fend;
         uint32_t j = 0;
+        constexpr int U = 1;                     // steps per iteration (4: slower, 8.4 vs 6.8 ms at k = 70)
+        const uint32_t n0 = plen < 8 ? plen : 8;
         while (f < fe) {
-            const uint64_t g = f + lane;
-            const bool act = g < fe;
-            // lane's line: the last j' >= j (its line is no earlier than the
-            // previous step's) with B_j' <= g, 6 shuffle steps
-            j = 0;
+            uint64_t st[U], s[U], L[U], lidx[U], wf[U], wr[U];
+            bool act[U];
 #pragma unroll
-            for (uint32_t st = 32; st >= 1; st >>= 1) {
-                const uint64_t bj = __shfl(B, (int)(j + st));
-                if (j + st < 64 && bj <= g) j += st;
-            }
-            const uint64_t start = __shfl(sl.start, (int)j), L = __shfl(sl.len, (int)j),
-                           lidx = __shfl(sl.line_index, (int)j);
-            const uint64_t s = g - __shfl(B, (int)j);
-            bool fw = false, rv = false;
-            if (act) {
-                const uint8_t *line = a.data + start;
-                fw = gen_match(line + s, a.P, plen, P8);
-                rv = gen_match(line + s + k - plen, a.RP, plen, R8);
-            }
-            const unsigned long long mf = __ballot(fw), mr = __ballot(rv);
-            const uint32_t n = (uint32_t)(__popcll(mf) + __popcll(mr));
-            if (n) {
-                if (cnt + n > GW_Q) flush();
-                const unsigned long long below = (1ull << lane) - 1ull;
-                const uint64_t lo_key = lidx << (a.pbits + 1);
-                if (fw) {
-                    Record r;
-                    r.order = lo_key | s;
-                    r.pos = start + s;
-                    r.len = k;
-                    r.strand = 0;
-                    wq[cnt + __popcll(mf & below)] = r;
+            for (int u = 0; u < U; ++u) {
+                const uint64_t g = f + 64 * u + lane;
+                act[u] = g < fe;
+                // lane's line: the last j with B_j <= g, 6 shuffle steps
+                j = 0;
+#pragma unroll
+                for (uint32_t sp = 32; sp >= 1; sp >>= 1) {
+                    const uint64_t bj = __shfl(B, (int)(j + sp));
+                    if (j + sp < 64 && bj <= g) j += sp;
                 }
-                if (rv) {
-                    Record r;
-                    r.order = lo_key | (1ull << a.pbits) | (L - k - s);
-                    r.pos = start + s;
-                    r.len = k;
-                    r.strand = 1;
-                    wq[cnt + __popcll(mf) + __popcll(mr & below)] = r;
-                }
-                cnt += n;
+                st[u] = __shfl(sl.start, (int)j);
+                L[u] = __shfl(sl.len, (int)j);
+                lidx[u] = __shfl(sl.line_index, (int)j);
+                s[u] = g - __shfl(B, (int)j);
             }
-            f += 64;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                wf[u] = wr[u] = ~0ull;
+                if (act[u]) {
+                    const uint8_t *line = a.data + st[u];
+                    wf[u] = gen_load8(line + s[u], n0);
+                    wr[u] = gen_load8(line + s[u] + k - plen, n0);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                bool fw = act[u] && wf[u] == P8, rv = act[u] && wr[u] == R8;
+                if (plen > 8) {                      // (long prefixes: the rest byte for byte)
+                    const uint8_t *line = a.data + st[u];
+                    fw = fw && gen_match(line + s[u], a.P, plen, P8);
+                    rv = rv && gen_match(line + s[u] + k - plen, a.RP, plen, R8);
+                }
+                const unsigned long long mf = __ballot(fw), mr = __ballot(rv);
+                const uint32_t n = (uint32_t)(__popcll(mf) + __popcll(mr));
+                if (n) {
+                    if (cnt + n > GW_Q) flush();
+                    const unsigned long long below = (1ull << lane) - 1ull;
+                    const uint64_t lo_key = lidx[u] << (a.pbits + 1);
+                    if (fw) {
+                        Record r;
+                        r.order = lo_key | s[u];
+                        r.pos = st[u] + s[u];
+                        r.len = k;
+                        r.strand = 0;
+                        wq[cnt + __popcll(mf & below)] = r;
+                    }
+                    if (rv) {
+                        Record r;
+                        r.order = lo_key | (1ull << a.pbits) | (L[u] - k - s[u]);
+                        r.pos = st[u] + s[u];
+                        r.len = k;
+                        r.strand = 1;
+                        wq[cnt + __popcll(mf) + __popcll(mr & below)] = r;
+                    }
+                    cnt += n;
+                }
+            }
+            f += 64 * U;
         }
         // next 64 lines: from the line holding position f (f >= E: line li + 64 on)
         if (f >= E) {
