@@ -573,14 +573,9 @@ __device__ __forceinline__ void emit_hit(const ScanArgs &a, const uint8_t *buf, 
     r.qm = (uint32_t)q | (strand << 14) | ((exotic ? 1u : 0u) << 15) | ((lstart >= 0 ? 1u : 0u) << 16) | (slot << 17);
     r.c_local = c_local;
     r.lstart = lstart >= 0 ? (uint32_t)lstart : 0u;
-    if (KH_ABLATE(a) & 8u) {                         // experiments: the record computed, not stored
-        if (r.code == 0x0123456789ABCDEFull && r.qm == 7u && r.lstart == 3u) atomicOr(a.err, 0u);
-        return;
-    }
-    if (KH_ABLATE(a) & 16u) {                        // experiments: every record to the same 64 slots
-        a.hits[threadIdx.x & 63u] = r;
-        return;
-    }
+    // (round 5: the ablations "record computed, not stored" and "every record
+    // to the same 64 slots" are gone -- they leave the hit kernel reading
+    // unwritten records, which faulted in the finish)
     if (slot < HMAX) {
         a.hits[(uint64_t)tile * HMAX + slot] = r;
         if (WIDE) a.hits_hi[(uint64_t)tile * HMAX + slot] = chi;
