@@ -267,7 +267,7 @@ kmer_status kmer_close(kmer_ctx *c) {
     c->rec_keys.release();
     c->tmp.release();
     c->batch.release();
-    for (auto *b : {&c->tb1, &c->tb2, &c->tHs, &c->tstart, &c->tp1, &c->tpb, &c->tsend, &c->tspill}) b->release();
+    for (auto *b : {&c->tb1, &c->tb2, &c->tHs, &c->tstart, &c->tp1, &c->tpb, &c->tsend}) b->release();
     c->tspc.release();
     c->tseg.release();
     c->tpc.release();

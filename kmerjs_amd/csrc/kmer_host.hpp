@@ -237,8 +237,7 @@ struct kmer_ctx {
     DBuf<uint32_t> tH, tnd;        // pass-1 / pass-2 histograms; distinct entries per bucket
     DBuf<uint64_t> tHs, tstart;    // their scans; bucket starts (TAB_NQ + 1)
     DBuf<uint64_t> tp1;            // pass-1 partition starts of the last chunk (TAB_NB)
-    DBuf<uint64_t> tspill;         // pass-1 keys past their fixed run (tab_scatter1f)
-    DBuf<unsigned long long> tspc; // [0] spill count, [1, 1 + TAB_NB) its histogram, then TAB_NB cursors
+    DBuf<unsigned long long> tspc; // pass-1 spill-area cursors (TAB_NB) + overflow count
     DBuf<TabUnit> tunits;          // pass-2 units, then TAB_NB partition heads
     DBuf<TabBig> tbig;             // entries with counts >= TAB_CMAX
     DBuf<uint32_t> tpc;            // pieces per sequence line (long lines)

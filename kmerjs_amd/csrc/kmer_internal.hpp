@@ -477,14 +477,14 @@ struct TabArgs {
     unsigned long long *rec_count;
     uint64_t rec_cap;
     unsigned int *err;
-    // pass 1 without the counting pass (tab_scatter1f): workgroup w's run of
-    // partition p starts at base + p * R + pcw[w] and holds pcw[w + 1] - pcw[w]
-    // keys; keys past it go to spill[0 .. spill_cap) (count: *spill_n)
+    // pass 1 without the counting pass (tab_scatter1f): partition p owns
+    // [base + p * PS, base + (p + 1) * PS), PS = R + S: workgroup w's run at
+    // p * PS + pcw[w] (pcw[w + 1] - pcw[w] keys), then S spill slots for the
+    // keys past their run (cursor pcur[p]; a full spill area counts in
+    // pcur[TAB_NB] and the chunk is redone by the counted pass)
     const uint64_t *pcw;
-    uint64_t R;
-    uint64_t *spill;
-    unsigned long long *spill_n;
-    uint64_t spill_cap;
+    uint64_t R, S, PS;
+    unsigned long long *pcur;
 };
 
 // Pass-1 filler of a run's unused tail (tab_scatter1f), skipped by pass 2:
@@ -543,11 +543,10 @@ hipError_t launch_tab_starts(const uint64_t *H2s, const uint32_t *H2, uint64_t n
 hipError_t launch_tab_scatter1f(const TabArgs &a, hipStream_t s);
 hipError_t launch_tab_wg_windows(const SeqLine *lines, uint64_t n, uint64_t lpw, uint32_t k, uint32_t nwg,
                                  uint64_t *W, hipStream_t s);
-// pass-1 spill (tab_scatter1f): keys by partition (hist: TAB_NB counters), then
-// placed at cur[partition]++ (cur: absolute B1 offsets)
-hipError_t launch_tab_spill_hist(const uint64_t *keys, uint64_t n, unsigned long long *hist, hipStream_t s);
-hipError_t launch_tab_spill_place(const uint64_t *keys, uint64_t n, unsigned long long *cur, uint64_t *B1,
-                                  hipStream_t s);
+// pass-1 spill areas (tab_scatter1f): the unused slots of each partition's
+// spill area filled with TAB_SENT
+hipError_t launch_tab_spill_fill(uint64_t *B1, uint64_t base, uint64_t R, uint64_t S, uint64_t PS,
+                                 const unsigned long long *pcur, hipStream_t s);
 hipError_t launch_tab_final(const TabFinal &a, uint32_t grid, hipStream_t s);
 hipError_t launch_tab_sort_final(const TabFinal &a, uint32_t grid, hipStream_t s);
 constexpr uint32_t TAB_SWG = 512;                      // sort-final workgroup (8 waves, two per CU)

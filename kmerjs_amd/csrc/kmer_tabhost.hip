@@ -24,7 +24,7 @@ kmer_status table_scatter1(kmer_ctx *c, TabArgs &a, hipStream_t s, hipError_t (*
         a.rec_count = c->d_rec_count;
         a.rec_cap = c->recs.cap;
         HIPCHK(c, hipMemsetAsync(c->d_rec_count, 0, 8, s));
-        if (attempt && a.spill_n) HIPCHK(c, hipMemsetAsync(a.spill_n, 0, 8, s));
+        if (attempt && a.pcur) HIPCHK(c, hipMemsetAsync(a.pcur, 0, (TAB_NB + 1) * 8, s));   // (a redo: the spill areas again)
         HIPCHK(c, hipEventRecord(c->tev[2], s));
         HIPCHK(c, launch(a, s));
         HIPCHK(c, hipEventRecord(c->tev[3], s));
@@ -76,12 +76,15 @@ kmer_status table_pass1_counted(kmer_ctx *c, TabArgs &a, hipStream_t s) {
 }
 
 // Pass 1 with fixed runs (tab_scatter1f): workgroup w's run in partition p
-// holds its mean share of keys + 2 standard deviations + 4, rounded up to 8 (a hash partition's
-// count is ~Poisson; at C3 ~5 % of the slots are filler, ~2 % of the runs
-// spill a few keys), sized from the workgroups' window counts.  *done false:
-// the runs would be more than 1/12 filler (small shares), or the spill list
-// overflowed (crowded partitions: repeated k-mers); nothing of the chunk is
-// kept and the caller runs the counted pass.
+// holds its mean share of keys + 2 standard deviations + 4, rounded up to 8 (a
+// hash partition's count is ~Poisson; at C3 ~5 % of the slots are filler, ~2 %
+// of the runs spill a few keys), sized from the workgroups' window counts.
+// Each partition's runs are followed by a spill area of S = R / 64 slots
+// (>= 256), so the chunk's partition p is one contiguous range [p PS,
+// (p + 1) PS) for pass 2, its unused slots TAB_SENT.  *done false: the runs
+// would be more than 1/12 filler (small shares), or a spill area overflowed
+// (crowded partitions: repeated k-mers); nothing of the chunk is kept and the
+// caller runs the counted pass.
 kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done) {
     *done = false;
     uint64_t *W = c->tHs.p, *pcw = c->tHs.p + a.nwg;
@@ -101,61 +104,43 @@ kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done
         tot += hw[w];
     }
     const uint64_t R = hp[a.nwg];
-    const uint64_t spill_cap = std::max<uint64_t>(1u << 20, tot / 256);
-    const uint64_t region = (uint64_t)TAB_NB * R;
+    const uint64_t S = (std::max<uint64_t>(256, R / 64) + 7) & ~7ull, PS = R + S;
+    const uint64_t region = (uint64_t)TAB_NB * PS;
     // small shares (C5's 1 GB of contigs: ~256 keys per run, 16 % filler) move
     // more filler through pass 2 than the counting pass costs: counted instead
     if (region > tot + tot / 12 && !(c->p.flags & KMER_FLAG_TABLE_FIXED_TEST)) return KMER_OK;
     const uint64_t cb = (c->t_keys + 7) & ~7ull;  // (runs of multiples of 8 keys start at 64-B boundaries)
-    HIPCHK(c, c->tb1.ensure(cb + region + spill_cap, s, true, c->t_keys));
-    HIPCHK(c, c->tspill.ensure(spill_cap, s));
-    HIPCHK(c, c->tspc.ensure(1 + 2 * TAB_NB, s));
+    HIPCHK(c, c->tb1.ensure(cb + region, s, true, c->t_keys));
+    HIPCHK(c, c->tspc.ensure(TAB_NB + 1, s));
     kmer_status st = upload(c, pcw, hp.data(), hp.size() * 8, s);
     if (st) return st;
     a.pcw = pcw;
     a.R = R;
+    a.S = S;
+    a.PS = PS;
     a.base = cb;
     a.B1 = c->tb1.p;
-    a.spill = c->tspill.p;
-    a.spill_n = c->tspc.p;
-    a.spill_cap = spill_cap;
-    HIPCHK(c, hipMemsetAsync(c->tspc.p, 0, (1 + TAB_NB) * 8, s));
+    a.pcur = c->tspc.p;
+    HIPCHK(c, hipMemsetAsync(c->tspc.p, 0, (TAB_NB + 1) * 8, s));
     st = table_scatter1(c, a, s, launch_tab_scatter1f);
     if (st) return st;
-    unsigned long long ns = 0;
-    HIPCHK(c, hipMemcpyAsync(&ns, c->tspc.p, 8, hipMemcpyDeviceToHost, s));
+    unsigned long long over = 0;
+    HIPCHK(c, hipMemcpyAsync(&over, c->tspc.p + TAB_NB, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
-    if (ns > spill_cap) {                      // (records of the attempt are dropped: the counted pass redoes them)
-        if (exp_env("KMERHIP_TAB_SPILL_LOG")) fprintf(stderr, "tab pass 1: spill list overflow (%llu)\n", ns);
+    if (over) {                                // (records of the attempt are dropped: the counted pass redoes them)
+        if (exp_env("KMERHIP_TAB_SPILL_LOG")) fprintf(stderr, "tab pass 1: spill area overflow (%llu)\n", over);
         return KMER_OK;
     }
+    HIPCHK(c, launch_tab_spill_fill(c->tb1.p, cb, R, S, PS, c->tspc.p, s));
     std::vector<uint64_t> off(TAB_NB + 1);
-    for (uint32_t p = 0; p <= TAB_NB; ++p) off[p] = (uint64_t)p * R;
+    for (uint32_t p = 0; p <= TAB_NB; ++p) off[p] = (uint64_t)p * PS;
     c->t_cbase.push_back(cb);
     c->t_coff.push_back(std::move(off));
     c->t_keys = cb + region;
-    c->t_fill += region - std::min<uint64_t>(region, tot - std::min<uint64_t>(tot, ns));
-    if (ns) {                                  // the spill list: one more chunk, partition-major
-        std::vector<unsigned long long> hh(TAB_NB), cur(TAB_NB);
-        std::vector<uint64_t> so(TAB_NB + 1);
-        HIPCHK(c, launch_tab_spill_hist(c->tspill.p, ns, c->tspc.p + 1, s));
-        HIPCHK(c, hipMemcpyAsync(hh.data(), c->tspc.p + 1, TAB_NB * 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipStreamSynchronize(s));
-        so[0] = 0;
-        for (uint32_t p = 0; p < TAB_NB; ++p) {
-            cur[p] = c->t_keys + so[p];
-            so[p + 1] = so[p] + hh[p];
-        }
-        st = upload(c, c->tspc.p + 1 + TAB_NB, cur.data(), TAB_NB * 8, s);
-        if (st) return st;
-        HIPCHK(c, launch_tab_spill_place(c->tspill.p, ns, c->tspc.p + 1 + TAB_NB, c->tb1.p, s));
-        c->t_cbase.push_back(c->t_keys);
-        c->t_coff.push_back(std::move(so));
-        c->t_keys += ns;
-    }
+    c->t_fill += region - std::min<uint64_t>(region, tot);
     if (exp_env("KMERHIP_TAB_SPILL_LOG"))
-        fprintf(stderr, "tab pass 1: %llu keys, %llu slots, %llu spilled\n", (unsigned long long)tot,
-                (unsigned long long)region, ns);
+        fprintf(stderr, "tab pass 1: %llu keys, %llu slots (spill areas of %llu)\n", (unsigned long long)tot,
+                (unsigned long long)region, (unsigned long long)S);
     c->t_ms[0] += ms0;
     c->t_ms[1] += ms1;
     *done = true;
@@ -278,14 +263,20 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
     std::vector<TabUnit> units;
     std::vector<TabUnit> heads(TAB_NB);
     uint64_t ubase = 0;
+    // a partition's run in a chunk is cut into ceil(len / cap) units of equal
+    // length (KMERHIP_TAB_UNIT: the cap, A/B experiments)
+    uint64_t ucap = TAB_UNIT;
+    if (const char *e = exp_env("KMERHIP_TAB_UNIT")) ucap = std::max<uint64_t>(8192, strtoull(e, nullptr, 10));
     for (uint32_t p = 0; p < TAB_NB; ++p) {
         const size_t first = units.size();
         for (size_t ch = 0; ch < c->t_cbase.size(); ++ch) {
             const uint64_t a0 = c->t_coff[ch][p], a1 = c->t_coff[ch][p + 1];
-            for (uint64_t o = a0; o < a1; o += TAB_UNIT) {
+            if (a1 <= a0) continue;
+            const uint64_t nu = (a1 - a0 + ucap - 1) / ucap, ul = (a1 - a0 + nu - 1) / nu;
+            for (uint64_t o = a0; o < a1; o += ul) {
                 TabUnit u{};
                 u.start = c->t_cbase[ch] + o;
-                u.len = (uint32_t)std::min<uint64_t>(TAB_UNIT, a1 - o);
+                u.len = (uint32_t)std::min<uint64_t>(ul, a1 - o);
                 units.push_back(u);
             }
         }

@@ -356,11 +356,12 @@ __global__ __launch_bounds__(TAB_WGH) void tab_scatter1h_kernel(TabArgs a) {
 // p * R + pcw[w] (the workgroup's mean share mu + 2 sqrt(mu) + 4, rounded up
 // to 8 keys: table_pass1_fixed in kmer_tabhost.hip), in the same LDS-sorted rounds as
 // tab_scatter1h; the run's unused tail is filled with TAB_SENT, which pass 2
-// skips.  A key past its run's capacity goes to the spill list (one atomic per
-// wave and write-out step), which the host places partition-major after the
-// runs as one more chunk (tab_spill_*; an overfull list: the chunk is redone
-// with the counting pass).  Saves tab_hist1's second formation of every
-// window.
+// skips.  A key past its run's capacity goes to its partition's spill area,
+// right after the partition's runs (one LDS-free global atomic per spilled
+// key: ~2 % of the runs spill a few keys), so a partition stays ONE
+// contiguous range for pass 2; a full spill area (a repeated k-mer crowding
+// one partition) sends the chunk to the counting pass.  Saves tab_hist1's
+// second formation of every window.
 template <bool PFX>
 __global__ __launch_bounds__(TAB_WGH) void tab_scatter1f_kernel(TabArgs a) {
     __shared__ uint64_t srt[TAB_RPL * TAB_WGH];
@@ -371,7 +372,7 @@ __global__ __launch_bounds__(TAB_WGH) void tab_scatter1f_kernel(TabArgs a) {
     const uint32_t t = threadIdx.x, b0 = 2 * t, b1 = 2 * t + 1;
     const uint64_t r0 = a.base + a.pcw[blockIdx.x];
     const uint32_t cap = (uint32_t)(a.pcw[blockIdx.x + 1] - a.pcw[blockIdx.x]);
-    const uint64_t R = a.R;
+    const uint64_t R = a.PS;                         // (partition stride: runs + spill area)
     fill[b0] = 0;
     fill[b1] = 0;
     bcnt[b0] = 0;
@@ -401,17 +402,12 @@ __global__ __launch_bounds__(TAB_WGH) void tab_scatter1f_kernel(TabArgs a) {
             const uint64_t h = srt[i];
             const uint32_t p = (uint32_t)(h >> (64 - TAB_L1));
             const uint32_t j = fill[p] + (i - bst[p]);
-            const bool sp = j >= cap;
-            if (!sp) a.B1[r0 + p * R + j] = h;
-            const uint64_t m = __ballot(sp);
-            if (m) {
-                const uint32_t lane = t & 63, lead = (uint32_t)__ffsll((unsigned long long)m) - 1;
-                unsigned long long o = 0;
-                if (lane == lead) o = atomicAdd(a.spill_n, (unsigned long long)__popcll(m));
-                o = (unsigned long long)(uint32_t)__shfl((int)(uint32_t)o, (int)lead) |
-                    ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(o >> 32), (int)lead) << 32);
-                o += (unsigned long long)__popcll(m & ((1ull << lane) - 1));
-                if (sp && o < a.spill_cap) a.spill[o] = h;
+            if (j < cap) {
+                a.B1[r0 + p * R + j] = h;
+            } else {                                 // past the run: the partition's spill area
+                const unsigned long long o = atomicAdd(&a.pcur[p], 1ull);
+                if (o < a.S) a.B1[a.base + p * R + a.R + o] = h;
+                else atomicAdd(&a.pcur[TAB_NB], 1ull);
             }
         }
         __syncthreads();
@@ -428,26 +424,12 @@ __global__ __launch_bounds__(TAB_WGH) void tab_scatter1f_kernel(TabArgs a) {
     }
 }
 
-// the spill list of tab_scatter1f, partition-major (order within a partition
-// is free: table mode has none)
-__global__ __launch_bounds__(256) void tab_spill_hist_kernel(const uint64_t *keys, uint64_t n,
-                                                             unsigned long long *hist) {
-    __shared__ uint32_t h[TAB_NB];
-    for (uint32_t i = threadIdx.x; i < TAB_NB; i += 256) h[i] = 0;
-    __syncthreads();
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
-        atomicAdd(&h[keys[i] >> (64 - TAB_L1)], 1u);
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < TAB_NB; i += 256)
-        if (h[i]) atomicAdd(&hist[i], (unsigned long long)h[i]);
-}
-
-__global__ __launch_bounds__(256) void tab_spill_place_kernel(const uint64_t *keys, uint64_t n,
-                                                              unsigned long long *cur, uint64_t *B1) {
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-        const uint64_t h = keys[i];
-        B1[atomicAdd(&cur[h >> (64 - TAB_L1)], 1ull)] = h;
-    }
+// the unused slots of the spill areas (tab_scatter1f): TAB_SENT, skipped by pass 2
+__global__ __launch_bounds__(256) void tab_spill_fill_kernel(uint64_t *B1, uint64_t base, uint64_t R, uint64_t S,
+                                                             uint64_t PS, const unsigned long long *pcur) {
+    const uint32_t p = blockIdx.x;
+    const uint64_t used = pcur[p] < S ? pcur[p] : S;
+    for (uint64_t i = used + threadIdx.x; i < S; i += 256) B1[base + p * PS + R + i] = TAB_SENT;
 }
 
 // keys (windows) of each pass-1 workgroup's share of lines: the fixed runs of
@@ -1634,16 +1616,9 @@ hipError_t launch_tab_scatter1f(const TabArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_tab_spill_hist(const uint64_t *keys, uint64_t n, unsigned long long *hist, hipStream_t s) {
-    const uint32_t g = (uint32_t)std::min<uint64_t>(1024, (n + 255) / 256);
-    hipLaunchKernelGGL(tab_spill_hist_kernel, dim3(std::max(g, 1u)), dim3(256), 0, s, keys, n, hist);
-    return hipGetLastError();
-}
-
-hipError_t launch_tab_spill_place(const uint64_t *keys, uint64_t n, unsigned long long *cur, uint64_t *B1,
-                                  hipStream_t s) {
-    const uint32_t g = (uint32_t)std::min<uint64_t>(4096, (n + 255) / 256);
-    hipLaunchKernelGGL(tab_spill_place_kernel, dim3(std::max(g, 1u)), dim3(256), 0, s, keys, n, cur, B1);
+hipError_t launch_tab_spill_fill(uint64_t *B1, uint64_t base, uint64_t R, uint64_t S, uint64_t PS,
+                                 const unsigned long long *pcur, hipStream_t s) {
+    hipLaunchKernelGGL(tab_spill_fill_kernel, dim3(TAB_NB), dim3(256), 0, s, B1, base, R, S, PS, pcur);
     return hipGetLastError();
 }
 

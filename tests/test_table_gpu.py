@@ -187,11 +187,11 @@ def test_table_big_counts(native):
 
 @pytest.mark.parametrize("k", [16, 31])
 def test_table_fixed_runs_spill(native, k):
-    # no prefix: pass 1 writes fixed per-workgroup runs (tab_scatter1f); a
-    # poly-A read every 8th record crowds one partition far past its runs, so
-    # ~390 K keys take the spill list (placed as one more chunk), and a second
-    # feed of poly-A alone overflows the list (> 2^20 keys: the chunk is redone
-    # with the counting pass) -- every route must give the oracle's Map
+    # no prefix: pass 1 writes fixed per-workgroup runs (tab_scatter1f); keys
+    # past a run go to their partition's spill area; a poly-A read every 8th
+    # record crowds one partition far past its runs and its spill area, so the
+    # chunk is redone with the counting pass, and a second feed of poly-A alone
+    # does the same -- every route must give the oracle's Map
     from oracle import oracle
     from tests.util import packed_sorted, result_packed_sorted, same_packed
     arr = np.frombuffer(bytearray(oracle.synth_fastq(21, 0, 24000)), dtype=np.uint8).reshape(-1, 317).copy()
