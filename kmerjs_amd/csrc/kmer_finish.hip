@@ -307,14 +307,27 @@ kmer_status general_merge(kmer_ctx *c) {
         HIPCHK(c, hipMemsetAsync(c->gm_flag.p, 0, sizeof(unsigned int), s));
         HIPCHK(c, launch_gen_hash(c->gm_keys.p, n, (uint32_t)k, 0x6A09E667F3BCC909ull + attempt, c->gm_h1.p, c->gm_h2.p,
                                   c->gm_idx.p, s));
-        ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, c->gm_h2.p, c->gm_h2b.p, c->gm_idx.p, c->gm_idx2.p, (size_t)n,
-                                                 0, 64, s));
-        HIPCHK(c, launch_gather_u64(c->gm_h1.p, c->gm_idx2.p, n, c->gm_h1b.p, s));
-        ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, c->gm_h1b.p, c->gm_h1.p, c->gm_idx2.p, c->gm_idx.p, (size_t)n,
-                                                 0, 64, s));
-        HIPCHK(c, launch_gather_u64(c->gm_h2.p, c->gm_idx.p, n, c->gm_h2b.p, s));   // (h2 of each sorted entry)
-        HIPCHK(c, launch_gen_heads(c->gm_h1.p, c->gm_h2b.p, c->gm_idx.p, n, c->gm_keys.p, (uint32_t)k, c->gm_head.p,
-                                   c->gm_flag.p, s));
+        // first attempt: one radix sort by h1 (a 64-bit collision between two
+        // distinct keys -- p ~ n^2 / 2^65 -- is caught by the byte check and
+        // redone); later attempts: the LSD pair (h2, then h1, stable)
+        const uint32_t *idx_sorted;
+        if (attempt == 0) {
+            ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, c->gm_h1.p, c->gm_h1b.p, c->gm_idx.p, c->gm_idx2.p,
+                                                     (size_t)n, 0, 64, s));
+            HIPCHK(c, launch_gen_heads(c->gm_h1b.p, c->gm_h1b.p, c->gm_idx2.p, n, c->gm_keys.p, (uint32_t)k,
+                                       c->gm_head.p, c->gm_flag.p, s));
+            idx_sorted = c->gm_idx2.p;
+        } else {
+            ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, c->gm_h2.p, c->gm_h2b.p, c->gm_idx.p, c->gm_idx2.p,
+                                                     (size_t)n, 0, 64, s));
+            HIPCHK(c, launch_gather_u64(c->gm_h1.p, c->gm_idx2.p, n, c->gm_h1b.p, s));
+            ROCPRIM_RUN(c, rocprim::radix_sort_pairs(t, b, c->gm_h1b.p, c->gm_h1.p, c->gm_idx2.p, c->gm_idx.p,
+                                                     (size_t)n, 0, 64, s));
+            HIPCHK(c, launch_gather_u64(c->gm_h2.p, c->gm_idx.p, n, c->gm_h2b.p, s));   // (h2 of each sorted entry)
+            HIPCHK(c, launch_gen_heads(c->gm_h1.p, c->gm_h2b.p, c->gm_idx.p, n, c->gm_keys.p, (uint32_t)k,
+                                       c->gm_head.p, c->gm_flag.p, s));
+            idx_sorted = c->gm_idx.p;
+        }
         ROCPRIM_RUN(c, rocprim::inclusive_scan(t, b, c->gm_head.p, c->gm_gid.p, (size_t)n, rocprim::plus<uint32_t>(), s));
         uint32_t hv[2] = {0, 0};
         HIPCHK(c, hipMemcpyAsync(&hv[0], c->gm_flag.p, 4, hipMemcpyDeviceToHost, s));
@@ -326,7 +339,7 @@ kmer_status general_merge(kmer_ctx *c) {
         HIPCHK(c, c->gm_cnt2.ensure(ng, s));
         HIPCHK(c, c->gm_first2.ensure(ng, s));
         HIPCHK(c, launch_gen_starts(c->gm_head.p, c->gm_gid.p, n, c->gm_start.p, s));
-        HIPCHK(c, launch_gen_reduce(c->gm_start.p, ng, c->gm_idx.p, c->gm_keys.p, c->gm_cnt.p, c->gm_first.p,
+        HIPCHK(c, launch_gen_reduce(c->gm_start.p, ng, idx_sorted, c->gm_keys.p, c->gm_cnt.p, c->gm_first.p,
                                     (uint32_t)k, c->gm_keys2.p, c->gm_cnt2.p, c->gm_first2.p, s));
         std::swap(c->gm_keys, c->gm_keys2);
         std::swap(c->gm_cnt, c->gm_cnt2);

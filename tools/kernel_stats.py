@@ -1,14 +1,14 @@
 """Per-kernel duration statistics of the TIMED steps of a bench.py run under
 `rocprofv3 --kernel-trace` (profiles/ evidence).
 
-bench.py runs W warmup steps, then K timed steps; with its side legs switched
+bench.py runs W warmup steps, K timed steps, then one more step (E = 1) that
+reads the result size outside the timed region; with its side legs switched
 off (--no-pcie --no-e2e --no-pipelined --no-match --no-cpu-baseline) every
 kernel is dispatched the same number of times per step, so the timed steps are
-the last K x (dispatches / (W + K)) dispatches of each kernel.  Kernels whose
-dispatch count is not a multiple of W + K are reported over all dispatches and
-flagged.
+the K x per dispatches before the last E x per, per = (dispatches - E) /
+(W + K).  Kernels whose count does not fit that are flagged (not exact).
 
-usage: python tools/kernel_stats.py TRACE_DIR WARMUP STEPS [out.csv]
+usage: python tools/kernel_stats.py TRACE_DIR WARMUP STEPS [out.csv] [E]
 """
 import csv
 import glob
@@ -19,6 +19,7 @@ from collections import defaultdict
 
 root, W, K = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 out = sys.argv[4] if len(sys.argv) > 4 else None
+E = int(sys.argv[5]) if len(sys.argv) > 5 else 1
 rows = []
 for path in glob.glob(root + "/**/*kernel_trace.csv", recursive=True):
     rows += list(csv.DictReader(open(path)))
@@ -33,9 +34,11 @@ for name, d in by.items():
     n = len(d)
     # (bench.py may dispatch a kernel once more before its warmup: e.g. a
     # verification count; the timed steps are still the LAST ones)
-    per = n // (W + K)
-    exact = n % (W + K) == 0
-    take = d[-per * K:] if per else d
+    # (bench.py's extra pass after the timed steps -- the result-size read --
+    # dispatches E = 1 more step's kernels: the timed window ends before it)
+    per = (n - E) // (W + K)
+    exact = per > 0 and (n - E) % (W + K) == 0
+    take = d[n - E - per * K:n - E] if per else d
     res.append({"kernel": name, "dispatches_total": n, "dispatches_timed": len(take),
                 "timed_window_exact": exact, "avg_us": statistics.mean(take), "min_us": min(take),
                 "max_us": max(take), "stdev_us": statistics.pstdev(take), "sum_us": sum(take)})

@@ -23,9 +23,12 @@ run c3 --config c3 --steps 5 --warmup 1
 run c4 --config c4 --steps 10 --warmup 2
 run c5 --config c5 --steps 10 --warmup 2
 run c5_ordered --config c5 --ordered --steps 10 --warmup 2
+run c5_fasta --config c5 --fasta --steps 10 --warmup 2
 run k40 --k 40 --steps 10 --warmup 2 --no-cpu-baseline
 run k64_AT --k 64 --prefix AT --reads 2000000 --steps 3 --warmup 1 --no-cpu-baseline
 run k16_AT --prefix AT --steps 5 --warmup 1 --no-cpu-baseline
 run k21_noprefix --k 21 --prefix "" --reads 4000000 --steps 5 --warmup 1 --no-cpu-baseline
-run k70 --k 70 --steps 3 --warmup 1 --no-cpu-baseline
+run k70 --k 70 --steps 10 --warmup 2 --no-cpu-baseline
+run k150 --k 150 --steps 10 --warmup 2 --no-cpu-baseline
+run k40_noprefix --k 40 --prefix "" --reads 1000000 --steps 3 --warmup 1 --no-cpu-baseline
 exit 0
