@@ -249,7 +249,7 @@ def load_traffic(args, kern_name):
     try:
         with open(path) as f:
             d = json.load(f)
-        e = d.get(args.config, {})
+        e = d.get(args.config + ("fa" if getattr(args, "fasta", False) else ""), {})
         reads = args.reads if args.config in ("c2", "c3", "c4") else 0   # (c1/c5 inputs are not read-based)
         if e.get("reads") not in (None, reads) or e.get("k") not in (None, args.k) or \
                 e.get("prefix") not in (None, args.prefix):
@@ -679,7 +679,8 @@ def main():
             # per window; the accepted windows are merged on the device
             # (general_merge: hash sort + byte-checked groups) -- the feed
             # kernels together (lines, windows, append)
-            kern_name = "lines_kernel + windows_kernel (general path, device merge at finish)"
+            kern_name = "nl_slots_kernel + seq_lines_slots_kernel + gen_windows_kernel + gen_append_kernel " \
+                        "(general path feed; device merge at finish)"
             kern_ms = sum(feed_ms_l) / len(feed_ms_l)
             algo_bytes = nbytes + (24 + args.k) * (accepted / world)
         elif args.flags & 2 or not set(args.prefix) <= set("ACGT"):

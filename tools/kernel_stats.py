@@ -26,7 +26,7 @@ for path in glob.glob(root + "/**/*kernel_trace.csv", recursive=True):
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 by = defaultdict(list)
 for r in rows:
-    m = re.findall(r"kmerhip::(\w+)", r["Kernel_Name"])
+    m = re.findall(r"kmerhip::(?:\(anonymous namespace\)::)?(\w+)", r["Kernel_Name"])
     name = m[0] if m else r["Kernel_Name"].split("(")[0][:60]
     by[name].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)   # us
 res = []

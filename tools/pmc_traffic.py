@@ -24,7 +24,7 @@ vals = defaultdict(lambda: defaultdict(list))
 for path in glob.glob(root + "/pmc*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"]
-        m = re.findall(r"kmerhip::(\w+)", name)
+        m = re.findall(r"kmerhip::(?:\(anonymous namespace\)::)?(\w+)", name)
         short = m[0] if m else name[:40]
         vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
 kernels = {}
