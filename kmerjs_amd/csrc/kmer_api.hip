@@ -179,6 +179,8 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
         if (ok) ok &= hipMemcpy(c->d_PR, pr.data(), pr.size(), hipMemcpyHostToDevice) == hipSuccess;
     }
     ok &= dalloc(&c->d_ticket, 4) == hipSuccess;
+    ok &= dalloc(&c->d_bticket, 1) == hipSuccess;
+    if (ok) ok &= hipMemset(c->d_bticket, 0, sizeof(unsigned int)) == hipSuccess;
     ok &= dalloc(&c->d_scal, 16) == hipSuccess;
     if (ok) {
         ok &= hipMemset(c->d_scal, 0, 128) == hipSuccess;
@@ -284,7 +286,7 @@ kmer_status kmer_close(kmer_ctx *c) {
         b->release();
     for (auto *b : {&c->gm_idx, &c->gm_idx2, &c->gm_head, &c->gm_gid, &c->gm_start}) b->release();
     c->gm_flag.release();
-    dfree(c->d_ticket); dfree(c->d_scal); dfree(c->d_pos); dfree(c->d_pos_saved);
+    dfree(c->d_ticket); dfree(c->d_bticket); dfree(c->d_scal); dfree(c->d_pos); dfree(c->d_pos_saved);
     dfree(c->d_P); dfree(c->d_PR);
     if (c->h_small) (void)hipHostFree(c->h_small);
     if (c->h_tail) (void)hipHostFree(c->h_tail);

@@ -101,10 +101,8 @@ kmer_status bucket_heads(kmer_ctx *c, uint64_t n) {
     HIPCHK(c, c->bbase.ensure(2 * BKT_MAX + 2, s));   // bucket totals [0, nb), starts [BKT_MAX, BKT_MAX + nb]
     uint32_t *btot = c->bbase.p, *bstart = c->bbase.p + BKT_MAX;
     HIPCHK(c, launch_bucket_hist(c->rkey32.p, n, invalid, shift, nb, nblk, c->bH.p, c->hcnt.p, s));
-    HIPCHK(c, launch_bucket_offsets(c->bH.p, nb, nblk, c->bHs.p, btot, s));
-    if (nblk == 0) HIPCHK(c, hipMemsetAsync(bstart, 0, (nb + 1) * sizeof(uint32_t), s));   // no scatter workgroup writes them
-    else HIPCHK(c, launch_bucket_scatter(c->rkey32.p, n, invalid, shift, nb, nblk, c->bHs.p, btot, bstart, c->pkey16.p,
-                                         c->ridx2.p, s));
+    HIPCHK(c, launch_bucket_offsets(c->bH.p, nb, nblk, c->bHs.p, btot, bstart, c->d_bticket, s));
+    HIPCHK(c, launch_bucket_scatter(c->rkey32.p, n, invalid, shift, nb, nblk, c->bHs.p, bstart, c->pkey16.p, c->ridx2.p, s));
     HIPCHK(c, launch_bucket_heads(c->pkey16.p, c->ridx2.p, bstart, nb, shift, c->hcnt.p, s));
     return KMER_OK;
 }

@@ -193,6 +193,7 @@ struct kmer_ctx {
     // [5] err (u32) [6] line count [7] chunk ends open
     uint64_t *d_scal = nullptr;
     unsigned int *d_ticket = nullptr, *d_err = nullptr;
+    unsigned int *d_bticket = nullptr;   // bucket_offsets_kernel last-block ticket (returned to 0 by it)
     unsigned long long *d_rec_count = nullptr, *d_line_count = nullptr, *d_ovf_count = nullptr;
     unsigned long long *d_xcount = nullptr, *d_chunk_hits = nullptr, *d_ends_open = nullptr;
     uint64_t *d_nuniq = nullptr;

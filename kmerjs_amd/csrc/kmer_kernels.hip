@@ -1613,7 +1613,7 @@ __device__ __forceinline__ bool gen_match(const uint8_t *p, const uint8_t *P, ui
     return ok;
 }
 
-constexpr uint32_t GW_Q = 256;                   // records queued per wave
+constexpr uint32_t GW_Q = 128;                   // records queued per wave (>= the 128 of one step; 12 KB of LDS per workgroup)
 
 __global__ __launch_bounds__(256) void gen_windows_kernel(GenWinArgs a) {
     __shared__ Record q[4][GW_Q];
@@ -2425,12 +2425,15 @@ __global__ __launch_bounds__(256) void bucket_hist_kernel(const uint32_t *key, u
 
 // Offsets of the partition (one launch, no library scan): workgroup b scans
 // bucket b's row of block counts (H[b * nblk + blk] -> Hs, bucket-relative)
-// and writes the bucket's total; the buckets' starts are scanned by every
-// bucket_scatter workgroup from the totals (a kernel boundary apart: no
-// cross-workgroup handoff inside this kernel).
+// and publishes the bucket's total; the last workgroup to finish turns the
+// totals into the buckets' starts (bbase[nb] = all keys).  The ticket add is
+// acquire-release at agent scope (HIP memory model); the totals are read
+// back by atomics.
 __global__ __launch_bounds__(256) void bucket_offsets_kernel(const uint32_t *H, uint32_t nb, uint32_t nblk,
-                                                             uint32_t *Hs, uint32_t *btot) {
+                                                             uint32_t *Hs, uint32_t *btot, uint32_t *bbase,
+                                                             unsigned int *ticket) {
     __shared__ uint32_t ws[4];
+    __shared__ bool last;
     const uint32_t b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t per = (nblk + 255) / 256, j0 = tid * per, j1 = min(j0 + per, nblk);
     const uint32_t *row = H + (uint64_t)b * nblk;
@@ -2447,46 +2450,52 @@ __global__ __launch_bounds__(256) void bucket_offsets_kernel(const uint32_t *H, 
         out[j] = pre;
         pre += v;
     }
-    if (tid == 0) btot[b] = ws[0] + ws[1] + ws[2] + ws[3];
+    if (tid == 0) {
+        // release (the total reaches memory before the ticket announces it) and
+        // acquire (the last workgroup sees every earlier total) at agent scope:
+        // the compiler emits the L2 writeback / invalidate the XCDs need
+        __hip_atomic_store(btot + b, ws[0] + ws[1] + ws[2] + ws[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nb - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    // bucket starts: nb <= BKT_MAX totals, 8 per thread
+    uint32_t v[BKT_MAX / 256], s = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < BKT_MAX / 256; ++u) {
+        const uint32_t q = tid * (BKT_MAX / 256) + u;
+        // (read by an atomic, at the memory side: an agent-scope load may be
+        // served by this XCD's L2, which can hold the line from an earlier call)
+        v[u] = q < nb ? __hip_atomic_fetch_add(btot + q, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        s += v[u];
+    }
+    const uint32_t inc2 = wave_incl_sum(s);
+    __syncthreads();
+    if (lane == 63) ws[wid] = inc2;
+    __syncthreads();
+    uint32_t p = inc2 - s;
+    for (uint32_t w = 0; w < wid; ++w) p += ws[w];
+#pragma unroll
+    for (uint32_t u = 0; u < BKT_MAX / 256; ++u) {
+        const uint32_t q = tid * (BKT_MAX / 256) + u;
+        if (q < nb) bbase[q] = p;
+        p += v[u];
+    }
+    if (tid == 255) bbase[nb] = p;
+    if (tid == 0) *ticket = 0;
 }
 
 // Scatter with the block's elements first grouped by bucket in LDS, so that
 // each bucket's run goes out as one contiguous (coalesced) piece.
-// (the buckets' starts: an exclusive scan of the totals, done by every
-// workgroup for its own use; workgroup 0 also writes them to bbase for
-// bucket_heads, bbase[nb] = all keys)
 __global__ __launch_bounds__(256) void bucket_scatter_kernel(const uint32_t *key, uint64_t n, uint32_t invalid,
                                                              uint32_t shift, uint32_t nb, uint32_t nblk,
-                                                             const uint32_t *Hs, const uint32_t *btot, uint32_t *bbase,
-                                                             uint16_t *pkey, uint32_t *prank) {
+                                                             const uint32_t *Hs, const uint32_t *bbase, uint16_t *pkey,
+                                                             uint32_t *prank) {
     __shared__ uint32_t cnt[BKT_MAX];          // per bucket: count, then local start
     __shared__ uint32_t skey[BKT_EPB];
     __shared__ uint32_t srank[BKT_EPB];
-    __shared__ uint32_t wtot[4], wtot2[4];
+    __shared__ uint32_t wtot[4];
     for (uint32_t b = threadIdx.x; b < nb; b += 256) cnt[b] = 0;
-    uint32_t bst[BKT_MAX / 256];               // global starts of this thread's buckets (same mapping as loc below)
-    {
-        uint32_t t8[BKT_MAX / 256], sum = 0;
-#pragma unroll
-        for (uint32_t u = 0; u < BKT_MAX / 256; ++u) {
-            const uint32_t b = threadIdx.x * (BKT_MAX / 256) + u;
-            t8[u] = b < nb ? btot[b] : 0u;
-            sum += t8[u];
-        }
-        const uint32_t incl = wave_incl_sum(sum);
-        if ((threadIdx.x & 63) == 63) wtot2[threadIdx.x >> 6] = incl;
-        __syncthreads();
-        uint32_t pre = incl - sum;
-        for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) pre += wtot2[w];
-#pragma unroll
-        for (uint32_t u = 0; u < BKT_MAX / 256; ++u) {
-            const uint32_t b = threadIdx.x * (BKT_MAX / 256) + u;
-            bst[u] = pre;
-            if (b < nb && blockIdx.x == 0) bbase[b] = pre;
-            pre += t8[u];
-        }
-        if (blockIdx.x == 0 && threadIdx.x == 255) bbase[nb] = pre;
-    }
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * BKT_EPB;
     uint32_t kk[BKT_EPB / 256], li[BKT_EPB / 256];
@@ -2533,7 +2542,7 @@ __global__ __launch_bounds__(256) void bucket_scatter_kernel(const uint32_t *key
 #pragma unroll
     for (uint32_t u = 0; u < BKT_MAX / 256; ++u) {
         const uint32_t b = threadIdx.x * (BKT_MAX / 256) + u;
-        if (b < nb && loc[u]) cnt[b] = bst[u] + Hs[(uint64_t)b * nblk + blockIdx.x] - lst[u];
+        if (b < nb && loc[u]) cnt[b] = bbase[b] + Hs[(uint64_t)b * nblk + blockIdx.x] - lst[u];
     }
     __syncthreads();
     const uint32_t lo_mask = (1u << shift) - 1u;
@@ -2872,20 +2881,28 @@ __global__ __launch_bounds__(256) void gather_records_kernel(const Record *recs,
 // Ordered merge of per-rank result lists: row i of the output is source row
 // idx[i] (k-byte key, count, first-occurrence key).  One thread per row; keys
 // copied 4 bytes at a time when k allows.
+// out row i = in row idx[i] (k-byte keys with their count and first): a wave
+// copies 64 / k rows at a time (k <= 64; lane = row * k + byte) or one row
+// (k > 64, lanes stride over its bytes), so the byte loads and stores of a
+// wave are contiguous runs instead of one thread walking a whole row
 __global__ __launch_bounds__(256) void permute_rows_kernel(const uint8_t *keys, const uint64_t *cnt,
                                                            const uint64_t *first, const uint32_t *idx, uint64_t n,
                                                            uint32_t k, uint8_t *okeys, uint64_t *ocnt,
                                                            uint64_t *ofirst) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t rpw = k <= 64 ? 64 / k : 1u;            // rows per wave step
+    const uint32_t r = k <= 64 ? lane / k : 0u, b0 = k <= 64 ? lane % k : lane;
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    for (uint64_t w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); w * rpw < n; w += nw) {
+        const uint64_t i = w * rpw + r;
+        if (r >= rpw || i >= n) continue;
         const uint64_t j = idx[i];
-        ocnt[i] = cnt[j];
-        ofirst[i] = first[j];
         const uint8_t *src = keys + j * k;
         uint8_t *dst = okeys + i * k;
-        if ((k & 3) == 0) {
-            for (uint32_t b = 0; b < k; b += 4) *(uint32_t *)(dst + b) = *(const uint32_t *)(src + b);
-        } else {
-            for (uint32_t b = 0; b < k; ++b) dst[b] = src[b];
+        for (uint32_t b = b0; b < k; b += 64) dst[b] = src[b];
+        if (b0 == 0) {
+            ocnt[i] = cnt[j];
+            ofirst[i] = first[j];
         }
     }
 }
@@ -2893,8 +2910,9 @@ __global__ __launch_bounds__(256) void permute_rows_kernel(const uint8_t *keys, 
 hipError_t launch_permute_rows(const uint8_t *keys, const uint64_t *cnt, const uint64_t *first, const uint32_t *idx,
                                uint64_t n, uint32_t k, uint8_t *okeys, uint64_t *ocnt, uint64_t *ofirst,
                                hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    uint64_t blocks = (n + 255) / 256;
+    if (n == 0 || k == 0) return hipSuccess;
+    const uint64_t rpw = k <= 64 ? 64 / k : 1;
+    uint64_t blocks = ((n + rpw - 1) / rpw + 3) / 4;
     if (blocks > 16384) blocks = 16384;
     hipLaunchKernelGGL(permute_rows_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, keys, cnt, first, idx, n, k,
                        okeys, ocnt, ofirst);
@@ -3147,16 +3165,15 @@ hipError_t launch_bucket_hist(const uint32_t *key, uint64_t n, uint32_t invalid,
     return hipGetLastError();
 }
 hipError_t launch_bucket_offsets(const uint32_t *H, uint32_t nb, uint32_t nblk, uint32_t *Hs, uint32_t *btot,
-                                 hipStream_t s) {
-    hipLaunchKernelGGL(bucket_offsets_kernel, dim3(nb), dim3(256), 0, s, H, nb, nblk, Hs, btot);
+                                 uint32_t *bbase, unsigned int *ticket, hipStream_t s) {
+    hipLaunchKernelGGL(bucket_offsets_kernel, dim3(nb), dim3(256), 0, s, H, nb, nblk, Hs, btot, bbase, ticket);
     return hipGetLastError();
 }
-
 hipError_t launch_bucket_scatter(const uint32_t *key, uint64_t n, uint32_t invalid, uint32_t shift, uint32_t nb,
-                                 uint32_t nblk, const uint32_t *Hs, const uint32_t *btot, uint32_t *bbase,
-                                 uint16_t *pkey, uint32_t *prank, hipStream_t s) {
-    hipLaunchKernelGGL(bucket_scatter_kernel, dim3(nblk), dim3(256), 0, s, key, n, invalid, shift, nb, nblk, Hs, btot,
-                       bbase, pkey, prank);
+                                 uint32_t nblk, const uint32_t *Hs, const uint32_t *bbase, uint16_t *pkey,
+                                 uint32_t *prank, hipStream_t s) {
+    hipLaunchKernelGGL(bucket_scatter_kernel, dim3(nblk), dim3(256), 0, s, key, n, invalid, shift, nb, nblk, Hs, bbase,
+                       pkey, prank);
     return hipGetLastError();
 }
 hipError_t launch_bucket_heads(const uint16_t *pkey, const uint32_t *prank, const uint32_t *bbase, uint32_t nb,
