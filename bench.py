@@ -675,11 +675,14 @@ def main():
                          "final": "tab_sort_final_kernel (+ tab_final_kernel on its leftover units)",
                          "fasta": "fa_tiles_kernel + fa_write_kernel (FASTA rewrite)"}[kern_name]
         elif args.k > 64 or (not args.prefix and args.k > 31):
-            # general path (k > 64, unprefixed k > 31): line arrays + one thread
-            # per window; the accepted windows are merged on the device
+            # general path (k > 64, unprefixed k > 31): line arrays, the windows
+            # (A/C/G/T prefix: plane candidates; else one lane per window
+            # position); the accepted windows are merged on the device
             # (general_merge: hash sort + byte-checked groups) -- the feed
             # kernels together (lines, windows, append)
-            kern_name = "nl_slots_kernel + seq_lines_slots_kernel + gen_windows_kernel + gen_append_kernel " \
+            wk = ("gen_cand_kernel" if args.prefix and set(args.prefix) <= set("ACGT") and not args.flags & 4
+                  else "gen_windows_kernel")
+            kern_name = "nl_slots_kernel + seq_lines_slots_kernel + " + wk + " + gen_append_kernel " \
                         "(general path feed; device merge at finish)"
             kern_ms = sum(feed_ms_l) / len(feed_ms_l)
             algo_bytes = nbytes + (24 + args.k) * (accepted / world)

@@ -151,7 +151,8 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
     c->narrow = packed_keys && c->kbits <= 31;
     c->wide = packed_keys && c->kbits >= 64;
     c->planes = (c->mode == MODE_PACKED || c->mode == MODE_TILE_REC) && acgt && !(pp->flags & KMER_FLAG_BYTE_SCAN);
-    if (c->planes) {
+    c->gen_planes = c->gm_on && acgt && !(pp->flags & KMER_FLAG_BYTE_SCAN);
+    if (c->planes || c->gen_planes) {
         // plane bits of a base: bit 1 (plane L) and bit 2 (plane H) of its ASCII byte
         auto code = [](char ch) -> uint32_t { return (((uint8_t)ch >> 1) & 1u) | ((((uint8_t)ch >> 2) & 1u) << 1); };
         c->pargs.pb = std::min<uint32_t>(plen, 5);
@@ -263,6 +264,7 @@ kmer_status kmer_close(kmer_ctx *c) {
     c->uval.release();
     c->keys_out.release();
     c->recs.release();
+    c->gcand.release();
     c->lines.release();
     c->rec_keys.release();
     c->tmp.release();

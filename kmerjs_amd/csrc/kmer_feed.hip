@@ -528,6 +528,8 @@ kmer_status general_feed_dev(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32
         w.len = len;
         w.lines = c->lines.p;
         w.wbase = c->wbase.p;
+        w.tbase = c->tbase.p;
+        w.first = (1u - (uint32_t)li0) & 3u;
         w.n_lines = n_seq;
         w.total = total;
         w.k = c->p.k;
@@ -536,12 +538,16 @@ kmer_status general_feed_dev(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32
         w.P = c->d_PR + 2 * KMAX_TILE;
         w.RP = w.P + c->prefix.size();
         w.err = c->d_err;
+        // A/C/G/T prefix: candidates from the planes (gen_cand), then the
+        // windows that fit their lines (gen_fix); else the flattened windows
+        DBuf<Record> &out = c->gen_planes ? c->gcand : c->recs;
         for (int attempt = 0;; ++attempt) {
-            w.recs = c->recs.p;
+            w.recs = out.p;
             w.rec_count = c->d_rec_count;
-            w.rec_cap = c->recs.cap;
+            w.rec_cap = out.cap;
             HIPCHK(c, hipMemsetAsync(c->d_rec_count, 0, 8, s));
-            HIPCHK(c, launch_gen_windows(w, s));
+            if (c->gen_planes) HIPCHK(c, launch_gen_cand(w, c->pargs, s));
+            else HIPCHK(c, launch_gen_windows(w, s));
             HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
             HIPCHK(c, hipStreamSynchronize(s));
             const uint32_t e = (uint32_t)c->h_small[5];
@@ -550,10 +556,23 @@ kmer_status general_feed_dev(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32
             if (!(e & ERR_REC_OVERFLOW)) break;
             if (attempt == 7) return fail(c, KMER_E_OOM, "record list kept overflowing");
             HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
-            st = ensure_records(c, c->h_small[0] + 1024);
+            if (c->gen_planes) HIPCHK(c, c->gcand.ensure(c->h_small[0] + 1024, s));
+            else st = ensure_records(c, c->h_small[0] + 1024);
             if (st) return st;
         }
         nrec = c->h_small[0];
+        if (c->gen_planes && nrec) {
+            st = ensure_records(c, nrec);       // (records <= candidates: no overflow)
+            if (st) return st;
+            HIPCHK(c, hipMemsetAsync(c->d_rec_count, 0, 8, s));
+            HIPCHK(c, launch_gen_fix(c->gcand.p, nrec, c->lines.p, w.k, w.plen, w.pbits, c->recs.p, c->d_rec_count,
+                                     c->recs.cap, c->d_err, s));
+            HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            st = check_err(c, (uint32_t)c->h_small[5]);
+            if (st) return st;
+            nrec = c->h_small[0];
+        }
     }
     if (nrec) {
         st = general_append(c, d, nrec, s);

@@ -159,6 +159,7 @@ struct kmer_ctx {
     DBuf<uint32_t> rkey32, rkey32b;   // narrow keys: 2(k-|P|) + 1 <= 32 bits
     bool narrow = false;
     bool planes = false;           // ACGT prefix: bit-plane scan kernel
+    bool gen_planes = false;       // general path, A/C/G/T prefix: windows from the plane candidates (gen_cand_kernel)
     PlaneArgs pargs{};
     DBuf<uint32_t> ridx, ridx2, ecnt, bbase;
     DBuf<uint64_t> epre;
@@ -184,6 +185,7 @@ struct kmer_ctx {
     uint64_t n_out = 0;            // ordered entries of the last finish (device)
     // records & lines
     DBuf<Record> recs;
+    DBuf<Record> gcand;            // general path, A/C/G/T prefix: window candidates (gen_cand_kernel)
     DBuf<SeqLine> lines;
     DBuf<uint8_t> rec_keys;
     // scratch

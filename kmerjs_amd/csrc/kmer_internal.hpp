@@ -282,6 +282,8 @@ struct GenWinArgs {
     uint64_t len;
     const SeqLine *lines;
     const uint64_t *wbase;
+    const uint64_t *tbase;         // newlines before each TILE of the chunk (chunk_lines)
+    uint64_t first;                // line index (from the chunk start) of the first sequence line
     uint64_t n_lines, total;       // lines, windows of both strands
     uint32_t k, plen, pbits;
     const uint8_t *P, *RP;         // the prefix and its reverse complement (device)
@@ -291,6 +293,10 @@ struct GenWinArgs {
     unsigned int *err;
 };
 hipError_t launch_gen_windows(const GenWinArgs &a, hipStream_t s);
+hipError_t launch_gen_cand(const GenWinArgs &a, const PlaneArgs &pa, hipStream_t s);   // A/C/G/T prefix
+hipError_t launch_gen_fix(const Record *cand, uint64_t n, const SeqLine *lines, uint32_t k, uint32_t plen,
+                          uint32_t pbits, Record *recs, unsigned long long *rec_count, uint64_t rec_cap,
+                          unsigned int *err, hipStream_t s);
 
 struct WindowArgs {
     const uint8_t *data;

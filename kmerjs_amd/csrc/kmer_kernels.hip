@@ -1563,18 +1563,25 @@ __global__ __launch_bounds__(256) void windows_kernel(WindowArgs a) {
 // every pair of neighbours with equal hashes (a collision is reported, never
 // merged), and reduces each group to (key, count sum, min first).
 // ---------------------------------------------------------------------------
-// (one wave per record: lanes copy consecutive bytes -- the keys are >= 32
-// bytes on this path -- so loads and stores stay coalesced)
-__global__ __launch_bounds__(256) void gen_append_kernel(const Record *recs, uint64_t n, const uint8_t *data,
-                                                         uint32_t k, uint8_t *keys, uint64_t *cnt, uint64_t *first) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t nw = (uint64_t)gridDim.x * 4;
-    for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += nw) {
+// (GEN_G lanes per record, 64 / GEN_G records per wave step: several rows'
+// loads in flight per wave -- one wave per row was latency-bound)
+constexpr uint32_t GEN_G = 8;
+__global__ __launch_bounds__(256) void gen_append_kernel(const Record *__restrict__ recs, uint64_t n,
+                                                         const uint8_t *__restrict__ data, uint32_t k,
+                                                         uint8_t *__restrict__ keys, uint64_t *__restrict__ cnt,
+                                                         uint64_t *__restrict__ first) {
+    const uint32_t lane = threadIdx.x & 63, sub = lane % GEN_G;
+    const uint64_t nw = (uint64_t)gridDim.x * 4 * (64 / GEN_G);
+    for (uint64_t i = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * (64 / GEN_G) + lane / GEN_G; i < n; i += nw) {
         const Record r = recs[i];
         uint8_t *o = keys + i * k;
         const uint8_t *src = data + r.pos;
-        for (uint32_t b = lane; b < k; b += 64) o[b] = r.strand ? comp_byte(src[k - 1 - b]) : src[b];
-        if (lane == 0) {
+        if (r.strand) {
+            for (uint32_t b = sub; b < k; b += GEN_G) o[b] = comp_byte(src[k - 1 - b]);
+        } else {
+            for (uint32_t b = sub; b < k; b += GEN_G) o[b] = src[b];
+        }
+        if (sub == 0) {
             cnt[i] = 1;
             first[i] = r.order;
         }
@@ -1731,36 +1738,274 @@ __global__ __launch_bounds__(256) void gen_windows_kernel(GenWinArgs a) {
     if (cnt) flush();
 }
 
+// Windows of the general path for an A/C/G/T prefix (the common case: k > 64
+// with a prefix such as ATGAC), from the raw chunk instead of the flattened
+// window space: a workgroup takes 16 KiB of the chunk, each thread its own 64
+// bytes, turned into the two bit planes of scan_planes_kernel, and the first
+// min(|P|, 5) bases of P and of rc(P) are tested at 32 positions per bit-op.
+// A candidate x (rare) is checked byte for byte against P / rc(P) (the planes
+// alias other bytes); its line is r = the newlines before x -- the tile's
+// count from chunk_lines (tbase) plus the newlines of the tile before x (a
+// block scan of the threads' newline masks) -- so no search: x is in a
+// sequence line iff r = first + 4m (the mod-4 record rule, as chunk_lines).
+// Candidates (x, m, strand) go out; gen_fix_kernel keeps those whose window
+// lies inside line m: forward window [x, x + k), reverse window
+// [x + |P| - k, x + |P|) (lib/kmers.js:88-100, 153: the reverse strand's
+// window at L - k - s).
+// Candidates are queued in LDS and written with one atomic per workgroup.
+constexpr uint32_t GC_Q = 512;                   // records queued per workgroup
+constexpr uint32_t GC_TPB = 32;                  // tiles per workgroup (one queue flush per ~32 tiles)
+
+__device__ __forceinline__ bool gen_bytes_eq(const uint8_t *d, uint64_t len, uint64_t x, const uint8_t *P,
+                                             uint32_t plen) {
+    if (x + plen > len) return false;
+    for (uint32_t b = 0; b < plen; ++b)
+        if (d[x + b] != P[b]) return false;
+    return true;
+}
+
+__global__ __launch_bounds__(256) void gen_cand_kernel(GenWinArgs a, PlaneArgs pa) {
+    __shared__ __attribute__((aligned(16))) uint8_t buf[TILE + 16];
+    __shared__ Record q[GC_Q];
+    __shared__ uint32_t qn, wsum[4];
+    __shared__ unsigned long long qbase;
+    __shared__ uint8_t sp[2 * 16];                   // P, rc(P) (|P| <= 16: verified in LDS)
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t plen = a.plen, k = a.k;
+    const bool lds_verify = plen <= 16;
+    if (lds_verify && tid < 2 * plen) sp[tid < plen ? tid : 16 + tid - plen] = tid < plen ? a.P[tid] : a.RP[tid - plen];
+    if (tid == 0) qn = 0;
+    const uint64_t ntiles = (a.len + TILE - 1) / TILE;
+    const uint64_t t0 = (uint64_t)blockIdx.x * GC_TPB, t1 = t0 + GC_TPB < ntiles ? t0 + GC_TPB : ntiles;
+    // the queue goes out with one atomic when it is half full (and at the end):
+    // one device-scope atomic on one address costs ~12 ns, serialised -- one
+    // per 16 KiB tile was 2 ms at C2 size
+    auto flush = [&]() {
+        const uint32_t nq = min(qn, GC_Q);
+        if (tid == 0 && nq) qbase = atomicAdd(a.rec_count, (unsigned long long)nq);
+        __syncthreads();
+        for (uint32_t i = tid; i < nq; i += 256) {
+            if (qbase + i < a.rec_cap) a.recs[qbase + i] = q[i];
+            else atomicOr(a.err, ERR_REC_OVERFLOW);
+        }
+        __syncthreads();
+        if (tid == 0) qn = 0;
+    };
+    for (uint64_t tile = t0; tile < t1; ++tile) {
+        const int64_t g0 = (int64_t)tile * TILE;
+        {
+            uint4 v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = load_chunk(a.data, g0 + 16 * (int64_t)(tid + TPB * i), a.len);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) *(uint4 *)(buf + 16 * (tid + TPB * i)) = v[i];
+            if (tid == 0) *(uint4 *)(buf + TILE) = load_chunk(a.data, g0 + TILE, a.len);
+        }
+        __syncthreads();
+        uint32_t w[17];
+        {
+            const uint4 *src = (const uint4 *)(buf + 64 * tid);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint4 x = src[j];
+                w[4 * j] = x.x;
+                w[4 * j + 1] = x.y;
+                w[4 * j + 2] = x.z;
+                w[4 * j + 3] = x.w;
+            }
+            w[16] = *(const uint32_t *)(buf + 64 * tid + 64);
+        }
+        // planes of the 68 bytes (as scan_planes_kernel: one v_dot4 per 8 bases and plane)
+        const uint32_t W0 = 0x08040201u;
+        uint32_t L[3], H[3];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            uint32_t gl[4], gh[4];
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const uint32_t x0 = w[8 * h + 2 * p], x1 = w[8 * h + 2 * p + 1];
+                const uint32_t y = (x0 & 0x0F0F0F0Fu) | ((x1 << 4) & 0xF0F0F0F0u);
+                gl[p] = __builtin_amdgcn_udot4(y & 0x22222222u, W0, 0u, false);
+                gh[p] = __builtin_amdgcn_udot4(y & 0x44444444u, W0, 0u, false);
+            }
+            L[h] = (gl[0] >> 1) | (gl[1] << 7) | (gl[2] << 15) | (gl[3] << 23);
+            H[h] = (gh[0] >> 2) | (gh[1] << 6) | (gh[2] << 14) | (gh[3] << 22);
+        }
+        L[2] = __builtin_amdgcn_udot4(w[16] & 0x02020202u, W0, 0u, false) >> 1;
+        H[2] = __builtin_amdgcn_udot4(w[16] & 0x04040404u, W0, 0u, false) >> 2;
+        uint32_t m4[4];                              // forward h = 0, 1; reverse h = 0, 1
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            uint32_t SL[5], SH[5];
+            SL[0] = L[h];
+            SH[0] = H[h];
+#pragma unroll
+            for (uint32_t i = 1; i < 5; ++i) {
+                SL[i] = __builtin_amdgcn_alignbit(L[h + 1], L[h], i);
+                SH[i] = __builtin_amdgcn_alignbit(H[h + 1], H[h], i);
+            }
+            m4[h] = plane_match(L[h], H[h], L[h + 1], H[h + 1], pa.kl, pa.kh, pa.pb, SL, SH);
+            m4[2 + h] = plane_match(L[h], H[h], L[h + 1], H[h + 1], pa.rl, pa.rh, pa.pb, SL, SH);
+        }
+        // newlines of this thread's 64 bytes (bit b: byte b is '\n'), and the
+        // tile's newlines before them (bytes past the chunk read as '\n': they
+        // only follow every position that is tested)
+        uint64_t nlm = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t z = w[j] ^ 0x0A0A0A0Au;
+            const uint32_t ne = (((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u;   // 0x80: not '\n'
+            nlm |= (uint64_t)__builtin_amdgcn_udot4((~ne & 0x80808080u) >> 7, W0, 0u, false) << (4 * j);
+        }
+        const uint32_t nc = (uint32_t)__popcll(nlm);
+        const uint32_t incl = wave_incl_sum(nc);
+        if (lane == 63) wsum[wid] = incl;
+        __syncthreads();
+        uint64_t r0 = a.tbase[tile] + incl - nc;                  // newlines before this thread's bytes
+        for (uint32_t v = 0; v < wid; ++v) r0 += wsum[v];
+#pragma unroll
+        for (int hs = 0; hs < 4; ++hs) {
+            uint32_t m = m4[hs];
+            const uint32_t strand = (uint32_t)hs >> 1;
+            while (m) {
+                const uint32_t bit = __ffs(m) - 1;
+                m &= m - 1;
+                const int64_t xs = g0 + 64 * (int64_t)tid + 32 * (hs & 1) + bit;
+                const uint64_t x = (uint64_t)xs;
+                if (x >= a.len) continue;
+                if (lds_verify) {                      // the tile's bytes (+ 16 of halo) are in LDS
+                    const uint32_t o = (uint32_t)(xs - g0);
+                    const uint8_t *pp = sp + (strand ? 16 : 0);
+                    uint32_t dif = 0;
+                    for (uint32_t bb = 0; bb < plen; ++bb) dif |= (uint32_t)(buf[o + bb] ^ pp[bb]);
+                    if (dif || x + plen > a.len) continue;
+                } else if (!gen_bytes_eq(a.data, a.len, x, strand ? a.RP : a.P, plen)) {
+                    continue;
+                }
+                // the line holding x: r = newlines before x; a sequence line iff r = first + 4m
+                const uint32_t b = 32 * (hs & 1) + bit;
+                const uint64_t rl = r0 + (uint64_t)__popcll(nlm & ((1ull << b) - 1ull));
+                if (rl < a.first || ((rl - a.first) & 3u) != 0) continue;
+                const uint64_t m_ = (rl - a.first) >> 2;
+                if (m_ >= a.n_lines) continue;
+                // a candidate (position, sequence ordinal, strand): gen_fix_kernel
+                // reads its line and keeps it iff the window fits
+                Record r;
+                r.pos = x;
+                r.order = m_;
+                r.len = k;
+                r.strand = strand;
+                const uint32_t qi = atomicAdd(&qn, 1u);
+                if (qi < GC_Q) {
+                    q[qi] = r;
+                } else {                                   // (a crowded tile: straight to the list)
+                    const unsigned long long gi = atomicAdd(a.rec_count, 1ull);
+                    if (gi < a.rec_cap) a.recs[gi] = r;
+                    else atomicOr(a.err, ERR_REC_OVERFLOW);
+                }
+            }
+        }
+        __syncthreads();                               // (buf and wsum are reused by the next tile)
+        if (qn >= GC_Q / 2 || tile + 1 == t1) flush();
+    }
+}
+
+// gen_cand_kernel's candidates -> records: the candidate's sequence line (one
+// load per candidate, all in flight together -- inside the tile kernel this
+// load held every wave with a candidate), the window inside it or dropped;
+// the kept records compacted with one atomic per wave
+__global__ __launch_bounds__(256) void gen_fix_kernel(const Record *__restrict__ cand, uint64_t n,
+                                                      const SeqLine *__restrict__ lines, uint32_t k, uint32_t plen,
+                                                      uint32_t pbits, Record *__restrict__ recs,
+                                                      unsigned long long *rec_count, uint64_t rec_cap,
+                                                      unsigned int *err) {
+    // a workgroup takes a contiguous range of candidates in rounds of 256,
+    // kept records queued in LDS, one atomic per GF_Q of them
+    constexpr uint32_t GF_Q = 2048;
+    __shared__ Record q[GF_Q];
+    __shared__ uint32_t qn;
+    __shared__ unsigned long long qbase;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t per = ((n + gridDim.x - 1) / gridDim.x + 255) / 256 * 256;
+    const uint64_t i0 = (uint64_t)blockIdx.x * per, i1 = i0 + per < n ? i0 + per : n;
+    if (tid == 0) qn = 0;
+    __syncthreads();
+    auto flush = [&]() {
+        const uint32_t nq = min(qn, GF_Q);
+        if (tid == 0 && nq) qbase = atomicAdd(rec_count, (unsigned long long)nq);
+        __syncthreads();
+        for (uint32_t i = tid; i < nq; i += 256) {
+            if (qbase + i < rec_cap) recs[qbase + i] = q[i];
+            else atomicOr(err, ERR_REC_OVERFLOW);
+        }
+        __syncthreads();
+        if (tid == 0) qn = 0;
+        __syncthreads();
+    };
+    for (uint64_t b = i0; b < i1; b += 256) {
+        const uint64_t i = b + tid;
+        if (i < i1) {
+            const Record c = cand[i];
+            const SeqLine sl = lines[c.order];
+            const uint64_t x = c.pos, end = sl.start + sl.len;
+            Record r;
+            r.len = k;
+            r.strand = c.strand;
+            bool keep = false;
+            if (sl.len && x >= sl.start) {
+                if (!c.strand) {
+                    keep = x + k <= end;
+                    r.order = (sl.line_index << (pbits + 1)) | (x - sl.start);
+                    r.pos = x;
+                } else {
+                    keep = x + plen <= end && x + plen >= sl.start + k;
+                    const uint64_t sp = x + plen - k - sl.start;           // window start in the line
+                    r.order = (sl.line_index << (pbits + 1)) | (1ull << pbits) | (sl.len - k - sp);
+                    r.pos = sl.start + sp;
+                }
+            }
+            if (keep) q[atomicAdd(&qn, 1u)] = r;        // (<= 256 per round, flushed below)
+        }
+        __syncthreads();
+        if (qn > GF_Q - 256 || b + 256 >= i1) flush();
+    }
+}
+
 __device__ __forceinline__ uint64_t gen_mix(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
 
-// two independent 64-bit hashes of each k-byte key, one wave per key: lane l
-// takes the key's 8-byte words l, l + 64, ...; each word is mixed with its
+// two independent 64-bit hashes of each k-byte key, GEN_G lanes per key: lane
+// l takes the key's 8-byte words l, l + GEN_G, ...; each word is mixed with its
 // position (so the sums over the lanes are position-sensitive), the mixed
-// words are summed over the wave, and the sums finalised
-__global__ __launch_bounds__(256) void gen_hash_kernel(const uint8_t *keys, uint64_t n, uint32_t k, uint64_t seed,
-                                                       uint64_t *h1, uint64_t *h2, uint32_t *idx) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t nw = (uint64_t)gridDim.x * 4;
-    for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += nw) {
-        const uint8_t *p = keys + i * k;
+// words are summed over the lanes, and the sums finalised
+__global__ __launch_bounds__(256) void gen_hash_kernel(const uint8_t *__restrict__ keys, uint64_t n, uint32_t k,
+                                                       uint64_t seed, uint64_t *__restrict__ h1,
+                                                       uint64_t *__restrict__ h2, uint32_t *__restrict__ idx) {
+    const uint32_t lane = threadIdx.x & 63, sub = lane % GEN_G;
+    const uint64_t nw = (uint64_t)gridDim.x * 4 * (64 / GEN_G);
+    const uint64_t i0 = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * (64 / GEN_G) + lane / GEN_G;
+    const uint64_t nstep = (n + nw - 1) / nw;                 // (uniform trip count: the shuffles below)
+    for (uint64_t t = 0; t < nstep; ++t) {
+        const uint64_t i = i0 + t * nw;
+        const bool live = i < n;
+        const uint8_t *p = keys + (live ? i : 0) * k;
         uint64_t a = 0, b = 0;
-        for (uint32_t j = 8 * lane; j < k; j += 512) {
+        for (uint32_t j = 8 * sub; live && j < k; j += 8 * GEN_G) {
             uint64_t w = 0;
             const uint32_t m = k - j < 8 ? k - j : 8;
-            for (uint32_t t = 0; t < m; ++t) w |= (uint64_t)p[j + t] << (8 * t);
+            for (uint32_t q = 0; q < m; ++q) w |= (uint64_t)p[j + q] << (8 * q);
             a += gen_mix(w ^ (seed + (uint64_t)j * 0x9E3779B97F4A7C15ull));
             b += gen_mix((w + 0x632BE59BD9B4E019ull) ^ (~seed + (uint64_t)j * 0xD6E8FEB86659FD93ull));
         }
 #pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            a += __shfl_xor(a, d);
-            b += __shfl_xor(b, d);
+        for (uint32_t d = GEN_G / 2; d >= 1; d >>= 1) {
+            a += __shfl_xor(a, (int)d);
+            b += __shfl_xor(b, (int)d);
         }
-        if (lane == 0) {
+        if (live && sub == 0) {
             h1[i] = gen_mix(a ^ k);
             h2[i] = gen_mix(b + k);
             idx[i] = (uint32_t)i;
@@ -1795,30 +2040,39 @@ __global__ __launch_bounds__(256) void gen_starts_kernel(const uint32_t *head, c
     }
 }
 
-// one wave per group: its key (the head's bytes, copied by the lanes), the
+// GEN_G lanes per group: its key (the head's bytes, copied by the lanes), the
 // count sum and the min first (lanes stride over the group's members)
-__global__ __launch_bounds__(256) void gen_reduce_kernel(const uint32_t *start, uint64_t ng, const uint32_t *idx,
-                                                         const uint8_t *keys, const uint64_t *cnt, const uint64_t *first,
-                                                         uint32_t k, uint8_t *okeys, uint64_t *ocnt, uint64_t *ofirst) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t nw = (uint64_t)gridDim.x * 4;
-    for (uint64_t g = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); g < ng; g += nw) {
-        const uint32_t s0 = start[g], s1 = start[g + 1];
+__global__ __launch_bounds__(256) void gen_reduce_kernel(const uint32_t *__restrict__ start, uint64_t ng,
+                                                         const uint32_t *__restrict__ idx,
+                                                         const uint8_t *__restrict__ keys,
+                                                         const uint64_t *__restrict__ cnt,
+                                                         const uint64_t *__restrict__ first, uint32_t k,
+                                                         uint8_t *__restrict__ okeys, uint64_t *__restrict__ ocnt,
+                                                         uint64_t *__restrict__ ofirst) {
+    const uint32_t lane = threadIdx.x & 63, sub = lane % GEN_G;
+    const uint64_t nw = (uint64_t)gridDim.x * 4 * (64 / GEN_G);
+    const uint64_t g0 = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * (64 / GEN_G) + lane / GEN_G;
+    const uint64_t nstep = (ng + nw - 1) / nw;                // (uniform trip count: the shuffles below)
+    for (uint64_t t = 0; t < nstep; ++t) {
+        const uint64_t g = g0 + t * nw;
+        const bool live = g < ng;
+        const uint32_t s0 = live ? start[g] : 0u, s1 = live ? start[g + 1] : 0u;
         uint64_t c = 0, f = ~0ull;
-        for (uint32_t i = s0 + lane; i < s1; i += 64) {
+        for (uint32_t i = s0 + sub; i < s1; i += GEN_G) {
             const uint32_t j = idx[i];
             c += cnt[j];
             f = min(f, first[j]);
         }
 #pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            c += __shfl_xor(c, d);
-            f = min(f, (uint64_t)__shfl_xor(f, d));
+        for (uint32_t d = GEN_G / 2; d >= 1; d >>= 1) {
+            c += __shfl_xor(c, (int)d);
+            f = min(f, (uint64_t)__shfl_xor(f, (int)d));
         }
+        if (!live) continue;
         const uint8_t *src = keys + (uint64_t)idx[s0] * k;
         uint8_t *o = okeys + g * k;
-        for (uint32_t b = lane; b < k; b += 64) o[b] = src[b];
-        if (lane == 0) {
+        for (uint32_t b = sub; b < k; b += GEN_G) o[b] = src[b];
+        if (sub == 0) {
             ocnt[g] = c;
             ofirst[g] = f;
         }
@@ -2015,12 +2269,11 @@ __device__ __forceinline__ void put_seq_line(uint64_t st, uint64_t en, uint64_t 
                                              unsigned int *err) {
     SeqLine sl;
     sl.line_index = li;
-    sl.start = 0;
+    sl.start = st;                 // (also without windows: the starts stay ascending -- gen_cand_kernel searches them)
     sl.len = 0;
     uint64_t w2 = 0;
     const uint64_t L = en > st ? en - st : 0;
     if (L > 1 && L >= k) {
-        sl.start = st;
         sl.len = L;
         const uint64_t W = L - k + 1;
         // (err null: no order key, no limit)
@@ -2077,8 +2330,8 @@ __global__ __launch_bounds__(256) void seq_lines_kernel(const uint64_t *nl, uint
             const uint64_t st = r == 0 ? 0 : nl[r - 1] + 1;
             const uint64_t en = r < n_nl ? nl[r] : len;    // (r == n_nl: the open trailing segment)
             const uint64_t L = en > st ? en - st : 0;
+            sl.start = st;                                 // (ascending starts, as put_seq_line)
             if (L > 1 && L >= k) {
-                sl.start = st;
                 sl.len = L;
                 const uint64_t W = L - k + 1;
                 // (err null: no order key, no limit)
@@ -2881,17 +3134,18 @@ __global__ __launch_bounds__(256) void gather_records_kernel(const Record *recs,
 // Ordered merge of per-rank result lists: row i of the output is source row
 // idx[i] (k-byte key, count, first-occurrence key).  One thread per row; keys
 // copied 4 bytes at a time when k allows.
-// out row i = in row idx[i] (k-byte keys with their count and first): a wave
-// copies 64 / k rows at a time (k <= 64; lane = row * k + byte) or one row
-// (k > 64, lanes stride over its bytes), so the byte loads and stores of a
-// wave are contiguous runs instead of one thread walking a whole row
-__global__ __launch_bounds__(256) void permute_rows_kernel(const uint8_t *keys, const uint64_t *cnt,
-                                                           const uint64_t *first, const uint32_t *idx, uint64_t n,
-                                                           uint32_t k, uint8_t *okeys, uint64_t *ocnt,
-                                                           uint64_t *ofirst) {
+// out row i = in row idx[i] (k-byte keys with their count and first): G lanes
+// per row (G = k for k <= 8, else GEN_G), 64 / G rows per wave step, lanes
+// striding over the row's bytes -- several rows' loads in flight per wave
+__global__ __launch_bounds__(256) void permute_rows_kernel(const uint8_t *__restrict__ keys,
+                                                           const uint64_t *__restrict__ cnt,
+                                                           const uint64_t *__restrict__ first,
+                                                           const uint32_t *__restrict__ idx, uint64_t n, uint32_t k,
+                                                           uint8_t *__restrict__ okeys, uint64_t *__restrict__ ocnt,
+                                                           uint64_t *__restrict__ ofirst) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t rpw = k <= 64 ? 64 / k : 1u;            // rows per wave step
-    const uint32_t r = k <= 64 ? lane / k : 0u, b0 = k <= 64 ? lane % k : lane;
+    const uint32_t G = k <= GEN_G ? k : GEN_G, rpw = 64 / G;   // rows per wave step
+    const uint32_t r = lane / G, b0 = lane % G;
     const uint64_t nw = (uint64_t)gridDim.x * 4;
     for (uint64_t w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); w * rpw < n; w += nw) {
         const uint64_t i = w * rpw + r;
@@ -2899,7 +3153,7 @@ __global__ __launch_bounds__(256) void permute_rows_kernel(const uint8_t *keys, 
         const uint64_t j = idx[i];
         const uint8_t *src = keys + j * k;
         uint8_t *dst = okeys + i * k;
-        for (uint32_t b = b0; b < k; b += 64) dst[b] = src[b];
+        for (uint32_t b = b0; b < k; b += G) dst[b] = src[b];
         if (b0 == 0) {
             ocnt[i] = cnt[j];
             ofirst[i] = first[j];
@@ -2911,7 +3165,7 @@ hipError_t launch_permute_rows(const uint8_t *keys, const uint64_t *cnt, const u
                                uint64_t n, uint32_t k, uint8_t *okeys, uint64_t *ocnt, uint64_t *ofirst,
                                hipStream_t s) {
     if (n == 0 || k == 0) return hipSuccess;
-    const uint64_t rpw = k <= 64 ? 64 / k : 1;
+    const uint64_t rpw = 64 / (k <= GEN_G ? k : GEN_G);
     uint64_t blocks = ((n + rpw - 1) / rpw + 3) / 4;
     if (blocks > 16384) blocks = 16384;
     hipLaunchKernelGGL(permute_rows_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, keys, cnt, first, idx, n, k,
@@ -3052,6 +3306,23 @@ static uint32_t grid_for(uint64_t n) {
     return (uint32_t)(blocks ? blocks : 1);
 }
 
+hipError_t launch_gen_cand(const GenWinArgs &a, const PlaneArgs &pa, hipStream_t s) {
+    if (a.len == 0 || a.n_lines == 0) return hipSuccess;
+    const uint64_t tiles = (a.len + TILE - 1) / TILE;
+    hipLaunchKernelGGL(gen_cand_kernel, dim3((uint32_t)((tiles + GC_TPB - 1) / GC_TPB)), dim3(256), 0, s, a, pa);
+    return hipGetLastError();
+}
+
+hipError_t launch_gen_fix(const Record *cand, uint64_t n, const SeqLine *lines, uint32_t k, uint32_t plen,
+                          uint32_t pbits, Record *recs, unsigned long long *rec_count, uint64_t rec_cap,
+                          unsigned int *err, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint64_t blocks = std::min<uint64_t>(2048, (n + 4095) / 4096);   // >= 4 K candidates per workgroup
+    hipLaunchKernelGGL(gen_fix_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, cand, n, lines, k, plen, pbits, recs,
+                       rec_count, rec_cap, err);
+    return hipGetLastError();
+}
+
 hipError_t launch_gen_windows(const GenWinArgs &a, hipStream_t s) {
     if (a.total == 0) return hipSuccess;
     const uint64_t waves = std::min<uint64_t>(65536, (a.total / 2 + 255) / 256);   // >= 256 positions per wave
@@ -3062,14 +3333,14 @@ hipError_t launch_gen_windows(const GenWinArgs &a, hipStream_t s) {
 hipError_t launch_gen_append(const Record *recs, uint64_t n, const uint8_t *data, uint32_t k, uint8_t *keys,
                              uint64_t *cnt, uint64_t *first, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(gen_append_kernel, dim3(grid_for(64 * n)), dim3(256), 0, s, recs, n, data, k, keys, cnt, first);
+    hipLaunchKernelGGL(gen_append_kernel, dim3(grid_for(GEN_G * n)), dim3(256), 0, s, recs, n, data, k, keys, cnt, first);
     return hipGetLastError();
 }
 
 hipError_t launch_gen_hash(const uint8_t *keys, uint64_t n, uint32_t k, uint64_t seed, uint64_t *h1, uint64_t *h2,
                            uint32_t *idx, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(gen_hash_kernel, dim3(grid_for(64 * n)), dim3(256), 0, s, keys, n, k, seed, h1, h2, idx);
+    hipLaunchKernelGGL(gen_hash_kernel, dim3(grid_for(GEN_G * n)), dim3(256), 0, s, keys, n, k, seed, h1, h2, idx);
     return hipGetLastError();
 }
 
@@ -3090,7 +3361,7 @@ hipError_t launch_gen_reduce(const uint32_t *start, uint64_t ng, const uint32_t 
                              const uint64_t *cnt, const uint64_t *first, uint32_t k, uint8_t *okeys, uint64_t *ocnt,
                              uint64_t *ofirst, hipStream_t s) {
     if (ng == 0) return hipSuccess;
-    hipLaunchKernelGGL(gen_reduce_kernel, dim3(grid_for(64 * ng)), dim3(256), 0, s, start, ng, idx, keys, cnt, first, k,
+    hipLaunchKernelGGL(gen_reduce_kernel, dim3(grid_for(GEN_G * ng)), dim3(256), 0, s, start, ng, idx, keys, cnt, first, k,
                        okeys, ocnt, ofirst);
     return hipGetLastError();
 }

@@ -31,20 +31,22 @@ def _reads_with_n(seed, n, p_n=0.002):
 
 
 @pytest.mark.parametrize("k,prefix", [(65, b"ATGAC"), (80, b"A"), (150, b""), (100, b"ATG"), (70, b"NNA"),
-                                      (40, b""), (64, b"")])
+                                      (40, b""), (64, b""), (70, b"ATGACGTTCA"), (66, b"GTCAT")])
 def test_general_device_merge_vs_oracle(native, k, prefix):
     # synthetic reads with N bytes (non-ACGT windows are keys like any other:
-    # the merge works on bytes); one feed, then batches of 1 MiB
+    # the merge works on bytes); one feed, then batches of 1 MiB.  An A/C/G/T
+    # prefix takes the plane-candidate windows kernel, FLAG_BYTE_SCAN the
+    # flattened one (both against the oracle)
     from oracle import oracle
     data = _reads_with_n(k, 12000)
     want = oracle.count_buffer(data, prefix, k, 1)
-    for batch in (0, 1 << 20):
-        ctr = native.Counter(k=k, prefix=prefix, batch_bytes=batch)
+    for batch, flags in ((0, 0), (1 << 20, 0), (0, native.FLAG_BYTE_SCAN)):
+        ctr = native.Counter(k=k, prefix=prefix, batch_bytes=batch, flags=flags)
         res = ctr.count_buffer(data)
         got = res.entries()
         ctr.close()
-        assert len(got) == len(want), (k, prefix, batch)
-        assert first_diff(got, want) is None, (k, prefix, batch)
+        assert len(got) == len(want), (k, prefix, batch, flags)
+        assert first_diff(got, want) is None, (k, prefix, batch, flags)
         assert res.lines == data.count(b"\n")
 
 
