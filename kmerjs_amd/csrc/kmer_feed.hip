@@ -884,6 +884,7 @@ kmer_status reset(kmer_ctx *c) {
     c->t_keys = 0;
     c->t_fill = 0;
     c->gm_n = 0;
+    c->gm_last = 0;
     c->gm_merged = true;
     c->t_cbase.clear();
     c->t_coff.clear();

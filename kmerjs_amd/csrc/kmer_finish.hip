@@ -265,7 +265,9 @@ constexpr uint64_t GM_MERGE_AT = 1ull << 25;   // entries held before an interme
 // a chunk's records (c->recs) -> session entries (key bytes, count 1, first)
 kmer_status general_append(kmer_ctx *c, const uint8_t *d, uint64_t nrec, hipStream_t s) {
     const uint64_t k = c->p.k;
-    if (c->gm_n && c->gm_n + nrec > GM_MERGE_AT) {
+    // (an intermediate merge when the entries reach twice the last merge's
+    // output: distinct-heavy inputs are not re-sorted once per 2^25 entries)
+    if (c->gm_n && c->gm_n + nrec > std::max<uint64_t>(GM_MERGE_AT, 2 * c->gm_last)) {
         kmer_status st = general_merge(c);
         if (st) return st;
     }
@@ -345,6 +347,7 @@ kmer_status general_merge(kmer_ctx *c) {
         std::swap(c->gm_cnt, c->gm_cnt2);
         std::swap(c->gm_first, c->gm_first2);
         c->gm_n = ng;
+        c->gm_last = ng;
         c->gm_merged = true;
         if (c->p.max_keys && ng + c->exotic.size() > c->p.max_keys)
             return fail(c, KMER_E_TOO_MANY_KEYS, "more distinct keys than max_keys (reference Map limit)");

@@ -267,6 +267,7 @@ struct kmer_ctx {
     // session entries -- key bytes at stride k, counts, first-occurrence keys
     bool gm_on = false;
     bool gm_merged = true;         // entries unique (merged since the last append)
+    uint64_t gm_last = 0;          // entries after the last merge
     uint64_t gm_n = 0;
     DBuf<uint8_t> gm_keys, gm_keys2;
     DBuf<uint64_t> gm_cnt, gm_cnt2, gm_first, gm_first2, gm_h1, gm_h2, gm_h1b, gm_h2b;

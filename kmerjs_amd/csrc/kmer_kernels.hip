@@ -1630,8 +1630,11 @@ __global__ __launch_bounds__(256) void gen_windows_kernel(GenWinArgs a) {
     const uint64_t nw = (uint64_t)gridDim.x * 4, gw = (uint64_t)blockIdx.x * 4 + wv;
     uint64_t f = npos * gw / nw;
     const uint64_t fend = npos * (gw + 1) / nw;
-    if (f >= fend) return;
     const uint32_t k = a.k, plen = a.plen;
+    // (no prefix: every window is a record, at slots 2g / 2g + 1 of its
+    // flattened position g -- the host sized the list to the total)
+    if (plen == 0 && gw == 0 && lane == 0) *a.rec_count = a.total;
+    if (f >= fend) return;
     const uint64_t P8 = gen_load8(a.P, plen < 8 ? plen : 8), R8 = gen_load8(a.RP, plen < 8 ? plen : 8);
     // first line: the last li with wbase[li] / 2 <= f
     uint64_t lo = 0, hi = a.n_lines;                 // invariant: wbase[lo] / 2 <= f < wbase[hi] / 2 (hi: +inf)
@@ -1665,11 +1668,12 @@ __global__ __launch_bounds__(256) void gen_windows_kernel(GenWinArgs a) {
         constexpr int U = 1;                     // steps per iteration (4: slower, 8.4 vs 6.8 ms at k = 70)
         const uint32_t n0 = plen < 8 ? plen : 8;
         while (f < fe) {
-            uint64_t st[U], s[U], L[U], lidx[U], wf[U], wr[U];
+            uint64_t st[U], s[U], L[U], lidx[U], wf[U], wr[U], gg[U];
             bool act[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint64_t g = f + 64 * u + lane;
+                gg[u] = g;
                 act[u] = g < fe;
                 // lane's line: the last j with B_j <= g, 6 shuffle steps
                 j = 0;
@@ -1694,6 +1698,21 @@ __global__ __launch_bounds__(256) void gen_windows_kernel(GenWinArgs a) {
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
+                if (plen == 0) {                     // every window: position g's records at 2g, 2g + 1 (no queue)
+                    if (act[u]) {
+                        const uint64_t lo_key = lidx[u] << (a.pbits + 1);
+                        Record r;
+                        r.order = lo_key | s[u];
+                        r.pos = st[u] + s[u];
+                        r.len = k;
+                        r.strand = 0;
+                        a.recs[2 * gg[u]] = r;
+                        r.order = lo_key | (1ull << a.pbits) | (L[u] - k - s[u]);
+                        r.strand = 1;
+                        a.recs[2 * gg[u] + 1] = r;
+                    }
+                    continue;
+                }
                 bool fw = act[u] && wf[u] == P8, rv = act[u] && wr[u] == R8;
                 if (plen > 8) {                      // (long prefixes: the rest byte for byte)
                     const uint8_t *line = a.data + st[u];

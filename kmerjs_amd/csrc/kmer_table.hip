@@ -749,6 +749,39 @@ namespace {
 
 // LDS slot of a remainder: its low bits are weak (a product's low bits see
 // only the code's low bits), so the slot comes from a second multiply's top bits
+// A final workgroup's Map statistics -> 3 device atomics per WORKGROUP (wave
+// sums through LDS): device-scope atomics on one line serialise (~12 ns each),
+// and every wave of the grid reaches this point at about the same time
+__device__ __forceinline__ void tab_stats_out(unsigned long long *stats, uint64_t c, uint64_t kk, uint64_t sm,
+                                              uint32_t waves) {
+    __shared__ unsigned long long red[16][3];
+    for (int d = 32; d >= 1; d >>= 1) {
+        c += __shfl_xor(c, d);
+        kk += __shfl_xor(kk, d);
+        sm += __shfl_xor(sm, d);
+    }
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) {
+        red[w][0] = c;
+        red[w][1] = kk;
+        red[w][2] = sm;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t0 = 0, t1 = 0, t2 = 0;
+        for (uint32_t v = 0; v < waves; ++v) {
+            t0 += red[v][0];
+            t1 += red[v][1];
+            t2 += red[v][2];
+        }
+        if (t0) {
+            atomicAdd(&stats[0], t0);
+            atomicAdd(&stats[1], t1);
+            atomicAdd(&stats[2], t2);
+        }
+    }
+}
+
 __device__ __forceinline__ uint32_t tab_slot(uint64_t rem) {
     return (uint32_t)((rem * TAB_MUL) >> 51) & (TAB_SLOTS - 1);
 }
@@ -1220,17 +1253,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
     }
     if (prof)
         for (int i = 0; i < 6; ++i) a.prof[blockIdx.x * 8 + i] = pt[i];
-    // workgroup totals -> one atomic per wave
-    for (int d = 32; d >= 1; d >>= 1) {
-        st_canon += __shfl_xor(st_canon, d);
-        st_keys += __shfl_xor(st_keys, d);
-        st_sum += __shfl_xor(st_sum, d);
-    }
-    if (lane == 0 && st_canon) {
-        atomicAdd(&a.stats[0], (unsigned long long)st_canon);
-        atomicAdd(&a.stats[1], (unsigned long long)st_keys);
-        atomicAdd(&a.stats[2], (unsigned long long)st_sum);
-    }
+    tab_stats_out(a.stats, st_canon, st_keys, st_sum, TAB_FWG / 64);
 }
 
 // ---------------------------------------------------------------------------
@@ -1518,16 +1541,7 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
         for (uint32_t i = t; i < g; i += TAB_SWG) a.nd[q + i] = nout[i];
         q = qe;
     }
-    for (int d = 32; d >= 1; d >>= 1) {
-        st_canon += __shfl_xor(st_canon, d);
-        st_keys += __shfl_xor(st_keys, d);
-        st_sum += __shfl_xor(st_sum, d);
-    }
-    if (lane == 0 && st_canon) {
-        atomicAdd(&a.stats[0], (unsigned long long)st_canon);
-        atomicAdd(&a.stats[1], (unsigned long long)st_keys);
-        atomicAdd(&a.stats[2], (unsigned long long)st_sum);
-    }
+    tab_stats_out(a.stats, st_canon, st_keys, st_sum, TAB_SWG / 64);
 }
 
 // ---------------------------------------------------------------------------
