@@ -265,6 +265,8 @@ kmer_status kmer_close(kmer_ctx *c) {
     c->keys_out.release();
     c->recs.release();
     c->gcand.release();
+    c->cpcnt.release();
+    c->cpoff.release();
     c->lines.release();
     c->rec_keys.release();
     c->tmp.release();

@@ -107,14 +107,6 @@ kmer_status bucket_heads(kmer_ctx *c, uint64_t n) {
     return KMER_OK;
 }
 
-struct KeyValid32 {
-    uint32_t inv;
-    __host__ __device__ bool operator()(uint32_t k) const { return k != inv; }
-};
-struct KeyValid64 {
-    uint64_t inv;
-    __host__ __device__ bool operator()(uint64_t k) const { return k != inv; }
-};
 
 // Dense-hit path with a prefix: every window of a sequence line holds a rank
 // slot and the windows that do not start with the prefix (or its reverse
@@ -126,32 +118,28 @@ kmer_status compact_windows(kmer_ctx *c) {
     const uint64_t n = c->n_hits;
     if (n == 0) return KMER_OK;
     const uint64_t invalid = c->kbits >= 63 ? ~0ull : (1ull << c->kbits);
-    HIPCHK(c, c->ridx2.ensure(n, s));
-    HIPCHK(c, c->csel.ensure(1, s));
-    rocprim::counting_iterator<uint32_t> iota(0u);
-    if (c->narrow) {
-        auto fl = rocprim::make_transform_iterator(c->rkey32.p, KeyValid32{(uint32_t)invalid});
-        ROCPRIM_RUN(c, rocprim::select(t, b, iota, fl, c->ridx2.p, c->csel.p, (size_t)n, s));
-    } else {
-        auto fl = rocprim::make_transform_iterator(c->rkey.p, KeyValid64{invalid});
-        ROCPRIM_RUN(c, rocprim::select(t, b, iota, fl, c->ridx2.p, c->csel.p, (size_t)n, s));
-    }
-    HIPCHK(c, hipMemcpyAsync(c->h_small + 20, c->csel.p, 8, hipMemcpyDeviceToHost, s));
+    const uint64_t nb = (n + CP_BLOCK - 1) / CP_BLOCK;
+    // per-workgroup counts -> offsets (+ the total at [nb]) -> valid pairs written in rank order
+    HIPCHK(c, c->cpcnt.ensure(nb + 1, s));
+    HIPCHK(c, c->cpoff.ensure(nb + 1, s));
+    HIPCHK(c, hipMemsetAsync(c->cpcnt.p + nb, 0, sizeof(uint32_t), s));
+    const uint32_t *k32 = c->narrow ? c->rkey32.p : nullptr;
+    const uint64_t *k64 = c->narrow ? nullptr : c->rkey.p;
+    HIPCHK(c, launch_compact_count(k32, k64, n, invalid, c->cpcnt.p, s));
+    ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->cpcnt.p, c->cpoff.p, (uint64_t)0, (size_t)nb + 1,
+                                           rocprim::plus<uint64_t>(), s));
+    HIPCHK(c, hipMemcpyAsync(c->h_small + 20, c->cpoff.p + nb, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     const uint64_t n2 = c->h_small[20];
     if (n2 >= n) return KMER_OK;
-    // gathered into the second buffers, copied back (the session buffers keep their size)
-    if (c->narrow) {
-        HIPCHK(c, c->rkey32b.ensure(n2 + 1, s));
-        HIPCHK(c, launch_gather_u32(c->rkey32.p, c->ridx2.p, n2, c->rkey32b.p, s));
-        HIPCHK(c, hipMemcpyAsync(c->rkey32.p, c->rkey32b.p, n2 * 4, hipMemcpyDeviceToDevice, s));
-    } else {
-        HIPCHK(c, c->rkey2.ensure(n2 + 1, s));
-        HIPCHK(c, launch_gather_u64(c->rkey.p, c->ridx2.p, n2, c->rkey2.p, s));
-        HIPCHK(c, hipMemcpyAsync(c->rkey.p, c->rkey2.p, n2 * 8, hipMemcpyDeviceToDevice, s));
-    }
+    // written into the second buffers, copied back (the session buffers keep their size)
+    if (c->narrow) HIPCHK(c, c->rkey32b.ensure(n2 + 1, s));
+    else HIPCHK(c, c->rkey2.ensure(n2 + 1, s));
     HIPCHK(c, c->rord2.ensure(n2 + 1, s));
-    HIPCHK(c, launch_gather_u64(c->rord.p, c->ridx2.p, n2, c->rord2.p, s));
+    HIPCHK(c, launch_compact_write(k32, k64, c->rord.p, n, invalid, c->cpoff.p, c->narrow ? c->rkey32b.p : nullptr,
+                                   c->narrow ? nullptr : c->rkey2.p, c->rord2.p, s));
+    if (c->narrow) HIPCHK(c, hipMemcpyAsync(c->rkey32.p, c->rkey32b.p, n2 * 4, hipMemcpyDeviceToDevice, s));
+    else HIPCHK(c, hipMemcpyAsync(c->rkey.p, c->rkey2.p, n2 * 8, hipMemcpyDeviceToDevice, s));
     HIPCHK(c, hipMemcpyAsync(c->rord.p, c->rord2.p, n2 * 8, hipMemcpyDeviceToDevice, s));
     c->n_hits = n2;
     return KMER_OK;

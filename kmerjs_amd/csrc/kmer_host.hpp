@@ -184,6 +184,8 @@ struct kmer_ctx {
     DBuf<uint8_t> keys_out;
     uint64_t n_out = 0;            // ordered entries of the last finish (device)
     // records & lines
+    DBuf<uint32_t> cpcnt;          // dense-hit compaction: valid ranks per CP_BLOCK
+    DBuf<uint64_t> cpoff;          // ... their offsets (+ total)
     DBuf<Record> recs;
     DBuf<Record> gcand;            // general path, A/C/G/T prefix: window candidates (gen_cand_kernel)
     DBuf<SeqLine> lines;

@@ -378,6 +378,12 @@ constexpr uint64_t EMIT_DIRECT_MAX = 4096;   // emit workgroups that sum the ear
 // prefilled with 1, as launch_heads_sparse)
 hipError_t launch_gather_u64(const uint64_t *src, const uint32_t *idx, uint64_t n, uint64_t *dst, hipStream_t s);
 hipError_t launch_gather_u32(const uint32_t *src, const uint32_t *idx, uint64_t n, uint32_t *dst, hipStream_t s);
+constexpr uint64_t CP_BLOCK = 4096;   // ranks per compaction workgroup (compact_count / compact_write)
+hipError_t launch_compact_count(const uint32_t *k32, const uint64_t *k64, uint64_t n, uint64_t invalid, uint32_t *bcnt,
+                                hipStream_t s);
+hipError_t launch_compact_write(const uint32_t *k32, const uint64_t *k64, const uint64_t *ord, uint64_t n,
+                                uint64_t invalid, const uint64_t *boff, uint32_t *o32, uint64_t *o64, uint64_t *oord,
+                                hipStream_t s);
 hipError_t launch_cross_wide_fix(const uint32_t *xslot, uint64_t n, const uint64_t *xkeyl, const uint64_t *xkeyh,
                                  uint64_t *rkey, uint64_t *rkeyh, hipStream_t s);
 hipError_t launch_heads_wide(const uint64_t *shi, const uint64_t *slo, const uint32_t *srank, uint64_t n,

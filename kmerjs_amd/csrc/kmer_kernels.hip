@@ -2151,10 +2151,13 @@ __device__ __forceinline__ void win_record(const WinArgs &a, uint64_t order, uin
     }
 }
 
+// (an invalid key's order is never read -- compaction, exchange and the heads
+// read orders at valid ranks only -- so it is not written: at C2 size with a
+// 2-base prefix that skips 20 GB of stores)
 __device__ __forceinline__ void win_place(const WinArgs &a, uint64_t rank, uint64_t key, uint64_t order) {
     if (a.rkey32) a.rkey32[rank] = (uint32_t)key;
     else a.rkey[rank] = key;
-    a.rord[rank] = order;
+    if (key != a.invalid_key) a.rord[rank] = order;
 }
 
 // ---- sequence lines of a chunk without look-back (dense-hit path) ----
@@ -3404,6 +3407,89 @@ hipError_t launch_cross_segsort(uint64_t *ord, uint64_t *key, const uint32_t *sl
                               rord, pbits + 1);
     return hipGetLastError();
 }
+// ---------------------------------------------------------------------------
+// compaction of the dense-hit rank arrays (keys != invalid, in rank order):
+// count per 4,096 ranks, scan, then each workgroup writes its valid (key,
+// order) pairs at its offset + rank among them (row-major ballots) -- the
+// keys read twice, the orders only where valid; a library select over an
+// index iterator and two gathers took 39 ms for 2.7 G windows (C2, prefix AT)
+// ---------------------------------------------------------------------------
+constexpr uint32_t CP_ROWS = 16;                 // rows of 256 ranks per workgroup
+
+template <typename K>
+__global__ __launch_bounds__(256) void compact_count_kernel(const K *__restrict__ key, uint64_t n, K invalid,
+                                                            uint32_t *__restrict__ bcnt) {
+    __shared__ uint32_t ws[4];
+    const uint64_t base = (uint64_t)blockIdx.x * (256 * CP_ROWS);
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < CP_ROWS; ++j) {
+        const uint64_t i = base + 256 * j + threadIdx.x;
+        c += (i < n && key[i] != invalid) ? 1u : 0u;
+    }
+    c = wave_incl_sum(c);
+    if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) bcnt[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+template <typename K>
+__global__ __launch_bounds__(256) void compact_write_kernel(const K *__restrict__ key, const uint64_t *__restrict__ ord,
+                                                            uint64_t n, K invalid, const uint64_t *__restrict__ boff,
+                                                            K *__restrict__ okey, uint64_t *__restrict__ oord) {
+    __shared__ uint32_t wc[CP_ROWS * 4];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t base = (uint64_t)blockIdx.x * (256 * CP_ROWS);
+    K kv[CP_ROWS];
+    uint32_t below[CP_ROWS];
+    bool v[CP_ROWS];
+#pragma unroll
+    for (uint32_t j = 0; j < CP_ROWS; ++j) {
+        const uint64_t i = base + 256 * j + threadIdx.x;
+        kv[j] = i < n ? key[i] : invalid;
+        v[j] = kv[j] != invalid;
+        const unsigned long long m = __ballot(v[j]);
+        below[j] = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (lane == 0) wc[4 * j + w] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {                            // exclusive scan of the 64 (row, wave) counts
+        const uint32_t x = wc[threadIdx.x];
+        const uint32_t inc = wave_incl_sum(x);
+        wc[threadIdx.x] = inc - x;
+    }
+    __syncthreads();
+    const uint64_t o0 = boff[blockIdx.x];
+#pragma unroll
+    for (uint32_t j = 0; j < CP_ROWS; ++j) {
+        if (!v[j]) continue;
+        const uint64_t i = base + 256 * j + threadIdx.x;
+        const uint64_t o = o0 + wc[4 * j + w] + below[j];
+        okey[o] = kv[j];
+        oord[o] = ord[i];
+    }
+}
+
+hipError_t launch_compact_count(const uint32_t *k32, const uint64_t *k64, uint64_t n, uint64_t invalid, uint32_t *bcnt,
+                                hipStream_t s) {
+    const uint64_t nb = (n + 256 * CP_ROWS - 1) / (256 * CP_ROWS);
+    if (k32) hipLaunchKernelGGL(compact_count_kernel<uint32_t>, dim3((uint32_t)nb), dim3(256), 0, s, k32, n,
+                                (uint32_t)invalid, bcnt);
+    else hipLaunchKernelGGL(compact_count_kernel<uint64_t>, dim3((uint32_t)nb), dim3(256), 0, s, k64, n, invalid, bcnt);
+    return hipGetLastError();
+}
+
+hipError_t launch_compact_write(const uint32_t *k32, const uint64_t *k64, const uint64_t *ord, uint64_t n,
+                                uint64_t invalid, const uint64_t *boff, uint32_t *o32, uint64_t *o64, uint64_t *oord,
+                                hipStream_t s) {
+    const uint64_t nb = (n + 256 * CP_ROWS - 1) / (256 * CP_ROWS);
+    if (k32) hipLaunchKernelGGL(compact_write_kernel<uint32_t>, dim3((uint32_t)nb), dim3(256), 0, s, k32, ord, n,
+                                (uint32_t)invalid, boff, o32, oord);
+    else hipLaunchKernelGGL(compact_write_kernel<uint64_t>, dim3((uint32_t)nb), dim3(256), 0, s, k64, ord, n, invalid,
+                            boff, o64, oord);
+    return hipGetLastError();
+}
+
 hipError_t launch_gather_u32(const uint32_t *src, const uint32_t *idx, uint64_t n, uint32_t *dst, hipStream_t s) {
     if (n) hipLaunchKernelGGL(gather_u32_kernel, dim3(grid_for(n)), dim3(256), 0, s, src, idx, n, dst);
     return hipGetLastError();
