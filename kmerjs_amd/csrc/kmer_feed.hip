@@ -747,6 +747,7 @@ kmer_status windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n
     w.smask = (c->kbits >= 64) ? ~0ull : ((1ull << c->kbits) - 1ull);
     w.invalid_key = c->kbits >= 63 ? ~0ull : (1ull << c->kbits);
     w.out_base = c->n_hits;
+    w.block_lines = total > 1024 * n_seq ? 1u : 0u;   // (> 512 windows per strand and line on average)
     w.rkey = c->rkey.p;
     w.rkey32 = c->narrow ? c->rkey32.p : nullptr;
     w.rord = c->rord.p;

@@ -330,6 +330,7 @@ struct WinArgs {
     uint64_t pcode, rcode;         // P and rc(P) as 2-bit codes (first base most significant)
     uint64_t smask, invalid_key;
     uint64_t out_base;
+    uint32_t block_lines;          // lines of many windows (contigs): a workgroup per line, else a wave
     uint64_t *rkey;
     uint32_t *rkey32;
     uint64_t *rord;

@@ -2383,16 +2383,19 @@ __global__ void pos_after_kernel(StreamPos *pos, uint64_t lines, const uint8_t *
 // past L it is "" -- the short keys become records, the empty ones a count.
 // Order keys: step 1, line | strand | (strand ? maxrel - s : s) as on the
 // tile path; step > 1, line | strand | j (the loop index) on both strands.
-// One WAVE per sequence line (4 lines in flight per workgroup, the next
-// line's descriptor loaded while the current one is written): a workgroup
-// per line left half its lanes idle on 150-byte reads and walked its lines
-// one dependent chain at a time (21.8 ms at C2 size, prefix AT)
+// One WAVE per sequence line for reads (4 lines in flight per workgroup, the
+// next line's descriptor loaded while the current one is written: a
+// workgroup per line left half its lanes idle on 150-byte reads and walked
+// its lines one dependent chain at a time, 21.8 ms at C2 size, prefix AT);
+// one WORKGROUP per line when the lines are long (contigs: a few thousand
+// lines would leave most of the chip idle with a wave each)
 __global__ __launch_bounds__(256) void windows_packed_kernel(WinArgs a) {
     const uint32_t k = a.k, plen = a.plen;
     const uint32_t tailbits = 2 * (k - plen);
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t nwv = (uint64_t)gridDim.x * 4;
-    uint64_t li = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const bool bl = a.block_lines != 0;
+    const uint32_t lane = bl ? threadIdx.x : (threadIdx.x & 63), LW = bl ? 256u : 64u;
+    const uint64_t nwv = bl ? (uint64_t)gridDim.x : (uint64_t)gridDim.x * 4;
+    uint64_t li = bl ? (uint64_t)blockIdx.x : (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     SeqLine nxt = {0, 0, 0};
     if (li < a.n_lines) nxt = a.lines[li];
     for (; li < a.n_lines; li += nwv) {
@@ -2406,7 +2409,7 @@ __global__ __launch_bounds__(256) void windows_packed_kernel(WinArgs a) {
         const uint64_t lo = sl.line_index << (a.pbits + 1);
         const uint32_t step = a.step;
         const uint64_t Ws = (W + step - 1) / step;   // windows per strand
-        for (uint64_t s = lane; s < W; s += 64) {
+        for (uint64_t s = lane; s < W; s += LW) {
             const bool fw = step == 1 || s % step == 0, rv = step == 1 || (W - 1 - s) % step == 0;
             if (!fw && !rv) continue;
             const uint64_t pos = sl.start + s;
@@ -2440,7 +2443,7 @@ __global__ __launch_bounds__(256) void windows_packed_kernel(WinArgs a) {
         if (step == 1 || Ws >= W) continue;
         // indices j in [Ws, W) of each strand: p = j * step > L - k
         const uint64_t L = sl.len, ntail = W - Ws;
-        for (uint64_t t = lane; t < 2 * ntail; t += 64) {
+        for (uint64_t t = lane; t < 2 * ntail; t += LW) {
             const uint32_t strand = t >= ntail ? 1u : 0u;
             const uint64_t j = Ws + (strand ? t - ntail : t), p = j * step;
             if (p >= L) continue;                    // "": counted below
@@ -3651,8 +3654,9 @@ hipError_t launch_pos_after(StreamPos *pos, uint64_t lines, const uint8_t *data,
 }
 hipError_t launch_windows_packed(const WinArgs &a, hipStream_t s) {
     if (a.n_lines) {
-        const uint64_t w = a.n_lines < 262144 ? a.n_lines : 262144;   // waves (one line each at a time)
-        hipLaunchKernelGGL(windows_packed_kernel, dim3((uint32_t)((w + 3) / 4)), dim3(256), 0, s, a);
+        const uint64_t cap = a.block_lines ? 65536 : 262144;          // workgroups / waves, one line each at a time
+        const uint64_t w = a.n_lines < cap ? a.n_lines : cap;
+        hipLaunchKernelGGL(windows_packed_kernel, dim3((uint32_t)(a.block_lines ? w : (w + 3) / 4)), dim3(256), 0, s, a);
     }
     return hipGetLastError();
 }
