@@ -98,17 +98,38 @@ kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done
     hp[0] = 0;
     double sig = 2.0;                          // (KMERHIP_TAB_SIGMA: A/B experiments)
     if (const char *e = exp_env("KMERHIP_TAB_SIGMA")) sig = atof(e);
-    for (uint32_t w = 0; w < a.nwg; ++w) {
-        const double mu = (double)hw[w] / TAB_NB;
-        hp[w + 1] = hp[w] + (hw[w] ? ((uint64_t)(mu + sig * std::sqrt(mu)) + 4 + 7) & ~7ull : 0);
-        tot += hw[w];
+    for (uint32_t w = 0; w < a.nwg; ++w) tot += hw[w];
+    auto sized = [&](const std::vector<uint64_t> &ww, uint32_t nwg) {
+        hp.assign(nwg + 1, 0);
+        for (uint32_t w = 0; w < nwg; ++w) {
+            const double mu = (double)ww[w] / TAB_NB;
+            hp[w + 1] = hp[w] + (ww[w] ? ((uint64_t)(mu + sig * std::sqrt(mu)) + 4 + 7) & ~7ull : 0);
+        }
+        const uint64_t R = hp[nwg];
+        return (uint64_t)TAB_NB * (R + ((std::max<uint64_t>(256, R / 64) + 7) & ~7ull));
+    };
+    uint64_t region = sized(hw, a.nwg);
+    // small shares (C5's 1 GB of contigs cut into 4,096-window pieces: ~60
+    // keys per run) are mostly filler: merge the workgroups' shares in groups
+    // of 2, 4, ... (the sums of the window counts already measured -- share w'
+    // is shares w' f .. w' f + f - 1) while at least two workgroups per CU
+    // remain, until the filler is at most 1/12 of the keys
+    const uint32_t min_wg = 2u * (uint32_t)std::max(c->n_cu, 1);
+    while (region > tot + tot / 12 && a.nwg >= 2 * min_wg && !(c->p.flags & KMER_FLAG_TABLE_FIXED_TEST)) {
+        const uint32_t nwg2 = (a.nwg + 1) / 2;
+        std::vector<uint64_t> h2(nwg2, 0);
+        for (uint32_t w = 0; w < a.nwg; ++w) h2[w / 2] += hw[w];
+        hw.swap(h2);
+        a.nwg = nwg2;
+        a.lpw *= 2;
+        region = sized(hw, a.nwg);
     }
+    // (still more than 1/8 filler: the counting pass moves fewer bytes through
+    // pass 2 -- filler costs ~3 x 8 B per slot, the counting pass one more
+    // formation of every window)
+    if (region > tot + tot / 8 && !(c->p.flags & KMER_FLAG_TABLE_FIXED_TEST)) return KMER_OK;
     const uint64_t R = hp[a.nwg];
     const uint64_t S = (std::max<uint64_t>(256, R / 64) + 7) & ~7ull, PS = R + S;
-    const uint64_t region = (uint64_t)TAB_NB * PS;
-    // small shares (C5's 1 GB of contigs: ~256 keys per run, 16 % filler) move
-    // more filler through pass 2 than the counting pass costs: counted instead
-    if (region > tot + tot / 12 && !(c->p.flags & KMER_FLAG_TABLE_FIXED_TEST)) return KMER_OK;
     const uint64_t cb = (c->t_keys + 7) & ~7ull;  // (runs of multiples of 8 keys start at 64-B boundaries)
     HIPCHK(c, c->tb1.ensure(cb + region, s, true, c->t_keys));
     HIPCHK(c, c->tspc.ensure(TAB_NB + 1, s));
