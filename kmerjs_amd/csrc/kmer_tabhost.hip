@@ -98,6 +98,8 @@ kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done
     hp[0] = 0;
     double sig = 2.0;                          // (KMERHIP_TAB_SIGMA: A/B experiments)
     if (const char *e = exp_env("KMERHIP_TAB_SIGMA")) sig = atof(e);
+    uint64_t sdiv = 64;                        // spill area: R / sdiv slots (KMERHIP_TAB_SPILLDIV: A/B experiments)
+    if (const char *e = exp_env("KMERHIP_TAB_SPILLDIV")) sdiv = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
     for (uint32_t w = 0; w < a.nwg; ++w) tot += hw[w];
     auto sized = [&](const std::vector<uint64_t> &ww, uint32_t nwg) {
         hp.assign(nwg + 1, 0);
@@ -106,7 +108,7 @@ kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done
             hp[w + 1] = hp[w] + (ww[w] ? ((uint64_t)(mu + sig * std::sqrt(mu)) + 4 + 7) & ~7ull : 0);
         }
         const uint64_t R = hp[nwg];
-        return (uint64_t)TAB_NB * (R + ((std::max<uint64_t>(256, R / 64) + 7) & ~7ull));
+        return (uint64_t)TAB_NB * (R + ((std::max<uint64_t>(256, R / sdiv) + 7) & ~7ull));
     };
     uint64_t region = sized(hw, a.nwg);
     // small shares (C5's 1 GB of contigs cut into 4,096-window pieces: ~60
@@ -129,7 +131,7 @@ kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done
     // formation of every window)
     if (region > tot + tot / 8 && !(c->p.flags & KMER_FLAG_TABLE_FIXED_TEST)) return KMER_OK;
     const uint64_t R = hp[a.nwg];
-    const uint64_t S = (std::max<uint64_t>(256, R / 64) + 7) & ~7ull, PS = R + S;
+    const uint64_t S = (std::max<uint64_t>(256, R / sdiv) + 7) & ~7ull, PS = R + S;
     const uint64_t cb = (c->t_keys + 7) & ~7ull;  // (runs of multiples of 8 keys start at 64-B boundaries)
     HIPCHK(c, c->tb1.ensure(cb + region, s, true, c->t_keys));
     HIPCHK(c, c->tspc.ensure(TAB_NB + 1, s));
