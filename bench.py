@@ -669,8 +669,12 @@ def main():
             kern_name = max(phases, key=lambda x: phases[x])
             kern_ms = phases[kern_name]
             algo_bytes = pbytes[kern_name]
+            # pass 1 without the counting pass (fixed runs: "hist1" is then only
+            # the window counts per workgroup, well under a tenth of scatter1)
+            fixed = phases.get("hist1", 0.0) < 0.1 * phases.get("scatter1", 1.0)
             kern_name = {"lines": "nl_slots_kernel + seq_lines_slots_kernel",
-                         "hist1": "tab_hist1_kernel (+ scan)", "scatter1": "tab_scatter1h_kernel",
+                         "hist1": "tab_hist1_kernel (+ scan)",
+                         "scatter1": "tab_scatter1f_kernel" if fixed else "tab_scatter1h_kernel",
                          "hist2": "tab_hist2_kernel (+ scan)", "scatter2": "tab_scatter2c_kernel",
                          "final": "tab_sort_final_kernel (+ tab_final_kernel on its leftover units)",
                          "fasta": "fa_tiles_kernel + fa_write_kernel (FASTA rewrite)"}[kern_name]
