@@ -2106,7 +2106,31 @@ __global__ __launch_bounds__(256) void gen_reduce_kernel(const uint32_t *__restr
 __device__ __forceinline__ uint64_t window_code(const uint8_t *p, uint32_t k, bool safe, bool *exotic) {
     uint64_t code = 0;
     bool ex = false;
-    if (safe) {
+    if (safe && k <= (uint32_t)KMAX_DENSE) {
+        // every word of the window loaded before any is used (one memory
+        // round trip per window, not one per word: the dense-hit path's
+        // windows kernel was bound by that chain)
+        const uintptr_t ad = (uintptr_t)p;
+        const uint32_t *wp = (const uint32_t *)(ad & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)(ad & 3);
+        constexpr uint32_t NWMAX = KMAX_DENSE / 4 + 1;
+        const uint32_t nwk = (k + 3) / 4;
+        uint32_t wv[NWMAX];
+#pragma unroll
+        for (uint32_t i = 0; i < NWMAX; ++i) wv[i] = i <= nwk ? wp[i] : 0u;
+#pragma unroll
+        for (uint32_t i = 0; i < NWMAX - 1; ++i) {
+            const uint32_t b = 4 * i;
+            if (b >= k) break;
+            const uint32_t x = align4(wv[i + 1], wv[i], sh);
+            const uint32_t nb = k - b >= 4 ? 4u : k - b;
+            const uint32_t mk = nb == 4 ? 0xFFFFFFFFu : ((1u << (8 * nb)) - 1u);
+            const uint32_t c = ((x >> 1) ^ (x >> 2)) & 0x03030303u;
+            ex |= ((__builtin_amdgcn_perm(0u, 0x54474341u, c) ^ x) & mk) != 0;
+            const uint32_t pk = ((c & 3u) << 6) | (((c >> 8) & 3u) << 4) | (((c >> 16) & 3u) << 2) | ((c >> 24) & 3u);
+            code = (code << (2 * nb)) | (pk >> (2 * (4 - nb)));
+        }
+    } else if (safe) {
         const uintptr_t ad = (uintptr_t)p;
         const uint32_t *wp = (const uint32_t *)(ad & ~(uintptr_t)3);
         const uint32_t sh = (uint32_t)(ad & 3);
