@@ -1135,9 +1135,9 @@ __global__ __launch_bounds__(TPB) void scan_planes_kernel(ScanArgs a, PlaneArgs 
 // Returns the packed key (invalid_key when the hit does not count as a packed
 // key: non-sequence line, or a record) and writes records for exotic windows
 // / record mode.  *lk = order of the hit among its tile's hits (local).
-__device__ __forceinline__ uint64_t resolve_hit(const HitArgs &a, const HitRec &r, uint64_t code_hi,
-                                                const TileSum &tb, uint64_t *order_out, uint32_t *lk,
-                                                bool *lvalid_out, uint64_t *key_hi) {
+__device__ __forceinline__ uint64_t resolve_hit(const HitArgs &a, uint64_t pos_lines, const HitRec &r,
+                                                uint64_t code_hi, const TileSum &tb, uint64_t *order_out,
+                                                uint32_t *lk, bool *lvalid_out, uint64_t *key_hi) {
     const uint32_t t = r.tile;
     const uint32_t strand = (r.qm >> 14) & 1u;
     const bool exotic = (r.qm >> 15) & 1u;
@@ -1145,7 +1145,7 @@ __device__ __forceinline__ uint64_t resolve_hit(const HitArgs &a, const HitRec &
     const int q = (int)(r.qm & 0x3FFFu);
     const int s0 = strand ? q + (int)a.plen - (int)a.k : q;     // >= -63
     const uint64_t tile_abs = a.abs_offset + (uint64_t)t * TILE;
-    const uint64_t li = a.pos->lines + tb.cnt + r.c_local;
+    const uint64_t li = pos_lines + tb.cnt + r.c_local;
     const uint64_t lstart = lvalid ? tile_abs + r.lstart : tb.lnl;
     const uint64_t sabs = tile_abs + (uint64_t)(int64_t)s0;
     uint64_t rel = sabs - lstart;
@@ -1236,17 +1236,23 @@ __global__ __launch_bounds__(256) void hit_kernel(HitArgs a) {
     __shared__ uint64_t s_keyh[WIDE ? 4 : 1][WIDE ? HENT : 1];
     const uint32_t wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t t0 = __builtin_amdgcn_readfirstlane((blockIdx.x * 4 + wid) * HTPW);
-    if (t0 >= a.n_tiles || *a.ovf_count > a.ovf_cap) return;   // overflowed scan: the host redoes the chunk
+    if (t0 >= a.n_tiles) return;
+    // (the overflow count, the stream position and the tiles' sums issued
+    // together: one memory round trip before the hits, not three)
+    const unsigned long long ovf = *a.ovf_count;
+    const uint64_t pos_lines = a.pos->lines;
     TileSum ts[HTPW], tb[HTPW];
-    uint32_t off[HTPW + 1];
-    off[0] = 0;
 #pragma unroll
     for (uint32_t u = 0; u < HTPW; ++u) {
         const uint32_t t = min(t0 + u, a.n_tiles - 1);
         ts[u] = a.tsum[t];
         tb[u] = a.tscan[t];
-        off[u + 1] = off[u] + (t0 + u < a.n_tiles ? min(ts[u].nh, (uint32_t)HMAX) : 0u);
     }
+    if (ovf > a.ovf_cap) return;                 // overflowed scan: the host redoes the chunk
+    uint32_t off[HTPW + 1];
+    off[0] = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < HTPW; ++u) off[u + 1] = off[u] + (t0 + u < a.n_tiles ? min(ts[u].nh, (uint32_t)HMAX) : 0u);
     const uint32_t total = off[HTPW];
     // phase 1
     for (uint32_t e0 = 0; e0 < total; e0 += 64) {
@@ -1268,7 +1274,8 @@ __global__ __launch_bounds__(256) void hit_kernel(HitArgs a) {
             uint64_t order, kh;
             uint32_t lk;
             bool lvalid;
-            const uint64_t key = resolve_hit(a, r, a.k > 32 ? a.hits_hi[hslot] : 0, tbu, &order, &lk, &lvalid, &kh);
+            const uint64_t key = resolve_hit(a, pos_lines, r, a.k > 32 ? a.hits_hi[hslot] : 0, tbu, &order, &lk, &lvalid,
+                                             &kh);
             s_lk[wid][e] = lk;
             s_x[wid][e] = (tsu.nh > (uint32_t)HMAX || !lvalid || r.c_local == (uint32_t)tsu.cnt) ? 1 : 0;
             s_key[wid][e] = key;
@@ -1324,7 +1331,7 @@ __global__ __launch_bounds__(256) void hit_overflow_kernel(HitArgs a) {
         uint64_t order, kh;
         uint32_t lk;
         bool lvalid;
-        const uint64_t key = resolve_hit(a, r, a.k > 32 ? a.ovf_hi[i] : 0, tb, &order, &lk, &lvalid, &kh);
+        const uint64_t key = resolve_hit(a, a.pos->lines, r, a.k > 32 ? a.ovf_hi[i] : 0, tb, &order, &lk, &lvalid, &kh);
         if (!a.packed) continue;
         const uint32_t ord = r.qm >> 17;
         place_hit(a, a.out_base + tb.nh + ord, true, a.xbase + tb.nx + ord, key, kh, order);
