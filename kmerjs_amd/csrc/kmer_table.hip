@@ -1274,7 +1274,8 @@ namespace {
 constexpr int TS_KPT = 24;                            // keys held per thread
 constexpr uint32_t TS_CAP1 = TS_KPT * TAB_SWG;        // one bucket: 12,288 keys, 32-bit LDS entries
 constexpr uint32_t TS_CAPG = TS_CAP1 / 2;             // a group: 6,144 keys, 64-bit LDS entries
-constexpr uint32_t TS_NB = 4096;                      // bins
+constexpr uint32_t TS_NB = 8192;                      // bins (16-bit counts / starts, two per LDS word)
+constexpr uint32_t TS_NBB = 13;                       // log2(TS_NB)
 constexpr uint32_t TS_BINMAX = 64;                    // fuller bins: leftover (general kernel)
 constexpr uint32_t TS_GMAX = 64;                      // buckets per group
 constexpr uint32_t TS_SC = 512;                       // bucket starts cached per refill
@@ -1283,7 +1284,7 @@ constexpr uint32_t TS_SC = 512;                       // bucket starts cached pe
 
 __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) {
     __shared__ uint32_t lkey[TS_CAP1];                // sorted unit: u32 (one bucket) or u64 (a group)
-    __shared__ uint32_t bst[TS_NB];                   // bin counts, then starts
+    __shared__ uint32_t bst[TS_NB / 2];               // bin counts, then starts: bin b in half b & 1 of word b >> 1
     __shared__ uint64_t sc[TS_SC + 2];                // start[cbase .. cbase + TS_SC + 1]
     __shared__ uint32_t nout[TS_GMAX];
     __shared__ uint32_t ws[8], smax;
@@ -1387,7 +1388,7 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
         auto sort_unit = [&](auto one_tag) -> bool {
             constexpr bool ONE = decltype(one_tag)::value;
             constexpr int KPT = ONE ? TS_KPT : TS_KPT / 2;
-            const uint32_t bsh = TAB_RBITS + (ONE ? 0 : 32 - __clz(g - 1)) - 12;
+            const uint32_t bsh = TAB_RBITS + (ONE ? 0 : 32 - __clz(g - 1)) - TS_NBB;
             uint32_t lo[KPT], hi[ONE ? 1 : KPT], pk[KPT];
             {
                 const uint64_t *src = a.B2 + s0;
@@ -1400,7 +1401,7 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                 }
             }
             __syncthreads();                           // the previous unit is done with the LDS state
-            for (uint32_t i = t; i < TS_NB; i += TAB_SWG) bst[i] = 0;
+            for (uint32_t i = t; i < TS_NB / 2; i += TAB_SWG) bst[i] = 0;
             if (t == 0) smax = 0;
             for (uint32_t i = t; i < g; i += TAB_SWG) nout[i] = 0;
             __syncthreads();
@@ -1409,16 +1410,18 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
             for (int j = 0; j < KPT; ++j)
                 if (left > j * (int)TAB_SWG)
                     pk[j] = pk[j] << 14 |
-                            __hip_atomic_fetch_add(&bst[pk[j]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            ((__hip_atomic_fetch_add(&bst[pk[j] >> 1], 1u << (16 * (pk[j] & 1u)), __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP) >> (16 * (pk[j] & 1u))) & 0xFFFFu);
             __syncthreads();
             {
-                // bin starts: thread t scans bins 8t .. 8t + 7
+                // bin starts: thread t scans bins 16t .. 16t + 15 (words 8t .. 8t + 7)
                 uint32_t c8[8], sum = 0, mx = 0;
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
                     c8[i] = bst[8 * t + i];
-                    sum += c8[i];
-                    mx = max(mx, c8[i]);
+                    const uint32_t lo16 = c8[i] & 0xFFFFu, hi16 = c8[i] >> 16;
+                    sum += lo16 + hi16;
+                    mx = max(mx, max(lo16, hi16));
                 }
                 uint32_t tot;
                 uint32_t run = block_excl_512(sum, ws, &tot);
@@ -1426,8 +1429,9 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                 if (lane == 0) atomicMax(&smax, mx);
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
-                    bst[8 * t + i] = run;
-                    run += c8[i];
+                    const uint32_t lo16 = c8[i] & 0xFFFFu, hi16 = c8[i] >> 16;
+                    bst[8 * t + i] = run | (run + lo16) << 16;   // (starts < 2^14)
+                    run += lo16 + hi16;
                 }
             }
             __syncthreads();
@@ -1437,7 +1441,7 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
             for (int j = 0; j < KPT; ++j)
                 if (left > j * (int)TAB_SWG) {
                     const uint32_t b = pk[j] >> 14;
-                    const uint32_t pos = bst[b] + (pk[j] & 0x3FFFu);
+                    const uint32_t pos = ((bst[b >> 1] >> (16 * (b & 1u))) & 0xFFFFu) + (pk[j] & 0x3FFFu);
                     if (ONE)
                         lkey[pos] = lo[j];
                     else
@@ -1460,7 +1464,8 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                     const int j = g0 + u;
                     const bool valid = left > j * (int)TAB_SWG;
                     const uint32_t b = pk[j] >> 14;
-                    const uint32_t b0 = bst[b], b1 = (KH_ABLATE(a) & 8) ? b0 : b + 1 < TS_NB ? bst[b + 1] : (uint32_t)n;
+                    const uint32_t b0 = (bst[b >> 1] >> (16 * (b & 1u))) & 0xFFFFu;
+                    const uint32_t b1 = (KH_ABLATE(a) & 8) ? b0 : b + 1 < TS_NB ? (bst[(b + 1) >> 1] >> (16 * ((b + 1) & 1u))) & 0xFFFFu : (uint32_t)n;
                     const uint32_t c = valid ? b1 - b0 : 0u;
                     bb[u] = b0 | c << 14;
                     cf[u] = valid ? ((KH_ABLATE(a) & 8) ? 0x101u : 0x100u) : 0u;   // (experiments: no bin scan)
@@ -1500,7 +1505,9 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                 for (int u = 0; u < G; ++u) {
                     const int j = g0 + u;
                     const uint32_t b = pk[j] >> 14;
-                    const uint64_t xj = ((uint64_t)(ONE ? b : hi[ONE ? 0 : j]) << 32) | lo[j];
+                    // (one bucket: the bin is the remainder's top TS_NBB bits, bits 31 .. 43)
+                    const uint64_t xj = ONE ? (((uint64_t)b << (TAB_RBITS - TS_NBB)) | (lo[j] & ((1u << (TAB_RBITS - TS_NBB)) - 1u)))
+                                            : (((uint64_t)hi[ONE ? 0 : j] << 32) | lo[j]);
                     const bool first = (cf[u] >> 8) != 0u;
                     const uint32_t cnt = cf[u] & 0xFFu;
                     // output slots: one LDS counter bump per wave and bucket present
