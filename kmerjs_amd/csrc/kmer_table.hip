@@ -1261,12 +1261,12 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
 // per CU (their phases overlap each other's barriers and key loads).  A unit
 // -- one bucket of up to 12,288 keys (C3: ~11.4 K), or a group of consecutive
 // small buckets of up to 6,144 keys together (C5) -- is held in registers
-// (24 keys per thread), counting-sorted into 4,096 LDS bins by the top 12 bits
-// of (bucket offset << 44 | remainder), and every held key then scans its own
-// bin (~3 keys at C3): the first copy of a key emits it with the number of
-// copies.  One bucket's bin fixes the remainder's top 12 bits, so its LDS
-// entries keep only the low 32 (48 KiB for 12,288 keys); a group's keep all
-// 64 bits (6,144 keys, the same 48 KiB).  Units that do not fit -- larger
+// (24 keys per thread), counting-sorted into 8,192 LDS bins by the top 13 bits
+// of (bucket offset << 44 | remainder) -- 16-bit counts, two per LDS word --
+// and every held key then scans its own bin (~1.4 keys at C3): the first copy
+// of a key emits it with the number of copies.  One bucket's bin fixes the
+// remainder's top 13 bits, so its LDS entries keep only the low 32 (48 KiB for
+// 12,288 keys); a group's keep all 64 bits (6,144 keys, the same 48 KiB).  Units that do not fit -- larger
 // buckets, or a bin with more than TS_BINMAX keys (many copies of a key) --
 // go to the leftover list for the general kernel (hash path, range splits).
 // ---------------------------------------------------------------------------
@@ -1454,7 +1454,7 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
             // groups of G, element m of all G bins read together (G LDS reads
             // in flight per step, steps = the largest bin of the group: ~3 keys
             // per bin at C3) instead of one key's bin after another.
-            constexpr int G = ONE ? 8 : 4;
+            constexpr int G = ONE ? 6 : 4;           // (A/B at C3 / C5: ONE 4 / 6 / 8 / 12 -> 60.9 / 58.3 / 59.7 / 82 ms; groups 3 / 4 / 6)
 #pragma unroll
             for (int g0 = 0; g0 < KPT; g0 += G) {
                 if (!__any(left > g0 * (int)TAB_SWG)) break;
