@@ -747,8 +747,6 @@ __global__ __launch_bounds__(256) void tab_starts_kernel(const uint64_t *H2s, co
 
 namespace {
 
-// LDS slot of a remainder: its low bits are weak (a product's low bits see
-// only the code's low bits), so the slot comes from a second multiply's top bits
 // A final workgroup's Map statistics -> 3 device atomics per WORKGROUP (wave
 // sums through LDS): device-scope atomics on one line serialise (~12 ns each),
 // and every wave of the grid reaches this point at about the same time
@@ -782,6 +780,8 @@ __device__ __forceinline__ void tab_stats_out(unsigned long long *stats, uint64_
     }
 }
 
+// LDS slot of a remainder: its low bits are weak (a product's low bits see
+// only the code's low bits), so the slot comes from a second multiply's top bits
 __device__ __forceinline__ uint32_t tab_slot(uint64_t rem) {
     return (uint32_t)((rem * TAB_MUL) >> 51) & (TAB_SLOTS - 1);
 }
