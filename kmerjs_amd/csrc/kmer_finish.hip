@@ -103,6 +103,7 @@ kmer_status bucket_heads(kmer_ctx *c, uint64_t n) {
     HIPCHK(c, launch_bucket_hist(c->rkey32.p, n, invalid, shift, nb, nblk, c->bH.p, c->hcnt.p, s));
     HIPCHK(c, launch_bucket_offsets(c->bH.p, nb, nblk, c->bHs.p, btot, bstart, c->d_bticket, s));
     HIPCHK(c, launch_bucket_scatter(c->rkey32.p, n, invalid, shift, nb, nblk, c->bHs.p, bstart, c->pkey16.p, c->ridx2.p, s));
+    if (nb <= 8) HIPCHK(c, launch_l2_flush(s));   // (few workgroups read the whole partition: l2_flush_kernel)
     HIPCHK(c, launch_bucket_heads(c->pkey16.p, c->ridx2.p, bstart, nb, shift, c->hcnt.p, s));
     return KMER_OK;
 }

@@ -400,6 +400,7 @@ hipError_t launch_bucket_offsets(const uint32_t *H, uint32_t nb, uint32_t nblk, 
 hipError_t launch_bucket_scatter(const uint32_t *key, uint64_t n, uint32_t invalid, uint32_t shift, uint32_t nb,
                                  uint32_t nblk, const uint32_t *Hs, const uint32_t *bbase, uint16_t *pkey,
                                  uint32_t *prank, hipStream_t s);
+hipError_t launch_l2_flush(hipStream_t s);   // every XCD's L2 written back + invalidated
 hipError_t launch_bucket_heads(const uint16_t *pkey, const uint32_t *prank, const uint32_t *bbase, uint32_t nb,
                                uint32_t shift, uint32_t *hcnt, hipStream_t s);
 // multi-GPU hit exchange (kmer_exchange_prepare / kmer_finish_exchanged)

@@ -3596,6 +3596,21 @@ hipError_t launch_bucket_scatter(const uint32_t *key, uint64_t n, uint32_t inval
                        pkey, prank);
     return hipGetLastError();
 }
+// Every XCD's L2 written back and invalidated (system-scope fence per wave,
+// workgroups dealt round robin over the XCDs): issued before a bucket-table
+// kernel with few workgroups, which reads the whole partition through one or
+// two XCDs -- an ordered count with very few buckets (k = 3) lost counts
+// intermittently when run after table-mode counts in the same process,
+// consistent with stale L2 lines of a reused allocation
+__global__ __launch_bounds__(64) void l2_flush_kernel() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+}
+
+hipError_t launch_l2_flush(hipStream_t s) {
+    hipLaunchKernelGGL(l2_flush_kernel, dim3(256), dim3(64), 0, s);
+    return hipGetLastError();
+}
+
 hipError_t launch_bucket_heads(const uint16_t *pkey, const uint32_t *prank, const uint32_t *bbase, uint32_t nb,
                                uint32_t shift, uint32_t *hcnt, hipStream_t s) {
     hipLaunchKernelGGL(bucket_heads_kernel, dim3(nb), dim3(1024), 0, s, pkey, prank, bbase, shift, hcnt);
