@@ -655,7 +655,7 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2_kernel(const uint64_t *B
 // ~16-key runs that straddle lines, which left partial L2 lines to be evicted
 // before the next round completed them.  Thread t owns bucket t; bucket
 // order inside a range is free (table mode has no order).
-constexpr int TS2_RPL = 8;
+constexpr int TS2_RPL = 10;                           // (A/B: 8 / 9 / 10 -> C3 scatter2 56.8 / 56.2 / 56.2 ms)
 constexpr int TS2_ROUND = TS2_RPL * TAB_WG1;           // new keys per round
 constexpr int TS2_CARRY = 7;                           // carried keys per bucket (< one 64-B block)
 __global__ __launch_bounds__(TAB_WG1) void tab_scatter2c_kernel(const uint64_t *B1, const TabUnit *units,
