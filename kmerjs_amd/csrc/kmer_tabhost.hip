@@ -114,9 +114,10 @@ kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done
     // small shares (C5's 1 GB of contigs cut into 4,096-window pieces: ~60
     // keys per run) are mostly filler: merge the workgroups' shares in groups
     // of 2, 4, ... (the sums of the window counts already measured -- share w'
-    // is shares w' f .. w' f + f - 1) while at least two workgroups per CU
-    // remain, until the filler is at most 1/12 of the keys
-    const uint32_t min_wg = 2u * (uint32_t)std::max(c->n_cu, 1);
+    // is shares w' f .. w' f + f - 1) while at least one workgroup per CU
+    // remains, until the filler is at most 1/12 of the keys (C5: down to one
+    // per CU beat two per CU by ~1 %, A/B: less filler through pass 2)
+    const uint32_t min_wg = (uint32_t)std::max(c->n_cu, 1);
     while (region > tot + tot / 12 && a.nwg >= 2 * min_wg && !(c->p.flags & KMER_FLAG_TABLE_FIXED_TEST)) {
         const uint32_t nwg2 = (a.nwg + 1) / 2;
         std::vector<uint64_t> h2(nwg2, 0);
