@@ -103,7 +103,6 @@ kmer_status bucket_heads(kmer_ctx *c, uint64_t n) {
     HIPCHK(c, launch_bucket_hist(c->rkey32.p, n, invalid, shift, nb, nblk, c->bH.p, c->hcnt.p, s));
     HIPCHK(c, launch_bucket_offsets(c->bH.p, nb, nblk, c->bHs.p, btot, bstart, c->d_bticket, s));
     HIPCHK(c, launch_bucket_scatter(c->rkey32.p, n, invalid, shift, nb, nblk, c->bHs.p, bstart, c->pkey16.p, c->ridx2.p, s));
-    if (nb <= 8) HIPCHK(c, launch_l2_flush(s));   // (few workgroups read the whole partition: l2_flush_kernel)
     HIPCHK(c, launch_bucket_heads(c->pkey16.p, c->ridx2.p, bstart, nb, shift, c->hcnt.p, s));
     return KMER_OK;
 }
@@ -176,6 +175,10 @@ kmer_status rank_finish(kmer_ctx *c, uint64_t n, bool partial, bool with_counts,
     hipStream_t s = c->stream;
     *nu_out = 0;
     if (n == 0) return KMER_OK;
+    // every XCD's L2 written back and invalidated before the finish chain
+    // (l2_flush_kernel): no XCD keeps lines of these reused buffers from an
+    // earlier finish, whose stale copies intermittently cost counts / keys
+    HIPCHK(c, launch_l2_flush(s));
     if (c->narrow) HIPCHK(c, c->rkey32b.ensure(n, s));
     else HIPCHK(c, c->rkey2.ensure(n, s));
     HIPCHK(c, c->ridx2.ensure(n, s));

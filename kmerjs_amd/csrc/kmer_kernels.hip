@@ -3597,11 +3597,11 @@ hipError_t launch_bucket_scatter(const uint32_t *key, uint64_t n, uint32_t inval
     return hipGetLastError();
 }
 // Every XCD's L2 written back and invalidated (system-scope fence per wave,
-// workgroups dealt round robin over the XCDs): issued before a bucket-table
-// kernel with few workgroups, which reads the whole partition through one or
-// two XCDs -- an ordered count with very few buckets (k = 3) lost counts
-// intermittently when run after table-mode counts in the same process,
-// consistent with stale L2 lines of a reused allocation
+// workgroups dealt round robin over the XCDs): issued at the start of the
+// ordered and table finishes.  Ordered counts lost counts / keys
+// intermittently when buffers were reused (k = 3 after table-mode counts in
+// the same process; the C4 hit exchange), consistent with an XCD's L2 keeping
+// lines of a reused allocation across kernels
 __global__ __launch_bounds__(64) void l2_flush_kernel() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
 }

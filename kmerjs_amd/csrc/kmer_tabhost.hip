@@ -281,6 +281,7 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
     c->t_done = true;
     const uint64_t n = c->t_keys;
     if (n == 0) return KMER_OK;
+    HIPCHK(c, launch_l2_flush(s));            // (as rank_finish: no stale L2 lines of reused buffers)
     // the table is written over the pass-1 keys (dead after pass 2)
     if (!B1) B1 = c->tb1.p;
     c->t_ent = const_cast<uint64_t *>(B1);
