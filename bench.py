@@ -274,6 +274,22 @@ def table_phase_bytes(nbytes, n_keys, canonical):
             "scatter2": 16 * n_keys, "final": 8 * n_keys + 8 * canonical}
 
 
+def print_shard_plan(args, world, strong):
+    """--dry-run: the record-aligned shard each rank would count (reads-based
+    configs: multi.shard_plan; c5: the rank's own contig file), one JSON line
+    per rank -- no GPU is touched."""
+    from kmerjs_amd.multi import shard_plan
+    for r in range(world):
+        row = {"rank": r, "world": world, "config": args.config, "k": args.k, "prefix": args.prefix,
+               "merge": args.merge if world > 1 else None, "scaling": "strong" if strong else "weak"}
+        if args.config in ("c2", "c3", "c4"):
+            row.update(shard_plan(args.reads, r))
+            row["windows"] = args.reads * windows_per_read(args.k)
+        elif args.config == "c5":
+            row.update({"contig_seed": 5 + r, "contig_bytes": args.contig_bytes, "fasta": bool(args.fasta)})
+        print(json.dumps(row), flush=True)
+
+
 def rank_envs(n, port, base=None):
     """Environment of each of the n worker processes `--gpus n` starts when no
     launcher set WORLD_SIZE: one process per GPU, rank r on device r."""
@@ -339,6 +355,9 @@ def main():
                          "bench.py starts the N rank processes itself")
     ap.add_argument("--dry-run-launch", action="store_true",
                     help="print the rank environments --gpus N would start and exit (no GPU)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print the shard plan of each of the --gpus N ranks (one JSON line per rank) and exit "
+                         "(no GPU, no launch)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--reads", type=int, default=10_000_000, help="reads per GPU")
@@ -373,7 +392,7 @@ def main():
                          "gather: all partials to rank 0.  Default: dense for c4 (bytes independent of the input "
                          "size), hits otherwise")
     args = ap.parse_args()
-    if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.dry_run_launch):
+    if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.dry_run_launch) and not args.dry_run:
         sys.exit(launch_ranks(max(1, args.gpus), sys.argv[1:], dry_run=args.dry_run_launch))
     if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
         sys.exit("bench.py: WORLD_SIZE=%s but --gpus %d" % (os.environ["WORLD_SIZE"], args.gpus))
@@ -418,7 +437,7 @@ def main():
         args.merge = "dense" if args.config == "c4" and 2 * (args.k - len(args.prefix)) <= 26 else "hits"
     from kmerjs_amd._native import FLAG_CANONICAL as _FC
     table = bool(args.flags & (FLAG_UNORDERED | _FC))
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = args.gpus if args.dry_run else int(os.environ.get("WORLD_SIZE", "1"))
     strong = False
     if args.config == "c3" and world_env > 1 and "--reads" not in argv:
         # C3 names a job (100 M reads), not a per-GPU size; one rank's 100 M reads
@@ -426,6 +445,9 @@ def main():
         # N ranks split the 100 M reads (strong scaling)
         args.reads = 100_000_000 // world_env
         strong = True
+    if args.dry_run:
+        print_shard_plan(args, world_env, strong)
+        return
 
     import torch
     import torch.distributed as dist

@@ -91,7 +91,10 @@ enum {
     KMER_FLAG_FASTA = 1u << 16,
     /* debug: table pass 1 always with fixed per-workgroup runs (by default
      * only when their filler slots are <= 1/12 of the keys: large inputs) */
-    KMER_FLAG_TABLE_FIXED_TEST = 1u << 17
+    KMER_FLAG_TABLE_FIXED_TEST = 1u << 17,
+    /* debug: the general path's first merge attempt reports a hash collision,
+     * so the two-hash (h2, h1) retry runs (exercises the collision route) */
+    KMER_FLAG_GEN_COLLIDE_TEST = 1u << 18
 };
 
 typedef struct {
@@ -270,6 +273,12 @@ kmer_status kmer_table_device(kmer_ctx *ctx, const void **d_entries, const void 
  * of an exchanged table add up -- a size-independent check of a table that is
  * too large to compare entry by entry.  Record keys are not included. */
 kmer_status kmer_table_digest(kmer_ctx *ctx, uint64_t *digest);
+/* Diagnostics of table mode's pass 1 since the last reset: chunks whose keys
+ * went out in fixed-capacity runs (fixed), of them the chunks whose
+ * workgroup shares were merged first (merged: small shares, e.g. long
+ * contigs cut into pieces), and chunks counted by the two-pass route
+ * (counted).  Lets a test assert which route a workload took. */
+kmer_status kmer_table_pass1_routes(kmer_ctx *ctx, uint64_t *fixed, uint64_t *merged, uint64_t *counted);
 /* Table mode across ranks (replaces the one Map.set stream of lib/kmers.js:95
  * when the count is sharded over GPUs; reads are independent, :151-155).
  * Rank o (of `world` <= 1024) owns the pass-1 partitions [o*1024/world,

@@ -794,6 +794,29 @@ kmer_status kmer_table_digest(kmer_ctx *c, uint64_t *digest) {
     return KMER_OK;
 }
 
+kmer_status kmer_table_pass1_routes(kmer_ctx *c, uint64_t *fixed, uint64_t *merged, uint64_t *counted) {
+    if (!c) return KMER_E_BAD_PARAM;
+    uint64_t f = 0, m = 0, n = 0;
+    if (!c->group.empty()) {                         // a group: its children's routes add up
+        for (kmer_ctx *x : c->group) {
+            if (hipSetDevice(x->device) != hipSuccess) return KMER_E_DEVICE;
+            SETTLE(x);
+            f += x->t_p1_fixed;
+            m += x->t_p1_merged;
+            n += x->t_p1_counted;
+        }
+    } else {
+        SETTLE(c);
+        f = c->t_p1_fixed;
+        m = c->t_p1_merged;
+        n = c->t_p1_counted;
+    }
+    if (fixed) *fixed = f;
+    if (merged) *merged = m;
+    if (counted) *counted = n;
+    return KMER_OK;
+}
+
 kmer_status kmer_phase_times(kmer_ctx *c, uint32_t max, const char **names, double *ms, uint32_t *n) {
     if (!c || !n || (max && (!names || !ms))) return KMER_E_BAD_PARAM;
     SETTLE(c);

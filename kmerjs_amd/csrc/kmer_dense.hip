@@ -1,0 +1,318 @@
+// kmer_dense.hip — the dense-hit ordered path (a prefix of 0-3 bases, or none;
+// step 1, k <= 32): only the ACCEPTED windows are written, in rank order.
+//
+// lib/kmers.js:88-100 on a sequence line and on its complement (:151-155):
+// the Map's insertion order is line by line, the line's forward windows by
+// position s, then its complement's windows by position j, i.e. the reverse
+// strand's windows by DESCENDING s (j = W - 1 - s).  The round-5 windows
+// kernel gave every window of every line a rank slot (2.7 G slots at C2 size
+// with prefix AT, 168.8 M of them accepted), wrote all of them and compacted
+// before the finish; here two passes over the lines find each accepted
+// window's rank directly:
+//   count  per line, the accepted forward and reverse windows;
+//   (scan) per line, its first rank slot;
+//   write  per accepted window, slot = line base + its rank among the line's
+//          accepted windows of its strand (forward: those at smaller s;
+//          reverse: the line's forward count + those at LARGER s).
+// Window formation (both passes): a lane takes 16 CONSECUTIVE windows of one
+// line; the lanes of a wave are dealt out over its next 16 lines (ceil(windows
+// left / 16) lanes per line, as table mode's pass 1).  The lane loads the <= 50
+// bytes its windows span as 13 aligned dwords and packs their 2-bit codes
+// (A/C/G/T = 0..3) with one v_dot4 per dword into two streams -- first base
+// least significant (S) and most significant (R) -- so that window m is a
+// constant shift of each: its code (first base most significant, the key
+// layout of every ordered path) from R, its reverse complement ~S (the
+// complement of the bases in reverse order is the LS stream's bitwise not).
+// Non-ACGT bytes are flagged per byte (v_perm against "ACGT"); such windows
+// are not ranked but become records when their prefix bytes match.
+#include "kmer_internal.hpp"
+
+namespace kmerhip {
+
+namespace {
+
+constexpr int DW_NS = 16;              // windows per lane per round
+constexpr int DW_NDW = 13;             // dwords a lane loads: 16 + 32 - 1 bytes + 3 of alignment <= 52
+
+__device__ __forceinline__ uint32_t dw_incl_sum(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, true);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, true);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, true);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
+}
+
+__device__ __forceinline__ uint32_t rl32(uint32_t v, uint32_t i) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)i);
+}
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
+    return (uint64_t)(uint32_t)__shfl((int)(uint32_t)v, (int)src) |
+           ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)src) << 32);
+}
+
+// 128-bit (lo, hi) >> n, n < 128 (runtime)
+__device__ __forceinline__ void shr128(uint64_t &lo, uint64_t &hi, uint32_t n) {
+    if (n >= 64) {
+        lo = hi >> (n - 64);
+        hi = 0;
+    } else if (n) {
+        lo = (lo >> n) | (hi << (64 - n));
+        hi >>= n;
+    }
+}
+
+// the low 64 bits of (lo, hi) >> n, n < 64 (a constant once the window loops unroll)
+__device__ __forceinline__ uint64_t low_shr(uint64_t lo, uint64_t hi, uint32_t n) {
+    return n ? (lo >> n) | (hi << (64 - n)) : lo;
+}
+
+// A wave's position in its share of sequence lines; lane i < 16 holds the
+// descriptor (and, in the write pass, the counts and first slot) of line m + i.
+struct DCur {
+    uint64_t m, end, seg;              // next line, end of the share, first window of line m not yet taken
+    uint64_t dstart, dlen, dli, dcnt, dbase;
+    uint32_t cf, cr;                   // accepted windows of line m in earlier rounds (seg > 0)
+};
+
+template <bool WRITE>
+__device__ __forceinline__ void dw_fetch(const DenseArgs &a, DCur &c) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t mi = c.m + lane;
+    c.dstart = c.dlen = c.dli = c.dcnt = c.dbase = 0;
+    if (lane < 16 && mi < c.end) {
+        const SeqLine sl = a.lines[mi];
+        c.dstart = sl.start;
+        c.dlen = sl.len;
+        c.dli = sl.line_index;
+        if (WRITE) {
+            c.dcnt = a.cnt[mi];
+            c.dbase = a.hbase[mi];
+        }
+    }
+}
+
+// exotic window (a byte outside A/C/G/T): its strands whose prefix bytes match
+// become records (their keys are gathered later), as the tile paths do
+__device__ __forceinline__ void dw_record(const DenseArgs &a, uint64_t order, uint64_t pos, uint32_t strand) {
+    const unsigned long long n = atomicAdd(a.rec_count, 1ull);
+    if (n < a.rec_cap) {
+        Record r;
+        r.order = order;
+        r.pos = pos;
+        r.len = a.k;
+        r.strand = strand;
+        a.recs[n] = r;
+    } else {
+        atomicOr(a.err, ERR_REC_OVERFLOW);
+    }
+}
+
+}  // namespace
+
+// One pass over a wave's share of lines (lpw consecutive sequence ordinals).
+// COUNT (WRITE false): cnt[m] = accepted forward | accepted reverse << 32 and
+// tot[m] = their sum, per line.  WRITE: keys and order keys of the accepted
+// windows at their rank slots (out_base + hbase[m] + rank), records of the
+// exotic ones.
+template <bool WRITE>
+__global__ __launch_bounds__(256) void dense_windows_kernel(DenseArgs a) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t k = a.k, plen = a.plen;
+    const uint64_t maxrel = (1ull << a.pbits) - 1ull;
+    const uint64_t kmask2 = k >= 32 ? ~0ull : ((1ull << (2 * k)) - 1ull);
+    const uint32_t kmask1 = k >= 32 ? ~0u : ((1u << k) - 1u);
+    const uint32_t tb = 2 * (k - plen);               // prefix bits sit above the suffix
+    DCur c;
+    c.m = wave * a.lpw;
+    c.end = c.m + a.lpw < a.n_lines ? c.m + a.lpw : a.n_lines;
+    c.seg = 0;
+    c.cf = c.cr = 0;
+    if (c.m >= c.end) return;
+    dw_fetch<WRITE>(a, c);
+    const uint8_t *const dend = a.data + a.len;
+    while (c.m < c.end) {
+        // ---- deal the lanes over lines m .. m + 15 ----
+        const uint64_t Wraw = c.dlen >= k ? c.dlen - k + 1 : 0;
+        const uint64_t Wi = Wraw && Wraw - 1 <= maxrel ? Wraw : 0;   // (longer lines: reported by the line pass)
+        const uint64_t seg0 = c.seg;
+        const uint64_t rem = lane == 0 ? (Wi > seg0 ? Wi - seg0 : 0) : Wi;
+        const uint32_t need = lane < 16 ? (uint32_t)((rem + DW_NS - 1) / DW_NS) : 0u;
+        const uint32_t cum = dw_incl_sum(need);
+        const uint32_t tot = rl32(cum, 15);
+        uint32_t li = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 16; ++i) li += rl32(cum, i) <= lane ? 1u : 0u;
+        const bool act = lane < tot && li < 16;
+        const uint32_t lsrc = li < 16 ? li : 15u;
+        const uint32_t before = (uint32_t)__shfl((int)(cum - need), (int)lsrc);
+        const uint64_t st = shfl64(c.dstart, lsrc);
+        const uint64_t Wl = shfl64(Wi, lsrc);
+        const uint64_t lix = shfl64(c.dli, lsrc);
+        const uint64_t w0 = (li == 0 ? seg0 : 0) + (uint64_t)(lane - before) * DW_NS;
+        uint64_t lcnt = 0, lbase = 0;
+        if (WRITE) {
+            lcnt = shfl64(c.dcnt, lsrc);
+            lbase = shfl64(c.dbase, lsrc);
+        }
+        // the line lane 63 works on, and whether this round finishes it
+        uint32_t is = 15, ci = 0;
+        bool part = false;
+        if (tot > 64) {
+            is = rl32(li, 63);
+            ci = rl32(cum, is);
+            part = ci != 64;
+        }
+        // ---- the lane's 16 windows: codes of the bytes [st + w0, st + w0 + 16 + k - 1) ----
+        uint32_t fmask = 0, rmask = 0;
+        uint64_t S0 = 0, S1 = 0, R0 = 0, R1 = 0;        // the code streams (kept for the write-out)
+        const uint32_t nv = act ? (uint32_t)(Wl - w0 < (uint64_t)DW_NS ? Wl - w0 : (uint64_t)DW_NS) : 0u;
+        if (nv) {
+            const uint8_t *p = a.data + st + w0;
+            const uint32_t off = (uint32_t)((uintptr_t)p & 3u);
+            const uint32_t *pw = (const uint32_t *)(p - off);
+            uint64_t EX = 0;
+#pragma unroll
+            for (int i = 0; i < DW_NDW; ++i) {
+                uint32_t x = 0x41414141u;                // ('A' past the input: never inside a window)
+                const uint8_t *q = (const uint8_t *)(pw + i);
+                if (q < dend && (uint32_t)(4 * i) < off + nv + k - 1) {
+                    if (q + 4 <= dend) {
+                        x = pw[i];
+                    } else {
+                        for (int j = 0; j < 4; ++j)
+                            if (q + j < dend) x = (x & ~(0xFFu << (8 * j))) | ((uint32_t)q[j] << (8 * j));
+                    }
+                }
+                const uint32_t cc = ((x >> 1) ^ (x >> 2)) & 0x03030303u;       // A C G T -> 0 1 2 3
+                const uint32_t ls = __builtin_amdgcn_udot4(cc, 0x40100401u, 0u, false);   // first byte lowest
+                const uint32_t ms = __builtin_amdgcn_udot4(cc, 0x01041040u, 0u, false);   // first byte highest
+                const uint32_t ne = __builtin_amdgcn_perm(0u, 0x54474341u, cc) ^ x;     // 0 where A/C/G/T
+                const uint32_t nz = (((ne & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | ne) & 0x80808080u;
+                EX |= (uint64_t)__builtin_amdgcn_udot4(nz >> 7, 0x08040201u, 0u, false) << (4 * i);
+                if (i < 8) S0 |= (uint64_t)ls << (8 * i);
+                else S1 |= (uint64_t)ls << (8 * (i - 8));
+                const int rb = 8 * (DW_NDW - 1 - i);     // R: dword i's byte at bits [rb, rb + 8)
+                if (rb < 64) R0 |= (uint64_t)ms << rb;
+                else R1 |= (uint64_t)ms << (rb - 64);
+            }
+            // S >> 2 off: window m's LS code at bits [2m, 2m + 2k); R >> 2 (37 - off - k):
+            // window m's MS code at bits [2 (15 - m), 2 (15 - m) + 2k)
+            shr128(S0, S1, 2 * off);
+            shr128(R0, R1, 2 * (37 - off - k));
+            EX >>= off;
+#pragma unroll
+            for (int m = 0; m < DW_NS; ++m) {
+                if ((uint32_t)m >= nv) break;
+                const uint64_t ls = low_shr(S0, S1, 2 * m) & kmask2;
+                const uint64_t fc = low_shr(R0, R1, 2 * (DW_NS - 1 - m)) & kmask2;   // the window's code
+                const uint64_t rc = ~ls & kmask2;                                   // rc(window)'s code
+                const bool ex = ((uint32_t)(EX >> m) & kmask1) != 0;
+                bool mf = plen == 0 || (fc >> tb) == a.pcode;
+                bool mr = plen == 0 || (rc >> tb) == a.pcode;
+                if (ex) {
+                    if (WRITE && (mf || mr)) {
+                        // (non-ACGT bytes alias to a code: the prefix bytes themselves decide)
+                        const uint64_t pos = st + w0 + m;
+                        bool bf = true, br = true;
+                        for (uint32_t b = 0; b < plen; ++b) {
+                            bf = bf && a.data[pos + b] == a.P[b];
+                            br = br && a.data[pos + k - plen + b] == a.RP[b];
+                        }
+                        const uint64_t s = w0 + m, lo = lix << (a.pbits + 1);
+                        if (bf) dw_record(a, lo | s, pos, 0);
+                        if (br) dw_record(a, lo | (1ull << a.pbits) | (maxrel - s), pos, 1);
+                    }
+                    continue;
+                }
+                fmask |= mf ? 1u << m : 0u;
+                rmask |= mr ? 1u << m : 0u;
+            }
+        }
+        // ---- ranks inside each line: segmented wave scans of the lane counts ----
+        const uint32_t nf = __popc(fmask), nr = __popc(rmask);
+        const uint32_t F = dw_incl_sum(nf), R = dw_incl_sum(nr);
+        // carried counts of line m (seg0 > 0: earlier rounds took its first windows)
+        const uint32_t carf = seg0 ? c.cf : 0u, carr = seg0 ? c.cr : 0u;
+        // lane i < 16: line i's windows of this round = lanes [b_i, min(cum_i, 64))
+        const uint32_t bi_ = cum - need, ei_ = cum < 64 ? cum : 64u;
+        const uint32_t Fe = (uint32_t)__shfl((int)F, (int)(ei_ ? ei_ - 1 : 0));
+        const uint32_t Re = (uint32_t)__shfl((int)R, (int)(ei_ ? ei_ - 1 : 0));
+        const uint32_t Fb = (uint32_t)__shfl((int)F, (int)(bi_ ? bi_ - 1 : 0));
+        const uint32_t Rb = (uint32_t)__shfl((int)R, (int)(bi_ ? bi_ - 1 : 0));
+        const bool took = lane < 16 && need && bi_ < 64;
+        const uint32_t sf = took ? Fe - (bi_ ? Fb : 0u) : 0u, sr = took ? Re - (bi_ ? Rb : 0u) : 0u;
+        if (!WRITE) {
+            // complete lines: their totals (carried + this round); a line still
+            // open after the round carries its counts to the next
+            const bool present = lane < 16 && c.m + lane < c.end;
+            const bool complete = present && (tot <= 64 || lane < is || (lane == is && !part));
+            if (complete) {
+                const uint32_t f = sf + (lane == 0 ? carf : 0u), r = sr + (lane == 0 ? carr : 0u);
+                a.cnt[c.m + lane] = (uint64_t)f | ((uint64_t)r << 32);
+                a.tot[c.m + lane] = f + r;
+            }
+        } else if (nv) {
+            // this lane's rank base among its line's accepted windows of this round and before
+            const uint32_t Bf = before ? (uint32_t)__shfl((int)F, (int)(before - 1)) : 0u;
+            const uint32_t Br = before ? (uint32_t)__shfl((int)R, (int)(before - 1)) : 0u;
+            const uint32_t fb = F - nf - Bf + (li == 0 ? carf : 0u);
+            const uint32_t rb = R - nr - Br + (li == 0 ? carr : 0u);
+            const uint32_t LF = (uint32_t)lcnt, LR = (uint32_t)(lcnt >> 32);
+            const uint64_t hb = a.out_base + lbase;
+            const uint64_t lo = lix << (a.pbits + 1);
+#pragma unroll
+            for (int m = 0; m < DW_NS; ++m) {
+                const uint32_t below = (1u << m) - 1u;
+                const uint64_t s = w0 + m;
+                // (the codes again from the streams: constant shifts, no per-window key registers)
+                if (fmask & (1u << m)) {
+                    const uint64_t key = low_shr(R0, R1, 2 * (DW_NS - 1 - m)) & a.smask;
+                    const uint64_t slot = hb + fb + __popc(fmask & below);
+                    if (a.rkey32) a.rkey32[slot] = (uint32_t)key;
+                    else a.rkey[slot] = key;
+                    a.rord[slot] = lo | s;
+                }
+                if (rmask & (1u << m)) {
+                    const uint64_t key = ~low_shr(S0, S1, 2 * m) & a.smask;
+                    const uint64_t slot = hb + LF + (LR - 1u - (rb + __popc(rmask & below)));
+                    if (a.rkey32) a.rkey32[slot] = (uint32_t)key;
+                    else a.rkey[slot] = key;
+                    a.rord[slot] = lo | (1ull << a.pbits) | (maxrel - s);
+                }
+            }
+        }
+        // ---- advance: the next round starts at the first line not finished ----
+        if (tot <= 64) {
+            c.m += 16;
+            c.seg = 0;
+            c.cf = c.cr = 0;
+        } else if (!part) {
+            c.m += is + 1;
+            c.seg = 0;
+            c.cf = c.cr = 0;
+        } else {
+            const uint32_t bis = ci - rl32(need, is);
+            const uint32_t cfi = rl32(sf, is), cri = rl32(sr, is);
+            c.cf = (is == 0 ? carf : 0u) + cfi;
+            c.cr = (is == 0 ? carr : 0u) + cri;
+            c.seg = (is == 0 ? seg0 : 0) + (uint64_t)(64 - bis) * DW_NS;
+            c.m += is;
+        }
+        if (c.m < c.end) dw_fetch<WRITE>(a, c);
+    }
+}
+
+hipError_t launch_dense_windows(const DenseArgs &a, bool write, hipStream_t s) {
+    if (!a.n_lines) return hipSuccess;
+    const uint64_t waves = (a.n_lines + a.lpw - 1) / a.lpw;
+    const uint32_t grid = (uint32_t)((waves + 3) / 4);
+    if (write) hipLaunchKernelGGL(dense_windows_kernel<true>, dim3(grid), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(dense_windows_kernel<false>, dim3(grid), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace kmerhip

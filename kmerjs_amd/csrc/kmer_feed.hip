@@ -699,7 +699,96 @@ kmer_status chunk_lines(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_
     return KMER_OK;
 }
 
-// Dense-hit path: every window of every sequence line goes to its rank slot.
+// Dense-hit path, step 1, k <= 32 (kmer_dense.hip): a count pass over the
+// lines, a scan of the per-line counts, then the accepted windows written at
+// their rank slots -- the rank arrays hold only accepted windows.
+kmer_status dense_windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint64_t n_seq, uint64_t n_nl,
+                               uint64_t li0, hipStream_t s) {
+    DenseArgs g;
+    memset(&g, 0, sizeof(g));
+    g.data = d;
+    g.len = len;
+    g.lines = c->lines.p;
+    g.n_lines = n_seq;
+    g.lpw = std::max<uint64_t>(1, (n_seq + (1u << 17) - 1) >> 17);   // (<= 128 K waves)
+    g.k = c->p.k;
+    g.plen = (uint32_t)c->prefix.size();
+    g.pbits = c->pbits;
+    auto code = [](char ch) -> uint64_t { return ch == 'A' ? 0u : ch == 'C' ? 1u : ch == 'G' ? 2u : 3u; };
+    for (char ch : c->prefix) g.pcode = (g.pcode << 2) | code(ch);
+    g.smask = (c->kbits >= 64) ? ~0ull : ((1ull << c->kbits) - 1ull);
+    g.P = c->d_PR + 2 * KMAX_TILE;
+    g.RP = c->d_PR + 2 * KMAX_TILE + c->prefix.size();
+    g.err = c->d_err;
+    uint64_t total = 0;
+    if (n_seq) {
+        HIPCHK(c, c->dcnt.ensure(n_seq, s));
+        HIPCHK(c, c->dtot.ensure(n_seq, s));
+        HIPCHK(c, c->wbase.ensure(n_seq, s));
+        g.cnt = c->dcnt.p;
+        g.tot = c->dtot.p;
+        HIPCHK(c, launch_dense_windows(g, false, s));
+        ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->dtot.p, c->wbase.p, (uint64_t)0, (size_t)n_seq,
+                                               rocprim::plus<uint64_t>(), s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 14, c->wbase.p + n_seq - 1, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small + 15, c->dtot.p + n_seq - 1, 4, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(c, launch_pos_after(c->d_pos, li0 + n_nl, d, len, c->d_ends_open, s));
+    HIPCHK(c, hipEventRecord(c->ev1, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    if (n_seq) total = c->h_small[14] + (uint32_t)c->h_small[15];
+    c->host_lines = li0 + n_nl;
+    {
+        float ms = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        c->scan_ms += ms;
+        c->feed_ms += ms;
+    }
+    kmer_status st = ensure_rank_arrays(c, c->n_hits + total, c->n_hits, s);
+    if (st) return st;
+    HIPCHK(c, hipEventRecord(c->ev0, s));
+    g.hbase = c->wbase.p;
+    g.out_base = c->n_hits;
+    g.rkey = c->rkey.p;
+    g.rkey32 = c->narrow ? c->rkey32.p : nullptr;
+    g.rord = c->rord.p;
+    for (int attempt = 0; attempt < 8; ++attempt) {
+        g.recs = c->recs.p;
+        g.rec_count = c->d_rec_count;
+        g.rec_cap = c->recs.cap;
+        HIPCHK(c, hipMemsetAsync(c->d_rec_count, 0, 8, s));
+        HIPCHK(c, launch_dense_windows(g, true, s));
+        HIPCHK(c, hipEventRecord(c->ev1, s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        const uint32_t e = (uint32_t)c->h_small[5];
+        st = check_err(c, e);
+        if (st) return st;
+        float ms = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->ev0, c->ev1));
+        c->feed_ms += ms;
+        if (e & ERR_REC_OVERFLOW) {                 // (the redo writes the same slots)
+            HIPCHK(c, hipMemsetAsync(c->d_err, 0, 4, s));
+            st = ensure_records(c, c->h_small[0] + 1024);
+            if (st) return st;
+            continue;
+        }
+        break;
+    }
+    c->n_hits += total;
+    c->chunk_open = c->h_small[7] != 0;
+    const uint64_t nrec = c->h_small[0];
+    if (nrec) {
+        st = drain_records(c, d, nrec, s);
+        if (st) return st;
+    }
+    c->abs_offset += len;
+    return KMER_OK;
+}
+
+// Dense-hit path: every window of every sequence line goes to its rank slot
+// (step > 1, and KMERHIP_DENSE=slots in experiment builds); step 1 with
+// k <= 32 ranks only the accepted windows (dense_windows_feed).
 kmer_status windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s) {
     const uint64_t li0 = c->host_lines;
     kmer_status st;
@@ -707,6 +796,12 @@ kmer_status windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n
     uint64_t n_nl = 0, n_seq = 0;
     st = chunk_lines(c, d, len, n_tiles, s, true, &n_nl, &n_seq);
     if (st) return st;
+    static const bool slots_only = [] {
+        const char *e = exp_env("KMERHIP_DENSE");
+        return e && strcmp(e, "slots") == 0;
+    }();
+    if (c->p.step == 1 && c->p.k <= 32 && !slots_only) return dense_windows_feed(c, d, len, n_seq, n_nl, li0, s);
+    c->win_slots = true;                          // (the finish compacts the rejected windows' slots away)
     uint64_t total = 0;
     if (n_seq) {
         HIPCHK(c, c->wbase.ensure(n_seq, s));
@@ -884,6 +979,8 @@ kmer_status reset(kmer_ctx *c) {
     c->n_out = 0;
     c->t_keys = 0;
     c->t_fill = 0;
+    c->win_slots = false;
+    c->t_p1_fixed = c->t_p1_merged = c->t_p1_counted = 0;
     c->gm_n = 0;
     c->gm_last = 0;
     c->gm_merged = true;

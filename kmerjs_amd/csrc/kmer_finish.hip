@@ -175,10 +175,6 @@ kmer_status rank_finish(kmer_ctx *c, uint64_t n, bool partial, bool with_counts,
     hipStream_t s = c->stream;
     *nu_out = 0;
     if (n == 0) return KMER_OK;
-    // every XCD's L2 written back and invalidated before the finish chain
-    // (l2_flush_kernel): no XCD keeps lines of these reused buffers from an
-    // earlier finish, whose stale copies intermittently cost counts / keys
-    HIPCHK(c, launch_l2_flush(s));
     if (c->narrow) HIPCHK(c, c->rkey32b.ensure(n, s));
     else HIPCHK(c, c->rkey2.ensure(n, s));
     HIPCHK(c, c->ridx2.ensure(n, s));
@@ -327,6 +323,7 @@ kmer_status general_merge(kmer_ctx *c) {
         HIPCHK(c, hipMemcpyAsync(&hv[0], c->gm_flag.p, 4, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipMemcpyAsync(&hv[1], c->gm_gid.p + n - 1, 4, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
+        if (attempt == 0 && (c->p.flags & KMER_FLAG_GEN_COLLIDE_TEST)) hv[0] = 1;   // (debug: force the retry)
         if (hv[0]) continue;                       // a hash collision: another seed
         const uint64_t ng = hv[1];
         HIPCHK(c, c->gm_keys2.ensure(ng * k, s));
@@ -341,8 +338,16 @@ kmer_status general_merge(kmer_ctx *c) {
         c->gm_n = ng;
         c->gm_last = ng;
         c->gm_merged = true;
-        if (c->p.max_keys && ng + c->exotic.size() > c->p.max_keys)
-            return fail(c, KMER_E_TOO_MANY_KEYS, "more distinct keys than max_keys (reference Map limit)");
+        if (c->p.max_keys) {
+            // host records of k bytes may also be among the device entries
+            // (kmer_records_export / _import): only the other lengths are
+            // certainly distinct here; general_finish folds the k-byte ones
+            // in first, so its merge counts every key exactly once
+            uint64_t other = 0;
+            for (const auto &kv : c->exotic) other += kv.first.size() != k;
+            if (ng + other > c->p.max_keys)
+                return fail(c, KMER_E_TOO_MANY_KEYS, "more distinct keys than max_keys (reference Map limit)");
+        }
         return KMER_OK;
     }
     return fail(c, KMER_E_DEVICE, "general-path key hashes kept colliding");
@@ -498,7 +503,7 @@ kmer_status finish(kmer_ctx *c, kmer_result **out) {
     if (c->mode == MODE_PACKED || c->mode == MODE_WINDOWS) {
         st = apply_cross(c);
         if (st) return st;
-        if (c->mode == MODE_WINDOWS && !c->prefix.empty()) {
+        if (c->mode == MODE_WINDOWS && !c->prefix.empty() && c->win_slots) {
             st = compact_windows(c);
             if (st) return st;
         }

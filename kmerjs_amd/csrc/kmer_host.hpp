@@ -54,7 +54,7 @@
 using namespace kmerhip;
 
 // every KMER_FLAG_* of include/kmer_api.h
-constexpr uint32_t KMER_FLAGS_PUBLIC = 0xFFu | KMER_FLAG_FASTA | KMER_FLAG_TABLE_FIXED_TEST;
+constexpr uint32_t KMER_FLAGS_PUBLIC = 0xFFu | KMER_FLAG_FASTA | KMER_FLAG_TABLE_FIXED_TEST | KMER_FLAG_GEN_COLLIDE_TEST;
 
 namespace kmerhip {
 
@@ -143,6 +143,9 @@ struct kmer_ctx {
     uint64_t tile_cap = 0;
     DBuf<TileSum> tsum, tscan, bsum, bscan;
     DBuf<uint64_t> wcount, wbase;  // dense-hit path: windows / first rank per sequence line
+    DBuf<uint64_t> dcnt;           // dense-hit path (kmer_dense.hip): accepted forward | reverse << 32 per line
+    DBuf<uint32_t> dtot;           // ... their sum per line (scanned into wbase)
+    bool win_slots = false;        // a chunk of this session ranked every window (the finish compacts)
     DBuf<uint32_t> tcount;         // dense-hit path: '\n' per tile
     DBuf<uint64_t> tbase, nlpos;   // ... exclusive scan, chunk-relative '\n' positions (or sequence-line bounds)
     DBuf<uint16_t> nlslots;        // tile-relative '\n' positions, NL_SLOTS per tile
@@ -250,6 +253,7 @@ struct kmer_ctx {
     DBuf<SeqLine> tpieces;         // long lines cut into pieces of <= TAB_PIECE windows
     DBuf<unsigned long long> tstats;   // [0..2] final statistics, [3] big-list count, [4] digest
     uint64_t t_keys = 0;           // pass-1 slots of the session (keys, plus filler of fixed runs)
+    uint64_t t_p1_fixed = 0, t_p1_merged = 0, t_p1_counted = 0;   // pass-1 routes (kmer_table_pass1_routes)
     uint64_t t_fill = 0;           // ... of which filler slots (an estimate: windows with non-ACGT bytes are not keys)
     std::vector<uint64_t> t_cbase; // per chunk: first key in tb1
     std::vector<std::vector<uint64_t>> t_coff;   // per chunk: TAB_NB + 1 partition starts (chunk-relative)

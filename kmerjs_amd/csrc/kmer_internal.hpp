@@ -340,6 +340,33 @@ struct WinArgs {
     unsigned int *err;
 };
 
+// dense-hit path, step 1, k <= 32 (kmer_dense.hip): only accepted windows,
+// ranked by two passes over the lines
+struct DenseArgs {
+    const uint8_t *data;
+    uint64_t len;
+    const SeqLine *lines;          // by sequence ordinal (len 0: no windows)
+    uint64_t n_lines;
+    uint64_t lpw;                  // lines per wave
+    uint32_t k, plen;
+    uint32_t pbits;                // order-key position bits (PBITS_*)
+    uint64_t pcode;                // P as 2-bit codes (first base most significant)
+    uint64_t smask;                // the key: the low 2 (k - |P|) bits of the window code
+    uint64_t *cnt;                 // count pass: per line accepted forward | reverse << 32
+    uint32_t *tot;                 // count pass: per line forward + reverse
+    const uint64_t *hbase;         // write pass: per line first slot (chunk-relative, exclusive scan of tot)
+    uint64_t out_base;
+    uint32_t *rkey32;              // narrow keys (2 (k - |P|) <= 31 bits), else rkey
+    uint64_t *rkey;
+    uint64_t *rord;
+    const uint8_t *P, *RP;         // device: P and rc(P) (exotic windows' prefix bytes)
+    Record *recs;
+    unsigned long long *rec_count;
+    uint64_t rec_cap;
+    unsigned int *err;
+};
+hipError_t launch_dense_windows(const DenseArgs &a, bool write, hipStream_t s);
+
 // ---- launchers (kmer_kernels.hip) ------------------------------------------
 hipError_t launch_lines(const TileArgs &a, bool lookback, hipStream_t s);
 hipError_t launch_scan_tiles(const ScanArgs &a, hipStream_t s);
@@ -400,7 +427,6 @@ hipError_t launch_bucket_offsets(const uint32_t *H, uint32_t nb, uint32_t nblk, 
 hipError_t launch_bucket_scatter(const uint32_t *key, uint64_t n, uint32_t invalid, uint32_t shift, uint32_t nb,
                                  uint32_t nblk, const uint32_t *Hs, const uint32_t *bbase, uint16_t *pkey,
                                  uint32_t *prank, hipStream_t s);
-hipError_t launch_l2_flush(hipStream_t s);   // every XCD's L2 written back + invalidated
 hipError_t launch_bucket_heads(const uint16_t *pkey, const uint32_t *prank, const uint32_t *bbase, uint32_t nb,
                                uint32_t shift, uint32_t *hcnt, hipStream_t s);
 // multi-GPU hit exchange (kmer_exchange_prepare / kmer_finish_exchanged)

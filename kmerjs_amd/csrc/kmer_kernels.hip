@@ -1993,7 +1993,12 @@ __global__ __launch_bounds__(256) void gen_fix_kernel(const Record *__restrict__
             if (keep) q[atomicAdd(&qn, 1u)] = r;        // (<= 256 per round, flushed below)
         }
         __syncthreads();
-        if (qn > GF_Q - 256 || b + 256 >= i1) flush();
+        // one decision for the whole workgroup: read qn, then a barrier before
+        // any wave can add to it in the next round (else the waves could take
+        // different branches and meet different barriers)
+        const uint32_t nq = qn;
+        __syncthreads();
+        if (nq > GF_Q - 256 || b + 256 >= i1) flush();
     }
 }
 
@@ -2804,6 +2809,19 @@ __global__ __launch_bounds__(256) void bucket_offsets_kernel(const uint32_t *H, 
     if (tid == 0) *ticket = 0;
 }
 
+// (race probes for bucket_scatter_kernel, in experiment builds only: see the
+// Makefile's probes target and tools/bkt_race_probe.py)
+#if defined(KMERHIP_EXPERIMENTS) && defined(KMERHIP_PROBE_BKT_DELAY)
+#define BKT_PROBE_DELAY 1
+#else
+#define BKT_PROBE_DELAY 0
+#endif
+#if defined(KMERHIP_EXPERIMENTS) && defined(KMERHIP_PROBE_BKT_NOFIX)
+#define BKT_PROBE_NOFIX 1
+#else
+#define BKT_PROBE_NOFIX 0
+#endif
+
 // Scatter with the block's elements first grouped by bucket in LDS, so that
 // each bucket's run goes out as one contiguous (coalesced) piece.
 __global__ __launch_bounds__(256) void bucket_scatter_kernel(const uint32_t *key, uint64_t n, uint32_t invalid,
@@ -2833,6 +2851,15 @@ __global__ __launch_bounds__(256) void bucket_scatter_kernel(const uint32_t *key
         loc[u] = b < nb ? cnt[b] : 0u;
         sum += loc[u];
     }
+    // the global position of this block's first key of each owned bucket,
+    // loaded now so that the loads are in flight during the scan and the
+    // placement (one round trip, not one per bucket after them)
+    uint32_t gpos[BKT_MAX / 256];
+#pragma unroll
+    for (uint32_t u = 0; u < BKT_MAX / 256; ++u) {
+        const uint32_t b = threadIdx.x * (BKT_MAX / 256) + u;
+        gpos[u] = b < nb && loc[u] ? bbase[b] + Hs[(uint64_t)b * nblk + blockIdx.x] : 0u;
+    }
     const uint32_t incl = wave_incl_sum(sum);
     if ((threadIdx.x & 63) == 63) wtot[threadIdx.x >> 6] = incl;
     __syncthreads();
@@ -2848,26 +2875,45 @@ __global__ __launch_bounds__(256) void bucket_scatter_kernel(const uint32_t *key
     }
     const uint32_t valid = wtot[0] + wtot[1] + wtot[2] + wtot[3];
     __syncthreads();
+#if BKT_PROBE_DELAY
+    // race probe (experiment build only): waves 1..3 start placing late, so
+    // wave 0 reaches the rewrite of cnt[] below first
+    if (threadIdx.x >= 64)
+        for (int z = 0; z < 64; ++z) __builtin_amdgcn_s_sleep(127);
+#endif
 #pragma unroll
     for (uint32_t u = 0; u < BKT_EPB / 256; ++u) {
         if (kk[u] != invalid) {
             const uint32_t p = cnt[kk[u] >> shift] + li[u];
+#if BKT_PROBE_DELAY
+            if (p >= BKT_EPB) continue;             // (the probe keeps a raced store in range)
+#endif
             skey[p] = kk[u];
             srank[p] = (uint32_t)(base + u * 256 + threadIdx.x);
         }
     }
+    // every wave has read its local starts before cnt[] is rewritten (without
+    // this barrier a wave that got here first overwrote a bucket's local start
+    // while a slower wave still placed keys by it: keys landed in wrong skey
+    // slots, and stale slots went out -- the intermittent lost counts / keys)
+#if !BKT_PROBE_NOFIX
+    __syncthreads();
+#endif
     // cnt[b] := global position of local element 0 of bucket b (mod 2^32:
     // element e of bucket b goes to cnt[b] + e)
 #pragma unroll
     for (uint32_t u = 0; u < BKT_MAX / 256; ++u) {
         const uint32_t b = threadIdx.x * (BKT_MAX / 256) + u;
-        if (b < nb && loc[u]) cnt[b] = bbase[b] + Hs[(uint64_t)b * nblk + blockIdx.x] - lst[u];
+        if (b < nb && loc[u]) cnt[b] = gpos[u] - lst[u];
     }
     __syncthreads();
     const uint32_t lo_mask = (1u << shift) - 1u;
     for (uint32_t e = threadIdx.x; e < valid; e += 256) {
         const uint32_t k = skey[e], b = k >> shift;
         const uint32_t pos = cnt[b] + e;
+#if BKT_PROBE_DELAY
+        if (b >= nb || pos >= n) continue;          // (the probe keeps a raced store in range)
+#endif
         pkey[pos] = (uint16_t)(k & lo_mask);
         prank[pos] = srank[e];
     }
@@ -3596,21 +3642,6 @@ hipError_t launch_bucket_scatter(const uint32_t *key, uint64_t n, uint32_t inval
                        pkey, prank);
     return hipGetLastError();
 }
-// Every XCD's L2 written back and invalidated (system-scope fence per wave,
-// workgroups dealt round robin over the XCDs): issued at the start of the
-// ordered and table finishes.  Ordered counts lost counts / keys
-// intermittently when buffers were reused (k = 3 after table-mode counts in
-// the same process; the C4 hit exchange), consistent with an XCD's L2 keeping
-// lines of a reused allocation across kernels
-__global__ __launch_bounds__(64) void l2_flush_kernel() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
-}
-
-hipError_t launch_l2_flush(hipStream_t s) {
-    hipLaunchKernelGGL(l2_flush_kernel, dim3(256), dim3(64), 0, s);
-    return hipGetLastError();
-}
-
 hipError_t launch_bucket_heads(const uint16_t *pkey, const uint32_t *prank, const uint32_t *bbase, uint32_t nb,
                                uint32_t shift, uint32_t *hcnt, hipStream_t s) {
     hipLaunchKernelGGL(bucket_heads_kernel, dim3(nb), dim3(1024), 0, s, pkey, prank, bbase, shift, hcnt);

@@ -72,6 +72,7 @@ kmer_status table_pass1_counted(kmer_ctx *c, TabArgs &a, hipStream_t s) {
     c->t_cbase.push_back(c->t_keys);
     c->t_coff.push_back(std::move(off));
     c->t_keys += n_c;
+    c->t_p1_counted += 1;
     return KMER_OK;
 }
 
@@ -118,6 +119,7 @@ kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done
     // remains, until the filler is at most 1/12 of the keys (C5: down to one
     // per CU beat two per CU by ~1 %, A/B: less filler through pass 2)
     const uint32_t min_wg = (uint32_t)std::max(c->n_cu, 1);
+    bool merged = false;
     while (region > tot + tot / 12 && a.nwg >= 2 * min_wg && !(c->p.flags & KMER_FLAG_TABLE_FIXED_TEST)) {
         const uint32_t nwg2 = (a.nwg + 1) / 2;
         std::vector<uint64_t> h2(nwg2, 0);
@@ -126,6 +128,7 @@ kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done
         a.nwg = nwg2;
         a.lpw *= 2;
         region = sized(hw, a.nwg);
+        merged = true;
     }
     // (still more than 1/8 filler: the counting pass moves fewer bytes through
     // pass 2 -- filler costs ~3 x 8 B per slot, the counting pass one more
@@ -167,6 +170,8 @@ kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done
                 (unsigned long long)region, (unsigned long long)S);
     c->t_ms[0] += ms0;
     c->t_ms[1] += ms1;
+    c->t_p1_fixed += 1;
+    c->t_p1_merged += merged ? 1 : 0;
     *done = true;
     return KMER_OK;
 }
@@ -281,7 +286,6 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
     c->t_done = true;
     const uint64_t n = c->t_keys;
     if (n == 0) return KMER_OK;
-    HIPCHK(c, launch_l2_flush(s));            // (as rank_finish: no stale L2 lines of reused buffers)
     // the table is written over the pass-1 keys (dead after pass 2)
     if (!B1) B1 = c->tb1.p;
     c->t_ent = const_cast<uint64_t *>(B1);

@@ -439,6 +439,43 @@ int oracle_table_digest_buffer(const uint8_t *buf, size_t len, uint32_t k, uint6
     return ORACLE_OK;
 }
 
+/* the table digest of FASTA records (KMER_FLAG_FASTA; the record rules of
+ * oracle_count_fasta above: '>' opens a record, its other lines joined with one
+ * trailing '\r' each dropped, sequences of length > 1 counted) -- BASELINE C5's
+ * .fsa-style contigs in table mode */
+int oracle_table_digest_fasta(const uint8_t *buf, size_t len, uint32_t k, uint64_t *digest, uint64_t *windows) {
+    if (k == 0 || k > 31) return ORACLE_E_NONASCII + 2;
+    *digest = 0;
+    *windows = 0;
+    uint8_t *seq = NULL;
+    size_t seq_len = 0, seq_cap = 0, pos = 0;
+    while (pos < len) {
+        const uint8_t *nl = memchr(buf + pos, '\n', len - pos);
+        size_t end = nl ? (size_t)(nl - buf) : len;
+        size_t L = end - pos;
+        if (!nl && L == 0) break;
+        const uint8_t *line = buf + pos;
+        pos = nl ? end + 1 : len;
+        if (L > 0 && line[L - 1] == '\r') --L;
+        if (L > 0 && line[0] == '>') {
+            if (seq_len > 1) digest_line(seq, seq_len, k, digest, windows);
+            seq_len = 0;
+            continue;
+        }
+        if (seq_len + L > seq_cap) {
+            seq_cap = (seq_len + L) * 2 + 64;
+            uint8_t *q = realloc(seq, seq_cap);
+            if (!q) { free(seq); return ORACLE_E_OOM; }
+            seq = q;
+        }
+        if (L) memcpy(seq + seq_len, line, L);
+        seq_len += L;
+    }
+    if (seq_len > 1) digest_line(seq, seq_len, k, digest, windows);
+    free(seq);
+    return ORACLE_OK;
+}
+
 #include <pthread.h>
 
 typedef struct {

@@ -51,6 +51,9 @@ def lib():
         L.oracle_table_digest_buffer.restype = ctypes.c_int
         L.oracle_table_digest_buffer.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32,
                                                  ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        L.oracle_table_digest_fasta.restype = ctypes.c_int
+        L.oracle_table_digest_fasta.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint32,
+                                                ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         L.oracle_table_digest_synth.restype = ctypes.c_int
         L.oracle_table_digest_synth.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                                 ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64),
@@ -138,6 +141,16 @@ def table_digest(data: bytes, k: int):
     (digest, windows examined per strand)."""
     d, w = ctypes.c_uint64(), ctypes.c_uint64()
     st = lib().oracle_table_digest_buffer(data, len(data), k, ctypes.byref(d), ctypes.byref(w))
+    if st:
+        raise OracleError("oracle status %d" % st)
+    return d.value, w.value
+
+
+def table_digest_fasta(data: bytes, k: int):
+    """table_digest over FASTA records (KMER_FLAG_FASTA: a record's lines
+    joined): (digest, windows examined per strand)."""
+    d, w = ctypes.c_uint64(), ctypes.c_uint64()
+    st = lib().oracle_table_digest_fasta(data, len(data), k, ctypes.byref(d), ctypes.byref(w))
     if st:
         raise OracleError("oracle status %d" % st)
     return d.value, w.value

@@ -17,6 +17,11 @@ the build container:
 * C3  (100 M reads, seed 3, k 31, no prefix, table mode): the table digest
   (kmer_table_digest's definition: a sum over forward windows, no map) by
   oracle_table_digest_synth on `procs` threads.
+* C5  (1 GB of contigs per GPU, seed 5 = rank 0's, k 21, canonical table mode):
+  the table digest of bench.make_contigs' single-line file read by the
+  reference's rule (lines with index % 4 == 1, lib/kmers.js:151;
+  oracle_table_digest) -- "c5" -- and of the 60-column .fsa file counted by
+  record (KMER_FLAG_FASTA; oracle_table_digest_fasta) -- "c5fa".
 """
 import argparse
 import hashlib
@@ -67,7 +72,7 @@ def ordered_map(seed, n_reads, prefix, k, procs):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--procs", type=int, default=8)
-    ap.add_argument("--only", default="c2,c4,c3")
+    ap.add_argument("--only", default="c2,c4,c3,c5,c5fa")
     a = ap.parse_args()
     out_path = os.path.join(REPO, "tests", "golden", "fullsize.json")
     out = json.load(open(out_path)) if os.path.exists(out_path) else {}
@@ -84,6 +89,15 @@ def main():
             d, w = oracle.table_digest_synth(3, 0, 100_000_000, 31, a.procs)
             r = {"table_digest": d, "forward_windows": w,
                  "workload": "C3: 100 M reads, seed 3, k 31, no prefix (table digest)"}
+        elif cfg in ("c5", "c5fa"):
+            import bench
+            data, _ = bench.make_contigs(5, 1_000_000_000, 21, width=60 if cfg == "c5fa" else 0)
+            d, w = (oracle.table_digest_fasta if cfg == "c5fa" else oracle.table_digest)(data, 21)
+            r = {"table_digest": d, "forward_windows": w, "bytes": len(data),
+                 "workload": "C5%s: bench.make_contigs(seed 5, 1 GB%s), k 21, canonical table mode (table digest)"
+                             % (" FASTA" if cfg == "c5fa" else "",
+                                ", 60 columns, counted by record" if cfg == "c5fa" else
+                                ", single-line, lines % 4 == 1 counted")}
         else:
             raise SystemExit("unknown config " + cfg)
         r["seconds"] = round(time.time() - t, 1)

@@ -12,7 +12,7 @@ def header_symbols():
     for h in ("kmer_api.h", "kmer_match.h"):
         with open(os.path.join(REPO, "include", h)) as f:
             text += f.read()
-    return sorted(set(re.findall(r"\b(kmer_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(kmer_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_library_exports_every_header_symbol():
@@ -57,7 +57,7 @@ def test_product_does_not_reference_oracle():
 
 
 EXPERIMENT_ENV = ("KMERHIP_TAB_ABLATE", "KMERHIP_TAB_RANGE", "KMERHIP_TAB_FINAL", "KMERHIP_NL", "KMERHIP_TAB_S1",
-                  "KMERHIP_TAB_S2", "KMERHIP_ONE_STREAM", "KMERHIP_TAB_PROF")
+                  "KMERHIP_TAB_S2", "KMERHIP_ONE_STREAM", "KMERHIP_TAB_PROF", "KMERHIP_DENSE")
 
 
 def test_shipping_library_has_no_experiment_switches():

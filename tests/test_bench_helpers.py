@@ -83,3 +83,31 @@ def test_world_size_must_equal_gpus():
     p = subprocess.run([sys.executable, bench.__file__, "--gpus", "4"], env=env, capture_output=True, text=True,
                        timeout=60)
     assert p.returncode != 0 and "WORLD_SIZE=2 but --gpus 4" in p.stderr
+
+
+@pytest.mark.parametrize("config", ["c2", "c4", "c3"])
+def test_dry_run_plans_record_aligned_shards(config):
+    """`bench.py --gpus 8 --dry-run` (no GPU): 8 ranks, each holding a
+    record-aligned shard whose line / byte offsets are multi.shard_plan's --
+    rank r starts at read r * n (line 4 r n, byte 317 r n), the shards tile the
+    job without overlap; C3 splits its 100 M reads (strong scaling), C2 / C4
+    hold a fixed share per GPU (weak)."""
+    import json
+    import os
+    import subprocess
+    from kmerjs_amd.multi import shard_plan
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, bench.__file__, "--gpus", "8", "--dry-run", "--config", config], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    rows = [json.loads(x) for x in p.stdout.strip().splitlines()]
+    assert [r["rank"] for r in rows] == list(range(8))
+    n = {"c2": 10_000_000, "c4": 125_000_000, "c3": 100_000_000 // 8}[config]
+    for r in rows:
+        want = shard_plan(n, r["rank"])
+        assert {x: r[x] for x in want} == want
+        assert r["lines_before"] == 4 * n * r["rank"] and r["byte_offset"] == 317 * n * r["rank"]
+        assert r["scaling"] == ("strong" if config == "c3" else "weak")
+    for a, b in zip(rows, rows[1:]):
+        assert a["first_read"] + a["n_reads"] == b["first_read"]
+    assert rows[0]["merge"] == ("dense" if config == "c4" else "hits")

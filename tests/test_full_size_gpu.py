@@ -250,3 +250,45 @@ def test_c4_shard_full_size_properties(native):
     assert torch.equal(torch.as_tensor(_CudaArray(mk, mm * k, "|u1"), device=dev).view(mm, k), keys)
     for c in ctrs + [ctr]:
         c.close()
+
+
+@pytest.mark.parametrize("fasta", [False, True], ids=["single_line", "fasta60"])
+def test_c5_full_size_pins(native, fasta):
+    """BASELINE configs[4] at the size bench.py times: 1 GB of contigs (10 kb -
+    1 Mb, bench.make_contigs seed 5 = rank 0's), k = 21, canonical table mode.
+    Single-line: only lines with index % 4 == 1 count (lib/kmers.js:151);
+    fasta60: 60-column records joined (KMER_FLAG_FASTA, an extension).  The
+    table digest and Σ counts equal the oracle's streamed over the same bytes
+    (tests/golden/fullsize.json "c5" / "c5fa"), on the route the bench takes
+    (pass 1's workgroup shares merged: kmer_table_pass1_routes) and with that
+    merging disabled (KMER_FLAG_TABLE_FIXED_TEST)."""
+    import torch
+    from bench import make_contigs
+    from tests.util import fullsize_golden
+    gold = fullsize_golden()["c5fa" if fasta else "c5"]
+    data, _ = make_contigs(5, 1_000_000_000, 21, width=60 if fasta else 0)
+    assert len(data) == gold["bytes"]
+    buf = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    del data
+    base = native.FLAG_CANONICAL | (native.FLAG_FASTA if fasta else 0)
+    seen = []
+    for flags in (base, base | native.FLAG_TABLE_FIXED_TEST):
+        ctr = native.Counter(k=21, prefix=b"", flags=flags)
+        try:
+            for _ in range(2):                       # (a second finish on the reused buffers)
+                ctr.reset()
+                ctr.feed_device(buf.data_ptr(), buf.numel())
+                ctr.finish(want_result=False)
+                canon, keys, total = ctr.table_stats()
+                assert total == gold["forward_windows"] and keys == canon
+                assert ctr.table_digest() == gold["table_digest"]
+                routes = ctr.table_pass1_routes()
+                seen.append(routes)
+                assert routes["fixed"] >= 1
+                if flags & native.FLAG_TABLE_FIXED_TEST:
+                    assert routes["merged"] == 0
+                else:
+                    assert routes["merged"] == routes["fixed"] and routes["counted"] == 0, routes
+        finally:
+            ctr.close()
+    print("c5 routes", "fasta" if fasta else "single", seen)

@@ -121,3 +121,28 @@ def test_general_max_keys(native):
         ctr.count_buffer(data)
     assert e.value.status == 5
     ctr.close()
+
+
+def test_general_long_prefix_and_forced_collision_retry(native):
+    """Two routes the other cases miss: an A/C/G/T prefix longer than 16 bytes
+    (gen_cand_kernel verifies candidates byte for byte in global memory,
+    gen_bytes_eq, instead of in LDS), and the merge's collision retry (the
+    (h2, h1) LSD sort + gather of h2), forced on the first attempt by
+    KMER_FLAG_GEN_COLLIDE_TEST.  Both against the oracle (lib/kmers.js:88-100)."""
+    from oracle import oracle
+    data = bytearray(_reads_with_n(17, 12000))
+    arr = np.frombuffer(data, dtype=np.uint8).reshape(-1, 317)
+    p20 = bytes(arr[5, 13 + 10:13 + 30])
+    assert all(ch in b"ACGT" for ch in p20)
+    rc20 = oracle.complement(p20)
+    for i in range(0, 12000, 37):                 # the prefix and its complement planted in many reads
+        arr[i, 13 + 40:13 + 60] = np.frombuffer(p20 if i % 2 else rc20, dtype=np.uint8)
+    data = bytes(data)
+    for k, prefix, flags in ((70, p20, 0), (66, p20[:18], 0), (70, b"ATGAC", native.FLAG_GEN_COLLIDE_TEST),
+                             (40, b"", native.FLAG_GEN_COLLIDE_TEST)):
+        want = oracle.count_buffer(data, prefix, k, 1)
+        assert len(want) > 100
+        ctr = native.Counter(k=k, prefix=prefix, flags=flags)
+        got = ctr.count_buffer(data).entries()
+        ctr.close()
+        assert first_diff(got, want) is None, (k, prefix, flags)

@@ -477,3 +477,36 @@ def test_device_group_through_the_c_abi(native, golden, inputs, devs, tmp_path):
     with pytest.raises(native.KmerError):          # device-resident calls are single-device only
         ctr.reset()
     ctr.close()
+
+
+def test_bucket_finish_repeated_after_table_counts(native):
+    """Regression for the round-5 intermittent lost counts (DESIGN §8, round 6:
+    an LDS race in bucket_scatter_kernel -- a wave rewrote a bucket's local
+    start while slower waves still placed keys by it).  The failing sequences
+    of the records: ordered k = 3 (one bucket) right after table-mode counts in
+    the same process (gpurun_out/abtab/r8.txt: one count of CTT and the key CGT
+    lost), and C2's finish shape (k = 16, ATGAC: 256 buckets); each repeated on
+    the same reused buffers, every repeat exact against the oracle
+    (lib/kmers.js:95: Map counts are exact)."""
+    from oracle import oracle
+    rng = np.random.default_rng(3)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    recs = []
+    for i in range(12000):
+        L = 9 if i % 5 else 150
+        s = acgt[rng.integers(0, 4, L)].tobytes()
+        recs.append(b"@r%d\n%s\n+\n%s\n" % (i, s, b"I" * L))
+    short = b"".join(recs)
+    reads = oracle.synth_fastq(11, 0, 100_000)
+    tab = native.Counter(k=16, prefix=b"", flags=native.FLAG_UNORDERED)
+    tab.count_buffer(short)
+    tab.close()
+    for data, k, prefix in ((short, 3, b""), (short, 8, b"A"), (reads, 16, b"ATGAC"), (reads, 3, b"")):
+        want = oracle.count_buffer(data, prefix, k, 1)
+        ctr = native.Counter(k=k, prefix=prefix)
+        try:
+            for rep in range(6):
+                got = ctr.count_buffer(data).entries()
+                assert got == want, (k, prefix, rep, first_diff(got, want))
+        finally:
+            ctr.close()

@@ -145,6 +145,28 @@ def test_streamed_table_digest_equals_map_digest():
     assert oracle.table_digest_synth(3, 500, 4000, 31, 3) == oracle.table_digest(clean, 31)
 
 
+def test_streamed_fasta_table_digest_equals_fasta_map_digest():
+    # oracle_table_digest_fasta (C5 .fsa contigs, records joined) == the table
+    # digest of oracle_count_fasta's Map, on wrapped, CRLF, blank-line and
+    # headerless inputs; and the single-line contig file read as FASTQ (the
+    # reference's rule, lib/kmers.js:151) through oracle_table_digest
+    import bench
+    from tests.fasta_util import make_fasta
+    from tests.util import table_digest_from_map
+    cases = [make_fasta(1, 20, 400), make_fasta(2, 20, 300, crlf=True, blank=0.2),
+             make_fasta(3, 15, 200, headerless=True), make_fasta(4, 10, 100, width=1), b"", b">h\nA\nC\n"]
+    contigs60, _ = bench.make_contigs(5, 300_000, 21, width=60)
+    cases.append(contigs60)
+    for data in cases:
+        for k in (21, 4, 1):
+            ents = oracle.count_buffer(data, b"", k, 1, fasta=True)
+            got, _ = oracle.table_digest_fasta(data, k)
+            assert got == table_digest_from_map(ents, k), (data[:30], k)
+    single, _ = bench.make_contigs(5, 300_000, 21)
+    got, _ = oracle.table_digest(single, 21)
+    assert got == table_digest_from_map(oracle.count_buffer(single, b"", 21, 1), 21)
+
+
 def test_fullsize_golden_c2_is_the_reference_digest():
     # tests/golden/fullsize.json's C2 answer (the oracle, streamed and merged
     # over shards) equals the reference's own readFile() run on the same bytes
