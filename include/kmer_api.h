@@ -273,12 +273,15 @@ kmer_status kmer_table_device(kmer_ctx *ctx, const void **d_entries, const void 
  * of an exchanged table add up -- a size-independent check of a table that is
  * too large to compare entry by entry.  Record keys are not included. */
 kmer_status kmer_table_digest(kmer_ctx *ctx, uint64_t *digest);
-/* Diagnostics of table mode's pass 1 since the last reset: chunks whose keys
- * went out in fixed-capacity runs (fixed), of them the chunks whose
- * workgroup shares were merged first (merged: small shares, e.g. long
+/* Diagnostics of table mode's routes since the last reset.  Pass 1: chunks
+ * whose keys went out in fixed-capacity runs (p1_fixed), of them the chunks
+ * whose workgroup shares were merged first (p1_merged: small shares, e.g. long
  * contigs cut into pieces), and chunks counted by the two-pass route
- * (counted).  Lets a test assert which route a workload took. */
-kmer_status kmer_table_pass1_routes(kmer_ctx *ctx, uint64_t *fixed, uint64_t *merged, uint64_t *counted);
+ * (p1_counted).  Pass 2: finishes that ran with fixed bucket capacities and no
+ * histogram pass (p2_fixed: large buckets).  Lets a test assert which route a
+ * workload took. */
+kmer_status kmer_table_routes(kmer_ctx *ctx, uint64_t *p1_fixed, uint64_t *p1_merged, uint64_t *p1_counted,
+                              uint64_t *p2_fixed);
 /* Table mode across ranks (replaces the one Map.set stream of lib/kmers.js:95
  * when the count is sharded over GPUs; reads are independent, :151-155).
  * Rank o (of `world` <= 1024) owns the pass-1 partitions [o*1024/world,

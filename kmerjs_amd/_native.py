@@ -35,7 +35,7 @@ EXPORTS = ["kmer_open", "kmer_close", "kmer_count_file", "kmer_count_buffer", "k
            "kmer_lines", "kmer_result_size", "kmer_result_lines", "kmer_result_get",
            "kmer_result_arrays", "kmer_result_firsts", "kmer_result_write", "kmer_result_free",
            "kmer_synth_fastq_device",
-           "kmer_last_timing", "kmer_phase_times", "kmer_table_stats", "kmer_table_digest", "kmer_table_pass1_routes", "kmer_table_device",
+           "kmer_last_timing", "kmer_phase_times", "kmer_table_stats", "kmer_table_digest", "kmer_table_routes", "kmer_table_device",
            "kmer_table_exchange_prepare", "kmer_table_finish_exchanged",
            "kmer_status_string", "kmer_last_error", "kmer_version"]
 # include/kmer_match.h (the template matcher, same library)
@@ -122,7 +122,7 @@ def _load():
                                             ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32)]),
         "kmer_table_stats": (ctypes.c_int, [vp, pu64, pu64, pu64]),
         "kmer_table_digest": (ctypes.c_int, [vp, pu64]),
-        "kmer_table_pass1_routes": (ctypes.c_int, [vp, pu64, pu64, pu64]),
+        "kmer_table_routes": (ctypes.c_int, [vp, pu64, pu64, pu64, pu64]),
         "kmer_table_device": (ctypes.c_int, [vp, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.POINTER(vp),
                                              ctypes.POINTER(vp), pu64]),
         "kmer_table_exchange_prepare": (ctypes.c_int, [vp, ctypes.c_uint32, ctypes.POINTER(vp), pu64, pu64]),
@@ -377,12 +377,13 @@ class Counter:
         self._check(LIB.kmer_table_digest(self.h, ctypes.byref(d)), "table_digest")
         return d.value
 
-    def table_pass1_routes(self):
-        """Table mode pass-1 routes since the last reset: {fixed, merged, counted} chunks."""
-        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
-        self._check(LIB.kmer_table_pass1_routes(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)),
-                    "table_pass1_routes")
-        return {"fixed": a.value, "merged": b.value, "counted": c.value}
+    def table_routes(self):
+        """Table mode routes since the last reset: pass-1 chunks {fixed, merged, counted}, and
+        finishes whose pass 2 ran with fixed bucket capacities (p2_fixed)."""
+        a, b, c, d = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(LIB.kmer_table_routes(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c), ctypes.byref(d)),
+                    "table_routes")
+        return {"fixed": a.value, "merged": b.value, "counted": c.value, "p2_fixed": d.value}
 
     def table_device(self):
         """Table mode: (d_entries, d_bucket_start, d_bucket_len, d_big, n_big) in device memory."""

@@ -133,8 +133,8 @@ kmer_status kmer_open(const kmer_params *pp, kmer_ctx **out) {
     if ((pp->flags & (KMER_FLAG_UNORDERED | KMER_FLAG_CANONICAL)) && pp->step == 1 && plen <= k &&
         k <= (uint32_t)KMAX_PACKED && (plen == 0 || acgt))
         c->mode = MODE_TABLE;
-    else if (dense_ok && (plen == 0 ? k <= 31 : (acgt && plen <= 3 && k <= (uint32_t)KMAX_DENSE)))
-        c->mode = MODE_WINDOWS;
+    else if (dense_ok && (plen == 0 ? k <= 31 : (acgt && plen <= 3 && k <= (uint32_t)KMAX_TILE)))
+        c->mode = MODE_WINDOWS;                 // (a 1-3-base prefix hits densely: kmer_dense.hip, k <= 64)
     else if (win_step)
         c->mode = MODE_WINDOWS;                 // step > 1: every stepped window ranked (the tile scan has no line ends)
     else if (dense_ok && plen > 0 && k <= (uint32_t)KMAX_TILE)
@@ -794,9 +794,10 @@ kmer_status kmer_table_digest(kmer_ctx *c, uint64_t *digest) {
     return KMER_OK;
 }
 
-kmer_status kmer_table_pass1_routes(kmer_ctx *c, uint64_t *fixed, uint64_t *merged, uint64_t *counted) {
+kmer_status kmer_table_routes(kmer_ctx *c, uint64_t *p1_fixed, uint64_t *p1_merged, uint64_t *p1_counted,
+                              uint64_t *p2_fixed) {
     if (!c) return KMER_E_BAD_PARAM;
-    uint64_t f = 0, m = 0, n = 0;
+    uint64_t f = 0, m = 0, n = 0, f2 = 0;
     if (!c->group.empty()) {                         // a group: its children's routes add up
         for (kmer_ctx *x : c->group) {
             if (hipSetDevice(x->device) != hipSuccess) return KMER_E_DEVICE;
@@ -804,16 +805,19 @@ kmer_status kmer_table_pass1_routes(kmer_ctx *c, uint64_t *fixed, uint64_t *merg
             f += x->t_p1_fixed;
             m += x->t_p1_merged;
             n += x->t_p1_counted;
+            f2 += x->t_p2_fixed;
         }
     } else {
         SETTLE(c);
         f = c->t_p1_fixed;
         m = c->t_p1_merged;
         n = c->t_p1_counted;
+        f2 = c->t_p2_fixed;
     }
-    if (fixed) *fixed = f;
-    if (merged) *merged = m;
-    if (counted) *counted = n;
+    if (p1_fixed) *p1_fixed = f;
+    if (p1_merged) *p1_merged = m;
+    if (p1_counted) *p1_counted = n;
+    if (p2_fixed) *p2_fixed = f2;
     return KMER_OK;
 }
 

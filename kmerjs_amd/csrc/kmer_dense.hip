@@ -53,20 +53,32 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
            ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)src) << 32);
 }
 
-// 128-bit (lo, hi) >> n, n < 128 (runtime)
-__device__ __forceinline__ void shr128(uint64_t &lo, uint64_t &hi, uint32_t n) {
-    if (n >= 64) {
-        lo = hi >> (n - 64);
-        hi = 0;
-    } else if (n) {
-        lo = (lo >> n) | (hi << (64 - n));
-        hi >>= n;
+// the NW-word value w >>= n (runtime n < 64 NW)
+template <int NW>
+__device__ __forceinline__ void shrw(uint64_t (&w)[NW], uint32_t n) {
+    const uint32_t q = n >> 6, r = n & 63u;
+    uint64_t o[NW];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        uint64_t lo = 0, hi = 0;
+#pragma unroll
+        for (int j = 0; j < NW; ++j) {               // (selects: no dynamic register indexing)
+            lo = (uint32_t)j == i + q ? w[j] : lo;
+            hi = (uint32_t)j == i + q + 1 ? w[j] : hi;
+        }
+        o[i] = r ? (lo >> r) | (hi << (64 - r)) : lo;
     }
+#pragma unroll
+    for (int i = 0; i < NW; ++i) w[i] = o[i];
 }
 
-// the low 64 bits of (lo, hi) >> n, n < 64 (a constant once the window loops unroll)
-__device__ __forceinline__ uint64_t low_shr(uint64_t lo, uint64_t hi, uint32_t n) {
-    return n ? (lo >> n) | (hi << (64 - n)) : lo;
+// bits [n, n + 128) of w (n < 64, a constant once the window loops unroll):
+// *lo = the first 64, *hi = the next 64 (0 past the stream)
+template <int NW>
+__device__ __forceinline__ void extract(const uint64_t (&w)[NW], uint32_t n, uint64_t *lo, uint64_t *hi) {
+    *lo = n ? (w[0] >> n) | (w[1] << (64 - n)) : w[0];
+    if (NW > 2) *hi = n ? (w[1] >> n) | (w[NW > 2 ? 2 : 1] << (64 - n)) : w[1];
+    else *hi = n ? w[1] >> n : w[1];
 }
 
 // A wave's position in its share of sequence lines; lane i < 16 holds the
@@ -110,21 +122,42 @@ __device__ __forceinline__ void dw_record(const DenseArgs &a, uint64_t order, ui
     }
 }
 
+// a refused rank slot (count and write passes disagree): ERR_DENSE_RANK, and
+// the first one's context for the host's error message
+__device__ __forceinline__ void dw_refuse(const DenseArgs &a, uint64_t line, uint64_t s, uint32_t strand, uint64_t lcnt,
+                                          uint64_t rank, uint64_t slot) {
+    atomicOr(a.err, ERR_DENSE_RANK);
+    if (a.dbg && atomicCAS(&a.dbg[0], 0ull, 1ull) == 0ull) {
+        a.dbg[1] = line;
+        a.dbg[2] = s;
+        a.dbg[3] = strand;
+        a.dbg[4] = lcnt;
+        a.dbg[5] = rank;
+        a.dbg[6] = slot;
+        a.dbg[7] = a.out_end;
+    }
+}
+
 }  // namespace
 
 // One pass over a wave's share of lines (lpw consecutive sequence ordinals).
 // COUNT (WRITE false): cnt[m] = accepted forward | accepted reverse << 32 and
 // tot[m] = their sum, per line.  WRITE: keys and order keys of the accepted
 // windows at their rank slots (out_base + hbase[m] + rank), records of the
-// exotic ones.
-template <bool WRITE>
+// exotic ones.  WIDE (32 < k <= 64): 21 dwords per lane, 192-bit streams,
+// 128-bit window codes (key = the low 64 bits, keyh = the bits above).
+template <bool WRITE, bool WIDE>
 __global__ __launch_bounds__(256) void dense_windows_kernel(DenseArgs a) {
+    constexpr int NDW = WIDE ? 21 : 13;            // 16 + k - 1 bytes + 3 of alignment
+    constexpr int NW = WIDE ? 3 : 2;               // stream words
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t wave = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const uint32_t k = a.k, plen = a.plen;
     const uint64_t maxrel = (1ull << a.pbits) - 1ull;
-    const uint64_t kmask2 = k >= 32 ? ~0ull : ((1ull << (2 * k)) - 1ull);
-    const uint32_t kmask1 = k >= 32 ? ~0u : ((1u << k) - 1u);
+    // masks of a 2k-bit code (lo, hi) and of k per-byte flags
+    const uint64_t cm_lo = k >= 32 ? ~0ull : ((1ull << (2 * k)) - 1ull);
+    const uint64_t cm_hi = k <= 32 ? 0ull : k >= 64 ? ~0ull : ((1ull << (2 * k - 64)) - 1ull);
+    const uint64_t kmask1 = k >= 64 ? ~0ull : ((1ull << k) - 1ull);
     const uint32_t tb = 2 * (k - plen);               // prefix bits sit above the suffix
     DCur c;
     c.m = wave * a.lpw;
@@ -134,6 +167,11 @@ __global__ __launch_bounds__(256) void dense_windows_kernel(DenseArgs a) {
     if (c.m >= c.end) return;
     dw_fetch<WRITE>(a, c);
     const uint8_t *const dend = a.data + a.len;
+    // the top 2 |P| bits of a code (lo, hi)
+    auto top = [&](uint64_t lo, uint64_t hi) -> uint64_t {
+        if (!WIDE || tb < 64) return tb == 0 ? lo : (lo >> tb) | (WIDE && tb ? hi << (64 - tb) : 0ull);
+        return hi >> (tb - 64);
+    };
     while (c.m < c.end) {
         // ---- deal the lanes over lines m .. m + 15 ----
         const uint64_t Wraw = c.dlen >= k ? c.dlen - k + 1 : 0;
@@ -168,15 +206,17 @@ __global__ __launch_bounds__(256) void dense_windows_kernel(DenseArgs a) {
         }
         // ---- the lane's 16 windows: codes of the bytes [st + w0, st + w0 + 16 + k - 1) ----
         uint32_t fmask = 0, rmask = 0;
-        uint64_t S0 = 0, S1 = 0, R0 = 0, R1 = 0;        // the code streams (kept for the write-out)
+        uint64_t S[NW], R[NW];                          // the code streams (kept for the write-out)
+#pragma unroll
+        for (int w = 0; w < NW; ++w) S[w] = R[w] = 0;
         const uint32_t nv = act ? (uint32_t)(Wl - w0 < (uint64_t)DW_NS ? Wl - w0 : (uint64_t)DW_NS) : 0u;
         if (nv) {
             const uint8_t *p = a.data + st + w0;
             const uint32_t off = (uint32_t)((uintptr_t)p & 3u);
             const uint32_t *pw = (const uint32_t *)(p - off);
-            uint64_t EX = 0;
+            uint64_t EX0 = 0, EX1 = 0;
 #pragma unroll
-            for (int i = 0; i < DW_NDW; ++i) {
+            for (int i = 0; i < NDW; ++i) {
                 uint32_t x = 0x41414141u;                // ('A' past the input: never inside a window)
                 const uint8_t *q = (const uint8_t *)(pw + i);
                 if (q < dend && (uint32_t)(4 * i) < off + nv + k - 1) {
@@ -192,28 +232,32 @@ __global__ __launch_bounds__(256) void dense_windows_kernel(DenseArgs a) {
                 const uint32_t ms = __builtin_amdgcn_udot4(cc, 0x01041040u, 0u, false);   // first byte highest
                 const uint32_t ne = __builtin_amdgcn_perm(0u, 0x54474341u, cc) ^ x;     // 0 where A/C/G/T
                 const uint32_t nz = (((ne & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | ne) & 0x80808080u;
-                EX |= (uint64_t)__builtin_amdgcn_udot4(nz >> 7, 0x08040201u, 0u, false) << (4 * i);
-                if (i < 8) S0 |= (uint64_t)ls << (8 * i);
-                else S1 |= (uint64_t)ls << (8 * (i - 8));
-                const int rb = 8 * (DW_NDW - 1 - i);     // R: dword i's byte at bits [rb, rb + 8)
-                if (rb < 64) R0 |= (uint64_t)ms << rb;
-                else R1 |= (uint64_t)ms << (rb - 64);
+                const uint64_t e4 = __builtin_amdgcn_udot4(nz >> 7, 0x08040201u, 0u, false);
+                if (i < 16) EX0 |= e4 << (4 * i);
+                else EX1 |= e4 << (4 * (i - 16));
+                S[i / 8] |= (uint64_t)ls << (8 * (i % 8));
+                const int rb = 8 * (NDW - 1 - i);        // R: dword i's byte at bits [rb, rb + 8)
+                R[rb / 64] |= (uint64_t)ms << (rb % 64);
             }
-            // S >> 2 off: window m's LS code at bits [2m, 2m + 2k); R >> 2 (37 - off - k):
+            // S >> 2 off: window m's LS code at bits [2m, 2m + 2k); R >> 2 (4 NDW - 15 - off - k):
             // window m's MS code at bits [2 (15 - m), 2 (15 - m) + 2k)
-            shr128(S0, S1, 2 * off);
-            shr128(R0, R1, 2 * (37 - off - k));
-            EX >>= off;
+            shrw<NW>(S, 2 * off);
+            shrw<NW>(R, 2 * (4 * NDW - (DW_NS - 1) - off - k));
+            EX0 = (EX0 >> off) | (off ? EX1 << (64 - off) : 0ull);
+            EX1 >>= off;
 #pragma unroll
             for (int m = 0; m < DW_NS; ++m) {
                 if ((uint32_t)m >= nv) break;
-                const uint64_t ls = low_shr(S0, S1, 2 * m) & kmask2;
-                const uint64_t fc = low_shr(R0, R1, 2 * (DW_NS - 1 - m)) & kmask2;   // the window's code
-                const uint64_t rc = ~ls & kmask2;                                   // rc(window)'s code
-                const bool ex = ((uint32_t)(EX >> m) & kmask1) != 0;
-                bool mf = plen == 0 || (fc >> tb) == a.pcode;
-                bool mr = plen == 0 || (rc >> tb) == a.pcode;
-                if (ex) {
+                uint64_t fl, fh, sl, sh;
+                extract<NW>(R, 2 * (DW_NS - 1 - m), &fl, &fh);   // the window's code
+                extract<NW>(S, 2 * m, &sl, &sh);
+                fl &= cm_lo;
+                fh &= cm_hi;
+                const uint64_t rl = ~sl & cm_lo, rh = ~sh & cm_hi;          // rc(window)'s code
+                const uint64_t exm = (m ? (EX0 >> m) | (EX1 << (64 - m)) : EX0) & kmask1;
+                bool mf = plen == 0 || top(fl, fh) == a.pcode;
+                bool mr = plen == 0 || top(rl, rh) == a.pcode;
+                if (exm) {
                     if (WRITE && (mf || mr)) {
                         // (non-ACGT bytes alias to a code: the prefix bytes themselves decide)
                         const uint64_t pos = st + w0 + m;
@@ -234,17 +278,22 @@ __global__ __launch_bounds__(256) void dense_windows_kernel(DenseArgs a) {
         }
         // ---- ranks inside each line: segmented wave scans of the lane counts ----
         const uint32_t nf = __popc(fmask), nr = __popc(rmask);
-        const uint32_t F = dw_incl_sum(nf), R = dw_incl_sum(nr);
+        const uint32_t F = dw_incl_sum(nf), Rs = dw_incl_sum(nr);
         // carried counts of line m (seg0 > 0: earlier rounds took its first windows)
         const uint32_t carf = seg0 ? c.cf : 0u, carr = seg0 ? c.cr : 0u;
         // lane i < 16: line i's windows of this round = lanes [b_i, min(cum_i, 64))
         const uint32_t bi_ = cum - need, ei_ = cum < 64 ? cum : 64u;
         const uint32_t Fe = (uint32_t)__shfl((int)F, (int)(ei_ ? ei_ - 1 : 0));
-        const uint32_t Re = (uint32_t)__shfl((int)R, (int)(ei_ ? ei_ - 1 : 0));
+        const uint32_t Re = (uint32_t)__shfl((int)Rs, (int)(ei_ ? ei_ - 1 : 0));
         const uint32_t Fb = (uint32_t)__shfl((int)F, (int)(bi_ ? bi_ - 1 : 0));
-        const uint32_t Rb = (uint32_t)__shfl((int)R, (int)(bi_ ? bi_ - 1 : 0));
+        const uint32_t Rb = (uint32_t)__shfl((int)Rs, (int)(bi_ ? bi_ - 1 : 0));
         const bool took = lane < 16 && need && bi_ < 64;
         const uint32_t sf = took ? Fe - (bi_ ? Fb : 0u) : 0u, sr = took ? Re - (bi_ ? Rb : 0u) : 0u;
+        // this lane's line starts at lane `before`: the scans there, read by
+        // every lane (a bpermute from a lane outside EXEC returns 0, so the
+        // reads must not sit in a branch that disables the source lane)
+        const uint32_t Fbl = (uint32_t)__shfl((int)F, (int)(before ? before - 1 : 0));
+        const uint32_t Rbl = (uint32_t)__shfl((int)Rs, (int)(before ? before - 1 : 0));
         if (!WRITE) {
             // complete lines: their totals (carried + this round); a line still
             // open after the round carries its counts to the next
@@ -257,10 +306,10 @@ __global__ __launch_bounds__(256) void dense_windows_kernel(DenseArgs a) {
             }
         } else if (nv) {
             // this lane's rank base among its line's accepted windows of this round and before
-            const uint32_t Bf = before ? (uint32_t)__shfl((int)F, (int)(before - 1)) : 0u;
-            const uint32_t Br = before ? (uint32_t)__shfl((int)R, (int)(before - 1)) : 0u;
+            const uint32_t Bf = before ? Fbl : 0u;
+            const uint32_t Br = before ? Rbl : 0u;
             const uint32_t fb = F - nf - Bf + (li == 0 ? carf : 0u);
-            const uint32_t rb = R - nr - Br + (li == 0 ? carr : 0u);
+            const uint32_t rb = Rs - nr - Br + (li == 0 ? carr : 0u);
             const uint32_t LF = (uint32_t)lcnt, LR = (uint32_t)(lcnt >> 32);
             const uint64_t hb = a.out_base + lbase;
             const uint64_t lo = lix << (a.pbits + 1);
@@ -270,17 +319,30 @@ __global__ __launch_bounds__(256) void dense_windows_kernel(DenseArgs a) {
                 const uint64_t s = w0 + m;
                 // (the codes again from the streams: constant shifts, no per-window key registers)
                 if (fmask & (1u << m)) {
-                    const uint64_t key = low_shr(R0, R1, 2 * (DW_NS - 1 - m)) & a.smask;
+                    uint64_t kl, kh;
+                    extract<NW>(R, 2 * (DW_NS - 1 - m), &kl, &kh);
                     const uint64_t slot = hb + fb + __popc(fmask & below);
-                    if (a.rkey32) a.rkey32[slot] = (uint32_t)key;
-                    else a.rkey[slot] = key;
+                    if (slot >= a.out_end) {             // (never: the count pass sized the arrays)
+                        dw_refuse(a, c.m + lsrc, s, 0, lcnt, fb + __popc(fmask & below), slot);
+                        continue;
+                    }
+                    if (a.rkey32) a.rkey32[slot] = (uint32_t)(kl & a.smask);
+                    else a.rkey[slot] = kl & a.smask;
+                    if (WIDE && a.rkeyh) a.rkeyh[slot] = kh & a.smask_hi;
                     a.rord[slot] = lo | s;
                 }
                 if (rmask & (1u << m)) {
-                    const uint64_t key = ~low_shr(S0, S1, 2 * m) & a.smask;
-                    const uint64_t slot = hb + LF + (LR - 1u - (rb + __popc(rmask & below)));
-                    if (a.rkey32) a.rkey32[slot] = (uint32_t)key;
-                    else a.rkey[slot] = key;
+                    uint64_t kl, kh;
+                    extract<NW>(S, 2 * m, &kl, &kh);
+                    const uint32_t rr = rb + __popc(rmask & below);
+                    const uint64_t slot = hb + LF + (LR - 1u - rr);
+                    if (rr >= LR || slot >= a.out_end) {
+                        dw_refuse(a, c.m + lsrc, s, 1, lcnt, rr, slot);
+                        continue;
+                    }
+                    if (a.rkey32) a.rkey32[slot] = (uint32_t)(~kl & a.smask);
+                    else a.rkey[slot] = ~kl & a.smask;
+                    if (WIDE && a.rkeyh) a.rkeyh[slot] = ~kh & a.smask_hi;
                     a.rord[slot] = lo | (1ull << a.pbits) | (maxrel - s);
                 }
             }
@@ -310,8 +372,11 @@ hipError_t launch_dense_windows(const DenseArgs &a, bool write, hipStream_t s) {
     if (!a.n_lines) return hipSuccess;
     const uint64_t waves = (a.n_lines + a.lpw - 1) / a.lpw;
     const uint32_t grid = (uint32_t)((waves + 3) / 4);
-    if (write) hipLaunchKernelGGL(dense_windows_kernel<true>, dim3(grid), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(dense_windows_kernel<false>, dim3(grid), dim3(256), 0, s, a);
+    const bool wide = a.k > 32;
+    if (write && wide) hipLaunchKernelGGL((dense_windows_kernel<true, true>), dim3(grid), dim3(256), 0, s, a);
+    else if (write) hipLaunchKernelGGL((dense_windows_kernel<true, false>), dim3(grid), dim3(256), 0, s, a);
+    else if (wide) hipLaunchKernelGGL((dense_windows_kernel<false, true>), dim3(grid), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((dense_windows_kernel<false, false>), dim3(grid), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -146,6 +146,7 @@ kmer_status check_err(kmer_ctx *c, uint32_t e) {
                     c->pbits == PBITS_DEFAULT ? "sequence line longer than 2^23 bytes (KMER_FLAG_LONG_LINES)"
                                               : "long-line mode: a line longer than 2^40 bytes or more than 2^23 lines");
     if (e & ERR_LOOKBACK_TIMEOUT) return fail(c, KMER_E_DEVICE, "tile look-back timed out");
+    if (e & ERR_DENSE_RANK) return fail(c, KMER_E_DEVICE, "dense-hit path: rank slot past the counted hits");
     return KMER_OK;
 }
 
@@ -699,7 +700,7 @@ kmer_status chunk_lines(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_
     return KMER_OK;
 }
 
-// Dense-hit path, step 1, k <= 32 (kmer_dense.hip): a count pass over the
+// Dense-hit path, step 1, k <= 64 (kmer_dense.hip): a count pass over the
 // lines, a scan of the per-line counts, then the accepted windows written at
 // their rank slots -- the rank arrays hold only accepted windows.
 kmer_status dense_windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint64_t n_seq, uint64_t n_nl,
@@ -717,6 +718,7 @@ kmer_status dense_windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint
     auto code = [](char ch) -> uint64_t { return ch == 'A' ? 0u : ch == 'C' ? 1u : ch == 'G' ? 2u : 3u; };
     for (char ch : c->prefix) g.pcode = (g.pcode << 2) | code(ch);
     g.smask = (c->kbits >= 64) ? ~0ull : ((1ull << c->kbits) - 1ull);
+    g.smask_hi = c->kbits <= 64 ? 0ull : c->kbits >= 128 ? ~0ull : ((1ull << (c->kbits - 64)) - 1ull);
     g.P = c->d_PR + 2 * KMAX_TILE;
     g.RP = c->d_PR + 2 * KMAX_TILE + c->prefix.size();
     g.err = c->d_err;
@@ -749,8 +751,13 @@ kmer_status dense_windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint
     HIPCHK(c, hipEventRecord(c->ev0, s));
     g.hbase = c->wbase.p;
     g.out_base = c->n_hits;
+    g.out_end = c->n_hits + total;
+    HIPCHK(c, c->ddbg.ensure(8, s));
+    HIPCHK(c, hipMemsetAsync(c->ddbg.p, 0, 64, s));
+    g.dbg = (unsigned long long *)c->ddbg.p;
     g.rkey = c->rkey.p;
     g.rkey32 = c->narrow ? c->rkey32.p : nullptr;
+    g.rkeyh = c->wide ? c->rkeyh.p : nullptr;
     g.rord = c->rord.p;
     for (int attempt = 0; attempt < 8; ++attempt) {
         g.recs = c->recs.p;
@@ -762,6 +769,18 @@ kmer_status dense_windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint
         HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
         const uint32_t e = (uint32_t)c->h_small[5];
+        if (e & ERR_DENSE_RANK) {                   // (a defect, reported with its context)
+            uint64_t d[8];
+            HIPCHK(c, hipMemcpy(d, c->ddbg.p, 64, hipMemcpyDeviceToHost));
+            char msg[256];
+            snprintf(msg, sizeof(msg),
+                     "dense-hit path: rank slot past the counted hits (line %llu s %llu strand %llu counts %llx "
+                     "rank %llu slot %llu end %llu, lines %llu lpw %llu)",
+                     (unsigned long long)d[1], (unsigned long long)d[2], (unsigned long long)d[3],
+                     (unsigned long long)d[4], (unsigned long long)d[5], (unsigned long long)d[6],
+                     (unsigned long long)d[7], (unsigned long long)n_seq, (unsigned long long)g.lpw);
+            return fail(c, KMER_E_DEVICE, msg);
+        }
         st = check_err(c, e);
         if (st) return st;
         float ms = 0.f;
@@ -800,7 +819,8 @@ kmer_status windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n
         const char *e = exp_env("KMERHIP_DENSE");
         return e && strcmp(e, "slots") == 0;
     }();
-    if (c->p.step == 1 && c->p.k <= 32 && !slots_only) return dense_windows_feed(c, d, len, n_seq, n_nl, li0, s);
+    if (c->p.step == 1 && (c->p.k > (uint32_t)KMAX_DENSE || !slots_only))
+        return dense_windows_feed(c, d, len, n_seq, n_nl, li0, s);
     c->win_slots = true;                          // (the finish compacts the rejected windows' slots away)
     uint64_t total = 0;
     if (n_seq) {
@@ -981,6 +1001,7 @@ kmer_status reset(kmer_ctx *c) {
     c->t_fill = 0;
     c->win_slots = false;
     c->t_p1_fixed = c->t_p1_merged = c->t_p1_counted = 0;
+    c->t_p2_fixed = 0;
     c->gm_n = 0;
     c->gm_last = 0;
     c->gm_merged = true;

@@ -116,7 +116,7 @@ kmer_status group_count(kmer_ctx *g, GroupSrc &src, kmer_result **out) {
     kmer_ctx *c0 = g->group[0];
     const int mode = c0->mode;
     // (keys of >= 64 bits have no packed partials: devices[0] counts alone)
-    const bool ordered = (mode == MODE_PACKED && !c0->wide) || mode == MODE_WINDOWS;
+    const bool ordered = (mode == MODE_PACKED || mode == MODE_WINDOWS) && !c0->wide;
     const size_t W = (ordered || mode == MODE_TABLE) ? N : 1;    // children that take batches
     g->t_done = false;
     // -- the batch stream, dealt round robin over W worker threads

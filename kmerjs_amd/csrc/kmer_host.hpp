@@ -145,6 +145,7 @@ struct kmer_ctx {
     DBuf<uint64_t> wcount, wbase;  // dense-hit path: windows / first rank per sequence line
     DBuf<uint64_t> dcnt;           // dense-hit path (kmer_dense.hip): accepted forward | reverse << 32 per line
     DBuf<uint32_t> dtot;           // ... their sum per line (scanned into wbase)
+    DBuf<uint64_t> ddbg;           // ... a refused rank slot's context (diagnostics)
     bool win_slots = false;        // a chunk of this session ranked every window (the finish compacts)
     DBuf<uint32_t> tcount;         // dense-hit path: '\n' per tile
     DBuf<uint64_t> tbase, nlpos;   // ... exclusive scan, chunk-relative '\n' positions (or sequence-line bounds)
@@ -253,7 +254,8 @@ struct kmer_ctx {
     DBuf<SeqLine> tpieces;         // long lines cut into pieces of <= TAB_PIECE windows
     DBuf<unsigned long long> tstats;   // [0..2] final statistics, [3] big-list count, [4] digest
     uint64_t t_keys = 0;           // pass-1 slots of the session (keys, plus filler of fixed runs)
-    uint64_t t_p1_fixed = 0, t_p1_merged = 0, t_p1_counted = 0;   // pass-1 routes (kmer_table_pass1_routes)
+    uint64_t t_p1_fixed = 0, t_p1_merged = 0, t_p1_counted = 0;   // pass-1 routes (kmer_table_routes)
+    uint64_t t_p2_fixed = 0;       // finishes whose pass 2 ran with fixed bucket capacities (tab_scatter2f)
     uint64_t t_fill = 0;           // ... of which filler slots (an estimate: windows with non-ACGT bytes are not keys)
     std::vector<uint64_t> t_cbase; // per chunk: first key in tb1
     std::vector<std::vector<uint64_t>> t_coff;   // per chunk: TAB_NB + 1 partition starts (chunk-relative)

@@ -62,6 +62,8 @@ enum : uint32_t {
     ERR_COUNT_OVERFLOW = 1u << 7,    // table mode: one key counted 2^32 times in one bucket
     ERR_BIG_OVERFLOW = 1u << 8,      // table mode: big-count list full
     ERR_TAB_SPLIT = 1u << 9,         // table mode: bucket range could not be split further
+    ERR_DENSE_RANK = 1u << 10,       // dense-hit path: a rank slot past the counted hits (count / write disagree)
+    ERR_TAB_CAP = 1u << 11,          // table mode: a bucket past its fixed pass-2 capacity (counted route redoes it)
     // not an error: a tile without '\n' had hits, or a tile overflowed its hit
     // slots -- cross segments may be long (finish sorts the whole cross list)
     INFO_LONGSEG = 1u << 16,
@@ -340,7 +342,7 @@ struct WinArgs {
     unsigned int *err;
 };
 
-// dense-hit path, step 1, k <= 32 (kmer_dense.hip): only accepted windows,
+// dense-hit path, step 1, k <= 64 (kmer_dense.hip): only accepted windows,
 // ranked by two passes over the lines
 struct DenseArgs {
     const uint8_t *data;
@@ -351,13 +353,16 @@ struct DenseArgs {
     uint32_t k, plen;
     uint32_t pbits;                // order-key position bits (PBITS_*)
     uint64_t pcode;                // P as 2-bit codes (first base most significant)
-    uint64_t smask;                // the key: the low 2 (k - |P|) bits of the window code
+    uint64_t smask, smask_hi;      // the key: the low 2 (k - |P|) bits of the window code (hi: above bit 64)
     uint64_t *cnt;                 // count pass: per line accepted forward | reverse << 32
     uint32_t *tot;                 // count pass: per line forward + reverse
     const uint64_t *hbase;         // write pass: per line first slot (chunk-relative, exclusive scan of tot)
     uint64_t out_base;
+    uint64_t out_end;              // write pass: out_base + the counted hits (slots past it are refused)
+    unsigned long long *dbg;       // write pass: the first refused slot's context (8 words, [0] = taken)
     uint32_t *rkey32;              // narrow keys (2 (k - |P|) <= 31 bits), else rkey
     uint64_t *rkey;
+    uint64_t *rkeyh;               // wide keys (2 (k - |P|) >= 64 bits): the bits above 64
     uint64_t *rord;
     const uint8_t *P, *RP;         // device: P and rc(P) (exotic windows' prefix bytes)
     Record *recs;
@@ -566,6 +571,11 @@ struct TabFinal {
     // [qlo, qhi) when `left` is set
     uint32_t *left;
     unsigned int *left_n;
+    // fixed-capacity pass 2 (tab_scatter2f): bucket q's keys are B2[q capq ..
+    // q capq + inlen[q]) and `start` is the compact OUTPUT layout (the scan
+    // of inlen); no bucket groups.  capq 0: contiguous buckets, start for both.
+    uint64_t capq;
+    const uint32_t *inlen;
 };
 
 constexpr uint64_t TAB_PIECE = 4096;                   // windows per piece of a long line (pass 1)
@@ -580,6 +590,13 @@ hipError_t launch_tab_scatter2(const uint64_t *B1, const TabUnit *units, uint32_
                                uint64_t *B2, hipStream_t s);
 hipError_t launch_tab_starts(const uint64_t *H2s, const uint32_t *H2, uint64_t nh, const TabUnit *pfirst,
                              uint64_t *start, hipStream_t s);
+// pass 2 without its histogram: one workgroup per partition p in [p0, p0 +
+// np), bucket q's keys at B2[q cap ..) (capacity cap, a multiple of 8);
+// blen[q] = its keys; a bucket past its capacity sets ERR_TAB_CAP (the caller
+// redoes pass 2 with the counted route)
+hipError_t launch_tab_scatter2f(const uint64_t *B1, const TabUnit *units, const uint32_t *ufirst, uint32_t p0,
+                                uint32_t np, uint64_t cap, uint64_t *B2, uint32_t *blen, unsigned int *err,
+                                hipStream_t s);
 hipError_t launch_tab_scatter1f(const TabArgs &a, hipStream_t s);
 hipError_t launch_tab_wg_windows(const SeqLine *lines, uint64_t n, uint64_t lpw, uint32_t k, uint32_t nwg,
                                  uint64_t *W, hipStream_t s);

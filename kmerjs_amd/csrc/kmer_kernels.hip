@@ -2912,7 +2912,8 @@ __global__ __launch_bounds__(256) void bucket_scatter_kernel(const uint32_t *key
         const uint32_t k = skey[e], b = k >> shift;
         const uint32_t pos = cnt[b] + e;
 #if BKT_PROBE_DELAY
-        if (b >= nb || pos >= n) continue;          // (the probe keeps a raced store in range)
+        // (the probe keeps a raced store, and the ranks later kernels index by, in range)
+        if (b >= nb || pos >= n || srank[e] >= n) continue;
 #endif
         pkey[pos] = (uint16_t)(k & lo_mask);
         prank[pos] = srank[e];
@@ -2930,10 +2931,24 @@ __global__ __launch_bounds__(1024) void bucket_heads_kernel(const uint16_t *pkey
     }
     __syncthreads();
     const uint32_t lo = bbase[b], hi = bbase[b + 1];
-    for (uint32_t e = lo + threadIdx.x; e < hi; e += blockDim.x) {
-        const uint32_t j = pkey[e], r = prank[e];
-        atomicMin(&minr[j], r);
-        atomicAdd(&cnt[j], 1u);
+    // 16 keys per thread loaded before any is used: one memory round trip per
+    // 16 K keys, not one per 1 K (the loop waited on every load, ~10 per bucket)
+    constexpr uint32_t U = 16;
+    for (uint32_t e0 = lo; e0 < hi; e0 += U * 1024) {
+        uint32_t j[U], r[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            const uint32_t e = e0 + u * 1024 + threadIdx.x;
+            j[u] = e < hi ? pkey[e] : 0u;
+            r[u] = e < hi ? prank[e] : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            if (e0 + u * 1024 + threadIdx.x < hi) {
+                atomicMin(&minr[j[u]], r[u]);
+                atomicAdd(&cnt[j[u]], 1u);
+            }
+        }
     }
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < nk; j += blockDim.x) {
@@ -2990,6 +3005,26 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
         hm[i] = __ballot(hcr[i] != 0);
         if (lane == 0) s_w[i][wid] = (uint32_t)__popcll(hm[i]);
     }
+    // every head's key, count and first occurrence loaded now, all rounds'
+    // loads in flight together (the rounds' stores would otherwise order them)
+    uint64_t ekey[NR], ecnt[NR], efirst[NR], ekeyh[NR];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) {
+        const uint64_t r = rb + 256 * i + tid;
+        ekey[i] = ecnt[i] = efirst[i] = ekeyh[i] = 0;
+        if (hcr[i]) {
+            if (a.hrec) {
+                const HeadRec v = a.hrec[r];
+                ekey[i] = v.key;
+                ecnt[i] = v.count;
+            } else {
+                ekey[i] = a.rkey32 ? (uint64_t)a.rkey32[r] : a.rkey64[r];
+                if (a.rkeyh) ekeyh[i] = a.rkeyh[r];
+                ecnt[i] = hcr[i];
+            }
+            efirst[i] = a.rord[r];
+        }
+    }
     if (a.epre) {                                // scanned workgroup prefixes
         if (tid == 0) s_pre = a.epre[blockIdx.x];
     } else {                                     // few workgroups: sum the earlier ones' counts
@@ -3026,17 +3061,7 @@ __global__ __launch_bounds__(256) void emit_kernel(EmitArgs a) {
         }
         const uint64_t o = o64;
         if (f) {
-            uint64_t key, cnt, keyh = 0;
-            if (a.hrec) {
-                const HeadRec v = a.hrec[r];
-                key = v.key;
-                cnt = v.count;
-            } else {
-                key = a.rkey32 ? (uint64_t)a.rkey32[r] : a.rkey64[r];
-                if (a.rkeyh) keyh = a.rkeyh[r];
-                cnt = hc;
-            }
-            const uint64_t first = a.rord[r];
+            const uint64_t key = ekey[i], cnt = ecnt[i], keyh = ekeyh[i], first = efirst[i];
             if (a.partial) {
                 a.ukey[o] = key;
                 Agg v;

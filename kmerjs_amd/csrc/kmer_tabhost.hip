@@ -291,6 +291,7 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
     c->t_ent = const_cast<uint64_t *>(B1);
     std::vector<TabUnit> units;
     std::vector<TabUnit> heads(TAB_NB);
+    std::vector<uint32_t> ufirst(TAB_NB);
     uint64_t ubase = 0;
     // a partition's run in a chunk is cut into ceil(len / cap) units of equal
     // length (KMERHIP_TAB_UNIT: the cap, A/B experiments)
@@ -317,6 +318,7 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
             units[i].hbase = ubase * TAB_NB;
         }
         heads[p] = units[first];
+        ufirst[p] = (uint32_t)first;
         ubase += nun;
     }
     const uint64_t n_units = units.size();
@@ -328,24 +330,65 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
     const uint64_t nh = n_units * TAB_NB;
     HIPCHK(c, c->tH.ensure(nh, s));
     HIPCHK(c, c->tHs.ensure(nh, s));
-    HIPCHK(c, c->tb2.ensure(n, s));
     HIPCHK(c, c->tstart.ensure(TAB_NQ + 1, s));
     HIPCHK(c, c->tnd.ensure(TAB_NQ, s));
     HIPCHK(c, c->tbig.ensure(1 << 16, s));
     HIPCHK(c, c->tstats.ensure(5, s));
-    HIPCHK(c, hipEventRecord(c->tev[4], s));
-    HIPCHK(c, launch_tab_hist2(B1, c->tunits.p, (uint32_t)n_units, c->tH.p, s));
-    ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tH.p, c->tHs.p, (uint64_t)0, (size_t)nh,
-                                           rocprim::plus<uint64_t>(), s));
-    HIPCHK(c, hipEventRecord(c->tev[5], s));
-    HIPCHK(c, launch_tab_scatter2(B1, c->tunits.p, (uint32_t)n_units, c->tHs.p, c->tb2.p, s));
-    HIPCHK(c, hipEventRecord(c->tev[6], s));
-    HIPCHK(c, launch_tab_starts(c->tHs.p, c->tH.p, nh, c->tunits.p + n_units, c->tstart.p, s));
+    // Pass 2 with fixed bucket capacities (tab_scatter2f, no histogram pass)
+    // when buckets are large -- a count near its mean: mean + 6 sigma + 16
+    // slots -- else (small buckets, C5: ~480 keys, where the slack would be
+    // large) or after a capacity overflow, the counted route: tab_hist2, a
+    // scan, tab_scatter2c, bucket starts.  (KMERHIP_TAB_P2=count: always
+    // counted, A/B experiments.)
+    const uint64_t n_est = n - std::min(n, c->t_fill);             // keys (filler slots excluded; an upper bound)
+    const double mu = (double)n_est / TAB_NQ;
+    const char *p2 = exp_env("KMERHIP_TAB_P2");
+    uint64_t capq = 0;
+    if (mu >= 2048.0 && !(c->p.flags & KMER_FLAG_TABLE_SPLIT_TEST) && !(p2 && strcmp(p2, "count") == 0) &&
+        (qlo & (TAB_NB - 1)) == 0 && (qhi & (TAB_NB - 1)) == 0) {
+        capq = ((uint64_t)(mu + 6.0 * std::sqrt(mu)) + 16 + 7) & ~7ull;
+        HIPCHK(c, c->tb2.ensure((uint64_t)TAB_NQ * capq, s));
+        HIPCHK(c, c->tH.ensure((uint64_t)TAB_NQ + 1, s));
+        HIPCHK(c, c->tHs.ensure(TAB_NB, s));
+        st = upload(c, c->tHs.p, ufirst.data(), TAB_NB * sizeof(uint32_t), s);
+        if (st) return st;
+        uint32_t *blen = c->tH.p;
+        HIPCHK(c, hipMemsetAsync(blen, 0, ((uint64_t)TAB_NQ + 1) * sizeof(uint32_t), s));
+        HIPCHK(c, hipEventRecord(c->tev[4], s));
+        HIPCHK(c, hipEventRecord(c->tev[5], s));
+        HIPCHK(c, launch_tab_scatter2f(B1, c->tunits.p, (const uint32_t *)c->tHs.p, qlo >> TAB_L2,
+                                       (qhi - qlo) >> TAB_L2, capq, c->tb2.p, blen, c->d_err, s));
+        HIPCHK(c, hipEventRecord(c->tev[6], s));
+        HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        if ((uint32_t)c->h_small[5] & ERR_TAB_CAP) {   // (a crowded bucket: the counted route)
+            HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)c->d_err, (int)((uint32_t)c->h_small[5] & ~ERR_TAB_CAP), 1, s));
+            capq = 0;
+        } else {
+            // entries go out compactly: start = the scan of the buckets' key counts
+            ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, blen, c->tstart.p, (uint64_t)0, (size_t)TAB_NQ + 1,
+                                                   rocprim::plus<uint64_t>(), s));
+            c->t_p2_fixed += 1;
+        }
+    }
+    if (!capq) {
+        HIPCHK(c, c->tb2.ensure(n, s));
+        HIPCHK(c, hipEventRecord(c->tev[4], s));
+        HIPCHK(c, launch_tab_hist2(B1, c->tunits.p, (uint32_t)n_units, c->tH.p, s));
+        ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tH.p, c->tHs.p, (uint64_t)0, (size_t)nh,
+                                               rocprim::plus<uint64_t>(), s));
+        HIPCHK(c, hipEventRecord(c->tev[5], s));
+        HIPCHK(c, launch_tab_scatter2(B1, c->tunits.p, (uint32_t)n_units, c->tHs.p, c->tb2.p, s));
+        HIPCHK(c, hipEventRecord(c->tev[6], s));
+        HIPCHK(c, launch_tab_starts(c->tHs.p, c->tH.p, nh, c->tunits.p + n_units, c->tstart.p, s));
+    }
     HIPCHK(c, hipMemsetAsync(c->tstats.p, 0, 4 * sizeof(unsigned long long), s));
     TabFinal f;
     memset(&f, 0, sizeof(f));
     f.B2 = c->tb2.p;
     f.start = c->tstart.p;
+    f.capq = capq;
+    f.inlen = capq ? c->tH.p : nullptr;
     f.out = c->t_ent;
     f.nd = c->tnd.p;
     const uint64_t mean = (n - std::min(n, c->t_fill)) / TAB_NQ;   // (keys, not filler slots)

@@ -733,6 +733,112 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2c_kernel(const uint64_t *
     }
 }
 
+// pass 2 without the histogram pass (tab_hist2): when a bucket holds many
+// keys (C3: ~11.4 K) its count is close to its mean, so bucket q gets a FIXED
+// capacity region B2[q cap, (q + 1) cap) (mean + 6 sigma + 16, rounded to 8:
+// one bucket in ~10^9 overflows, and then ERR_TAB_CAP sends the finish back
+// to the counted route).  One workgroup per pass-1 partition walks the
+// partition's units in order with scatter2c's rounds (LDS sort, aligned
+// write-out, the carry in the bucket owner's registers across rounds AND
+// units); the regions start on 64-B boundaries, so every block but the
+// bucket's last is written whole.  blen[q] = the bucket's keys.  The unused
+// tail of a region is never written nor read: the final takes (q cap,
+// blen[q]) and writes its entries compactly (start = the scan of blen).
+__global__ __launch_bounds__(TAB_WG1) void tab_scatter2f_kernel(const uint64_t *B1, const TabUnit *units,
+                                                                const uint32_t *ufirst, uint32_t p0, uint64_t cap,
+                                                                uint64_t *B2, uint32_t *blen, unsigned int *err) {
+    __shared__ uint64_t srt[TS2_ROUND + TS2_CARRY * TAB_WG1];
+    __shared__ uint64_t cur[TAB_NB];
+    __shared__ uint32_t bcnt[TAB_NB], bst[TAB_NB];
+    __shared__ uint32_t ws[16];
+    __shared__ uint32_t sovf;
+    const uint32_t t = threadIdx.x, p = p0 + blockIdx.x;
+    const uint64_t q = ((uint64_t)p << TAB_L2) | t;
+    const uint64_t pbase = ((uint64_t)p << TAB_L2) * cap;   // (region of bucket (p, b): pbase + b cap)
+    uint64_t dest = q * cap;                       // next B2 slot of bucket t
+    const uint64_t cend = dest + cap;
+    bcnt[t] = 0;
+    if (t == 0) sovf = 0;
+    uint32_t cc = 0;                               // carried keys of bucket t
+    uint64_t ck[TS2_CARRY];
+#pragma unroll
+    for (int i = 0; i < TS2_CARRY; ++i) ck[i] = 0;
+    __syncthreads();
+    const uint32_t u0 = ufirst[p], nun = units[u0].nunits;
+    for (uint32_t ui = 0; ui < nun; ++ui) {
+        const TabUnit un = units[u0 + ui];
+        const uint64_t *src = B1 + un.start;
+        uint64_t key[TS2_RPL];
+#pragma unroll
+        for (int j = 0; j < TS2_RPL; ++j) {
+            const uint32_t i = j * TAB_WG1 + t;
+            key[j] = i < un.len ? src[i] : 0;
+        }
+        for (uint32_t r0 = 0; r0 < un.len; r0 += TS2_ROUND) {
+            const bool last = ui + 1 == nun && r0 + TS2_ROUND >= un.len;
+            uint32_t rank[TS2_RPL];
+#pragma unroll
+            for (int j = 0; j < TS2_RPL; ++j) {
+                const uint32_t i = r0 + j * TAB_WG1 + t;
+                rank[j] = i < un.len && key[j] != TAB_SENT
+                              ? atomicAdd(&bcnt[(uint32_t)(key[j] >> TAB_RBITS) & (TAB_NB - 1)], 1u) : 0u;
+            }
+            __syncthreads();
+            const uint32_t n_new = bcnt[t], tot = n_new + cc;
+            uint32_t total;
+            const uint32_t my_st = block_excl_1024(tot, ws, &total);
+            const uint64_t aend = last ? dest + tot : ((dest + tot) & ~7ull);
+            const uint32_t full = aend > dest ? (uint32_t)(aend - dest) : 0u;
+            bst[t] = my_st;
+            cur[t] = dest - my_st;
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < TS2_RPL; ++j) {
+                const uint32_t i = r0 + j * TAB_WG1 + t;
+                if (i < un.len && key[j] != TAB_SENT)
+                    srt[bst[(uint32_t)(key[j] >> TAB_RBITS) & (TAB_NB - 1)] + rank[j]] = key[j];
+            }
+#pragma unroll
+            for (int i = 0; i < TS2_CARRY; ++i)
+                if ((uint32_t)i < cc) srt[my_st + n_new + i] = ck[i];
+            bcnt[t] = my_st + full;
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < TS2_RPL; ++j) {
+                const uint32_t i = r0 + TS2_ROUND + j * TAB_WG1 + t;
+                key[j] = i < un.len ? src[i] : 0;
+            }
+            for (uint32_t i = t; i < total; i += TAB_WG1) {
+                const uint64_t h = srt[i];
+                const uint32_t b = (uint32_t)(h >> TAB_RBITS) & (TAB_NB - 1);
+                if (i < bcnt[b]) {
+                    const uint64_t pos = cur[b] + i;
+                    if (pos < pbase + (uint64_t)(b + 1) * cap) B2[pos] = h;
+                    else sovf = 1;                   // (benign race: any writer sets it)
+                }
+            }
+            cc = tot - full;
+#pragma unroll
+            for (int i = 0; i < TS2_CARRY; ++i)
+                if ((uint32_t)i < cc) ck[i] = srt[my_st + full + i];
+            dest += full;
+            __syncthreads();
+            bcnt[t] = 0;
+            __syncthreads();
+        }
+    }
+    blen[q] = (uint32_t)((dest < cend ? dest : cend) - q * cap);
+    if (t == 0 && sovf) atomicOr(err, ERR_TAB_CAP);
+}
+
+hipError_t launch_tab_scatter2f(const uint64_t *B1, const TabUnit *units, const uint32_t *ufirst, uint32_t p0,
+                                uint32_t np, uint64_t cap, uint64_t *B2, uint32_t *blen, unsigned int *err,
+                                hipStream_t s) {
+    if (np) hipLaunchKernelGGL(tab_scatter2f_kernel, dim3(np), dim3(TAB_WG1), 0, s, B1, units, ufirst, p0, cap, B2,
+                               blen, err);
+    return hipGetLastError();
+}
+
 // bucket q = (p, b) starts at the scanned H2 entry of (p, b, unit 0)
 // (the end: the keys counted by pass 2 -- B1 may hold TAB_SENT slots)
 __global__ __launch_bounds__(256) void tab_starts_kernel(const uint64_t *H2s, const uint32_t *H2, uint64_t nh,
@@ -943,8 +1049,15 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
     // (groups for the sort path fill the registers; the hash path's ranges
     // split a group whose distinct keys overflow the table)
     const uint64_t gk = !(KH_ABLATE(a) & 4) ? (uint64_t)TAB_REG_MAX : rk;
+    // (fixed-capacity buckets, capq: one bucket per unit, keys at B2[q capq ..
+    // q capq + inlen[q]), entries out at start[q])
+    auto unit_n = [&](uint32_t u, uint32_t e) -> uint64_t {
+        return a.capq ? (uint64_t)a.inlen[u] : sc[e - cbase] - sc[u - cbase];
+    };
+    auto unit_in = [&](uint32_t u) -> uint64_t { return a.capq ? (uint64_t)u * a.capq : sc[u - cbase]; };
     auto unit_end = [&](uint32_t u) -> uint32_t {
         uint32_t e = u + 1;
+        if (a.capq) return e;
         uint64_t tot = sc[u + 1 - cbase] - sc[u - cbase];
         if (tot > gk) return e;
         while (e < q1 && e - cbase < TAB_SC && e - u < TAB_GMAX) {
@@ -973,19 +1086,19 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
     cbase = q0;
     refill(cbase);
     uint32_t q = q0, qe = q0 < q1 ? unit_end(q0) : q0;
-    if (q0 < q1) load_keys(sc[0], sc[qe - cbase] - sc[0]);
+    if (q0 < q1) load_keys(unit_in(q0), unit_n(q0, qe));
     while (q < q1) {
         if (q - cbase >= TAB_SC) {
             cbase = q;
             refill(cbase);
         }
         const uint32_t g = qe - q;                        // buckets in the unit
-        const uint64_t s0 = sc[q - cbase], n = sc[qe - cbase] - s0;
+        const uint64_t s0 = sc[q - cbase], n = unit_n(q, qe), s0in = unit_in(q);   // (s0: output start)
         const uint64_t qbase = (uint64_t)q << TAB_RBITS;
         // the next unit (its keys are loaded while this one is emitted)
         const uint32_t qn = qe, qne = qn < q1 ? unit_end(qn) : qn;
         const bool more = qn < q1;
-        const uint64_t s0n = more ? sc[qn - cbase] : 0, nn = more ? sc[qne - cbase] - s0n : 0;
+        const uint64_t s0n = more ? unit_in(qn) : 0, nn = more ? unit_n(qn, qne) : 0;
         const bool inreg = n <= TAB_REG_MAX;
         if (n == 0) {
             for (uint32_t i = t; i < g; i += TAB_FWG) a.nd[q + i] = 0;
@@ -1156,7 +1269,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
                 for (int d = 32; d >= 1; d >>= 1) cl += __shfl_xor(cl, d);
                 if (lane == 0 && cl) atomicAdd(&occ, cl);
             } else {
-                const uint64_t *src = a.B2 + s0;
+                const uint64_t *src = a.B2 + s0in;
                 for (uint64_t i = t; i < n; i += TAB_FWG) {
                     if (lds_flag(&ovf)) break;
                     uint64_t r1[1] = {src[i] - qbase};
@@ -1358,8 +1471,8 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
         }
         // the unit at q (uniform: every thread reads the same cached starts)
         uint32_t qe = q + 1;
-        uint64_t n = sc[q + 1 - cbase] - sc[q - cbase];
-        if (n <= TS_CAPG) {
+        uint64_t n = a.capq ? (uint64_t)a.inlen[q] : sc[q + 1 - cbase] - sc[q - cbase];
+        if (n <= TS_CAPG && !a.capq) {               // (fixed-capacity buckets: one per unit)
             while (qe < q1 && qe - cbase < TS_SC && qe - q < TS_GMAX) {
                 const uint64_t ne = sc[qe + 1 - cbase] - sc[qe - cbase];
                 if (n + ne > TS_CAPG) break;
@@ -1368,7 +1481,8 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
             }
         }
         const uint32_t g = qe - q;
-        const uint64_t s0 = sc[q - cbase];
+        const uint64_t s0 = sc[q - cbase];             // output (and, capq 0, input) start
+        const uint64_t s0in = a.capq ? (uint64_t)q * a.capq : s0;
         if (n == 0) {
             for (uint32_t i = t; i < g; i += TAB_SWG) a.nd[q + i] = 0;
             q = qe;
@@ -1391,7 +1505,7 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
             const uint32_t bsh = TAB_RBITS + (ONE ? 0 : 32 - __clz(g - 1)) - TS_NBB;
             uint32_t lo[KPT], hi[ONE ? 1 : KPT], pk[KPT];
             {
-                const uint64_t *src = a.B2 + s0;
+                const uint64_t *src = a.B2 + s0in;
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
                     const uint64_t x = src[left > j * (int)TAB_SWG ? j * TAB_SWG + t : 0u] - qbase;

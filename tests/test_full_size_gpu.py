@@ -112,6 +112,7 @@ def test_c3_full_size_properties(native):
         assert ctr.lines() == 4 * n
         canon, keys, total = ctr.table_stats()
         d = ctr.table_digest()
+        assert ctr.table_routes()["p2_fixed"] == 1          # (pass 2 without its histogram pass)
         assert total == 2 * 120 * n == 24_000_000_000
         assert keys == 2 * canon
         # the oracle's table digest of the same 100 M reads (a streamed sum
@@ -260,7 +261,7 @@ def test_c5_full_size_pins(native, fasta):
     fasta60: 60-column records joined (KMER_FLAG_FASTA, an extension).  The
     table digest and Σ counts equal the oracle's streamed over the same bytes
     (tests/golden/fullsize.json "c5" / "c5fa"), on the route the bench takes
-    (pass 1's workgroup shares merged: kmer_table_pass1_routes) and with that
+    (pass 1's workgroup shares merged: kmer_table_routes) and with that
     merging disabled (KMER_FLAG_TABLE_FIXED_TEST)."""
     import torch
     from bench import make_contigs
@@ -282,7 +283,7 @@ def test_c5_full_size_pins(native, fasta):
                 canon, keys, total = ctr.table_stats()
                 assert total == gold["forward_windows"] and keys == canon
                 assert ctr.table_digest() == gold["table_digest"]
-                routes = ctr.table_pass1_routes()
+                routes = ctr.table_routes()
                 seen.append(routes)
                 assert routes["fixed"] >= 1
                 if flags & native.FLAG_TABLE_FIXED_TEST:

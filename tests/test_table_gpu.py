@@ -510,3 +510,39 @@ def test_table_exchange_matches_one_table(native, world, k, flags_name, with_n, 
     for c in ctrs:
         c.close()
     del recvs
+
+
+def test_table_fixed_pass2_vs_oracle(native):
+    """Pass 2 without its histogram pass (tab_scatter2f, kmer_table_routes
+    p2_fixed): at 20 M reads and k = 31 the buckets average 2,289 keys (>= 2,048),
+    so each gets a fixed capacity region; the table digest and Σ counts equal
+    the oracle's streamed over the same reads (lib/kmers.js:88-100 on both
+    strands).  Then 300 K copies of one read appended: each of its k-mers'
+    buckets far past its capacity -> ERR_TAB_CAP -> the counted route redoes
+    pass 2 (p2_fixed 0), and the digest is the sum of the parts (linearity)."""
+    import torch
+    from oracle import oracle
+    n, k = 20_000_000, 31
+    buf = _device_input(n, seed=13)
+    want_d, want_w = oracle.table_digest_synth(13, 0, n, k, 16)
+    ctr = native.Counter(k=k, prefix=b"", flags=native.FLAG_UNORDERED)
+    try:
+        ctr.reset()
+        ctr.feed_device(buf.data_ptr(), buf.numel())
+        ctr.finish(want_result=False)
+        assert ctr.table_routes()["p2_fixed"] == 1
+        canon, keys, total = ctr.table_stats()
+        assert total == 2 * want_w and ctr.table_digest() == want_d
+        rec = buf[:317].clone()
+        reps = 300_000
+        buf2 = torch.cat([buf, rec.repeat(reps)])
+        del buf
+        ctr.reset()
+        ctr.feed_device(buf2.data_ptr(), buf2.numel())
+        ctr.finish(want_result=False)
+        assert ctr.table_routes()["p2_fixed"] == 0
+        one_d, one_w = oracle.table_digest(bytes(rec.cpu().numpy()), k)
+        assert ctr.table_stats()[2] == 2 * (want_w + reps * one_w)
+        assert ctr.table_digest() == (want_d + reps * one_d) % (1 << 64)
+    finally:
+        ctr.close()
