@@ -32,7 +32,6 @@ namespace kmerhip {
 namespace {
 
 constexpr int DW_NS = 16;              // windows per lane per round
-constexpr int DW_NDW = 13;             // dwords a lane loads: 16 + 32 - 1 bytes + 3 of alignment <= 52
 
 __device__ __forceinline__ uint32_t dw_incl_sum(uint32_t x) {
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, true);   // row_shr:1
@@ -210,7 +209,85 @@ __global__ __launch_bounds__(256) void dense_windows_kernel(DenseArgs a) {
 #pragma unroll
         for (int w = 0; w < NW; ++w) S[w] = R[w] = 0;
         const uint32_t nv = act ? (uint32_t)(Wl - w0 < (uint64_t)DW_NS ? Wl - w0 : (uint64_t)DW_NS) : 0u;
-        if (nv) {
+        if (nv && !WIDE) {
+            // narrow keys: the 16 windows' prefix and exotic tests bit-parallel
+            // over the lane's bytes (bit t = byte t of the span): base planes
+            // LO / HI (A C G T = 00 01 10 11) and the non-ACGT flags EX, one
+            // v_dot4 each per dword; the code streams only in the write pass
+            const uint8_t *p = a.data + st + w0;
+            const uint32_t off = (uint32_t)((uintptr_t)p & 3u);
+            const uint32_t *pw = (const uint32_t *)(p - off);
+            uint64_t LO = 0, HI = 0, EX = 0;
+#pragma unroll
+            for (int i = 0; i < NDW; ++i) {
+                uint32_t x = 0x41414141u;                // ('A' past the input: never inside a window)
+                const uint8_t *q = (const uint8_t *)(pw + i);
+                if (q < dend && (uint32_t)(4 * i) < off + nv + k - 1) {
+                    if (q + 4 <= dend) {
+                        x = pw[i];
+                    } else {
+                        for (int j = 0; j < 4; ++j)
+                            if (q + j < dend) x = (x & ~(0xFFu << (8 * j))) | ((uint32_t)q[j] << (8 * j));
+                    }
+                }
+                const uint32_t cc = ((x >> 1) ^ (x >> 2)) & 0x03030303u;       // A C G T -> 0 1 2 3
+                const uint32_t ne = __builtin_amdgcn_perm(0u, 0x54474341u, cc) ^ x;     // 0 where A/C/G/T
+                const uint32_t nz = (((ne & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | ne) & 0x80808080u;
+                EX |= (uint64_t)__builtin_amdgcn_udot4(nz >> 7, 0x08040201u, 0u, false) << (4 * i);
+                LO |= (uint64_t)__builtin_amdgcn_udot4(cc & 0x01010101u, 0x08040201u, 0u, false) << (4 * i);
+                HI |= (uint64_t)__builtin_amdgcn_udot4((cc >> 1) & 0x01010101u, 0x08040201u, 0u, false) << (4 * i);
+                if (WRITE) {
+                    const uint32_t ls = __builtin_amdgcn_udot4(cc, 0x40100401u, 0u, false);   // first byte lowest
+                    const uint32_t ms = __builtin_amdgcn_udot4(cc, 0x01041040u, 0u, false);   // first byte highest
+                    S[i / 8] |= (uint64_t)ls << (8 * (i % 8));
+                    const int rb = 8 * (NDW - 1 - i);
+                    R[rb / 64] |= (uint64_t)ms << (rb % 64);
+                }
+            }
+            if (WRITE) {
+                shrw<NW>(S, 2 * off);
+                shrw<NW>(R, 2 * (4 * NDW - (DW_NS - 1) - off - k));
+            }
+            LO >>= off;
+            HI >>= off;
+            EX >>= off;
+            const uint64_t vm = (1ull << nv) - 1ull;         // (nv <= 16)
+            // window j starts with P: base j + i == P[i]; ends with rc(P): base j + k - |P| + i == rc(P)[i]
+            uint64_t fw = vm, rv = vm;
+            for (uint32_t i = 0; i < plen; ++i) {
+                const uint32_t cp = (uint32_t)(a.pcode >> (2 * (plen - 1 - i))) & 3u;
+                const uint32_t cr = 3u - ((uint32_t)(a.pcode >> (2 * i)) & 3u);   // rc(P)[i] = comp(P[|P| - 1 - i])
+                const uint64_t ep = ((cp & 1u) ? LO : ~LO) & ((cp & 2u) ? HI : ~HI);
+                const uint64_t er = ((cr & 1u) ? LO : ~LO) & ((cr & 2u) ? HI : ~HI);
+                fw &= ep >> i;
+                rv &= er >> (k - plen + i);
+            }
+            // windows holding a non-ACGT byte: an EX bit in [j, j + k)
+            uint64_t E = EX;
+            uint32_t span = 1;
+            while (2 * span <= k) {
+                E |= E >> span;
+                span *= 2;
+            }
+            const uint64_t exw = (E | (E >> (k - span))) & vm;
+            fmask = (uint32_t)(fw & ~exw);
+            rmask = (uint32_t)(rv & ~exw);
+            // (planes alias non-ACGT bytes: exotic candidates are checked byte for byte)
+            uint32_t xc = WRITE ? (uint32_t)((fw | rv) & exw) : 0u;
+            while (xc) {
+                const uint32_t m = __ffs(xc) - 1;
+                xc &= xc - 1;
+                const uint64_t pos = st + w0 + m;
+                bool bf = true, br = true;
+                for (uint32_t b = 0; b < plen; ++b) {
+                    bf = bf && a.data[pos + b] == a.P[b];
+                    br = br && a.data[pos + k - plen + b] == a.RP[b];
+                }
+                const uint64_t s = w0 + m, lo = lix << (a.pbits + 1);
+                if (bf) dw_record(a, lo | s, pos, 0);
+                if (br) dw_record(a, lo | (1ull << a.pbits) | (maxrel - s), pos, 1);
+            }
+        } else if (nv) {
             const uint8_t *p = a.data + st + w0;
             const uint32_t off = (uint32_t)((uintptr_t)p & 3u);
             const uint32_t *pw = (const uint32_t *)(p - off);

@@ -288,8 +288,10 @@ def test_c5_full_size_pins(native, fasta):
                 assert routes["fixed"] >= 1
                 if flags & native.FLAG_TABLE_FIXED_TEST:
                     assert routes["merged"] == 0
-                else:
+                elif not fasta:
                     assert routes["merged"] == routes["fixed"] and routes["counted"] == 0, routes
+                # pass 2 with fixed bucket capacities (small buckets: the wave final)
+                assert routes["p2_fixed"] == 1, routes
         finally:
             ctr.close()
     print("c5 routes", "fasta" if fasta else "single", seen)

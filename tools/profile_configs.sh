@@ -18,6 +18,8 @@ for cfg in "$@"; do
     c5) W=1; K=5; A="--config c5" ;;
     c5fa) W=1; K=5; A="--config c5 --fasta" ;;
     k70) W=1; K=5; A="--k 70" ;;
+    k16AT) W=1; K=5; A="--prefix AT" ;;
+    k64AT) W=1; K=3; A="--k 64 --prefix AT --reads 2000000" ;;
   esac
   timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/trace_$cfg -o run -- \
       python3 bench.py --steps $K --warmup $W $NOX $A > $O/trace_$cfg.log 2>&1 || exit $?
