@@ -594,9 +594,6 @@ hipError_t launch_tab_starts(const uint64_t *H2s, const uint32_t *H2, uint64_t n
 // np), bucket q's keys at B2[q cap ..) (capacity cap, a multiple of 8);
 // blen[q] = its keys; a bucket past its capacity sets ERR_TAB_CAP (the caller
 // redoes pass 2 with the counted route)
-// final for small fixed-capacity buckets (capq <= 1,280: one wave per bucket)
-hipError_t launch_tab_wave_final(const TabFinal &a, uint32_t grid, hipStream_t s);
-constexpr uint64_t TAB_WAVE_CAP = 1280;
 hipError_t launch_tab_scatter2f(const uint64_t *B1, const TabUnit *units, const uint32_t *ufirst, uint32_t p0,
                                 uint32_t np, uint64_t cap, uint64_t *B2, uint32_t *blen, unsigned int *err,
                                 hipStream_t s);

@@ -343,13 +343,15 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
     const uint64_t n_est = n - std::min(n, c->t_fill);             // keys (filler slots excluded; an upper bound)
     const double mu = (double)n_est / TAB_NQ;
     const char *p2 = exp_env("KMERHIP_TAB_P2");
-    // Two cases take it: large buckets (mean >= 2,048: the sort final's
-    // one-bucket units, C3) and small ones whose region fits one wave's
-    // merge (capacity <= TAB_WAVE_CAP: the wave final, C5); tables of fewer
-    // than 2^24 keys keep the counted route (its regions are cheap anyway).
+    // Large buckets only (mean >= 2,048: the sort final's one-bucket units,
+    // C3): small ones (C5) are read by the final in groups of consecutive
+    // buckets, which needs them contiguous (a wave-per-bucket final over
+    // fixed regions measured slower than hist2 + the grouped final: C5 4.14
+    // vs 3.38 ms final).  KMER_FLAG_TABLE_FIXED_TEST: from any
+    // table size (by default from 2^24 keys).
     const uint64_t cap6 = ((uint64_t)(mu + 6.0 * std::sqrt(mu)) + 16 + 7) & ~7ull;
     uint64_t capq = 0;
-    if ((mu >= 2048.0 || cap6 <= TAB_WAVE_CAP) && (n_est >= (1ull << 24) || (c->p.flags & KMER_FLAG_TABLE_FIXED_TEST)) &&
+    if (mu >= 2048.0 && (n_est >= (1ull << 24) || (c->p.flags & KMER_FLAG_TABLE_FIXED_TEST)) &&
         !(c->p.flags & KMER_FLAG_TABLE_SPLIT_TEST) && !(p2 && strcmp(p2, "count") == 0) &&
         (qlo & (TAB_NB - 1)) == 0 && (qhi & (TAB_NB - 1)) == 0) {
         capq = cap6;
@@ -439,19 +441,15 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
     const char *fk = exp_env("KMERHIP_TAB_FINAL");
     const bool sort_first = !(fk && strcmp(fk, "general") == 0) && !f.prof &&
                             !(c->p.flags & KMER_FLAG_TABLE_SPLIT_TEST);
-    // small fixed-capacity buckets: one wave per bucket (every bucket fits)
-    const bool wave_final = capq && capq <= TAB_WAVE_CAP && !(fk && strcmp(fk, "general") == 0) && !f.prof;
     HIPCHK(c, hipEventRecord(c->tev[2], s));
-    if (wave_final) {
-        HIPCHK(c, launch_tab_wave_final(f, 16 * fgrid, s));
-    } else if (sort_first) {
+    if (sort_first) {
         HIPCHK(c, c->tleft.ensure(2ull * TAB_NQ + 1, s));
         f.left = c->tleft.p + 1;
         f.left_n = c->tleft.p;
         HIPCHK(c, hipMemsetAsync(c->tleft.p, 0, 4, s));
         HIPCHK(c, launch_tab_sort_final(f, 2 * fgrid, s));
     }
-    if (!wave_final) HIPCHK(c, launch_tab_final(f, fgrid, s));
+    HIPCHK(c, launch_tab_final(f, fgrid, s));
     HIPCHK(c, hipEventRecord(c->tev[7], s));
     if (f.prof) {
         HIPCHK(c, hipMemcpyAsync(hprof.data(), f.prof, fgrid * 64ull, hipMemcpyDeviceToHost, s));

@@ -1666,205 +1666,6 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
 }
 
 // ---------------------------------------------------------------------------
-// Wave final: small fixed-capacity buckets (tab_scatter2f with capq <= WF_CAP:
-// C5's ~480 keys per bucket), ONE WAVE PER BUCKET -- no workgroup barriers,
-// no bucket groups.  A wave walks a contiguous range of buckets; bucket q's
-// keys (B2[q capq ..], inlen[q] of them, <= 12 per lane) are loaded while the
-// previous bucket is merged.  Merge: a counting sort of the remainders into
-// 1,024 LDS bins by their top 10 bits (16-bit counts, two per word; the
-// returning atomic is the key's rank in its bin), a wave scan of the bins,
-// the scatter, then every held key scans its bin for copies of itself and the
-// first copy emits (remainder, copies) at out[start[q] + its ballot rank].
-// Statistics as the sort final.  LDS per wave: 2 KiB of bins + 6 or 10 KiB
-// of keys (<= 768 or <= 1,280 keys: 12 or 20 per lane).
-// ---------------------------------------------------------------------------
-namespace {
-constexpr uint32_t WF_NB = 1024;                      // bins
-constexpr uint32_t WF_NBB = 10;                       // log2(WF_NB)
-constexpr uint32_t WF_WPG = 4;                        // waves per workgroup
-
-// LDS written by some lanes and read by others of the same wave: the
-// compiler must neither reorder nor cache across this point
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-}  // namespace
-
-template <uint32_t WF_KPL>                            // keys per lane: buckets of <= 64 WF_KPL keys
-__global__ __launch_bounds__(64 * WF_WPG) void tab_wave_final_kernel(TabFinal a) {
-    constexpr uint32_t WF_CAP = 64 * WF_KPL;
-    __shared__ uint32_t sbin[WF_WPG][WF_NB / 2];      // bin counts, then starts (bin b in half b & 1 of word b >> 1)
-    __shared__ uint64_t skey[WF_WPG][WF_CAP];
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t *const bin = sbin[w];
-    uint64_t *const key = skey[w];
-    const uint32_t k = a.k;
-    const uint32_t kmask = k >= 32 ? ~0u : ((1u << k) - 1u), sh = 32 - k;
-    const bool plain_odd = a.pmask == 0 && !a.canonical && (k & 1u);
-    const bool plain_canon = a.pmask == 0 && a.canonical;
-    uint64_t st_canon = 0, st_keys = 0, st_sum = 0;
-    auto account = [&](uint64_t h, uint64_t cnt) {
-        if (plain_odd) {
-            st_canon += 1;
-            st_keys += 2;
-            st_sum += 2 * cnt;
-            return;
-        }
-        if (plain_canon) {
-            st_canon += 1;
-            st_keys += 1;
-            st_sum += cnt;
-            return;
-        }
-        const uint64_t code = h * a.inv;
-        const uint32_t lo = (uint32_t)code & kmask, hi = (uint32_t)(code >> k) & kmask;
-        const uint32_t rlo2 = __brev(~lo & kmask) >> sh, rhi2 = __brev(~hi & kmask) >> sh;
-        const bool pal = lo == rlo2 && hi == rhi2;
-        st_canon += 1;
-        if (a.canonical) {
-            const uint32_t dif = (lo ^ rlo2) | (hi ^ rhi2);
-            const uint32_t j = dif ? __ffs(dif) - 1 : 0;
-            const uint32_t bw = (((hi >> j) & 1u) << 1) | ((lo >> j) & 1u);
-            const uint32_t br = (((rhi2 >> j) & 1u) << 1) | ((rlo2 >> j) & 1u);
-            const bool wmin = dif == 0 || bw < br;
-            const uint32_t clo = wmin ? lo : rlo2, chi = wmin ? hi : rhi2;
-            const bool cs = (((clo ^ a.plo) | (chi ^ a.phi)) & a.pmask) == 0;
-            st_keys += cs ? 1u : 0u;
-            st_sum += cs ? cnt : 0;
-        } else {
-            const bool fs = (((lo ^ a.plo) | (hi ^ a.phi)) & a.pmask) == 0;
-            const bool rs = !pal && (((rlo2 ^ a.plo) | (rhi2 ^ a.phi)) & a.pmask) == 0;
-            st_keys += (fs ? 1u : 0u) + (rs ? 1u : 0u);
-            st_sum += (fs ? (pal ? 2 * cnt : cnt) : 0) + (rs ? cnt : 0);
-        }
-    };
-    const uint32_t nwv = gridDim.x * WF_WPG, gw = blockIdx.x * WF_WPG + w;
-    const uint32_t per = (a.qhi - a.qlo + nwv - 1) / nwv;
-    const uint32_t q0 = min(a.qlo + gw * per, a.qhi), q1 = min(q0 + per, a.qhi);
-    // bucket q's count and keys into (n, x)
-    // bucket q's region (all capq slots: in bounds, so the loads need not
-    // wait for the bucket's count)
-    const uint32_t capq = (uint32_t)a.capq;
-    auto load = [&](uint32_t q, uint64_t (&x)[WF_KPL]) {
-        const uint64_t *src = a.B2 + (uint64_t)q * capq;
-#pragma unroll
-        for (uint32_t j = 0; j < WF_KPL; ++j) x[j] = j * 64 + lane < capq ? src[j * 64 + lane] : 0ull;
-    };
-    uint64_t x[WF_KPL];
-    if (q0 < q1) load(q0, x);
-    uint32_t mlen = 0;                             // lane i: count of bucket (q & ~63) + i
-    uint64_t mst = 0;                              // ... and its output start
-    for (uint32_t q = q0; q < q1; ++q) {
-        const uint32_t qi = (q - q0) & 63u;
-        if (qi == 0) {                             // the next 64 buckets' counts and starts, one load each
-            const uint32_t ql = q + lane;
-            mlen = ql < q1 ? a.inlen[ql] : 0u;
-            mst = ql < q1 ? a.start[ql] : 0ull;
-        }
-        const uint32_t nc = (uint32_t)__builtin_amdgcn_readlane((int)mlen, (int)qi);   // this bucket's keys
-        const uint64_t ob = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mst, (int)qi) |
-                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mst >> 32), (int)qi) << 32);
-        if (nc == 0) {
-            if (lane == 0) a.nd[q] = 0;
-            if (q + 1 < q1) load(q + 1, x);
-            continue;
-        }
-        const uint64_t qbase = (uint64_t)q << TAB_RBITS;
-        uint32_t pk[WF_KPL];                       // bin << 16 | rank in the bin
-#pragma unroll
-        for (uint32_t i = 0; i < WF_NB / 2 / 64; ++i) bin[i * 64 + lane] = 0;
-        wave_lds_sync();
-#pragma unroll
-        for (uint32_t j = 0; j < WF_KPL; ++j) {
-            x[j] -= qbase;                         // the remainder (44 bits)
-            const uint32_t b = (uint32_t)(x[j] >> (TAB_RBITS - WF_NBB)) & (WF_NB - 1);
-            pk[j] = 0;
-            if (j * 64 + lane < nc)
-                pk[j] = b << 16 | ((__hip_atomic_fetch_add(&bin[b >> 1], 1u << (16 * (b & 1u)), __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_WORKGROUP) >> (16 * (b & 1u))) & 0xFFFFu);
-        }
-        wave_lds_sync();
-        {
-            // bin starts: lane l scans bins 16 l .. 16 l + 15 (words 8 l .. 8 l + 7)
-            uint32_t c8[8], sum = 0;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                c8[i] = bin[8 * lane + i];
-                sum += (c8[i] & 0xFFFFu) + (c8[i] >> 16);
-            }
-            uint32_t incl = sum;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
-                if (lane >= (uint32_t)d) incl += y;
-            }
-            uint32_t run = incl - sum;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const uint32_t lo16 = c8[i] & 0xFFFFu, hi16 = c8[i] >> 16;
-                bin[8 * lane + i] = run | (run + lo16) << 16;
-                run += lo16 + hi16;
-            }
-        }
-        wave_lds_sync();
-        // scatter; pk becomes bin start << 20 | rank << 10 | bin size (each < 1,024)
-#pragma unroll
-        for (uint32_t j = 0; j < WF_KPL; ++j) {
-            const uint32_t b = pk[j] >> 16, r = pk[j] & 0xFFFFu;
-            const uint32_t b0 = (bin[b >> 1] >> (16 * (b & 1u))) & 0xFFFFu;
-            const uint32_t e = b + 1 < WF_NB ? (bin[(b + 1) >> 1] >> (16 * ((b + 1) & 1u))) & 0xFFFFu : nc;
-            const bool valid = j * 64 + lane < nc;
-            if (valid) key[b0 + r] = x[j];
-            pk[j] = valid ? b0 << 20 | r << 10 | (e - b0) : 0u;
-        }
-        wave_lds_sync();
-        // the registers are free: the next bucket's keys load during the merge
-        if (q + 1 < q1) load(q + 1, x);
-        // copies of each key in its bin (the key read back from LDS); the
-        // first copy (lowest rank in the bin) emits (remainder, copies)
-        uint32_t o = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < WF_KPL; ++j) {
-            const bool valid = j * 64 + lane < nc;
-            const uint32_t b0 = pk[j] >> 20, r = (pk[j] >> 10) & 0x3FFu, bc = pk[j] & 0x3FFu;
-            const uint64_t me = key[b0 + r];
-            uint32_t cmax = bc;
-            for (int d = 32; d >= 1; d >>= 1) cmax = max(cmax, (uint32_t)__shfl_xor((int)cmax, d));
-            uint32_t cnt = 0;
-            bool first = valid;
-            for (uint32_t m = 0; m < cmax; ++m) {
-                const bool eq = m < bc && key[b0 + m] == me;
-                cnt += eq ? 1u : 0u;
-                if (eq && m < r) first = false;
-            }
-            const unsigned long long fm = __ballot(first);
-            if (first) {
-                const uint32_t pos = o + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32),
-                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
-                a.out[ob + pos] = ((me & TAB_RMASK) << 20) | cnt;
-                account(qbase + me, cnt);
-            }
-            o += (uint32_t)__popcll(fm);
-        }
-        if (lane == 0) a.nd[q] = o;
-        wave_lds_sync();                           // (the next bucket reuses the bins and keys)
-    }
-    tab_stats_out(a.stats, st_canon, st_keys, st_sum, WF_WPG);
-}
-
-hipError_t launch_tab_wave_final(const TabFinal &a, uint32_t grid, hipStream_t s) {
-    if (a.capq <= 768)
-        hipLaunchKernelGGL(tab_wave_final_kernel<12>, dim3(grid), dim3(64 * WF_WPG), 0, s, a);
-    else if (a.capq <= TAB_WAVE_CAP)
-        hipLaunchKernelGGL(tab_wave_final_kernel<20>, dim3(grid), dim3(64 * WF_WPG), 0, s, a);
-    else
-        return hipErrorInvalidValue;
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
 hipError_t launch_tab_hist1(const TabArgs &a, hipStream_t s) {
