@@ -91,8 +91,8 @@ enum {
     KMER_FLAG_FASTA = 1u << 16,
     /* debug: table pass 1 always with fixed per-workgroup runs (by default
      * only when their filler slots are <= 1/12 of the keys: large inputs), and
-     * pass 2 with fixed bucket capacities (large buckets) at any table size
-     * (by default from 2^24 keys) */
+     * pass 2 with fixed region capacities at any table size (by default from
+     * 2^24 keys) */
     KMER_FLAG_TABLE_FIXED_TEST = 1u << 17,
     /* debug: the general path's first merge attempt reports a hash collision,
      * so the two-hash (h2, h1) retry runs (exercises the collision route) */

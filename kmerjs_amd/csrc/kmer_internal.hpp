@@ -571,12 +571,25 @@ struct TabFinal {
     // [qlo, qhi) when `left` is set
     uint32_t *left;
     unsigned int *left_n;
-    // fixed-capacity pass 2 (tab_scatter2f): bucket q's keys are B2[q capq ..
-    // q capq + inlen[q]) and `start` is the compact OUTPUT layout (the scan
-    // of inlen); no bucket groups.  capq 0: contiguous buckets, start for both.
+    // fixed-capacity pass 2 (tab_scatter2f): REGION r = tab_region(q) holds
+    // the keys of qg consecutive buckets of one partition (1: one bucket) at
+    // B2[r capq .. r capq + inlen[r]), in no order; rstart = the scan of inlen
+    // (the compact OUTPUT layout: entries of region r from rstart[r]).  qg 1:
+    // rstart is `start`; qg > 1: `start` holds rstart[tab_region(q)] (from
+    // tab_region_starts) and the sort final writes each bucket's exact start
+    // (wstart) from its counting sort.  capq 0: contiguous buckets, start for
+    // both.
     uint64_t capq;
     const uint32_t *inlen;
+    uint32_t qg, rpp, gmag;        // buckets per region, regions per partition, ceil(2^20 / qg)
+    const uint64_t *rstart;
+    uint64_t *wstart;
 };
+
+// fixed pass-2 region of bucket q (qg buckets per region, rpp regions per partition)
+__host__ __device__ inline uint32_t tab_region(uint32_t q, uint32_t rpp, uint32_t gmag) {
+    return (q >> TAB_L2) * rpp + (((q & (TAB_NB - 1)) * gmag) >> 20);
+}
 
 constexpr uint64_t TAB_PIECE = 4096;                   // windows per piece of a long line (pass 1)
 hipError_t launch_tab_piece_count(const uint64_t *wcount, uint64_t n, uint32_t *pc, uint32_t *split, hipStream_t s);
@@ -595,8 +608,11 @@ hipError_t launch_tab_starts(const uint64_t *H2s, const uint32_t *H2, uint64_t n
 // blen[q] = its keys; a bucket past its capacity sets ERR_TAB_CAP (the caller
 // redoes pass 2 with the counted route)
 hipError_t launch_tab_scatter2f(const uint64_t *B1, const TabUnit *units, const uint32_t *ufirst, uint32_t p0,
-                                uint32_t np, uint64_t cap, uint64_t *B2, uint32_t *blen, unsigned int *err,
-                                hipStream_t s);
+                                uint32_t np, uint64_t cap, uint32_t rpp, uint32_t gmag, uint64_t *B2, uint32_t *blen,
+                                unsigned int *err, hipStream_t s);
+// start[q] = rstart[tab_region(q)] for every bucket, start[TAB_NQ] = the total
+hipError_t launch_tab_region_starts(const uint64_t *rstart, uint32_t rpp, uint32_t gmag, uint64_t *start,
+                                    hipStream_t s);
 hipError_t launch_tab_scatter1f(const TabArgs &a, hipStream_t s);
 hipError_t launch_tab_wg_windows(const SeqLine *lines, uint64_t n, uint64_t lpw, uint32_t k, uint32_t nwg,
                                  uint64_t *W, hipStream_t s);
@@ -606,7 +622,8 @@ hipError_t launch_tab_spill_fill(uint64_t *B1, uint64_t base, uint64_t R, uint64
                                  const unsigned long long *pcur, hipStream_t s);
 hipError_t launch_tab_final(const TabFinal &a, uint32_t grid, hipStream_t s);
 hipError_t launch_tab_sort_final(const TabFinal &a, uint32_t grid, hipStream_t s);
-constexpr uint32_t TAB_SWG = 512;                      // sort-final workgroup (8 waves, two per CU)
+constexpr uint32_t TAB_SWG = 512;
+constexpr uint64_t TAB_SORT_GROUP_KEYS = 6144;          // sort final: keys of a unit of several buckets (TS_CAPG)                      // sort-final workgroup (8 waves, two per CU)
 hipError_t launch_tab_digest(const uint64_t *ent, const uint64_t *start, const uint32_t *nd, unsigned long long *out,
                              hipStream_t s);
 // multi-GPU table exchange: copy n segments {src offset, dst offset, length}

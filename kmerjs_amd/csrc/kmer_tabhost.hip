@@ -334,48 +334,63 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
     HIPCHK(c, c->tnd.ensure(TAB_NQ, s));
     HIPCHK(c, c->tbig.ensure(1 << 16, s));
     HIPCHK(c, c->tstats.ensure(5, s));
-    // Pass 2 with fixed bucket capacities (tab_scatter2f, no histogram pass)
-    // when buckets are large -- a count near its mean: mean + 6 sigma + 16
-    // slots -- else (small buckets, C5: ~480 keys, where the slack would be
-    // large) or after a capacity overflow, the counted route: tab_hist2, a
-    // scan, tab_scatter2c, bucket starts.  (KMERHIP_TAB_P2=count: always
-    // counted, A/B experiments.)
+    // Pass 2 with fixed capacities (tab_scatter2f, no histogram pass): a
+    // REGION of qg consecutive buckets of a partition holds mean + 6 sigma +
+    // 16 slots (a count near its mean).  Large buckets (mean >= 2,048: C3's
+    // ~11.4 K, the sort final's one-bucket units) get a region each; small
+    // ones (C5: ~480 keys) share one, as many as keep its capacity within a
+    // sort-final group (TS_CAPG keys: C5 11 buckets).  Else (small tables,
+    // < 2^24 keys) or after a capacity overflow, the counted route:
+    // tab_hist2, a scan, tab_scatter2c, bucket starts.
+    // KMER_FLAG_TABLE_FIXED_TEST: from any table size.  (KMERHIP_TAB_P2=count:
+    // always counted, A/B experiments.)
     const uint64_t n_est = n - std::min(n, c->t_fill);             // keys (filler slots excluded; an upper bound)
     const double mu = (double)n_est / TAB_NQ;
     const char *p2 = exp_env("KMERHIP_TAB_P2");
-    // Large buckets only (mean >= 2,048: the sort final's one-bucket units,
-    // C3): small ones (C5) are read by the final in groups of consecutive
-    // buckets, which needs them contiguous (a wave-per-bucket final over
-    // fixed regions measured slower than hist2 + the grouped final: C5 4.14
-    // vs 3.38 ms final).  KMER_FLAG_TABLE_FIXED_TEST: from any
-    // table size (by default from 2^24 keys).
-    const uint64_t cap6 = ((uint64_t)(mu + 6.0 * std::sqrt(mu)) + 16 + 7) & ~7ull;
+    auto cap6 = [](double m) { return ((uint64_t)(m + 6.0 * std::sqrt(m)) + 16 + 7) & ~7ull; };
+    const bool sort_ok = !exp_env("KMERHIP_TAB_FINAL") && !exp_env("KMERHIP_TAB_PROF");   // (general final alone: qg 1)
+    uint32_t qg = 0;
+    if (mu >= 2048.0) {
+        qg = 1;
+    } else if (sort_ok) {
+        for (uint32_t g = 64; g >= 2 && !qg; --g)
+            if (cap6(g * mu) <= TAB_SORT_GROUP_KEYS) qg = g;
+    }
     uint64_t capq = 0;
-    if (mu >= 2048.0 && (n_est >= (1ull << 24) || (c->p.flags & KMER_FLAG_TABLE_FIXED_TEST)) &&
+    uint32_t rpp = TAB_NB, gmag = 1u << 20;
+    if (qg && (n_est >= (1ull << 24) || (c->p.flags & KMER_FLAG_TABLE_FIXED_TEST)) &&
         !(c->p.flags & KMER_FLAG_TABLE_SPLIT_TEST) && !(p2 && strcmp(p2, "count") == 0) &&
         (qlo & (TAB_NB - 1)) == 0 && (qhi & (TAB_NB - 1)) == 0) {
-        capq = cap6;
-        HIPCHK(c, c->tb2.ensure((uint64_t)TAB_NQ * capq, s));
-        HIPCHK(c, c->tH.ensure((uint64_t)TAB_NQ + 1, s));
-        HIPCHK(c, c->tHs.ensure(TAB_NB, s));
+        capq = cap6(qg * mu);
+        rpp = (TAB_NB + qg - 1) / qg;
+        gmag = ((1u << 20) + qg - 1) / qg;
+        for (uint32_t b = 0; b < TAB_NB; ++b)      // (the region map is exact)
+            if (tab_region(b, rpp, gmag) != b / qg) return fail(c, KMER_E_DEVICE, "table region map");
+        const uint64_t nr = (uint64_t)TAB_NB * rpp;
+        HIPCHK(c, c->tb2.ensure(nr * capq, s));
+        HIPCHK(c, c->tH.ensure(nr + 1, s));
+        HIPCHK(c, c->tHs.ensure(TAB_NB / 2 + nr + 1, s));   // ufirst (u32), then the region starts
         st = upload(c, c->tHs.p, ufirst.data(), TAB_NB * sizeof(uint32_t), s);
         if (st) return st;
         uint32_t *blen = c->tH.p;
-        HIPCHK(c, hipMemsetAsync(blen, 0, ((uint64_t)TAB_NQ + 1) * sizeof(uint32_t), s));
+        HIPCHK(c, hipMemsetAsync(blen, 0, (nr + 1) * sizeof(uint32_t), s));
         HIPCHK(c, hipEventRecord(c->tev[4], s));
         HIPCHK(c, hipEventRecord(c->tev[5], s));
         HIPCHK(c, launch_tab_scatter2f(B1, c->tunits.p, (const uint32_t *)c->tHs.p, qlo >> TAB_L2,
-                                       (qhi - qlo) >> TAB_L2, capq, c->tb2.p, blen, c->d_err, s));
+                                       (qhi - qlo) >> TAB_L2, capq, rpp, gmag, c->tb2.p, blen, c->d_err, s));
         HIPCHK(c, hipEventRecord(c->tev[6], s));
         HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
-        if ((uint32_t)c->h_small[5] & ERR_TAB_CAP) {   // (a crowded bucket: the counted route)
+        if ((uint32_t)c->h_small[5] & ERR_TAB_CAP) {   // (a crowded region: the counted route)
             HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)c->d_err, (int)((uint32_t)c->h_small[5] & ~ERR_TAB_CAP), 1, s));
             capq = 0;
         } else {
-            // entries go out compactly: start = the scan of the buckets' key counts
-            ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, blen, c->tstart.p, (uint64_t)0, (size_t)TAB_NQ + 1,
+            // entries go out compactly: region starts = the scan of the regions'
+            // key counts (one bucket per region: the bucket starts themselves)
+            uint64_t *rst = qg == 1 ? c->tstart.p : c->tHs.p + TAB_NB / 2;
+            ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, blen, rst, (uint64_t)0, (size_t)(nr + 1),
                                                    rocprim::plus<uint64_t>(), s));
+            if (qg > 1) HIPCHK(c, launch_tab_region_starts(rst, rpp, gmag, c->tstart.p, s));
             c->t_p2_fixed += 1;
         }
     }
@@ -397,6 +412,11 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
     f.start = c->tstart.p;
     f.capq = capq;
     f.inlen = capq ? c->tH.p : nullptr;
+    f.qg = capq ? qg : 1;
+    f.rpp = rpp;
+    f.gmag = gmag;
+    f.rstart = capq ? (qg == 1 ? c->tstart.p : c->tHs.p + TAB_NB / 2) : nullptr;
+    f.wstart = c->tstart.p;
     f.out = c->t_ent;
     f.nd = c->tnd.p;
     const uint64_t mean = (n - std::min(n, c->t_fill)) / TAB_NQ;   // (keys, not filler slots)

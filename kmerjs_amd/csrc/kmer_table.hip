@@ -744,18 +744,26 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2c_kernel(const uint64_t *
 // bucket's last is written whole.  blen[q] = the bucket's keys.  The unused
 // tail of a region is never written nor read: the final takes (q cap,
 // blen[q]) and writes its entries compactly (start = the scan of blen).
+// Small buckets (C5: ~480 keys) share a REGION: qg consecutive buckets of the
+// partition (rpp = ceil(1,024 / qg) regions per partition, region of bucket
+// offset b = b gmag >> 20), whose summed count is again near its mean (C5: 11
+// buckets, ~5.3 K keys, 8 % slack); the final sorts a region's keys by bucket
+// anyway.  Fewer, larger regions also give longer write-out runs.
 __global__ __launch_bounds__(TAB_WG1) void tab_scatter2f_kernel(const uint64_t *B1, const TabUnit *units,
                                                                 const uint32_t *ufirst, uint32_t p0, uint64_t cap,
-                                                                uint64_t *B2, uint32_t *blen, unsigned int *err) {
+                                                                uint32_t rpp, uint32_t gmag, uint64_t *B2,
+                                                                uint32_t *blen, unsigned int *err) {
     __shared__ uint64_t srt[TS2_ROUND + TS2_CARRY * TAB_WG1];
     __shared__ uint64_t cur[TAB_NB];
     __shared__ uint32_t bcnt[TAB_NB], bst[TAB_NB];
     __shared__ uint32_t ws[16];
     __shared__ uint32_t sovf;
     const uint32_t t = threadIdx.x, p = p0 + blockIdx.x;
-    const uint64_t q = ((uint64_t)p << TAB_L2) | t;
-    const uint64_t pbase = ((uint64_t)p << TAB_L2) * cap;   // (region of bucket (p, b): pbase + b cap)
-    uint64_t dest = q * cap;                       // next B2 slot of bucket t
+    // region (p, b) of a key (threads t < rpp own regions)
+    auto reg = [&](uint64_t h) { return (((uint32_t)(h >> TAB_RBITS) & (TAB_NB - 1)) * gmag) >> 20; };
+    const uint64_t q = (uint64_t)p * rpp + t;
+    const uint64_t pbase = (uint64_t)p * rpp * cap;   // (region (p, b): pbase + b cap)
+    uint64_t dest = q * cap;                       // next B2 slot of region t
     const uint64_t cend = dest + cap;
     bcnt[t] = 0;
     if (t == 0) sovf = 0;
@@ -781,7 +789,7 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2f_kernel(const uint64_t *
             for (int j = 0; j < TS2_RPL; ++j) {
                 const uint32_t i = r0 + j * TAB_WG1 + t;
                 rank[j] = i < un.len && key[j] != TAB_SENT
-                              ? atomicAdd(&bcnt[(uint32_t)(key[j] >> TAB_RBITS) & (TAB_NB - 1)], 1u) : 0u;
+                              ? atomicAdd(&bcnt[reg(key[j])], 1u) : 0u;
             }
             __syncthreads();
             const uint32_t n_new = bcnt[t], tot = n_new + cc;
@@ -796,7 +804,7 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2f_kernel(const uint64_t *
             for (int j = 0; j < TS2_RPL; ++j) {
                 const uint32_t i = r0 + j * TAB_WG1 + t;
                 if (i < un.len && key[j] != TAB_SENT)
-                    srt[bst[(uint32_t)(key[j] >> TAB_RBITS) & (TAB_NB - 1)] + rank[j]] = key[j];
+                    srt[bst[reg(key[j])] + rank[j]] = key[j];
             }
 #pragma unroll
             for (int i = 0; i < TS2_CARRY; ++i)
@@ -810,7 +818,7 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2f_kernel(const uint64_t *
             }
             for (uint32_t i = t; i < total; i += TAB_WG1) {
                 const uint64_t h = srt[i];
-                const uint32_t b = (uint32_t)(h >> TAB_RBITS) & (TAB_NB - 1);
+                const uint32_t b = reg(h);
                 if (i < bcnt[b]) {
                     const uint64_t pos = cur[b] + i;
                     if (pos < pbase + (uint64_t)(b + 1) * cap) B2[pos] = h;
@@ -827,15 +835,29 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2f_kernel(const uint64_t *
             __syncthreads();
         }
     }
-    blen[q] = (uint32_t)((dest < cend ? dest : cend) - q * cap);
+    if (t < rpp) blen[q] = (uint32_t)((dest < cend ? dest : cend) - q * cap);
     if (t == 0 && sovf) atomicOr(err, ERR_TAB_CAP);
 }
 
 hipError_t launch_tab_scatter2f(const uint64_t *B1, const TabUnit *units, const uint32_t *ufirst, uint32_t p0,
-                                uint32_t np, uint64_t cap, uint64_t *B2, uint32_t *blen, unsigned int *err,
-                                hipStream_t s) {
-    if (np) hipLaunchKernelGGL(tab_scatter2f_kernel, dim3(np), dim3(TAB_WG1), 0, s, B1, units, ufirst, p0, cap, B2,
-                               blen, err);
+                                uint32_t np, uint64_t cap, uint32_t rpp, uint32_t gmag, uint64_t *B2, uint32_t *blen,
+                                unsigned int *err, hipStream_t s) {
+    if (rpp == 0 || rpp > TAB_NB || (cap & 7)) return hipErrorInvalidValue;
+    if (np) hipLaunchKernelGGL(tab_scatter2f_kernel, dim3(np), dim3(TAB_WG1), 0, s, B1, units, ufirst, p0, cap, rpp,
+                               gmag, B2, blen, err);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void tab_region_starts_kernel(const uint64_t *rstart, uint32_t rpp, uint32_t gmag,
+                                                                uint64_t *start) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < TAB_NQ) start[q] = rstart[tab_region(q, rpp, gmag)];
+    if (q == 0) start[TAB_NQ] = rstart[(uint64_t)TAB_NB * rpp];
+}
+
+hipError_t launch_tab_region_starts(const uint64_t *rstart, uint32_t rpp, uint32_t gmag, uint64_t *start,
+                                    hipStream_t s) {
+    hipLaunchKernelGGL(tab_region_starts_kernel, dim3(TAB_NQ / 256), dim3(256), 0, s, rstart, rpp, gmag, start);
     return hipGetLastError();
 }
 
@@ -1051,13 +1073,17 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
     const uint64_t gk = !(KH_ABLATE(a) & 4) ? (uint64_t)TAB_REG_MAX : rk;
     // (fixed-capacity buckets, capq: one bucket per unit, keys at B2[q capq ..
     // q capq + inlen[q]), entries out at start[q])
+    // (regions of qg buckets: u is a region's first bucket; the general kernel
+    // sees them only in list mode, whole regions)
     auto unit_n = [&](uint32_t u, uint32_t e) -> uint64_t {
-        return a.capq ? (uint64_t)a.inlen[u] : sc[e - cbase] - sc[u - cbase];
+        return a.capq ? (uint64_t)a.inlen[tab_region(u, a.rpp, a.gmag)] : sc[e - cbase] - sc[u - cbase];
     };
-    auto unit_in = [&](uint32_t u) -> uint64_t { return a.capq ? (uint64_t)u * a.capq : sc[u - cbase]; };
+    auto unit_in = [&](uint32_t u) -> uint64_t {
+        return a.capq ? (uint64_t)tab_region(u, a.rpp, a.gmag) * a.capq : sc[u - cbase];
+    };
     auto unit_end = [&](uint32_t u) -> uint32_t {
         uint32_t e = u + 1;
-        if (a.capq) return e;
+        if (a.capq) return min(u + a.qg, ((u >> TAB_L2) + 1) << TAB_L2);
         uint64_t tot = sc[u + 1 - cbase] - sc[u - cbase];
         if (tot > gk) return e;
         while (e < q1 && e - cbase < TAB_SC && e - u < TAB_GMAX) {
@@ -1387,6 +1413,7 @@ namespace {
 constexpr int TS_KPT = 24;                            // keys held per thread
 constexpr uint32_t TS_CAP1 = TS_KPT * TAB_SWG;        // one bucket: 12,288 keys, 32-bit LDS entries
 constexpr uint32_t TS_CAPG = TS_CAP1 / 2;             // a group: 6,144 keys, 64-bit LDS entries
+static_assert(TS_CAPG == TAB_SORT_GROUP_KEYS, "the host sizes regions of several buckets by TS_CAPG");
 constexpr uint32_t TS_NB = 8192;                      // bins (16-bit counts / starts, two per LDS word)
 constexpr uint32_t TS_NBB = 13;                       // log2(TS_NB)
 constexpr uint32_t TS_BINMAX = 64;                    // fuller bins: leftover (general kernel)
@@ -1405,8 +1432,21 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
     const uint32_t t = threadIdx.x, lane = t & 63;
     const uint32_t k = a.k;
     const uint32_t kmask = k >= 32 ? ~0u : ((1u << k) - 1u), sh = 32 - k;
-    const uint32_t per = (a.qhi - a.qlo + gridDim.x - 1) / gridDim.x;
-    const uint32_t q0 = min(a.qlo + blockIdx.x * per, a.qhi), q1 = q0 + per < a.qhi ? q0 + per : a.qhi;
+    uint32_t q0, q1;
+    if (a.capq) {
+        // fixed regions (one bucket or qg of them): shares of whole regions
+        // (qlo, qhi: partition boundaries)
+        const uint32_t rlo = (a.qlo >> TAB_L2) * a.rpp, nr = ((a.qhi - a.qlo) >> TAB_L2) * a.rpp;
+        const uint32_t per = (nr + gridDim.x - 1) / gridDim.x;
+        const uint32_t r0 = rlo + min(blockIdx.x * per, nr), r1 = min(r0 + per, rlo + nr);
+        auto first_bucket = [&](uint32_t r) { return (r / a.rpp) << TAB_L2 | (r % a.rpp) * a.qg; };
+        q0 = first_bucket(r0);
+        q1 = first_bucket(r1);
+    } else {
+        const uint32_t per = (a.qhi - a.qlo + gridDim.x - 1) / gridDim.x;
+        q0 = min(a.qlo + blockIdx.x * per, a.qhi);
+        q1 = q0 + per < a.qhi ? q0 + per : a.qhi;
+    }
     uint64_t st_canon = 0, st_keys = 0, st_sum = 0;
     // no prefix, odd k, Map view (C3): every entry is two Map keys, never a
     // palindrome; no prefix, canonical view (C5): every entry is one key with
@@ -1462,27 +1502,36 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
             a.left[2 * i + 1] = qb;
         }
     };
-    refill(cbase);
+    if (!a.capq) refill(cbase);
     uint32_t q = q0;
     while (q < q1) {
-        if (q - cbase >= TS_SC) {
+        if (!a.capq && q - cbase >= TS_SC) {
             cbase = q;
             refill(cbase);
         }
-        // the unit at q (uniform: every thread reads the same cached starts)
+        // the unit at q (uniform: every thread reads the same cached starts):
+        // a fixed region, or consecutive contiguous buckets up to TS_CAPG keys
         uint32_t qe = q + 1;
-        uint64_t n = a.capq ? (uint64_t)a.inlen[q] : sc[q + 1 - cbase] - sc[q - cbase];
-        if (n <= TS_CAPG && !a.capq) {               // (fixed-capacity buckets: one per unit)
-            while (qe < q1 && qe - cbase < TS_SC && qe - q < TS_GMAX) {
-                const uint64_t ne = sc[qe + 1 - cbase] - sc[qe - cbase];
-                if (n + ne > TS_CAPG) break;
-                n += ne;
-                ++qe;
+        uint64_t n, s0, s0in;                          // keys, output start, input start
+        if (a.capq) {
+            const uint32_t r = tab_region(q, a.rpp, a.gmag);
+            qe = min(q + a.qg, ((q >> TAB_L2) + 1) << TAB_L2);
+            n = a.inlen[r];
+            s0 = a.rstart[r];
+            s0in = (uint64_t)r * a.capq;
+        } else {
+            n = sc[q + 1 - cbase] - sc[q - cbase];
+            if (n <= TS_CAPG) {
+                while (qe < q1 && qe - cbase < TS_SC && qe - q < TS_GMAX) {
+                    const uint64_t ne = sc[qe + 1 - cbase] - sc[qe - cbase];
+                    if (n + ne > TS_CAPG) break;
+                    n += ne;
+                    ++qe;
+                }
             }
+            s0 = s0in = sc[q - cbase];
         }
         const uint32_t g = qe - q;
-        const uint64_t s0 = sc[q - cbase];             // output (and, capq 0, input) start
-        const uint64_t s0in = a.capq ? (uint64_t)q * a.capq : s0;
         if (n == 0) {
             for (uint32_t i = t; i < g; i += TAB_SWG) a.nd[q + i] = 0;
             q = qe;
@@ -1549,6 +1598,11 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                 }
             }
             __syncthreads();
+            // a region of several buckets: each bucket's exact output start
+            // (its keys' bins are consecutive: bins j << sbb .. of offset j),
+            // also for a region left to the general kernel
+            const uint32_t sbb = TS_NBB - (ONE ? 0 : 32 - __clz(g - 1));
+            if (!ONE && a.capq && t < g) a.wstart[q + t] = s0 + (bst[(t << sbb) >> 1] & 0xFFFFu);
             if (smax > TS_BINMAX) return false;        // (uniform) many copies of a key
             // counting-sort scatter: bin start + rank in the bin (bst[b] stays the start of bin b)
 #pragma unroll
@@ -1563,6 +1617,23 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                     pk[j] = b << 14 | pos;
                 }
             __syncthreads();
+            // a group: the held keys are taken again in SORTED order (key j of
+            // thread t = sorted position 512 j + t), so a wave's keys are
+            // consecutive bins -- mostly one bucket, and the first copies'
+            // output slots take one counter bump per wave and bucket present
+            // (in load order a wave held keys of every bucket of a fixed
+            // region: C5 final 6.0 vs 3.4 ms)
+            if (!ONE) {
+#pragma unroll
+                for (int j = 0; j < KPT; ++j)
+                    if (left > j * (int)TAB_SWG) {
+                        const uint32_t i = j * TAB_SWG + t;
+                        const uint64_t x = lkey64[i];
+                        lo[j] = (uint32_t)x;
+                        hi[ONE ? 0 : j] = (uint32_t)(x >> 32);
+                        pk[j] = ((uint32_t)(x >> bsh) & (TS_NB - 1)) << 14 | i;
+                    }
+            }
             // every held key scans its bin [end of bin b - 1, end of bin b) for
             // copies of itself; the first copy emits (key, copies).  Keys go in
             // groups of G, element m of all G bins read together (G LDS reads
@@ -1645,7 +1716,8 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                     }
                     if (first) {
                         if (!(KH_ABLATE(a) & 32))
-                            a.out[(ONE ? s0 : sc[q + ql - cbase]) + pos] = ((xj & TAB_RMASK) << 20) | cnt;
+                            a.out[(ONE ? s0 : a.capq ? s0 + (bst[(ql << sbb) >> 1] & 0xFFFFu) : sc[q + ql - cbase]) + pos] =
+                                ((xj & TAB_RMASK) << 20) | cnt;
                         if (!(KH_ABLATE(a) & 16)) account(qbase + xj, cnt);
                     }
                 }

@@ -290,7 +290,7 @@ def test_c5_full_size_pins(native, fasta):
                     assert routes["merged"] == 0
                 elif not fasta:
                     assert routes["merged"] == routes["fixed"] and routes["counted"] == 0, routes
-                assert routes["p2_fixed"] == 0, routes   # (small buckets: the counted pass 2)
+                assert routes["p2_fixed"] == 1, routes   # (regions of 11 / 6 small buckets)
         finally:
             ctr.close()
     print("c5 routes", "fasta" if fasta else "single", seen)

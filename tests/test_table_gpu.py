@@ -512,17 +512,20 @@ def test_table_exchange_matches_one_table(native, world, k, flags_name, with_n, 
     del recvs
 
 
-def test_table_fixed_pass2_vs_oracle(native):
+@pytest.mark.parametrize("n", [20_000_000, 3_000_000])
+def test_table_fixed_pass2_vs_oracle(native, n):
     """Pass 2 without its histogram pass (tab_scatter2f, kmer_table_routes
     p2_fixed): at 20 M reads and k = 31 the buckets average 2,289 keys (>= 2,048),
-    so each gets a fixed capacity region; the table digest and Σ counts equal
-    the oracle's streamed over the same reads (lib/kmers.js:88-100 on both
-    strands).  Then 300 K copies of one read appended: each of its k-mers'
-    buckets far past its capacity -> ERR_TAB_CAP -> the counted route redoes
-    pass 2 (p2_fixed 0), and the digest is the sum of the parts (linearity)."""
+    so each gets a fixed capacity region; at 3 M reads (343 keys) 16
+    consecutive buckets share one (the sort final splits a region by bucket:
+    C5's case).  The table digest and Σ counts equal the oracle's streamed
+    over the same reads (lib/kmers.js:88-100 on both strands).  Then 300 K
+    copies of one read appended: each of its k-mers' regions far past its
+    capacity -> ERR_TAB_CAP -> the counted route redoes pass 2 (p2_fixed 0),
+    and the digest is the sum of the parts (linearity)."""
     import torch
     from oracle import oracle
-    n, k = 20_000_000, 31
+    k = 31
     buf = _device_input(n, seed=13)
     want_d, want_w = oracle.table_digest_synth(13, 0, n, k, 16)
     ctr = native.Counter(k=k, prefix=b"", flags=native.FLAG_UNORDERED)
