@@ -782,14 +782,16 @@ kmer_status kmer_table_digest(kmer_ctx *c, uint64_t *digest) {
     hipStream_t s = c->stream;
     unsigned long long *d = c->tstats.p + 4;
     HIPCHK(c, hipMemsetAsync(d, 0, 8, s));
-    HIPCHK(c, launch_tab_digest(c->t_ent, c->tstart.p, c->tnd.p, d, s));
+    const bool narrow = c->p.k <= TAB_NARROW_K;
+    HIPCHK(c, launch_tab_digest(c->t_ent, c->tstart.p, c->tnd.p, narrow ? 1u : 0u, d, s));
     uint64_t acc = 0;
     std::vector<TabBig> big(c->t_nbig);
     HIPCHK(c, hipMemcpyAsync(&acc, d, 8, hipMemcpyDeviceToHost, s));
     if (!big.empty())
         HIPCHK(c, hipMemcpyAsync(big.data(), c->tbig.p, big.size() * sizeof(TabBig), hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
-    for (const TabBig &b : big) acc += (b.count - TAB_CMAX) * tab_digest_mix(b.h);   // entries hold TAB_CMAX
+    for (const TabBig &b : big)   // (entries hold TAB_CMAX)
+        acc += (b.count - TAB_CMAX) * tab_digest_mix(narrow ? tab_mix(tab_unmix(b.h, true, TAB_INV)) : b.h);
     *digest = acc;
     return KMER_OK;
 }

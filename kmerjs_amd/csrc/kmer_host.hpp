@@ -419,7 +419,6 @@ kmer_status chunk_lines(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_
 kmer_status windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s);
 float ev_ms(kmer_ctx *c, hipEvent_t a, hipEvent_t b);
 kmer_status table_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s);
-uint64_t inv_odd(uint64_t a);   // inverse of an odd number mod 2^64 (Newton)
 kmer_status table_finish(kmer_ctx *c, const uint64_t *B1 = nullptr, uint32_t qlo = 0, uint32_t qhi = TAB_NQ);
 std::unordered_map<std::string, uint64_t> canonical_records(const kmer_ctx *c);
 kmer_status build_table_result(kmer_ctx *c, uint64_t lines, kmer_result **out);

@@ -495,6 +495,26 @@ constexpr uint32_t TAB_CAP = 7000;                     // distinct keys per rang
 // top bits -- partition and bucket -- depend on every bit of the code
 constexpr uint64_t TAB_MUL = 0x9E3779B97F4A7C15ull;
 __host__ __device__ inline uint64_t tab_mix(uint64_t x) { return x * TAB_MUL; }
+// NARROW keys (k <= 21: codes < 2^42): h = f(c) << 22 with f(c) = (c ^ (c >> 21))
+// TAB_MUL mod 2^42, a bijection of [0, 2^42) (the xor-shift lets the bucket bits
+// see every bit of c).  The remainder's low 22 bits are then 0, so pass 2 can
+// keep a key in 32 bits (bucket offset << 22 | the remainder's top 22 bits).
+constexpr uint32_t TAB_NSH = 22;
+constexpr uint64_t tab_inv_odd(uint64_t a) {   // inverse of an odd number mod 2^64 (Newton: 3 -> 96 bits)
+    uint64_t x = a;
+    for (int i = 0; i < 5; ++i) x *= 2 - a * x;
+    return x;
+}
+constexpr uint64_t TAB_INV = tab_inv_odd(TAB_MUL);
+static_assert(TAB_INV * TAB_MUL == 1, "TAB_INV");
+constexpr uint32_t TAB_NARROW_K = 21;
+__host__ __device__ inline uint64_t tab_mix_n(uint64_t c) { return ((c ^ (c >> 21)) * TAB_MUL) << TAB_NSH; }
+// the code of h (inv = TAB_MUL^-1 mod 2^64)
+__host__ __device__ inline uint64_t tab_unmix(uint64_t h, bool narrow, uint64_t inv) {
+    if (!narrow) return h * inv;
+    const uint64_t z = ((h >> TAB_NSH) * inv) & ((1ull << 42) - 1);
+    return z ^ (z >> 21);
+}
 // Table digest weight of a key h: the splitmix64 finalizer (kmer_table_digest)
 __host__ __device__ inline uint64_t tab_digest_mix(uint64_t h) {
     h ^= h >> 30;
@@ -514,6 +534,7 @@ struct TabArgs {
     uint32_t k;
     uint32_t plo, phi, pmask;      // prefix planes (base i at bit i), mask of |P| bits
     uint32_t canonical;            // non-ACGT windows: forward-strand records, unfiltered (KMER_FLAG_CANONICAL)
+    uint32_t narrow;               // k <= 21: h = tab_mix_n(c), else tab_mix(c)
     uint32_t *H1;                  // hist: [p * nwg + g]
     const uint64_t *H1s;           // scatter: exclusive scan of H1 (chunk-relative)
     uint64_t base;                 // scatter: session keys before this chunk
@@ -562,7 +583,9 @@ struct TabFinal {
     unsigned int *err;
     uint32_t k, plo, phi, pmask;
     uint32_t canonical;            // statistics of the canonical-k-mer view (KMER_FLAG_CANONICAL)
-    uint64_t inv;                  // inverse of TAB_MUL mod 2^64 (tab_mix^-1)
+    uint64_t inv;                  // inverse of TAB_MUL mod 2^64 (tab_unmix)
+    uint32_t narrow;               // keys h = tab_mix_n(c) (k <= 21)
+    uint32_t b2n;                  // (narrow, capq) B2 holds 32-bit keys: (uint32_t)(h >> 22) (bucket offset, remainder)
     unsigned long long *stats;     // [0] canonical entries [1] Map keys [2] sum of Map counts
     uint64_t *prof;                // experiments only (KMERHIP_TAB_PROF): per-workgroup phase clocks, 8 each
     uint32_t qlo, qhi;             // buckets [qlo, qhi) of this table (multi-GPU: the rank's partitions)
@@ -608,8 +631,8 @@ hipError_t launch_tab_starts(const uint64_t *H2s, const uint32_t *H2, uint64_t n
 // blen[q] = its keys; a bucket past its capacity sets ERR_TAB_CAP (the caller
 // redoes pass 2 with the counted route)
 hipError_t launch_tab_scatter2f(const uint64_t *B1, const TabUnit *units, const uint32_t *ufirst, uint32_t p0,
-                                uint32_t np, uint64_t cap, uint32_t rpp, uint32_t gmag, uint64_t *B2, uint32_t *blen,
-                                unsigned int *err, hipStream_t s);
+                                uint32_t np, uint64_t cap, uint32_t rpp, uint32_t gmag, bool narrow, void *B2,
+                                uint32_t *blen, unsigned int *err, hipStream_t s);
 // start[q] = rstart[tab_region(q)] for every bucket, start[TAB_NQ] = the total
 hipError_t launch_tab_region_starts(const uint64_t *rstart, uint32_t rpp, uint32_t gmag, uint64_t *start,
                                     hipStream_t s);
@@ -623,8 +646,10 @@ hipError_t launch_tab_spill_fill(uint64_t *B1, uint64_t base, uint64_t R, uint64
 hipError_t launch_tab_final(const TabFinal &a, uint32_t grid, hipStream_t s);
 hipError_t launch_tab_sort_final(const TabFinal &a, uint32_t grid, hipStream_t s);
 constexpr uint32_t TAB_SWG = 512;
+constexpr uint64_t TAB_SORT_KEYS = 12288;               // sort final: keys of a unit (one bucket, or narrow keys: TS_CAP1)
 constexpr uint64_t TAB_SORT_GROUP_KEYS = 6144;          // sort final: keys of a unit of several buckets (TS_CAPG)                      // sort-final workgroup (8 waves, two per CU)
-hipError_t launch_tab_digest(const uint64_t *ent, const uint64_t *start, const uint32_t *nd, unsigned long long *out,
+hipError_t launch_tab_digest(const uint64_t *ent, const uint64_t *start, const uint32_t *nd, uint32_t narrow,
+                            unsigned long long *out,
                              hipStream_t s);
 // multi-GPU table exchange: copy n segments {src offset, dst offset, length}
 // of u64 keys (one workgroup per segment, grid-strided)

@@ -233,6 +233,7 @@ kmer_status table_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_t
         }
         a.pmask = c->prefix.size() >= 32 ? ~0u : ((1u << c->prefix.size()) - 1u);
         a.canonical = (c->p.flags & KMER_FLAG_CANONICAL) ? 1u : 0u;
+        a.narrow = c->p.k <= TAB_NARROW_K ? 1u : 0u;
         a.err = c->d_err;
         const uint64_t nh = (uint64_t)TAB_NB * a.nwg;
         HIPCHK(c, c->tH.ensure(nh, s));
@@ -269,11 +270,6 @@ kmer_status table_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_t
     return KMER_OK;
 }
 
-uint64_t inv_odd(uint64_t a) {   // inverse of an odd number mod 2^64 (Newton)
-    uint64_t x = a;
-    for (int i = 0; i < 5; ++i) x *= 2 - a * x;
-    return x;
-}
 
 // Pass 2 + final of the session: pass-1 partitions (one run per chunk) are
 // cut into units; each unit's keys go to their 2^20 buckets in tb2; the
@@ -347,14 +343,19 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
     const uint64_t n_est = n - std::min(n, c->t_fill);             // keys (filler slots excluded; an upper bound)
     const double mu = (double)n_est / TAB_NQ;
     const char *p2 = exp_env("KMERHIP_TAB_P2");
-    auto cap6 = [](double m) { return ((uint64_t)(m + 6.0 * std::sqrt(m)) + 16 + 7) & ~7ull; };
+    // Narrow keys (k <= 21, tab_mix_n): B2 holds 32-bit keys, and the sort
+    // final takes a region of up to TAB_SORT_KEYS of them (C5: 24 buckets).
+    const bool narrow = c->p.k <= TAB_NARROW_K;
+    const uint64_t al = narrow ? 16 : 8;            // (64-B blocks of keys)
+    auto cap6 = [&](double m) { return ((uint64_t)(m + 6.0 * std::sqrt(m)) + 16 + al - 1) & ~(al - 1); };
     const bool sort_ok = !exp_env("KMERHIP_TAB_FINAL") && !exp_env("KMERHIP_TAB_PROF");   // (general final alone: qg 1)
     uint32_t qg = 0;
-    if (mu >= 2048.0) {
+    if (mu >= 2048.0 && !narrow) {
         qg = 1;
-    } else if (sort_ok) {
-        for (uint32_t g = 64; g >= 2 && !qg; --g)
-            if (cap6(g * mu) <= TAB_SORT_GROUP_KEYS) qg = g;
+    } else {
+        const uint64_t lim = narrow ? TAB_SORT_KEYS : TAB_SORT_GROUP_KEYS;
+        for (uint32_t g = sort_ok ? 64 : 1; g >= 1 && !qg; --g)
+            if (cap6(g * mu) <= lim && (g >= 2 || narrow)) qg = g;
     }
     uint64_t capq = 0;
     uint32_t rpp = TAB_NB, gmag = 1u << 20;
@@ -367,7 +368,7 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
         for (uint32_t b = 0; b < TAB_NB; ++b)      // (the region map is exact)
             if (tab_region(b, rpp, gmag) != b / qg) return fail(c, KMER_E_DEVICE, "table region map");
         const uint64_t nr = (uint64_t)TAB_NB * rpp;
-        HIPCHK(c, c->tb2.ensure(nr * capq, s));
+        HIPCHK(c, c->tb2.ensure(narrow ? nr * capq / 2 : nr * capq, s));
         HIPCHK(c, c->tH.ensure(nr + 1, s));
         HIPCHK(c, c->tHs.ensure(TAB_NB / 2 + nr + 1, s));   // ufirst (u32), then the region starts
         st = upload(c, c->tHs.p, ufirst.data(), TAB_NB * sizeof(uint32_t), s);
@@ -377,7 +378,7 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
         HIPCHK(c, hipEventRecord(c->tev[4], s));
         HIPCHK(c, hipEventRecord(c->tev[5], s));
         HIPCHK(c, launch_tab_scatter2f(B1, c->tunits.p, (const uint32_t *)c->tHs.p, qlo >> TAB_L2,
-                                       (qhi - qlo) >> TAB_L2, capq, rpp, gmag, c->tb2.p, blen, c->d_err, s));
+                                       (qhi - qlo) >> TAB_L2, capq, rpp, gmag, narrow, c->tb2.p, blen, c->d_err, s));
         HIPCHK(c, hipEventRecord(c->tev[6], s));
         HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
@@ -437,7 +438,9 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
         f.phi |= (((uint32_t)ch >> 2) & 1u) << i;
     }
     f.pmask = c->prefix.size() >= 32 ? ~0u : ((1u << c->prefix.size()) - 1u);
-    f.inv = inv_odd(TAB_MUL);
+    f.inv = TAB_INV;
+    f.narrow = narrow ? 1u : 0u;
+    f.b2n = narrow && capq ? 1u : 0u;
     f.canonical = (c->p.flags & KMER_FLAG_CANONICAL) ? 1u : 0u;
     f.stats = c->tstats.p;
     f.qlo = qlo;
@@ -546,7 +549,7 @@ kmer_status build_table_result(kmer_ctx *c, uint64_t lines, kmer_result **out) {
         }
         std::unordered_map<uint64_t, uint64_t> bigc;
         for (auto &b : big) bigc[b.h] = b.count;
-        const uint64_t inv = inv_odd(TAB_MUL);
+        const bool narrow = k <= TAB_NARROW_K;
         const bool canon = (c->p.flags & KMER_FLAG_CANONICAL) != 0;
         const uint64_t kmask = k >= 32 ? 0xFFFFFFFFull : ((1ull << k) - 1);
         std::string key(k, 'A'), rkey(k, 'A');
@@ -556,7 +559,7 @@ kmer_status build_table_result(kmer_ctx *c, uint64_t lines, kmer_result **out) {
                 const uint64_t h = ((uint64_t)q << TAB_RBITS) | (w >> 20);
                 uint64_t cnt = w & TAB_CMAX;
                 if (cnt == TAB_CMAX) cnt = bigc[h];
-                const uint64_t x = h * inv;          // tab_mix^-1
+                const uint64_t x = tab_unmix(h, narrow, TAB_INV);
                 const uint64_t lo = x & kmask, hi = (x >> k) & kmask;
                 for (uint32_t j = 0; j < k; ++j) {
                     const uint32_t v = (uint32_t)(((hi >> j) & 1u) << 1 | ((lo >> j) & 1u));

@@ -231,7 +231,7 @@ __device__ __forceinline__ uint32_t tab_round(const TabArgs &a, TabCur &c, bool 
                 const uint32_t rlo = (uint32_t)(RLO >> (64 - m - k)) & kmask;
                 const uint32_t rhi = (uint32_t)(RHI >> (64 - m - k)) & kmask;
                 const uint64_t cf = ((uint64_t)fhi << k) | flo, cr = ((uint64_t)rhi << k) | rlo;
-                key[OFF + m] = tab_mix(cf < cr ? cf : cr);
+                key[OFF + m] = a.narrow ? tab_mix_n(cf < cr ? cf : cr) : tab_mix(cf < cr ? cf : cr);
             }
             return ((nv >= 32 ? ~0u : (1u << nv) - 1u)) << OFF;
         }
@@ -249,7 +249,7 @@ __device__ __forceinline__ uint32_t tab_round(const TabArgs &a, TabCur &c, bool 
         if (fx == 0) {
             if (fm || rm) {
                 const uint64_t cf = ((uint64_t)fhi << k) | flo, cr = ((uint64_t)rhi << k) | rlo;
-                key[OFF + m] = tab_mix(cf < cr ? cf : cr);
+                key[OFF + m] = a.narrow ? tab_mix_n(cf < cr ? cf : cr) : tab_mix(cf < cr ? cf : cr);
                 valid |= 1u << m;
             }
         } else if (rec) {
@@ -749,11 +749,22 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2c_kernel(const uint64_t *
 // offset b = b gmag >> 20), whose summed count is again near its mean (C5: 11
 // buckets, ~5.3 K keys, 8 % slack); the final sorts a region's keys by bucket
 // anyway.  Fewer, larger regions also give longer write-out runs.
+// NAR (narrow keys, k <= 21: h's low 22 bits are 0): B2 holds the 32-bit key
+// (uint32_t)(h >> 22) = bucket offset << 22 | the remainder's top 22 bits (the
+// partition is the region's), half the bytes; the LDS sort runs on those
+// 32-bit keys and the write-out aligns to 16 keys (64 B).
+template <bool NAR>
 __global__ __launch_bounds__(TAB_WG1) void tab_scatter2f_kernel(const uint64_t *B1, const TabUnit *units,
                                                                 const uint32_t *ufirst, uint32_t p0, uint64_t cap,
-                                                                uint32_t rpp, uint32_t gmag, uint64_t *B2,
+                                                                uint32_t rpp, uint32_t gmag, void *B2v,
                                                                 uint32_t *blen, unsigned int *err) {
-    __shared__ uint64_t srt[TS2_ROUND + TS2_CARRY * TAB_WG1];
+    using KT = typename std::conditional<NAR, uint32_t, uint64_t>::type;
+    constexpr int CARRY = NAR ? 15 : TS2_CARRY;    // (< one 64-B block of keys)
+    constexpr uint64_t AL = NAR ? 16 : 8;
+    __shared__ uint64_t srt_raw[TS2_ROUND + TS2_CARRY * TAB_WG1];
+    static_assert(sizeof(KT) * (TS2_ROUND + CARRY * TAB_WG1) <= sizeof(srt_raw), "scatter2f LDS");
+    KT *const srt = (KT *)srt_raw;
+    KT *const B2 = (KT *)B2v;
     __shared__ uint64_t cur[TAB_NB];
     __shared__ uint32_t bcnt[TAB_NB], bst[TAB_NB];
     __shared__ uint32_t ws[16];
@@ -761,16 +772,20 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2f_kernel(const uint64_t *
     const uint32_t t = threadIdx.x, p = p0 + blockIdx.x;
     // region (p, b) of a key (threads t < rpp own regions)
     auto reg = [&](uint64_t h) { return (((uint32_t)(h >> TAB_RBITS) & (TAB_NB - 1)) * gmag) >> 20; };
+    auto regk = [&](KT x) {
+        return NAR ? (((uint32_t)x >> (TAB_RBITS - TAB_NSH)) * gmag) >> 20 : reg((uint64_t)x);
+    };
+    auto kt = [&](uint64_t h) { return NAR ? (KT)(h >> TAB_NSH) : (KT)h; };
     const uint64_t q = (uint64_t)p * rpp + t;
     const uint64_t pbase = (uint64_t)p * rpp * cap;   // (region (p, b): pbase + b cap)
     uint64_t dest = q * cap;                       // next B2 slot of region t
     const uint64_t cend = dest + cap;
     bcnt[t] = 0;
     if (t == 0) sovf = 0;
-    uint32_t cc = 0;                               // carried keys of bucket t
-    uint64_t ck[TS2_CARRY];
+    uint32_t cc = 0;                               // carried keys of region t
+    KT ck[CARRY];
 #pragma unroll
-    for (int i = 0; i < TS2_CARRY; ++i) ck[i] = 0;
+    for (int i = 0; i < CARRY; ++i) ck[i] = 0;
     __syncthreads();
     const uint32_t u0 = ufirst[p], nun = units[u0].nunits;
     for (uint32_t ui = 0; ui < nun; ++ui) {
@@ -795,7 +810,7 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2f_kernel(const uint64_t *
             const uint32_t n_new = bcnt[t], tot = n_new + cc;
             uint32_t total;
             const uint32_t my_st = block_excl_1024(tot, ws, &total);
-            const uint64_t aend = last ? dest + tot : ((dest + tot) & ~7ull);
+            const uint64_t aend = last ? dest + tot : ((dest + tot) & ~(AL - 1));
             const uint32_t full = aend > dest ? (uint32_t)(aend - dest) : 0u;
             bst[t] = my_st;
             cur[t] = dest - my_st;
@@ -804,10 +819,10 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2f_kernel(const uint64_t *
             for (int j = 0; j < TS2_RPL; ++j) {
                 const uint32_t i = r0 + j * TAB_WG1 + t;
                 if (i < un.len && key[j] != TAB_SENT)
-                    srt[bst[reg(key[j])] + rank[j]] = key[j];
+                    srt[bst[reg(key[j])] + rank[j]] = kt(key[j]);
             }
 #pragma unroll
-            for (int i = 0; i < TS2_CARRY; ++i)
+            for (int i = 0; i < CARRY; ++i)
                 if ((uint32_t)i < cc) srt[my_st + n_new + i] = ck[i];
             bcnt[t] = my_st + full;
             __syncthreads();
@@ -817,8 +832,8 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2f_kernel(const uint64_t *
                 key[j] = i < un.len ? src[i] : 0;
             }
             for (uint32_t i = t; i < total; i += TAB_WG1) {
-                const uint64_t h = srt[i];
-                const uint32_t b = reg(h);
+                const KT h = srt[i];
+                const uint32_t b = regk(h);
                 if (i < bcnt[b]) {
                     const uint64_t pos = cur[b] + i;
                     if (pos < pbase + (uint64_t)(b + 1) * cap) B2[pos] = h;
@@ -827,7 +842,7 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2f_kernel(const uint64_t *
             }
             cc = tot - full;
 #pragma unroll
-            for (int i = 0; i < TS2_CARRY; ++i)
+            for (int i = 0; i < CARRY; ++i)
                 if ((uint32_t)i < cc) ck[i] = srt[my_st + full + i];
             dest += full;
             __syncthreads();
@@ -840,11 +855,16 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2f_kernel(const uint64_t *
 }
 
 hipError_t launch_tab_scatter2f(const uint64_t *B1, const TabUnit *units, const uint32_t *ufirst, uint32_t p0,
-                                uint32_t np, uint64_t cap, uint32_t rpp, uint32_t gmag, uint64_t *B2, uint32_t *blen,
-                                unsigned int *err, hipStream_t s) {
-    if (rpp == 0 || rpp > TAB_NB || (cap & 7)) return hipErrorInvalidValue;
-    if (np) hipLaunchKernelGGL(tab_scatter2f_kernel, dim3(np), dim3(TAB_WG1), 0, s, B1, units, ufirst, p0, cap, rpp,
-                               gmag, B2, blen, err);
+                                uint32_t np, uint64_t cap, uint32_t rpp, uint32_t gmag, bool narrow, void *B2,
+                                uint32_t *blen, unsigned int *err, hipStream_t s) {
+    if (rpp == 0 || rpp > TAB_NB || (cap & (narrow ? 15 : 7))) return hipErrorInvalidValue;
+    if (!np) return hipSuccess;
+    if (narrow)
+        hipLaunchKernelGGL(tab_scatter2f_kernel<true>, dim3(np), dim3(TAB_WG1), 0, s, B1, units, ufirst, p0, cap, rpp,
+                           gmag, B2, blen, err);
+    else
+        hipLaunchKernelGGL(tab_scatter2f_kernel<false>, dim3(np), dim3(TAB_WG1), 0, s, B1, units, ufirst, p0, cap, rpp,
+                           gmag, B2, blen, err);
     return hipGetLastError();
 }
 
@@ -1025,13 +1045,23 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
     };
     // a unit's keys (lanes past its end re-read its first key and are masked
     // at use): unconditional loads, all in flight together
-    auto load_keys = [&](uint64_t s0x, uint64_t nx) {
+    // (narrow B2, b2n: 32-bit keys h >> 22 without the partition bits, which
+    // come from the unit's bucket ux)
+    auto load_keys = [&](uint32_t ux, uint64_t s0x, uint64_t nx) {
         if (nx - 1 < (uint64_t)TAB_REG_MAX) {
             // (lane tests as t < nx - 1024 j: immediates, no per-j index registers)
-            const uint64_t *src = a.B2 + s0x;
             const int left = (int)nx - (int)t;
+            if (a.b2n) {
+                const uint32_t *src = (const uint32_t *)a.B2 + s0x;
+                const uint64_t pb = (uint64_t)(ux >> TAB_L2) << (64 - TAB_L1);
 #pragma unroll
-            for (int j = 0; j < TAB_KPT; ++j) kn[j] = src[left > j * (int)TAB_FWG ? j * TAB_FWG + t : 0u];
+                for (int j = 0; j < TAB_KPT; ++j)
+                    kn[j] = pb | (uint64_t)src[left > j * (int)TAB_FWG ? j * TAB_FWG + t : 0u] << TAB_NSH;
+            } else {
+                const uint64_t *src = a.B2 + s0x;
+#pragma unroll
+                for (int j = 0; j < TAB_KPT; ++j) kn[j] = src[left > j * (int)TAB_FWG ? j * TAB_FWG + t : 0u];
+            }
         }
     };
     auto refill = [&](uint32_t cb) {
@@ -1041,7 +1071,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
     };
     // Map statistics of one canonical entry h (App. A.6)
     auto account = [&](uint64_t h, uint64_t cnt) {
-        const uint64_t code = h * a.inv;
+        const uint64_t code = tab_unmix(h, a.narrow, a.inv);
         const uint32_t lo = (uint32_t)code & kmask, hi = (uint32_t)(code >> k) & kmask;
         const uint32_t rlo2 = __brev(~lo & kmask) >> sh, rhi2 = __brev(~hi & kmask) >> sh;
         const bool pal = lo == rlo2 && hi == rhi2;
@@ -1112,7 +1142,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
     cbase = q0;
     refill(cbase);
     uint32_t q = q0, qe = q0 < q1 ? unit_end(q0) : q0;
-    if (q0 < q1) load_keys(unit_in(q0), unit_n(q0, qe));
+    if (q0 < q1) load_keys(q0, unit_in(q0), unit_n(q0, qe));
     while (q < q1) {
         if (q - cbase >= TAB_SC) {
             cbase = q;
@@ -1128,7 +1158,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
         const bool inreg = n <= TAB_REG_MAX;
         if (n == 0) {
             for (uint32_t i = t; i < g; i += TAB_FWG) a.nd[q + i] = 0;
-            if (more) load_keys(s0n, nn);
+            if (more) load_keys(qn, s0n, nn);
             mark(5);
             q = qn;
             qe = qne;
@@ -1209,7 +1239,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
                             lbuf[sst[(uint32_t)(kn[j] >> bsh) & (TAB_SB - 1)] + rank[j]] = kn[j];
                 }
                 // the registers are free: the next unit's keys load during the dedupe
-                if (more) load_keys(s0n, nn);
+                if (more) load_keys(qn, s0n, nn);
                 __syncthreads();
                 // each distinct key once, with the count of its copies (a
                 // key's copies share its bin); output slots from one LDS
@@ -1296,9 +1326,11 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
                 if (lane == 0 && cl) atomicAdd(&occ, cl);
             } else {
                 const uint64_t *src = a.B2 + s0in;
+                const uint32_t *src32 = (const uint32_t *)a.B2 + s0in;
+                const uint64_t pb = (uint64_t)(q >> TAB_L2) << (64 - TAB_L1);
                 for (uint64_t i = t; i < n; i += TAB_FWG) {
                     if (lds_flag(&ovf)) break;
-                    uint64_t r1[1] = {src[i] - qbase};
+                    uint64_t r1[1] = {(a.b2n ? pb | (uint64_t)src32[i] << TAB_NSH : src[i]) - qbase};
                     if (r1[0] >= rlo && r1[0] < rhi) {
                         uint32_t cl = tab_insert_grp<1>(tkey, tcnt, r1, 0, 1u, &ovf);
                         if (cl) atomicAdd(&occ, cl);
@@ -1330,7 +1362,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
             }
             // the unit's last range is merged: load the next unit's keys now,
             // in flight while this one is emitted
-            if (top == 1 && more) load_keys(s0n, nn);
+            if (top == 1 && more) load_keys(qn, s0n, nn);
             // emit (and clear) the occupied slots: per wave, one LDS counter
             // bump per bucket present among the wave's entries
 #pragma unroll 1
@@ -1413,7 +1445,7 @@ namespace {
 constexpr int TS_KPT = 24;                            // keys held per thread
 constexpr uint32_t TS_CAP1 = TS_KPT * TAB_SWG;        // one bucket: 12,288 keys, 32-bit LDS entries
 constexpr uint32_t TS_CAPG = TS_CAP1 / 2;             // a group: 6,144 keys, 64-bit LDS entries
-static_assert(TS_CAPG == TAB_SORT_GROUP_KEYS, "the host sizes regions of several buckets by TS_CAPG");
+static_assert(TS_CAPG == TAB_SORT_GROUP_KEYS && TS_CAP1 == TAB_SORT_KEYS, "the host sizes regions by TS_CAPG / TS_CAP1");
 constexpr uint32_t TS_NB = 8192;                      // bins (16-bit counts / starts, two per LDS word)
 constexpr uint32_t TS_NBB = 13;                       // log2(TS_NB)
 constexpr uint32_t TS_BINMAX = 64;                    // fuller bins: leftover (general kernel)
@@ -1467,7 +1499,7 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
             st_sum += cnt;
             return;
         }
-        const uint64_t code = h * a.inv;
+        const uint64_t code = tab_unmix(h, a.narrow, a.inv);
         const uint32_t lo = (uint32_t)code & kmask, hi = (uint32_t)(code >> k) & kmask;
         const uint32_t rlo2 = __brev(~lo & kmask) >> sh, rhi2 = __brev(~hi & kmask) >> sh;
         const bool pal = lo == rlo2 && hi == rhi2;
@@ -1544,22 +1576,37 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
         }
         const uint64_t qbase = (uint64_t)q << TAB_RBITS;
         const int left = (int)n - (int)t;
-        // One bucket (ONE) or a group: separate instantiations, so that each
-        // keeps only its own registers live.  Held keys: lo = low 32 bits,
-        // hi = the rest (a group's; one bucket's are its bin), pk = bin, later
+        // Three instantiations, so that each keeps only its own registers
+        // live: ONE bucket of 64-bit keys (its bin fixes the remainder's top
+        // bits: 32-bit LDS entries), a GRoup of buckets of 64-bit keys (64-bit
+        // entries, half the keys), and NARrow keys (a fixed region of 32-bit
+        // keys, bucket offset << 22 | the remainder's top 22 bits: one bucket
+        // or a group, 32-bit entries, all the keys).  Held keys: lo = low 32
+        // bits (narrow: the key), hi = the rest (a group's), pk = bin, later
         // bin << 14 | sorted position.  Returns false when a bin is crowded.
-        auto sort_unit = [&](auto one_tag) -> bool {
-            constexpr bool ONE = decltype(one_tag)::value;
-            constexpr int KPT = ONE ? TS_KPT : TS_KPT / 2;
-            const uint32_t bsh = TAB_RBITS + (ONE ? 0 : 32 - __clz(g - 1)) - TS_NBB;
-            uint32_t lo[KPT], hi[ONE ? 1 : KPT], pk[KPT];
-            {
+        auto sort_unit = [&](auto mode_tag) -> bool {
+            constexpr int MODE = decltype(mode_tag)::value;
+            constexpr bool ONE = MODE == 0, GRP = MODE == 1, NAR = MODE == 2;
+            constexpr int KPT = GRP ? TS_KPT / 2 : TS_KPT;
+            const uint32_t obits = g > 1 ? 32 - __clz(g - 1) : 0;
+            const uint32_t bsh = (NAR ? TAB_RBITS - TAB_NSH : TAB_RBITS) + obits - TS_NBB;
+            const bool single = g == 1;                  // (ONE: always)
+            uint32_t lo[KPT], hi[GRP ? KPT : 1], pk[KPT];
+            if (NAR) {
+                const uint32_t *src = (const uint32_t *)a.B2 + s0in;
+                const uint32_t qoff = (q & (TAB_NB - 1)) << (TAB_RBITS - TAB_NSH);
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) {
+                    lo[j] = src[left > j * (int)TAB_SWG ? j * TAB_SWG + t : 0u] - qoff;
+                    pk[j] = (lo[j] >> bsh) & (TS_NB - 1);
+                }
+            } else {
                 const uint64_t *src = a.B2 + s0in;
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
                     const uint64_t x = src[left > j * (int)TAB_SWG ? j * TAB_SWG + t : 0u] - qbase;
                     lo[j] = (uint32_t)x;
-                    if (!ONE) hi[ONE ? 0 : j] = (uint32_t)(x >> 32);
+                    if (GRP) hi[GRP ? j : 0] = (uint32_t)(x >> 32);
                     pk[j] = (uint32_t)(x >> bsh) & (TS_NB - 1);
                 }
             }
@@ -1601,8 +1648,8 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
             // a region of several buckets: each bucket's exact output start
             // (its keys' bins are consecutive: bins j << sbb .. of offset j),
             // also for a region left to the general kernel
-            const uint32_t sbb = TS_NBB - (ONE ? 0 : 32 - __clz(g - 1));
-            if (!ONE && a.capq && t < g) a.wstart[q + t] = s0 + (bst[(t << sbb) >> 1] & 0xFFFFu);
+            const uint32_t sbb = TS_NBB - obits;
+            if (!single && a.capq && t < g) a.wstart[q + t] = s0 + (bst[(t << sbb) >> 1] & 0xFFFFu);
             if (smax > TS_BINMAX) return false;        // (uniform) many copies of a key
             // counting-sort scatter: bin start + rank in the bin (bst[b] stays the start of bin b)
 #pragma unroll
@@ -1610,10 +1657,10 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                 if (left > j * (int)TAB_SWG) {
                     const uint32_t b = pk[j] >> 14;
                     const uint32_t pos = ((bst[b >> 1] >> (16 * (b & 1u))) & 0xFFFFu) + (pk[j] & 0x3FFFu);
-                    if (ONE)
-                        lkey[pos] = lo[j];
+                    if (GRP)
+                        lkey64[pos] = (uint64_t)hi[GRP ? j : 0] << 32 | lo[j];
                     else
-                        lkey64[pos] = (uint64_t)hi[ONE ? 0 : j] << 32 | lo[j];
+                        lkey[pos] = lo[j];
                     pk[j] = b << 14 | pos;
                 }
             __syncthreads();
@@ -1623,15 +1670,20 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
             // output slots take one counter bump per wave and bucket present
             // (in load order a wave held keys of every bucket of a fixed
             // region: C5 final 6.0 vs 3.4 ms)
-            if (!ONE) {
+            if (!single) {
 #pragma unroll
                 for (int j = 0; j < KPT; ++j)
                     if (left > j * (int)TAB_SWG) {
                         const uint32_t i = j * TAB_SWG + t;
-                        const uint64_t x = lkey64[i];
-                        lo[j] = (uint32_t)x;
-                        hi[ONE ? 0 : j] = (uint32_t)(x >> 32);
-                        pk[j] = ((uint32_t)(x >> bsh) & (TS_NB - 1)) << 14 | i;
+                        if (GRP) {
+                            const uint64_t x = lkey64[i];
+                            lo[j] = (uint32_t)x;
+                            hi[GRP ? j : 0] = (uint32_t)(x >> 32);
+                            pk[j] = ((uint32_t)(x >> bsh) & (TS_NB - 1)) << 14 | i;
+                        } else {
+                            lo[j] = lkey[i];
+                            pk[j] = ((lo[j] >> bsh) & (TS_NB - 1)) << 14 | i;
+                        }
                     }
             }
             // every held key scans its bin [end of bin b - 1, end of bin b) for
@@ -1639,7 +1691,7 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
             // groups of G, element m of all G bins read together (G LDS reads
             // in flight per step, steps = the largest bin of the group: ~3 keys
             // per bin at C3) instead of one key's bin after another.
-            constexpr int G = ONE ? 6 : 4;           // (A/B at C3 / C5: ONE 4 / 6 / 8 / 12 -> 60.9 / 58.3 / 59.7 / 82 ms; groups 3 / 4 / 6)
+            constexpr int G = GRP ? 4 : 6;           // (A/B at C3 / C5: ONE 4 / 6 / 8 / 12 -> 60.9 / 58.3 / 59.7 / 82 ms; groups 3 / 4 / 6)
 #pragma unroll
             for (int g0 = 0; g0 < KPT; g0 += G) {
                 if (!__any(left > g0 * (int)TAB_SWG)) break;
@@ -1664,11 +1716,11 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                         const bool in = m < c;
                         const uint32_t mm = in ? b0 + m : b0;
                         bool eq;
-                        if (ONE) {
-                            eq = in && lkey[mm] == lo[j];
-                        } else {
-                            const uint64_t xk = ((uint64_t)hi[ONE ? 0 : j] << 32) | lo[j];
+                        if (GRP) {
+                            const uint64_t xk = ((uint64_t)hi[GRP ? j : 0] << 32) | lo[j];
                             eq = in && lkey64[mm] == xk;
+                        } else {
+                            eq = in && lkey[mm] == lo[j];
                         }
                         cf[u] += eq ? 1u : 0u;
                         if (eq && b0 + m < (pk[j] & 0x3FFFu)) cf[u] &= 0xFFu;    // an earlier copy
@@ -1676,7 +1728,7 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                 }
                 // one bucket: the group's output slots from ONE counter bump per wave
                 uint32_t gbase = 0;
-                if (ONE) {
+                if (single) {
                     uint32_t tot = 0;
 #pragma unroll
                     for (int u = 0; u < G; ++u) tot += (uint32_t)__popcll(__ballot((cf[u] >> 8) != 0u));
@@ -1692,13 +1744,14 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                     const uint32_t b = pk[j] >> 14;
                     // (one bucket: the bin is the remainder's top TS_NBB bits, bits 31 .. 43)
                     const uint64_t xj = ONE ? (((uint64_t)b << (TAB_RBITS - TS_NBB)) | (lo[j] & ((1u << (TAB_RBITS - TS_NBB)) - 1u)))
-                                            : (((uint64_t)hi[ONE ? 0 : j] << 32) | lo[j]);
+                                        : GRP ? (((uint64_t)hi[GRP ? j : 0] << 32) | lo[j])
+                                              : (uint64_t)lo[j] << TAB_NSH;
                     const bool first = (cf[u] >> 8) != 0u;
                     const uint32_t cnt = cf[u] & 0xFFu;
                     // output slots: one LDS counter bump per wave and bucket present
                     unsigned long long fm = __ballot(first);
                     uint32_t pos = 0, ql = 0;
-                    if (ONE) {
+                    if (single) {
                         pos = gbase + (uint32_t)__popcll(fm & below);
                         gbase += (uint32_t)__popcll(fm);
                     } else {
@@ -1716,7 +1769,7 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                     }
                     if (first) {
                         if (!(KH_ABLATE(a) & 32))
-                            a.out[(ONE ? s0 : a.capq ? s0 + (bst[(ql << sbb) >> 1] & 0xFFFFu) : sc[q + ql - cbase]) + pos] =
+                            a.out[(single ? s0 : a.capq ? s0 + (bst[(ql << sbb) >> 1] & 0xFFFFu) : sc[q + ql - cbase]) + pos] =
                                 ((xj & TAB_RMASK) << 20) | cnt;
                         if (!(KH_ABLATE(a) & 16)) account(qbase + xj, cnt);
                     }
@@ -1724,7 +1777,8 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
             }
             return true;
         };
-        const bool ok = g == 1 ? sort_unit(std::true_type{}) : sort_unit(std::false_type{});
+        const bool ok = a.b2n ? sort_unit(std::integral_constant<int, 2>{})
+                        : g == 1 ? sort_unit(std::integral_constant<int, 0>{}) : sort_unit(std::integral_constant<int, 1>{});
         if (!ok) {
             leftover(q, qe);
             q = qe;
@@ -1850,7 +1904,8 @@ hipError_t launch_tab_segcopy(const uint64_t *src, const TabSeg *segs, uint32_t 
 // (mod 2^64; counts >= TAB_CMAX are corrected on the host from the big list).
 // One wave per bucket; one atomic per wave.
 __global__ __launch_bounds__(256) void tab_digest_kernel(const uint64_t *ent, const uint64_t *start,
-                                                         const uint32_t *nd, unsigned long long *out) {
+                                                         const uint32_t *nd, uint32_t narrow,
+                                                         unsigned long long *out) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
     uint64_t acc = 0;
@@ -1859,16 +1914,18 @@ __global__ __launch_bounds__(256) void tab_digest_kernel(const uint64_t *ent, co
         const uint32_t n = nd[q];
         for (uint32_t i = lane; i < n; i += 64) {
             const uint64_t w = ent[s0 + i];
-            acc += (w & TAB_CMAX) * tab_digest_mix(((uint64_t)q << TAB_RBITS) | (w >> 20));
+            const uint64_t h = ((uint64_t)q << TAB_RBITS) | (w >> 20);
+            // (the weight of the code's tab_mix hash, for narrow keys too)
+            acc += (w & TAB_CMAX) * tab_digest_mix(narrow ? tab_mix(tab_unmix(h, true, TAB_INV)) : h);
         }
     }
     for (int d = 32; d >= 1; d >>= 1) acc += (uint64_t)__shfl_xor((long long)acc, d);
     if (lane == 0 && acc) atomicAdd(out, (unsigned long long)acc);
 }
 
-hipError_t launch_tab_digest(const uint64_t *ent, const uint64_t *start, const uint32_t *nd, unsigned long long *out,
-                             hipStream_t s) {
-    hipLaunchKernelGGL(tab_digest_kernel, dim3(4096), dim3(256), 0, s, ent, start, nd, out);
+hipError_t launch_tab_digest(const uint64_t *ent, const uint64_t *start, const uint32_t *nd, uint32_t narrow,
+                            unsigned long long *out, hipStream_t s) {
+    hipLaunchKernelGGL(tab_digest_kernel, dim3(4096), dim3(256), 0, s, ent, start, nd, narrow, out);
     return hipGetLastError();
 }
 

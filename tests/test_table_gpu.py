@@ -512,20 +512,22 @@ def test_table_exchange_matches_one_table(native, world, k, flags_name, with_n, 
     del recvs
 
 
-@pytest.mark.parametrize("n", [20_000_000, 3_000_000])
-def test_table_fixed_pass2_vs_oracle(native, n):
+@pytest.mark.parametrize("n,k", [(20_000_000, 31), (3_000_000, 31), (3_000_000, 21)])
+def test_table_fixed_pass2_vs_oracle(native, n, k):
     """Pass 2 without its histogram pass (tab_scatter2f, kmer_table_routes
     p2_fixed): at 20 M reads and k = 31 the buckets average 2,289 keys (>= 2,048),
     so each gets a fixed capacity region; at 3 M reads (343 keys) 16
-    consecutive buckets share one (the sort final splits a region by bucket:
-    C5's case).  The table digest and Σ counts equal the oracle's streamed
-    over the same reads (lib/kmers.js:88-100 on both strands).  Then 300 K
-    copies of one read appended: each of its k-mers' regions far past its
-    capacity -> ERR_TAB_CAP -> the counted route redoes pass 2 (p2_fixed 0),
-    and the digest is the sum of the parts (linearity)."""
+    consecutive buckets share one (the sort final splits a region by bucket);
+    k = 21: narrow keys (tab_mix_n, 32-bit keys in B2), 31 buckets per region
+    (C5's case).  The table digest and Σ counts equal the oracle's streamed
+    over the same reads (lib/kmers.js:88-100 on both strands).  Then 100
+    copies of one read appended: its k-mers' bins hold > 64 keys, so their
+    regions go to the general final (still p2_fixed); then 300 K copies: each
+    of its k-mers' regions far past its capacity -> ERR_TAB_CAP -> the counted
+    route redoes pass 2 (p2_fixed 0).  The digests are the sums of the parts
+    (linearity)."""
     import torch
     from oracle import oracle
-    k = 31
     buf = _device_input(n, seed=13)
     want_d, want_w = oracle.table_digest_synth(13, 0, n, k, 16)
     ctr = native.Counter(k=k, prefix=b"", flags=native.FLAG_UNORDERED)
@@ -537,15 +539,15 @@ def test_table_fixed_pass2_vs_oracle(native, n):
         canon, keys, total = ctr.table_stats()
         assert total == 2 * want_w and ctr.table_digest() == want_d
         rec = buf[:317].clone()
-        reps = 300_000
-        buf2 = torch.cat([buf, rec.repeat(reps)])
-        del buf
-        ctr.reset()
-        ctr.feed_device(buf2.data_ptr(), buf2.numel())
-        ctr.finish(want_result=False)
-        assert ctr.table_routes()["p2_fixed"] == 0
         one_d, one_w = oracle.table_digest(bytes(rec.cpu().numpy()), k)
-        assert ctr.table_stats()[2] == 2 * (want_w + reps * one_w)
-        assert ctr.table_digest() == (want_d + reps * one_d) % (1 << 64)
+        for reps, fixed in ((100, 1), (300_000, 0)):
+            buf2 = torch.cat([buf, rec.repeat(reps)])
+            ctr.reset()
+            ctr.feed_device(buf2.data_ptr(), buf2.numel())
+            ctr.finish(want_result=False)
+            del buf2
+            assert ctr.table_routes()["p2_fixed"] == fixed, reps
+            assert ctr.table_stats()[2] == 2 * (want_w + reps * one_w)
+            assert ctr.table_digest() == (want_d + reps * one_d) % (1 << 64)
     finally:
         ctr.close()
