@@ -234,6 +234,8 @@ kmer_status table_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_t
         a.pmask = c->prefix.size() >= 32 ? ~0u : ((1u << c->prefix.size()) - 1u);
         a.canonical = (c->p.flags & KMER_FLAG_CANONICAL) ? 1u : 0u;
         a.narrow = c->p.k <= TAB_NARROW_K ? 1u : 0u;
+        if (const char *hx = exp_env("KMERHIP_TAB_HASH"))   // (A/B experiments: shift = no mix, results wrong)
+            if (a.narrow && strcmp(hx, "shift") == 0) a.narrow = 2;
         a.err = c->d_err;
         const uint64_t nh = (uint64_t)TAB_NB * a.nwg;
         HIPCHK(c, c->tH.ensure(nh, s));

@@ -144,6 +144,13 @@ __device__ __forceinline__ uint64_t tab_brev64(uint64_t x) {
     return ((uint64_t)__brev((uint32_t)x) << 32) | __brev((uint32_t)(x >> 32));
 }
 
+__device__ __forceinline__ uint64_t tab_key(const TabArgs &a, uint64_t c) {
+#ifdef KMERHIP_EXPERIMENTS
+    if (a.narrow == 2) return (c << 54) | ((c >> 10) << TAB_NSH);   // (A/B only, results WRONG: the cost of the mix)
+#endif
+    return a.narrow ? tab_mix_n(c) : tab_mix(c);
+}
+
 template <int NS, int OFF, bool PFX>
 __device__ __forceinline__ uint32_t tab_round(const TabArgs &a, TabCur &c, bool rec, uint64_t (&key)[TAB_RPL]) {
     const uint32_t lane = threadIdx.x & 63;
@@ -231,7 +238,7 @@ __device__ __forceinline__ uint32_t tab_round(const TabArgs &a, TabCur &c, bool 
                 const uint32_t rlo = (uint32_t)(RLO >> (64 - m - k)) & kmask;
                 const uint32_t rhi = (uint32_t)(RHI >> (64 - m - k)) & kmask;
                 const uint64_t cf = ((uint64_t)fhi << k) | flo, cr = ((uint64_t)rhi << k) | rlo;
-                key[OFF + m] = a.narrow ? tab_mix_n(cf < cr ? cf : cr) : tab_mix(cf < cr ? cf : cr);
+                key[OFF + m] = tab_key(a, cf < cr ? cf : cr);
             }
             return ((nv >= 32 ? ~0u : (1u << nv) - 1u)) << OFF;
         }
@@ -249,7 +256,7 @@ __device__ __forceinline__ uint32_t tab_round(const TabArgs &a, TabCur &c, bool 
         if (fx == 0) {
             if (fm || rm) {
                 const uint64_t cf = ((uint64_t)fhi << k) | flo, cr = ((uint64_t)rhi << k) | rlo;
-                key[OFF + m] = a.narrow ? tab_mix_n(cf < cr ? cf : cr) : tab_mix(cf < cr ? cf : cr);
+                key[OFF + m] = tab_key(a, cf < cr ? cf : cr);
                 valid |= 1u << m;
             }
         } else if (rec) {

@@ -5,9 +5,10 @@ import sys
 
 path = sys.argv[1]
 which = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+anchor = sys.argv[3] if len(sys.argv) > 3 else 'scan_tile|scan_planes'   # (a kernel launched once per step)
 r = list(csv.DictReader(open(path)))
 r.sort(key=lambda x: int(x['Start_Timestamp']))
-idx = [i for i, x in enumerate(r) if 'scan_tile' in x['Kernel_Name'] or 'scan_planes' in x['Kernel_Name']]
+idx = [i for i, x in enumerate(r) if re.search(anchor, x['Kernel_Name'])]
 a, b = idx[which], idx[which + 1]
 t0 = int(r[a]['Start_Timestamp'])
 prev = None
