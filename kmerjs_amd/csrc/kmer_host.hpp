@@ -212,7 +212,7 @@ struct kmer_ctx {
     uint64_t abs_offset = 0;
     bool open_stream = false;      // reset called, not finished
     std::unordered_map<std::string, Ent> exotic;
-    uint64_t *h_small = nullptr;   // pinned (24 words): [0..7] copy of d_scal, [8..11] pos, [12..16] table feed
+    uint64_t *h_small = nullptr;   // pinned (24 words): [0..7] copy of d_scal, [8..11] pos, [12..17] table feed
     uint64_t *h_tail = nullptr;    // pinned, mapped, coherent: d_scal[0..7] written by the chunk tail kernel
     // pinned staging of every host -> device upload (upload()): a pageable
     // hipMemcpyAsync may read its host buffer after the call returns, so the

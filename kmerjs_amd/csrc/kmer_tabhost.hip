@@ -29,6 +29,8 @@ kmer_status table_scatter1(kmer_ctx *c, TabArgs &a, hipStream_t s, hipError_t (*
         HIPCHK(c, launch(a, s));
         HIPCHK(c, hipEventRecord(c->tev[3], s));
         HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
+        if (a.pcur)                                  // (fixed runs: the spill overflow count, same wait)
+            HIPCHK(c, hipMemcpyAsync(c->h_small + 17, a.pcur + TAB_NB, 8, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
         const float ms_s1 = ev_ms(c, c->tev[2], c->tev[3]);
         const uint32_t e = (uint32_t)c->h_small[5];
@@ -151,9 +153,7 @@ kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done
     HIPCHK(c, hipMemsetAsync(c->tspc.p, 0, (TAB_NB + 1) * 8, s));
     st = table_scatter1(c, a, s, launch_tab_scatter1f);
     if (st) return st;
-    unsigned long long over = 0;
-    HIPCHK(c, hipMemcpyAsync(&over, c->tspc.p + TAB_NB, 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipStreamSynchronize(s));
+    const unsigned long long over = c->h_small[17];   // (read with table_scatter1's wait)
     if (over) {                                // (records of the attempt are dropped: the counted pass redoes them)
         if (exp_env("KMERHIP_TAB_SPILL_LOG")) fprintf(stderr, "tab pass 1: spill area overflow (%llu)\n", over);
         return KMER_OK;
@@ -359,9 +359,13 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
         for (uint32_t g = sort_ok ? 64 : 1; g >= 1 && !qg; --g)
             if (cap6(g * mu) <= lim && (g >= 2 || narrow)) qg = g;
     }
+    // (a crowded region sets ERR_TAB_CAP: the finals then do nothing, and the
+    // check after them -- no wait between the passes -- redoes pass 2 and the
+    // finals on the counted route)
+    for (bool try_fixed = true;; try_fixed = false) {
     uint64_t capq = 0;
     uint32_t rpp = TAB_NB, gmag = 1u << 20;
-    if (qg && (n_est >= (1ull << 24) || (c->p.flags & KMER_FLAG_TABLE_FIXED_TEST)) &&
+    if (try_fixed && qg && (n_est >= (1ull << 24) || (c->p.flags & KMER_FLAG_TABLE_FIXED_TEST)) &&
         !(c->p.flags & KMER_FLAG_TABLE_SPLIT_TEST) && !(p2 && strcmp(p2, "count") == 0) &&
         (qlo & (TAB_NB - 1)) == 0 && (qhi & (TAB_NB - 1)) == 0) {
         capq = cap6(qg * mu);
@@ -382,20 +386,12 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
         HIPCHK(c, launch_tab_scatter2f(B1, c->tunits.p, (const uint32_t *)c->tHs.p, qlo >> TAB_L2,
                                        (qhi - qlo) >> TAB_L2, capq, rpp, gmag, narrow, c->tb2.p, blen, c->d_err, s));
         HIPCHK(c, hipEventRecord(c->tev[6], s));
-        HIPCHK(c, hipMemcpyAsync(c->h_small, c->d_scal, 8 * 8, hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipStreamSynchronize(s));
-        if ((uint32_t)c->h_small[5] & ERR_TAB_CAP) {   // (a crowded region: the counted route)
-            HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)c->d_err, (int)((uint32_t)c->h_small[5] & ~ERR_TAB_CAP), 1, s));
-            capq = 0;
-        } else {
-            // entries go out compactly: region starts = the scan of the regions'
-            // key counts (one bucket per region: the bucket starts themselves)
-            uint64_t *rst = qg == 1 ? c->tstart.p : c->tHs.p + TAB_NB / 2;
-            ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, blen, rst, (uint64_t)0, (size_t)(nr + 1),
-                                                   rocprim::plus<uint64_t>(), s));
-            if (qg > 1) HIPCHK(c, launch_tab_region_starts(rst, rpp, gmag, c->tstart.p, s));
-            c->t_p2_fixed += 1;
-        }
+        // entries go out compactly: region starts = the scan of the regions'
+        // key counts (one bucket per region: the bucket starts themselves)
+        uint64_t *rst = qg == 1 ? c->tstart.p : c->tHs.p + TAB_NB / 2;
+        ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, blen, rst, (uint64_t)0, (size_t)(nr + 1),
+                                               rocprim::plus<uint64_t>(), s));
+        if (qg > 1) HIPCHK(c, launch_tab_region_starts(rst, rpp, gmag, c->tstart.p, s));
     }
     if (!capq) {
         HIPCHK(c, c->tb2.ensure(n, s));
@@ -497,6 +493,14 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
     c->t_ms[3] += ev_ms(c, c->tev[4], c->tev[5]);
     c->t_ms[4] += ev_ms(c, c->tev[5], c->tev[6]);
     c->t_ms[5] += ev_ms(c, c->tev[2], c->tev[7]);
+    const uint32_t e = (uint32_t)c->h_small[5];
+    if (capq && (e & ERR_TAB_CAP)) {             // (a crowded region: the counted route)
+        HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)c->d_err, (int)(e & ~ERR_TAB_CAP), 1, s));
+        continue;
+    }
+    if (capq) c->t_p2_fixed += 1;
+    break;
+    }
     const uint32_t e = (uint32_t)c->h_small[5];
     if (e & ERR_COUNT_OVERFLOW) return fail(c, KMER_E_TOO_MANY_KEYS, "a k-mer count exceeds 2^32 - 1");
     if (e & ERR_BIG_OVERFLOW) return fail(c, KMER_E_OOM, "too many k-mers with counts >= 2^20");

@@ -1016,7 +1016,10 @@ constexpr uint32_t TAB_GMAX = 64;             // buckets per unit
 constexpr uint32_t TAB_SB = 4096;             // sort path: bins (top 12 remainder bits)
 constexpr uint32_t TAB_SORT_RUN = 128;        // sort path: largest 4-bin run a thread dedupes
 
+__device__ __forceinline__ bool tab_cap_failed(const TabFinal &a);
+
 __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
+    if (tab_cap_failed(a)) return;
     // hash table (8,192 slots of u64 key + u32 count) = the sort path's key array (12,288 u64)
     __shared__ uint64_t lbuf[TAB_SLOTS + TAB_SLOTS / 2];
     uint64_t *const tkey = lbuf;
@@ -1461,7 +1464,14 @@ constexpr uint32_t TS_SC = 512;                       // bucket starts cached pe
 
 }  // namespace
 
+// a fixed-capacity pass 2 that overflowed (ERR_TAB_CAP): the finals leave B1
+// (the pass-1 keys, under the table) intact for the counted route's redo
+__device__ __forceinline__ bool tab_cap_failed(const TabFinal &a) {
+    return a.capq && (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ERR_TAB_CAP);
+}
+
 __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) {
+    if (tab_cap_failed(a)) return;
     __shared__ uint32_t lkey[TS_CAP1];                // sorted unit: u32 (one bucket) or u64 (a group)
     __shared__ uint32_t bst[TS_NB / 2];               // bin counts, then starts: bin b in half b & 1 of word b >> 1
     __shared__ uint64_t sc[TS_SC + 2];                // start[cbase .. cbase + TS_SC + 1]
