@@ -264,10 +264,13 @@ kmer_status kmer_table_stats(kmer_ctx *ctx, uint64_t *canonical, uint64_t *keys,
  * h = q << 44 | remainder = c * 0x9E3779B97F4A7C15 (mod 2^64), a bijection of the canonical
  * planar code c = min(code(w), code(rc w)) with code = hi_plane << k | lo_plane,
  * base i of the k-mer at bit i of each plane, A/C/G/T = (hi,lo) 00/01/10/11.
- * k <= 21 (narrow keys): h = f(c) << 22 with f(c) = (c ^ (c >> 21)) *
- * 0x9E3779B97F4A7C15 mod 2^42 (so the remainder's low 22 bits are 0); then
- * c = z ^ (z >> 21), z = (h >> 22) * 0x9E3779B97F4A7C15^-1 mod 2^42.  (The
- * digest weighs c * 0x9E3779B97F4A7C15 for every k.)
+ * k <= 21 (narrow keys): h = f(c') << 23, f(x) = (x ^ (x >> 21)) *
+ * 0x9E3779B97F4A7C15 mod 2^41 (the remainder's low 23 bits are 0), where c'
+ * is, for even k, c; for odd k, the planar code of the orientation (w or
+ * rc w) whose middle base is A or C, with that base's high-plane bit (bit
+ * k + (k - 1) / 2, zero) taken out.  Inverse: x = z ^ (z >> 21), z = (h >>
+ * 23) * 0x9E3779B97F4A7C15^-1 mod 2^41, then (odd k) a zero bit put back at
+ * k + (k - 1) / 2.  (The digest weighs c * 0x9E3779B97F4A7C15 for every k.)
  * big = n_big {uint64 h, uint64 count} pairs.  Valid until the next reset. */
 kmer_status kmer_table_device(kmer_ctx *ctx, const void **d_entries, const void **d_bucket_start,
                               const void **d_bucket_len, const void **d_big, uint64_t *n_big);

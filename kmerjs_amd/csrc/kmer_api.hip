@@ -560,7 +560,10 @@ kmer_status kmer_table_exchange_prepare(kmer_ctx *c, uint32_t world, const void 
     *d_send = nullptr;
     const uint64_t n = c->t_keys;
     if (n == 0) return KMER_OK;
-    if (nch == 1 && c->t_cbase[0] == 0) {
+    // (narrow keys: the 32-bit pass-1 keys go out widened to h, the receiving
+    // side's table_finish reads 64-bit keys)
+    const bool narrow = c->p.k <= TAB_NARROW_K;
+    if (nch == 1 && c->t_cbase[0] == 0 && !narrow) {
         *d_send = c->tb1.p;
         return KMER_OK;
     }
@@ -569,7 +572,7 @@ kmer_status kmer_table_exchange_prepare(kmer_ctx *c, uint32_t world, const void 
     for (uint32_t p = 0; p < TAB_NB; ++p)
         for (size_t ch = 0; ch < nch; ++ch) {
             const uint64_t a0 = c->t_coff[ch][p], a1 = c->t_coff[ch][p + 1];
-            if (a1 > a0) segs.push_back(TabSeg{c->t_cbase[ch] + a0, dst, a1 - a0});
+            if (a1 > a0) segs.push_back(TabSeg{c->t_cbase[ch] + a0, dst, a1 - a0, p});
             dst += a1 - a0;
         }
     if (segs.size() >= (1ull << 31)) return fail(c, KMER_E_BAD_PARAM, "too many table segments");
@@ -577,7 +580,10 @@ kmer_status kmer_table_exchange_prepare(kmer_ctx *c, uint32_t world, const void 
     HIPCHK(c, c->tseg.ensure(segs.size(), s));
     kmer_status st = upload(c, c->tseg.p, segs.data(), segs.size() * sizeof(TabSeg), s);
     if (st) return st;
-    HIPCHK(c, launch_tab_segcopy(c->tb1.p, c->tseg.p, (uint32_t)segs.size(), c->tsend.p, s));
+    if (narrow)
+        HIPCHK(c, launch_tab_widen((const uint32_t *)c->tb1.p, c->tseg.p, (uint32_t)segs.size(), c->tsend.p, s));
+    else
+        HIPCHK(c, launch_tab_segcopy(c->tb1.p, c->tseg.p, (uint32_t)segs.size(), c->tsend.p, s));
     HIPCHK(c, hipStreamSynchronize(s));        // (the caller's collective follows)
     *d_send = c->tsend.p;
     return KMER_OK;
@@ -783,7 +789,7 @@ kmer_status kmer_table_digest(kmer_ctx *c, uint64_t *digest) {
     unsigned long long *d = c->tstats.p + 4;
     HIPCHK(c, hipMemsetAsync(d, 0, 8, s));
     const bool narrow = c->p.k <= TAB_NARROW_K;
-    HIPCHK(c, launch_tab_digest(c->t_ent, c->tstart.p, c->tnd.p, narrow ? 1u : 0u, d, s));
+    HIPCHK(c, launch_tab_digest(c->t_ent, c->tstart.p, c->tnd.p, c->p.k, narrow ? 1u : 0u, d, s));
     uint64_t acc = 0;
     std::vector<TabBig> big(c->t_nbig);
     HIPCHK(c, hipMemcpyAsync(&acc, d, 8, hipMemcpyDeviceToHost, s));
@@ -791,7 +797,7 @@ kmer_status kmer_table_digest(kmer_ctx *c, uint64_t *digest) {
         HIPCHK(c, hipMemcpyAsync(big.data(), c->tbig.p, big.size() * sizeof(TabBig), hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     for (const TabBig &b : big)   // (entries hold TAB_CMAX)
-        acc += (b.count - TAB_CMAX) * tab_digest_mix(narrow ? tab_mix(tab_unmix(b.h, true, TAB_INV)) : b.h);
+        acc += (b.count - TAB_CMAX) * tab_digest_mix(tab_digest_key(b.h, c->p.k, narrow));
     *digest = acc;
     return KMER_OK;
 }

@@ -495,11 +495,6 @@ constexpr uint32_t TAB_CAP = 7000;                     // distinct keys per rang
 // top bits -- partition and bucket -- depend on every bit of the code
 constexpr uint64_t TAB_MUL = 0x9E3779B97F4A7C15ull;
 __host__ __device__ inline uint64_t tab_mix(uint64_t x) { return x * TAB_MUL; }
-// NARROW keys (k <= 21: codes < 2^42): h = f(c) << 22 with f(c) = (c ^ (c >> 21))
-// TAB_MUL mod 2^42, a bijection of [0, 2^42) (the xor-shift lets the bucket bits
-// see every bit of c).  The remainder's low 22 bits are then 0, so pass 2 can
-// keep a key in 32 bits (bucket offset << 22 | the remainder's top 22 bits).
-constexpr uint32_t TAB_NSH = 22;
 constexpr uint64_t tab_inv_odd(uint64_t a) {   // inverse of an odd number mod 2^64 (Newton: 3 -> 96 bits)
     uint64_t x = a;
     for (int i = 0; i < 5; ++i) x *= 2 - a * x;
@@ -507,13 +502,50 @@ constexpr uint64_t tab_inv_odd(uint64_t a) {   // inverse of an odd number mod 2
 }
 constexpr uint64_t TAB_INV = tab_inv_odd(TAB_MUL);
 static_assert(TAB_INV * TAB_MUL == 1, "TAB_INV");
+// NARROW keys (k <= 21).  The key code c' has 41 bits: odd k -- the
+// orientation (w or rc w) whose middle base is A or C, with that base's zero
+// high-plane bit taken out (exactly one orientation qualifies: complementing a
+// base flips both its bits, and the middle base is its own mirror); even k --
+// min(code(w), code(rc w)) (< 2^40).  h = f(c') << 23 with f(x) = (x ^ (x >>
+// 21)) TAB_MUL mod 2^41, a bijection of [0, 2^41) (the xor-shift lets the
+// bucket bits see every bit).  The remainder's low 23 bits are then 0, and a
+// key below its partition fits 31 bits: (uint32_t)(h >> 23) = bucket offset
+// << 21 | the remainder's top 21 bits -- the 32-bit keys of pass 1's runs
+// (B1) and of pass 2's regions (B2), with TAB_SENT32 free for filler slots.
+constexpr uint32_t TAB_NSH = 23;
 constexpr uint32_t TAB_NARROW_K = 21;
-__host__ __device__ inline uint64_t tab_mix_n(uint64_t c) { return ((c ^ (c >> 21)) * TAB_MUL) << TAB_NSH; }
-// the code of h (inv = TAB_MUL^-1 mod 2^64)
-__host__ __device__ inline uint64_t tab_unmix(uint64_t h, bool narrow, uint64_t inv) {
+constexpr uint32_t TAB_SENT32 = 0xFFFFFFFFu;
+__host__ __device__ inline uint64_t tab_mix_n(uint64_t x) { return ((x ^ (x >> 21)) * TAB_MUL) << TAB_NSH; }
+// pass 1: the narrow key code of a window from its two orientations' codes
+__host__ __device__ inline uint64_t tab_canon_n(uint64_t cf, uint64_t cr, uint32_t k) {
+    if (!(k & 1)) return cf < cr ? cf : cr;
+    const uint32_t pos = k + (k - 1) / 2;             // the middle base's high-plane bit
+    const uint64_t c = ((cf >> pos) & 1) ? cr : cf;
+    return ((c >> (pos + 1)) << pos) | (c & ((1ull << pos) - 1));
+}
+// the planar code of h: the canonical code (wide keys) or an orientation of
+// the window (narrow keys); inv = TAB_MUL^-1 mod 2^64
+__host__ __device__ inline uint64_t tab_code(uint64_t h, uint32_t k, bool narrow, uint64_t inv) {
     if (!narrow) return h * inv;
-    const uint64_t z = ((h >> TAB_NSH) * inv) & ((1ull << 42) - 1);
-    return z ^ (z >> 21);
+    const uint64_t z = ((h >> TAB_NSH) * inv) & ((1ull << 41) - 1);
+    const uint64_t x = z ^ (z >> 21);
+    if (!(k & 1)) return x;
+    const uint32_t pos = k + (k - 1) / 2;
+    return ((x >> pos) << (pos + 1)) | (x & ((1ull << pos) - 1));
+}
+// reverse complement of a planar code (k <= 32)
+__host__ __device__ inline uint64_t tab_rc_code(uint64_t code, uint32_t k) {
+    const uint32_t km = k >= 32 ? ~0u : ((1u << k) - 1u);
+    const uint32_t lo = (uint32_t)code & km, hi = (uint32_t)(code >> k) & km;
+    const uint32_t rlo = __builtin_bitreverse32(~lo & km) >> (32 - k);
+    const uint32_t rhi = __builtin_bitreverse32(~hi & km) >> (32 - k);
+    return ((uint64_t)rhi << k) | rlo;
+}
+// the hash the table digest weighs: tab_mix(min(code(w), code(rc w))) for every k
+__host__ __device__ inline uint64_t tab_digest_key(uint64_t h, uint32_t k, bool narrow) {
+    if (!narrow) return h;
+    const uint64_t c = tab_code(h, k, true, TAB_INV), r = tab_rc_code(c, k);
+    return tab_mix(c < r ? c : r);
 }
 // Table digest weight of a key h: the splitmix64 finalizer (kmer_table_digest)
 __host__ __device__ inline uint64_t tab_digest_mix(uint64_t h) {
@@ -534,7 +566,7 @@ struct TabArgs {
     uint32_t k;
     uint32_t plo, phi, pmask;      // prefix planes (base i at bit i), mask of |P| bits
     uint32_t canonical;            // non-ACGT windows: forward-strand records, unfiltered (KMER_FLAG_CANONICAL)
-    uint32_t narrow;               // k <= 21: h = tab_mix_n(c), else tab_mix(c)
+    uint32_t narrow;               // k <= 21: h = tab_mix_n(tab_canon_n(..)), and B1 holds 32-bit keys (h >> 23)
     uint32_t *H1;                  // hist: [p * nwg + g]
     const uint64_t *H1s;           // scatter: exclusive scan of H1 (chunk-relative)
     uint64_t base;                 // scatter: session keys before this chunk
@@ -560,7 +592,7 @@ constexpr uint64_t TAB_SENT = 0ull - TAB_MUL;
 struct TabUnit {                   // pass 2: a run of one pass-1 partition's keys
     uint64_t start;                // first key in B1
     uint64_t hbase;                // H2 index of (bin 0, unit 0) of the partition
-    uint32_t len, u, nunits, pad;  // keys, unit index within the partition, units of the partition
+    uint32_t len, u, nunits, part; // keys, unit index within the partition, units of the partition, the partition
 };
 
 struct TabBig {                    // entries whose count does not fit the 20-bit field
@@ -583,9 +615,9 @@ struct TabFinal {
     unsigned int *err;
     uint32_t k, plo, phi, pmask;
     uint32_t canonical;            // statistics of the canonical-k-mer view (KMER_FLAG_CANONICAL)
-    uint64_t inv;                  // inverse of TAB_MUL mod 2^64 (tab_unmix)
+    uint64_t inv;                  // inverse of TAB_MUL mod 2^64 (tab_code)
     uint32_t narrow;               // keys h = tab_mix_n(c) (k <= 21)
-    uint32_t b2n;                  // (narrow, capq) B2 holds 32-bit keys: (uint32_t)(h >> 22) (bucket offset, remainder)
+    uint32_t b2n;                  // (narrow, capq) B2 holds 32-bit keys: (uint32_t)(h >> 23) (bucket offset, remainder)
     unsigned long long *stats;     // [0] canonical entries [1] Map keys [2] sum of Map counts
     uint64_t *prof;                // experiments only (KMERHIP_TAB_PROF): per-workgroup phase clocks, 8 each
     uint32_t qlo, qhi;             // buckets [qlo, qhi) of this table (multi-GPU: the rank's partitions)
@@ -631,8 +663,8 @@ hipError_t launch_tab_starts(const uint64_t *H2s, const uint32_t *H2, uint64_t n
 // blen[q] = its keys; a bucket past its capacity sets ERR_TAB_CAP (the caller
 // redoes pass 2 with the counted route)
 hipError_t launch_tab_scatter2f(const uint64_t *B1, const TabUnit *units, const uint32_t *ufirst, uint32_t p0,
-                                uint32_t np, uint64_t cap, uint32_t rpp, uint32_t gmag, bool narrow, void *B2,
-                                uint32_t *blen, unsigned int *err, hipStream_t s);
+                                uint32_t np, uint64_t cap, uint32_t rpp, uint32_t gmag, bool narrow, bool b1n,
+                                void *B2, uint32_t *blen, unsigned int *err, hipStream_t s);
 // start[q] = rstart[tab_region(q)] for every bucket, start[TAB_NQ] = the total
 hipError_t launch_tab_region_starts(const uint64_t *rstart, uint32_t rpp, uint32_t gmag, uint64_t *start,
                                     hipStream_t s);
@@ -641,22 +673,25 @@ hipError_t launch_tab_wg_windows(const SeqLine *lines, uint64_t n, uint64_t lpw,
                                  uint64_t *W, hipStream_t s);
 // pass-1 spill areas (tab_scatter1f): the unused slots of each partition's
 // spill area filled with TAB_SENT
-hipError_t launch_tab_spill_fill(uint64_t *B1, uint64_t base, uint64_t R, uint64_t S, uint64_t PS,
+hipError_t launch_tab_spill_fill(bool narrow, uint64_t *B1, uint64_t base, uint64_t R, uint64_t S, uint64_t PS,
                                  const unsigned long long *pcur, hipStream_t s);
 hipError_t launch_tab_final(const TabFinal &a, uint32_t grid, hipStream_t s);
 hipError_t launch_tab_sort_final(const TabFinal &a, uint32_t grid, hipStream_t s);
 constexpr uint32_t TAB_SWG = 512;
 constexpr uint64_t TAB_SORT_KEYS = 12288;               // sort final: keys of a unit (one bucket, or narrow keys: TS_CAP1)
 constexpr uint64_t TAB_SORT_GROUP_KEYS = 6144;          // sort final: keys of a unit of several buckets (TS_CAPG)                      // sort-final workgroup (8 waves, two per CU)
-hipError_t launch_tab_digest(const uint64_t *ent, const uint64_t *start, const uint32_t *nd, uint32_t narrow,
-                            unsigned long long *out,
+hipError_t launch_tab_digest(const uint64_t *ent, const uint64_t *start, const uint32_t *nd, uint32_t k,
+                            uint32_t narrow, unsigned long long *out,
                              hipStream_t s);
 // multi-GPU table exchange: copy n segments {src offset, dst offset, length}
 // of u64 keys (one workgroup per segment, grid-strided)
 struct TabSeg {
     uint64_t src, dst, len;
+    uint64_t part;                 // (tab_widen) the segment's pass-1 partition
 };
 hipError_t launch_tab_segcopy(const uint64_t *src, const TabSeg *segs, uint32_t n, uint64_t *dst, hipStream_t s);
+// 32-bit pass-1 keys (narrow) -> 64-bit h (segment src/dst in keys; filler -> TAB_SENT)
+hipError_t launch_tab_widen(const uint32_t *src, const TabSeg *segs, uint32_t n, uint64_t *dst, hipStream_t s);
 // FASTA input (kmer_fasta.hip, KMER_FLAG_FASTA): a chunk of FASTA rewritten
 // as FASTQ-shaped lines (header, joined sequence, "", "" per record).  A tile
 // of 16 KiB is a function of the header state it inherits: kind 0 passes the

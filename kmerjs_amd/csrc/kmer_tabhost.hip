@@ -104,14 +104,16 @@ kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done
     uint64_t sdiv = 64;                        // spill area: R / sdiv slots (KMERHIP_TAB_SPILLDIV: A/B experiments)
     if (const char *e = exp_env("KMERHIP_TAB_SPILLDIV")) sdiv = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
     for (uint32_t w = 0; w < a.nwg; ++w) tot += hw[w];
+    // (runs of whole 64-B blocks: 8 keys, narrow keys 16)
+    const uint64_t al = a.narrow ? 16 : 8;
     auto sized = [&](const std::vector<uint64_t> &ww, uint32_t nwg) {
         hp.assign(nwg + 1, 0);
         for (uint32_t w = 0; w < nwg; ++w) {
             const double mu = (double)ww[w] / TAB_NB;
-            hp[w + 1] = hp[w] + (ww[w] ? ((uint64_t)(mu + sig * std::sqrt(mu)) + 4 + 7) & ~7ull : 0);
+            hp[w + 1] = hp[w] + (ww[w] ? ((uint64_t)(mu + sig * std::sqrt(mu)) + 4 + al - 1) & ~(al - 1) : 0);
         }
         const uint64_t R = hp[nwg];
-        return (uint64_t)TAB_NB * (R + ((std::max<uint64_t>(256, R / sdiv) + 7) & ~7ull));
+        return (uint64_t)TAB_NB * (R + ((std::max<uint64_t>(256, R / sdiv) + al - 1) & ~(al - 1)));
     };
     uint64_t region = sized(hw, a.nwg);
     // small shares (C5's 1 GB of contigs cut into 4,096-window pieces: ~60
@@ -137,8 +139,8 @@ kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done
     // formation of every window)
     if (region > tot + tot / 8 && !(c->p.flags & KMER_FLAG_TABLE_FIXED_TEST)) return KMER_OK;
     const uint64_t R = hp[a.nwg];
-    const uint64_t S = (std::max<uint64_t>(256, R / sdiv) + 7) & ~7ull, PS = R + S;
-    const uint64_t cb = (c->t_keys + 7) & ~7ull;  // (runs of multiples of 8 keys start at 64-B boundaries)
+    const uint64_t S = (std::max<uint64_t>(256, R / sdiv) + al - 1) & ~(al - 1), PS = R + S;
+    const uint64_t cb = (c->t_keys + al - 1) & ~(al - 1);   // (runs of whole blocks start at 64-B boundaries)
     HIPCHK(c, c->tb1.ensure(cb + region, s, true, c->t_keys));
     HIPCHK(c, c->tspc.ensure(TAB_NB + 1, s));
     kmer_status st = upload(c, pcw, hp.data(), hp.size() * 8, s);
@@ -158,7 +160,7 @@ kmer_status table_pass1_fixed(kmer_ctx *c, TabArgs &a, hipStream_t s, bool *done
         if (exp_env("KMERHIP_TAB_SPILL_LOG")) fprintf(stderr, "tab pass 1: spill area overflow (%llu)\n", over);
         return KMER_OK;
     }
-    HIPCHK(c, launch_tab_spill_fill(c->tb1.p, cb, R, S, PS, c->tspc.p, s));
+    HIPCHK(c, launch_tab_spill_fill(a.narrow != 0, c->tb1.p, cb, R, S, PS, c->tspc.p, s));
     std::vector<uint64_t> off(TAB_NB + 1);
     for (uint32_t p = 0; p <= TAB_NB; ++p) off[p] = (uint64_t)p * PS;
     c->t_cbase.push_back(cb);
@@ -279,6 +281,9 @@ kmer_status table_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_t
 // B1: the pass-1 keys (default: this session's, tb1); [qlo, qhi): the buckets
 // present (multi-GPU: this rank's partitions; the others are left empty).
 kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t qhi) {
+    // this session's own pass-1 keys (B1 null) are 32 bits for narrow keys;
+    // received ones (exchanged) are 64-bit h
+    const bool b1n = !B1 && c->p.k <= TAB_NARROW_K;
     hipStream_t s = c->stream;
     c->t_canon = c->t_nkeys = c->t_sum = c->t_nbig = 0;
     c->t_done = true;
@@ -305,6 +310,7 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
                 TabUnit u{};
                 u.start = c->t_cbase[ch] + o;
                 u.len = (uint32_t)std::min<uint64_t>(ul, a1 - o);
+                u.part = p;
                 units.push_back(u);
             }
         }
@@ -362,6 +368,7 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
     // (a crowded region sets ERR_TAB_CAP: the finals then do nothing, and the
     // check after them -- no wait between the passes -- redoes pass 2 and the
     // finals on the counted route)
+    const uint64_t *B1w = nullptr;                 // (narrow pass-1 keys widened for the counted route)
     for (bool try_fixed = true;; try_fixed = false) {
     uint64_t capq = 0;
     uint32_t rpp = TAB_NB, gmag = 1u << 20;
@@ -384,7 +391,8 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
         HIPCHK(c, hipEventRecord(c->tev[4], s));
         HIPCHK(c, hipEventRecord(c->tev[5], s));
         HIPCHK(c, launch_tab_scatter2f(B1, c->tunits.p, (const uint32_t *)c->tHs.p, qlo >> TAB_L2,
-                                       (qhi - qlo) >> TAB_L2, capq, rpp, gmag, narrow, c->tb2.p, blen, c->d_err, s));
+                                       (qhi - qlo) >> TAB_L2, capq, rpp, gmag, narrow, b1n, c->tb2.p, blen, c->d_err,
+                                       s));
         HIPCHK(c, hipEventRecord(c->tev[6], s));
         // entries go out compactly: region starts = the scan of the regions'
         // key counts (one bucket per region: the bucket starts themselves)
@@ -394,13 +402,29 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
         if (qg > 1) HIPCHK(c, launch_tab_region_starts(rst, rpp, gmag, c->tstart.p, s));
     }
     if (!capq) {
+        if (b1n && !B1w) {
+            // the counted route reads 64-bit keys: widen the 32-bit pass-1
+            // keys once (h rebuilt from each unit's partition), the table then
+            // goes over the widened copy
+            std::vector<TabSeg> segs;
+            for (uint64_t i = 0; i < n_units; ++i)
+                if (units[i].len) segs.push_back(TabSeg{units[i].start, units[i].start, units[i].len, units[i].part});
+            HIPCHK(c, c->tsend.ensure(n, s));
+            HIPCHK(c, c->tseg.ensure(std::max<size_t>(segs.size(), 1), s));
+            st = upload(c, c->tseg.p, segs.data(), segs.size() * sizeof(TabSeg), s);
+            if (st) return st;
+            HIPCHK(c, launch_tab_widen((const uint32_t *)B1, c->tseg.p, (uint32_t)segs.size(), c->tsend.p, s));
+            B1w = c->tsend.p;
+        }
+        const uint64_t *B1c = b1n ? B1w : B1;
+        c->t_ent = const_cast<uint64_t *>(B1c);
         HIPCHK(c, c->tb2.ensure(n, s));
         HIPCHK(c, hipEventRecord(c->tev[4], s));
-        HIPCHK(c, launch_tab_hist2(B1, c->tunits.p, (uint32_t)n_units, c->tH.p, s));
+        HIPCHK(c, launch_tab_hist2(B1c, c->tunits.p, (uint32_t)n_units, c->tH.p, s));
         ROCPRIM_RUN(c, rocprim::exclusive_scan(t, b, c->tH.p, c->tHs.p, (uint64_t)0, (size_t)nh,
                                                rocprim::plus<uint64_t>(), s));
         HIPCHK(c, hipEventRecord(c->tev[5], s));
-        HIPCHK(c, launch_tab_scatter2(B1, c->tunits.p, (uint32_t)n_units, c->tHs.p, c->tb2.p, s));
+        HIPCHK(c, launch_tab_scatter2(B1c, c->tunits.p, (uint32_t)n_units, c->tHs.p, c->tb2.p, s));
         HIPCHK(c, hipEventRecord(c->tev[6], s));
         HIPCHK(c, launch_tab_starts(c->tHs.p, c->tH.p, nh, c->tunits.p + n_units, c->tstart.p, s));
     }
@@ -565,7 +589,7 @@ kmer_status build_table_result(kmer_ctx *c, uint64_t lines, kmer_result **out) {
                 const uint64_t h = ((uint64_t)q << TAB_RBITS) | (w >> 20);
                 uint64_t cnt = w & TAB_CMAX;
                 if (cnt == TAB_CMAX) cnt = bigc[h];
-                const uint64_t x = tab_unmix(h, narrow, TAB_INV);
+                const uint64_t x = tab_code(h, k, narrow, TAB_INV);
                 const uint64_t lo = x & kmask, hi = (x >> k) & kmask;
                 for (uint32_t j = 0; j < k; ++j) {
                     const uint32_t v = (uint32_t)(((hi >> j) & 1u) << 1 | ((lo >> j) & 1u));

@@ -144,11 +144,24 @@ __device__ __forceinline__ uint64_t tab_brev64(uint64_t x) {
     return ((uint64_t)__brev((uint32_t)x) << 32) | __brev((uint32_t)(x >> 32));
 }
 
-__device__ __forceinline__ uint64_t tab_key(const TabArgs &a, uint64_t c) {
+__device__ __forceinline__ uint64_t tab_key(const TabArgs &a, uint64_t cf, uint64_t cr) {
 #ifdef KMERHIP_EXPERIMENTS
-    if (a.narrow == 2) return (c << 54) | ((c >> 10) << TAB_NSH);   // (A/B only, results WRONG: the cost of the mix)
+    if (a.narrow == 2) {                             // (A/B only, results WRONG: the cost of the mix)
+        const uint64_t c = tab_canon_n(cf, cr, a.k);
+        return (c << 54) | ((c >> 10) << TAB_NSH);
+    }
 #endif
-    return a.narrow ? tab_mix_n(c) : tab_mix(c);
+    return a.narrow ? tab_mix_n(tab_canon_n(cf, cr, a.k)) : tab_mix(cf < cr ? cf : cr);
+}
+
+// pass-1 key stores: narrow keys as 32 bits below the partition (h >> 23)
+__device__ __forceinline__ void b1_store(const TabArgs &a, uint64_t i, uint64_t h) {
+    if (a.narrow) ((uint32_t *)a.B1)[i] = (uint32_t)(h >> TAB_NSH) & 0x7FFFFFFFu;
+    else a.B1[i] = h;
+}
+__device__ __forceinline__ void b1_fill(const TabArgs &a, uint64_t i) {
+    if (a.narrow) ((uint32_t *)a.B1)[i] = TAB_SENT32;
+    else a.B1[i] = TAB_SENT;
 }
 
 template <int NS, int OFF, bool PFX>
@@ -238,7 +251,7 @@ __device__ __forceinline__ uint32_t tab_round(const TabArgs &a, TabCur &c, bool 
                 const uint32_t rlo = (uint32_t)(RLO >> (64 - m - k)) & kmask;
                 const uint32_t rhi = (uint32_t)(RHI >> (64 - m - k)) & kmask;
                 const uint64_t cf = ((uint64_t)fhi << k) | flo, cr = ((uint64_t)rhi << k) | rlo;
-                key[OFF + m] = tab_key(a, cf < cr ? cf : cr);
+                key[OFF + m] = tab_key(a, cf, cr);
             }
             return ((nv >= 32 ? ~0u : (1u << nv) - 1u)) << OFF;
         }
@@ -256,7 +269,7 @@ __device__ __forceinline__ uint32_t tab_round(const TabArgs &a, TabCur &c, bool 
         if (fx == 0) {
             if (fm || rm) {
                 const uint64_t cf = ((uint64_t)fhi << k) | flo, cr = ((uint64_t)rhi << k) | rlo;
-                key[OFF + m] = tab_key(a, cf < cr ? cf : cr);
+                key[OFF + m] = tab_key(a, cf, cr);
                 valid |= 1u << m;
             }
         } else if (rec) {
@@ -346,7 +359,7 @@ __global__ __launch_bounds__(TAB_WGH) void tab_scatter1h_kernel(TabArgs a) {
         __syncthreads();
         for (uint32_t i = t; i < total; i += TAB_WGH) {
             const uint64_t h = srt[i];
-            a.B1[cur[(uint32_t)(h >> (64 - TAB_L1))] + i] = h;
+            b1_store(a, cur[(uint32_t)(h >> (64 - TAB_L1))] + i, h);
         }
         __syncthreads();
         cur[b0] += st0 + c0;
@@ -410,10 +423,10 @@ __global__ __launch_bounds__(TAB_WGH) void tab_scatter1f_kernel(TabArgs a) {
             const uint32_t p = (uint32_t)(h >> (64 - TAB_L1));
             const uint32_t j = fill[p] + (i - bst[p]);
             if (j < cap) {
-                a.B1[r0 + p * R + j] = h;
+                b1_store(a, r0 + p * R + j, h);
             } else {                                 // past the run: the partition's spill area
                 const unsigned long long o = atomicAdd(&a.pcur[p], 1ull);
-                if (o < a.S) a.B1[a.base + p * R + a.R + o] = h;
+                if (o < a.S) b1_store(a, a.base + p * R + a.R + o, h);
                 else atomicAdd(&a.pcur[TAB_NB], 1ull);
             }
         }
@@ -427,16 +440,19 @@ __global__ __launch_bounds__(TAB_WGH) void tab_scatter1f_kernel(TabArgs a) {
     // the runs' unused tails (a wave per partition)
     for (uint32_t p = t >> 6; p < TAB_NB; p += TAB_WGH / 64) {
         const uint32_t f = min(fill[p], cap);
-        for (uint32_t j = f + (t & 63); j < cap; j += 64) a.B1[r0 + p * R + j] = TAB_SENT;
+        for (uint32_t j = f + (t & 63); j < cap; j += 64) b1_fill(a, r0 + p * R + j);
     }
 }
 
 // the unused slots of the spill areas (tab_scatter1f): TAB_SENT, skipped by pass 2
-__global__ __launch_bounds__(256) void tab_spill_fill_kernel(uint64_t *B1, uint64_t base, uint64_t R, uint64_t S,
-                                                             uint64_t PS, const unsigned long long *pcur) {
+__global__ __launch_bounds__(256) void tab_spill_fill_kernel(bool narrow, uint64_t *B1, uint64_t base, uint64_t R,
+                                                             uint64_t S, uint64_t PS, const unsigned long long *pcur) {
     const uint32_t p = blockIdx.x;
     const uint64_t used = pcur[p] < S ? pcur[p] : S;
-    for (uint64_t i = used + threadIdx.x; i < S; i += 256) B1[base + p * PS + R + i] = TAB_SENT;
+    for (uint64_t i = used + threadIdx.x; i < S; i += 256) {
+        if (narrow) ((uint32_t *)B1)[base + p * PS + R + i] = TAB_SENT32;
+        else B1[base + p * PS + R + i] = TAB_SENT;
+    }
 }
 
 // keys (windows) of each pass-1 workgroup's share of lines: the fixed runs of
@@ -491,11 +507,7 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter1_kernel(TabArgs a) {
 #ifndef TAB_EXP_S1_NOSTORE                         // (experiment builds only)
         for (uint32_t i = t; i < total; i += TAB_WG1) {
             const uint64_t h = srt[i];
-#ifdef TAB_EXP_NT
-            __builtin_nontemporal_store(h, &a.B1[cur[(uint32_t)(h >> (64 - TAB_L1))] + i]);
-#else
-            a.B1[cur[(uint32_t)(h >> (64 - TAB_L1))] + i] = h;
-#endif
+            b1_store(a, cur[(uint32_t)(h >> (64 - TAB_L1))] + i, h);
         }
 #endif
         __syncthreads();
@@ -760,7 +772,8 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2c_kernel(const uint64_t *
 // (uint32_t)(h >> 22) = bucket offset << 22 | the remainder's top 22 bits (the
 // partition is the region's), half the bytes; the LDS sort runs on those
 // 32-bit keys and the write-out aligns to 16 keys (64 B).
-template <bool NAR>
+// B1N: pass-1 keys of 32 bits (narrow, from this session's pass 1)
+template <bool NAR, bool B1N>
 __global__ __launch_bounds__(TAB_WG1) void tab_scatter2f_kernel(const uint64_t *B1, const TabUnit *units,
                                                                 const uint32_t *ufirst, uint32_t p0, uint64_t cap,
                                                                 uint32_t rpp, uint32_t gmag, void *B2v,
@@ -782,7 +795,15 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2f_kernel(const uint64_t *
     auto regk = [&](KT x) {
         return NAR ? (((uint32_t)x >> (TAB_RBITS - TAB_NSH)) * gmag) >> 20 : reg((uint64_t)x);
     };
-    auto kt = [&](uint64_t h) { return NAR ? (KT)(h >> TAB_NSH) : (KT)h; };
+    auto kt = [&](uint64_t h) { return NAR ? (KT)((h >> TAB_NSH) & 0x7FFFFFFFu) : (KT)h; };
+    // a pass-1 slot as loaded (B1N: 32 bits), and as h (B1N: without the
+    // partition bits, which no step here reads) -- converted at use, so the
+    // next round's loads stay in flight through the write-out
+    using LT = typename std::conditional<B1N, uint32_t, uint64_t>::type;
+    auto hk = [&](LT v) -> uint64_t {
+        if (!B1N) return (uint64_t)v;
+        return (uint32_t)v == TAB_SENT32 ? TAB_SENT : (uint64_t)v << TAB_NSH;
+    };
     const uint64_t q = (uint64_t)p * rpp + t;
     const uint64_t pbase = (uint64_t)p * rpp * cap;   // (region (p, b): pbase + b cap)
     uint64_t dest = q * cap;                       // next B2 slot of region t
@@ -797,8 +818,8 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2f_kernel(const uint64_t *
     const uint32_t u0 = ufirst[p], nun = units[u0].nunits;
     for (uint32_t ui = 0; ui < nun; ++ui) {
         const TabUnit un = units[u0 + ui];
-        const uint64_t *src = B1 + un.start;
-        uint64_t key[TS2_RPL];
+        const LT *src = (const LT *)B1 + un.start;
+        LT key[TS2_RPL];
 #pragma unroll
         for (int j = 0; j < TS2_RPL; ++j) {
             const uint32_t i = j * TAB_WG1 + t;
@@ -810,8 +831,8 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2f_kernel(const uint64_t *
 #pragma unroll
             for (int j = 0; j < TS2_RPL; ++j) {
                 const uint32_t i = r0 + j * TAB_WG1 + t;
-                rank[j] = i < un.len && key[j] != TAB_SENT
-                              ? atomicAdd(&bcnt[reg(key[j])], 1u) : 0u;
+                rank[j] = i < un.len && hk(key[j]) != TAB_SENT
+                              ? atomicAdd(&bcnt[reg(hk(key[j]))], 1u) : 0u;
             }
             __syncthreads();
             const uint32_t n_new = bcnt[t], tot = n_new + cc;
@@ -825,8 +846,8 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2f_kernel(const uint64_t *
 #pragma unroll
             for (int j = 0; j < TS2_RPL; ++j) {
                 const uint32_t i = r0 + j * TAB_WG1 + t;
-                if (i < un.len && key[j] != TAB_SENT)
-                    srt[bst[reg(key[j])] + rank[j]] = kt(key[j]);
+                if (i < un.len && hk(key[j]) != TAB_SENT)
+                    srt[bst[reg(hk(key[j]))] + rank[j]] = kt(hk(key[j]));
             }
 #pragma unroll
             for (int i = 0; i < CARRY; ++i)
@@ -862,16 +883,19 @@ __global__ __launch_bounds__(TAB_WG1) void tab_scatter2f_kernel(const uint64_t *
 }
 
 hipError_t launch_tab_scatter2f(const uint64_t *B1, const TabUnit *units, const uint32_t *ufirst, uint32_t p0,
-                                uint32_t np, uint64_t cap, uint32_t rpp, uint32_t gmag, bool narrow, void *B2,
-                                uint32_t *blen, unsigned int *err, hipStream_t s) {
-    if (rpp == 0 || rpp > TAB_NB || (cap & (narrow ? 15 : 7))) return hipErrorInvalidValue;
+                                uint32_t np, uint64_t cap, uint32_t rpp, uint32_t gmag, bool narrow, bool b1n,
+                                void *B2, uint32_t *blen, unsigned int *err, hipStream_t s) {
+    if (rpp == 0 || rpp > TAB_NB || (cap & (narrow ? 15 : 7)) || (b1n && !narrow)) return hipErrorInvalidValue;
     if (!np) return hipSuccess;
-    if (narrow)
-        hipLaunchKernelGGL(tab_scatter2f_kernel<true>, dim3(np), dim3(TAB_WG1), 0, s, B1, units, ufirst, p0, cap, rpp,
-                           gmag, B2, blen, err);
+    if (b1n)
+        hipLaunchKernelGGL((tab_scatter2f_kernel<true, true>), dim3(np), dim3(TAB_WG1), 0, s, B1, units, ufirst, p0,
+                           cap, rpp, gmag, B2, blen, err);
+    else if (narrow)
+        hipLaunchKernelGGL((tab_scatter2f_kernel<true, false>), dim3(np), dim3(TAB_WG1), 0, s, B1, units, ufirst, p0,
+                           cap, rpp, gmag, B2, blen, err);
     else
-        hipLaunchKernelGGL(tab_scatter2f_kernel<false>, dim3(np), dim3(TAB_WG1), 0, s, B1, units, ufirst, p0, cap, rpp,
-                           gmag, B2, blen, err);
+        hipLaunchKernelGGL((tab_scatter2f_kernel<false, false>), dim3(np), dim3(TAB_WG1), 0, s, B1, units, ufirst, p0,
+                           cap, rpp, gmag, B2, blen, err);
     return hipGetLastError();
 }
 
@@ -1081,7 +1105,7 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
     };
     // Map statistics of one canonical entry h (App. A.6)
     auto account = [&](uint64_t h, uint64_t cnt) {
-        const uint64_t code = tab_unmix(h, a.narrow, a.inv);
+        const uint64_t code = tab_code(h, k, a.narrow, a.inv);
         const uint32_t lo = (uint32_t)code & kmask, hi = (uint32_t)(code >> k) & kmask;
         const uint32_t rlo2 = __brev(~lo & kmask) >> sh, rhi2 = __brev(~hi & kmask) >> sh;
         const bool pal = lo == rlo2 && hi == rhi2;
@@ -1516,7 +1540,7 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
             st_sum += cnt;
             return;
         }
-        const uint64_t code = tab_unmix(h, a.narrow, a.inv);
+        const uint64_t code = tab_code(h, k, a.narrow, a.inv);
         const uint32_t lo = (uint32_t)code & kmask, hi = (uint32_t)(code >> k) & kmask;
         const uint32_t rlo2 = __brev(~lo & kmask) >> sh, rhi2 = __brev(~hi & kmask) >> sh;
         const bool pal = lo == rlo2 && hi == rhi2;
@@ -1894,9 +1918,9 @@ hipError_t launch_tab_scatter1f(const TabArgs &a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_tab_spill_fill(uint64_t *B1, uint64_t base, uint64_t R, uint64_t S, uint64_t PS,
+hipError_t launch_tab_spill_fill(bool narrow, uint64_t *B1, uint64_t base, uint64_t R, uint64_t S, uint64_t PS,
                                  const unsigned long long *pcur, hipStream_t s) {
-    hipLaunchKernelGGL(tab_spill_fill_kernel, dim3(TAB_NB), dim3(256), 0, s, B1, base, R, S, PS, pcur);
+    hipLaunchKernelGGL(tab_spill_fill_kernel, dim3(TAB_NB), dim3(256), 0, s, narrow, B1, base, R, S, PS, pcur);
     return hipGetLastError();
 }
 
@@ -1917,11 +1941,27 @@ hipError_t launch_tab_segcopy(const uint64_t *src, const TabSeg *segs, uint32_t 
     return hipGetLastError();
 }
 
+// narrow pass-1 keys (32 bits below the partition) -> h
+__global__ __launch_bounds__(256) void tab_widen_kernel(const uint32_t *src, const TabSeg *segs, uint64_t *dst) {
+    const TabSeg g = segs[blockIdx.x];
+    const uint64_t pb = g.part << (64 - TAB_L1);
+    for (uint64_t i = threadIdx.x; i < g.len; i += 256) {
+        const uint32_t x = src[g.src + i];
+        dst[g.dst + i] = x == TAB_SENT32 ? TAB_SENT : pb | (uint64_t)x << TAB_NSH;
+    }
+}
+
+hipError_t launch_tab_widen(const uint32_t *src, const TabSeg *segs, uint32_t n, uint64_t *dst, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(tab_widen_kernel, dim3(n), dim3(256), 0, s, src, segs, dst);
+    return hipGetLastError();
+}
+
 // Linear digest of a table: sum over entries of count x tab_digest_mix(h)
 // (mod 2^64; counts >= TAB_CMAX are corrected on the host from the big list).
 // One wave per bucket; one atomic per wave.
 __global__ __launch_bounds__(256) void tab_digest_kernel(const uint64_t *ent, const uint64_t *start,
-                                                         const uint32_t *nd, uint32_t narrow,
+                                                         const uint32_t *nd, uint32_t k, uint32_t narrow,
                                                          unsigned long long *out) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = (gridDim.x * blockDim.x) >> 6;
@@ -1933,16 +1973,16 @@ __global__ __launch_bounds__(256) void tab_digest_kernel(const uint64_t *ent, co
             const uint64_t w = ent[s0 + i];
             const uint64_t h = ((uint64_t)q << TAB_RBITS) | (w >> 20);
             // (the weight of the code's tab_mix hash, for narrow keys too)
-            acc += (w & TAB_CMAX) * tab_digest_mix(narrow ? tab_mix(tab_unmix(h, true, TAB_INV)) : h);
+            acc += (w & TAB_CMAX) * tab_digest_mix(tab_digest_key(h, k, narrow));
         }
     }
     for (int d = 32; d >= 1; d >>= 1) acc += (uint64_t)__shfl_xor((long long)acc, d);
     if (lane == 0 && acc) atomicAdd(out, (unsigned long long)acc);
 }
 
-hipError_t launch_tab_digest(const uint64_t *ent, const uint64_t *start, const uint32_t *nd, uint32_t narrow,
-                            unsigned long long *out, hipStream_t s) {
-    hipLaunchKernelGGL(tab_digest_kernel, dim3(4096), dim3(256), 0, s, ent, start, nd, narrow, out);
+hipError_t launch_tab_digest(const uint64_t *ent, const uint64_t *start, const uint32_t *nd, uint32_t k,
+                            uint32_t narrow, unsigned long long *out, hipStream_t s) {
+    hipLaunchKernelGGL(tab_digest_kernel, dim3(4096), dim3(256), 0, s, ent, start, nd, k, narrow, out);
     return hipGetLastError();
 }
 
