@@ -269,9 +269,12 @@ def load_traffic(args, kern_name):
 # pass-1 key count n (8-B keys) -- DESIGN.md §5.  final: every key read once
 # (a bucket is held in registers across its LDS ranges) + one 8-B entry written
 # per distinct canonical k-mer.
-def table_phase_bytes(nbytes, n_keys, canonical):
-    return {"lines": nbytes, "hist1": nbytes, "scatter1": nbytes + 8 * n_keys, "hist2": 8 * n_keys,
-            "scatter2": 16 * n_keys, "final": 8 * n_keys + 8 * canonical}
+def table_phase_bytes(nbytes, n_keys, canonical, key_bytes=8):
+    """Algorithmic bytes of the table phases: pass-1 keys of `key_bytes` (4:
+    narrow keys, k <= 21 -- kmer_internal.hpp TAB_NSH), entries of 8 B."""
+    kb = key_bytes
+    return {"lines": nbytes, "hist1": nbytes, "scatter1": nbytes + kb * n_keys, "hist2": kb * n_keys,
+            "scatter2": 2 * kb * n_keys, "final": kb * n_keys + 8 * canonical}
 
 
 def print_shard_plan(args, world, strong):
@@ -686,7 +689,7 @@ def main():
             # pass-1 keys = forward windows counted (no prefix): the Map sum is
             # twice that, the canonical sum once
             n_keys = (accepted if args.flags & _FC else accepted // 2) if not args.prefix else None
-            pbytes = table_phase_bytes(nbytes, n_keys or 0, canonical)
+            pbytes = table_phase_bytes(nbytes, n_keys or 0, canonical, 4 if args.k <= 21 else 8)
             pbytes["fasta"] = 2 * nbytes      # (the rewrite: the chunk read once, about its size written)
             kern_name = max(phases, key=lambda x: phases[x])
             kern_ms = phases[kern_name]
@@ -697,7 +700,7 @@ def main():
             kern_name = {"lines": "nl_slots_kernel + seq_lines_slots_kernel",
                          "hist1": "tab_hist1_kernel (+ scan)",
                          "scatter1": "tab_scatter1f_kernel" if fixed else "tab_scatter1h_kernel",
-                         "hist2": "tab_hist2_kernel (+ scan)", "scatter2": "tab_scatter2c_kernel",
+                         "hist2": "tab_hist2_kernel (+ scan)", "scatter2": "tab_scatter2f_kernel (fixed regions; counted route: tab_scatter2c_kernel)",
                          "final": "tab_sort_final_kernel (+ tab_final_kernel on its leftover units)",
                          "fasta": "fa_tiles_kernel + fa_write_kernel (FASTA rewrite)"}[kern_name]
         elif args.k > 64 or (not args.prefix and args.k > 31):
