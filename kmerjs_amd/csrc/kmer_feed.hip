@@ -806,8 +806,11 @@ kmer_status dense_windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint
 }
 
 // Dense-hit path: every window of every sequence line goes to its rank slot
-// (step > 1, and KMERHIP_DENSE=slots in experiment builds); step 1 with
-// k <= 32 ranks only the accepted windows (dense_windows_feed).
+// (step > 1; no prefix, where every ACGT window is accepted and the count
+// pass would only repeat the line lengths: k 21 / 4 M reads 78.1 vs 97.0 ms,
+// C5 ordered 78.9 vs 95.4 ms, profiles/r06_ab/dense_*; and KMERHIP_DENSE=slots
+// in experiment builds); with a prefix (step 1), and always past k = 32, only
+// the accepted windows are ranked (dense_windows_feed: k 16 / AT 15.6 vs 33.3 ms).
 kmer_status windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n_tiles, hipStream_t s) {
     const uint64_t li0 = c->host_lines;
     kmer_status st;
@@ -819,7 +822,7 @@ kmer_status windows_feed(kmer_ctx *c, const uint8_t *d, uint64_t len, uint32_t n
         const char *e = exp_env("KMERHIP_DENSE");
         return e && strcmp(e, "slots") == 0;
     }();
-    if (c->p.step == 1 && (c->p.k > (uint32_t)KMAX_DENSE || !slots_only))
+    if (c->p.step == 1 && (c->p.k > (uint32_t)KMAX_DENSE || (!slots_only && !c->prefix.empty())))
         return dense_windows_feed(c, d, len, n_seq, n_nl, li0, s);
     c->win_slots = true;                          // (the finish compacts the rejected windows' slots away)
     uint64_t total = 0;
