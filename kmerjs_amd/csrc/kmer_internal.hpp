@@ -679,6 +679,7 @@ hipError_t launch_tab_final(const TabFinal &a, uint32_t grid, hipStream_t s);
 hipError_t launch_tab_sort_final(const TabFinal &a, uint32_t grid, hipStream_t s);
 constexpr uint32_t TAB_SWG = 512;
 constexpr uint64_t TAB_SORT_KEYS = 12288;               // sort final: keys of a unit (one bucket, or narrow keys: TS_CAP1)
+constexpr uint64_t TAB_SORT_KEYS_BIG = 12160;           // ... with 16,384 bins (fixed regions: tab_sort_final_kernel<14>)
 constexpr uint64_t TAB_SORT_GROUP_KEYS = 6144;          // sort final: keys of a unit of several buckets (TS_CAPG)                      // sort-final workgroup (8 waves, two per CU)
 hipError_t launch_tab_digest(const uint64_t *ent, const uint64_t *start, const uint32_t *nd, uint32_t k,
                             uint32_t narrow, unsigned long long *out,

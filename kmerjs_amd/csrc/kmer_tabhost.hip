@@ -361,7 +361,7 @@ kmer_status table_finish(kmer_ctx *c, const uint64_t *B1, uint32_t qlo, uint32_t
     if (mu >= 2048.0 && !narrow) {
         qg = 1;
     } else {
-        const uint64_t lim = narrow ? TAB_SORT_KEYS : TAB_SORT_GROUP_KEYS;
+        const uint64_t lim = narrow ? TAB_SORT_KEYS_BIG : TAB_SORT_GROUP_KEYS;
         for (uint32_t g = sort_ok ? 64 : 1; g >= 1 && !qg; --g)
             if (cap6(g * mu) <= lim && (g >= 2 || narrow)) qg = g;
     }

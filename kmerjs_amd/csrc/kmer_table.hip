@@ -930,8 +930,7 @@ namespace {
 // sums through LDS): device-scope atomics on one line serialise (~12 ns each),
 // and every wave of the grid reaches this point at about the same time
 __device__ __forceinline__ void tab_stats_out(unsigned long long *stats, uint64_t c, uint64_t kk, uint64_t sm,
-                                              uint32_t waves) {
-    __shared__ unsigned long long red[16][3];
+                                              uint32_t waves, unsigned long long (*red)[3]) {
     for (int d = 32; d >= 1; d >>= 1) {
         c += __shfl_xor(c, d);
         kk += __shfl_xor(kk, d);
@@ -1458,7 +1457,10 @@ __global__ __launch_bounds__(TAB_FWG) void tab_final_kernel(TabFinal a) {
     }
     if (prof)
         for (int i = 0; i < 6; ++i) a.prof[blockIdx.x * 8 + i] = pt[i];
-    tab_stats_out(a.stats, st_canon, st_keys, st_sum, TAB_FWG / 64);
+    {
+        __shared__ unsigned long long red[16][3];
+        tab_stats_out(a.stats, st_canon, st_keys, st_sum, TAB_FWG / 64, red);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1494,11 +1496,20 @@ __device__ __forceinline__ bool tab_cap_failed(const TabFinal &a) {
     return a.capq && (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ERR_TAB_CAP);
 }
 
+// NBB_: log2 of the bins.  14 (fixed regions of one wide bucket or of narrow
+// keys, the common case at size): 16,384 bins, half the keys per bin for the
+// copy scan, in the LDS the group path's bucket-start cache (and 128 keys of
+// the unit) gave up: units of <= 12,160 keys, no groups of 64-bit keys.  13:
+// everything else.
+template <uint32_t NBB_>
 __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) {
+    constexpr uint32_t NB = 1u << NBB_;
+    constexpr uint32_t CAP1 = NBB_ == 14 ? (uint32_t)TAB_SORT_KEYS_BIG : TS_CAP1;
+    constexpr uint32_t WPT = NB / 2 / TAB_SWG;          // bin-count words per thread (scan)
     if (tab_cap_failed(a)) return;
-    __shared__ uint32_t lkey[TS_CAP1];                // sorted unit: u32 (one bucket) or u64 (a group)
-    __shared__ uint32_t bst[TS_NB / 2];               // bin counts, then starts: bin b in half b & 1 of word b >> 1
-    __shared__ uint64_t sc[TS_SC + 2];                // start[cbase .. cbase + TS_SC + 1]
+    __shared__ __attribute__((aligned(16))) uint32_t lkey[CAP1];   // sorted unit: u32 (one bucket) or u64 (a group)
+    __shared__ uint32_t bst[NB / 2];                  // bin counts, then starts: bin b in half b & 1 of word b >> 1
+    __shared__ uint64_t sc[NBB_ == 13 ? TS_SC + 2 : 1];   // start[cbase .. cbase + TS_SC + 1]
     __shared__ uint32_t nout[TS_GMAX];
     __shared__ uint32_t ws[8], smax;
     uint64_t *const lkey64 = (uint64_t *)lkey;
@@ -1610,7 +1621,7 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
             q = qe;
             continue;
         }
-        if (n > TS_CAP1) {                             // (g == 1) a crowded bucket
+        if (n > CAP1) {                             // (g == 1) a crowded bucket
             leftover(q, qe);
             q = qe;
             continue;
@@ -1630,7 +1641,7 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
             constexpr bool ONE = MODE == 0, GRP = MODE == 1, NAR = MODE == 2;
             constexpr int KPT = GRP ? TS_KPT / 2 : TS_KPT;
             const uint32_t obits = g > 1 ? 32 - __clz(g - 1) : 0;
-            const uint32_t bsh = (NAR ? TAB_RBITS - TAB_NSH : TAB_RBITS) + obits - TS_NBB;
+            const uint32_t bsh = (NAR ? TAB_RBITS - TAB_NSH : TAB_RBITS) + obits - NBB_;
             const bool single = g == 1;                  // (ONE: always)
             uint32_t lo[KPT], hi[GRP ? KPT : 1], pk[KPT];
             if (NAR) {
@@ -1639,7 +1650,7 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
                     lo[j] = src[left > j * (int)TAB_SWG ? j * TAB_SWG + t : 0u] - qoff;
-                    pk[j] = (lo[j] >> bsh) & (TS_NB - 1);
+                    pk[j] = (lo[j] >> bsh) & (NB - 1);
                 }
             } else {
                 const uint64_t *src = a.B2 + s0in;
@@ -1648,11 +1659,11 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                     const uint64_t x = src[left > j * (int)TAB_SWG ? j * TAB_SWG + t : 0u] - qbase;
                     lo[j] = (uint32_t)x;
                     if (GRP) hi[GRP ? j : 0] = (uint32_t)(x >> 32);
-                    pk[j] = (uint32_t)(x >> bsh) & (TS_NB - 1);
+                    pk[j] = (uint32_t)(x >> bsh) & (NB - 1);
                 }
             }
             __syncthreads();                           // the previous unit is done with the LDS state
-            for (uint32_t i = t; i < TS_NB / 2; i += TAB_SWG) bst[i] = 0;
+            for (uint32_t i = t; i < NB / 2; i += TAB_SWG) bst[i] = 0;
             if (t == 0) smax = 0;
             for (uint32_t i = t; i < g; i += TAB_SWG) nout[i] = 0;
             __syncthreads();
@@ -1665,12 +1676,15 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                                                      __HIP_MEMORY_SCOPE_WORKGROUP) >> (16 * (pk[j] & 1u))) & 0xFFFFu);
             __syncthreads();
             {
-                // bin starts: thread t scans bins 16t .. 16t + 15 (words 8t .. 8t + 7)
-                uint32_t c8[8], sum = 0, mx = 0;
+                // bin starts: thread t scans words WPT t .. WPT t + WPT - 1
+                // (16 words: read again after the block scan rather than held)
+                constexpr int HOLD = WPT <= 8 ? (int)WPT : 1;
+                uint32_t c8[HOLD], sum = 0, mx = 0;
 #pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    c8[i] = bst[8 * t + i];
-                    const uint32_t lo16 = c8[i] & 0xFFFFu, hi16 = c8[i] >> 16;
+                for (int i = 0; i < (int)WPT; ++i) {
+                    const uint32_t c = bst[WPT * t + i];
+                    if (WPT <= 8) c8[i < HOLD ? i : 0] = c;
+                    const uint32_t lo16 = c & 0xFFFFu, hi16 = c >> 16;
                     sum += lo16 + hi16;
                     mx = max(mx, max(lo16, hi16));
                 }
@@ -1679,9 +1693,10 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                 for (int d = 32; d >= 1; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d));
                 if (lane == 0) atomicMax(&smax, mx);
 #pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const uint32_t lo16 = c8[i] & 0xFFFFu, hi16 = c8[i] >> 16;
-                    bst[8 * t + i] = run | (run + lo16) << 16;   // (starts < 2^14)
+                for (int i = 0; i < (int)WPT; ++i) {
+                    const uint32_t c = WPT <= 8 ? c8[i < HOLD ? i : 0] : bst[WPT * t + i];
+                    const uint32_t lo16 = c & 0xFFFFu, hi16 = c >> 16;
+                    bst[WPT * t + i] = run | (run + lo16) << 16;   // (starts < 2^14)
                     run += lo16 + hi16;
                 }
             }
@@ -1689,7 +1704,7 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
             // a region of several buckets: each bucket's exact output start
             // (its keys' bins are consecutive: bins j << sbb .. of offset j),
             // also for a region left to the general kernel
-            const uint32_t sbb = TS_NBB - obits;
+            const uint32_t sbb = NBB_ - obits;
             if (!single && a.capq && t < g) a.wstart[q + t] = s0 + (bst[(t << sbb) >> 1] & 0xFFFFu);
             if (smax > TS_BINMAX) return false;        // (uniform) many copies of a key
             // counting-sort scatter: bin start + rank in the bin (bst[b] stays the start of bin b)
@@ -1720,10 +1735,10 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                             const uint64_t x = lkey64[i];
                             lo[j] = (uint32_t)x;
                             hi[GRP ? j : 0] = (uint32_t)(x >> 32);
-                            pk[j] = ((uint32_t)(x >> bsh) & (TS_NB - 1)) << 14 | i;
+                            pk[j] = ((uint32_t)(x >> bsh) & (NB - 1)) << 14 | i;
                         } else {
                             lo[j] = lkey[i];
-                            pk[j] = ((lo[j] >> bsh) & (TS_NB - 1)) << 14 | i;
+                            pk[j] = ((lo[j] >> bsh) & (NB - 1)) << 14 | i;
                         }
                     }
             }
@@ -1743,7 +1758,7 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                     const bool valid = left > j * (int)TAB_SWG;
                     const uint32_t b = pk[j] >> 14;
                     const uint32_t b0 = (bst[b >> 1] >> (16 * (b & 1u))) & 0xFFFFu;
-                    const uint32_t b1 = (KH_ABLATE(a) & 8) ? b0 : b + 1 < TS_NB ? (bst[(b + 1) >> 1] >> (16 * ((b + 1) & 1u))) & 0xFFFFu : (uint32_t)n;
+                    const uint32_t b1 = (KH_ABLATE(a) & 8) ? b0 : b + 1 < NB ? (bst[(b + 1) >> 1] >> (16 * ((b + 1) & 1u))) & 0xFFFFu : (uint32_t)n;
                     const uint32_t c = valid ? b1 - b0 : 0u;
                     bb[u] = b0 | c << 14;
                     cf[u] = valid ? ((KH_ABLATE(a) & 8) ? 0x101u : 0x100u) : 0u;   // (experiments: no bin scan)
@@ -1783,8 +1798,8 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
                 for (int u = 0; u < G; ++u) {
                     const int j = g0 + u;
                     const uint32_t b = pk[j] >> 14;
-                    // (one bucket: the bin is the remainder's top TS_NBB bits, bits 31 .. 43)
-                    const uint64_t xj = ONE ? (((uint64_t)b << (TAB_RBITS - TS_NBB)) | (lo[j] & ((1u << (TAB_RBITS - TS_NBB)) - 1u)))
+                    // (one bucket: the bin is the remainder's top NBB_ bits, bits 31 .. 43)
+                    const uint64_t xj = ONE ? (((uint64_t)b << (TAB_RBITS - NBB_)) | (lo[j] & ((1u << (TAB_RBITS - NBB_)) - 1u)))
                                         : GRP ? (((uint64_t)hi[GRP ? j : 0] << 32) | lo[j])
                                               : (uint64_t)lo[j] << TAB_NSH;
                     const bool first = (cf[u] >> 8) != 0u;
@@ -1818,8 +1833,13 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
             }
             return true;
         };
-        const bool ok = a.b2n ? sort_unit(std::integral_constant<int, 2>{})
-                        : g == 1 ? sort_unit(std::integral_constant<int, 0>{}) : sort_unit(std::integral_constant<int, 1>{});
+        bool ok = false;
+        if (a.b2n)
+            ok = sort_unit(std::integral_constant<int, 2>{});
+        else if (g == 1 || NBB_ == 14)           // (NBB_ 14: one wide bucket per region, g == 1)
+            ok = sort_unit(std::integral_constant<int, 0>{});
+        else if constexpr (NBB_ == 13)
+            ok = sort_unit(std::integral_constant<int, 1>{});
         if (!ok) {
             leftover(q, qe);
             q = qe;
@@ -1829,7 +1849,8 @@ __global__ __launch_bounds__(TAB_SWG, 4) void tab_sort_final_kernel(TabFinal a) 
         for (uint32_t i = t; i < g; i += TAB_SWG) a.nd[q + i] = nout[i];
         q = qe;
     }
-    tab_stats_out(a.stats, st_canon, st_keys, st_sum, TAB_SWG / 64);
+    __syncthreads();                                 // (the key array is free: the reduction's scratch)
+    tab_stats_out(a.stats, st_canon, st_keys, st_sum, TAB_SWG / 64, (unsigned long long (*)[3])lkey);
 }
 
 // ---------------------------------------------------------------------------
@@ -1987,7 +2008,16 @@ hipError_t launch_tab_digest(const uint64_t *ent, const uint64_t *start, const u
 }
 
 hipError_t launch_tab_sort_final(const TabFinal &a, uint32_t grid, hipStream_t s) {
-    hipLaunchKernelGGL(tab_sort_final_kernel, dim3(grid), dim3(TAB_SWG), 0, s, a);
+    // (16,384 bins for fixed regions of one wide bucket or of narrow keys;
+    // KMERHIP_TAB_BINS=8192: always 8,192, A/B experiments)
+    static const bool big_ok = [] {
+        const char *e = exp_env("KMERHIP_TAB_BINS");
+        return !(e && strcmp(e, "8192") == 0);
+    }();
+    if (a.capq && a.capq <= TAB_SORT_KEYS_BIG && (a.qg == 1 || a.b2n) && big_ok)
+        hipLaunchKernelGGL(tab_sort_final_kernel<14>, dim3(grid), dim3(TAB_SWG), 0, s, a);
+    else
+        hipLaunchKernelGGL(tab_sort_final_kernel<13>, dim3(grid), dim3(TAB_SWG), 0, s, a);
     return hipGetLastError();
 }
 
