@@ -721,14 +721,19 @@ def main():
             kern_name = ("scan_planes_kernel" if set(args.prefix) <= set("ACGT") else
                          "scan_tile_kernel") + " (tile records path; host record merge dominates the step)"
             algo_bytes = nbytes + 24 * (accepted / world)
-        elif (args.prefix and len(args.prefix) <= 3) or not args.prefix:
-            # dense-hit path (1-3 base prefixes or none, k <= 64): the timed
-            # phase is the line split -- one streaming pass over the input
+        elif args.prefix and len(args.prefix) <= 3:
+            # dense-hit path with a 1-3 base prefix (k <= 64): the timed phase
+            # is the line split -- one streaming pass over the input
             # (nl_slots_kernel) + the sequence-line descriptors -- and the count
             # pass over the sequence lines (dense_windows_kernel<count>: the
             # 150 sequence bytes of a 317-B record read once more)
             kern_name = "nl_slots_kernel + seq_lines_slots_kernel + dense_windows_kernel<count> (dense-hit path)"
             algo_bytes = nbytes * (1.0 + 150.0 / 317.0)
+        elif not args.prefix:
+            # dense-hit path without a prefix (every window ranked): the timed
+            # phase is the line split alone
+            kern_name = "nl_slots_kernel + seq_lines_slots_kernel (dense-hit path line split)"
+            algo_bytes = nbytes
         elif args.k > 32:
             # packed path with 128-bit window codes (k in 33..64, ACGT prefix)
             kern_name = "scan_planes_kernel (k > 32: 128-bit window codes)"
