@@ -1482,8 +1482,6 @@ constexpr int TS_KPT = 24;                            // keys held per thread
 constexpr uint32_t TS_CAP1 = TS_KPT * TAB_SWG;        // one bucket: 12,288 keys, 32-bit LDS entries
 constexpr uint32_t TS_CAPG = TS_CAP1 / 2;             // a group: 6,144 keys, 64-bit LDS entries
 static_assert(TS_CAPG == TAB_SORT_GROUP_KEYS && TS_CAP1 == TAB_SORT_KEYS, "the host sizes regions by TS_CAPG / TS_CAP1");
-constexpr uint32_t TS_NB = 8192;                      // bins (16-bit counts / starts, two per LDS word)
-constexpr uint32_t TS_NBB = 13;                       // log2(TS_NB)
 constexpr uint32_t TS_BINMAX = 64;                    // fuller bins: leftover (general kernel)
 constexpr uint32_t TS_GMAX = 64;                      // buckets per group
 constexpr uint32_t TS_SC = 512;                       // bucket starts cached per refill
